@@ -1,0 +1,127 @@
+"""Synthetic registration pairs.
+
+No dataset is reachable from this image, so the benchmark and the tests use
+clouds of the same shape as the reference's test inputs:
+
+* ``modelnet_like_pair(i)`` -- a 2048-point raw cloud (uniform samples on the
+  faces of a random box, normalised to max|p| = 1) pushed through the steps of
+  the reference's ModelNet *test* transforms (data_loaders/modelnet.py:111-117):
+  SplitSourceRef -> RandomCrop([0.7, 0.7]) -> RandomTransformSE3_euler(45 deg,
+  0.5) -> Resampler(1024) which yields 717 points per cloud
+  (data_loaders/modelnet_transforms.py:92-93) -> RandomJitter(0.01, clip 0.05)
+  -> ShufflePoints. Every step is re-implemented here with a per-pair seeded
+  generator; it reproduces the shapes and statistics, not the reference's RNG
+  stream.
+* ``indoor_like_pair(i)`` -- a 3DMatch-like fragment pair: points on the floor
+  and four walls of a 3 x 3 x 2.5 m room with 5 mm noise; the second fragment
+  is an independent sample under a random rotation <= 15 deg and translation
+  <= 0.3 m.
+"""
+import math
+
+import numpy as np
+
+
+def _euler_rotation(angles):
+    ax, ay, az = angles
+    cx, sx, cy, sy, cz, sz = (math.cos(ax), math.sin(ax), math.cos(ay), math.sin(ay),
+                              math.cos(az), math.sin(az))
+    rx = np.array([[1, 0, 0], [0, cx, -sx], [0, sx, cx]])
+    ry = np.array([[cy, 0, sy], [0, 1, 0], [-sy, 0, cy]])
+    rz = np.array([[cz, -sz, 0], [sz, cz, 0], [0, 0, 1]])
+    return rx @ ry @ rz
+
+
+def _box_surface(rng, n):
+    ext = rng.uniform(0.3, 1.0, 3)
+    face = rng.integers(0, 6, n)
+    uv = rng.uniform(-0.5, 0.5, (n, 3))
+    axis = face % 3
+    side = np.where(face < 3, -0.5, 0.5)
+    uv[np.arange(n), axis] = side
+    p = uv * ext
+    p /= np.max(np.linalg.norm(p, axis=1))
+    return p
+
+
+def _crop(rng, pts, p_keep):
+    v = rng.normal(size=3)
+    v /= np.linalg.norm(v)
+    d = (pts - pts.mean(0)) @ v
+    return pts[d > np.percentile(d, (1.0 - p_keep) * 100)]
+
+
+def _resample(rng, pts, k):
+    if k <= len(pts):
+        idx = rng.choice(len(pts), k, replace=False)
+    else:
+        idx = np.concatenate([rng.permutation(len(pts)), rng.choice(len(pts), k - len(pts))])
+    return pts[idx]
+
+
+def modelnet_like_pair(i, n_raw=2048, n_keep=717, rot_mag=45.0, trans_mag=0.5):
+    """Returns (src (n_keep,3) f32, tgt (n_keep,3) f32, pose (3,4) f32: src -> tgt)."""
+    rng = np.random.default_rng(1000003 * (i + 1))
+    raw = _box_surface(rng, n_raw)
+    src = _crop(rng, raw, 0.7)
+    tgt = _crop(rng, raw, 0.7)
+    ang = np.deg2rad(rng.uniform(-rot_mag, rot_mag, 3))
+    R = _euler_rotation(ang)
+    t = rng.uniform(-trans_mag, trans_mag, 3)
+    src = src @ R.T + t                       # transform applied to the source
+    n_keep = min(n_keep, 717 if n_raw >= 1024 else n_keep)
+    if n_raw < 1024:
+        n_keep = min(n_keep, int(math.ceil(0.7 * n_raw)))
+    src = _resample(rng, src, n_keep)
+    tgt = _resample(rng, tgt, n_keep)
+    jit = lambda p: p + np.clip(rng.normal(0.0, 0.01, p.shape), -0.05, 0.05)
+    src, tgt = jit(src), jit(tgt)
+    src = src[rng.permutation(len(src))]
+    tgt = tgt[rng.permutation(len(tgt))]
+    Rinv = R.T
+    pose = np.concatenate([Rinv, (-Rinv @ t)[:, None]], 1)  # maps src back onto tgt frame
+    return src.astype(np.float32), tgt.astype(np.float32), pose.astype(np.float32)
+
+
+def _room(rng, n, size=(3.0, 3.0, 2.5)):
+    sx, sy, sz = size
+    areas = np.array([sx * sy, sx * sz, sx * sz, sy * sz, sy * sz])
+    surf = rng.choice(5, n, p=areas / areas.sum())
+    u, v = rng.uniform(0, 1, n), rng.uniform(0, 1, n)
+    p = np.zeros((n, 3))
+    f = surf == 0
+    p[f] = np.stack([u[f] * sx, v[f] * sy, np.zeros(f.sum())], 1)
+    f = surf == 1
+    p[f] = np.stack([u[f] * sx, np.zeros(f.sum()), v[f] * sz], 1)
+    f = surf == 2
+    p[f] = np.stack([u[f] * sx, np.full(f.sum(), sy), v[f] * sz], 1)
+    f = surf == 3
+    p[f] = np.stack([np.zeros(f.sum()), u[f] * sy, v[f] * sz], 1)
+    f = surf == 4
+    p[f] = np.stack([np.full(f.sum(), sx), u[f] * sy, v[f] * sz], 1)
+    p += rng.normal(0.0, 0.005, p.shape)
+    return p - np.array([sx, sy, sz]) / 2
+
+
+def indoor_like_pair(i, n_points=20000, max_rot_deg=15.0, max_trans=0.3):
+    """Returns (src (N,3) f32, tgt (N,3) f32, pose (3,4) f32: src -> tgt)."""
+    rng = np.random.default_rng(7919 * (i + 1))
+    tgt = _room(rng, n_points)
+    src0 = _room(rng, n_points)
+    axis = rng.normal(size=3)
+    axis /= np.linalg.norm(axis)
+    ang = np.deg2rad(rng.uniform(0, max_rot_deg))
+    K = np.array([[0, -axis[2], axis[1]], [axis[2], 0, -axis[0]], [-axis[1], axis[0], 0]])
+    R = np.eye(3) + math.sin(ang) * K + (1 - math.cos(ang)) * K @ K
+    t = rng.uniform(-max_trans, max_trans, 3)
+    src = (src0 - t) @ R                         # src = R^T (x - t): pose maps src -> tgt
+    pose = np.concatenate([R, t[:, None]], 1)
+    return src.astype(np.float32), tgt.astype(np.float32), pose.astype(np.float32)
+
+
+def make_batch(kind, batch_size, start=0, **kw):
+    """List-of-clouds batch in the reference's collate_pair layout (collate_functions.py:4-22)."""
+    gen = modelnet_like_pair if kind == 'modelnet' else indoor_like_pair
+    pairs = [gen(start + b, **kw) for b in range(batch_size)]
+    return ([p[0] for p in pairs], [p[1] for p in pairs],
+            np.stack([p[2] for p in pairs]).astype(np.float32))

@@ -1,0 +1,432 @@
+#!/usr/bin/env python3
+"""Generate the golden vectors under tests/golden/ by running the REFERENCE itself.
+
+TEST INFRASTRUCTURE ONLY. Runs in the build container (it needs /root/reference
+and oracle/_ref/libkpconv_ref.so, built by `make -C oracle ref`); nothing on the
+GPU box executes it. Only the .npz files it writes travel.
+
+How the reference is run:
+  * the reference Python modules are imported from /root/reference with
+    import-only stand-ins for packages that are absent here and never executed on
+    the CPU path (MinkowskiEngine, pytorch3d, tensorboard, nibabel, easydict,
+    open3d-based visualisation);
+  * KPConv preprocessing uses the reference's own CPU `Preprocessor`
+    (models/backbone_kpconv/finegrained_kpconv.py:296-419) whose native calls
+    (`cpp_neighbors.batch_query`, `cpp_subsampling.subsample_batch`) are served by
+    the reference's unmodified C++ algorithms (oracle/_ref/libkpconv_ref.so) through
+    ctypes instead of the reference's NumPy-1 CPython wrapper;
+  * `fast_compute_rigid_transform` hard-codes `.to(device='cuda')`
+    (utils/se3_torch.py:240); it is called unmodified with `Tensor.to('cuda')`
+    redirected to CPU for the duration of the call.
+
+Usage:  python tests/golden/make_golden.py        (writes tests/golden/*.npz)
+"""
+import contextlib
+import ctypes
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+REF = os.environ.get('FGREG_REFERENCE', '/root/reference')
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+LIBREF = os.path.join(REPO, 'oracle', '_ref', 'libkpconv_ref.so')
+sys.dont_write_bytecode = True
+
+
+# --------------------------------------------------------------------------------------
+# Reference native calls via ctypes (reference algorithm code, our adaptor)
+# --------------------------------------------------------------------------------------
+_lib = ctypes.CDLL(LIBREF)
+_fp = ctypes.POINTER(ctypes.c_float)
+_ip = ctypes.POINTER(ctypes.c_int)
+_lib.ref_neighbors_run.restype = ctypes.c_int
+_lib.ref_neighbors_run.argtypes = [_fp, ctypes.c_int, _fp, ctypes.c_int, _ip, _ip, ctypes.c_int,
+                                   ctypes.c_float]
+_lib.ref_neighbors_fetch.argtypes = [_ip]
+_lib.ref_subsample_run.restype = ctypes.c_int
+_lib.ref_subsample_run.argtypes = [_fp, ctypes.c_int, _ip, ctypes.c_int, ctypes.c_float]
+_lib.ref_subsample_fetch.argtypes = [_fp, _ip]
+
+
+def _f32(a):
+    return np.ascontiguousarray(np.asarray(a, dtype=np.float32))
+
+
+def _i32(a):
+    return np.ascontiguousarray(np.asarray(a, dtype=np.int32))
+
+
+def ref_batch_query(queries, supports, q_batches, s_batches, radius):
+    q, s, qb, sb = _f32(queries), _f32(supports), _i32(q_batches), _i32(s_batches)
+    w = _lib.ref_neighbors_run(q.ctypes.data_as(_fp), q.shape[0], s.ctypes.data_as(_fp), s.shape[0],
+                               qb.ctypes.data_as(_ip), sb.ctypes.data_as(_ip), qb.shape[0],
+                               ctypes.c_float(radius))
+    out = np.empty((q.shape[0], w), dtype=np.int32)
+    _lib.ref_neighbors_fetch(out.ctypes.data_as(_ip))
+    return out
+
+
+def ref_subsample_batch(points, batches, sampleDl=0.1, max_p=0, verbose=0):
+    assert max_p == 0
+    p, b = _f32(points), _i32(batches)
+    m = _lib.ref_subsample_run(p.ctypes.data_as(_fp), p.shape[0], b.ctypes.data_as(_ip), b.shape[0],
+                               ctypes.c_float(sampleDl))
+    pts = np.empty((m, 3), dtype=np.float32)
+    lens = np.empty((b.shape[0],), dtype=np.int32)
+    _lib.ref_subsample_fetch(pts.ctypes.data_as(_fp), lens.ctypes.data_as(_ip))
+    return pts, lens
+
+
+# --------------------------------------------------------------------------------------
+# Import the reference with import-only stand-ins
+# --------------------------------------------------------------------------------------
+def _stub(name, **attrs):
+    m = types.ModuleType(name)
+    m.__dict__.update(attrs)
+    sys.modules[name] = m
+    return m
+
+
+class _EasyDict(dict):
+    def __getattr__(self, k):
+        try:
+            return self[k]
+        except KeyError as e:
+            raise AttributeError(k) from e
+
+    def __setattr__(self, k, v):
+        self[k] = v
+
+
+def _never(*a, **k):
+    raise RuntimeError('stand-in called: this dependency is not available here')
+
+
+def import_reference():
+    _stub('MinkowskiEngine')
+    _stub('pytorch3d')
+    _stub('pytorch3d.ops', packed_to_padded=_never, ball_query=_never)
+
+    class _SW:
+        def __init__(self, *a, **k):
+            pass
+
+    _stub('torch.utils.tensorboard', SummaryWriter=_SW)
+    _stub('nibabel')
+    _stub('nibabel.quaternions', mat2quat=_never)
+    _stub('easydict', EasyDict=_EasyDict)
+    _stub('utils.viz', visualize_registration=_never)
+    sys.path[:0] = [REF, os.path.join(REF, 'models'), os.path.join(REF, 'utils')]
+    cwd = os.getcwd()
+    os.chdir(REF)
+    try:
+        # same import order as the reference's entry points (train.py / test.py import
+        # `models` first; models/__init__.py:18-21 then imports models/finegrained_regtr.py)
+        import models  # noqa: F401,E402
+        fr = sys.modules['models.finegrained_regtr']
+        import backbone_kpconv.finegrained_kpconv as fk  # noqa: E402
+    finally:
+        os.chdir(cwd)
+    fk.cpp_neighbors = types.SimpleNamespace(batch_query=ref_batch_query)
+    fk.cpp_subsampling = types.SimpleNamespace(subsample_batch=ref_subsample_batch)
+    return fr, fk
+
+
+@contextlib.contextmanager
+def cuda_to_cpu():
+    """Redirect `tensor.to(device='cuda')` to CPU (utils/se3_torch.py:240 hard-codes it)."""
+    orig = torch.Tensor.to
+
+    def to(self, *args, **kwargs):
+        dev = kwargs.get('device', args[0] if args else None)
+        if isinstance(dev, str) and dev.startswith('cuda'):
+            return self
+        return orig(self, *args, **kwargs)
+
+    torch.Tensor.to = to
+    try:
+        yield
+    finally:
+        torch.Tensor.to = orig
+
+
+def load_cfg(name, **overrides):
+    import yaml
+    with open(os.path.join(REF, 'conf', name)) as f:
+        raw = yaml.safe_load(f)
+    cfg = _EasyDict()
+    for sect in raw.values():
+        for k, v in sect.items():
+            cfg[k] = v
+    cfg.update(overrides)
+    return cfg
+
+
+# --------------------------------------------------------------------------------------
+# Synthetic inputs (our own generator; same recipe the package uses)
+# --------------------------------------------------------------------------------------
+sys.path.insert(0, os.path.join(REPO, 'boosting-fine-grained-feature-fusion-in-3d-point-cloud-registration_amd'))
+from fgreg.synthetic import modelnet_like_pair, indoor_like_pair  # noqa: E402
+
+
+def save(name, **arrays):
+    path = os.path.join(HERE, name + '.npz')
+    np.savez_compressed(path, **arrays)
+    print(f'wrote {path} ({os.path.getsize(path) / 1024:.1f} KiB)')
+
+
+# --------------------------------------------------------------------------------------
+# Geometry fixtures: reference C++ grid subsampling and radius search
+# --------------------------------------------------------------------------------------
+def make_geometry():
+    cases = {}
+    # ModelNet-like pair, B=2 (4 clouds packed src0, src1, tgt0, tgt1)
+    pairs = [modelnet_like_pair(i) for i in range(2)]
+    clouds = [p[0] for p in pairs] + [p[1] for p in pairs]
+    cases['modelnet'] = (clouds, 0.03 * 2.75, 50)
+    # indoor-like fragment pair, downsized
+    src, tgt, _ = indoor_like_pair(0, n_points=3000)
+    cases['indoor'] = ([src, tgt], 0.025 * 2.5, 40)
+    # edge cases: single point cloud, duplicated points, lattice points on voxel
+    # boundaries (exact multiples of dl), negative coordinates
+    rng = np.random.default_rng(7)
+    lattice = (np.stack(np.meshgrid(np.arange(-3, 4), np.arange(-3, 4), np.arange(-2, 3),
+                                    indexing='ij'), -1).reshape(-1, 3) * 0.06).astype(np.float32)
+    dup = rng.uniform(-0.3, 0.3, (40, 3)).astype(np.float32)
+    dup = np.concatenate([dup, dup[:10]], 0)
+    single = np.array([[0.1, -0.2, 0.3]], np.float32)
+    cases['edge'] = ([lattice, dup, single], 0.03 * 2.75, 50)
+
+    for name, (clouds, r0, limit) in cases.items():
+        pts = np.concatenate(clouds, 0).astype(np.float32)
+        lens = np.array([len(c) for c in clouds], np.int32)
+        dl1 = 2 * r0 / (2.75 if name != 'indoor' else 2.5)
+        sub_pts, sub_lens = ref_subsample_batch(pts, lens, sampleDl=dl1)
+        conv = ref_batch_query(pts, pts, lens, lens, r0)
+        pool = ref_batch_query(sub_pts, pts, sub_lens, lens, r0)
+        up = ref_batch_query(pts, sub_pts, lens, sub_lens, 2 * r0)
+        conv1 = ref_batch_query(sub_pts, sub_pts, sub_lens, sub_lens, 2 * r0)
+        save(f'geom_{name}', points=pts, lengths=lens, dl=np.float64(dl1), r0=np.float64(r0),
+             limit=np.int64(limit), sub_points=sub_pts, sub_lengths=sub_lens,
+             conv=conv, pool=pool, up=up, conv1=conv1)
+
+    # Exact-boundary radius case: supports at |d| == r exactly in float32 must be excluded
+    # (strict d2 < r2, nanoflann.hpp:249-250).
+    r = np.float32(0.25)
+    q = np.zeros((1, 3), np.float32)
+    s = np.array([[0.25, 0, 0], [0, -0.25, 0], [0, 0, 0.2499999], [0.1, 0.1, 0.1], [0.3, 0, 0]],
+                 np.float32)
+    nb = ref_batch_query(q, s, [1], [5], float(r))
+    save('geom_boundary', queries=q, supports=s, radius=np.float64(r), nb=nb)
+
+
+# --------------------------------------------------------------------------------------
+# Module fixtures
+# --------------------------------------------------------------------------------------
+def make_modules(fr, fk):
+    import backbone_kpconv.finegrained_kpconv_blocks as fb
+    from transformer.transformers import TransformerCrossEncoderLayer
+    from transformer.position_embedding import PositionEmbeddingCoordsSine
+    import se3_torch
+
+    g = np.load(os.path.join(HERE, 'geom_modelnet.npz'))
+    pts, lens = g['points'], g['lengths']
+    limit = int(g['limit'])
+    neighb = g['conv'][:, :limit].astype(np.int64)
+    pools = g['pool'][:, :limit].astype(np.int64)
+
+    # ---- KPConv (rigid, linear influence, sum) on the real neighbour table
+    torch.manual_seed(1)
+    np.random.seed(1)
+    cwd = os.getcwd()
+    os.chdir(REF)
+    try:
+        kp = fb.KPConv(15, 3, 16, 24, KP_extent=0.06, radius=0.0825,
+                       fixed_kernel_points='center', KP_influence='linear',
+                       aggregation_mode='sum')
+    finally:
+        os.chdir(cwd)
+    kp.eval()
+    x = torch.randn(len(pts), 16)
+    x[::7] = -x[::7].abs()  # rows whose feature sum is <= 0 do not count (blocks:395-399)
+    with torch.no_grad():
+        out = kp(torch.from_numpy(pts), torch.from_numpy(pts), torch.from_numpy(neighb), x)
+        sub = torch.from_numpy(g['sub_points'])
+        out_strided = kp(sub, torch.from_numpy(pts), torch.from_numpy(pools), x)
+        mp = fb.max_pool(x, torch.from_numpy(pools))
+    save('kpconv_block', q=pts, s=pts, idx=neighb.astype(np.int32), x=x.numpy(), W=kp.weights.detach().numpy(),
+         kp=kp.kernel_points.detach().numpy(), extent=np.float64(kp.KP_extent), out=out.numpy(),
+         sub=g['sub_points'], pools=pools.astype(np.int32), out_strided=out_strided.numpy(), maxpool=mp.numpy())
+
+    # ---- InstanceNorm per cloud (BatchNormBlock, blocks:462-518)
+    bn = fb.BatchNormBlock(24, True, 0.02)
+    y = torch.randn(len(pts), 24) * 3 + 1
+    with torch.no_grad():
+        yn = bn(y, torch.from_numpy(lens.astype(np.int64)))
+    save('instnorm', x=y.numpy(), lengths=lens, out=yn.numpy())
+
+    # ---- Transformer cross-encoder layer (transformers.py:84-258), pre-norm, B=2 unequal
+    torch.manual_seed(2)
+    layer = TransformerCrossEncoderLayer(64, 8, 128, 0.0, activation='relu',
+                                         normalize_before=True, sa_val_has_pos_emb=True,
+                                         ca_val_has_pos_emb=True)
+    layer.eval()
+    with torch.no_grad():
+        for m in (layer.norm1, layer.norm2, layer.norm3):
+            m.weight.copy_(1 + 0.1 * torch.randn(m.weight.shape))
+            m.bias.copy_(0.1 * torch.randn(m.bias.shape))
+    ns, nt = [37, 29], [23, 41]
+    S, T = max(ns), max(nt)
+    src = torch.randn(S, 2, 64)
+    tgt = torch.randn(T, 2, 64)
+    spos = torch.randn(S, 2, 64)
+    tpos = torch.randn(T, 2, 64)
+    smask = torch.zeros(2, S, dtype=torch.bool)
+    tmask = torch.zeros(2, T, dtype=torch.bool)
+    for b in range(2):
+        smask[b, ns[b]:] = True
+        tmask[b, nt[b]:] = True
+    with torch.no_grad():
+        so, to = layer(src, tgt, src_key_padding_mask=smask, tgt_key_padding_mask=tmask,
+                       src_pos=spos, tgt_pos=tpos)
+    sd = {f'w.{k}': v.numpy() for k, v in layer.state_dict().items()}
+    save('transformer_layer', src=src.numpy(), tgt=tgt.numpy(), src_pos=spos.numpy(),
+         tgt_pos=tpos.numpy(), src_mask=smask.numpy(), tgt_mask=tmask.numpy(),
+         src_out=so.numpy(), tgt_out=to.numpy(), **sd)
+
+    # ---- Sine position embedding (position_embedding.py:8-49)
+    pe = PositionEmbeddingCoordsSine(3, 256, scale=1.0)
+    xyz = torch.from_numpy(pts[:100])
+    pe512 = PositionEmbeddingCoordsSine(3, 512, scale=1.0)
+    pe64 = PositionEmbeddingCoordsSine(3, 64, scale=1.0)
+    save('pos_embed', xyz=xyz.numpy(), pe256=pe(xyz).numpy(), pe512=pe512(xyz).numpy(),
+         pe64=pe64(xyz).numpy())
+
+    # ---- Weighted Procrustes (se3_torch.py:131-173, 226-273)
+    rng = np.random.default_rng(3)
+    cases = {}
+    # (a) regular: noisy rigid correspondences, weights partly above 0.85
+    def rigid(n, seed, noise=0.01):
+        r = np.random.default_rng(seed)
+        a = r.uniform(-1, 1, (6, n, 3)).astype(np.float32)
+        from scipy.spatial.transform import Rotation
+        R = Rotation.from_rotvec(r.normal(size=3) * 0.6).as_matrix().astype(np.float32)
+        t = r.normal(size=3).astype(np.float32) * 0.3
+        b = a @ R.T + t + r.normal(scale=noise, size=a.shape).astype(np.float32)
+        return a, b.astype(np.float32)
+    a, b = rigid(200, 4)
+    w = rng.uniform(0.5, 1.0, (6, 200)).astype(np.float32)
+    cases['regular'] = (a, b, w)
+    # (b) reflection: b is a mirrored copy of a -> det(V U^T) < 0 branch
+    a2 = rng.uniform(-1, 1, (6, 50, 3)).astype(np.float32)
+    b2 = a2 * np.array([1, 1, -1], np.float32)
+    w2 = rng.uniform(0.9, 1.0, (6, 50)).astype(np.float32)
+    cases['reflection'] = (a2, b2, w2)
+    # (c) all weights <= 0.85 -> zero covariance -> identity rotation
+    a3, b3 = rigid(64, 5)
+    w3 = rng.uniform(0.0, 0.85, (6, 64)).astype(np.float32)
+    cases['allzero'] = (a3, b3, w3)
+    # (d) weights exactly at the threshold (kept only if strictly greater)
+    a4, b4 = rigid(32, 6)
+    w4 = np.full((6, 32), 0.85, np.float32)
+    w4[:, ::3] = 0.95
+    cases['threshold'] = (a4, b4, w4)
+    out = {}
+    for name, (a_, b_, w_) in cases.items():
+        with torch.no_grad(), cuda_to_cpu():
+            fast = se3_torch.fast_compute_rigid_transform(
+                torch.from_numpy(a_), torch.from_numpy(b_), torch.from_numpy(w_.copy()))
+            full = se3_torch.compute_rigid_transform(
+                torch.from_numpy(a_), torch.from_numpy(b_), torch.from_numpy(w_))
+        out[f'{name}_a'], out[f'{name}_b'], out[f'{name}_w'] = a_, b_, w_
+        out[f'{name}_fast'], out[f'{name}_full'] = fast.numpy(), full.numpy()
+    save('procrustes', **out)
+
+
+# --------------------------------------------------------------------------------------
+# End-to-end forward fixtures
+# --------------------------------------------------------------------------------------
+SMALL_MODELNET = dict(first_feats_dim=32, d_embed=32, d_feedforward=64)
+
+
+def run_forward(fr, fk, cfg, clouds_src, clouds_tgt, bias=4.0, seed=0):
+    torch.manual_seed(seed)
+    np.random.seed(seed)
+    cwd = os.getcwd()
+    os.chdir(REF)
+    try:
+        model = fr.RegTR(cfg)
+    finally:
+        os.chdir(cwd)
+    model.preprocessor = fk.Preprocessor(cfg)  # the reference's own CPU preprocessor
+    with torch.no_grad():
+        model.correspondence_decoder.conf_logits_decoder.bias.fill_(bias)
+        # Non-trivial normalisation statistics, so that BatchNorm folding and LayerNorm
+        # affine terms are exercised (a fresh init has mean 0 / var 1 / weight 1 / bias 0).
+        g = torch.Generator().manual_seed(seed + 123)
+        for m in model.modules():
+            if isinstance(m, torch.nn.BatchNorm1d):
+                m.running_mean.copy_(0.1 * torch.randn(m.running_mean.shape, generator=g))
+                m.running_var.copy_(0.75 + 0.5 * torch.rand(m.running_var.shape, generator=g))
+            if isinstance(m, (torch.nn.BatchNorm1d, torch.nn.LayerNorm)):
+                m.weight.copy_(1 + 0.1 * torch.randn(m.weight.shape, generator=g))
+                m.bias.copy_(0.1 * torch.randn(m.bias.shape, generator=g))
+    model.eval()
+    batch = {'src_xyz': [torch.from_numpy(c) for c in clouds_src],
+             'tgt_xyz': [torch.from_numpy(c) for c in clouds_tgt]}
+    with torch.no_grad(), cuda_to_cpu():
+        out = model(batch)
+    meta = batch['kpconv_meta']
+    return model, meta, out
+
+
+def pack_forward(model, meta, out, cfg_over, clouds_src, clouds_tgt, bias):
+    arrays = {}
+    B = len(clouds_src)
+    for b in range(B):
+        arrays[f'in.src_xyz.{b}'] = clouds_src[b]
+        arrays[f'in.tgt_xyz.{b}'] = clouds_tgt[b]
+    for key in ('points', 'neighbors', 'pools', 'upsamples', 'stack_lengths'):
+        for l, t in enumerate(meta[key]):
+            a = t.numpy()
+            arrays[f'meta.{key}.{l}'] = a.astype(np.int32) if a.dtype == np.int64 else a
+    for k in ('src_feat_un', 'tgt_feat_un', 'src_feat', 'tgt_feat', 'src_kp', 'src_kp_warped',
+              'tgt_kp', 'tgt_kp_warped', 'src_overlap', 'tgt_overlap'):
+        for b, t in enumerate(out[k]):
+            arrays[f'out.{k}.{b}'] = t.numpy()
+    arrays['out.pose'] = out['pose'].numpy()
+    for k, v in model.state_dict().items():
+        if k.startswith('feature_criterion'):
+            continue  # loss-only parameters
+        arrays[f'sd.{k}'] = v.numpy()
+    arrays['cfg_overrides'] = np.array(repr(cfg_over))
+    arrays['bias'] = np.float64(bias)
+    return arrays
+
+
+def make_forward(fr, fk):
+    # (1) reduced-width ModelNet config (same architecture/semantics, small state_dict)
+    cfg = load_cfg('modelnet.yaml', **SMALL_MODELNET)
+    pairs = [modelnet_like_pair(i, n_raw=512) for i in range(2)]
+    src = [p[0] for p in pairs]
+    tgt = [p[1] for p in pairs]
+    model, meta, out = run_forward(fr, fk, cfg, src, tgt)
+    save('forward_modelnet_small', **pack_forward(model, meta, out, SMALL_MODELNET, src, tgt, 4.0))
+
+    # (2) reduced-width 3DMatch config (4 levels, limits 40, d_embed 64)
+    over = dict(first_feats_dim=16, d_embed=32, d_feedforward=64)
+    cfg = load_cfg('3dmatch.yaml', **over)
+    s, t, _ = indoor_like_pair(1, n_points=1500)
+    model, meta, out = run_forward(fr, fk, cfg, [s], [t])
+    save('forward_3dmatch_small', **pack_forward(model, meta, out, over, [s], [t], 4.0))
+
+
+if __name__ == '__main__':
+    fr, fk = import_reference()
+    make_geometry()
+    make_modules(fr, fk)
+    make_forward(fr, fk)
