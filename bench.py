@@ -1,0 +1,195 @@
+#!/usr/bin/env python3
+"""Benchmark: point-cloud pairs/s of the registration forward on MI355X.
+
+Workload (BASELINE.json configs[1] / configs[3]): ModelNet40-like 2048-pt pairs through
+the reference's test transforms (717 + 717 points per pair, fgreg.synthetic), 8 pairs
+per GPU, full RegTR forward (preprocessing, KPConv/Res2Net encoder, 6-layer cross
+encoder, correspondence head, pose) in fp32 with random-init weights of the reference
+ModelNet architecture. One step = one forward over one batch already resident in HBM.
+N GPUs = N processes (torchrun), pairs sharded 8 per rank with no data-path collective
+(weak scaling); each step ends with an RCCL all-gather of the per-pair poses.
+
+Prints ONE JSON line on rank 0 (contract in the task statement), with
+  roofline:     the KPConv gather kernel (HBM-bound): algorithmic bytes per launch /
+                average launch time from HIP events over the timed region;
+  cpu_baseline: the CPU restatement (oracle/model_oracle.py, kind "port") timed on the
+                host cores on a bounded sample of the same workload (rank 0, N = 1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, 'boosting-fine-grained-feature-fusion-in-3d-point-cloud-registration_amd'))
+
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
+FP32_MFMA_PEAK_TFLOPS = 157.3
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument('--gpus', type=int, default=1)
+    p.add_argument('--steps', type=int, default=20)
+    p.add_argument('--warmup', type=int, default=5)
+    p.add_argument('--pairs-per-gpu', type=int, default=8)
+    p.add_argument('--cpu-seconds', type=float, default=10.0,
+                   help='budget of the CPU baseline sample (0 disables it)')
+    p.add_argument('--no-cpu-baseline', action='store_true')
+    return p.parse_args()
+
+
+def _pmc_traffic():
+    """Per-launch HBM bytes of the gather kernel from the committed PMC summary, if any."""
+    path = os.path.join(REPO, 'profiles', 'pmc_kpconv_gather.json')
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f).get('hbm_bytes_per_launch')
+
+
+def main():
+    args = parse()
+    import fgreg
+    from fgreg import ops
+    from fgreg.synthetic import make_batch
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local_rank = int(os.environ.get('LOCAL_RANK', '0'))
+    if world != args.gpus:
+        raise SystemExit(f'--gpus {args.gpus} but WORLD_SIZE={world}')
+    torch.cuda.set_device(local_rank)
+    dev = torch.device('cuda', local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group('nccl', device_id=dev)
+
+    cfg = fgreg.config.get('modelnet')
+    torch.manual_seed(0)
+    np.random.seed(0)
+    model = fgreg.RegTR(cfg).to(dev).eval()
+    P = args.pairs_per_gpu
+    src, tgt, _ = make_batch('modelnet', P, start=rank * P)     # this rank's shard of pairs
+    batch_src = [torch.from_numpy(s).to(dev) for s in src]
+    batch_tgt = [torch.from_numpy(t).to(dev) for t in tgt]
+    gathered = [torch.empty((6, P, 3, 4), device=dev) for _ in range(world)] if world > 1 else None
+
+    def step():
+        out = model({'src_xyz': batch_src, 'tgt_xyz': batch_tgt})
+        if dist is not None:
+            dist.all_gather(gathered, out['pose'].contiguous())
+        return out
+
+    with torch.no_grad():
+        for _ in range(max(args.warmup, 1)):
+            step()
+        # algorithmic work per launch (untimed pass with counting on)
+        timer = ops.KernelTimer(['kpconv_gather', 'attention'])
+        timer.count = True
+        ops.TIMER = timer
+        step()
+        torch.cuda.synchronize()
+        gather_bytes = list(timer.work['kpconv_gather'])
+        attn_flops = list(timer.work['attention'])
+        timer.count = False
+        timer.reset_events()
+
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        ops.TIMER = None
+
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if dist is not None:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+
+    g_ms = timer.total_ms('kpconv_gather')
+    g_launches = len(timer.events['kpconv_gather'])
+    a_ms = timer.total_ms('attention')
+    a_launches = len(timer.events['attention'])
+    g_bytes_step = float(sum(gather_bytes))
+    a_flops_step = float(sum(attn_flops))
+    g_avg_s = g_ms / 1e3 / max(g_launches, 1)
+    g_bytes_launch = g_bytes_step / max(len(gather_bytes), 1)
+    g_achieved = g_bytes_launch / g_avg_s / 1e9 if g_avg_s > 0 else 0.0
+    a_achieved = a_flops_step * args.steps / (a_ms / 1e3) / 1e12 if a_ms > 0 else 0.0
+    traffic = _pmc_traffic()
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_seconds > 0:
+        cpu = cpu_baseline(cfg, model, src, tgt, args.cpu_seconds)
+
+    if rank == 0:
+        pairs = world * P * args.steps
+        line = {
+            'metric': 'point-cloud pairs/sec (forward) on ModelNet 2048-pt pairs',
+            'value': pairs / elapsed,
+            'unit': 'pairs/s',
+            'n_gpus': world,
+            'steps': args.steps,
+            'warmup': args.warmup,
+            'ms_per_step': elapsed / args.steps * 1e3,
+            'higher_is_better': True,
+            'scaling': 'weak',
+            'vs_baseline': None,
+            'dtype': 'f32',
+            'data': 'synthetic ModelNet-like pairs (box surfaces, 2048 raw pts -> crop 0.7 -> '
+                    '717+717 pts), random-init weights of the reference ModelNet architecture',
+            'config': {'workload': 'ModelNet40 2048-pt pairs, 8 pairs per GPU (BASELINE configs[1]'
+                                   ' at N=1, configs[3] at N=8)',
+                       'pairs_per_gpu': P, 'global_batch': P * world, 'points_per_cloud': 717,
+                       'parallelism': f'pair-sharded dp{world}'},
+            'roofline': {'kernel': 'fgr_kpconv_gather', 'bound': 'hbm',
+                         'achieved': g_achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                         'frac': g_achieved / HBM_PEAK_GBS, 'traffic': traffic,
+                         'algorithmic_bytes_per_launch': g_bytes_launch,
+                         'avg_launch_us': g_avg_s * 1e6, 'launches_per_step': len(gather_bytes),
+                         'share_of_step': g_ms / (elapsed * 1e3)},
+            'roofline_attention': {'kernel': 'fgr_attention', 'bound': 'mfma',
+                                   'achieved': a_achieved, 'peak': FP32_MFMA_PEAK_TFLOPS,
+                                   'unit': 'TFLOP/s', 'frac': a_achieved / FP32_MFMA_PEAK_TFLOPS,
+                                   'flops_per_step': a_flops_step,
+                                   'avg_launch_us': a_ms * 1e3 / max(a_launches, 1),
+                                   'share_of_step': a_ms / (elapsed * 1e3)},
+            'cpu_baseline': cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(cfg, model, src, tgt, budget_s):
+    """CPU restatement (oracle/model_oracle.py, "port") on the same pairs, for ~budget_s."""
+    sys.path.insert(0, os.path.join(REPO, 'oracle'))
+    import model_oracle as mo
+    sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    threads = torch.get_num_threads()
+    n_pairs, t_tot, it = 0, 0.0, 0
+    while t_tot < budget_s and it < 64:
+        b = it % len(src)
+        t0 = time.perf_counter()
+        mo.forward(cfg, sd, [src[b]], [tgt[b]], mode=mo.geom.INDEX)
+        t_tot += time.perf_counter() - t0
+        n_pairs += 1
+        it += 1
+    return {'value': n_pairs / t_tot, 'unit': 'pairs/s', 'cores': threads, 'kind': 'port',
+            'sample': f'{n_pairs} ModelNet-like pairs (B=1 forwards) of the same workload, '
+                      f'{t_tot:.1f} s, torch CPU fp32 with {threads} threads'}
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,202 @@
+// Fused multi-head attention (flash-style, online softmax) on packed, unpadded
+// segments, fp32 in / fp32 accumulate on the CDNA4 matrix cores
+// (v_mfma_f32_16x16x4_f32: exact fp32 products, one rounding per FMA).
+//
+// Replaces the core of nn.MultiheadAttention as used by the reference's cross
+// encoder (transformers.py:95-96, 197-226): o = softmax((q * scale) k^T + mask) v
+// with the key padding mask expressed as the end of the key segment.
+//
+// Work decomposition: block = 4 waves = 64 query rows of one (segment, head);
+// each wave owns 16 rows. K/V tiles of 64 keys are staged in LDS and shared by the
+// 4 waves. S = Q K^T and O += P V run on 16x16x4 MFMAs; P crosses LDS once to be
+// re-read in the A-operand layout.
+//
+// MFMA 16x16x4 f32 lane maps (lane l, g = l >> 4, c = l & 15):
+//   A[i = c][k = g], B[k = g][j = c], C/D[row = 4g + r][col = c], r = 0..3.
+#include "common.h"
+
+namespace fgr {
+namespace {
+
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+
+constexpr int kBQ = 64;   // query rows per block
+constexpr int kBK = 64;   // keys per tile
+
+template <int DH>
+__global__ void __launch_bounds__(256)
+attn_fwd_kernel(const float* __restrict__ q, int64_t ld_q, const float* __restrict__ k,
+                int64_t ld_k, const float* __restrict__ v, int64_t ld_v, float* __restrict__ o,
+                int64_t ld_o, const int64_t* __restrict__ q_off, const int64_t* __restrict__ kv_off,
+                const int32_t* __restrict__ kv_seg, float scale) {
+    constexpr int KS = DH / 4;                       // k-steps of S
+    constexpr int NT = DH < 16 ? 1 : DH / 16;        // 16-wide output column tiles
+    constexpr int LDK = DH + 1;
+    constexpr int LDP = kBK + 4;
+    __shared__ float k_lds[kBK * LDK];
+    __shared__ float v_lds[kBK * LDK];
+    __shared__ float p_lds[4][16 * LDP];
+
+    const int seg = blockIdx.z, head = blockIdx.y;
+    const int64_t qb = q_off[seg], qe = q_off[seg + 1];
+    const int64_t q0 = qb + (int64_t)blockIdx.x * kBQ;
+    if (q0 >= qe) return;                              // block-uniform
+    const int ks = kv_seg[seg];
+    const int64_t kb = kv_off[ks], ke = kv_off[ks + 1];
+    const int nk = (int)(ke - kb);
+
+    const int tid = threadIdx.x, wv = tid / 64, lane = tid % 64;
+    const int g = lane >> 4, c = lane & 15;
+    const int64_t my_q = q0 + wv * 16 + c;             // A-operand row of this lane
+    const bool q_ok = my_q < qe;
+
+    // Q fragment (pre-scaled like the reference's q * sqrt(1/E))
+    float qf[KS];
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk)
+        qf[kk] = q_ok ? q[my_q * ld_q + head * DH + kk * 4 + g] * scale : 0.f;
+
+    f32x4 acc_o[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc_o[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m_run[4], l_run[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { m_run[r] = -INFINITY; l_run[r] = 0.f; }
+
+    for (int k0 = 0; k0 < nk; k0 += kBK) {
+        const int nt = min(kBK, nk - k0);
+        __syncthreads();
+        for (int e = tid; e < kBK * DH; e += 256) {
+            const int key = e / DH, d = e - key * DH;
+            float kv = 0.f, vv = 0.f;
+            if (key < nt) {
+                const int64_t row = kb + k0 + key;
+                kv = k[row * ld_k + head * DH + d];
+                vv = v[row * ld_v + head * DH + d];
+            }
+            k_lds[key * LDK + d] = kv;
+            v_lds[key * LDK + d] = vv;
+        }
+        __syncthreads();
+
+        // S tile (16 rows x 64 keys per wave) = 4 MFMA column tiles
+        f32x4 s[4];
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+            s[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kk = 0; kk < KS; ++kk) {
+                const float b = k_lds[(n * 16 + c) * LDK + kk * 4 + g];
+                s[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(qf[kk], b, s[n], 0, 0, 0);
+            }
+        }
+        // key padding -> -inf; online softmax per row 4g + r
+        float alpha[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            float mx = -INFINITY;
+#pragma unroll
+            for (int n = 0; n < 4; ++n) {
+                if (n * 16 + c >= nt) s[n][r] = -INFINITY;
+                mx = fmaxf(mx, s[n][r]);
+            }
+#pragma unroll
+            for (int o2 = 8; o2 > 0; o2 >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o2, 64));
+            const float m_new = fmaxf(m_run[r], mx);
+            const float m_use = m_new == -INFINITY ? 0.f : m_new;
+            alpha[r] = expf(m_run[r] - m_use);
+            float rs = 0.f;
+#pragma unroll
+            for (int n = 0; n < 4; ++n) {
+                const float p = expf(s[n][r] - m_use);
+                s[n][r] = p;
+                rs += p;
+            }
+#pragma unroll
+            for (int o2 = 8; o2 > 0; o2 >>= 1) rs += __shfl_xor(rs, o2, 64);
+            l_run[r] = l_run[r] * alpha[r] + rs;
+            m_run[r] = m_new;
+        }
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc_o[t][r] *= alpha[r];
+
+        // P: C layout -> LDS -> A layout
+        float* pw = p_lds[wv];
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) pw[(4 * g + r) * LDP + n * 16 + c] = s[n][r];
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int kk = 0; kk < kBK / 4; ++kk) {
+            const float a = pw[c * LDP + kk * 4 + g];
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                const int col = t * 16 + c;
+                const float b = col < DH ? v_lds[(kk * 4 + g) * LDK + col] : 0.f;
+                acc_o[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc_o[t], 0, 0, 0);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+
+    // O / l -> rows 4g + r, cols t*16 + c
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int64_t row = q0 + wv * 16 + 4 * g + r;
+        if (row >= qe) continue;
+        const float inv = 1.0f / l_run[r];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const int col = t * 16 + c;
+            if (col < DH) o[row * ld_o + head * DH + col] = acc_o[t][r] * inv;
+        }
+    }
+}
+
+template <int DH>
+void launch(dim3 grid, hipStream_t st, const float* q, int64_t ld_q, const float* k, int64_t ld_k,
+            const float* v, int64_t ld_v, float* o, int64_t ld_o, const int64_t* q_off,
+            const int64_t* kv_off, const int32_t* kv_seg, float scale) {
+    hipLaunchKernelGGL(attn_fwd_kernel<DH>, grid, dim3(256), 0, st, q, ld_q, k, ld_k, v, ld_v, o,
+                       ld_o, q_off, kv_off, kv_seg, scale);
+}
+
+}  // namespace
+}  // namespace fgr
+
+using namespace fgr;
+
+extern "C" int fgr_attention(const float* q, int64_t ld_q, const float* k, int64_t ld_k,
+                             const float* v, int64_t ld_v, float* o, int64_t ld_o,
+                             const int64_t* q_off, const int64_t* kv_off, const int32_t* kv_seg,
+                             int32_t n_seg, int32_t max_q_len, int32_t n_head, int32_t head_dim,
+                             float scale, void* stream) {
+    FGR_REQUIRE(q && k && v && o && q_off && kv_off && kv_seg && n_seg > 0 && n_head > 0 &&
+                    max_q_len >= 0,
+                "fgr_attention: bad arguments");
+    FGR_REQUIRE(ld_q >= n_head * head_dim && ld_k >= n_head * head_dim &&
+                    ld_v >= n_head * head_dim && ld_o >= n_head * head_dim,
+                "fgr_attention: row stride smaller than n_head * head_dim");
+    if (max_q_len == 0) return FGR_OK;
+    dim3 grid((unsigned)ceil_div(max_q_len, kBQ), (unsigned)n_head, (unsigned)n_seg);
+    hipStream_t st = as_stream(stream);
+    switch (head_dim) {
+        case 4: launch<4>(grid, st, q, ld_q, k, ld_k, v, ld_v, o, ld_o, q_off, kv_off, kv_seg, scale); break;
+        case 8: launch<8>(grid, st, q, ld_q, k, ld_k, v, ld_v, o, ld_o, q_off, kv_off, kv_seg, scale); break;
+        case 16: launch<16>(grid, st, q, ld_q, k, ld_k, v, ld_v, o, ld_o, q_off, kv_off, kv_seg, scale); break;
+        case 32: launch<32>(grid, st, q, ld_q, k, ld_k, v, ld_v, o, ld_o, q_off, kv_off, kv_seg, scale); break;
+        case 64: launch<64>(grid, st, q, ld_q, k, ld_k, v, ld_v, o, ld_o, q_off, kv_off, kv_seg, scale); break;
+        case 128: launch<128>(grid, st, q, ld_q, k, ld_k, v, ld_v, o, ld_o, q_off, kv_off, kv_seg, scale); break;
+        case 256: launch<256>(grid, st, q, ld_q, k, ld_k, v, ld_v, o, ld_o, q_off, kv_off, kv_seg, scale); break;
+        default:
+            set_error("fgr_attention: head_dim %d unsupported (4, 8, 16, 32, 64, 128, 256)", head_dim);
+            return FGR_E_ARG;
+    }
+    FGR_CHECK_LAUNCH("attn_fwd_kernel");
+    return FGR_OK;
+}

@@ -1,0 +1,71 @@
+// Shared helpers for the libfgreg kernels (gfx950 / CDNA4, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "../../include/fgreg.h"
+
+namespace fgr {
+
+// Per-thread last-error string (the only mutable global state of the library).
+void set_error(const char* fmt, ...);
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Checks a kernel launch / runtime call; on failure records a message and returns.
+#define FGR_CHECK_LAUNCH(what)                                                        \
+    do {                                                                              \
+        hipError_t e_ = hipGetLastError();                                            \
+        if (e_ != hipSuccess) {                                                       \
+            ::fgr::set_error("%s: %s", what, hipGetErrorString(e_));                  \
+            return FGR_E_LAUNCH;                                                      \
+        }                                                                             \
+    } while (0)
+
+#define FGR_CHECK_HIP(call)                                                           \
+    do {                                                                              \
+        hipError_t e_ = (call);                                                       \
+        if (e_ != hipSuccess) {                                                       \
+            ::fgr::set_error("%s: %s", #call, hipGetErrorString(e_));                 \
+            return FGR_E_LAUNCH;                                                      \
+        }                                                                             \
+    } while (0)
+
+#define FGR_REQUIRE(cond, ...)                                                        \
+    do {                                                                              \
+        if (!(cond)) {                                                                \
+            ::fgr::set_error(__VA_ARGS__);                                            \
+            return FGR_E_ARG;                                                         \
+        }                                                                             \
+    } while (0)
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+    return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
+    return v;
+}
+
+// Index of the segment containing row r, given sorted offsets off[0..n] (off[0] = 0).
+__device__ __forceinline__ int find_segment(const int64_t* off, int n, int64_t r) {
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+        int mid = (lo + hi + 1) >> 1;
+        if (off[mid] <= r) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+}  // namespace fgr

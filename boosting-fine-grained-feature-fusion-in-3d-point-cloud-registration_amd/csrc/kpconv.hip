@@ -1,0 +1,272 @@
+// KPConv gather-weight stage and max-pool shortcut on gfx950.
+//
+// fgr_kpconv_gather computes, for every query q,
+//   wf[q, k, c] = sum_{valid h} w(q, h, k) * x[idx[q, h], c],
+//   w(q, h, k)  = max(0, 1 - sqrt(|(s[idx[q,h]] - q) - kp[k]|^2) / extent)
+// (finegrained_kpconv_blocks.py:296-381) and the KPConv normaliser
+//   nnorm[q] = max(1, #{valid h : sum_c x[idx[q, h], c] > 0})            (:395-399).
+// Shadow entries (idx >= ns) carry zero weight and a zero feature row in the
+// reference, so they are skipped here: only valid neighbours are read.
+//
+// HBM-bound. Per query the algorithmic traffic is
+//   8*width (idx row) + 12 (q) + v*(12 + 4*cin) (valid neighbour xyz + feature row)
+//   + 4*K*cin (wf row) + 4 (nnorm),
+// dominated by the wf write. Wide-channel layers (cin % 64 == 0) run one wave per
+// query with channels on lanes (VEC contiguous floats per lane -> 16-B loads/stores);
+// narrow layers (cin < 64) run one thread per (query, kernel point).
+#include "common.h"
+
+namespace fgr {
+namespace {
+
+constexpr int kMaxKp = 32;         // kernel points supported (configs use 15)
+constexpr int kGatherWaves = 4;    // waves (= queries) per block, wide kernel
+
+template <int VEC>
+struct VecT;
+template <> struct VecT<1> { using T = float; };
+template <> struct VecT<2> { using T = float2; };
+template <> struct VecT<4> { using T = float4; };
+
+template <int VEC>
+__device__ __forceinline__ void load_vec(const float* p, float (&v)[VEC]) {
+    if constexpr (VEC == 1) {
+        v[0] = p[0];
+    } else if constexpr (VEC == 2) {
+        float2 t = *reinterpret_cast<const float2*>(p);
+        v[0] = t.x; v[1] = t.y;
+    } else {
+#pragma unroll
+        for (int j = 0; j < VEC; j += 4) {
+            float4 t = *reinterpret_cast<const float4*>(p + j);
+            v[j] = t.x; v[j + 1] = t.y; v[j + 2] = t.z; v[j + 3] = t.w;
+        }
+    }
+}
+
+template <int VEC>
+__device__ __forceinline__ void store_vec(float* p, const float (&v)[VEC]) {
+    if constexpr (VEC == 1) {
+        p[0] = v[0];
+    } else if constexpr (VEC == 2) {
+        *reinterpret_cast<float2*>(p) = make_float2(v[0], v[1]);
+    } else {
+#pragma unroll
+        for (int j = 0; j < VEC; j += 4)
+            *reinterpret_cast<float4*>(p + j) = make_float4(v[j], v[j + 1], v[j + 2], v[j + 3]);
+    }
+}
+
+__device__ __forceinline__ float kp_weight(float nx, float ny, float nz, const float* kp, int k,
+                                           float inv_extent) {
+    float dx = nx - kp[3 * k], dy = ny - kp[3 * k + 1], dz = nz - kp[3 * k + 2];
+    float d2 = dx * dx + dy * dy + dz * dz;
+    return fmaxf(1.0f - sqrtf(d2) * inv_extent, 0.0f);
+}
+
+// One wave per query, cin = 64 * VEC, K kernel points (runtime, <= kMaxKp, unrolled by KU).
+template <int VEC, int KU>
+__global__ void __launch_bounds__(64 * kGatherWaves)
+kpconv_gather_wide(const float* __restrict__ q, const float* __restrict__ s, int64_t nq, int64_t ns,
+                   const int64_t* __restrict__ idx, int width, const float* __restrict__ x,
+                   const float* __restrict__ kp_g, int n_kp, float inv_extent,
+                   float* __restrict__ wf, float* __restrict__ nnorm) {
+    constexpr int CIN = 64 * VEC;
+    __shared__ float w_lds[kGatherWaves][64][KU];
+    __shared__ int nb_lds[kGatherWaves][64];
+    __shared__ float kp[3 * kMaxKp];
+    const int wv = threadIdx.x / 64, lane = threadIdx.x % 64;
+    for (int i = threadIdx.x; i < 3 * n_kp; i += blockDim.x) kp[i] = kp_g[i];
+    __syncthreads();
+    const int64_t qi = (int64_t)blockIdx.x * kGatherWaves + wv;
+    if (qi >= nq) return;
+    const float qx = q[3 * qi], qy = q[3 * qi + 1], qz = q[3 * qi + 2];
+
+    float acc[KU][VEC];
+#pragma unroll
+    for (int k = 0; k < KU; ++k)
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) acc[k][j] = 0.f;
+    int n_pos = 0;
+    const int64_t* row = idx + qi * width;
+
+    for (int h0 = 0; h0 < width; h0 += 64) {
+        // compact the valid neighbours of this 64-wide chunk (wave ballot)
+        const int h = h0 + lane;
+        const int64_t id = h < width ? row[h] : ns;
+        const bool valid = id >= 0 && id < ns;
+        const unsigned long long m = __ballot(valid);
+        const int v = __popcll(m);
+        if (v == 0) continue;
+        const int pos = __popcll(m & ((1ull << lane) - 1ull));
+        if (valid) nb_lds[wv][pos] = (int)id;
+        __builtin_amdgcn_wave_barrier();
+        // kernel-point influences of the valid neighbours -> LDS
+        for (int t = lane; t < v * n_kp; t += 64) {
+            const int hh = t / n_kp, k = t - hh * n_kp;
+            const int sid = nb_lds[wv][hh];
+            // neighbours are centred first, then compared with the kernel points (:302, :313)
+            const float nx = s[3 * sid] - qx, ny = s[3 * sid + 1] - qy, nz = s[3 * sid + 2] - qz;
+            w_lds[wv][hh][k] = kp_weight(nx, ny, nz, kp, k, inv_extent);
+        }
+        __builtin_amdgcn_wave_barrier();
+        for (int hh = 0; hh < v; ++hh) {
+            const int sid = nb_lds[wv][hh];
+            float xv[VEC];
+            load_vec<VEC>(x + (int64_t)sid * CIN + lane * VEC, xv);
+            float rs = 0.f;
+#pragma unroll
+            for (int j = 0; j < VEC; ++j) rs += xv[j];
+            rs = wave_sum(rs);
+            n_pos += rs > 0.f ? 1 : 0;
+#pragma unroll
+            for (int k = 0; k < KU; ++k) {
+                if (k < n_kp) {
+                    const float w = w_lds[wv][hh][k];
+#pragma unroll
+                    for (int j = 0; j < VEC; ++j) acc[k][j] = fmaf(w, xv[j], acc[k][j]);
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    float* out = wf + qi * (int64_t)n_kp * CIN + lane * VEC;
+#pragma unroll
+    for (int k = 0; k < KU; ++k)
+        if (k < n_kp) store_vec<VEC>(out + (int64_t)k * CIN, acc[k]);
+    if (lane == 0) nnorm[qi] = (float)(n_pos > 1 ? n_pos : 1);
+}
+
+// One thread per (query, kernel point); cin <= 64 (narrow layers, incl. the cin = 1 stem).
+template <int CMAX>
+__global__ void __launch_bounds__(256)
+kpconv_gather_narrow(const float* __restrict__ q, const float* __restrict__ s, int64_t nq,
+                     int64_t ns, const int64_t* __restrict__ idx, int width,
+                     const float* __restrict__ x, int cin, const float* __restrict__ kp_g,
+                     int n_kp, float inv_extent, float* __restrict__ wf,
+                     float* __restrict__ nnorm) {
+    __shared__ float kp[3 * kMaxKp];
+    for (int i = threadIdx.x; i < 3 * n_kp; i += blockDim.x) kp[i] = kp_g[i];
+    __syncthreads();
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nq * n_kp) return;
+    const int64_t qi = t / n_kp;
+    const int k = (int)(t - qi * n_kp);
+    const float qx = q[3 * qi], qy = q[3 * qi + 1], qz = q[3 * qi + 2];
+    float acc[CMAX];
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c) acc[c] = 0.f;
+    int n_pos = 0;
+    const int64_t* row = idx + qi * width;
+    for (int h = 0; h < width; ++h) {
+        const int64_t id = row[h];
+        if (id < 0 || id >= ns) continue;
+        const float nx = s[3 * id] - qx, ny = s[3 * id + 1] - qy, nz = s[3 * id + 2] - qz;
+        const float w = kp_weight(nx, ny, nz, kp, k, inv_extent);
+        const float* xr = x + id * cin;
+        float rs = 0.f;
+#pragma unroll
+        for (int c = 0; c < CMAX; ++c) {
+            if (c < cin) {
+                const float xv = xr[c];
+                rs += xv;
+                acc[c] = fmaf(w, xv, acc[c]);
+            }
+        }
+        n_pos += rs > 0.f ? 1 : 0;
+    }
+    float* out = wf + t * cin;
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c)
+        if (c < cin) out[c] = acc[c];
+    if (k == 0) nnorm[qi] = (float)(n_pos > 1 ? n_pos : 1);
+}
+
+template <int CMAX>
+void launch_narrow(const float* q, const float* s, int64_t nq, int64_t ns, const int64_t* idx,
+                   int width, const float* x, int cin, const float* kp, int n_kp, float inv_ext,
+                   float* wf, float* nnorm, hipStream_t st) {
+    const int64_t n = nq * n_kp;
+    hipLaunchKernelGGL(kpconv_gather_narrow<CMAX>, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0,
+                       st, q, s, nq, ns, idx, width, x, cin, kp, n_kp, inv_ext, wf, nnorm);
+}
+
+template <int VEC>
+void launch_wide(const float* q, const float* s, int64_t nq, int64_t ns, const int64_t* idx,
+                 int width, const float* x, const float* kp, int n_kp, float inv_ext, float* wf,
+                 float* nnorm, hipStream_t st) {
+    dim3 grid((unsigned)ceil_div(nq, kGatherWaves));
+    if (n_kp <= 16)
+        hipLaunchKernelGGL((kpconv_gather_wide<VEC, 16>), grid, dim3(64 * kGatherWaves), 0, st, q,
+                           s, nq, ns, idx, width, x, kp, n_kp, inv_ext, wf, nnorm);
+    else
+        hipLaunchKernelGGL((kpconv_gather_wide<VEC, kMaxKp>), grid, dim3(64 * kGatherWaves), 0,
+                           st, q, s, nq, ns, idx, width, x, kp, n_kp, inv_ext, wf, nnorm);
+}
+
+// max_pool: one thread per (query, channel); shadows contribute the appended zero row.
+__global__ void max_pool_kernel(const float* __restrict__ x, int64_t ns, int c,
+                                const int64_t* __restrict__ idx, int64_t nq, int width,
+                                float* __restrict__ out) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nq * c) return;
+    const int64_t qi = t / c;
+    const int ch = (int)(t - qi * c);
+    const int64_t* row = idx + qi * width;
+    float m = -INFINITY;
+    for (int h = 0; h < width; ++h) {
+        const int64_t id = row[h];
+        const float v = (id >= 0 && id < ns) ? x[id * c + ch] : 0.f;
+        m = fmaxf(m, v);
+    }
+    out[t] = m;
+}
+
+}  // namespace
+}  // namespace fgr
+
+using namespace fgr;
+
+extern "C" int fgr_kpconv_gather(const float* q, const float* s, int64_t nq, int64_t ns,
+                                 const int64_t* idx, int32_t width, const float* x, int32_t cin,
+                                 const float* kp, int32_t n_kp, float extent, float* wf,
+                                 float* nnorm, void* stream) {
+    FGR_REQUIRE(nq >= 0 && ns >= 0 && width >= 0 && cin > 0 && n_kp > 0 && n_kp <= kMaxKp &&
+                    extent > 0.f,
+                "fgr_kpconv_gather: bad arguments (cin %d, n_kp %d, width %d)", cin, n_kp, width);
+    FGR_REQUIRE(nq == 0 || (q && s && x && kp && wf && nnorm && (idx || width == 0)),
+                "fgr_kpconv_gather: null pointer");
+    if (nq == 0) return FGR_OK;
+    hipStream_t st = as_stream(stream);
+    const float inv_ext = 1.0f / extent;
+    if (cin % 64 == 0 && cin <= 256) {
+        switch (cin / 64) {
+            case 1: launch_wide<1>(q, s, nq, ns, idx, width, x, kp, n_kp, inv_ext, wf, nnorm, st); break;
+            case 2: launch_wide<2>(q, s, nq, ns, idx, width, x, kp, n_kp, inv_ext, wf, nnorm, st); break;
+            default: launch_wide<4>(q, s, nq, ns, idx, width, x, kp, n_kp, inv_ext, wf, nnorm, st); break;
+        }
+    } else if (cin <= 64) {
+        if (cin == 1) launch_narrow<1>(q, s, nq, ns, idx, width, x, cin, kp, n_kp, inv_ext, wf, nnorm, st);
+        else if (cin <= 8) launch_narrow<8>(q, s, nq, ns, idx, width, x, cin, kp, n_kp, inv_ext, wf, nnorm, st);
+        else if (cin <= 16) launch_narrow<16>(q, s, nq, ns, idx, width, x, cin, kp, n_kp, inv_ext, wf, nnorm, st);
+        else if (cin <= 32) launch_narrow<32>(q, s, nq, ns, idx, width, x, cin, kp, n_kp, inv_ext, wf, nnorm, st);
+        else launch_narrow<64>(q, s, nq, ns, idx, width, x, cin, kp, n_kp, inv_ext, wf, nnorm, st);
+    } else {
+        set_error("fgr_kpconv_gather: cin %d unsupported (need <= 64 or a multiple of 64 <= 256)", cin);
+        return FGR_E_ARG;
+    }
+    FGR_CHECK_LAUNCH("kpconv_gather");
+    return FGR_OK;
+}
+
+extern "C" int fgr_max_pool(const float* x, int64_t ns, int32_t c, const int64_t* idx, int64_t nq,
+                            int32_t width, float* out, void* stream) {
+    FGR_REQUIRE(ns >= 0 && c > 0 && nq >= 0 && width > 0, "fgr_max_pool: bad arguments");
+    FGR_REQUIRE(nq == 0 || (x && idx && out), "fgr_max_pool: null pointer");
+    if (nq == 0) return FGR_OK;
+    const int64_t n = nq * c;
+    hipLaunchKernelGGL(max_pool_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0,
+                       as_stream(stream), x, ns, c, idx, nq, width, out);
+    FGR_CHECK_LAUNCH("max_pool_kernel");
+    return FGR_OK;
+}

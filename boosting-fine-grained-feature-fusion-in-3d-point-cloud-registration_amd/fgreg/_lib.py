@@ -1,0 +1,78 @@
+"""Loader of libfgreg.so (the C ABI declared in include/fgreg.h).
+
+The library is built in-tree (csrc/Makefile -> fgreg/libfgreg.so) and loaded with
+ctypes; torch tensors cross the boundary only as raw device pointers. There is no
+fallback: if the library is missing, or no GPU is visible, every op raises.
+"""
+import ctypes
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, 'libfgreg.so')
+CSRC = os.path.join(os.path.dirname(HERE), 'csrc')
+
+_vp = ctypes.c_void_p
+_i32 = ctypes.c_int32
+_i64 = ctypes.c_int64
+_f32 = ctypes.c_float
+_sz = ctypes.c_size_t
+
+# name -> argtypes (all return int status)
+SIGNATURES = {
+    'fgr_grid_subsample_workspace': [_i64, _i32, ctypes.POINTER(_sz)],
+    'fgr_grid_subsample_count': [_vp, _vp, _i32, _i64, _f32, _vp, _sz, _vp, _vp],
+    'fgr_grid_subsample_fill': [_i64, _i32, _i64, _vp, _sz, _vp, _vp, _vp, _vp],
+    'fgr_radius_count': [_vp, _vp, _vp, _vp, _i32, _i64, _i32, _f32, _vp, _vp, _vp],
+    'fgr_radius_search': [_vp, _vp, _vp, _vp, _i32, _i64, _i64, _i32, _f32, _i32, _i32, _vp, _vp],
+    'fgr_kpconv_gather': [_vp, _vp, _i64, _i64, _vp, _i32, _vp, _i32, _vp, _i32, _f32, _vp, _vp,
+                          _vp],
+    'fgr_max_pool': [_vp, _i64, _i32, _vp, _i64, _i32, _vp, _vp],
+    'fgr_instnorm': [_vp, _i64, _i32, _vp, _i32, _vp, _f32, _i32, _vp, _i32, _vp, _vp],
+    'fgr_layernorm': [_vp, _i64, _i32, _vp, _vp, _f32, _vp, _vp, _vp],
+    'fgr_sine_pos_embed': [_vp, _i64, _i32, _f32, _f32, _vp, _vp],
+    'fgr_attention': [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i32, _i32, _i32,
+                      _i32, _f32, _vp],
+    'fgr_procrustes': [_vp, _vp, _vp, _i64, _i64, _f32, _vp, _vp],
+    'fgr_pair_pose': [_vp, _vp, _vp, _i64, _vp, _i32, _i32, _f32, _vp, _vp],
+}
+
+NB_INDEX, NB_DIST = 0, 1
+ACT_NONE, ACT_LEAKY, ACT_RELU = 0, 1, 2
+
+_lib = None
+
+
+class FgrError(RuntimeError):
+    pass
+
+
+def build(jobs=8):
+    """Compile csrc/ into fgreg/libfgreg.so for gfx950 (hipcc cross-compiles without a GPU)."""
+    subprocess.check_call(['make', '-s', '-C', CSRC, f'-j{jobs}'])
+
+
+def load():
+    """Returns the ctypes handle, raising FgrError if the library cannot be loaded."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise FgrError(f'{LIB_PATH} not built: run `make -C {CSRC}` (or __graft_entry__.build())')
+    L = ctypes.CDLL(LIB_PATH)
+    L.fgr_abi_version.restype = ctypes.c_int
+    L.fgr_last_error.restype = ctypes.c_char_p
+    for name, argtypes in SIGNATURES.items():
+        fn = getattr(L, name)
+        fn.restype = ctypes.c_int
+        fn.argtypes = argtypes
+    if L.fgr_abi_version() != 1:
+        raise FgrError('libfgreg ABI version mismatch')
+    _lib = L
+    return L
+
+
+def check(rc, name):
+    if rc != 0:
+        msg = load().fgr_last_error().decode(errors='replace')
+        raise FgrError(f'{name} failed ({rc}): {msg}')

@@ -1,0 +1,329 @@
+"""Torch-facing wrappers of the libfgreg kernels.
+
+Every function takes CUDA(HIP) tensors, validates shapes on the host (a kernel is
+never launched on operands that do not match what it assumes), allocates the
+outputs with the torch caching allocator and launches on torch's current stream.
+There is deliberately no CPU path: on a tensor that is not on a GPU, or without
+libfgreg.so, these raise.
+"""
+import math
+from typing import Sequence, Tuple
+
+import torch
+
+from . import _lib
+from ._lib import ACT_LEAKY, ACT_NONE, ACT_RELU, NB_DIST, NB_INDEX  # noqa: F401
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+class KernelTimer:
+    """Optional per-op instrumentation for bench.py: HIP events recorded on the launch
+    stream around each launch of the named ops, plus the algorithmic bytes / flops of
+    every launch (computed only while ``count`` is on, outside any timed region)."""
+
+    def __init__(self, names):
+        self.names = set(names)
+        self.events = {n: [] for n in names}
+        self.work = {n: [] for n in names}
+        self.count = False
+
+    def begin(self, name):
+        if name not in self.names:
+            return None
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        return ev
+
+    def end(self, name, start, work=None):
+        if start is None:
+            return
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        self.events[name].append((start, ev))
+        if self.count and work is not None:
+            self.work[name].append(work() if callable(work) else work)
+
+    def reset_events(self):
+        self.events = {n: [] for n in self.names}
+
+    def total_ms(self, name):
+        return sum(a.elapsed_time(b) for a, b in self.events[name])
+
+
+TIMER = None  # set to a KernelTimer to instrument
+
+
+def _begin(name):
+    return TIMER.begin(name) if TIMER is not None else None
+
+
+def _end(name, start, work=None):
+    if TIMER is not None:
+        TIMER.end(name, start, work)
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _dev(*tensors):
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise _lib.FgrError('fgreg ops need GPU tensors (no CPU fallback by design)')
+
+
+def _c(t, dtype):
+    if t.dtype != dtype:
+        raise _lib.FgrError(f'expected {dtype}, got {t.dtype}')
+    return t.contiguous()
+
+
+def offsets(lengths: Sequence[int], device) -> torch.Tensor:
+    """Host lengths -> device int64 row offsets (len + 1)."""
+    o = [0]
+    for n in lengths:
+        o.append(o[-1] + int(n))
+    return torch.tensor(o, dtype=torch.int64, device=device)
+
+
+# ------------------------------------------------------------------------------------------
+# geometry
+# ------------------------------------------------------------------------------------------
+def grid_subsample(points: torch.Tensor, off: torch.Tensor, lengths: Sequence[int], dl: float,
+                   return_keys=False):
+    """Barycentre grid subsampling per cloud (grid_subsampling.cpp semantics).
+
+    Returns (sub_points (M,3) f32, sub_lengths List[int][, keys (M,) int64]). One host
+    sync (the voxel counts), as in the reference's own GPU path.
+    """
+    _dev(points, off)
+    pts = _c(points, torch.float32)
+    n, nc = pts.shape[0], len(lengths)
+    assert pts.dim() == 2 and pts.shape[1] == 3 and off.numel() == nc + 1
+    L = _lib.load()
+    ws_bytes = _lib._sz(0)
+    _lib.check(L.fgr_grid_subsample_workspace(n, nc, ws_bytes), 'fgr_grid_subsample_workspace')
+    ws = torch.empty(ws_bytes.value, dtype=torch.uint8, device=pts.device)
+    counts = torch.empty(nc + 1, dtype=torch.int64, device=pts.device)
+    st = _stream()
+    _lib.check(L.fgr_grid_subsample_count(_ptr(pts), _ptr(off), nc, n, float(dl), _ptr(ws),
+                                          ws_bytes.value, _ptr(counts), st),
+               'fgr_grid_subsample_count')
+    host = counts.cpu().tolist()  # host sync: output size is data-dependent
+    m = host[nc]
+    out = torch.empty((m, 3), dtype=torch.float32, device=pts.device)
+    keys = torch.empty((m,), dtype=torch.int64, device=pts.device) if return_keys else None
+    _lib.check(L.fgr_grid_subsample_fill(n, nc, m, _ptr(ws), ws_bytes.value, _ptr(pts), _ptr(out),
+                                         _ptr(keys), st), 'fgr_grid_subsample_fill')
+    if return_keys:
+        return out, host[:nc], keys
+    return out, host[:nc]
+
+
+def radius_count(q, q_off, q_lengths, s, s_off, radius) -> Tuple[torch.Tensor, int]:
+    """Uncapped neighbour counts (int32 per query) and their max (host int, one sync)."""
+    _dev(q, q_off, s, s_off)
+    q, s = _c(q, torch.float32), _c(s, torch.float32)
+    counts = torch.empty(q.shape[0], dtype=torch.int32, device=q.device)
+    mx = torch.empty(1, dtype=torch.int32, device=q.device)
+    max_q = max(q_lengths) if len(q_lengths) else 0
+    _lib.check(_lib.load().fgr_radius_count(_ptr(q), _ptr(q_off), _ptr(s), _ptr(s_off),
+                                            len(q_lengths), q.shape[0], max_q, float(radius), _ptr(counts),
+                                            _ptr(mx), _stream()), 'fgr_radius_count')
+    return counts, int(mx.item())
+
+
+def radius_search(q: torch.Tensor, q_off: torch.Tensor, q_lengths: Sequence[int], s: torch.Tensor,
+                  s_off: torch.Tensor, s_lengths: Sequence[int], radius: float, limit: int,
+                  mode: int = NB_INDEX) -> torch.Tensor:
+    """Radius neighbours, (Nq, width) int64 padded with the shadow index Ns_total.
+
+    mode NB_INDEX: ball_query semantics, width = limit (no host sync).
+    mode NB_DIST:  nanoflann semantics, width = min(max count, limit) (one host sync).
+    """
+    _dev(q, q_off, s, s_off)
+    q, s = _c(q, torch.float32), _c(s, torch.float32)
+    assert q.dim() == 2 and q.shape[1] == 3 and s.dim() == 2 and s.shape[1] == 3
+    nc = len(q_lengths)
+    assert len(s_lengths) == nc and q_off.numel() == nc + 1 and s_off.numel() == nc + 1
+    assert sum(q_lengths) == q.shape[0] and sum(s_lengths) == s.shape[0]
+    L = _lib.load()
+    st = _stream()
+    max_q = max(q_lengths) if nc else 0
+    r = float(radius)
+    if mode == NB_INDEX:
+        if limit <= 0:
+            raise _lib.FgrError('ball_query semantics need a positive neighbour limit')
+        width = int(limit)
+    else:
+        counts = torch.empty(q.shape[0], dtype=torch.int32, device=q.device)
+        mx = torch.empty(1, dtype=torch.int32, device=q.device)
+        _lib.check(L.fgr_radius_count(_ptr(q), _ptr(q_off), _ptr(s), _ptr(s_off), nc, q.shape[0],
+                                      max_q, r, _ptr(counts), _ptr(mx), st), 'fgr_radius_count')
+        m = int(mx.item())
+        width = m if limit <= 0 else min(m, int(limit))
+    out = torch.empty((q.shape[0], width), dtype=torch.int64, device=q.device)
+    _lib.check(L.fgr_radius_search(_ptr(q), _ptr(q_off), _ptr(s), _ptr(s_off), nc, q.shape[0],
+                                   s.shape[0], max_q, r, int(mode), width, _ptr(out), st),
+               'fgr_radius_search')
+    return out
+
+
+# ------------------------------------------------------------------------------------------
+# KPConv
+# ------------------------------------------------------------------------------------------
+def kpconv_gather(q, s, idx, x, kernel_points, extent) -> Tuple[torch.Tensor, torch.Tensor]:
+    """-> (wf (Nq, K, Cin), nnorm (Nq,) f32) of the KPConv gather-weight stage."""
+    _dev(q, s, idx, x, kernel_points)
+    q, s, x = _c(q, torch.float32), _c(s, torch.float32), _c(x, torch.float32)
+    idx = _c(idx, torch.int64)
+    kp = _c(kernel_points, torch.float32)
+    nq, ns = q.shape[0], s.shape[0]
+    assert idx.dim() == 2 and idx.shape[0] == nq and x.dim() == 2 and x.shape[0] == ns
+    assert kp.dim() == 2 and kp.shape[1] == 3
+    K, cin = kp.shape[0], x.shape[1]
+    wf = torch.empty((nq, K, cin), dtype=torch.float32, device=q.device)
+    nnorm = torch.empty((nq,), dtype=torch.float32, device=q.device)
+    t0 = _begin('kpconv_gather')
+    _lib.check(_lib.load().fgr_kpconv_gather(_ptr(q), _ptr(s), nq, ns, _ptr(idx), idx.shape[1],
+                                             _ptr(x), cin, _ptr(kp), K, float(extent), _ptr(wf),
+                                             _ptr(nnorm), _stream()), 'fgr_kpconv_gather')
+    _end('kpconv_gather', t0, lambda: gather_bytes(idx, ns, cin, K))
+    return wf, nnorm
+
+
+def gather_bytes(idx, ns, cin, n_kp):
+    """Algorithmic HBM bytes of one fgr_kpconv_gather launch:
+    sum_q [8*H (idx row) + 12 (q) + v_q*(12 + 4*cin) (valid xyz + feature rows)
+           + 4*K*cin (wf row) + 4 (nnorm)]."""
+    nq, H = idx.shape
+    v = int((idx < ns).sum().item())
+    return nq * (8 * H + 12 + 4 * n_kp * cin + 4) + v * (12 + 4 * cin)
+
+
+def max_pool(x, idx) -> torch.Tensor:
+    _dev(x, idx)
+    x, idx = _c(x, torch.float32), _c(idx, torch.int64)
+    out = torch.empty((idx.shape[0], x.shape[1]), dtype=torch.float32, device=x.device)
+    _lib.check(_lib.load().fgr_max_pool(_ptr(x), x.shape[0], x.shape[1], _ptr(idx), idx.shape[0],
+                                        idx.shape[1], _ptr(out), _stream()), 'fgr_max_pool')
+    return out
+
+
+# ------------------------------------------------------------------------------------------
+# normalisation / embedding
+# ------------------------------------------------------------------------------------------
+def instnorm(x, seg_off, n_seg, row_div=None, act=ACT_NONE, residual=None, post_act=ACT_NONE,
+             eps=1e-5, out=None) -> torch.Tensor:
+    _dev(x, seg_off, row_div, residual)
+    x = _c(x, torch.float32)
+    n, c = x.shape
+    if residual is not None:
+        residual = _c(residual, torch.float32)
+        assert residual.shape == x.shape
+    if row_div is not None:
+        row_div = _c(row_div, torch.float32)
+        assert row_div.shape == (n,)
+    assert seg_off.numel() == n_seg + 1
+    if out is None:
+        out = torch.empty_like(x)
+    _lib.check(_lib.load().fgr_instnorm(_ptr(x), n, c, _ptr(seg_off), n_seg, _ptr(row_div),
+                                        float(eps), act, _ptr(residual), post_act, _ptr(out),
+                                        _stream()), 'fgr_instnorm')
+    return out
+
+
+def layernorm(x, weight, bias, eps=1e-5, add=None) -> torch.Tensor:
+    _dev(x, weight, bias, add)
+    x = _c(x, torch.float32)
+    n, d = x.shape
+    if add is not None:
+        add = _c(add, torch.float32)
+        assert add.shape == x.shape
+    out = torch.empty_like(x)
+    _lib.check(_lib.load().fgr_layernorm(_ptr(x), n, d, _ptr(weight.contiguous()),
+                                         _ptr(bias.contiguous()), float(eps), _ptr(add), _ptr(out),
+                                         _stream()), 'fgr_layernorm')
+    return out
+
+
+def sine_pos_embed(xyz, d_model, temperature=10000.0, scale=1.0) -> torch.Tensor:
+    _dev(xyz)
+    xyz = _c(xyz, torch.float32)
+    assert xyz.dim() == 2 and xyz.shape[1] == 3
+    out = torch.empty((xyz.shape[0], d_model), dtype=torch.float32, device=xyz.device)
+    _lib.check(_lib.load().fgr_sine_pos_embed(_ptr(xyz), xyz.shape[0], d_model, float(temperature),
+                                              float(scale * 2 * math.pi), _ptr(out), _stream()),
+               'fgr_sine_pos_embed')
+    return out
+
+
+# ------------------------------------------------------------------------------------------
+# attention
+# ------------------------------------------------------------------------------------------
+def attention(q, k, v, q_off, kv_off, kv_seg, max_q_len, n_head, out=None) -> torch.Tensor:
+    """Packed-segment MHA core: rows of query segment i attend to key segment kv_seg[i].
+
+    q, k, v: (rows, n_head * dh) views with unit column stride (may be column slices of
+    one fused QKV tensor). Returns o (Nq, n_head * dh).
+    """
+    _dev(q, k, v, q_off, kv_off, kv_seg)
+    for t in (q, k, v):
+        assert t.dtype == torch.float32 and t.dim() == 2 and t.stride(1) == 1
+    d = q.shape[1]
+    assert k.shape[1] == d and v.shape[1] == d and d % n_head == 0
+    dh = d // n_head
+    if out is None:
+        out = torch.empty((q.shape[0], d), dtype=torch.float32, device=q.device)
+    n_seg = q_off.numel() - 1
+    assert kv_seg.dtype == torch.int32 and kv_seg.numel() == n_seg
+    t0 = _begin('attention')
+    _lib.check(_lib.load().fgr_attention(_ptr(q), q.stride(0), _ptr(k), k.stride(0), _ptr(v),
+                                         v.stride(0), _ptr(out), out.stride(0), _ptr(q_off),
+                                         _ptr(kv_off), _ptr(kv_seg), n_seg, int(max_q_len), n_head,
+                                         dh, float(math.sqrt(1.0 / float(dh))), _stream()),
+               'fgr_attention')
+    _end('attention', t0, lambda: attention_flops(q_off, kv_off, kv_seg, d))
+    return out
+
+
+def attention_flops(q_off, kv_off, kv_seg, d):
+    """Algorithmic flops of one fgr_attention launch: 4 * Nq * Nk * d per segment
+    (QK^T + AV over all heads)."""
+    qo, ko, ks = q_off.tolist(), kv_off.tolist(), kv_seg.tolist()
+    return sum(4 * (qo[i + 1] - qo[i]) * (ko[ks[i] + 1] - ko[ks[i]]) * d for i in range(len(ks)))
+
+
+# ------------------------------------------------------------------------------------------
+# pose
+# ------------------------------------------------------------------------------------------
+def procrustes(a, b, w, threshold=0.85) -> torch.Tensor:
+    """(…, N, 3), (…, N, 3), (…, N) -> (…, 3, 4); threshold None = unthresholded."""
+    _dev(a, b, w)
+    lead = a.shape[:-2]
+    n = a.shape[-2]
+    a2 = _c(a, torch.float32).reshape(-1, n, 3)
+    b2 = _c(b, torch.float32).reshape(-1, n, 3)
+    w2 = _c(w, torch.float32).reshape(-1, n)
+    out = torch.empty((a2.shape[0], 3, 4), dtype=torch.float32, device=a.device)
+    thr = -1.0 if threshold is None else float(threshold)
+    _lib.check(_lib.load().fgr_procrustes(_ptr(a2), _ptr(b2), _ptr(w2), a2.shape[0], n, thr,
+                                          _ptr(out), _stream()), 'fgr_procrustes')
+    return out.reshape(*lead, 3, 4)
+
+
+def pair_pose(xyz, corr, logits, seg_off, n_pairs, threshold=0.85) -> torch.Tensor:
+    """Pose stage of the forward from packed tensors -> (L, B, 3, 4)."""
+    _dev(xyz, corr, logits, seg_off)
+    xyz, corr, logits = (_c(t, torch.float32) for t in (xyz, corr, logits))
+    n_layers, n_tot = corr.shape[0], corr.shape[1]
+    assert xyz.shape == (n_tot, 3) and logits.shape == (n_layers, n_tot)
+    assert seg_off.numel() == 2 * n_pairs + 1
+    out = torch.empty((n_layers, n_pairs, 3, 4), dtype=torch.float32, device=xyz.device)
+    _lib.check(_lib.load().fgr_pair_pose(_ptr(xyz), _ptr(corr), _ptr(logits), n_tot,
+                                         _ptr(seg_off), n_pairs, n_layers, float(threshold),
+                                         _ptr(out), _stream()), 'fgr_pair_pose')
+    return out

@@ -1,0 +1,169 @@
+"""RegTR (fine-grained fusion variant) on the MI355X kernels.
+
+Mirrors models/finegrained_regtr.py: same constructor ``RegTR(cfg)``, same
+submodule / state_dict names, same ``forward(batch) -> outputs`` keys and shapes
+(:233-249), ``batch['kpconv_meta']`` filled as the reference does (:122). Inside,
+the forward is re-laid out for the GPU:
+
+* preprocessing on HIP kernels with one host sync per pyramid level (voxel counts);
+* all 2B clouds kept packed end to end (no padding, no per-cloud Python loops);
+* one launch per op for all clouds, self- and cross-attention included;
+* pose for all (layer, pair) problems in one launch, straight from packed tensors.
+The returned per-cloud lists are views into the packed tensors.
+"""
+import logging
+
+import torch
+import torch.nn as nn
+
+from . import ops
+from .backbone import KPFEncoder, PreprocessorHIP, host_layout
+from .transformer import (PositionEmbeddingCoordsSine, Segments, TransformerCrossEncoder,
+                          TransformerCrossEncoderLayer)
+
+_logger = logging.getLogger(__name__)
+
+
+class CorrespondenceRegressor(nn.Module):
+    """finegrained_regtr.py:411-455 (direct_regress_coor: True, the shipped configs)."""
+
+    def __init__(self, d_embed):
+        super().__init__()
+        self.coor_mlp = nn.Sequential(nn.Linear(d_embed, d_embed), nn.ReLU(),
+                                      nn.Linear(d_embed, d_embed), nn.ReLU(),
+                                      nn.Linear(d_embed, 3))
+        self.conf_logits_decoder = nn.Linear(d_embed, 1)
+
+    def forward_packed(self, feats):
+        """feats (L, N, d) -> corr (L, N, 3), logits (L, N, 1)."""
+        L, N, d = feats.shape
+        f = feats.reshape(L * N, d)
+        m = self.coor_mlp
+        h = torch.addmm(m[0].bias, f, m[0].weight.t()).relu_()
+        h = torch.addmm(m[2].bias, h, m[2].weight.t()).relu_()
+        corr = torch.addmm(m[4].bias, h, m[4].weight.t())
+        logits = torch.addmm(self.conf_logits_decoder.bias, f, self.conf_logits_decoder.weight.t())
+        return corr.view(L, N, 3), logits.view(L, N, 1)
+
+
+class CorrespondenceDecoder(nn.Module):
+    """finegrained_regtr.py:312-408 (direct_regress_coor: False): single-head attention
+    whose values are the other cloud's coordinates. Parameter layout of the reference;
+    evaluated with the fused attention kernel per layer (values zero-padded to width d)."""
+
+    def __init__(self, d_embed, use_pos_emb, pos_embed=None, num_neighbors=0):
+        super().__init__()
+        if num_neighbors > 0:
+            raise NotImplementedError('top-k neighbour masking is not in the reference configs')
+        self.use_pos_emb = use_pos_emb
+        self.pos_embed = pos_embed
+        self.q_norm = nn.LayerNorm(d_embed)   # present in the reference, unused by its forward
+        self.q_proj = nn.Linear(d_embed, d_embed)
+        self.k_proj = nn.Linear(d_embed, d_embed)
+        self.conf_logits_decoder = nn.Linear(d_embed, 1)
+        self.num_neighbors = num_neighbors
+
+    def forward_packed(self, feats, xyz, pos, seg: Segments):
+        L, N, d = feats.shape
+        f = feats + pos.unsqueeze(0) if self.use_pos_emb else feats
+        q = torch.addmm(self.q_proj.bias, f.reshape(L * N, d), self.q_proj.weight.t())
+        k = torch.addmm(self.k_proj.bias, f.reshape(L * N, d), self.k_proj.weight.t())
+        # one head of width d; the 3 value columns ride in a zero-padded width-d value matrix
+        vfull = torch.zeros((N, d), dtype=feats.dtype, device=feats.device)
+        vfull[:, :3] = xyz
+        corr = torch.empty((L, N, 3), dtype=feats.dtype, device=feats.device)
+        for l in range(L):
+            ql, kl = q[l * N:(l + 1) * N], k[l * N:(l + 1) * N]
+            o = ops.attention(ql, kl, vfull, seg.off, seg.off, seg.cross_seg, seg.max_len, 1)
+            corr[l] = o[:, :3]
+        logits = torch.addmm(self.conf_logits_decoder.bias, feats.reshape(L * N, d),
+                             self.conf_logits_decoder.weight.t())
+        return corr, logits.view(L, N, 1)
+
+
+class _LossParams(nn.Module):
+    """Holds InfoNCELossFull's parameter W (models/losses/feature_loss.py:246-266) so that
+    reference checkpoints load strictly; the loss itself is not part of the forward."""
+
+    def __init__(self, d_embed):
+        super().__init__()
+        self.W = nn.Parameter(torch.zeros(d_embed, d_embed))
+        nn.init.normal_(self.W, std=0.1)
+
+
+class RegTR(nn.Module):
+    """models/finegrained_regtr.py:23-250."""
+
+    def __init__(self, cfg, *args, neighbor_mode='ball_query', **kwargs):
+        super().__init__()
+        self.cfg = cfg
+        self.preprocessor = PreprocessorHIP(cfg, neighbor_mode=neighbor_mode)
+        self.kpf_encoder = KPFEncoder(cfg, cfg.d_embed)
+        self.feat_proj = nn.Linear(self.kpf_encoder.encoder_skip_dims[-1], cfg.d_embed, bias=True)
+        if cfg.get('pos_emb_type', 'sine') != 'sine':
+            raise NotImplementedError('pos_emb_type other than sine is not in the reference configs')
+        self.pos_embed = PositionEmbeddingCoordsSine(3, cfg.d_embed,
+                                                     scale=cfg.get('pos_emb_scaling', 1.0))
+        layer = TransformerCrossEncoderLayer(
+            cfg.d_embed, cfg.nhead, cfg.d_feedforward, cfg.dropout,
+            activation=cfg.transformer_act, normalize_before=cfg.pre_norm,
+            sa_val_has_pos_emb=cfg.sa_val_has_pos_emb, ca_val_has_pos_emb=cfg.ca_val_has_pos_emb,
+            attention_type=cfg.attention_type)
+        norm = nn.LayerNorm(cfg.d_embed) if cfg.pre_norm else None
+        self.transformer_encoder = TransformerCrossEncoder(layer, cfg.num_encoder_layers, norm,
+                                                           return_intermediate=True)
+        if cfg.get('direct_regress_coor', False):
+            self.correspondence_decoder = CorrespondenceRegressor(cfg.d_embed)
+        else:
+            self.correspondence_decoder = CorrespondenceDecoder(
+                cfg.d_embed, cfg.corr_decoder_has_pos_emb, self.pos_embed)
+        if cfg.get('feature_loss_type', 'infonce') == 'infonce':
+            self.feature_criterion = _LossParams(cfg.d_embed)
+            self.feature_criterion_un = _LossParams(cfg.d_embed)
+        self.pose_threshold = 0.85   # hard-coded in fast_compute_rigid_transform (se3_torch.py:226)
+
+    @torch.no_grad()
+    def forward(self, batch):
+        if torch.is_grad_enabled() and self.training:
+            raise NotImplementedError('fgreg implements the inference forward only')
+        B = len(batch['src_xyz'])
+        meta = self.preprocessor(list(batch['src_xyz']) + list(batch['tgt_xyz']))
+        batch['kpconv_meta'] = meta
+        n_lvl = len(meta['points'])
+        slens_c, off_c = host_layout(meta, n_lvl - 1)
+        pts0 = meta['points'][0]
+        feats0 = torch.ones((pts0.shape[0], 1), dtype=torch.float32, device=pts0.device)
+
+        feats_un, _ = self.kpf_encoder(feats0, meta)
+        both = torch.addmm(self.feat_proj.bias, feats_un, self.feat_proj.weight.t())
+        xyz_c = meta['points'][-1]
+        pe = self.pos_embed(xyz_c)
+        seg = Segments(slens_c, xyz_c.device)
+        pos = pe if self.cfg.transformer_encoder_has_pos_emb else None
+        if pos is None:
+            pos = torch.zeros_like(both)
+        feats = self.transformer_encoder.forward_packed(both, pos, seg)        # (L, N, d)
+        if isinstance(self.correspondence_decoder, CorrespondenceRegressor):
+            corr, logits = self.correspondence_decoder.forward_packed(feats)
+        else:
+            corr, logits = self.correspondence_decoder.forward_packed(feats, xyz_c, pe, seg)
+        pose = ops.pair_pose(xyz_c, corr, logits[..., 0], seg.off, B, self.pose_threshold)
+
+        offs = [0]
+        for n in slens_c:
+            offs.append(offs[-1] + n)
+        rows = [(offs[c], offs[c + 1]) for c in range(2 * B)]
+        outputs = {
+            'src_feat_un': [both[b:e] for b, e in rows[:B]],
+            'tgt_feat_un': [both[b:e] for b, e in rows[B:]],
+            'src_feat': [feats[:, b:e] for b, e in rows[:B]],
+            'tgt_feat': [feats[:, b:e] for b, e in rows[B:]],
+            'src_kp': [xyz_c[b:e] for b, e in rows[:B]],
+            'src_kp_warped': [corr[:, b:e] for b, e in rows[:B]],
+            'tgt_kp': [xyz_c[b:e] for b, e in rows[B:]],
+            'tgt_kp_warped': [corr[:, b:e] for b, e in rows[B:]],
+            'src_overlap': [logits[:, b:e] for b, e in rows[:B]],
+            'tgt_overlap': [logits[:, b:e] for b, e in rows[B:]],
+            'pose': pose,
+        }
+        return outputs

@@ -1,0 +1,142 @@
+"""Cross-encoder transformer on packed, unpadded clouds.
+
+Parameter names follow models/transformer/transformers.py (``layers.{i}.self_attn``,
+``multihead_attn`` as nn.MultiheadAttention, ``linear1/2``, ``norm1-3``, final
+``norm``), so reference checkpoints load unchanged. The compute differs in layout:
+the reference pads src and tgt to (N_max, B, d) and runs every op twice (src, tgt)
+with key padding masks (finegrained_regtr.py:164-179); here all 2B clouds stay
+packed in one (N_tot, d) tensor in the encoder's cloud order
+(src_0..src_{B-1}, tgt_0..tgt_{B-1}) and
+
+* self-attention = one QKV GEMM over all rows + fgr_attention with every cloud
+  attending to itself;
+* cross-attention = one QKV GEMM over all rows + fgr_attention with cloud c
+  attending to its partner (c + B) mod 2B -- both directions in one launch, reading
+  the same pre-update activations exactly like the reference's simultaneous update
+  (transformers.py:213-229);
+* LayerNorm (+ positional embedding add) = fgr_layernorm.
+Masked keys never exist, so no -inf masking is needed; padded query rows never exist,
+so no work is wasted on them.
+"""
+import copy
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import ops
+
+
+class Segments:
+    """Device-side segment tables of one packed batch of 2B clouds."""
+
+    def __init__(self, lengths, device):
+        self.lengths = [int(n) for n in lengths]
+        n = len(self.lengths)
+        assert n % 2 == 0
+        self.B = n // 2
+        self.off = ops.offsets(self.lengths, device)
+        self.self_seg = torch.arange(n, dtype=torch.int32, device=device)
+        self.cross_seg = torch.tensor([(c + self.B) % n for c in range(n)], dtype=torch.int32,
+                                      device=device)
+        self.max_len = max(self.lengths) if n else 0
+
+
+class TransformerCrossEncoderLayer(nn.Module):
+    """transformers.py:84-258 (pre-norm forward_pre; dropout must be 0 at inference)."""
+
+    def __init__(self, d_model, nhead, dim_feedforward=2048, dropout=0.1, activation='relu',
+                 normalize_before=False, sa_val_has_pos_emb=False, ca_val_has_pos_emb=False,
+                 attention_type='dot_prod'):
+        super().__init__()
+        if attention_type != 'dot_prod':
+            raise NotImplementedError(attention_type)
+        if activation != 'relu':
+            raise NotImplementedError('transformer_act other than relu is not in the configs')
+        if not normalize_before:
+            raise NotImplementedError('post-norm (pre_norm: False) is not in the reference configs')
+        self.self_attn = nn.MultiheadAttention(d_model, nhead, dropout=dropout)
+        self.multihead_attn = nn.MultiheadAttention(d_model, nhead, dropout=dropout)
+        self.linear1 = nn.Linear(d_model, dim_feedforward)
+        self.linear2 = nn.Linear(dim_feedforward, d_model)
+        self.norm1 = nn.LayerNorm(d_model)
+        self.norm2 = nn.LayerNorm(d_model)
+        self.norm3 = nn.LayerNorm(d_model)
+        self.nhead = nhead
+        self.normalize_before = normalize_before
+        self.sa_val_has_pos_emb = sa_val_has_pos_emb
+        self.ca_val_has_pos_emb = ca_val_has_pos_emb
+
+    def _attend(self, mha, h_pos, h_nopos, val_has_pos, seg, kv_seg):
+        d = h_pos.shape[1]
+        W, b = mha.in_proj_weight, mha.in_proj_bias
+        if val_has_pos:
+            qkv = torch.addmm(b, h_pos, W.t())                        # (N, 3d): [q | k | v]
+            q, k, v = qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:]
+        else:
+            qk = torch.addmm(b[:2 * d], h_pos, W[:2 * d].t())
+            q, k = qk[:, :d], qk[:, d:]
+            v = torch.addmm(b[2 * d:], h_nopos, W[2 * d:].t())
+        o = ops.attention(q, k, v, seg.off, seg.off, kv_seg, seg.max_len, self.nhead)
+        return o
+
+    def forward_packed(self, x, pos, seg: Segments):
+        """x (N_tot, d) packed clouds -> updated x (forward_pre, transformers.py:183-244)."""
+        # self-attention, shared weights for src and tgt (:193-210)
+        h = ops.layernorm(x, self.norm1.weight, self.norm1.bias, self.norm1.eps, add=pos)
+        h0 = None if self.sa_val_has_pos_emb else ops.layernorm(x, self.norm1.weight,
+                                                                 self.norm1.bias, self.norm1.eps)
+        o = self._attend(self.self_attn, h, h0, self.sa_val_has_pos_emb, seg, seg.self_seg)
+        x = torch.addmm(x, o, self.self_attn.out_proj.weight.t()).add_(self.self_attn.out_proj.bias)
+        # cross-attention, both directions at once (:212-229)
+        h = ops.layernorm(x, self.norm2.weight, self.norm2.bias, self.norm2.eps, add=pos)
+        h0 = None if self.ca_val_has_pos_emb else ops.layernorm(x, self.norm2.weight,
+                                                                 self.norm2.bias, self.norm2.eps)
+        o = self._attend(self.multihead_attn, h, h0, self.ca_val_has_pos_emb, seg, seg.cross_seg)
+        x = torch.addmm(x, o, self.multihead_attn.out_proj.weight.t()).add_(
+            self.multihead_attn.out_proj.bias)
+        # position-wise feed-forward (:231-238)
+        h = ops.layernorm(x, self.norm3.weight, self.norm3.bias, self.norm3.eps)
+        h = torch.addmm(self.linear1.bias, h, self.linear1.weight.t()).relu_()
+        return torch.addmm(x, h, self.linear2.weight.t()).add_(self.linear2.bias)
+
+
+class TransformerCrossEncoder(nn.Module):
+    """transformers.py:18-59 with return_intermediate=True semantics."""
+
+    def __init__(self, cross_encoder_layer, num_layers, norm=None, return_intermediate=False):
+        super().__init__()
+        self.layers = nn.ModuleList([copy.deepcopy(cross_encoder_layer) for _ in range(num_layers)])
+        self.num_layers = num_layers
+        self.norm = norm
+        self.return_intermediate = return_intermediate
+
+    def forward_packed(self, x, pos, seg: Segments):
+        """-> (L, N_tot, d) normalised intermediates (or (1, N_tot, d))."""
+        inter = []
+        for layer in self.layers:
+            x = layer.forward_packed(x, pos, seg)
+            if self.return_intermediate:
+                inter.append(self._norm(x))
+        if self.return_intermediate:
+            return torch.stack(inter)
+        return self._norm(x).unsqueeze(0)
+
+    def _norm(self, x):
+        if self.norm is None:
+            return x
+        return ops.layernorm(x, self.norm.weight, self.norm.bias, self.norm.eps)
+
+
+class PositionEmbeddingCoordsSine(nn.Module):
+    """position_embedding.py:8-49 on fgr_sine_pos_embed."""
+
+    def __init__(self, n_dim=1, d_model=256, temperature=10000, scale=None):
+        super().__init__()
+        if n_dim != 3:
+            raise NotImplementedError('coordinates are 3-D in this path')
+        self.n_dim, self.d_model, self.temperature = n_dim, d_model, temperature
+        self.scale = 1.0 if scale is None else scale
+
+    def forward(self, xyz):
+        return ops.sine_pos_embed(xyz, self.d_model, self.temperature, self.scale)

@@ -1,0 +1,152 @@
+/* fgreg.h -- C ABI of libfgreg.so, the MI355X (gfx950) kernels of the per-pair
+ * registration forward of "Boosting Fine-grained Feature Fusion in 3D Point
+ * Cloud Registration" (a REGTR fork: KPConv + Res2Net backbone, cross-attention
+ * transformer, weighted-Procrustes pose).
+ *
+ * Conventions (every entry point):
+ *  - all array arguments are DEVICE pointers allocated by the caller; nothing
+ *    is allocated inside (data-dependent sizes use a count call + a fill call,
+ *    scratch comes from a caller-provided workspace sized by *_workspace());
+ *  - `stream` is a hipStream_t passed as void*; all work is stream-ordered,
+ *    no call synchronises the device or the host;
+ *  - return 0 on success, a negative FGR_E* code on error; the message of the
+ *    last error on the calling thread is returned by fgr_last_error();
+ *  - no C++ exception crosses the ABI; no mutable global state besides a
+ *    per-thread error string.
+ *
+ * Packed layout: clouds are stacked along rows in the reference's order
+ * src_0..src_{B-1}, tgt_0..tgt_{B-1} (models/finegrained_regtr.py:121), with
+ * int64 row offsets `off[n_clouds + 1]`. A neighbour table is (Nq, width)
+ * int64 whose missing entries hold the "shadow" index Ns_total
+ * (finegrained_kpconv.py:288-291).
+ */
+#ifndef FGREG_H
+#define FGREG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FGR_ABI_VERSION 1
+
+enum {
+    FGR_OK = 0,
+    FGR_E_ARG = -1,      /* invalid argument / shape            */
+    FGR_E_LAUNCH = -2,   /* HIP launch or runtime error          */
+    FGR_E_WORKSPACE = -3 /* workspace too small                  */
+};
+
+/* radius-search row semantics */
+enum {
+    FGR_NB_INDEX = 0, /* PyTorch3D ball_query: first `width` supports in index order
+                         (finegrained_kpconv.py:266-293, PreprocessorGPU)          */
+    FGR_NB_DIST = 1   /* nanoflann radiusSearch(sorted) + [:, :K]: the `width`
+                         nearest, ties by index (neighbors.cpp:211-332, :260-261)  */
+};
+
+/* activation codes */
+enum { FGR_ACT_NONE = 0, FGR_ACT_LEAKY = 1, FGR_ACT_RELU = 2 };
+
+int fgr_abi_version(void);
+const char* fgr_last_error(void);
+
+/* ---- grid subsampling ------------------------------------------------------------
+ * Replaces batch_grid_subsampling_kpconv_gpu (finegrained_kpconv.py:218-245; ME
+ * UNWEIGHTED_AVERAGE) and its CPU twin subsample_batch
+ * (cpp_subsampling/wrapper.cpp:62-333 -> grid_subsampling.cpp:5-211).
+ * Voxel key and barycentre follow grid_subsampling.cpp bit for bit; voxels are
+ * emitted in ascending key order per cloud.
+ * 1) fgr_grid_subsample_count: writes counts[c] (voxels of cloud c) and
+ *    counts[n_clouds] (total) as int64; keeps the sorted state in `ws`.
+ * 2) fgr_grid_subsample_fill: writes out_points (total, 3) and optionally the
+ *    voxel keys (total) from the same `ws` (must follow the count call). */
+int fgr_grid_subsample_workspace(int64_t n_points, int32_t n_clouds, size_t* bytes);
+int fgr_grid_subsample_count(const float* points, const int64_t* off, int32_t n_clouds,
+                             int64_t n_points, float dl, void* ws, size_t ws_bytes,
+                             int64_t* counts, void* stream);
+int fgr_grid_subsample_fill(int64_t n_points, int32_t n_clouds, int64_t n_out, void* ws,
+                            size_t ws_bytes, const float* points, float* out_points,
+                            int64_t* out_keys, void* stream);
+
+/* ---- radius neighbour search -----------------------------------------------------
+ * Replaces batch_neighbors_kpconv_gpu (ball_query, finegrained_kpconv.py:266-293)
+ * and batch_neighbors_kpconv (cpp_neighbors.batch_query, :248-263).
+ * d2 = ((qx-sx)^2 + (qy-sy)^2) + (qz-sz)^2 in fp32 without FMA, kept iff d2 < r*r.
+ * fgr_radius_count: uncapped neighbour count per query + the max (int32 scalar);
+ * fgr_radius_search: fills out (nq, width) int64 (mode FGR_NB_*; DIST needs width <= 64). */
+int fgr_radius_count(const float* q, const int64_t* q_off, const float* s, const int64_t* s_off,
+                     int32_t n_clouds, int64_t nq, int32_t max_q_len, float radius,
+                     int32_t* counts, int32_t* max_count, void* stream);
+int fgr_radius_search(const float* q, const int64_t* q_off, const float* s, const int64_t* s_off,
+                      int32_t n_clouds, int64_t nq, int64_t ns, int32_t max_q_len, float radius,
+                      int32_t mode, int32_t width, int64_t* out, void* stream);
+
+/* ---- KPConv ------------------------------------------------------------------------
+ * The gather-weight stage of KPConv.forward (finegrained_kpconv_blocks.py:296-381,
+ * rigid, linear influence, sum aggregation):
+ *   wf[q, k, c] = sum_{valid h} max(0, 1 - |(s[idx[q,h]] - q) - kp[k]| / extent) * x[idx[q,h], c]
+ * and the normaliser of :395-399: nnorm[q] = max(1, #{valid h : sum_c x[idx[q,h], c] > 0}).
+ * The caller finishes with (wf.view(nq, K*cin) @ W.view(K*cin, cout)) / nnorm. */
+int fgr_kpconv_gather(const float* q, const float* s, int64_t nq, int64_t ns, const int64_t* idx,
+                      int32_t width, const float* x, int32_t cin, const float* kp, int32_t n_kp,
+                      float extent, float* wf, float* nnorm, void* stream);
+
+/* max_pool (finegrained_kpconv_blocks.py:125-141): out[q, c] = max over the row of
+ * x[idx[q, h], c], shadow entries contributing 0 (the appended zero row). */
+int fgr_max_pool(const float* x, int64_t ns, int32_t c, const int64_t* idx, int64_t nq,
+                 int32_t width, float* out, void* stream);
+
+/* ---- normalisation -----------------------------------------------------------------
+ * Segmented instance norm, nn.InstanceNorm1d(affine=False) applied per cloud
+ * (BatchNormBlock, finegrained_kpconv_blocks.py:498-507), fused with:
+ *   v   = row_div ? x[r, c] / row_div[r] : x[r, c]       (KPConv normaliser, :399)
+ *   y   = act((v - mean_seg,c) / sqrt(var_seg,c + eps))   (biased variance)
+ *   out = residual ? post_act(y + residual[r, c]) : y     (bottleneck sum, :725) */
+int fgr_instnorm(const float* x, int64_t n, int32_t c, const int64_t* seg_off, int32_t n_seg,
+                 const float* row_div, float eps, int32_t act, const float* residual,
+                 int32_t post_act, float* out, void* stream);
+
+/* Row LayerNorm (nn.LayerNorm, transformers.py:105-107) with an optional added
+ * tensor (the positional embedding, transformers.py:194-195): out = LN(x)*g + b (+ add). */
+int fgr_layernorm(const float* x, int64_t n, int32_t d, const float* gamma, const float* beta,
+                  float eps, const float* add, float* out, void* stream);
+
+/* PositionEmbeddingCoordsSine (position_embedding.py:29-49) for 3-D input. */
+int fgr_sine_pos_embed(const float* xyz, int64_t n, int32_t d_model, float temperature,
+                       float scale, float* out, void* stream);
+
+/* ---- attention ---------------------------------------------------------------------
+ * Multi-head scaled-dot-product attention core of nn.MultiheadAttention
+ * (transformers.py:95-96, 197-226) on packed, unpadded segments: query segment
+ * i (rows q_off[i]..q_off[i+1]) attends to key segment kv_seg[i] (rows
+ * kv_off[j]..kv_off[j+1]); the reference's key padding mask is the segment end.
+ * Head h reads columns [h*dh, (h+1)*dh) of q/k/v rows (row strides ld_*).
+ * o = softmax((q * scale) k^T) v, fp32 in/out, fp32 MFMA (v_mfma_f32_16x16x4_f32). */
+int fgr_attention(const float* q, int64_t ld_q, const float* k, int64_t ld_k, const float* v,
+                  int64_t ld_v, float* o, int64_t ld_o, const int64_t* q_off,
+                  const int64_t* kv_off, const int32_t* kv_seg, int32_t n_seg,
+                  int32_t max_q_len, int32_t n_head, int32_t head_dim, float scale, void* stream);
+
+/* ---- pose ----------------------------------------------------------------------------
+ * fast_compute_rigid_transform (utils/se3_torch.py:226-273; threshold < 0 gives the
+ * unthresholded compute_rigid_transform, :131-173) on n_batch independent problems
+ * a, b (n_batch, n_pts, 3), w (n_batch, n_pts) -> out (n_batch, 3, 4). */
+int fgr_procrustes(const float* a, const float* b, const float* w, int64_t n_batch, int64_t n_pts,
+                   float threshold, float* out, void* stream);
+
+/* The forward's pose stage (models/finegrained_regtr.py:198-218) straight from the
+ * packed tensors: for pair p and layer l, a = [src_kp ; tgt_corr_l], b = [src_corr_l ;
+ * tgt_kp], w = sigmoid([src_logit_l ; tgt_logit_l]) thresholded at `threshold`.
+ * xyz (n_tot, 3) coarse points, corr (n_layers, n_tot, 3), logits (n_layers, n_tot),
+ * seg_off (2*n_pairs + 1) -> out (n_layers, n_pairs, 3, 4). */
+int fgr_pair_pose(const float* xyz, const float* corr, const float* logits, int64_t n_tot,
+                  const int64_t* seg_off, int32_t n_pairs, int32_t n_layers, float threshold,
+                  float* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FGREG_H */

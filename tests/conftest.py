@@ -1,0 +1,68 @@
+"""Shared test setup: markers, import paths, golden-fixture loaders.
+
+`-m "not gpu"` tests run on any CPU host; `-m gpu` tests need an MI355X and call the
+HIP path through the C ABI (libfgreg.so). The oracle (oracle/) is only ever used
+here as the checker.
+"""
+import ast
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, 'boosting-fine-grained-feature-fusion-in-3d-point-cloud-registration_amd')
+GOLDEN = os.path.join(REPO, 'tests', 'golden')
+for p in (PKG, os.path.join(REPO, 'oracle')):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line('markers', 'gpu: needs an AMD MI355X GPU (HIP path through libfgreg.so)')
+
+
+def golden(name):
+    return np.load(os.path.join(GOLDEN, name + '.npz'), allow_pickle=False)
+
+
+def forward_fixture(name):
+    """-> (cfg, state_dict, src list, tgt list, meta dict of CPU tensors, fixture npz)."""
+    import fgreg.config as fc
+    d = golden(name)
+    over = ast.literal_eval(str(d['cfg_overrides']))
+    base = 'modelnet' if 'modelnet' in name else '3dmatch'
+    cfg = fc.get(base, **over)
+    sd = {k[3:]: torch.from_numpy(d[k]) for k in d.files if k.startswith('sd.')}
+    n_lvl = sum(1 for k in d.files if k.startswith('meta.points.'))
+    meta = {}
+    for key in ('points', 'neighbors', 'pools', 'upsamples', 'stack_lengths'):
+        meta[key] = []
+        for l in range(n_lvl):
+            a = d[f'meta.{key}.{l}']
+            meta[key].append(torch.from_numpy(a.astype(np.int64) if a.dtype == np.int32 else a))
+    B = sum(1 for k in d.files if k.startswith('in.src_xyz.'))
+    src = [d[f'in.src_xyz.{b}'] for b in range(B)]
+    tgt = [d[f'in.tgt_xyz.{b}'] for b in range(B)]
+    return cfg, sd, src, tgt, meta, d
+
+
+def rel_err(a, b):
+    """Normwise relative error max|a - b| / max|b| (the fp32 parity metric, <= 1e-4)."""
+    a = a.detach().double().cpu() if torch.is_tensor(a) else torch.as_tensor(np.asarray(a, np.float64))
+    b = b.detach().double().cpu() if torch.is_tensor(b) else torch.as_tensor(np.asarray(b, np.float64))
+    assert a.shape == b.shape, (a.shape, b.shape)
+    if b.numel() == 0:
+        return 0.0
+    return float((a - b).abs().max() / max(float(b.abs().max()), 1e-30))
+
+
+@pytest.fixture(scope='session')
+def gpu():
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    import fgreg
+    fgreg.load()
+    return torch.device('cuda:0')

@@ -1,0 +1,120 @@
+"""End-to-end parity of RegTR.forward on the GPU.
+
+1. On the reference's own kpconv_meta (FixedMetaPreprocessor): every output of the
+   reference forward (tests/golden/forward_*.npz) within 1e-4 normwise relative.
+2. With the HIP preprocessor in 'nanoflann' mode (the reference CPU path's neighbour
+   semantics): neighbour tables of level 0 bit-exact with the reference; the coarse
+   points equal as sets; per-point outputs matched by coordinates within 1e-4; poses
+   within 1e-4.
+3. Full-size ModelNet and 3DMatch configs (random init, synthetic pairs) in the default
+   'ball_query' mode against the CPU oracle run with the same semantics.
+"""
+import numpy as np
+import pytest
+import torch
+
+import model_oracle as mo
+from conftest import forward_fixture, rel_err
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-4
+FIXTURES = ['forward_modelnet_small', 'forward_3dmatch_small']
+KEYS = ['src_feat_un', 'tgt_feat_un', 'src_feat', 'tgt_feat', 'src_kp', 'tgt_kp',
+        'src_kp_warped', 'tgt_kp_warped', 'src_overlap', 'tgt_overlap']
+
+
+def _model(cfg, sd, dev, mode='ball_query'):
+    import fgreg
+    m = fgreg.RegTR(cfg, neighbor_mode=mode)
+    missing, unexpected = m.load_state_dict(sd, strict=False)
+    assert not unexpected and all(k.startswith('feature_criterion') for k in missing)
+    return m.to(dev).eval()
+
+
+def _batch(src, tgt, dev):
+    return {'src_xyz': [torch.from_numpy(s).to(dev) for s in src],
+            'tgt_xyz': [torch.from_numpy(t).to(dev) for t in tgt]}
+
+
+@pytest.mark.parametrize('name', FIXTURES)
+def test_forward_on_reference_meta(gpu, name):
+    import fgreg
+    cfg, sd, src, tgt, meta, d = forward_fixture(name)
+    model = _model(cfg, sd, gpu)
+    model.preprocessor = fgreg.FixedMetaPreprocessor(
+        {k: [t.to(gpu) for t in v] for k, v in meta.items()})
+    out = model(_batch(src, tgt, gpu))
+    B = len(src)
+    for k in KEYS:
+        for b in range(B):
+            assert rel_err(out[k][b], d[f'out.{k}.{b}']) < TOL, (k, b)
+    assert np.abs(out['pose'].cpu().numpy() - d['out.pose']).max() < TOL
+
+
+def _match(a, b, tol):
+    """Row permutation p with b[p] ~= a: coarse points agree bit for bit at levels 0/1 and
+    to float rounding deeper (the reference sums barycentres in its unordered_map order)."""
+    from scipy.spatial import cKDTree
+    dist, p = cKDTree(b).query(a)
+    assert dist.max() <= tol and len(np.unique(p)) == len(p)
+    return p
+
+
+@pytest.mark.parametrize('name', FIXTURES)
+def test_forward_end_to_end_nanoflann_mode(gpu, name):
+    cfg, sd, src, tgt, meta, d = forward_fixture(name)
+    model = _model(cfg, sd, gpu, mode='nanoflann')
+    batch = _batch(src, tgt, gpu)
+    out = model(batch)
+    mine = batch['kpconv_meta']
+    # level 0: same points -> same neighbour table (ties canonical by index in both)
+    ref_nb0 = meta['neighbors'][0].numpy()
+    assert np.array_equal(mine['neighbors'][0].cpu().numpy(), ref_nb0)
+    B = len(src)
+    for b in range(B):
+        for side in ('src', 'tgt'):
+            a = out[f'{side}_kp'][b].cpu().numpy()
+            r = d[f'out.{side}_kp.{b}']
+            p = _match(r, a, 0.0 if len(meta['points']) <= 2 else 1e-6)   # a[p] ~= r
+            assert rel_err(out[f'{side}_feat'][b][:, p], d[f'out.{side}_feat.{b}']) < TOL
+            assert rel_err(out[f'{side}_kp_warped'][b][:, p], d[f'out.{side}_kp_warped.{b}']) < TOL
+            assert rel_err(out[f'{side}_overlap'][b][:, p], d[f'out.{side}_overlap.{b}']) < TOL
+    assert np.abs(out['pose'].cpu().numpy() - d['out.pose']).max() < TOL
+
+
+def _random_model(cfg, seed):
+    import fgreg
+    torch.manual_seed(seed)
+    np.random.seed(seed)
+    m = fgreg.RegTR(cfg)
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for mod in m.modules():
+            if isinstance(mod, torch.nn.BatchNorm1d):
+                mod.running_mean.copy_(0.1 * torch.randn(mod.running_mean.shape, generator=g))
+                mod.running_var.copy_(0.75 + 0.5 * torch.rand(mod.running_var.shape, generator=g))
+        m.correspondence_decoder.conf_logits_decoder.bias.fill_(4.0)
+    return m.eval()
+
+
+@pytest.mark.parametrize('kind,B', [('modelnet', 2), ('3dmatch', 1)])
+def test_forward_full_config_vs_oracle(gpu, kind, B):
+    import fgreg.config as fc
+    from fgreg.synthetic import make_batch
+    cfg = fc.get(kind)
+    model = _random_model(cfg, 11)
+    sd = {k: v.clone() for k, v in model.state_dict().items()}
+    kw = {} if kind == 'modelnet' else {'n_points': 8000}
+    src, tgt, _ = make_batch(kind, B, **kw)
+    model = model.to(gpu)
+    batch = _batch(src, tgt, gpu)
+    out = model(batch)
+    ref = mo.forward(cfg, sd, src, tgt, mode=mo.geom.INDEX)
+    for lvl in range(len(ref['kpconv_meta']['points'])):
+        for key in ('points', 'neighbors', 'pools', 'upsamples', 'stack_lengths'):
+            assert torch.equal(batch['kpconv_meta'][key][lvl].cpu(), ref['kpconv_meta'][key][lvl]), \
+                (key, lvl)
+    for k in KEYS:
+        for b in range(B):
+            assert rel_err(out[k][b], ref[k][b]) < TOL, (k, b)
+    assert np.abs(out['pose'].cpu().numpy() - ref['pose'].numpy()).max() < TOL

@@ -1,0 +1,193 @@
+"""GPU parity of the floating-point kernels against the reference's own outputs
+(tests/golden/*.npz) and against plain PyTorch fp32 references of the same op.
+
+Tolerance: normwise relative error max|a-b|/max|b| <= 1e-4 (fp32, SURVEY.md scope),
+poses <= 1e-4 absolute on rotation entries and relative on translations.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+import model_oracle as mo
+from conftest import golden, rel_err
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-4
+
+
+def test_kpconv_block_vs_reference(gpu):
+    """KPConv.forward (finegrained_kpconv_blocks.py:265-401) on the reference's own
+    neighbour table, conv and strided (pool) variants, plus the max-pool shortcut."""
+    from fgreg.backbone import KPConv
+    import fgreg.ops as ops
+    g = golden('kpconv_block')
+    W = torch.from_numpy(g['W'])
+    conv = KPConv(15, 3, W.shape[1], W.shape[2], float(g['extent']), 0.0825).to(gpu)
+    with torch.no_grad():
+        conv.weights.copy_(W.to(gpu))
+        conv.kernel_points.copy_(torch.from_numpy(g['kp']).to(gpu))
+    t = lambda a, dt=None: torch.from_numpy(a if dt is None else a.astype(dt)).to(gpu)
+    out = conv(t(g['q']), t(g['s']), t(g['idx'], np.int64), t(g['x']))
+    assert rel_err(out, g['out']) < TOL
+    out_s = conv(t(g['sub']), t(g['s']), t(g['pools'], np.int64), t(g['x']))
+    assert rel_err(out_s, g['out_strided']) < TOL
+    mp = ops.max_pool(t(g['x']), t(g['pools'], np.int64))
+    assert torch.equal(mp.cpu(), torch.from_numpy(g['maxpool']))
+
+
+@pytest.mark.parametrize('cin', [1, 3, 16, 32, 64, 128, 256])
+def test_kpconv_gather_vs_torch(gpu, cin):
+    """Gather-weight stage vs the fp32 torch restatement (all channel widths in the configs)."""
+    import fgreg.ops as ops
+    rng = np.random.default_rng(cin)
+    ns, nq, H = 900, 700, 50
+    s = rng.uniform(-1, 1, (ns, 3)).astype(np.float32)
+    q = s[rng.choice(ns, nq, replace=False)] + rng.normal(0, 0.01, (nq, 3)).astype(np.float32)
+    idx = rng.integers(0, ns, (nq, H))
+    idx[rng.uniform(size=(nq, H)) < 0.6] = ns            # shadows
+    x = rng.normal(size=(ns, cin)).astype(np.float32)
+    kp = (rng.normal(size=(15, 3)) * 0.3).astype(np.float32)
+    ext = 0.5
+    T = lambda a: torch.from_numpy(a).to(gpu)
+    wf, nn_ = ops.kpconv_gather(T(q), T(s), T(idx), T(x), T(kp), ext)
+    # torch fp32 reference of the same op (blocks:296-381, 395-398)
+    sp = torch.cat([torch.from_numpy(s), torch.zeros(1, 3) + 1e6])
+    nb = sp[torch.from_numpy(idx)] - torch.from_numpy(q).unsqueeze(1)
+    d2 = ((nb.unsqueeze(2) - torch.from_numpy(kp)) ** 2).sum(3)
+    w = torch.clamp(1 - torch.sqrt(d2) / ext, min=0).transpose(1, 2)
+    xp = torch.cat([torch.from_numpy(x), torch.zeros(1, cin)])
+    nx = xp[torch.from_numpy(idx)]
+    ref = torch.matmul(w, nx)
+    assert rel_err(wf, ref) < TOL
+    cnt = torch.clamp((nx.sum(-1) > 0).sum(-1), min=1).float()
+    assert torch.equal(nn_.cpu(), cnt)
+
+
+def test_instnorm_vs_reference(gpu):
+    import fgreg.ops as ops
+    g = golden('instnorm')
+    lens = [int(v) for v in g['lengths']]
+    out = ops.instnorm(torch.from_numpy(g['x']).to(gpu), ops.offsets(lens, gpu), len(lens))
+    assert rel_err(out, g['out']) < TOL
+
+
+def test_instnorm_fusions_vs_torch(gpu):
+    import fgreg.ops as ops
+    rng = np.random.default_rng(5)
+    lens = [700, 1, 33, 512]
+    x = torch.from_numpy(rng.normal(2, 3, (sum(lens), 72)).astype(np.float32))
+    div = torch.from_numpy(rng.integers(1, 9, sum(lens)).astype(np.float32))
+    res = torch.from_numpy(rng.normal(size=x.shape).astype(np.float32))
+    ref = mo.instance_norm(x / div[:, None], torch.tensor(lens))
+    ref_act = torch.nn.functional.leaky_relu(ref, 0.1)
+    ref_res = torch.nn.functional.leaky_relu(ref + res, 0.1)
+    off = ops.offsets(lens, gpu)
+    X, D, R = x.to(gpu), div.to(gpu), res.to(gpu)
+    assert rel_err(ops.instnorm(X, off, 4, row_div=D), ref) < TOL
+    assert rel_err(ops.instnorm(X, off, 4, row_div=D, act=ops.ACT_LEAKY), ref_act) < TOL
+    assert rel_err(ops.instnorm(X, off, 4, row_div=D, residual=R, post_act=ops.ACT_LEAKY),
+                   ref_res) < TOL
+
+
+@pytest.mark.parametrize('d', [32, 256, 512])
+def test_sine_pos_embed_vs_reference(gpu, d):
+    import fgreg.ops as ops
+    g = golden('pos_embed')
+    xyz = torch.from_numpy(g['xyz']).to(gpu)
+    if d == 32:
+        ref = mo.sine_pos_embed(torch.from_numpy(g['xyz']), 32)
+    else:
+        ref = torch.from_numpy(g[f'pe{d}'])
+    assert rel_err(ops.sine_pos_embed(xyz, d), ref) < TOL
+
+
+def test_layernorm_vs_torch(gpu):
+    import fgreg.ops as ops
+    rng = np.random.default_rng(1)
+    for d in (32, 256, 512):
+        x = torch.from_numpy(rng.normal(1, 2, (333, d)).astype(np.float32))
+        w = torch.from_numpy(rng.normal(1, 0.1, d).astype(np.float32))
+        b = torch.from_numpy(rng.normal(0, 0.1, d).astype(np.float32))
+        a = torch.from_numpy(rng.normal(size=(333, d)).astype(np.float32))
+        ref = torch.nn.functional.layer_norm(x, (d,), w, b, 1e-5) + a
+        out = ops.layernorm(x.to(gpu), w.to(gpu), b.to(gpu), 1e-5, add=a.to(gpu))
+        assert rel_err(out, ref) < TOL
+
+
+def _attn_ref(q, k, v, qlens, klens, kv_seg, nhead):
+    """Per-segment fp32 softmax attention with torch (MHA core, scale sqrt(1/dh))."""
+    d = q.shape[1]
+    dh = d // nhead
+    qo = np.cumsum([0] + qlens)
+    ko = np.cumsum([0] + klens)
+    out = torch.zeros_like(q)
+    for i in range(len(qlens)):
+        j = kv_seg[i]
+        qs = q[qo[i]:qo[i + 1]].view(-1, nhead, dh).transpose(0, 1) * math.sqrt(1.0 / dh)
+        ks = k[ko[j]:ko[j + 1]].view(-1, nhead, dh).transpose(0, 1)
+        vs = v[ko[j]:ko[j + 1]].view(-1, nhead, dh).transpose(0, 1)
+        a = torch.softmax(qs @ ks.transpose(1, 2), -1) @ vs
+        out[qo[i]:qo[i + 1]] = a.transpose(0, 1).reshape(-1, d)
+    return out
+
+
+@pytest.mark.parametrize('nhead,d', [(8, 32), (8, 64), (8, 256), (8, 512), (1, 256), (2, 16)])
+def test_attention_vs_torch(gpu, nhead, d):
+    import fgreg.ops as ops
+    rng = np.random.default_rng(d + nhead)
+    lens = [575, 1, 64, 130, 300, 65]   # 3 "pairs": segment c attends to (c + 3) % 6
+    n = sum(lens)
+    qkv = torch.from_numpy(rng.normal(size=(n, 3 * d)).astype(np.float32)) * 2
+    q, k, v = qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:]
+    for kv_seg in ([0, 1, 2, 3, 4, 5], [3, 4, 5, 0, 1, 2]):
+        ref = _attn_ref(q, k, v, lens, lens, kv_seg, nhead)
+        g = qkv.to(gpu)
+        off = ops.offsets(lens, gpu)
+        seg = torch.tensor(kv_seg, dtype=torch.int32, device=gpu)
+        out = ops.attention(g[:, :d], g[:, d:2 * d], g[:, 2 * d:], off, off, seg, max(lens), nhead)
+        assert rel_err(out, ref) < TOL
+
+
+def test_transformer_layer_vs_reference(gpu):
+    """One TransformerCrossEncoderLayer.forward_pre (transformers.py:183-244), B = 2 with
+    unequal lengths, against the reference module's output (padded rows excluded)."""
+    from fgreg.transformer import Segments, TransformerCrossEncoderLayer
+    g = golden('transformer_layer')
+    layer = TransformerCrossEncoderLayer(64, 8, 128, 0.0, normalize_before=True,
+                                         sa_val_has_pos_emb=True, ca_val_has_pos_emb=True)
+    sd = {k[2:]: torch.from_numpy(g[k]) for k in g.files if k.startswith('w.')}
+    layer.load_state_dict(sd)
+    layer = layer.to(gpu).eval()
+    smask, tmask = g['src_mask'], g['tgt_mask']
+    ns = [int((~smask[b]).sum()) for b in range(2)]
+    nt = [int((~tmask[b]).sum()) for b in range(2)]
+    rows = [g['src'][:ns[b], b] for b in range(2)] + [g['tgt'][:nt[b], b] for b in range(2)]
+    prow = [g['src_pos'][:ns[b], b] for b in range(2)] + [g['tgt_pos'][:nt[b], b] for b in range(2)]
+    x = torch.from_numpy(np.concatenate(rows)).to(gpu)
+    pos = torch.from_numpy(np.concatenate(prow)).to(gpu)
+    seg = Segments(ns + nt, gpu)
+    with torch.no_grad():
+        y = layer.forward_packed(x, pos, seg).cpu().numpy()
+    ref = np.concatenate([g['src_out'][:ns[b], b] for b in range(2)] +
+                         [g['tgt_out'][:nt[b], b] for b in range(2)])
+    assert rel_err(y, ref) < TOL
+
+
+@pytest.mark.parametrize('case', ['regular', 'reflection', 'allzero', 'threshold'])
+def test_procrustes_vs_reference(gpu, case):
+    from fgreg.pose import compute_rigid_transform, fast_compute_rigid_transform
+    g = golden('procrustes')
+    a, b, w = (torch.from_numpy(g[f'{case}_{k}']).to(gpu) for k in 'abw')
+    w_copy = w.clone()
+    fast = fast_compute_rigid_transform(a, b, w_copy)
+    full = compute_rigid_transform(a, b, w)
+    for got, want in ((fast, g[f'{case}_fast']), (full, g[f'{case}_full'])):
+        got = got.cpu().numpy()
+        assert np.abs(got[..., :3] - want[..., :3]).max() < TOL
+        assert np.abs(got[..., 3] - want[..., 3]).max() < TOL * max(1.0, np.abs(want[..., 3]).max())
+    # in-place thresholding, as the reference (se3_torch.py:240-242)
+    thr = g[f'{case}_w'].copy()
+    thr[~(thr > 0.85)] = 0
+    assert np.array_equal(w_copy.cpu().numpy(), thr)
