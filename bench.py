@@ -78,12 +78,12 @@ def main():
     src, tgt, _ = make_batch('modelnet', P, start=rank * P)     # this rank's shard of pairs
     batch_src = [torch.from_numpy(s).to(dev) for s in src]
     batch_tgt = [torch.from_numpy(t).to(dev) for t in tgt]
-    gathered = [torch.empty((6, P, 3, 4), device=dev) for _ in range(world)] if world > 1 else None
+    from fgreg import dist as fdist
 
     def step():
         out = model({'src_xyz': batch_src, 'tgt_xyz': batch_tgt})
-        if dist is not None:
-            dist.all_gather(gathered, out['pose'].contiguous())
+        if dist is not None:   # the one exchange: per-pair poses of every rank (RCCL)
+            out['pose_all'] = fdist.gather_pair_results(out['pose'], [P] * world, pair_dim=1)
         return out
 
     with torch.no_grad():

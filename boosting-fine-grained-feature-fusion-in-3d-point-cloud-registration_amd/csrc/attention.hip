@@ -158,6 +158,202 @@ attn_fwd_kernel(const float* __restrict__ q, int64_t ld_q, const float* __restri
     }
 }
 
+// ------------------------------------------------------------------------------------
+// v2 (DH in {16, 32, 64}): each wave owns RG x 16 query rows sharing every K/V operand
+// read; LDS images are laid out so that each lane's operands for 4 consecutive k-steps
+// are contiguous (one ds_read_b128 per 4 MFMAs); the next K/V tile is prefetched into
+// registers while the current one is consumed; softmax in base 2 on a log2(e)-prescaled Q.
+//   K image  k_lds[key][g][kk]      (d = 4 kk + g),           row pad 4
+//   V image  v_lds[g][dim][kk]      (key = 4 kk + g),         row pad 4
+//   P image  p_lds[wave][row][g][kk] (key = 4 kk + g),        row pad 4
+// ------------------------------------------------------------------------------------
+template <int DH, int RG>
+__global__ void __launch_bounds__(256)
+attn_fwd_v2(const float* __restrict__ q, int64_t ld_q, const float* __restrict__ k,
+            int64_t ld_k, const float* __restrict__ v, int64_t ld_v, float* __restrict__ o,
+            int64_t ld_o, const int64_t* __restrict__ q_off, const int64_t* __restrict__ kv_off,
+            const int32_t* __restrict__ kv_seg, float scale_log2) {
+    constexpr int KS = DH / 4;             // k-steps of S (multiple of 4)
+    constexpr int NT = DH / 16;            // output column tiles
+    constexpr int KROW = DH + 4;           // K image row (floats)
+    constexpr int VROW = kBK / 4 + 4;      // V image (g, dim) row: 16 kk + pad
+    constexpr int PROW = kBK + 4;          // P image row
+    constexpr int BQ = 64 * RG;            // query rows per block
+    constexpr int F4 = kBK * DH / 4 / 256; // float4 per thread per tile (K and V each)
+    static_assert(KS % 4 == 0 && F4 >= 1, "DH must be a multiple of 16");
+    __shared__ float k_lds[kBK * KROW];
+    __shared__ float v_lds[4 * DH * VROW];
+    __shared__ float p_lds[4][16 * PROW];
+
+    const int seg = blockIdx.z, head = blockIdx.y;
+    const int64_t qb = q_off[seg], qe = q_off[seg + 1];
+    const int64_t q0 = qb + (int64_t)blockIdx.x * BQ;
+    if (q0 >= qe) return;                              // block-uniform
+    const int ks = kv_seg[seg];
+    const int64_t kb = kv_off[ks];
+    const int nk = (int)(kv_off[ks + 1] - kb);
+    const int tid = threadIdx.x, wv = tid / 64, lane = tid % 64;
+    const int g = lane >> 4, c = lane & 15;
+
+    float qf[RG][KS];
+#pragma unroll
+    for (int rg = 0; rg < RG; ++rg) {
+        const int64_t row = q0 + wv * 16 * RG + rg * 16 + c;
+        const bool ok = row < qe;
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk)
+            qf[rg][kk] = ok ? q[row * ld_q + head * DH + kk * 4 + g] * scale_log2 : 0.f;
+    }
+    f32x4 acc[RG][NT];
+    float m_run[RG][4], l_run[RG][4];
+#pragma unroll
+    for (int rg = 0; rg < RG; ++rg) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[rg][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { m_run[rg][r] = -INFINITY; l_run[rg][r] = 0.f; }
+    }
+
+    // tile staging: thread handles F4 float4 of K and of V per tile
+    float4 kr[F4], vr[F4];
+    auto load_tile = [&](int k0) {
+#pragma unroll
+        for (int i = 0; i < F4; ++i) {
+            const int e = tid + 256 * i;             // float4 index in the 64 x DH tile
+            const int key = e / (DH / 4), d0 = (e % (DH / 4)) * 4;
+            if (k0 + key < nk) {
+                const int64_t row = kb + k0 + key;
+                kr[i] = *reinterpret_cast<const float4*>(k + row * ld_k + head * DH + d0);
+                vr[i] = *reinterpret_cast<const float4*>(v + row * ld_v + head * DH + d0);
+            } else {
+                kr[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+                vr[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        }
+    };
+    auto store_tile = [&]() {
+#pragma unroll
+        for (int i = 0; i < F4; ++i) {
+            const int e = tid + 256 * i;
+            const int key = e / (DH / 4), d0 = (e % (DH / 4)) * 4;
+            const int kk = d0 >> 2;                  // d = 4 kk + g, g = 0..3
+            float* kp = k_lds + key * KROW + kk;
+            kp[0 * KS] = kr[i].x; kp[1 * KS] = kr[i].y; kp[2 * KS] = kr[i].z; kp[3 * KS] = kr[i].w;
+            const int vg = key & 3, vkk = key >> 2;  // key = 4 kk + g
+            float* vp = v_lds + (vg * DH + d0) * VROW + vkk;
+            vp[0 * VROW] = vr[i].x; vp[1 * VROW] = vr[i].y; vp[2 * VROW] = vr[i].z; vp[3 * VROW] = vr[i].w;
+        }
+    };
+
+    load_tile(0);
+    for (int k0 = 0; k0 < nk; k0 += kBK) {
+        const int nt = min(kBK, nk - k0);
+        __syncthreads();                             // previous tile fully consumed
+        store_tile();
+        __syncthreads();
+        if (k0 + kBK < nk) load_tile(k0 + kBK);      // prefetch next tile (in flight)
+
+#pragma unroll
+        for (int rg = 0; rg < RG; ++rg) {
+            // S = Q K^T (16 rows x 64 keys), base-2 logits
+            f32x4 sv[4];
+#pragma unroll
+            for (int n = 0; n < 4; ++n) sv[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int k4 = 0; k4 < KS; k4 += 4) {
+                float4 b4[4];
+#pragma unroll
+                for (int n = 0; n < 4; ++n)
+                    b4[n] = *reinterpret_cast<const float4*>(k_lds + (n * 16 + c) * KROW + g * KS + k4);
+                // 4 independent accumulators interleaved (dependent-issue latency 40 > 32)
+#pragma unroll
+                for (int n = 0; n < 4; ++n) sv[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(qf[rg][k4 + 0], b4[n].x, sv[n], 0, 0, 0);
+#pragma unroll
+                for (int n = 0; n < 4; ++n) sv[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(qf[rg][k4 + 1], b4[n].y, sv[n], 0, 0, 0);
+#pragma unroll
+                for (int n = 0; n < 4; ++n) sv[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(qf[rg][k4 + 2], b4[n].z, sv[n], 0, 0, 0);
+#pragma unroll
+                for (int n = 0; n < 4; ++n) sv[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(qf[rg][k4 + 3], b4[n].w, sv[n], 0, 0, 0);
+            }
+            float alpha[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float mx = -INFINITY;
+#pragma unroll
+                for (int n = 0; n < 4; ++n) {
+                    if (n * 16 + c >= nt) sv[n][r] = -INFINITY;
+                    mx = fmaxf(mx, sv[n][r]);
+                }
+                mx = row16_max(mx);
+                const float m_new = fmaxf(m_run[rg][r], mx);
+                const float m_use = m_new == -INFINITY ? 0.f : m_new;
+                alpha[r] = exp2f(m_run[rg][r] - m_use);
+                float rs = 0.f;
+#pragma unroll
+                for (int n = 0; n < 4; ++n) {
+                    const float p = exp2f(sv[n][r] - m_use);
+                    sv[n][r] = p;
+                    rs += p;
+                }
+                rs = row16_sum(rs);
+                l_run[rg][r] = l_run[rg][r] * alpha[r] + rs;
+                m_run[rg][r] = m_new;
+            }
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) acc[rg][t][r] *= alpha[r];
+            // P (C layout) -> p_lds[row][g][kk] -> A operand
+            float* pw = p_lds[wv];
+#pragma unroll
+            for (int n = 0; n < 4; ++n) {
+                const int pg = c & 3, pkk = n * 4 + (c >> 2);   // key n*16 + c = 4 pkk + pg
+#pragma unroll
+                for (int r = 0; r < 4; ++r) pw[(4 * g + r) * PROW + pg * 16 + pkk] = sv[n][r];
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int k4 = 0; k4 < kBK / 4; k4 += 4) {
+                const float4 a4 = *reinterpret_cast<const float4*>(pw + c * PROW + g * 16 + k4);
+#pragma unroll
+                for (int t = 0; t < NT; ++t) {
+                    const float4 b4 = *reinterpret_cast<const float4*>(
+                        v_lds + (g * DH + t * 16 + c) * VROW + k4);
+                    acc[rg][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.x, b4.x, acc[rg][t], 0, 0, 0);
+                    acc[rg][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.y, b4.y, acc[rg][t], 0, 0, 0);
+                    acc[rg][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.z, b4.z, acc[rg][t], 0, 0, 0);
+                    acc[rg][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.w, b4.w, acc[rg][t], 0, 0, 0);
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+    }
+#pragma unroll
+    for (int rg = 0; rg < RG; ++rg) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int64_t row = q0 + wv * 16 * RG + rg * 16 + 4 * g + r;
+            if (row >= qe) continue;
+            const float inv = 1.0f / l_run[rg][r];
+#pragma unroll
+            for (int t = 0; t < NT; ++t) o[row * ld_o + head * DH + t * 16 + c] = acc[rg][t][r] * inv;
+        }
+    }
+}
+
+template <int DH, int RG>
+void launch_v2(int max_q_len, int n_head, int n_seg, hipStream_t st, const float* q, int64_t ld_q,
+               const float* k, int64_t ld_k, const float* v, int64_t ld_v, float* o, int64_t ld_o,
+               const int64_t* q_off, const int64_t* kv_off, const int32_t* kv_seg, float scale) {
+    dim3 grid((unsigned)ceil_div(max_q_len, 64 * RG), (unsigned)n_head, (unsigned)n_seg);
+    hipLaunchKernelGGL((attn_fwd_v2<DH, RG>), grid, dim3(256), 0, st, q, ld_q, k, ld_k, v, ld_v,
+                       o, ld_o, q_off, kv_off, kv_seg, scale * 1.4426950408889634f);
+}
+
 template <int DH>
 void launch(dim3 grid, hipStream_t st, const float* q, int64_t ld_q, const float* k, int64_t ld_k,
             const float* v, int64_t ld_v, float* o, int64_t ld_o, const int64_t* q_off,
@@ -188,9 +384,9 @@ extern "C" int fgr_attention(const float* q, int64_t ld_q, const float* k, int64
     switch (head_dim) {
         case 4: launch<4>(grid, st, q, ld_q, k, ld_k, v, ld_v, o, ld_o, q_off, kv_off, kv_seg, scale); break;
         case 8: launch<8>(grid, st, q, ld_q, k, ld_k, v, ld_v, o, ld_o, q_off, kv_off, kv_seg, scale); break;
-        case 16: launch<16>(grid, st, q, ld_q, k, ld_k, v, ld_v, o, ld_o, q_off, kv_off, kv_seg, scale); break;
-        case 32: launch<32>(grid, st, q, ld_q, k, ld_k, v, ld_v, o, ld_o, q_off, kv_off, kv_seg, scale); break;
-        case 64: launch<64>(grid, st, q, ld_q, k, ld_k, v, ld_v, o, ld_o, q_off, kv_off, kv_seg, scale); break;
+        case 16: launch_v2<16, 2>(max_q_len, n_head, n_seg, st, q, ld_q, k, ld_k, v, ld_v, o, ld_o, q_off, kv_off, kv_seg, scale); break;
+        case 32: launch_v2<32, 2>(max_q_len, n_head, n_seg, st, q, ld_q, k, ld_k, v, ld_v, o, ld_o, q_off, kv_off, kv_seg, scale); break;
+        case 64: launch_v2<64, 2>(max_q_len, n_head, n_seg, st, q, ld_q, k, ld_k, v, ld_v, o, ld_o, q_off, kv_off, kv_seg, scale); break;
         case 128: launch<128>(grid, st, q, ld_q, k, ld_k, v, ld_v, o, ld_o, q_off, kv_off, kv_seg, scale); break;
         case 256: launch<256>(grid, st, q, ld_q, k, ld_k, v, ld_v, o, ld_o, q_off, kv_off, kv_seg, scale); break;
         default:

@@ -56,6 +56,27 @@ __device__ __forceinline__ float wave_max(float v) {
     return v;
 }
 
+// Reductions over the 16 lanes of a DPP row (lanes 16k..16k+15) on the VALU (no LDS
+// crossbar): xor 1, xor 2 (quad_perm), then half-row and row mirrors.
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row16_max(float v) {
+    v = fmaxf(v, dpp<0xB1>(v));    // quad_perm [1,0,3,2]
+    v = fmaxf(v, dpp<0x4E>(v));    // quad_perm [2,3,0,1]
+    v = fmaxf(v, dpp<0x141>(v));   // row_half_mirror
+    v = fmaxf(v, dpp<0x140>(v));   // row_mirror
+    return v;
+}
+__device__ __forceinline__ float row16_sum(float v) {
+    v += dpp<0xB1>(v);
+    v += dpp<0x4E>(v);
+    v += dpp<0x141>(v);
+    v += dpp<0x140>(v);
+    return v;
+}
+
 // Index of the segment containing row r, given sorted offsets off[0..n] (off[0] = 0).
 __device__ __forceinline__ int find_segment(const int64_t* off, int n, int64_t r) {
     int lo = 0, hi = n - 1;

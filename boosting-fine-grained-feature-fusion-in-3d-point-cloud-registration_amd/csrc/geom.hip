@@ -233,6 +233,36 @@ radius_index_kernel(const float* __restrict__ q, const int64_t* __restrict__ q_o
     }
 }
 
+// mode INDEX, one wave per query: the wave sweeps the cloud's supports 64 at a time in
+// index order (coalesced 768-B loads), keeps hits with a ballot and writes them at their
+// prefix-count positions, and stops as soon as `width` hits are stored.
+constexpr int kWaveQueries = 4;
+
+__global__ void __launch_bounds__(64 * kWaveQueries)
+radius_index_wave_kernel(const float* __restrict__ q, const int64_t* __restrict__ q_off,
+                         const float* __restrict__ s, const int64_t* __restrict__ s_off, float r2,
+                         int width, int64_t ns_total, int64_t* __restrict__ out) {
+    const int c = blockIdx.y;
+    const int lane = threadIdx.x % 64;
+    const int64_t qb = q_off[c], qe = q_off[c + 1];
+    const int64_t qi = qb + (int64_t)blockIdx.x * kWaveQueries + threadIdx.x / 64;
+    if (qi >= qe) return;                                   // wave-uniform
+    const int64_t sb = s_off[c], se = s_off[c + 1];
+    const float qx = q[3 * qi], qy = q[3 * qi + 1], qz = q[3 * qi + 2];
+    int64_t* row = out + qi * width;
+    int cnt = 0;
+    for (int64_t j0 = sb; j0 < se && cnt < width; j0 += 64) {
+        const int64_t j = j0 + lane;
+        bool hit = false;
+        if (j < se) hit = dist2(qx, qy, qz, s[3 * j], s[3 * j + 1], s[3 * j + 2]) < r2;
+        const unsigned long long m = __ballot(hit);
+        const int pos = cnt + __popcll(m & ((1ull << lane) - 1ull));
+        if (hit && pos < width) row[pos] = j;
+        cnt += __popcll(m);
+    }
+    for (int k = (cnt < width ? cnt : width) + lane; k < width; k += 64) row[k] = ns_total;
+}
+
 // mode DIST (nanoflann sorted + [:, :K]): per-thread sorted (d2, idx) list in LDS.
 constexpr int kDistBlock = 64;
 constexpr int kDistTile = 512;
@@ -392,9 +422,9 @@ extern "C" int fgr_radius_search(const float* q, const int64_t* q_off, const flo
     hipStream_t st = as_stream(stream);
     const float r2 = radius * radius;
     if (mode == FGR_NB_INDEX) {
-        dim3 grid((unsigned)ceil_div(max_q_len, kRadBlock), (unsigned)n_clouds);
-        hipLaunchKernelGGL(radius_index_kernel<false>, grid, dim3(kRadBlock), 0, st, q, q_off, s,
-                           s_off, r2, width, ns, out, (int*)nullptr, (int*)nullptr);
+        dim3 grid((unsigned)ceil_div(max_q_len, kWaveQueries), (unsigned)n_clouds);
+        hipLaunchKernelGGL(radius_index_wave_kernel, grid, dim3(64 * kWaveQueries), 0, st, q, q_off,
+                           s, s_off, r2, width, ns, out);
     } else {
         dim3 grid((unsigned)ceil_div(max_q_len, kDistBlock), (unsigned)n_clouds);
         hipLaunchKernelGGL(radius_dist_kernel, grid, dim3(kDistBlock), 0, st, q, q_off, s, s_off,

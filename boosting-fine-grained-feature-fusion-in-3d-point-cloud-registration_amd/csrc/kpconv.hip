@@ -23,12 +23,6 @@ constexpr int kMaxKp = 32;         // kernel points supported (configs use 15)
 constexpr int kGatherWaves = 4;    // waves (= queries) per block, wide kernel
 
 template <int VEC>
-struct VecT;
-template <> struct VecT<1> { using T = float; };
-template <> struct VecT<2> { using T = float2; };
-template <> struct VecT<4> { using T = float4; };
-
-template <int VEC>
 __device__ __forceinline__ void load_vec(const float* p, float (&v)[VEC]) {
     if constexpr (VEC == 1) {
         v[0] = p[0];
@@ -204,6 +198,47 @@ void launch_wide(const float* q, const float* s, int64_t nq, int64_t ns, const i
                            st, q, s, nq, ns, idx, width, x, kp, n_kp, inv_ext, wf, nnorm);
 }
 
+// max_pool, one wave per query (c % 64 == 0, VEC floats per lane): valid neighbours are
+// compacted by ballot, their feature rows read with 16-B loads; a shadow entry in the
+// row contributes the appended zero row (blocks:134-140).
+template <int VEC>
+__global__ void __launch_bounds__(256)
+max_pool_wave(const float* __restrict__ x, int64_t ns, const int64_t* __restrict__ idx,
+              int64_t nq, int width, float* __restrict__ out) {
+    constexpr int C = 64 * VEC;
+    __shared__ int nb_lds[4][64];
+    const int wv = threadIdx.x / 64, lane = threadIdx.x % 64;
+    const int64_t qi = (int64_t)blockIdx.x * 4 + wv;
+    if (qi >= nq) return;
+    const int64_t* row = idx + qi * width;
+    float m[VEC];
+    bool shadow = false;
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) m[j] = -INFINITY;
+    for (int h0 = 0; h0 < width; h0 += 64) {
+        const int h = h0 + lane;
+        const int64_t id = h < width ? row[h] : 0;
+        const bool valid = h < width && id >= 0 && id < ns;
+        shadow |= (h < width && !valid);
+        const unsigned long long bm = __ballot(valid);
+        const int v = __popcll(bm);
+        if (valid) nb_lds[wv][__popcll(bm & ((1ull << lane) - 1ull))] = (int)id;
+        __builtin_amdgcn_wave_barrier();
+        for (int hh = 0; hh < v; ++hh) {
+            float xv[VEC];
+            load_vec<VEC>(x + (int64_t)nb_lds[wv][hh] * C + lane * VEC, xv);
+#pragma unroll
+            for (int j = 0; j < VEC; ++j) m[j] = fmaxf(m[j], xv[j]);
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (__ballot(shadow) != 0ull) {
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) m[j] = fmaxf(m[j], 0.f);
+    }
+    store_vec<VEC>(out + qi * C + lane * VEC, m);
+}
+
 // max_pool: one thread per (query, channel); shadows contribute the appended zero row.
 __global__ void max_pool_kernel(const float* __restrict__ x, int64_t ns, int c,
                                 const int64_t* __restrict__ idx, int64_t nq, int width,
@@ -264,9 +299,18 @@ extern "C" int fgr_max_pool(const float* x, int64_t ns, int32_t c, const int64_t
     FGR_REQUIRE(ns >= 0 && c > 0 && nq >= 0 && width > 0, "fgr_max_pool: bad arguments");
     FGR_REQUIRE(nq == 0 || (x && idx && out), "fgr_max_pool: null pointer");
     if (nq == 0) return FGR_OK;
-    const int64_t n = nq * c;
-    hipLaunchKernelGGL(max_pool_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0,
-                       as_stream(stream), x, ns, c, idx, nq, width, out);
+    hipStream_t st = as_stream(stream);
+    if (c == 64 || c == 128 || c == 256 || c == 512) {
+        dim3 grid((unsigned)ceil_div(nq, 4));
+        if (c == 64) hipLaunchKernelGGL(max_pool_wave<1>, grid, dim3(256), 0, st, x, ns, idx, nq, width, out);
+        else if (c == 128) hipLaunchKernelGGL(max_pool_wave<2>, grid, dim3(256), 0, st, x, ns, idx, nq, width, out);
+        else if (c == 256) hipLaunchKernelGGL(max_pool_wave<4>, grid, dim3(256), 0, st, x, ns, idx, nq, width, out);
+        else hipLaunchKernelGGL(max_pool_wave<8>, grid, dim3(256), 0, st, x, ns, idx, nq, width, out);
+    } else {
+        const int64_t n = nq * c;
+        hipLaunchKernelGGL(max_pool_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, st, x,
+                           ns, c, idx, nq, width, out);
+    }
     FGR_CHECK_LAUNCH("max_pool_kernel");
     return FGR_OK;
 }

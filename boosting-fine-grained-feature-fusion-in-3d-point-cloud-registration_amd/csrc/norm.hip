@@ -11,81 +11,145 @@ __device__ __forceinline__ float act_fn(float v, int act) {
     return v;
 }
 
-constexpr int kInWaves = 8;  // waves per block, each sweeps rows with stride kInWaves
+// Segmented instance norm. Block = 16 waves x 64 channels (lane = channel); a block
+// owns a chunk of up to kChunk rows of one segment and keeps it in registers
+// (kRpw rows per wave), so x is read from HBM once. Segments longer than one chunk
+// are reduced in two launches: per-chunk (n, mean, M2) partials, then a Chan merge
+// fused with the normalising write.
+constexpr int kInW = 16;               // waves per block
+constexpr int kRpw = 48;               // rows per wave held in registers (no spills)
+constexpr int kChunk = kInW * kRpw;    // rows per block
 
-// Block = (segment, 64-channel slab). Two-pass mean / biased variance over the segment's
-// rows, then the normalised write (nn.InstanceNorm1d, affine=False, eps inside the sqrt).
-__global__ void __launch_bounds__(64 * kInWaves)
-instnorm_kernel(const float* __restrict__ x, int c, const int64_t* __restrict__ seg_off,
-                const float* __restrict__ row_div, float eps, int act,
-                const float* __restrict__ residual, int post_act, float* __restrict__ out) {
-    __shared__ float red[kInWaves][64];
-    const int seg = blockIdx.y;
+struct InArgs {
+    const float* x;
+    int c;
+    const int64_t* seg_off;
+    const float* row_div;
+    float eps;
+    int act;
+    const float* residual;
+    int post_act;
+    float* out;
+    float* part;      // [n_seg][n_chunks][3][c] partials (multi-chunk only)
+    int n_chunks;
+};
+
+__device__ __forceinline__ float block_sum16(float v, float (*red)[64], int wv, int lane) {
+    red[wv][lane] = v;
+    __syncthreads();
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < kInW; ++w) t += red[w][lane];
+    __syncthreads();
+    return t;
+}
+
+// MODE 0: single chunk -> stats + normalise; MODE 1: write partials; MODE 2: merge + normalise.
+template <int MODE>
+__global__ void __launch_bounds__(64 * kInW) instnorm_chunk_kernel(InArgs a) {
+    __shared__ float red[kInW][64];
+    const int seg = blockIdx.y, chunk = blockIdx.z;
     const int wv = threadIdx.x / 64, lane = threadIdx.x % 64;
     const int ch = blockIdx.x * 64 + lane;
-    const bool cok = ch < c;
-    const int64_t b = seg_off[seg], e = seg_off[seg + 1];
-    const float n = (float)(e - b);
+    const bool cok = ch < a.c;
+    const int64_t b = a.seg_off[seg], e = a.seg_off[seg + 1];
+    const int64_t cb = b + (int64_t)chunk * kChunk;
+    if (cb >= e && !(MODE == 0 && chunk == 0)) return;      // block-uniform
     if (e <= b) return;
-
+    const int64_t ce = min(e, cb + kChunk);
+    float v[kRpw];
     float s = 0.f;
-    for (int64_t r = b + wv; r < e; r += kInWaves) {
-        if (cok) {
-            float v = x[r * c + ch];
-            if (row_div) v = v / row_div[r];
-            s += v;
-        }
-    }
-    red[wv][lane] = s;
-    __syncthreads();
-    float tot = 0.f;
+    const int nrow = (int)(ce - cb);                     // rows of this chunk (<= kChunk)
+    const float* xp = a.x + (cb + wv) * a.c + ch;
+    const float* dp = a.row_div ? a.row_div + cb + wv : nullptr;
+    const int step = kInW * a.c;
 #pragma unroll
-    for (int w = 0; w < kInWaves; ++w) tot += red[w][lane];
-    const float mean = tot / n;
-    __syncthreads();
-
-    float sq = 0.f;
-    for (int64_t r = b + wv; r < e; r += kInWaves) {
-        if (cok) {
-            float v = x[r * c + ch];
-            if (row_div) v = v / row_div[r];
-            const float d = v - mean;
+    for (int j = 0; j < kRpw; ++j) {
+        const int rr = wv + kInW * j;
+        float t = 0.f;
+        if (rr < nrow && cok) {
+            t = xp[j * step];
+            if (dp) t = t / dp[j * kInW];
+        }
+        v[j] = t;
+        s += t;
+    }
+    float mean, rstd;
+    if (MODE == 2) {
+        // merge the per-chunk partials of this segment (Chan et al.)
+        float n = 0.f, m = 0.f, m2 = 0.f;
+        const float* pp = a.part + (int64_t)seg * a.n_chunks * 3 * a.c;
+        for (int k = 0; k < a.n_chunks; ++k) {
+            const int64_t kb = b + (int64_t)k * kChunk;
+            if (kb >= e || !cok) break;
+            const float nb = pp[(k * 3 + 0) * a.c + ch];
+            const float mb = pp[(k * 3 + 1) * a.c + ch];
+            const float qb = pp[(k * 3 + 2) * a.c + ch];
+            const float nn = n + nb;
+            const float d = mb - m;
+            m = m + d * (nb / nn);
+            m2 = m2 + qb + d * d * (n * nb / nn);
+            n = nn;
+        }
+        mean = m;
+        rstd = 1.0f / sqrtf(m2 / (float)(e - b) + a.eps);
+    } else {
+        const float cnt = (float)(ce - cb);
+        mean = block_sum16(s, red, wv, lane) / cnt;
+        float sq = 0.f;
+#pragma unroll
+        for (int j = 0; j < kRpw; ++j) {
+            const float d = (wv + kInW * j < nrow) ? v[j] - mean : 0.f;
             sq += d * d;
         }
+        const float m2 = block_sum16(sq, red, wv, lane);
+        if (MODE == 1) {
+            if (wv == 0 && cok) {
+                float* pp = a.part + ((int64_t)seg * a.n_chunks + chunk) * 3 * a.c;
+                pp[0 * a.c + ch] = cnt;
+                pp[1 * a.c + ch] = mean;
+                pp[2 * a.c + ch] = m2;
+            }
+            return;
+        }
+        rstd = 1.0f / sqrtf(m2 / cnt + a.eps);
     }
-    red[wv][lane] = sq;
-    __syncthreads();
-    float tsq = 0.f;
-#pragma unroll
-    for (int w = 0; w < kInWaves; ++w) tsq += red[w][lane];
-    const float rstd = 1.0f / sqrtf(tsq / n + eps);
-
     if (!cok) return;
-    for (int64_t r = b + wv; r < e; r += kInWaves) {
-        float v = x[r * c + ch];
-        if (row_div) v = v / row_div[r];
-        float y = act_fn((v - mean) * rstd, act);
-        if (residual) y = act_fn(y + residual[r * c + ch], post_act);
-        out[r * c + ch] = y;
+    const int64_t o0 = (cb + wv) * a.c + ch;
+    const float* rp = a.residual ? a.residual + o0 : nullptr;
+    float* op = a.out + o0;
+#pragma unroll
+    for (int j = 0; j < kRpw; ++j) {
+        if (wv + kInW * j < nrow) {
+            float y = act_fn((v[j] - mean) * rstd, a.act);
+            if (rp) y = act_fn(y + rp[j * step], a.post_act);
+            op[j * step] = y;
+        }
     }
 }
 
 // One wave per row; d <= 64 * 16.
+// `pre_bias` (optional): x[r] += pre_bias is applied first and written back to x (the
+// pending Linear bias of the residual branch that produced x), then normalised.
 template <int PER>
 __global__ void __launch_bounds__(256)
-layernorm_kernel(const float* __restrict__ x, int64_t n, int d, const float* __restrict__ g,
+layernorm_kernel(float* __restrict__ x, int64_t n, int d, const float* __restrict__ g,
                  const float* __restrict__ bta, float eps, const float* __restrict__ add,
-                 float* __restrict__ out) {
+                 const float* __restrict__ pre_bias, float* __restrict__ out) {
     const int64_t r = (int64_t)blockIdx.x * 4 + threadIdx.x / 64;
     const int lane = threadIdx.x % 64;
     if (r >= n) return;
-    const float* xr = x + r * d;
+    float* xr = x + r * d;
     float v[PER];
     float s = 0.f;
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
         const int col = lane + 64 * j;
         v[j] = col < d ? xr[col] : 0.f;
+        if (pre_bias && col < d) {
+            v[j] += pre_bias[col];
+            xr[col] = v[j];
+        }
         s += v[j];
     }
     const float mean = wave_sum(s) / (float)d;
@@ -136,36 +200,58 @@ __global__ void sine_pe_kernel(const float* __restrict__ xyz, int64_t n, int d, 
 
 using namespace fgr;
 
+extern "C" int fgr_instnorm_workspace(int64_t max_seg_len, int32_t c, int32_t n_seg,
+                                      size_t* bytes) {
+    FGR_REQUIRE(bytes && max_seg_len >= 0 && c > 0 && n_seg > 0, "fgr_instnorm_workspace: bad arguments");
+    const int64_t chunks = ceil_div(max_seg_len, kChunk);
+    *bytes = chunks > 1 ? (size_t)n_seg * chunks * 3 * c * sizeof(float) : 0;
+    return FGR_OK;
+}
+
 extern "C" int fgr_instnorm(const float* x, int64_t n, int32_t c, const int64_t* seg_off,
-                            int32_t n_seg, const float* row_div, float eps, int32_t act,
-                            const float* residual, int32_t post_act, float* out, void* stream) {
-    FGR_REQUIRE(n >= 0 && c > 0 && n_seg > 0 && seg_off && eps >= 0.f,
+                            int32_t n_seg, int64_t max_seg_len, const float* row_div, float eps,
+                            int32_t act, const float* residual, int32_t post_act, float* out,
+                            void* ws, size_t ws_bytes, void* stream) {
+    FGR_REQUIRE(n >= 0 && c > 0 && n_seg > 0 && seg_off && eps >= 0.f && max_seg_len >= 0,
                 "fgr_instnorm: bad arguments");
     FGR_REQUIRE(n == 0 || (x && out), "fgr_instnorm: null pointer");
-    if (n == 0) return FGR_OK;
-    dim3 grid((unsigned)ceil_div(c, 64), (unsigned)n_seg);
-    hipLaunchKernelGGL(instnorm_kernel, grid, dim3(64 * kInWaves), 0, as_stream(stream), x, c,
-                       seg_off, row_div, eps, act, residual, post_act, out);
+    if (n == 0 || max_seg_len == 0) return FGR_OK;
+    const int64_t chunks = ceil_div(max_seg_len, kChunk);
+    InArgs a{x, c, seg_off, row_div, eps, act, residual, post_act, out, (float*)ws, (int)chunks};
+    hipStream_t st = as_stream(stream);
+    const unsigned cx = (unsigned)ceil_div(c, 64);
+    if (chunks == 1) {
+        hipLaunchKernelGGL(instnorm_chunk_kernel<0>, dim3(cx, n_seg, 1), dim3(64 * kInW), 0, st, a);
+    } else {
+        const size_t need = (size_t)n_seg * chunks * 3 * c * sizeof(float);
+        if (!ws || ws_bytes < need) {
+            set_error("fgr_instnorm: workspace %zu < %zu bytes", ws_bytes, need);
+            return FGR_E_WORKSPACE;
+        }
+        hipLaunchKernelGGL(instnorm_chunk_kernel<1>, dim3(cx, n_seg, (unsigned)chunks), dim3(64 * kInW), 0, st, a);
+        FGR_CHECK_LAUNCH("instnorm_partials");
+        hipLaunchKernelGGL(instnorm_chunk_kernel<2>, dim3(cx, n_seg, (unsigned)chunks), dim3(64 * kInW), 0, st, a);
+    }
     FGR_CHECK_LAUNCH("instnorm_kernel");
     return FGR_OK;
 }
 
-extern "C" int fgr_layernorm(const float* x, int64_t n, int32_t d, const float* gamma,
-                             const float* beta, float eps, const float* add, float* out,
-                             void* stream) {
+extern "C" int fgr_layernorm(float* x, int64_t n, int32_t d, const float* gamma,
+                             const float* beta, float eps, const float* add,
+                             const float* pre_bias, float* out, void* stream) {
     FGR_REQUIRE(n >= 0 && d > 0 && d <= 1024 && gamma && beta, "fgr_layernorm: bad arguments");
     FGR_REQUIRE(n == 0 || (x && out), "fgr_layernorm: null pointer");
     if (n == 0) return FGR_OK;
     dim3 grid((unsigned)ceil_div(n, 4));
     hipStream_t st = as_stream(stream);
     if (d <= 64)
-        hipLaunchKernelGGL(layernorm_kernel<1>, grid, dim3(256), 0, st, x, n, d, gamma, beta, eps, add, out);
+        hipLaunchKernelGGL(layernorm_kernel<1>, grid, dim3(256), 0, st, x, n, d, gamma, beta, eps, add, pre_bias, out);
     else if (d <= 256)
-        hipLaunchKernelGGL(layernorm_kernel<4>, grid, dim3(256), 0, st, x, n, d, gamma, beta, eps, add, out);
+        hipLaunchKernelGGL(layernorm_kernel<4>, grid, dim3(256), 0, st, x, n, d, gamma, beta, eps, add, pre_bias, out);
     else if (d <= 512)
-        hipLaunchKernelGGL(layernorm_kernel<8>, grid, dim3(256), 0, st, x, n, d, gamma, beta, eps, add, out);
+        hipLaunchKernelGGL(layernorm_kernel<8>, grid, dim3(256), 0, st, x, n, d, gamma, beta, eps, add, pre_bias, out);
     else
-        hipLaunchKernelGGL(layernorm_kernel<16>, grid, dim3(256), 0, st, x, n, d, gamma, beta, eps, add, out);
+        hipLaunchKernelGGL(layernorm_kernel<16>, grid, dim3(256), 0, st, x, n, d, gamma, beta, eps, add, pre_bias, out);
     FGR_CHECK_LAUNCH("layernorm_kernel");
     return FGR_OK;
 }

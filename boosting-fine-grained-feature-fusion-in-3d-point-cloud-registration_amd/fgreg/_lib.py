@@ -28,11 +28,14 @@ SIGNATURES = {
     'fgr_kpconv_gather': [_vp, _vp, _i64, _i64, _vp, _i32, _vp, _i32, _vp, _i32, _f32, _vp, _vp,
                           _vp],
     'fgr_max_pool': [_vp, _i64, _i32, _vp, _i64, _i32, _vp, _vp],
-    'fgr_instnorm': [_vp, _i64, _i32, _vp, _i32, _vp, _f32, _i32, _vp, _i32, _vp, _vp],
-    'fgr_layernorm': [_vp, _i64, _i32, _vp, _vp, _f32, _vp, _vp, _vp],
+    'fgr_instnorm_workspace': [_i64, _i32, _i32, ctypes.POINTER(_sz)],
+    'fgr_instnorm': [_vp, _i64, _i32, _vp, _i32, _i64, _vp, _f32, _i32, _vp, _i32, _vp, _vp, _sz,
+                     _vp],
+    'fgr_layernorm': [_vp, _i64, _i32, _vp, _vp, _f32, _vp, _vp, _vp, _vp],
     'fgr_sine_pos_embed': [_vp, _i64, _i32, _f32, _f32, _vp, _vp],
     'fgr_attention': [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i32, _i32, _i32,
                       _i32, _f32, _vp],
+    'fgr_res2net_chain': [_vp, _i64, _i32, _i32, _vp, _vp, _vp, _i32, _vp, _i64, _vp],
     'fgr_procrustes': [_vp, _vp, _vp, _i64, _i64, _f32, _vp, _vp],
     'fgr_pair_pose': [_vp, _vp, _vp, _i64, _vp, _i32, _i32, _f32, _vp, _vp],
 }

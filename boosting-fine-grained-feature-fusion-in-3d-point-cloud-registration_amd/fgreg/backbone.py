@@ -198,9 +198,9 @@ class BatchNormBlock(nn.Module):
             raise NotImplementedError('use_batch_norm=False is not used by the reference configs')
         self.in_dim = in_dim
 
-    def forward(self, x, off, n_seg, row_div=None, act=ops.ACT_NONE, residual=None,
+    def forward(self, x, off, lengths, row_div=None, act=ops.ACT_NONE, residual=None,
                 post_act=ops.ACT_NONE):
-        return ops.instnorm(x, off, n_seg, row_div=row_div, act=act, residual=residual,
+        return ops.instnorm(x, off, lengths, row_div=row_div, act=act, residual=residual,
                             post_act=post_act)
 
 
@@ -213,10 +213,10 @@ class UnaryBlock(nn.Module):
         self.mlp = nn.Linear(in_dim, out_dim, bias=False)
         self.batch_norm = BatchNormBlock(out_dim, use_bn, bn_momentum)
 
-    def forward(self, x, off, n_seg, residual=None, post_act=ops.ACT_NONE):
+    def forward(self, x, off, lengths, residual=None, post_act=ops.ACT_NONE):
         y = torch.mm(x, self.mlp.weight.t())
         act = ops.ACT_NONE if self.no_relu else ops.ACT_LEAKY
-        return self.batch_norm(y, off, n_seg, act=act, residual=residual, post_act=post_act)
+        return self.batch_norm(y, off, lengths, act=act, residual=residual, post_act=post_act)
 
 
 class my_Bottle2neck(nn.Module):  # noqa: N801 -- reference name (res2net.py:84)
@@ -258,28 +258,38 @@ class my_Bottle2neck(nn.Module):  # noqa: N801 -- reference name (res2net.py:84)
                     b3d = (b3 + bd).contiguous()
                 else:
                     w3d, b3d = w3, b3
-            self._folded = (key, w1, b1, ws, w3d, b3d)
+                chain = None
+                if w1.is_cuda and ops.res2net_chain_supported(self.width) and self.nums > 0:
+                    chain = (ops.res2net_fragments(torch.stack([wi for wi, _ in ws])),
+                             torch.stack([bi for _, bi in ws]).contiguous())
+            self._folded = (key, w1, b1, ws, w3d, b3d, chain)
         return self._folded[1:]
 
     def forward(self, x):
         if self.training:
             return self._forward_train(x)
-        w1, b1, ws, w3d, b3d = self._folded_params()
-        out = torch.addmm(b1, x, w1.t()).relu_()
+        w1, b1, ws, w3d, b3d, chain = self._folded_params()
+        out = torch._addmm_activation(b1, x, w1.t())
         w = self.width
+        if chain is not None and self.downsample is not None:
+            # one launch for the whole hierarchy + the [.. | x] concat (fgr_res2net_chain)
+            cat_in = torch.empty((x.shape[0], w * self.scale + x.shape[1]), dtype=x.dtype,
+                                 device=x.device)
+            ops.res2net_chain(out, w, self.scale, chain[0], chain[1], x, cat_in)
+            return torch._addmm_activation(b3d, cat_in, w3d.t())
         cat_in = torch.empty((x.shape[0], w * self.scale + (x.shape[1] if self.downsample is not None else 0)),
                              dtype=x.dtype, device=x.device)
         sp = None
         for i in range(self.nums):
             chunk = out[:, i * w:(i + 1) * w]
             sp = chunk if i == 0 else sp + chunk
-            sp = torch.addmm(ws[i][1], sp, ws[i][0].t()).relu_()
+            sp = torch._addmm_activation(ws[i][1], sp, ws[i][0].t())
             cat_in[:, i * w:(i + 1) * w] = sp
         if self.scale != 1:
             cat_in[:, self.nums * w:self.scale * w] = out[:, self.nums * w:self.scale * w]
         if self.downsample is not None:
             cat_in[:, self.scale * w:] = x
-            return torch.addmm(b3d, cat_in, w3d.t()).relu_()
+            return torch._addmm_activation(b3d, cat_in, w3d.t())
         return (torch.addmm(b3d, cat_in, w3d.t()) + x).relu_()
 
     def _forward_train(self, x):
@@ -344,7 +354,7 @@ class SimpleBlock(nn.Module):
         q, s, idx, post = _level_inputs(self.block_name, self.layer_ind, batch)
         lens, off = host_layout(batch, post)
         y, nnorm = self.KPConv.forward_unnormalized(q, s, idx, x)
-        return self.batch_norm(y, off, len(lens), row_div=nnorm, act=ops.ACT_LEAKY)
+        return self.batch_norm(y, off, lens, row_div=nnorm, act=ops.ACT_LEAKY)
 
 
 class ResnetBottleneckBlock(nn.Module):
@@ -374,17 +384,17 @@ class ResnetBottleneckBlock(nn.Module):
         lens_pre, off_pre = host_layout(batch, self.layer_ind)
         lens_post, off_post = host_layout(batch, post)
         if isinstance(self.unary1, UnaryBlock):
-            x = self.unary1(features, off_pre, len(lens_pre))
+            x = self.unary1(features, off_pre, lens_pre)
         else:
             x = features
         y, nnorm = self.KPConv.forward_unnormalized(q, s, idx, x)
-        y = self.batch_norm_conv(y, off_post, len(lens_post), row_div=nnorm)
+        y = self.batch_norm_conv(y, off_post, lens_post, row_div=nnorm)
         # res2net ends in ReLU, so the reference's LeakyReLU at :715 is the identity here
         y = self.res2net(y)
         shortcut = ops.max_pool(features, idx) if 'strided' in self.block_name else features
         if isinstance(self.unary_shortcut, UnaryBlock):
             # LeakyReLU(y + IN(shortcut @ W^T)) in one kernel (:722-725)
-            return self.unary_shortcut(shortcut, off_post, len(lens_post), residual=y,
+            return self.unary_shortcut(shortcut, off_post, lens_post, residual=y,
                                        post_act=ops.ACT_LEAKY)
         return F.leaky_relu(y + shortcut, 0.1)
 

@@ -216,37 +216,51 @@ def max_pool(x, idx) -> torch.Tensor:
 # ------------------------------------------------------------------------------------------
 # normalisation / embedding
 # ------------------------------------------------------------------------------------------
-def instnorm(x, seg_off, n_seg, row_div=None, act=ACT_NONE, residual=None, post_act=ACT_NONE,
+def instnorm(x, seg_off, lengths, row_div=None, act=ACT_NONE, residual=None, post_act=ACT_NONE,
              eps=1e-5, out=None) -> torch.Tensor:
+    """Per-segment InstanceNorm1d with fused row division / activation / residual.
+    ``lengths`` are the host-side segment lengths (their count and max size the launch)."""
     _dev(x, seg_off, row_div, residual)
     x = _c(x, torch.float32)
     n, c = x.shape
+    n_seg = len(lengths)
+    max_len = max(lengths) if n_seg else 0
     if residual is not None:
         residual = _c(residual, torch.float32)
         assert residual.shape == x.shape
     if row_div is not None:
         row_div = _c(row_div, torch.float32)
         assert row_div.shape == (n,)
-    assert seg_off.numel() == n_seg + 1
+    assert seg_off.numel() == n_seg + 1 and sum(lengths) == n
     if out is None:
         out = torch.empty_like(x)
-    _lib.check(_lib.load().fgr_instnorm(_ptr(x), n, c, _ptr(seg_off), n_seg, _ptr(row_div),
-                                        float(eps), act, _ptr(residual), post_act, _ptr(out),
-                                        _stream()), 'fgr_instnorm')
+    L = _lib.load()
+    nb = _lib._sz(0)
+    _lib.check(L.fgr_instnorm_workspace(max_len, c, n_seg, nb), 'fgr_instnorm_workspace')
+    ws = torch.empty(nb.value, dtype=torch.uint8, device=x.device) if nb.value else None
+    _lib.check(L.fgr_instnorm(_ptr(x), n, c, _ptr(seg_off), n_seg, max_len, _ptr(row_div),
+                              float(eps), act, _ptr(residual), post_act, _ptr(out), _ptr(ws),
+                              nb.value, _stream()), 'fgr_instnorm')
     return out
 
 
-def layernorm(x, weight, bias, eps=1e-5, add=None) -> torch.Tensor:
-    _dev(x, weight, bias, add)
-    x = _c(x, torch.float32)
+def layernorm(x, weight, bias, eps=1e-5, add=None, pre_bias=None, out=None) -> torch.Tensor:
+    """LN(x) * weight + bias (+ add). ``pre_bias``: x += pre_bias IN PLACE first."""
+    _dev(x, weight, bias, add, pre_bias)
+    assert x.dtype == torch.float32 and x.is_contiguous()
     n, d = x.shape
     if add is not None:
         add = _c(add, torch.float32)
         assert add.shape == x.shape
-    out = torch.empty_like(x)
+    if pre_bias is not None:
+        pre_bias = _c(pre_bias, torch.float32)
+        assert pre_bias.shape == (d,)
+    if out is None:
+        out = torch.empty_like(x)
+    assert out.is_contiguous() and out.shape == x.shape
     _lib.check(_lib.load().fgr_layernorm(_ptr(x), n, d, _ptr(weight.contiguous()),
-                                         _ptr(bias.contiguous()), float(eps), _ptr(add), _ptr(out),
-                                         _stream()), 'fgr_layernorm')
+                                         _ptr(bias.contiguous()), float(eps), _ptr(add),
+                                         _ptr(pre_bias), _ptr(out), _stream()), 'fgr_layernorm')
     return out
 
 
@@ -259,6 +273,36 @@ def sine_pos_embed(xyz, d_model, temperature=10000.0, scale=1.0) -> torch.Tensor
                                               float(scale * 2 * math.pi), _ptr(out), _stream()),
                'fgr_sine_pos_embed')
     return out
+
+
+# ------------------------------------------------------------------------------------------
+# Res2Net hierarchy
+# ------------------------------------------------------------------------------------------
+def res2net_fragments(weights: torch.Tensor) -> torch.Tensor:
+    """(nums, w, w) Linear weights (out, in) -> MFMA fragment order [i][jt][k4][lane][4]
+    with value W_i[jt*16 + (lane & 15)][(4*k4 + q)*4 + (lane >> 4)]."""
+    nums, w, _ = weights.shape
+    t = weights.reshape(nums, w // 16, 16, w // 16, 4, 4)      # [i, jt, c, k4, q, g]
+    return t.permute(0, 1, 3, 5, 2, 4).contiguous()             # [i, jt, k4, g, c, q]
+
+
+def res2net_chain_supported(w):
+    return w in (112, 224)
+
+
+def res2net_chain(h, w, scale, w_frag, bias, x, cat):
+    """cat[:, :] = [sp_0..sp_{scale-2} | h_{scale-1} | x] (fgr_res2net_chain)."""
+    _dev(h, w_frag, bias, x, cat)
+    h = _c(h, torch.float32)
+    n = h.shape[0]
+    assert h.shape[1] == scale * w and cat.shape[0] == n and cat.stride(1) == 1
+    cin = 0 if x is None else x.shape[1]
+    if x is not None:
+        x = _c(x, torch.float32)
+    _lib.check(_lib.load().fgr_res2net_chain(_ptr(h), n, w, scale, _ptr(w_frag), _ptr(bias),
+                                             _ptr(x), cin, _ptr(cat), cat.stride(0), _stream()),
+               'fgr_res2net_chain')
+    return cat
 
 
 # ------------------------------------------------------------------------------------------

@@ -39,8 +39,8 @@ class CorrespondenceRegressor(nn.Module):
         L, N, d = feats.shape
         f = feats.reshape(L * N, d)
         m = self.coor_mlp
-        h = torch.addmm(m[0].bias, f, m[0].weight.t()).relu_()
-        h = torch.addmm(m[2].bias, h, m[2].weight.t()).relu_()
+        h = torch._addmm_activation(m[0].bias, f, m[0].weight.t())
+        h = torch._addmm_activation(m[2].bias, h, m[2].weight.t())
         corr = torch.addmm(m[4].bias, h, m[4].weight.t())
         logits = torch.addmm(self.conf_logits_decoder.bias, f, self.conf_logits_decoder.weight.t())
         return corr.view(L, N, 3), logits.view(L, N, 1)
@@ -96,6 +96,12 @@ class RegTR(nn.Module):
 
     def __init__(self, cfg, *args, neighbor_mode='ball_query', **kwargs):
         super().__init__()
+        self.build_modules(cfg, neighbor_mode)
+
+    def build_modules(self, cfg, neighbor_mode='ball_query'):
+        """Registers the submodules on ``self`` under the reference's names
+        (finegrained_regtr.py:25-106). Usable on any nn.Module: the drop-in shim of
+        INTEGRATION.md calls it on a GenericRegModel subclass."""
         self.cfg = cfg
         self.preprocessor = PreprocessorHIP(cfg, neighbor_mode=neighbor_mode)
         self.kpf_encoder = KPFEncoder(cfg, cfg.d_embed)

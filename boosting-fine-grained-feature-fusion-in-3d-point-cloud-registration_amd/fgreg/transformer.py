@@ -80,25 +80,31 @@ class TransformerCrossEncoderLayer(nn.Module):
         o = ops.attention(q, k, v, seg.off, seg.off, kv_seg, seg.max_len, self.nhead)
         return o
 
-    def forward_packed(self, x, pos, seg: Segments):
-        """x (N_tot, d) packed clouds -> updated x (forward_pre, transformers.py:183-244)."""
+    def forward_packed(self, x, pos, seg: Segments, pending_bias=None):
+        """x (N_tot, d) packed clouds -> (x, pending bias) (forward_pre, transformers.py:183-244).
+
+        Each residual GEMM adds its product into x without the Linear's bias; that bias is
+        returned as 'pending' and folded into the next LayerNorm launch (which writes the
+        biased x back), saving one elementwise pass per residual branch."""
         # self-attention, shared weights for src and tgt (:193-210)
-        h = ops.layernorm(x, self.norm1.weight, self.norm1.bias, self.norm1.eps, add=pos)
+        h = ops.layernorm(x, self.norm1.weight, self.norm1.bias, self.norm1.eps, add=pos,
+                          pre_bias=pending_bias)
         h0 = None if self.sa_val_has_pos_emb else ops.layernorm(x, self.norm1.weight,
                                                                  self.norm1.bias, self.norm1.eps)
         o = self._attend(self.self_attn, h, h0, self.sa_val_has_pos_emb, seg, seg.self_seg)
-        x = torch.addmm(x, o, self.self_attn.out_proj.weight.t()).add_(self.self_attn.out_proj.bias)
+        x = torch.addmm(x, o, self.self_attn.out_proj.weight.t())
         # cross-attention, both directions at once (:212-229)
-        h = ops.layernorm(x, self.norm2.weight, self.norm2.bias, self.norm2.eps, add=pos)
+        h = ops.layernorm(x, self.norm2.weight, self.norm2.bias, self.norm2.eps, add=pos,
+                          pre_bias=self.self_attn.out_proj.bias)
         h0 = None if self.ca_val_has_pos_emb else ops.layernorm(x, self.norm2.weight,
                                                                  self.norm2.bias, self.norm2.eps)
         o = self._attend(self.multihead_attn, h, h0, self.ca_val_has_pos_emb, seg, seg.cross_seg)
-        x = torch.addmm(x, o, self.multihead_attn.out_proj.weight.t()).add_(
-            self.multihead_attn.out_proj.bias)
+        x = torch.addmm(x, o, self.multihead_attn.out_proj.weight.t())
         # position-wise feed-forward (:231-238)
-        h = ops.layernorm(x, self.norm3.weight, self.norm3.bias, self.norm3.eps)
-        h = torch.addmm(self.linear1.bias, h, self.linear1.weight.t()).relu_()
-        return torch.addmm(x, h, self.linear2.weight.t()).add_(self.linear2.bias)
+        h = ops.layernorm(x, self.norm3.weight, self.norm3.bias, self.norm3.eps,
+                          pre_bias=self.multihead_attn.out_proj.bias)
+        h = torch._addmm_activation(self.linear1.bias, h, self.linear1.weight.t())
+        return torch.addmm(x, h, self.linear2.weight.t()), self.linear2.bias
 
 
 class TransformerCrossEncoder(nn.Module):
@@ -113,19 +119,27 @@ class TransformerCrossEncoder(nn.Module):
 
     def forward_packed(self, x, pos, seg: Segments):
         """-> (L, N_tot, d) normalised intermediates (or (1, N_tot, d))."""
-        inter = []
-        for layer in self.layers:
-            x = layer.forward_packed(x, pos, seg)
-            if self.return_intermediate:
-                inter.append(self._norm(x))
-        if self.return_intermediate:
-            return torch.stack(inter)
-        return self._norm(x).unsqueeze(0)
+        L = len(self.layers)
+        n, d = x.shape
+        inter = torch.empty((L if self.return_intermediate else 1, n, d), dtype=x.dtype,
+                            device=x.device)
+        x = x.clone()                      # the residual stream is updated in place
+        pending = None
+        for l, layer in enumerate(self.layers):
+            x, pending = layer.forward_packed(x, pos, seg, pending)
+            if self.return_intermediate or l == L - 1:
+                self._norm(x, pending, inter[l if self.return_intermediate else 0])
+                pending = None
+        return inter
 
-    def _norm(self, x):
+    def _norm(self, x, pending, out):
         if self.norm is None:
-            return x
-        return ops.layernorm(x, self.norm.weight, self.norm.bias, self.norm.eps)
+            if pending is not None:
+                x.add_(pending)
+            out.copy_(x)
+            return out
+        return ops.layernorm(x, self.norm.weight, self.norm.bias, self.norm.eps,
+                             pre_bias=pending, out=out)
 
 
 class PositionEmbeddingCoordsSine(nn.Module):

@@ -104,19 +104,37 @@ int fgr_max_pool(const float* x, int64_t ns, int32_t c, const int64_t* idx, int6
  * (BatchNormBlock, finegrained_kpconv_blocks.py:498-507), fused with:
  *   v   = row_div ? x[r, c] / row_div[r] : x[r, c]       (KPConv normaliser, :399)
  *   y   = act((v - mean_seg,c) / sqrt(var_seg,c + eps))   (biased variance)
- *   out = residual ? post_act(y + residual[r, c]) : y     (bottleneck sum, :725) */
+ *   out = residual ? post_act(y + residual[r, c]) : y     (bottleneck sum, :725)
+ * Segments of up to 1024 rows are normalised from registers in one launch; longer
+ * ones need a workspace of fgr_instnorm_workspace() bytes (two launches). */
+int fgr_instnorm_workspace(int64_t max_seg_len, int32_t c, int32_t n_seg, size_t* bytes);
 int fgr_instnorm(const float* x, int64_t n, int32_t c, const int64_t* seg_off, int32_t n_seg,
-                 const float* row_div, float eps, int32_t act, const float* residual,
-                 int32_t post_act, float* out, void* stream);
+                 int64_t max_seg_len, const float* row_div, float eps, int32_t act,
+                 const float* residual, int32_t post_act, float* out, void* ws, size_t ws_bytes,
+                 void* stream);
 
 /* Row LayerNorm (nn.LayerNorm, transformers.py:105-107) with an optional added
- * tensor (the positional embedding, transformers.py:194-195): out = LN(x)*g + b (+ add). */
-int fgr_layernorm(const float* x, int64_t n, int32_t d, const float* gamma, const float* beta,
-                  float eps, const float* add, float* out, void* stream);
+ * tensor (the positional embedding, transformers.py:194-195): out = LN(x)*g + b (+ add).
+ * If pre_bias is given, x += pre_bias is applied first and written back to x (the
+ * deferred bias of the Linear that produced the residual stream). */
+int fgr_layernorm(float* x, int64_t n, int32_t d, const float* gamma, const float* beta,
+                  float eps, const float* add, const float* pre_bias, float* out, void* stream);
 
 /* PositionEmbeddingCoordsSine (position_embedding.py:29-49) for 3-D input. */
 int fgr_sine_pos_embed(const float* xyz, int64_t n, int32_t d_model, float temperature,
                        float scale, float* out, void* stream);
+
+/* ---- Res2Net hierarchy ----------------------------------------------------------------
+ * The fine-grained fusion core of my_Bottle2neck (res2net.py:126-148), eval BatchNorm
+ * folded into the Linears: for i < scale - 1,
+ *   sp_i = ReLU(W_i (sp_{i-1} + h_i) + b_i)          (sp_{-1} = 0)
+ * writing cat = [sp_0 .. sp_{scale-2} | h_{scale-1} | x] (the conv3 / downsample operand).
+ * h (n, scale*w), x (n, cin) or NULL, cat (n, ld_cat); w_frag = the (scale-1) folded
+ * (w, w) weights permuted to MFMA fragment order [i][jt][k4][lane][4] (see fgreg/backbone.py);
+ * bias (scale-1, w). Needs w % 112 == 0 (w = 112, 224: the ModelNet / 3DMatch deep widths). */
+int fgr_res2net_chain(const float* h, int64_t n, int32_t w, int32_t scale, const float* w_frag,
+                      const float* bias, const float* x, int32_t cin, float* cat, int64_t ld_cat,
+                      void* stream);
 
 /* ---- attention ---------------------------------------------------------------------
  * Multi-head scaled-dot-product attention core of nn.MultiheadAttention

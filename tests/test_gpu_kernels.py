@@ -69,14 +69,15 @@ def test_instnorm_vs_reference(gpu):
     import fgreg.ops as ops
     g = golden('instnorm')
     lens = [int(v) for v in g['lengths']]
-    out = ops.instnorm(torch.from_numpy(g['x']).to(gpu), ops.offsets(lens, gpu), len(lens))
+    out = ops.instnorm(torch.from_numpy(g["x"]).to(gpu), ops.offsets(lens, gpu), lens)
     assert rel_err(out, g['out']) < TOL
 
 
-def test_instnorm_fusions_vs_torch(gpu):
+@pytest.mark.parametrize('lens', [[700, 1, 33, 512], [3000, 5, 1500, 1024, 1025]])
+def test_instnorm_fusions_vs_torch(gpu, lens):
+    """Register path (segments <= 1024 rows) and the two-launch chunked path."""
     import fgreg.ops as ops
     rng = np.random.default_rng(5)
-    lens = [700, 1, 33, 512]
     x = torch.from_numpy(rng.normal(2, 3, (sum(lens), 72)).astype(np.float32))
     div = torch.from_numpy(rng.integers(1, 9, sum(lens)).astype(np.float32))
     res = torch.from_numpy(rng.normal(size=x.shape).astype(np.float32))
@@ -85,9 +86,9 @@ def test_instnorm_fusions_vs_torch(gpu):
     ref_res = torch.nn.functional.leaky_relu(ref + res, 0.1)
     off = ops.offsets(lens, gpu)
     X, D, R = x.to(gpu), div.to(gpu), res.to(gpu)
-    assert rel_err(ops.instnorm(X, off, 4, row_div=D), ref) < TOL
-    assert rel_err(ops.instnorm(X, off, 4, row_div=D, act=ops.ACT_LEAKY), ref_act) < TOL
-    assert rel_err(ops.instnorm(X, off, 4, row_div=D, residual=R, post_act=ops.ACT_LEAKY),
+    assert rel_err(ops.instnorm(X, off, lens, row_div=D), ref) < TOL
+    assert rel_err(ops.instnorm(X, off, lens, row_div=D, act=ops.ACT_LEAKY), ref_act) < TOL
+    assert rel_err(ops.instnorm(X, off, lens, row_div=D, residual=R, post_act=ops.ACT_LEAKY),
                    ref_res) < TOL
 
 
@@ -169,7 +170,8 @@ def test_transformer_layer_vs_reference(gpu):
     pos = torch.from_numpy(np.concatenate(prow)).to(gpu)
     seg = Segments(ns + nt, gpu)
     with torch.no_grad():
-        y = layer.forward_packed(x, pos, seg).cpu().numpy()
+        y, pending = layer.forward_packed(x.clone(), pos, seg)
+        y = (y + pending).cpu().numpy()
     ref = np.concatenate([g['src_out'][:ns[b], b] for b in range(2)] +
                          [g['tgt_out'][:nt[b], b] for b in range(2)])
     assert rel_err(y, ref) < TOL
@@ -191,3 +193,27 @@ def test_procrustes_vs_reference(gpu, case):
     thr = g[f'{case}_w'].copy()
     thr[~(thr > 0.85)] = 0
     assert np.array_equal(w_copy.cpu().numpy(), thr)
+
+
+@pytest.mark.parametrize('cin,cout', [(128, 512), (256, 1024), (8, 32)])
+def test_res2net_block_vs_oracle(gpu, cin, cout):
+    """my_res2Net (res2net.py:84-159, 231-265) in eval: fused fgr_res2net_chain path for
+    widths 112 / 224, torch path for the narrow width, vs the CPU restatement."""
+    from fgreg.backbone import my_Bottle2neck, my_res2Net
+    torch.manual_seed(cout)
+    m = my_res2Net(my_Bottle2neck, cin, cout, baseWidth=14, scale=8)
+    g = torch.Generator().manual_seed(cin)
+    with torch.no_grad():
+        for mod in m.modules():
+            if isinstance(mod, torch.nn.BatchNorm1d):
+                mod.running_mean.copy_(0.1 * torch.randn(mod.running_mean.shape, generator=g))
+                mod.running_var.copy_(0.75 + 0.5 * torch.rand(mod.running_var.shape, generator=g))
+                mod.weight.copy_(1 + 0.1 * torch.randn(mod.weight.shape, generator=g))
+                mod.bias.copy_(0.1 * torch.randn(mod.bias.shape, generator=g))
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    x = torch.randn(1500, cin, generator=g)
+    ref = mo.res2net(sd, '', x) if False else mo.res2net({f'r.{k}': v for k, v in sd.items()}, 'r', x)
+    m = m.to(gpu).eval()
+    with torch.no_grad():
+        out = m(x.to(gpu))
+    assert rel_err(out, ref) < TOL
