@@ -1,0 +1,224 @@
+// Split-precision GEMM on the bf16 matrix cores: fp32-level accuracy at bf16 MFMA rate.
+//
+//   C[M, N] = act(A[M, K] . W[N, K]^T + bias[N] (+ R[M, N]))
+//
+// A (fp32 activations) is split on the fly, W (fp32 Linear weights, split once on the host)
+// is given as bf16 pairs:  x = x_hi + x_lo,  x_hi = bf16(x),  x_lo = bf16(x - x_hi),
+// and the product is accumulated in fp32 as  A_lo W_hi + A_hi W_lo + A_hi W_hi
+// (v_mfma_f32_16x16x32_bf16, 3 MFMAs per tile step). The dropped A_lo W_lo term and the
+// residual of the two-term split are ~2^-16 relative per product, far below the 1e-4
+// parity bar, while the bf16 MFMA is 16x the fp32 MFMA rate on gfx950 (no xf32 exists).
+//
+// Block = 4 waves (2 x 2), tile BM x BN x 32; each wave owns (BM/2) x (BN/2) as
+// (BM/32) x (BN/32) MFMA tiles. Per 32-deep k-step the next A / W tiles are loaded into
+// registers while the current ones (in LDS, rows padded to 80 B so ds_read_b128 fragment
+// loads are conflict-free) feed the MFMAs.
+#include "common.h"
+
+namespace fgr {
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BK = 32;
+constexpr int PITCH = BK + 8;        // bf16 elements per LDS row (80 B)
+
+struct GemmArgs {
+    const float* A; int64_t lda;
+    const __bf16* Whi; const __bf16* Wlo; int64_t ldw;   // (N, Kp) bf16, Kp % 32 == 0
+    float* C; int64_t ldc;
+    const float* bias;
+    const float* R; int64_t ldr;
+    int M, N, K, act;
+};
+
+template <int BM, int BN>
+__global__ void __launch_bounds__(256) gemm_bf16x3_kernel(GemmArgs p) {
+    constexpr int TM = BM / 32, TN = BN / 32;              // MFMA tiles per wave
+    constexpr int AF4 = BM * BK / 4 / 256;                 // A float4 per thread per k-step
+    constexpr int BV = BN * BK / 8 / 256;                  // W 16-B vectors (hi and lo) per thread
+    static_assert(AF4 >= 1 && BV >= 1, "tile too small");
+    __shared__ __attribute__((aligned(16))) __bf16 a_hi[BM * PITCH];
+    __shared__ __attribute__((aligned(16))) __bf16 a_lo[BM * PITCH];
+    __shared__ __attribute__((aligned(16))) __bf16 w_hi[BN * PITCH];
+    __shared__ __attribute__((aligned(16))) __bf16 w_lo[BN * PITCH];
+
+    // consecutive block ids walk the row panels of one W column panel
+    const int nbm = (p.M + BM - 1) / BM, nbn = (p.N + BN - 1) / BN;
+    const int bid = blockIdx.x;
+    const int bm = bid % nbm, bn = bid / nbm;
+    (void)nbn;
+    const int m0 = bm * BM, n0 = bn * BN;
+
+    const int tid = threadIdx.x, wv = tid / 64, lane = tid % 64;
+    const int wm = (wv >> 1) * (BM / 2), wn = (wv & 1) * (BN / 2);
+    const int fr = lane & 15, fk = (lane >> 4) * 8;
+
+    float4 ar[AF4];
+    uint4 whr[BV], wlr[BV];
+    auto load = [&](int k0) {
+#pragma unroll
+        for (int j = 0; j < AF4; ++j) {
+            const int f = tid + 256 * j;
+            const int row = f / (BK / 4), kc = (f % (BK / 4)) * 4;
+            const int m = m0 + row, k = k0 + kc;
+            ar[j] = (m < p.M && k < p.K)
+                        ? *reinterpret_cast<const float4*>(p.A + (int64_t)m * p.lda + k)
+                        : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int j = 0; j < BV; ++j) {
+            const int f = tid + 256 * j;
+            const int row = f / (BK / 8), kc = (f % (BK / 8)) * 8;
+            const int n = n0 + row;
+            if (n < p.N) {
+                whr[j] = *reinterpret_cast<const uint4*>(p.Whi + (int64_t)n * p.ldw + k0 + kc);
+                wlr[j] = *reinterpret_cast<const uint4*>(p.Wlo + (int64_t)n * p.ldw + k0 + kc);
+            } else {
+                whr[j] = make_uint4(0, 0, 0, 0);
+                wlr[j] = make_uint4(0, 0, 0, 0);
+            }
+        }
+    };
+    auto store = [&]() {
+#pragma unroll
+        for (int j = 0; j < AF4; ++j) {
+            const int f = tid + 256 * j;
+            const int row = f / (BK / 4), kc = (f % (BK / 4)) * 4;
+            const float4 a = ar[j];
+            bf16x4 hi, lo;
+            hi[0] = (__bf16)a.x; hi[1] = (__bf16)a.y; hi[2] = (__bf16)a.z; hi[3] = (__bf16)a.w;
+            lo[0] = (__bf16)(a.x - (float)hi[0]);
+            lo[1] = (__bf16)(a.y - (float)hi[1]);
+            lo[2] = (__bf16)(a.z - (float)hi[2]);
+            lo[3] = (__bf16)(a.w - (float)hi[3]);
+            *reinterpret_cast<bf16x4*>(a_hi + row * PITCH + kc) = hi;
+            *reinterpret_cast<bf16x4*>(a_lo + row * PITCH + kc) = lo;
+        }
+#pragma unroll
+        for (int j = 0; j < BV; ++j) {
+            const int f = tid + 256 * j;
+            const int row = f / (BK / 8), kc = (f % (BK / 8)) * 8;
+            *reinterpret_cast<uint4*>(w_hi + row * PITCH + kc) = whr[j];
+            *reinterpret_cast<uint4*>(w_lo + row * PITCH + kc) = wlr[j];
+        }
+    };
+
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int nk = (p.K + BK - 1) / BK;
+    load(0);
+    for (int kt = 0; kt < nk; ++kt) {
+        __syncthreads();
+        store();
+        __syncthreads();
+        if (kt + 1 < nk) load((kt + 1) * BK);
+        bf16x8 ah[TM], al[TM];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const int row = wm + i * 16 + fr;
+            ah[i] = *reinterpret_cast<const bf16x8*>(a_hi + row * PITCH + fk);
+            al[i] = *reinterpret_cast<const bf16x8*>(a_lo + row * PITCH + fk);
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int col = wn + j * 16 + fr;
+            const bf16x8 bh = *reinterpret_cast<const bf16x8*>(w_hi + col * PITCH + fk);
+            const bf16x8 bl = *reinterpret_cast<const bf16x8*>(w_lo + col * PITCH + fk);
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh, acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl, acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh, acc[i][j], 0, 0, 0);
+            }
+        }
+    }
+
+    // epilogue: C layout row = 4 * (lane >> 4) + r, col = lane & 15
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn + j * 16 + fr;
+        if (n >= p.N) continue;
+        const float b = p.bias ? p.bias[n] : 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int m = m0 + wm + i * 16 + (lane >> 4) * 4 + r;
+                if (m >= p.M) continue;
+                float y = acc[i][j][r] + b;
+                if (p.R) y += p.R[(int64_t)m * p.ldr + n];
+                if (p.act == FGR_ACT_RELU) y = fmaxf(y, 0.f);
+                p.C[(int64_t)m * p.ldc + n] = y;
+            }
+        }
+    }
+}
+
+// fp32 weights -> (hi, lo) bf16 pairs, rows zero-padded to ldw (multiple of 32)
+__global__ void split_weights_kernel(const float* __restrict__ w, int n, int k, int64_t ldw,
+                                     __bf16* __restrict__ hi, __bf16* __restrict__ lo) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (int64_t)n * ldw) return;
+    const int64_t r = t / ldw;
+    const int c = (int)(t - r * ldw);
+    const float x = c < k ? w[r * k + c] : 0.f;
+    const __bf16 h = (__bf16)x;
+    hi[t] = h;
+    lo[t] = (__bf16)(x - (float)h);
+}
+
+template <int BM, int BN>
+void launch(const GemmArgs& a, hipStream_t st) {
+    const int nbm = (a.M + BM - 1) / BM, nbn = (a.N + BN - 1) / BN;
+    hipLaunchKernelGGL((gemm_bf16x3_kernel<BM, BN>), dim3((unsigned)(nbm * nbn)), dim3(256), 0, st,
+                       a);
+}
+
+}  // namespace
+}  // namespace fgr
+
+using namespace fgr;
+
+extern "C" int fgr_split_weights(const float* w, int32_t n, int32_t k, int64_t ldw, void* w_hi,
+                                 void* w_lo, void* stream) {
+    FGR_REQUIRE(w && w_hi && w_lo && n > 0 && k > 0 && ldw >= k && ldw % 32 == 0,
+                "fgr_split_weights: bad arguments");
+    const int64_t tot = (int64_t)n * ldw;
+    hipLaunchKernelGGL(split_weights_kernel, dim3((unsigned)ceil_div(tot, 256)), dim3(256), 0,
+                       as_stream(stream), w, n, k, ldw, (__bf16*)w_hi, (__bf16*)w_lo);
+    FGR_CHECK_LAUNCH("split_weights_kernel");
+    return FGR_OK;
+}
+
+extern "C" int fgr_gemm_bf16x3(const float* a, int64_t lda, const void* w_hi, const void* w_lo,
+                               int64_t ldw, float* c, int64_t ldc, const float* bias,
+                               const float* r, int64_t ldr, int32_t m, int32_t n, int32_t k,
+                               int32_t act, void* stream) {
+    FGR_REQUIRE(a && w_hi && w_lo && c && m >= 0 && n > 0 && k > 0 && k % 4 == 0 &&
+                    lda >= k && lda % 4 == 0 && ldw >= k && ldw % 32 == 0 && ldc >= n &&
+                    (!r || ldr >= n),
+                "fgr_gemm_bf16x3: bad arguments (m %d n %d k %d lda %lld ldw %lld)", m, n, k,
+                (long long)lda, (long long)ldw);
+    FGR_REQUIRE((reinterpret_cast<uintptr_t>(a) & 15) == 0, "fgr_gemm_bf16x3: A not 16-B aligned");
+    if (m == 0) return FGR_OK;
+    GemmArgs g{a, lda, (const __bf16*)w_hi, (const __bf16*)w_lo, ldw, c, ldc, bias, r, ldr,
+               m, n, k, act};
+    hipStream_t st = as_stream(stream);
+    // tile choice: big tiles when they still give >= 2 blocks per CU-ish, else 64 x 64
+    const int64_t big = (int64_t)ceil_div(m, 128) * ceil_div(n, 128);
+    if (big >= 512)
+        launch<128, 128>(g, st);
+    else if ((int64_t)ceil_div(m, 128) * ceil_div(n, 64) >= 384)
+        launch<128, 64>(g, st);
+    else
+        launch<64, 64>(g, st);
+    FGR_CHECK_LAUNCH("gemm_bf16x3_kernel");
+    return FGR_OK;
+}

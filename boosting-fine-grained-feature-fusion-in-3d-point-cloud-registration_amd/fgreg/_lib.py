@@ -36,6 +36,9 @@ SIGNATURES = {
     'fgr_attention': [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i32, _i32, _i32,
                       _i32, _f32, _vp],
     'fgr_res2net_chain': [_vp, _i64, _i32, _i32, _vp, _vp, _vp, _i32, _vp, _i64, _vp],
+    'fgr_split_weights': [_vp, _i32, _i32, _i64, _vp, _vp, _vp],
+    'fgr_gemm_bf16x3': [_vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _vp, _i64, _i32, _i32, _i32,
+                        _i32, _vp],
     'fgr_procrustes': [_vp, _vp, _vp, _i64, _i64, _f32, _vp, _vp],
     'fgr_pair_pose': [_vp, _vp, _vp, _i64, _vp, _i32, _i32, _f32, _vp, _vp],
 }

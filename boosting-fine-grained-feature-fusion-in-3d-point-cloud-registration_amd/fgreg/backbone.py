@@ -26,6 +26,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import ops
+from .linear import linear
 
 
 # ------------------------------------------------------------------------------------------
@@ -181,7 +182,7 @@ class KPConv(nn.Module):
         by the second (:395-399); callers fuse that division into the next kernel."""
         wf, nnorm = ops.kpconv_gather(q_pts, s_pts, neighb_inds, x, self.kernel_points,
                                       self.KP_extent)
-        out = torch.mm(wf.view(wf.shape[0], -1), self.weights.view(-1, self.out_channels))
+        out = linear(wf.view(wf.shape[0], -1), self.weights, transpose=True)
         return out, nnorm
 
     def forward(self, q_pts, s_pts, neighb_inds, x):
@@ -214,7 +215,7 @@ class UnaryBlock(nn.Module):
         self.batch_norm = BatchNormBlock(out_dim, use_bn, bn_momentum)
 
     def forward(self, x, off, lengths, residual=None, post_act=ops.ACT_NONE):
-        y = torch.mm(x, self.mlp.weight.t())
+        y = linear(x, self.mlp.weight)
         act = ops.ACT_NONE if self.no_relu else ops.ACT_LEAKY
         return self.batch_norm(y, off, lengths, act=act, residual=residual, post_act=post_act)
 
@@ -269,14 +270,14 @@ class my_Bottle2neck(nn.Module):  # noqa: N801 -- reference name (res2net.py:84)
         if self.training:
             return self._forward_train(x)
         w1, b1, ws, w3d, b3d, chain = self._folded_params()
-        out = torch._addmm_activation(b1, x, w1.t())
+        out = linear(x, w1, b1, act=ops.ACT_RELU)
         w = self.width
         if chain is not None and self.downsample is not None:
             # one launch for the whole hierarchy + the [.. | x] concat (fgr_res2net_chain)
             cat_in = torch.empty((x.shape[0], w * self.scale + x.shape[1]), dtype=x.dtype,
                                  device=x.device)
             ops.res2net_chain(out, w, self.scale, chain[0], chain[1], x, cat_in)
-            return torch._addmm_activation(b3d, cat_in, w3d.t())
+            return linear(cat_in, w3d, b3d, act=ops.ACT_RELU)
         cat_in = torch.empty((x.shape[0], w * self.scale + (x.shape[1] if self.downsample is not None else 0)),
                              dtype=x.dtype, device=x.device)
         sp = None

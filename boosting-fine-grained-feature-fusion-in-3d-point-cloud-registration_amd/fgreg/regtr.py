@@ -17,6 +17,7 @@ import torch
 import torch.nn as nn
 
 from . import ops
+from .linear import linear
 from .backbone import KPFEncoder, PreprocessorHIP, host_layout
 from .transformer import (PositionEmbeddingCoordsSine, Segments, TransformerCrossEncoder,
                           TransformerCrossEncoderLayer)
@@ -39,10 +40,10 @@ class CorrespondenceRegressor(nn.Module):
         L, N, d = feats.shape
         f = feats.reshape(L * N, d)
         m = self.coor_mlp
-        h = torch._addmm_activation(m[0].bias, f, m[0].weight.t())
-        h = torch._addmm_activation(m[2].bias, h, m[2].weight.t())
-        corr = torch.addmm(m[4].bias, h, m[4].weight.t())
-        logits = torch.addmm(self.conf_logits_decoder.bias, f, self.conf_logits_decoder.weight.t())
+        h = linear(f, m[0].weight, m[0].bias, act=ops.ACT_RELU)
+        h = linear(h, m[2].weight, m[2].bias, act=ops.ACT_RELU)
+        corr = linear(h, m[4].weight, m[4].bias)
+        logits = linear(f, self.conf_logits_decoder.weight, self.conf_logits_decoder.bias)
         return corr.view(L, N, 3), logits.view(L, N, 1)
 
 
@@ -141,7 +142,7 @@ class RegTR(nn.Module):
         feats0 = torch.ones((pts0.shape[0], 1), dtype=torch.float32, device=pts0.device)
 
         feats_un, _ = self.kpf_encoder(feats0, meta)
-        both = torch.addmm(self.feat_proj.bias, feats_un, self.feat_proj.weight.t())
+        both = linear(feats_un, self.feat_proj.weight, self.feat_proj.bias)
         xyz_c = meta['points'][-1]
         pe = self.pos_embed(xyz_c)
         seg = Segments(slens_c, xyz_c.device)

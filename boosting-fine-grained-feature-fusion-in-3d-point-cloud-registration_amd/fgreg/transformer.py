@@ -25,6 +25,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import ops
+from .linear import linear
 
 
 class Segments:
@@ -71,7 +72,7 @@ class TransformerCrossEncoderLayer(nn.Module):
         d = h_pos.shape[1]
         W, b = mha.in_proj_weight, mha.in_proj_bias
         if val_has_pos:
-            qkv = torch.addmm(b, h_pos, W.t())                        # (N, 3d): [q | k | v]
+            qkv = linear(h_pos, W, b)                                 # (N, 3d): [q | k | v]
             q, k, v = qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:]
         else:
             qk = torch.addmm(b[:2 * d], h_pos, W[:2 * d].t())
@@ -92,19 +93,19 @@ class TransformerCrossEncoderLayer(nn.Module):
         h0 = None if self.sa_val_has_pos_emb else ops.layernorm(x, self.norm1.weight,
                                                                  self.norm1.bias, self.norm1.eps)
         o = self._attend(self.self_attn, h, h0, self.sa_val_has_pos_emb, seg, seg.self_seg)
-        x = torch.addmm(x, o, self.self_attn.out_proj.weight.t())
+        x = linear(o, self.self_attn.out_proj.weight, residual=x)
         # cross-attention, both directions at once (:212-229)
         h = ops.layernorm(x, self.norm2.weight, self.norm2.bias, self.norm2.eps, add=pos,
                           pre_bias=self.self_attn.out_proj.bias)
         h0 = None if self.ca_val_has_pos_emb else ops.layernorm(x, self.norm2.weight,
                                                                  self.norm2.bias, self.norm2.eps)
         o = self._attend(self.multihead_attn, h, h0, self.ca_val_has_pos_emb, seg, seg.cross_seg)
-        x = torch.addmm(x, o, self.multihead_attn.out_proj.weight.t())
+        x = linear(o, self.multihead_attn.out_proj.weight, residual=x)
         # position-wise feed-forward (:231-238)
         h = ops.layernorm(x, self.norm3.weight, self.norm3.bias, self.norm3.eps,
                           pre_bias=self.multihead_attn.out_proj.bias)
-        h = torch._addmm_activation(self.linear1.bias, h, self.linear1.weight.t())
-        return torch.addmm(x, h, self.linear2.weight.t()), self.linear2.bias
+        h = linear(h, self.linear1.weight, self.linear1.bias, act=ops.ACT_RELU)
+        return linear(h, self.linear2.weight, residual=x), self.linear2.bias
 
 
 class TransformerCrossEncoder(nn.Module):

@@ -136,6 +136,19 @@ int fgr_res2net_chain(const float* h, int64_t n, int32_t w, int32_t scale, const
                       const float* bias, const float* x, int32_t cin, float* cat, int64_t ld_cat,
                       void* stream);
 
+/* ---- dense layers ----------------------------------------------------------------------
+ * Split-precision GEMM for every Linear / KPConv-weight product of the forward:
+ *   C[m, n] = act(A[m, :] . W[n, :] + bias[n] (+ R[m, n]))
+ * A fp32 (row stride lda, 16-B aligned, k % 4 == 0); W given as bf16 (hi, lo) pairs of shape
+ * (n, ldw), ldw % 32 == 0, zero-padded beyond k (fgr_split_weights). Products accumulate in
+ * fp32 as A_lo W_hi + A_hi W_lo + A_hi W_hi on v_mfma_f32_16x16x32_bf16: ~2^-16 relative
+ * per product, at the bf16 matrix rate (gfx950 has no xf32). act: FGR_ACT_NONE / _RELU. */
+int fgr_split_weights(const float* w, int32_t n, int32_t k, int64_t ldw, void* w_hi, void* w_lo,
+                      void* stream);
+int fgr_gemm_bf16x3(const float* a, int64_t lda, const void* w_hi, const void* w_lo, int64_t ldw,
+                    float* c, int64_t ldc, const float* bias, const float* r, int64_t ldr,
+                    int32_t m, int32_t n, int32_t k, int32_t act, void* stream);
+
 /* ---- attention ---------------------------------------------------------------------
  * Multi-head scaled-dot-product attention core of nn.MultiheadAttention
  * (transformers.py:95-96, 197-226) on packed, unpadded segments: query segment

@@ -217,3 +217,25 @@ def test_res2net_block_vs_oracle(gpu, cin, cout):
     with torch.no_grad():
         out = m(x.to(gpu))
     assert rel_err(out, ref) < TOL
+
+
+@pytest.mark.parametrize('m,n,k', [(11472, 128, 1920), (9200, 1024, 2048), (1000, 3, 256),
+                                   (333, 896, 128), (64, 256, 36), (5000, 768, 256)])
+def test_gemm_bf16x3_vs_fp64(gpu, m, n, k):
+    """Split-precision GEMM (A_lo W_hi + A_hi W_lo + A_hi W_hi on bf16 MFMA) vs fp64: the
+    error must be at fp32 level (normwise <= 1e-5), bias / ReLU / residual epilogues."""
+    from fgreg import linear as fl
+    from fgreg import ops
+    g = torch.Generator().manual_seed(m + n + k)
+    x = torch.randn(m, k, generator=g)
+    w = torch.randn(n, k, generator=g) / math.sqrt(k)
+    b = torch.randn(n, generator=g)
+    r = torch.randn(m, n, generator=g)
+    ref = x.double() @ w.double().t() + b.double()
+    X, W, Bb, R = x.to(gpu), w.to(gpu), b.to(gpu), r.to(gpu)
+    assert rel_err(fl.linear(X, W, Bb), ref) < 1e-5
+    assert rel_err(fl.linear(X, W, Bb, act=ops.ACT_RELU), ref.clamp_min(0)) < 1e-5
+    assert rel_err(fl.linear(X, W, residual=R), ref - b.double() + r.double()) < 1e-5
+    # transposed (KPConv weight layout (K, Cin, Cout) used as (K*Cin, Cout))
+    wt = w.t().contiguous().view(k, n)
+    assert rel_err(fl.linear(X, wt.to(gpu), Bb, transpose=True), ref) < 1e-5
