@@ -35,6 +35,9 @@ SIGNATURES = {
     'fgr_sine_pos_embed': [_vp, _i64, _i32, _f32, _f32, _vp, _vp],
     'fgr_attention': [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i32, _i32, _i32,
                       _i32, _f32, _vp],
+    'fgr_attention_bf16x6_workspace': [_i64, _i32, _i32, ctypes.POINTER(_sz)],
+    'fgr_attention_bf16x6': [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i32, _i32,
+                             _i64, _i32, _i32, _i32, _i32, _f32, _vp, _i64, _vp],
     'fgr_res2net_chain': [_vp, _i64, _i32, _i32, _vp, _vp, _vp, _i32, _vp, _i64, _vp],
     'fgr_split_weights': [_vp, _i32, _i32, _i64, _vp, _vp, _vp],
     'fgr_gemm_bf16x3': [_vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _vp, _i64, _i32, _i32, _i32,

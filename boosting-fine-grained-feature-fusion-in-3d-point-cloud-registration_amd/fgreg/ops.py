@@ -7,6 +7,7 @@ There is deliberately no CPU path: on a tensor that is not on a GPU, or without
 libfgreg.so, these raise.
 """
 import math
+import os
 from typing import Sequence, Tuple
 
 import torch
@@ -308,30 +309,67 @@ def res2net_chain(h, w, scale, w_frag, bias, x, cat):
 # ------------------------------------------------------------------------------------------
 # attention
 # ------------------------------------------------------------------------------------------
-def attention(q, k, v, q_off, kv_off, kv_seg, max_q_len, n_head, out=None) -> torch.Tensor:
+# fgr_attention_bf16x6 (fp32-accurate split-bf16 MFMA) for head_dim 32, fgr_attention (fp32
+# MFMA) otherwise; FGREG_ATTN=fp32 forces the latter (a precision A/B switch, both on the GPU).
+ATTN_MODE = os.environ.get('FGREG_ATTN', 'bf16x6')
+
+
+def attention(q, k, v, q_off, kv_off, kv_seg, max_q_len, n_head, out=None,
+              max_kv_len=None) -> torch.Tensor:
     """Packed-segment MHA core: rows of query segment i attend to key segment kv_seg[i].
 
     q, k, v: (rows, n_head * dh) views with unit column stride (may be column slices of
-    one fused QKV tensor). Returns o (Nq, n_head * dh).
+    one fused QKV tensor). Returns o (Nq, n_head * dh). ``max_kv_len`` defaults to
+    ``max_q_len`` (self / cross attention over one segmentation).
     """
     _dev(q, k, v, q_off, kv_off, kv_seg)
     for t in (q, k, v):
         assert t.dtype == torch.float32 and t.dim() == 2 and t.stride(1) == 1
     d = q.shape[1]
-    assert k.shape[1] == d and v.shape[1] == d and d % n_head == 0
+    assert k.shape[1] == d and v.shape[1] == d and d % n_head == 0 and k.shape[0] == v.shape[0]
     dh = d // n_head
     if out is None:
         out = torch.empty((q.shape[0], d), dtype=torch.float32, device=q.device)
     n_seg = q_off.numel() - 1
+    n_kv_seg = kv_off.numel() - 1
     assert kv_seg.dtype == torch.int32 and kv_seg.numel() == n_seg
+    max_kv_len = max_q_len if max_kv_len is None else max_kv_len
+    L = _lib.load()
+    split = (ATTN_MODE == 'bf16x6' and dh == 32
+             and all(t.stride(0) % 4 == 0 and t.data_ptr() % 16 == 0 for t in (q, k, v, out)))
     t0 = _begin('attention')
-    _lib.check(_lib.load().fgr_attention(_ptr(q), q.stride(0), _ptr(k), k.stride(0), _ptr(v),
-                                         v.stride(0), _ptr(out), out.stride(0), _ptr(q_off),
-                                         _ptr(kv_off), _ptr(kv_seg), n_seg, int(max_q_len), n_head,
-                                         dh, float(math.sqrt(1.0 / float(dh))), _stream()),
-               'fgr_attention')
+    if split:
+        nb = _lib._sz(0)
+        _lib.check(L.fgr_attention_bf16x6_workspace(k.shape[0], n_kv_seg, n_head, nb),
+                   'fgr_attention_bf16x6_workspace')
+        ws = _workspace(q.device, nb.value)
+        _lib.check(L.fgr_attention_bf16x6(
+            _ptr(q), q.stride(0), _ptr(k), k.stride(0), _ptr(v), v.stride(0), _ptr(out),
+            out.stride(0), _ptr(q_off), _ptr(kv_off), _ptr(kv_seg), n_seg, n_kv_seg, k.shape[0],
+            int(max_q_len), int(max_kv_len), n_head, dh, float(math.sqrt(1.0 / float(dh))),
+            _ptr(ws), ws.numel(), _stream()), 'fgr_attention_bf16x6')
+    else:
+        _lib.check(L.fgr_attention(_ptr(q), q.stride(0), _ptr(k), k.stride(0), _ptr(v),
+                                   v.stride(0), _ptr(out), out.stride(0), _ptr(q_off),
+                                   _ptr(kv_off), _ptr(kv_seg), n_seg, int(max_q_len), n_head,
+                                   dh, float(math.sqrt(1.0 / float(dh))), _stream()),
+                   'fgr_attention')
     _end('attention', t0, lambda: attention_flops(q_off, kv_off, kv_seg, d))
     return out
+
+
+_WS = {}
+
+
+def _workspace(device, nbytes):
+    """Grow-only scratch buffer per device, reused by consecutive launches on the current
+    stream (stream order serialises the reuse)."""
+    key = (device, torch.cuda.current_stream(device).cuda_stream)
+    buf = _WS.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
+        _WS[key] = buf
+    return buf
 
 
 def attention_flops(q_off, kv_off, kv_seg, d):

@@ -161,6 +161,22 @@ int fgr_attention(const float* q, int64_t ld_q, const float* k, int64_t ld_k, co
                   const int64_t* kv_off, const int32_t* kv_seg, int32_t n_seg,
                   int32_t max_q_len, int32_t n_head, int32_t head_dim, float scale, void* stream);
 
+/* fp32-accurate attention on the bf16 matrix cores (head_dim 32, the reference configs'
+ * d_embed 256 / nhead 8): same semantics and arguments as fgr_attention, plus the key
+ * segment count / row count / longest key segment, and a caller workspace of
+ * fgr_attention_bf16x6_workspace() bytes holding the split K/V images. Every operand is
+ * split exactly into three bf16 terms and each product accumulates the six significant
+ * term products in fp32 (residual ~2^-27 relative, below fp32's own 2^-24 rounding).
+ * q/k/v/o 16-B aligned, row strides multiples of 4. */
+int fgr_attention_bf16x6_workspace(int64_t n_kv_rows, int32_t n_kv_seg, int32_t n_head,
+                                   size_t* bytes);
+int fgr_attention_bf16x6(const float* q, int64_t ld_q, const float* k, int64_t ld_k,
+                         const float* v, int64_t ld_v, float* o, int64_t ld_o,
+                         const int64_t* q_off, const int64_t* kv_off, const int32_t* kv_seg,
+                         int32_t n_seg, int32_t n_kv_seg, int64_t n_kv_rows, int32_t max_q_len,
+                         int32_t max_kv_len, int32_t n_head, int32_t head_dim, float scale,
+                         void* workspace, int64_t ws_bytes, void* stream);
+
 /* ---- pose ----------------------------------------------------------------------------
  * fast_compute_rigid_transform (utils/se3_torch.py:226-273; threshold < 0 gives the
  * unthresholded compute_rigid_transform, :131-173) on n_batch independent problems

@@ -1,0 +1,100 @@
+"""Per-op micro-benchmark on the GPU (development tool): times the attention core in both
+precision modes at the bench workload's shapes (16 clouds x ~600 superpoints, d 256,
+8 heads) with HIP events, and prints fp32-equivalent TFLOP/s."""
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, 'boosting-fine-grained-feature-fusion-in-3d-point-cloud-registration_amd')
+import fgreg.ops as ops  # noqa: E402
+
+
+def timeit(fn, iters=50):
+    for _ in range(5):
+        fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(iters):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / iters * 1e3  # us
+
+
+def attention(lens=(600,) * 16, d=256, nh=8):
+    dev = torch.device('cuda:0')
+    n = sum(lens)
+    qkv = torch.randn(n, 3 * d, device=dev)
+    off = ops.offsets(list(lens), dev)
+    B = len(lens) // 2
+    cross = torch.tensor([(c + B) % len(lens) for c in range(len(lens))], dtype=torch.int32, device=dev)
+    flops = sum(4 * l * lens[(i + B) % len(lens)] * d for i, l in enumerate(lens))
+    for mode in ('fp32', 'bf16x6'):
+        ops.ATTN_MODE = mode
+        us = timeit(lambda: ops.attention(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], off, off,
+                                          cross, max(lens), nh))
+        print(f'attention {mode:7s} lens={lens[0]}x{len(lens)} d={d}: {us:8.1f} us  '
+              f'{flops / us / 1e6:7.1f} TFLOP/s fp32-equivalent', flush=True)
+
+
+def gemm_shapes():
+    """Records every linear() call of one bench forward (B = 8 ModelNet pairs) and times each
+    shape in both GEMM modes."""
+    import collections
+    import numpy as np
+    import fgreg
+    import fgreg.linear as lin
+    from fgreg.synthetic import make_batch
+    dev = torch.device('cuda:0')
+    cfg = fgreg.config.get('modelnet')
+    torch.manual_seed(0)
+    model = fgreg.RegTR(cfg).to(dev).eval()
+    src, tgt, _ = make_batch('modelnet', 8)
+    batch = {'src_xyz': [torch.from_numpy(a).to(dev) for a in src],
+             'tgt_xyz': [torch.from_numpy(a).to(dev) for a in tgt]}
+    calls = []
+    orig = lin.linear
+
+    def rec(x, w, bias=None, act=0, residual=None, transpose=False, tag=None, out=None):
+        n = w.shape[-1] if transpose else w.shape[0]
+        calls.append((x.shape[0], n, x.shape[1], transpose, residual is not None))
+        return orig(x, w, bias, act, residual, transpose, tag, out)
+    import fgreg.backbone as bb, fgreg.transformer as tr, fgreg.regtr as rr
+    for m in (lin, bb, tr, rr):
+        if hasattr(m, 'linear'):
+            m.linear = rec
+    with torch.no_grad():
+        model(batch)
+    for m in (lin, bb, tr, rr):
+        if hasattr(m, 'linear'):
+            m.linear = orig
+    shapes = collections.Counter(calls)
+    tot = {'fp32': 0.0, 'bf16x3': 0.0}
+    flops = 0
+    for (M, N, K, tp, res), cnt in sorted(shapes.items(), key=lambda kv: -kv[0][0] * kv[0][1] * kv[0][2] * kv[1]):
+        x = torch.randn(M, K, device=dev)
+        w = torch.randn(K, N, device=dev) if tp else torch.randn(N, K, device=dev)
+        r = torch.randn(M, N, device=dev) if res else None
+        line = f'M={M:6d} N={N:5d} K={K:5d} x{cnt:2d} '
+        for mode in ('fp32', 'bf16x3'):
+            lin.set_mode(mode)
+            us = timeit(lambda: orig(x, w, None, 0, r, tp), iters=20)
+            tot[mode] += us * cnt
+            line += f' {mode} {us:7.1f} us ({2 * M * N * K / us / 1e6:6.1f} TF)'
+        flops += 2 * M * N * K * cnt
+        print(line, flush=True)
+    lin.set_mode('fp32')
+    print(f'total per forward: {flops / 1e9:.1f} GFLOP; ' +
+          ', '.join(f'{k} {v / 1e3:.3f} ms' for k, v in tot.items()), flush=True)
+
+
+if __name__ == '__main__':
+    import os
+    which = sys.argv[1:] or ['attention']
+    if 'attention' in which:
+        attention()
+        attention(lens=(2000,) * 2)
+    if 'gemm' in which:
+        gemm_shapes()
