@@ -181,6 +181,208 @@ void launch(const GemmArgs& a, hipStream_t st) {
                        a);
 }
 
+
+// ------------------------------------------------------------------------------------
+// bf16x6: fp32-accurate GEMM on the bf16 matrix cores.
+//   x = h + m + l exactly-split bf16 terms (residual <= 2^-27 |x|); per 16x16x32 step the
+//   six significant term products hh, hm, mh, hl, lh, mm accumulate in fp32 (dropped
+//   ml, lm, ll ~ 2^-27 relative) -- fp32-level accuracy at 6 x 16 = 96 cycles per step
+//   vs 8 x 32 = 256 on the fp32 MFMA.
+// W (static) is pre-split by fgr_split_weights3 into an image laid out as the kernel's
+// LDS tile: [n16 panel][k32 step][term 3][g 4][16 rows] x 16-B units (8 k each), so
+// staging W is a flat copy. A (fp32 activations) is split in registers while staging:
+// A LDS image [term 3][g 4][BM rows] units, row XOR (2g) so both the 16-B stores
+// (8-lane groups: 2 rows x 4 g) and the ds_read_b128 fragment loads are conflict-free.
+// 16x16x32 lane maps (lane l, g = l >> 4, c = l & 15): A[i = c][k = 8g + e],
+// B[k = 8g + e][j = c], C[i = 4g + r][j = c].
+// ------------------------------------------------------------------------------------
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void split3(float x, __bf16& h, __bf16& m, __bf16& l) {
+    h = (__bf16)x;
+    const float r = x - (float)h;
+    m = (__bf16)r;
+    l = (__bf16)(r - (float)m);
+}
+
+struct Gemm6Args {
+    const float* A; int64_t lda;
+    const u32x4* W; int ksteps;           // image, ksteps = ceil(K / 32)
+    float* C; int64_t ldc;
+    const float* bias;
+    const float* R; int64_t ldr;
+    int M, N, K, act;
+};
+
+template <int BM, int BN>
+__global__ void __launch_bounds__(256) gemm_bf16x6_kernel(Gemm6Args p) {
+    constexpr int TM = BM / 32, TN = BN / 32;         // 16x16 subtiles per wave (2 x 2 waves)
+    constexpr int UA = BM * 4 / 256;                   // A units (8 k of one row) per thread
+    constexpr int UW = 12 * BN / 256;                  // W image units per thread
+    static_assert(UA >= 1 && UW >= 1 && BM % 16 == 0 && BN % 16 == 0, "tile");
+    __shared__ u32x4 a_lds[3 * 4 * BM];
+    __shared__ u32x4 w_lds[12 * BN];
+
+    const int nbm = (p.M + BM - 1) / BM;
+    const int bm = blockIdx.x % nbm, bn = blockIdx.x / nbm;
+    const int m0 = bm * BM, n0 = bn * BN;
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+    const int wm = (wv >> 1) * (BM / 2), wn = (wv & 1) * (BN / 2);
+    const int g = lane >> 4, c = lane & 15;
+    const int npanel = (p.N + 15) / 16;
+
+    float4 ar[UA][2];
+    u32x4 wr[UW];
+    int64_t woff[UW];                                   // image unit of step 0
+    bool wok[UW];
+#pragma unroll
+    for (int j = 0; j < UW; ++j) {
+        const int v = tid + 256 * j;
+        const int pp = v / 192, rem = v % 192;
+        const int panel = n0 / 16 + pp;
+        wok[j] = panel < npanel;
+        woff[j] = (int64_t)panel * p.ksteps * 192 + rem;
+    }
+    const bool kvec8 = (p.K & 7) == 0;
+    auto load = [&](int s) {
+        const int k0 = s * 32;
+#pragma unroll
+        for (int j = 0; j < UA; ++j) {
+            const int u = tid + 256 * j;
+            const int row = u >> 2, gg = u & 3;
+            const int m = m0 + row, k = k0 + 8 * gg;
+            const float* src = p.A + (int64_t)m * p.lda + k;
+            if (m < p.M && k + 8 <= p.K && kvec8) {
+                ar[j][0] = *reinterpret_cast<const float4*>(src);
+                ar[j][1] = *reinterpret_cast<const float4*>(src + 4);
+            } else {
+                float t[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) t[e] = (m < p.M && k + e < p.K) ? src[e] : 0.f;
+                ar[j][0] = make_float4(t[0], t[1], t[2], t[3]);
+                ar[j][1] = make_float4(t[4], t[5], t[6], t[7]);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < UW; ++j)
+            wr[j] = wok[j] ? p.W[woff[j] + (int64_t)s * 192] : u32x4{0u, 0u, 0u, 0u};
+    };
+    auto store = [&]() {
+#pragma unroll
+        for (int j = 0; j < UA; ++j) {
+            const int u = tid + 256 * j;
+            const int row = u >> 2, gg = u & 3;
+            const float x[8] = {ar[j][0].x, ar[j][0].y, ar[j][0].z, ar[j][0].w,
+                                ar[j][1].x, ar[j][1].y, ar[j][1].z, ar[j][1].w};
+            bf16x8 th, tm, tl;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                __bf16 h, m, l;
+                split3(x[e], h, m, l);
+                th[e] = h; tm[e] = m; tl[e] = l;
+            }
+            const int r = row ^ (2 * gg);
+            a_lds[(0 * 4 + gg) * BM + r] = __builtin_bit_cast(u32x4, th);
+            a_lds[(1 * 4 + gg) * BM + r] = __builtin_bit_cast(u32x4, tm);
+            a_lds[(2 * 4 + gg) * BM + r] = __builtin_bit_cast(u32x4, tl);
+        }
+#pragma unroll
+        for (int j = 0; j < UW; ++j) w_lds[tid + 256 * j] = wr[j];
+    };
+
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int nk = (p.K + 31) / 32;
+    load(0);
+    for (int s = 0; s < nk; ++s) {
+        __syncthreads();
+        store();
+        __syncthreads();
+        if (s + 1 < nk) load(s + 1);
+        bf16x8 bw[TN][3];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int pp = (wn + 16 * j) >> 4;
+#pragma unroll
+            for (int t = 0; t < 3; ++t)
+                bw[j][t] = __builtin_bit_cast(bf16x8, w_lds[pp * 192 + (t * 4 + g) * 16 + c]);
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const int r = (wm + 16 * i + c) ^ (2 * g);
+            const bf16x8 ah = __builtin_bit_cast(bf16x8, a_lds[(0 * 4 + g) * BM + r]);
+            const bf16x8 am = __builtin_bit_cast(bf16x8, a_lds[(1 * 4 + g) * BM + r]);
+            const bf16x8 al = __builtin_bit_cast(bf16x8, a_lds[(2 * 4 + g) * BM + r]);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                f32x4 a = acc[i][j];
+                a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bw[j][1], a, 0, 0, 0);
+                a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bw[j][0], a, 0, 0, 0);
+                a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bw[j][2], a, 0, 0, 0);
+                a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bw[j][0], a, 0, 0, 0);
+                a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bw[j][1], a, 0, 0, 0);
+                a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bw[j][0], a, 0, 0, 0);
+                acc[i][j] = a;
+            }
+        }
+    }
+
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn + j * 16 + c;
+        if (n >= p.N) continue;
+        const float b = p.bias ? p.bias[n] : 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int m = m0 + wm + i * 16 + 4 * g + r;
+                if (m >= p.M) continue;
+                float y = acc[i][j][r] + b;
+                if (p.R) y += p.R[(int64_t)m * p.ldr + n];
+                if (p.act == FGR_ACT_RELU) y = fmaxf(y, 0.f);
+                p.C[(int64_t)m * p.ldc + n] = y;
+            }
+        }
+    }
+}
+
+// W (n x k, element (i, j) at w[i * sn + j * sk]) -> bf16x6 image (see above)
+__global__ void split_weights3_kernel(const float* __restrict__ w, int n, int k, int64_t sn,
+                                      int64_t sk, int ksteps, u32x4* __restrict__ img) {
+    const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // image unit
+    const int64_t total = (int64_t)((n + 15) / 16) * ksteps * 192;
+    if (u >= total) return;
+    const int i = (int)(u % 16);
+    const int g = (int)((u / 16) % 4);
+    const int t = (int)((u / 64) % 3);
+    const int64_t ps = u / 192;
+    const int s = (int)(ps % ksteps);
+    const int panel = (int)(ps / ksteps);
+    const int row = panel * 16 + i;
+    bf16x8 out;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const int col = s * 32 + 8 * g + e;
+        const float x = (row < n && col < k) ? w[row * sn + col * sk] : 0.f;
+        __bf16 h, m, l;
+        split3(x, h, m, l);
+        out[e] = t == 0 ? h : (t == 1 ? m : l);
+    }
+    img[u] = __builtin_bit_cast(u32x4, out);
+}
+
+template <int BM, int BN>
+void launch6(const Gemm6Args& a, hipStream_t st) {
+    const int nbm = (a.M + BM - 1) / BM, nbn = (a.N + BN - 1) / BN;
+    hipLaunchKernelGGL((gemm_bf16x6_kernel<BM, BN>), dim3((unsigned)(nbm * nbn)), dim3(256), 0, st,
+                       a);
+}
+
 }  // namespace
 }  // namespace fgr
 
@@ -220,5 +422,46 @@ extern "C" int fgr_gemm_bf16x3(const float* a, int64_t lda, const void* w_hi, co
     else
         launch<64, 64>(g, st);
     FGR_CHECK_LAUNCH("gemm_bf16x3_kernel");
+    return FGR_OK;
+}
+
+extern "C" int fgr_split_weights3_bytes(int32_t n, int32_t k, size_t* bytes) {
+    FGR_REQUIRE(bytes && n > 0 && k > 0, "fgr_split_weights3_bytes: bad arguments");
+    *bytes = (size_t)((n + 15) / 16) * ((k + 31) / 32) * 192 * 16;
+    return FGR_OK;
+}
+
+extern "C" int fgr_split_weights3(const float* w, int32_t n, int32_t k, int64_t stride_n,
+                                  int64_t stride_k, void* img, void* stream) {
+    FGR_REQUIRE(w && img && n > 0 && k > 0, "fgr_split_weights3: bad arguments");
+    const int ksteps = (k + 31) / 32;
+    const int64_t total = (int64_t)((n + 15) / 16) * ksteps * 192;
+    hipLaunchKernelGGL(split_weights3_kernel, dim3((unsigned)ceil_div(total, 256)), dim3(256), 0,
+                       as_stream(stream), w, n, k, stride_n, stride_k, ksteps, (u32x4*)img);
+    FGR_CHECK_LAUNCH("split_weights3_kernel");
+    return FGR_OK;
+}
+
+extern "C" int fgr_gemm_bf16x6(const float* a, int64_t lda, const void* w_img, float* c,
+                               int64_t ldc, const float* bias, const float* r, int64_t ldr,
+                               int32_t m, int32_t n, int32_t k, int32_t act, void* stream) {
+    FGR_REQUIRE(a && w_img && c && m >= 0 && n > 0 && k > 0 && lda >= k && ldc >= n &&
+                    (!r || ldr >= n),
+                "fgr_gemm_bf16x6: bad arguments (m %d n %d k %d lda %lld)", m, n, k,
+                (long long)lda);
+    const bool vec = (k % 8 == 0) && (lda % 4 == 0) && ((reinterpret_cast<uintptr_t>(a) & 15) == 0);
+    FGR_REQUIRE(vec || (k % 8 != 0), "fgr_gemm_bf16x6: A must be 16-B aligned with lda %% 4 == 0");
+    if (m == 0) return FGR_OK;
+    Gemm6Args g{a, lda, (const u32x4*)w_img, (k + 31) / 32, c, ldc, bias, r, ldr, m, n, k, act};
+    hipStream_t st = as_stream(stream);
+    const int64_t b128 = ceil_div(m, 128) * ceil_div(n, 128);
+    const int64_t b12864 = ceil_div(m, 128) * ceil_div(n, 64);
+    if (b128 >= 400)
+        launch6<128, 128>(g, st);
+    else if (b12864 >= 400)
+        launch6<128, 64>(g, st);
+    else
+        launch6<64, 64>(g, st);
+    FGR_CHECK_LAUNCH("gemm_bf16x6_kernel");
     return FGR_OK;
 }

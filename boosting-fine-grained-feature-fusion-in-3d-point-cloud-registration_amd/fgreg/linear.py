@@ -1,16 +1,14 @@
-"""Dense layers of the forward on the split-precision bf16x3 GEMM (fgr_gemm_bf16x3).
+"""Dense layers of the forward (every Linear / KPConv-weight product goes through
+``linear()``) on the GPU, in one of three precision modes (``FGREG_GEMM`` or ``set_mode``):
 
-Every Linear / KPConv-weight product goes through ``linear()``. Two precision modes,
-both on the GPU (selected by ``FGREG_GEMM`` or ``set_mode``):
-
-* ``fp32`` (default): PyTorch's fp32 GEMM (hipBLASLt, fp32 MFMA). Meets the 1e-4 parity
-  bar on every fixture.
-* ``bf16x3``: fgr_gemm_bf16x3, the split-precision bf16 MFMA GEMM (~2^-17 relative per
-  product; 1.2x faster end to end today). It passes every parity test except the pose of
-  the 3DMatch fixture (1.3e-4 vs 1e-4), so it is opt-in.
-Weights are split into bf16 (hi, lo) pairs once and cached against the fp32 tensor's
-identity, data pointer and version (a checkpoint load, .to() or in-place update
-invalidates the cache).
+* ``bf16x6`` (default): fgr_gemm_bf16x6, the fp32-accurate split-bf16 MFMA GEMM (operands
+  split exactly into three bf16 terms, six term products per step: ~2^-27 relative
+  residual, below fp32's own rounding). Meets the 1e-4 parity bar on every fixture.
+* ``fp32``: PyTorch's fp32 GEMM (hipBLASLt, fp32 MFMA) -- the A/B baseline.
+* ``bf16x3``: fgr_gemm_bf16x3, two-term split (~2^-17 relative per product); faster, but
+  the 3DMatch fixture's pose misses the 1e-4 bar (1.3e-4), so it is opt-in only.
+Split weights are built once and cached against the fp32 tensor's identity, data pointer
+and version (a checkpoint load, .to() or in-place update invalidates the cache).
 """
 import os
 
@@ -19,12 +17,12 @@ import torch
 from . import _lib
 from .ops import ACT_NONE, ACT_RELU, _dev, _ptr, _stream
 
-MODE = os.environ.get('FGREG_GEMM', 'fp32')
+MODE = os.environ.get('FGREG_GEMM', 'bf16x6')
 
 
 def set_mode(mode):
     global MODE
-    assert mode in ('fp32', 'bf16x3')
+    assert mode in ('fp32', 'bf16x3', 'bf16x6')
     MODE = mode
 
 
@@ -44,15 +42,48 @@ class SplitWeight:
         self.src, self.version, self.ptr = src, src._version, src.data_ptr()
 
 
+class SplitWeight3:
+    """bf16x6 image of W (n, k) (fgr_split_weights3); element (i, j) at w[i * sn + j * sk]."""
+    __slots__ = ('img', 'n', 'k', 'src', 'version', 'ptr')
+
+    def __init__(self, w2: torch.Tensor, n, k, sn, sk, src: torch.Tensor):
+        L = _lib.load()
+        nb = _lib._sz(0)
+        _lib.check(L.fgr_split_weights3_bytes(n, k, nb), 'fgr_split_weights3_bytes')
+        self.img = torch.empty(nb.value, dtype=torch.uint8, device=w2.device)
+        _lib.check(L.fgr_split_weights3(_ptr(w2), n, k, sn, sk, _ptr(self.img), _stream()),
+                   'fgr_split_weights3')
+        self.n, self.k = n, k
+        self.src, self.version, self.ptr = src, src._version, src.data_ptr()
+
+
 _CACHE = {}
+
+
+def _valid(ent, w):
+    return (ent is not None and ent.src is w and ent.version == w._version
+            and ent.ptr == w.data_ptr())            # .to() / load_state_dict swap .data
+
+
+def split_weight3(w: torch.Tensor, transpose=False, tag=None) -> SplitWeight3:
+    ck = (id(w), transpose, tag, 3)
+    ent = _CACHE.get(ck)
+    if not _valid(ent, w):
+        if transpose:                    # (K, Cin, Cout) as W[n = cout][k = K*Cin + cin]
+            w2 = w.reshape(-1, w.shape[-1]).contiguous()
+            ent = SplitWeight3(w2, w2.shape[1], w2.shape[0], 1, w2.shape[1], w)
+        else:
+            w2 = w.contiguous()
+            ent = SplitWeight3(w2, w2.shape[0], w2.shape[1], w2.shape[1], 1, w)
+        _CACHE[ck] = ent
+    return ent
 
 
 def split_weight(w: torch.Tensor, transpose=False, tag=None) -> SplitWeight:
     """Cached bf16 split of w (or of w.t() when transpose=True, e.g. KPConv (K*Cin, Cout))."""
     ck = (id(w), transpose, tag)
     ent = _CACHE.get(ck)
-    if (ent is None or ent.src is not w or ent.version != w._version
-            or ent.ptr != w.data_ptr()):           # .to() / load_state_dict swap .data
+    if not _valid(ent, w):
         ent = SplitWeight(w.reshape(-1, w.shape[-1]).t() if transpose else w, w)
         _CACHE[ck] = ent
     return ent
@@ -67,7 +98,20 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act=ACT_NONE, residual=N
     assert x.dim() == 2 and x.shape[1] == k and x.dtype == torch.float32
     if not x.is_cuda:
         _dev(x)
-    ok = (MODE == 'bf16x3' and x.is_cuda and k % 4 == 0 and x.stride(1) == 1
+    if residual is not None:
+        assert residual.shape == (x.shape[0], n) and residual.stride(1) == 1
+    if MODE == 'bf16x6' and x.stride(1) == 1 and (k % 8 != 0 or (x.stride(0) % 4 == 0
+                                                             and x.data_ptr() % 16 == 0)):
+        sw = split_weight3(w, transpose, tag)
+        m = x.shape[0]
+        if out is None:
+            out = torch.empty((m, n), dtype=torch.float32, device=x.device)
+        _lib.check(_lib.load().fgr_gemm_bf16x6(
+            _ptr(x), x.stride(0), _ptr(sw.img), _ptr(out), out.stride(0), _ptr(bias),
+            _ptr(residual), residual.stride(0) if residual is not None else 0, m, n, k, act,
+            _stream()), 'fgr_gemm_bf16x6')
+        return out
+    ok = (MODE == 'bf16x3' and k % 4 == 0 and x.stride(1) == 1
           and x.stride(0) % 4 == 0 and x.data_ptr() % 16 == 0)
     if not ok:
         W = w.reshape(k, n) if transpose else w.t()
@@ -85,8 +129,6 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act=ACT_NONE, residual=N
     m = x.shape[0]
     if out is None:
         out = torch.empty((m, n), dtype=torch.float32, device=x.device)
-    if residual is not None:
-        assert residual.shape == (m, n) and residual.stride(1) == 1
     _lib.check(_lib.load().fgr_gemm_bf16x3(_ptr(x), x.stride(0), _ptr(sw.hi), _ptr(sw.lo), sw.ldw,
                                            _ptr(out), out.stride(0), _ptr(bias), _ptr(residual),
                                            residual.stride(0) if residual is not None else 0,

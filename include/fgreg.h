@@ -149,6 +149,20 @@ int fgr_gemm_bf16x3(const float* a, int64_t lda, const void* w_hi, const void* w
                     float* c, int64_t ldc, const float* bias, const float* r, int64_t ldr,
                     int32_t m, int32_t n, int32_t k, int32_t act, void* stream);
 
+/* fp32-accurate split GEMM (the default for every dense layer of the forward):
+ *   C[m, n] = act(A[m, :] . W[n, :] + bias[n] (+ R[m, n]))
+ * Operands are split exactly into three bf16 terms (x = h + m + l, residual <= 2^-27 |x|)
+ * and the six significant term products accumulate in fp32 on v_mfma_f32_16x16x32_bf16.
+ * W is given as an image built once by fgr_split_weights3 (W element (i, j) read from
+ * w[i * stride_n + j * stride_k], so a (K, Cin, Cout) KPConv weight needs no transpose
+ * copy); A fp32 row-major, 16-B aligned with lda % 4 == 0 when k % 8 == 0. */
+int fgr_split_weights3_bytes(int32_t n, int32_t k, size_t* bytes);
+int fgr_split_weights3(const float* w, int32_t n, int32_t k, int64_t stride_n, int64_t stride_k,
+                       void* img, void* stream);
+int fgr_gemm_bf16x6(const float* a, int64_t lda, const void* w_img, float* c, int64_t ldc,
+                    const float* bias, const float* r, int64_t ldr, int32_t m, int32_t n,
+                    int32_t k, int32_t act, void* stream);
+
 /* ---- attention ---------------------------------------------------------------------
  * Multi-head scaled-dot-product attention core of nn.MultiheadAttention
  * (transformers.py:95-96, 197-226) on packed, unpadded segments: query segment

@@ -71,18 +71,27 @@ def gemm_shapes():
         if hasattr(m, 'linear'):
             m.linear = orig
     shapes = collections.Counter(calls)
-    tot = {'fp32': 0.0, 'bf16x3': 0.0}
+    tot = {'fp32': 0.0, 'bf16x3': 0.0, 'bf16x6': 0.0, 'lib_bf16_6K': 0.0}
     flops = 0
     for (M, N, K, tp, res), cnt in sorted(shapes.items(), key=lambda kv: -kv[0][0] * kv[0][1] * kv[0][2] * kv[1]):
         x = torch.randn(M, K, device=dev)
         w = torch.randn(K, N, device=dev) if tp else torch.randn(N, K, device=dev)
         r = torch.randn(M, N, device=dev) if res else None
         line = f'M={M:6d} N={N:5d} K={K:5d} x{cnt:2d} '
-        for mode in ('fp32', 'bf16x3'):
+        for mode in ('fp32', 'bf16x3', 'bf16x6'):
             lin.set_mode(mode)
             us = timeit(lambda: orig(x, w, None, 0, r, tp), iters=20)
             tot[mode] += us * cnt
             line += f' {mode} {us:7.1f} us ({2 * M * N * K / us / 1e6:6.1f} TF)'
+        # ceiling reference: hipBLASLt bf16 GEMM with K' = 6K and fp32 output
+        try:
+            a6 = torch.randn(M, 6 * K, device=dev).bfloat16()
+            w6 = torch.randn(6 * K, N, device=dev).bfloat16()
+            us = timeit(lambda: torch.mm(a6, w6, out_dtype=torch.float32), iters=20)
+            tot['lib_bf16_6K'] += us * cnt
+            line += f' lib_bf16_6K {us:7.1f} us'
+        except Exception as e:  # noqa: BLE001
+            line += f' lib_bf16_6K n/a ({type(e).__name__})'
         flops += 2 * M * N * K * cnt
         print(line, flush=True)
     lin.set_mode('fp32')
