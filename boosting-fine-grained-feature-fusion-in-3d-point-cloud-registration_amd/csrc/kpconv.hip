@@ -58,16 +58,39 @@ __device__ __forceinline__ float kp_weight(float nx, float ny, float nz, const f
     return fmaxf(1.0f - sqrtf(d2) * inv_extent, 0.0f);
 }
 
+// Row flags for the normaliser: pos[r] = (sum_c x[r, c] > 0), one wave per row. The
+// positivity of a source row does not depend on the query, so it is computed once per
+// call instead of once per (query, neighbour) -- the gather then counts positive
+// neighbours with one ballot per 64 neighbours instead of a 64-lane reduction each.
+template <int VEC>
+__global__ void __launch_bounds__(256)
+row_positive_kernel(const float* __restrict__ x, int64_t ns, unsigned char* __restrict__ pos) {
+    constexpr int CIN = 64 * VEC;
+    const int64_t r = (int64_t)blockIdx.x * 4 + threadIdx.x / 64;
+    const int lane = threadIdx.x % 64;
+    if (r >= ns) return;
+    float xv[VEC];
+    load_vec<VEC>(x + r * CIN + lane * VEC, xv);
+    float t = 0.f;
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) t += xv[j];
+    t = wave_sum(t);
+    if (lane == 0) pos[r] = t > 0.f ? 1 : 0;
+}
+
 // One wave per query, cin = 64 * VEC, K kernel points (runtime, <= kMaxKp, unrolled by KU).
+// Valid neighbours of each 64-wide chunk are compacted by ballot; their feature rows are
+// then streamed 4 at a time (4 x 16-B loads in flight per lane) into K accumulators.
 template <int VEC, int KU>
 __global__ void __launch_bounds__(64 * kGatherWaves)
 kpconv_gather_wide(const float* __restrict__ q, const float* __restrict__ s, int64_t nq, int64_t ns,
                    const int64_t* __restrict__ idx, int width, const float* __restrict__ x,
-                   const float* __restrict__ kp_g, int n_kp, float inv_extent,
-                   float* __restrict__ wf, float* __restrict__ nnorm) {
+                   const unsigned char* __restrict__ pos, const float* __restrict__ kp_g, int n_kp,
+                   float inv_extent, float* __restrict__ wf, float* __restrict__ nnorm) {
     constexpr int CIN = 64 * VEC;
-    __shared__ float w_lds[kGatherWaves][64][KU];
-    __shared__ int nb_lds[kGatherWaves][64];
+    constexpr int U = 4;                               // neighbour rows in flight
+    __shared__ float w_lds[kGatherWaves][64 + U][KU];
+    __shared__ int nb_lds[kGatherWaves][64 + U];
     __shared__ float kp[3 * kMaxKp];
     const int wv = threadIdx.x / 64, lane = threadIdx.x % 64;
     for (int i = threadIdx.x; i < 3 * n_kp; i += blockDim.x) kp[i] = kp_g[i];
@@ -85,42 +108,43 @@ kpconv_gather_wide(const float* __restrict__ q, const float* __restrict__ s, int
     const int64_t* row = idx + qi * width;
 
     for (int h0 = 0; h0 < width; h0 += 64) {
-        // compact the valid neighbours of this 64-wide chunk (wave ballot)
         const int h = h0 + lane;
         const int64_t id = h < width ? row[h] : ns;
         const bool valid = id >= 0 && id < ns;
         const unsigned long long m = __ballot(valid);
         const int v = __popcll(m);
         if (v == 0) continue;
-        const int pos = __popcll(m & ((1ull << lane) - 1ull));
-        if (valid) nb_lds[wv][pos] = (int)id;
+        n_pos += __popcll(__ballot(valid && pos[id] != 0));
+        const int p = __popcll(m & ((1ull << lane) - 1ull));
+        if (valid) nb_lds[wv][p] = (int)id;
+        if (lane < U) nb_lds[wv][v + lane] = 0;       // pad rows: weight 0, row 0
         __builtin_amdgcn_wave_barrier();
-        // kernel-point influences of the valid neighbours -> LDS
-        for (int t = lane; t < v * n_kp; t += 64) {
-            const int hh = t / n_kp, k = t - hh * n_kp;
-            const int sid = nb_lds[wv][hh];
-            // neighbours are centred first, then compared with the kernel points (:302, :313)
-            const float nx = s[3 * sid] - qx, ny = s[3 * sid + 1] - qy, nz = s[3 * sid + 2] - qz;
-            w_lds[wv][hh][k] = kp_weight(nx, ny, nz, kp, k, inv_extent);
+        // kernel-point influences of the valid neighbours -> LDS (pad rows get 0)
+        for (int t = lane; t < (v + U) * KU; t += 64) {
+            const int hh = t / KU, k = t - hh * KU;
+            float w = 0.f;
+            if (hh < v && k < n_kp) {
+                const int sid = nb_lds[wv][hh];
+                // neighbours are centred first, then compared with the kernel points (:302, :313)
+                const float nx = s[3 * sid] - qx, ny = s[3 * sid + 1] - qy, nz = s[3 * sid + 2] - qz;
+                w = kp_weight(nx, ny, nz, kp, k, inv_extent);
+            }
+            w_lds[wv][hh][k] = w;
         }
         __builtin_amdgcn_wave_barrier();
-        for (int hh = 0; hh < v; ++hh) {
-            const int sid = nb_lds[wv][hh];
-            float xv[VEC];
-            load_vec<VEC>(x + (int64_t)sid * CIN + lane * VEC, xv);
-            float rs = 0.f;
+        for (int hh = 0; hh < v; hh += U) {
+            float xv[U][VEC];
 #pragma unroll
-            for (int j = 0; j < VEC; ++j) rs += xv[j];
-            rs = wave_sum(rs);
-            n_pos += rs > 0.f ? 1 : 0;
+            for (int u = 0; u < U; ++u)
+                load_vec<VEC>(x + (int64_t)nb_lds[wv][hh + u] * CIN + lane * VEC, xv[u]);
 #pragma unroll
-            for (int k = 0; k < KU; ++k) {
-                if (k < n_kp) {
-                    const float w = w_lds[wv][hh][k];
+            for (int u = 0; u < U; ++u)
 #pragma unroll
-                    for (int j = 0; j < VEC; ++j) acc[k][j] = fmaf(w, xv[j], acc[k][j]);
+                for (int k = 0; k < KU; ++k) {
+                    const float w = w_lds[wv][hh + u][k];
+#pragma unroll
+                    for (int j = 0; j < VEC; ++j) acc[k][j] = fmaf(w, xv[u][j], acc[k][j]);
                 }
-            }
         }
         __builtin_amdgcn_wave_barrier();
     }
@@ -187,15 +211,18 @@ void launch_narrow(const float* q, const float* s, int64_t nq, int64_t ns, const
 
 template <int VEC>
 void launch_wide(const float* q, const float* s, int64_t nq, int64_t ns, const int64_t* idx,
-                 int width, const float* x, const float* kp, int n_kp, float inv_ext, float* wf,
-                 float* nnorm, hipStream_t st) {
+                 int width, const float* x, unsigned char* pos, const float* kp, int n_kp,
+                 float inv_ext, float* wf, float* nnorm, hipStream_t st) {
+    if (ns > 0)
+        hipLaunchKernelGGL(row_positive_kernel<VEC>, dim3((unsigned)ceil_div(ns, 4)), dim3(256), 0,
+                           st, x, ns, pos);
     dim3 grid((unsigned)ceil_div(nq, kGatherWaves));
     if (n_kp <= 16)
         hipLaunchKernelGGL((kpconv_gather_wide<VEC, 16>), grid, dim3(64 * kGatherWaves), 0, st, q,
-                           s, nq, ns, idx, width, x, kp, n_kp, inv_ext, wf, nnorm);
+                           s, nq, ns, idx, width, x, pos, kp, n_kp, inv_ext, wf, nnorm);
     else
         hipLaunchKernelGGL((kpconv_gather_wide<VEC, kMaxKp>), grid, dim3(64 * kGatherWaves), 0,
-                           st, q, s, nq, ns, idx, width, x, kp, n_kp, inv_ext, wf, nnorm);
+                           st, q, s, nq, ns, idx, width, x, pos, kp, n_kp, inv_ext, wf, nnorm);
 }
 
 // max_pool, one wave per query (c % 64 == 0, VEC floats per lane): valid neighbours are
@@ -262,10 +289,16 @@ __global__ void max_pool_kernel(const float* __restrict__ x, int64_t ns, int c,
 
 using namespace fgr;
 
+extern "C" int fgr_kpconv_gather_workspace(int64_t ns, int32_t cin, size_t* bytes) {
+    FGR_REQUIRE(bytes && ns >= 0 && cin > 0, "fgr_kpconv_gather_workspace: bad arguments");
+    *bytes = (cin % 64 == 0) ? (size_t)ns : 0;
+    return FGR_OK;
+}
+
 extern "C" int fgr_kpconv_gather(const float* q, const float* s, int64_t nq, int64_t ns,
                                  const int64_t* idx, int32_t width, const float* x, int32_t cin,
                                  const float* kp, int32_t n_kp, float extent, float* wf,
-                                 float* nnorm, void* stream) {
+                                 float* nnorm, void* workspace, size_t ws_bytes, void* stream) {
     FGR_REQUIRE(nq >= 0 && ns >= 0 && width >= 0 && cin > 0 && n_kp > 0 && n_kp <= kMaxKp &&
                     extent > 0.f,
                 "fgr_kpconv_gather: bad arguments (cin %d, n_kp %d, width %d)", cin, n_kp, width);
@@ -275,10 +308,13 @@ extern "C" int fgr_kpconv_gather(const float* q, const float* s, int64_t nq, int
     hipStream_t st = as_stream(stream);
     const float inv_ext = 1.0f / extent;
     if (cin % 64 == 0 && cin <= 256) {
+        FGR_REQUIRE(workspace && ws_bytes >= (size_t)ns,
+                    "fgr_kpconv_gather: workspace of %lld bytes needed", (long long)ns);
+        unsigned char* pos = (unsigned char*)workspace;
         switch (cin / 64) {
-            case 1: launch_wide<1>(q, s, nq, ns, idx, width, x, kp, n_kp, inv_ext, wf, nnorm, st); break;
-            case 2: launch_wide<2>(q, s, nq, ns, idx, width, x, kp, n_kp, inv_ext, wf, nnorm, st); break;
-            default: launch_wide<4>(q, s, nq, ns, idx, width, x, kp, n_kp, inv_ext, wf, nnorm, st); break;
+            case 1: launch_wide<1>(q, s, nq, ns, idx, width, x, pos, kp, n_kp, inv_ext, wf, nnorm, st); break;
+            case 2: launch_wide<2>(q, s, nq, ns, idx, width, x, pos, kp, n_kp, inv_ext, wf, nnorm, st); break;
+            default: launch_wide<4>(q, s, nq, ns, idx, width, x, pos, kp, n_kp, inv_ext, wf, nnorm, st); break;
         }
     } else if (cin <= 64) {
         if (cin == 1) launch_narrow<1>(q, s, nq, ns, idx, width, x, cin, kp, n_kp, inv_ext, wf, nnorm, st);

@@ -25,8 +25,9 @@ SIGNATURES = {
     'fgr_grid_subsample_fill': [_i64, _i32, _i64, _vp, _sz, _vp, _vp, _vp, _vp],
     'fgr_radius_count': [_vp, _vp, _vp, _vp, _i32, _i64, _i32, _f32, _vp, _vp, _vp],
     'fgr_radius_search': [_vp, _vp, _vp, _vp, _i32, _i64, _i64, _i32, _f32, _i32, _i32, _vp, _vp],
+    'fgr_kpconv_gather_workspace': [_i64, _i32, ctypes.POINTER(_sz)],
     'fgr_kpconv_gather': [_vp, _vp, _i64, _i64, _vp, _i32, _vp, _i32, _vp, _i32, _f32, _vp, _vp,
-                          _vp],
+                          _vp, _sz, _vp],
     'fgr_max_pool': [_vp, _i64, _i32, _vp, _i64, _i32, _vp, _vp],
     'fgr_instnorm_workspace': [_i64, _i32, _i32, ctypes.POINTER(_sz)],
     'fgr_instnorm': [_vp, _i64, _i32, _vp, _i32, _i64, _vp, _f32, _i32, _vp, _i32, _vp, _vp, _sz,

@@ -188,10 +188,14 @@ def kpconv_gather(q, s, idx, x, kernel_points, extent) -> Tuple[torch.Tensor, to
     K, cin = kp.shape[0], x.shape[1]
     wf = torch.empty((nq, K, cin), dtype=torch.float32, device=q.device)
     nnorm = torch.empty((nq,), dtype=torch.float32, device=q.device)
+    L = _lib.load()
+    nb = _lib._sz(0)
+    _lib.check(L.fgr_kpconv_gather_workspace(ns, cin, nb), 'fgr_kpconv_gather_workspace')
+    ws = _workspace(q.device, nb.value) if nb.value else None
     t0 = _begin('kpconv_gather')
-    _lib.check(_lib.load().fgr_kpconv_gather(_ptr(q), _ptr(s), nq, ns, _ptr(idx), idx.shape[1],
-                                             _ptr(x), cin, _ptr(kp), K, float(extent), _ptr(wf),
-                                             _ptr(nnorm), _stream()), 'fgr_kpconv_gather')
+    _lib.check(L.fgr_kpconv_gather(_ptr(q), _ptr(s), nq, ns, _ptr(idx), idx.shape[1], _ptr(x), cin,
+                                   _ptr(kp), K, float(extent), _ptr(wf), _ptr(nnorm), _ptr(ws),
+                                   nb.value, _stream()), 'fgr_kpconv_gather')
     _end('kpconv_gather', t0, lambda: gather_bytes(idx, ns, cin, K))
     return wf, nnorm
 

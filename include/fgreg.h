@@ -89,10 +89,13 @@ int fgr_radius_search(const float* q, const int64_t* q_off, const float* s, cons
  * rigid, linear influence, sum aggregation):
  *   wf[q, k, c] = sum_{valid h} max(0, 1 - |(s[idx[q,h]] - q) - kp[k]| / extent) * x[idx[q,h], c]
  * and the normaliser of :395-399: nnorm[q] = max(1, #{valid h : sum_c x[idx[q,h], c] > 0}).
- * The caller finishes with (wf.view(nq, K*cin) @ W.view(K*cin, cout)) / nnorm. */
+ * The caller finishes with (wf.view(nq, K*cin) @ W.view(K*cin, cout)) / nnorm.
+ * workspace: fgr_kpconv_gather_workspace() bytes (per-source-row flags of the normaliser). */
+int fgr_kpconv_gather_workspace(int64_t ns, int32_t cin, size_t* bytes);
 int fgr_kpconv_gather(const float* q, const float* s, int64_t nq, int64_t ns, const int64_t* idx,
                       int32_t width, const float* x, int32_t cin, const float* kp, int32_t n_kp,
-                      float extent, float* wf, float* nnorm, void* stream);
+                      float extent, float* wf, float* nnorm, void* workspace, size_t ws_bytes,
+                      void* stream);
 
 /* max_pool (finegrained_kpconv_blocks.py:125-141): out[q, c] = max over the row of
  * x[idx[q, h], c], shadow entries contributing 0 (the appended zero row). */

@@ -41,7 +41,7 @@ def test_argument_errors_are_reported_without_gpu():
     assert rc == -1
     assert b'fgr_radius_search' in L.fgr_last_error()
     rc = L.fgr_kpconv_gather(None, None, 10, 10, None, 4, None, 100, None, 15,
-                             ctypes.c_float(1.0), None, None, None)
+                             ctypes.c_float(1.0), None, None, None, 0, None)
     assert rc == -1 and b'kpconv' in L.fgr_last_error()
     rc = L.fgr_attention(None, 0, None, 0, None, 0, None, 0, None, None, None, 1, 1, 1, 32,
                          ctypes.c_float(1.0), None)
