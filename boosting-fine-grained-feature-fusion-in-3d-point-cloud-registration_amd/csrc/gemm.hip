@@ -214,7 +214,7 @@ struct Gemm6Args {
     int M, N, K, act;
 };
 
-template <int BM, int BN>
+template <int BM, int BN, bool KVEC>
 __global__ void __launch_bounds__(256) gemm_bf16x6_kernel(Gemm6Args p) {
     constexpr int TM = BM / 32, TN = BN / 32;         // 16x16 subtiles per wave (2 x 2 waves)
     constexpr int UA = BM * 4 / 256;                   // A units (8 k of one row) per thread
@@ -231,41 +231,49 @@ __global__ void __launch_bounds__(256) gemm_bf16x6_kernel(Gemm6Args p) {
     const int g = lane >> 4, c = lane & 15;
     const int npanel = (p.N + 15) / 16;
 
-    float4 ar[UA][2];
-    u32x4 wr[UW];
-    int64_t woff[UW];                                   // image unit of step 0
-    bool wok[UW];
+    // Branch-free staging: rows past M and panels past N read a clamped (valid) address
+    // -- their results are never stored; k past K is zeroed by a select.
+    const float* arow[UA];
+    int akk[UA];
+#pragma unroll
+    for (int j = 0; j < UA; ++j) {
+        const int u = tid + 256 * j;
+        arow[j] = p.A + (int64_t)min(m0 + (u >> 2), p.M - 1) * p.lda;
+        akk[j] = 8 * (u & 3);
+    }
+    const u32x4* wsrc[UW];
 #pragma unroll
     for (int j = 0; j < UW; ++j) {
         const int v = tid + 256 * j;
-        const int pp = v / 192, rem = v % 192;
-        const int panel = n0 / 16 + pp;
-        wok[j] = panel < npanel;
-        woff[j] = (int64_t)panel * p.ksteps * 192 + rem;
+        const int panel = min(n0 / 16 + v / 192, npanel - 1);
+        wsrc[j] = p.W + (int64_t)panel * p.ksteps * 192 + v % 192;
     }
-    const bool kvec8 = (p.K & 7) == 0;
+    float4 ar[UA][2];
+    u32x4 wr[UW];
     auto load = [&](int s) {
-        const int k0 = s * 32;
 #pragma unroll
         for (int j = 0; j < UA; ++j) {
-            const int u = tid + 256 * j;
-            const int row = u >> 2, gg = u & 3;
-            const int m = m0 + row, k = k0 + 8 * gg;
-            const float* src = p.A + (int64_t)m * p.lda + k;
-            if (m < p.M && k + 8 <= p.K && kvec8) {
-                ar[j][0] = *reinterpret_cast<const float4*>(src);
-                ar[j][1] = *reinterpret_cast<const float4*>(src + 4);
+            const int k = s * 32 + akk[j];
+            if constexpr (KVEC) {
+                const float* src = arow[j] + min(k, p.K - 8);
+                float4 x0 = *reinterpret_cast<const float4*>(src);
+                float4 x1 = *reinterpret_cast<const float4*>(src + 4);
+                const bool ok = k < p.K;
+                ar[j][0] = ok ? x0 : make_float4(0.f, 0.f, 0.f, 0.f);
+                ar[j][1] = ok ? x1 : make_float4(0.f, 0.f, 0.f, 0.f);
             } else {
                 float t[8];
 #pragma unroll
-                for (int e = 0; e < 8; ++e) t[e] = (m < p.M && k + e < p.K) ? src[e] : 0.f;
+                for (int e = 0; e < 8; ++e) {
+                    const float xv = arow[j][min(k + e, p.K - 1)];
+                    t[e] = k + e < p.K ? xv : 0.f;
+                }
                 ar[j][0] = make_float4(t[0], t[1], t[2], t[3]);
                 ar[j][1] = make_float4(t[4], t[5], t[6], t[7]);
             }
         }
 #pragma unroll
-        for (int j = 0; j < UW; ++j)
-            wr[j] = wok[j] ? p.W[woff[j] + (int64_t)s * 192] : u32x4{0u, 0u, 0u, 0u};
+        for (int j = 0; j < UW; ++j) wr[j] = wsrc[j][(int64_t)s * 192];
     };
     auto store = [&]() {
 #pragma unroll
@@ -319,14 +327,12 @@ __global__ void __launch_bounds__(256) gemm_bf16x6_kernel(Gemm6Args p) {
             const bf16x8 al = __builtin_bit_cast(bf16x8, a_lds[(2 * 4 + g) * BM + r]);
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
-                f32x4 a = acc[i][j];
-                a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bw[j][1], a, 0, 0, 0);
-                a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bw[j][0], a, 0, 0, 0);
-                a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bw[j][2], a, 0, 0, 0);
-                a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bw[j][0], a, 0, 0, 0);
-                a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bw[j][1], a, 0, 0, 0);
-                a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bw[j][0], a, 0, 0, 0);
-                acc[i][j] = a;
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bw[j][1], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bw[j][0], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bw[j][2], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bw[j][0], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bw[j][1], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bw[j][0], acc[i][j], 0, 0, 0);
             }
         }
     }
@@ -379,8 +385,12 @@ __global__ void split_weights3_kernel(const float* __restrict__ w, int n, int k,
 template <int BM, int BN>
 void launch6(const Gemm6Args& a, hipStream_t st) {
     const int nbm = (a.M + BM - 1) / BM, nbn = (a.N + BN - 1) / BN;
-    hipLaunchKernelGGL((gemm_bf16x6_kernel<BM, BN>), dim3((unsigned)(nbm * nbn)), dim3(256), 0, st,
-                       a);
+    if (a.K % 8 == 0)
+        hipLaunchKernelGGL((gemm_bf16x6_kernel<BM, BN, true>), dim3((unsigned)(nbm * nbn)),
+                           dim3(256), 0, st, a);
+    else
+        hipLaunchKernelGGL((gemm_bf16x6_kernel<BM, BN, false>), dim3((unsigned)(nbm * nbn)),
+                           dim3(256), 0, st, a);
 }
 
 }  // namespace
@@ -454,12 +464,18 @@ extern "C" int fgr_gemm_bf16x6(const float* a, int64_t lda, const void* w_img, f
     if (m == 0) return FGR_OK;
     Gemm6Args g{a, lda, (const u32x4*)w_img, (k + 31) / 32, c, ldc, bias, r, ldr, m, n, k, act};
     hipStream_t st = as_stream(stream);
-    const int64_t b128 = ceil_div(m, 128) * ceil_div(n, 128);
-    const int64_t b12864 = ceil_div(m, 128) * ceil_div(n, 64);
-    if (b128 >= 400)
+    // tile choice (measured on the forward's shapes, microbench.py tiles): 64 x 128 for wide
+    // outputs (N >= 512, N % 256 == 0), 64 x 64 otherwise -- small tiles at 4-5 blocks per
+    // CU hide the 2-barrier staging better than 128 x 128 at 2. FGR_GEMM6_TILE overrides it
+    // for tuning (a = 128x128, b = 128x64, c = 64x64, d = 64x128).
+    const char* force = getenv("FGR_GEMM6_TILE");
+    const char cfg = (force && force[0]) ? force[0] : (n >= 512 && n % 256 == 0) ? 'd' : 'c';
+    if (cfg == 'a')
         launch6<128, 128>(g, st);
-    else if (b12864 >= 400)
+    else if (cfg == 'b')
         launch6<128, 64>(g, st);
+    else if (cfg == 'd')
+        launch6<64, 128>(g, st);
     else
         launch6<64, 64>(g, st);
     FGR_CHECK_LAUNCH("gemm_bf16x6_kernel");

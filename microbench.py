@@ -99,6 +99,28 @@ def gemm_shapes():
           ', '.join(f'{k} {v / 1e3:.3f} ms' for k, v in tot.items()), flush=True)
 
 
+def gemm_tiles():
+    """bf16x6 GEMM per tile configuration (FGR_GEMM6_TILE a=128x128, b=128x64, c=64x64)."""
+    import os
+    import fgreg.linear as lin
+    dev = torch.device('cuda:0')
+    lin.set_mode('bf16x6')
+    shapes = [(9493, 1024, 2048), (9493, 768, 256), (9493, 256, 3840), (9493, 1024, 256),
+              (9493, 256, 1024), (11472, 512, 1024), (9493, 1792, 256), (9493, 256, 256),
+              (56958, 256, 256), (11472, 128, 1920), (9493, 512, 1024), (9493, 1024, 512),
+              (11472, 896, 128), (11472, 512, 256), (11472, 128, 512), (9493, 256, 512)]
+    for (M, N, K) in shapes:
+        x = torch.randn(M, K, device=dev)
+        w = torch.randn(N, K, device=dev)
+        line = f'M={M:6d} N={N:5d} K={K:5d}'
+        for t in 'acd':
+            os.environ['FGR_GEMM6_TILE'] = t
+            us = timeit(lambda: lin.linear(x, w), iters=20)
+            line += f'  {t}: {us:7.1f} us ({2 * M * N * K / us / 1e6:6.1f} TF)'
+        print(line, flush=True)
+    os.environ['FGR_GEMM6_TILE'] = ''
+
+
 if __name__ == '__main__':
     import os
     which = sys.argv[1:] or ['attention']
@@ -107,3 +129,5 @@ if __name__ == '__main__':
         attention(lens=(2000,) * 2)
     if 'gemm' in which:
         gemm_shapes()
+    if 'tiles' in which:
+        gemm_tiles()
