@@ -106,6 +106,139 @@ res2net_chain_kernel(const float* __restrict__ h, int64_t n, int scale, int nums
     }
 }
 
+
+// ------------------------------------------------------------------------------------
+// bf16x6 variant (fp32-accurate, see gemm.hip): the same hierarchy on the bf16 matrix
+// cores. Per step the A operand a = sp_{i-1} + h_i is formed in fp32, split exactly into
+// three bf16 terms and stored as fragment-ordered LDS images
+//   img[t][ks][g][row] (16-B units: row, k = 32 ks + 8 g .. + 7),
+// read with conflict-free ds_read_b128; sp_i stays in an fp32 LDS tile between steps.
+// W_i comes pre-split from the host in fragment order [i][jt][ks][t][g][c][8] (1 KB per
+// wave-load), streamed two k-steps ahead. K is padded to a multiple of 32 (w = 112 -> 128)
+// with zero weights and zero A columns. 2 barriers per step (build | MFMA + epilogue).
+// ------------------------------------------------------------------------------------
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void split3(float x, __bf16& h, __bf16& m, __bf16& l) {
+    h = (__bf16)x;
+    const float r = x - (float)h;
+    m = (__bf16)r;
+    l = (__bf16)(r - (float)m);
+}
+
+template <int KT>   // KT = w / 16 column tiles (= waves); KS = ceil(w / 32) k-steps
+__global__ void __launch_bounds__(64 * KT)
+res2net_chain6_kernel(const float* __restrict__ h, int64_t n, int scale, int nums,
+                      const u32x4* __restrict__ wf, const float* __restrict__ bias,
+                      const float* __restrict__ x, int cin, float* __restrict__ cat, int64_t ld) {
+    constexpr int W = 16 * KT, KS = (W + 31) / 32, NU = kRows * KS * 4;   // A units per term
+    __shared__ u32x4 img[3 * NU];
+    __shared__ float sp[kRows * W];
+    const int tid = threadIdx.x, nth = 64 * KT;
+    const int wv = tid / 64, lane = tid % 64, g = lane >> 4, c = lane & 15;
+    const int64_t r0 = (int64_t)blockIdx.x * kRows;
+    const int64_t hw = (int64_t)scale * W;
+    const int col = wv * 16 + c;
+
+    for (int i = 0; i < nums; ++i) {
+        const u32x4* wb = wf + (((int64_t)i * KT + wv) * KS) * 192 + lane;
+        u32x4 bq[3][3];                                // ring: k-steps ks, ks+1, ks+2
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+            if (q < KS) {
+#pragma unroll
+                for (int t = 0; t < 3; ++t) bq[q][t] = wb[(q * 3 + t) * 64];
+            }
+        const float bc = bias[i * W + col];
+        // build the split A images: unit u -> (row = u % 32, kg = u / 32), 8 k each
+        for (int u = tid; u < NU; u += nth) {
+            const int row = u % kRows, kg = u / kRows;       // kg = 4 ks + g'
+            const int k0 = 8 * kg;
+            float a[8];
+            const int64_t gr = r0 + row;
+#pragma unroll
+            for (int e = 0; e < 8; e += 4) {
+                float4 hv = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (gr < n && k0 + e < W)
+                    hv = *reinterpret_cast<const float4*>(h + gr * hw + (int64_t)i * W + k0 + e);
+                a[e] = hv.x; a[e + 1] = hv.y; a[e + 2] = hv.z; a[e + 3] = hv.w;
+            }
+            if (i > 0) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e)
+                    if (k0 + e < W) a[e] += sp[row * W + k0 + e];
+            }
+            bf16x8 th, tm, tl;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                __bf16 hh, mm, ll;
+                split3(a[e], hh, mm, ll);
+                th[e] = hh; tm[e] = mm; tl[e] = ll;
+            }
+            img[0 * NU + kg * kRows + row] = __builtin_bit_cast(u32x4, th);
+            img[1 * NU + kg * kRows + row] = __builtin_bit_cast(u32x4, tm);
+            img[2 * NU + kg * kRows + row] = __builtin_bit_cast(u32x4, tl);
+        }
+        __syncthreads();
+        f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            if (ks + 2 < KS) {
+#pragma unroll
+                for (int t = 0; t < 3; ++t) bq[(ks + 2) % 3][t] = wb[((ks + 2) * 3 + t) * 64];
+            }
+            const bf16x8 bh = __builtin_bit_cast(bf16x8, bq[ks % 3][0]);
+            const bf16x8 bm = __builtin_bit_cast(bf16x8, bq[ks % 3][1]);
+            const bf16x8 bl = __builtin_bit_cast(bf16x8, bq[ks % 3][2]);
+            const int base = (ks * 4 + g) * kRows;
+            const bf16x8 a0h = __builtin_bit_cast(bf16x8, img[0 * NU + base + c]);
+            const bf16x8 a0m = __builtin_bit_cast(bf16x8, img[1 * NU + base + c]);
+            const bf16x8 a0l = __builtin_bit_cast(bf16x8, img[2 * NU + base + c]);
+            const bf16x8 a1h = __builtin_bit_cast(bf16x8, img[0 * NU + base + 16 + c]);
+            const bf16x8 a1m = __builtin_bit_cast(bf16x8, img[1 * NU + base + 16 + c]);
+            const bf16x8 a1l = __builtin_bit_cast(bf16x8, img[2 * NU + base + 16 + c]);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0m, bm, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1m, bm, acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0l, bh, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1l, bh, acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0h, bl, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1h, bl, acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0m, bh, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1m, bh, acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0h, bm, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1h, bm, acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0h, bh, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1h, bh, acc1, 0, 0, 0);
+        }
+        // epilogue: sp_i -> cat and the fp32 LDS tile (read by the next step's build,
+        // which starts after the barrier below)
+#pragma unroll
+        for (int rg = 0; rg < 2; ++rg) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = rg * 16 + 4 * g + r;
+                const float y = fmaxf((rg ? acc1[r] : acc0[r]) + bc, 0.f);
+                if (r0 + row < n) cat[(r0 + row) * ld + (int64_t)i * W + col] = y;
+                sp[row * W + col] = y;
+            }
+        }
+        __syncthreads();
+    }
+    const int rest = (scale - nums) * W;
+    for (int e = tid; e < kRows * rest; e += nth) {
+        const int row = e / rest, cc = e - row * rest;
+        if (r0 + row < n)
+            cat[(r0 + row) * ld + (int64_t)nums * W + cc] = h[(r0 + row) * hw + (int64_t)nums * W + cc];
+    }
+    if (x) {
+        for (int e = tid; e < kRows * cin; e += nth) {
+            const int row = e / cin, cc = e - row * cin;
+            if (r0 + row < n) cat[(r0 + row) * ld + hw + cc] = x[(r0 + row) * cin + cc];
+        }
+    }
+}
+
 }  // namespace
 }  // namespace fgr
 
@@ -128,5 +261,27 @@ extern "C" int fgr_res2net_chain(const float* h, int64_t n, int32_t w, int32_t s
         hipLaunchKernelGGL(res2net_chain_kernel<14>, grid, dim3(64 * 14), 0, st, h, n, scale,
                            scale - 1, w_frag, bias, x, cin, cat, ld_cat);
     FGR_CHECK_LAUNCH("res2net_chain_kernel");
+    return FGR_OK;
+}
+
+extern "C" int fgr_res2net_chain6(const float* h, int64_t n, int32_t w, int32_t scale,
+                                  const void* w_img, const float* bias, const float* x,
+                                  int32_t cin, float* cat, int64_t ld_cat, void* stream) {
+    FGR_REQUIRE(n >= 0 && scale >= 2 && (w == 112 || w == 224) && cin >= 0,
+                "fgr_res2net_chain6: unsupported width %d / scale %d (needs 112 or 224)", w, scale);
+    FGR_REQUIRE(ld_cat >= (int64_t)scale * w + (x ? cin : 0), "fgr_res2net_chain6: ld_cat too small");
+    FGR_REQUIRE(n == 0 || (h && w_img && bias && cat), "fgr_res2net_chain6: null pointer");
+    FGR_REQUIRE(((reinterpret_cast<uintptr_t>(h) & 15) == 0) && (scale * w) % 4 == 0,
+                "fgr_res2net_chain6: h must be 16-B aligned");
+    if (n == 0) return FGR_OK;
+    const dim3 grid((unsigned)ceil_div(n, kRows));
+    hipStream_t st = as_stream(stream);
+    if (w == 112)
+        hipLaunchKernelGGL(res2net_chain6_kernel<7>, grid, dim3(64 * 7), 0, st, h, n, scale,
+                           scale - 1, (const u32x4*)w_img, bias, x, cin, cat, ld_cat);
+    else
+        hipLaunchKernelGGL(res2net_chain6_kernel<14>, grid, dim3(64 * 14), 0, st, h, n, scale,
+                           scale - 1, (const u32x4*)w_img, bias, x, cin, cat, ld_cat);
+    FGR_CHECK_LAUNCH("res2net_chain6_kernel");
     return FGR_OK;
 }

@@ -26,6 +26,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import ops
+from . import linear as lin
 from .linear import linear
 
 
@@ -261,8 +262,10 @@ class my_Bottle2neck(nn.Module):  # noqa: N801 -- reference name (res2net.py:84)
                     w3d, b3d = w3, b3
                 chain = None
                 if w1.is_cuda and ops.res2net_chain_supported(self.width) and self.nums > 0:
-                    chain = (ops.res2net_fragments(torch.stack([wi for wi, _ in ws])),
-                             torch.stack([bi for _, bi in ws]).contiguous())
+                    wst = torch.stack([wi for wi, _ in ws])
+                    chain = (ops.res2net_fragments(wst),
+                             torch.stack([bi for _, bi in ws]).contiguous(),
+                             ops.res2net_fragments3(wst))
             self._folded = (key, w1, b1, ws, w3d, b3d, chain)
         return self._folded[1:]
 
@@ -276,7 +279,10 @@ class my_Bottle2neck(nn.Module):  # noqa: N801 -- reference name (res2net.py:84)
             # one launch for the whole hierarchy + the [.. | x] concat (fgr_res2net_chain)
             cat_in = torch.empty((x.shape[0], w * self.scale + x.shape[1]), dtype=x.dtype,
                                  device=x.device)
-            ops.res2net_chain(out, w, self.scale, chain[0], chain[1], x, cat_in)
+            if lin.MODE == 'bf16x6':
+                ops.res2net_chain(out, w, self.scale, chain[2], chain[1], x, cat_in, split6=True)
+            else:
+                ops.res2net_chain(out, w, self.scale, chain[0], chain[1], x, cat_in)
             return linear(cat_in, w3d, b3d, act=ops.ACT_RELU)
         cat_in = torch.empty((x.shape[0], w * self.scale + (x.shape[1] if self.downsample is not None else 0)),
                              dtype=x.dtype, device=x.device)

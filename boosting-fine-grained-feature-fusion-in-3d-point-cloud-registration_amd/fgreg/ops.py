@@ -291,12 +291,30 @@ def res2net_fragments(weights: torch.Tensor) -> torch.Tensor:
     return t.permute(0, 1, 3, 5, 2, 4).contiguous()             # [i, jt, k4, g, c, q]
 
 
+def res2net_fragments3(weights: torch.Tensor) -> torch.Tensor:
+    """(nums, w, w) Linear weights (out, in) -> the bf16x6 image of fgr_res2net_chain6:
+    K zero-padded to a multiple of 32, each value split exactly into three bf16 terms
+    (h = bf16(x), m = bf16(x - h), l = bf16(x - h - m)), laid out in 16x16x32 B-fragment
+    order [i][jt][ks][term][g][c][8] with value W_i[16 jt + c][32 ks + 8 g + e]."""
+    nums, w, _ = weights.shape
+    ks = (w + 31) // 32
+    wp = torch.zeros((nums, w, ks * 32), dtype=torch.float32, device=weights.device)
+    wp[..., :w] = weights
+    hi = wp.to(torch.bfloat16)
+    r = wp - hi.float()
+    mid = r.to(torch.bfloat16)
+    lo = (r - mid.float()).to(torch.bfloat16)
+    t = torch.stack([hi, mid, lo], 0).reshape(3, nums, w // 16, 16, ks, 4, 8)
+    return t.permute(1, 2, 4, 0, 5, 3, 6).contiguous()     # [i, jt, ks, t, g, c, e]
+
+
 def res2net_chain_supported(w):
     return w in (112, 224)
 
 
-def res2net_chain(h, w, scale, w_frag, bias, x, cat):
-    """cat[:, :] = [sp_0..sp_{scale-2} | h_{scale-1} | x] (fgr_res2net_chain)."""
+def res2net_chain(h, w, scale, w_frag, bias, x, cat, split6=False):
+    """cat[:, :] = [sp_0..sp_{scale-2} | h_{scale-1} | x] (fgr_res2net_chain, fp32 MFMA;
+    or fgr_res2net_chain6, fp32-accurate split bf16, with w_frag = res2net_fragments3)."""
     _dev(h, w_frag, bias, x, cat)
     h = _c(h, torch.float32)
     n = h.shape[0]
@@ -304,9 +322,9 @@ def res2net_chain(h, w, scale, w_frag, bias, x, cat):
     cin = 0 if x is None else x.shape[1]
     if x is not None:
         x = _c(x, torch.float32)
-    _lib.check(_lib.load().fgr_res2net_chain(_ptr(h), n, w, scale, _ptr(w_frag), _ptr(bias),
-                                             _ptr(x), cin, _ptr(cat), cat.stride(0), _stream()),
-               'fgr_res2net_chain')
+    fn = _lib.load().fgr_res2net_chain6 if split6 else _lib.load().fgr_res2net_chain
+    _lib.check(fn(_ptr(h), n, w, scale, _ptr(w_frag), _ptr(bias), _ptr(x), cin, _ptr(cat),
+                  cat.stride(0), _stream()), 'fgr_res2net_chain6' if split6 else 'fgr_res2net_chain')
     return cat
 
 

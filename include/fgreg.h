@@ -138,6 +138,12 @@ int fgr_sine_pos_embed(const float* xyz, int64_t n, int32_t d_model, float tempe
 int fgr_res2net_chain(const float* h, int64_t n, int32_t w, int32_t scale, const float* w_frag,
                       const float* bias, const float* x, int32_t cin, float* cat, int64_t ld_cat,
                       void* stream);
+/* fp32-accurate bf16x6 variant (the default): w_img = the (nums, w, w) folded weights
+ * K-padded to a multiple of 32, split into three bf16 terms and laid out in 16x16x32
+ * fragment order [i][jt][ks][term][g][c][8] (fgreg.ops.res2net_fragments3); h 16-B aligned. */
+int fgr_res2net_chain6(const float* h, int64_t n, int32_t w, int32_t scale, const void* w_img,
+                       const float* bias, const float* x, int32_t cin, float* cat,
+                       int64_t ld_cat, void* stream);
 
 /* ---- dense layers ----------------------------------------------------------------------
  * Split-precision GEMM for every Linear / KPConv-weight product of the forward:

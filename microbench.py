@@ -131,3 +131,12 @@ if __name__ == '__main__':
         gemm_shapes()
     if 'tiles' in which:
         gemm_tiles()
+    if 'gemm1' in which:
+        import fgreg.linear as lin
+        lin.set_mode('bf16x6')
+        dev = torch.device('cuda:0')
+        for (M, N, K) in [(9493, 256, 1024), (9493, 1024, 2048)]:
+            x = torch.randn(M, K, device=dev)
+            w = torch.randn(N, K, device=dev)
+            us = timeit(lambda: lin.linear(x, w), iters=20)
+            print(f'M={M} N={N} K={K}: {us:.1f} us', flush=True)

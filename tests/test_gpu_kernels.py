@@ -228,11 +228,23 @@ def test_procrustes_vs_reference(gpu, case):
     assert np.array_equal(w_copy.cpu().numpy(), thr)
 
 
+@pytest.mark.parametrize('mode', ['bf16x6', 'fp32'])
 @pytest.mark.parametrize('cin,cout', [(128, 512), (256, 1024), (8, 32)])
-def test_res2net_block_vs_oracle(gpu, cin, cout):
-    """my_res2Net (res2net.py:84-159, 231-265) in eval: fused fgr_res2net_chain path for
-    widths 112 / 224, torch path for the narrow width, vs the CPU restatement."""
+def test_res2net_block_vs_oracle(gpu, cin, cout, mode):
+    """my_res2Net (res2net.py:84-159, 231-265) in eval: fused fgr_res2net_chain6 (bf16x6)
+    or fgr_res2net_chain (fp32 MFMA) path for widths 112 / 224, torch path for the narrow
+    width, vs the CPU restatement."""
+    from fgreg import linear as fl
     from fgreg.backbone import my_Bottle2neck, my_res2Net
+    old = fl.MODE
+    fl.set_mode(mode)
+    try:
+        _res2net_case(gpu, cin, cout, my_Bottle2neck, my_res2Net)
+    finally:
+        fl.set_mode(old)
+
+
+def _res2net_case(gpu, cin, cout, my_Bottle2neck, my_res2Net):
     torch.manual_seed(cout)
     m = my_res2Net(my_Bottle2neck, cin, cout, baseWidth=14, scale=8)
     g = torch.Generator().manual_seed(cin)

@@ -109,3 +109,23 @@ def test_kernel_disposition():
     assert kp.shape == (15, 3) and np.allclose(kp[0], 0)
     r = np.linalg.norm(kp[1:], axis=1)
     assert abs(r.mean() - 0.66) < 1e-6 and r.min() > 0.3
+
+
+def test_res2net_fragments3_layout():
+    """The bf16x6 weight image of fgr_res2net_chain6: three exact bf16 terms per value
+    (sum within 2^-24 relative), zero K padding, [i][jt][ks][t][g][c][e] order."""
+    from fgreg import ops
+    g = torch.Generator().manual_seed(3)
+    for w in (112, 224):
+        W = torch.randn(7, w, w, generator=g)
+        img = ops.res2net_fragments3(W)
+        ks = (w + 31) // 32
+        assert img.shape == (7, w // 16, ks, 3, 4, 16, 8) and img.dtype == torch.bfloat16
+        tot = img.float().sum(3)                               # h + m + l
+        i, jt, kk, gg, c, e = 5, 3, ks - 1, 2, 9, 6
+        k = 32 * kk + 8 * gg + e
+        want = W[i, 16 * jt + c, k] if k < w else torch.tensor(0.)
+        assert torch.allclose(tot[i, jt, kk, gg, c, e], want, rtol=2 ** -23, atol=0)
+        full = tot.permute(0, 1, 4, 2, 3, 5).reshape(7, w, ks * 32)
+        assert (full[..., :w] - W).abs().max() <= 2 ** -22 * W.abs().max()
+        assert bool((full[..., w:] == 0).all())
