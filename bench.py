@@ -29,6 +29,7 @@ sys.path.insert(0, os.path.join(REPO, 'boosting-fine-grained-feature-fusion-in-3
 
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
 FP32_MFMA_PEAK_TFLOPS = 157.3
+BF16_MFMA_PEAK_TFLOPS = 2500.0   # dense (MI355X_MICROARCH.md); the bf16x6 kernels issue 6 per product
 
 
 def parse():
@@ -90,15 +91,17 @@ def main():
         for _ in range(max(args.warmup, 1)):
             step()
         # algorithmic work per launch (untimed pass with counting on)
-        timer = ops.KernelTimer(['kpconv_gather', 'attention'])
+        timer = ops.KernelTimer(['kpconv_gather', 'attention', 'gemm'])
         timer.count = True
         ops.TIMER = timer
         step()
         torch.cuda.synchronize()
         gather_bytes = list(timer.work['kpconv_gather'])
         attn_flops = list(timer.work['attention'])
+        gemm_flops = list(timer.work['gemm'])
         timer.count = False
         timer.reset_events()
+        timer.names.discard('gemm')       # GEMM events: separate pass below, not in `value`
 
         if dist is not None:
             dist.barrier()
@@ -110,6 +113,12 @@ def main():
         if dist is not None:
             dist.barrier()
         elapsed = time.perf_counter() - t0
+        # instrumented pass for the GEMM roofline (every dense layer), outside the timed region
+        gtimer = ops.KernelTimer(['gemm'])
+        ops.TIMER = gtimer
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
         ops.TIMER = None
 
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -127,6 +136,9 @@ def main():
     g_bytes_launch = g_bytes_step / max(len(gather_bytes), 1)
     g_achieved = g_bytes_launch / g_avg_s / 1e9 if g_avg_s > 0 else 0.0
     a_achieved = a_flops_step * args.steps / (a_ms / 1e3) / 1e12 if a_ms > 0 else 0.0
+    m_ms = gtimer.total_ms('gemm')
+    m_flops_step = float(sum(gemm_flops))
+    m_achieved = m_flops_step * args.steps / (m_ms / 1e3) / 1e12 if m_ms > 0 else 0.0
     traffic = _pmc_traffic()
 
     cpu = None
@@ -164,7 +176,19 @@ def main():
                                    'unit': 'TFLOP/s', 'frac': a_achieved / FP32_MFMA_PEAK_TFLOPS,
                                    'flops_per_step': a_flops_step,
                                    'avg_launch_us': a_ms * 1e3 / max(a_launches, 1),
-                                   'share_of_step': a_ms / (elapsed * 1e3)},
+                                   'share_of_step': a_ms / (elapsed * 1e3),
+                                   'precision': 'fp32-accurate bf16x6 split (6 bf16 MFMA '
+                                                'products per fp32 product)',
+                                   'bf16_pipe_tflops': 6 * a_achieved,
+                                   'bf16_pipe_frac': 6 * a_achieved / BF16_MFMA_PEAK_TFLOPS},
+            'roofline_gemm': {'kernel': 'fgr_gemm_bf16x6 (all dense layers)', 'bound': 'mfma',
+                              'achieved': m_achieved, 'peak': FP32_MFMA_PEAK_TFLOPS,
+                              'unit': 'TFLOP/s (fp32-equivalent)',
+                              'frac': m_achieved / FP32_MFMA_PEAK_TFLOPS,
+                              'flops_per_step': m_flops_step,
+                              'launches_per_step': len(gemm_flops),
+                              'share_of_step': m_ms / (elapsed * 1e3),
+                              'bf16_pipe_frac': 6 * m_achieved / BF16_MFMA_PEAK_TFLOPS},
             'cpu_baseline': cpu,
         }
         print(json.dumps(line), flush=True)

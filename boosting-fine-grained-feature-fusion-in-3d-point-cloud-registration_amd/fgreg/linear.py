@@ -15,7 +15,7 @@ import os
 import torch
 
 from . import _lib
-from .ops import ACT_NONE, ACT_RELU, _dev, _ptr, _stream
+from .ops import ACT_NONE, ACT_RELU, _begin, _dev, _end, _ptr, _stream
 
 MODE = os.environ.get('FGREG_GEMM', 'bf16x6')
 
@@ -106,10 +106,12 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act=ACT_NONE, residual=N
         m = x.shape[0]
         if out is None:
             out = torch.empty((m, n), dtype=torch.float32, device=x.device)
+        t0 = _begin('gemm')
         _lib.check(_lib.load().fgr_gemm_bf16x6(
             _ptr(x), x.stride(0), _ptr(sw.img), _ptr(out), out.stride(0), _ptr(bias),
             _ptr(residual), residual.stride(0) if residual is not None else 0, m, n, k, act,
             _stream()), 'fgr_gemm_bf16x6')
+        _end('gemm', t0, 2 * m * n * k)
         return out
     ok = (MODE == 'bf16x3' and k % 4 == 0 and x.stride(1) == 1
           and x.stride(0) % 4 == 0 and x.data_ptr() % 16 == 0)
