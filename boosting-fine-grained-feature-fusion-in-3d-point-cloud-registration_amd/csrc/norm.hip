@@ -128,6 +128,138 @@ __global__ void __launch_bounds__(64 * kInW) instnorm_chunk_kernel(InArgs a) {
     }
 }
 
+// Segmented instance norm, one block per (16 channels, segment) for segments of up to
+// kSegRows rows: 16 waves x 4 row-lanes x 16 channel-lanes, every value held in registers
+// (x read from HBM once). 16 channels per block give C/16 x n_seg blocks -- 4x the blocks
+// of the 64-channel chunk kernel, which left most CUs idle at 16 clouds x 256 channels.
+constexpr int kSegRpl = 16;                        // rows per lane
+constexpr int kSegRows = kSegRpl * 4 * kInW;       // 1024
+
+__device__ __forceinline__ float xg16_32_sum(float v) {   // sum over lanes l, l^16, l^32, l^48
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    return v;
+}
+
+__global__ void __launch_bounds__(64 * kInW) instnorm_seg16_kernel(InArgs a) {
+    __shared__ float red[kInW][16];
+    const int seg = blockIdx.y;
+    const int wv = threadIdx.x / 64, lane = threadIdx.x % 64;
+    const int rl = lane >> 4, cc = lane & 15;
+    const int ch = blockIdx.x * 16 + cc;
+    const bool cok = ch < a.c;
+    const int64_t b = a.seg_off[seg], e = a.seg_off[seg + 1];
+    const int nrow = (int)(e - b);
+    if (nrow <= 0) return;
+    const int r0 = wv * 4 + rl;                          // this lane's first row
+    float v[kSegRpl];
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < kSegRpl; ++j) {
+        const int rr = r0 + 64 * j;
+        float t = 0.f;
+        if (rr < nrow && cok) {
+            t = a.x[(b + rr) * a.c + ch];
+            if (a.row_div) t = t / a.row_div[b + rr];
+        }
+        v[j] = t;
+        s += t;
+    }
+    s = xg16_32_sum(s);
+    if (rl == 0) red[wv][cc] = s;
+    __syncthreads();
+    float tot = 0.f;
+#pragma unroll
+    for (int w = 0; w < kInW; ++w) tot += red[w][cc];
+    const float cnt = (float)nrow;
+    const float mean = tot / cnt;
+    __syncthreads();
+    float sq = 0.f;
+#pragma unroll
+    for (int j = 0; j < kSegRpl; ++j) {
+        const float d = (r0 + 64 * j < nrow) ? v[j] - mean : 0.f;
+        sq += d * d;
+    }
+    sq = xg16_32_sum(sq);
+    if (rl == 0) red[wv][cc] = sq;
+    __syncthreads();
+    float m2 = 0.f;
+#pragma unroll
+    for (int w = 0; w < kInW; ++w) m2 += red[w][cc];
+    const float rstd = 1.0f / sqrtf(m2 / cnt + a.eps);
+    if (!cok) return;
+#pragma unroll
+    for (int j = 0; j < kSegRpl; ++j) {
+        const int rr = r0 + 64 * j;
+        if (rr < nrow) {
+            const int64_t o = (b + rr) * a.c + ch;
+            float y = act_fn((v[j] - mean) * rstd, a.act);
+            if (a.residual) y = act_fn(y + a.residual[o], a.post_act);
+            a.out[o] = y;
+        }
+    }
+}
+
+// LayerNorm, 16 lanes per row (4 rows per wave, 16 per block), d % 64 == 0 and
+// d <= 64 * V: each lane holds V/4 float4 (16-B loads / stores), row reductions on DPP
+// within a 16-lane row (no LDS). `pre_bias` as in layernorm_kernel below.
+template <int V>
+__global__ void __launch_bounds__(256)
+layernorm16_kernel(float* __restrict__ x, int64_t n, int d, const float* __restrict__ g,
+                   const float* __restrict__ bta, float eps, const float* __restrict__ add,
+                   const float* __restrict__ pre_bias, float* __restrict__ out) {
+    const int64_t r = (int64_t)blockIdx.x * 16 + threadIdx.x / 16;
+    const int l = threadIdx.x & 15;
+    const bool ok = r < n;                               // keep all lanes for the DPP sums
+    const int64_t rr = ok ? r : n - 1;
+    float4 v[V / 4];
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < V / 4; ++j) {
+        const int col = 4 * (l + 16 * j);
+        float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (col < d) {
+            t = *reinterpret_cast<const float4*>(x + rr * d + col);
+            if (pre_bias) {
+                const float4 pb = *reinterpret_cast<const float4*>(pre_bias + col);
+                t.x += pb.x; t.y += pb.y; t.z += pb.z; t.w += pb.w;
+                if (ok) *reinterpret_cast<float4*>(x + rr * d + col) = t;
+            }
+        }
+        v[j] = t;
+        s += (t.x + t.y) + (t.z + t.w);
+    }
+    const float mean = row16_sum(s) / (float)d;
+    float sq = 0.f;
+#pragma unroll
+    for (int j = 0; j < V / 4; ++j) {
+        if (4 * (l + 16 * j) < d) {
+            const float a0 = v[j].x - mean, a1 = v[j].y - mean, a2 = v[j].z - mean, a3 = v[j].w - mean;
+            sq += (a0 * a0 + a1 * a1) + (a2 * a2 + a3 * a3);
+        }
+    }
+    const float rstd = 1.0f / sqrtf(row16_sum(sq) / (float)d + eps);
+    if (!ok) return;
+#pragma unroll
+    for (int j = 0; j < V / 4; ++j) {
+        const int col = 4 * (l + 16 * j);
+        if (col < d) {
+            const float4 gg = *reinterpret_cast<const float4*>(g + col);
+            const float4 bb = *reinterpret_cast<const float4*>(bta + col);
+            float4 y;
+            y.x = (v[j].x - mean) * rstd * gg.x + bb.x;
+            y.y = (v[j].y - mean) * rstd * gg.y + bb.y;
+            y.z = (v[j].z - mean) * rstd * gg.z + bb.z;
+            y.w = (v[j].w - mean) * rstd * gg.w + bb.w;
+            if (add) {
+                const float4 ad = *reinterpret_cast<const float4*>(add + r * d + col);
+                y.x += ad.x; y.y += ad.y; y.z += ad.z; y.w += ad.w;
+            }
+            *reinterpret_cast<float4*>(out + r * d + col) = y;
+        }
+    }
+}
+
 // One wave per row; d <= 64 * 16.
 // `pre_bias` (optional): x[r] += pre_bias is applied first and written back to x (the
 // pending Linear bias of the residual branch that produced x), then normalised.
@@ -220,7 +352,10 @@ extern "C" int fgr_instnorm(const float* x, int64_t n, int32_t c, const int64_t*
     InArgs a{x, c, seg_off, row_div, eps, act, residual, post_act, out, (float*)ws, (int)chunks};
     hipStream_t st = as_stream(stream);
     const unsigned cx = (unsigned)ceil_div(c, 64);
-    if (chunks == 1) {
+    if (max_seg_len <= kSegRows) {
+        hipLaunchKernelGGL(instnorm_seg16_kernel, dim3((unsigned)ceil_div(c, 16), n_seg, 1),
+                           dim3(64 * kInW), 0, st, a);
+    } else if (chunks == 1) {
         hipLaunchKernelGGL(instnorm_chunk_kernel<0>, dim3(cx, n_seg, 1), dim3(64 * kInW), 0, st, a);
     } else {
         const size_t need = (size_t)n_seg * chunks * 3 * c * sizeof(float);
@@ -244,7 +379,19 @@ extern "C" int fgr_layernorm(float* x, int64_t n, int32_t d, const float* gamma,
     if (n == 0) return FGR_OK;
     dim3 grid((unsigned)ceil_div(n, 4));
     hipStream_t st = as_stream(stream);
-    if (d <= 64)
+    const bool vec = d % 64 == 0 && d <= 1024 &&
+                     ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(out) |
+                       reinterpret_cast<uintptr_t>(gamma) | reinterpret_cast<uintptr_t>(beta) |
+                       reinterpret_cast<uintptr_t>(add) | reinterpret_cast<uintptr_t>(pre_bias)) & 15) == 0;
+    if (vec) {
+        const dim3 g16((unsigned)ceil_div(n, 16));
+        if (d <= 256)
+            hipLaunchKernelGGL(layernorm16_kernel<16>, g16, dim3(256), 0, st, x, n, d, gamma, beta, eps, add, pre_bias, out);
+        else if (d <= 512)
+            hipLaunchKernelGGL(layernorm16_kernel<32>, g16, dim3(256), 0, st, x, n, d, gamma, beta, eps, add, pre_bias, out);
+        else
+            hipLaunchKernelGGL(layernorm16_kernel<64>, g16, dim3(256), 0, st, x, n, d, gamma, beta, eps, add, pre_bias, out);
+    } else if (d <= 64)
         hipLaunchKernelGGL(layernorm_kernel<1>, grid, dim3(256), 0, st, x, n, d, gamma, beta, eps, add, pre_bias, out);
     else if (d <= 256)
         hipLaunchKernelGGL(layernorm_kernel<4>, grid, dim3(256), 0, st, x, n, d, gamma, beta, eps, add, pre_bias, out);

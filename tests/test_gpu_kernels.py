@@ -73,7 +73,7 @@ def test_instnorm_vs_reference(gpu):
     assert rel_err(out, g['out']) < TOL
 
 
-@pytest.mark.parametrize('lens', [[700, 1, 33, 512], [3000, 5, 1500, 1024, 1025]])
+@pytest.mark.parametrize('lens', [[700, 1, 33, 512], [1024, 1000, 2], [3000, 5, 1500, 1024, 1025]])
 def test_instnorm_fusions_vs_torch(gpu, lens):
     """Register path (segments <= 1024 rows) and the two-launch chunked path."""
     import fgreg.ops as ops
@@ -107,14 +107,20 @@ def test_sine_pos_embed_vs_reference(gpu, d):
 def test_layernorm_vs_torch(gpu):
     import fgreg.ops as ops
     rng = np.random.default_rng(1)
-    for d in (32, 256, 512):
+    for d in (32, 96, 256, 512, 1024):
         x = torch.from_numpy(rng.normal(1, 2, (333, d)).astype(np.float32))
         w = torch.from_numpy(rng.normal(1, 0.1, d).astype(np.float32))
         b = torch.from_numpy(rng.normal(0, 0.1, d).astype(np.float32))
         a = torch.from_numpy(rng.normal(size=(333, d)).astype(np.float32))
+        pb = torch.from_numpy(rng.normal(size=d).astype(np.float32))
         ref = torch.nn.functional.layer_norm(x, (d,), w, b, 1e-5) + a
         out = ops.layernorm(x.to(gpu), w.to(gpu), b.to(gpu), 1e-5, add=a.to(gpu))
         assert rel_err(out, ref) < TOL
+        # pending residual bias: x += pre_bias in place, then normalised
+        X = x.to(gpu)
+        out = ops.layernorm(X, w.to(gpu), b.to(gpu), 1e-5, pre_bias=pb.to(gpu))
+        ref = torch.nn.functional.layer_norm(x + pb, (d,), w, b, 1e-5)
+        assert rel_err(out, ref) < TOL and rel_err(X, x + pb) < 1e-7
 
 
 def _attn_ref(q, k, v, qlens, klens, kv_seg, nhead):

@@ -1,6 +1,8 @@
 #!/bin/bash
 # One GPU session: parity tests, bench, kernel-trace profile, PMC traffic passes of the gather.
 # usage (on the GPU box, from the repo root): bash tools/gpu_round.sh <tag>
+# The profiled bench runs 3 warmup + 1 counting + 10 timed + 10 GEMM-instrumented forwards:
+# per-step kernel stats = python tools/kernel_stats.py <kernel_stats.csv> 24
 set -o pipefail
 tag=${1:-run}
 export TMPDIR=/tmp
