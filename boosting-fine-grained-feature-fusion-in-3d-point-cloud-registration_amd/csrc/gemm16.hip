@@ -1,0 +1,378 @@
+// fp32-accurate GEMM on the fp16 matrix cores with scaled two-term splits ("f16x3").
+//
+//   C[M, N] = act(A[M, K] . W[N, K]^T + bias[N] (+ R[M, N]))
+//
+// Precision design. gfx950 has no xf32; its fp32 MFMA runs at 1/16 of the fp16/bf16 rate.
+// An fp16 term carries 11 significant bits, so a two-term split x = h + m (h = f16(x),
+// m = f16(x - h), both round-to-nearest) represents x to 2^-22 relative -- PROVIDED both
+// terms stay in fp16's normal range. That is what the scales are for:
+//   * W rows (output channels n) are scaled once, by a power of two, so that the row's
+//     max |w| lies in [2^14, 2^15) (fgr_split_weights_h3, cached with the weight);
+//   * A rows (activations) are scaled in flight by a power of two per row, chosen from the
+//     first non-zero 32-wide k chunk so its max lands in [2^7, 2^8), and lowered (with the
+//     row's partial sums rescaled by the same exact power of two) only when a later chunk
+//     would pass 2^15 -- fp16 overflow is impossible and the common path costs one compare.
+// Per 16x16x32 step the three significant products hh, hm, mh accumulate in fp32 on
+// v_mfma_f32_16x16x32_f16; the dropped mm term is <= 2^-22 relative. Net: <= ~3 * 2^-22
+// per product (below fp32 accumulation's own rounding for K >= 16), at 3 MFMAs per step
+// where the bf16x6 split needs 6 -- half the matrix-core work, 2/3 of the operand bytes.
+//
+// Orientation ("swapped"): the MFMA computes C^T tiles, W fragments as the A operand and
+// activation fragments as the B operand, so every lane's four accumulator values belong to
+// ONE activation row (its column c): the per-row scale is lane-local and the epilogue
+// stores 16-B float4s of C.
+//
+// Tiling: 256-thread blocks, 2 x 2 waves over (n, m), block tile BN x BM x 32. W images are
+// flat-copied into LDS; A (fp32) is split in registers while staging into a
+// [term][g][row ^ 2g] LDS image (conflict-free 16-B stores and ds_read_b128 fragment
+// loads); the per-row scale exponents go through a small LDS array. Block ids are
+// remapped so the blocks sharing an A row panel run on one XCD (its L2 keeps the panel).
+// 16x16x32 f16 lane maps (lane l, g = l >> 4, c = l & 15): A[i = c][k = 8g + e],
+// B[k = 8g + e][j = c], C[i = 4g + r][j = c].
+#include "common.h"
+
+namespace fgr {
+namespace {
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int SH_UNSET = 0x3fff;     // "no non-zero chunk seen yet" (partial sums are 0)
+
+struct GemmH3Args {
+    const float* A; int64_t lda;
+    const u32x4* W; int ksteps;       // image [panel][kstep][term 2][g 4][16] x 16 B
+    const float* wsc;                 // per n: 2^-e_n (inverse of the W row scale)
+    float* C; int64_t ldc;
+    const float* bias;
+    const float* R; int64_t ldr;
+    int M, N, K, act, vec_out;
+};
+
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
+// scale exponent for a chunk whose max |x| is cm: cm * 2^sh in [2^7, 2^8)
+__device__ __forceinline__ int chunk_shift(float cm) {
+    return min(8 - __builtin_amdgcn_frexp_expf(cm), 127);
+}
+
+template <int BM, int BN, bool KVEC>
+__global__ void __launch_bounds__(256) gemm_f16x3_kernel(GemmH3Args p) {
+    constexpr int TM = BM / 32, TN = BN / 32;          // 16x16 subtiles per wave (m, n)
+    constexpr int UA = BM * 4 / 256;                    // A units (8 k of one row) per thread
+    constexpr int UW = 8 * BN / 256;                    // W image units per thread
+    static_assert(UA >= 1 && UW >= 1, "tile");
+    __shared__ u32x4 a_lds[2 * 4 * BM];
+    __shared__ u32x4 w_lds[8 * BN];
+    __shared__ int sh_lds[BM];
+
+    // XCD-aware order: hardware dispatches block b to XCD b % 8; remap (bijectively) so that
+    // each XCD gets a contiguous range of tiles, tiles ordered n-fastest within a row panel.
+    const int nbm = (p.M + BM - 1) / BM, nbn = (p.N + BN - 1) / BN;
+    const int nwg = nbm * nbn;
+    int t = blockIdx.x;
+    {
+        const int q = nwg / 8, r = nwg % 8, x = t % 8, lo = t / 8;
+        t = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + lo;
+    }
+    const int bm = t / nbn, bn = t % nbn;
+    const int m0 = bm * BM, n0 = bn * BN;
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+    const int wn = (wv >> 1) * (BN / 2), wm = (wv & 1) * (BM / 2);
+    const int g = lane >> 4, c = lane & 15;
+    const int npanel = (p.N + 15) / 16;
+
+    const float* arow[UA];
+    int akk[UA], sh[UA];
+#pragma unroll
+    for (int j = 0; j < UA; ++j) {
+        const int u = tid + 256 * j;
+        arow[j] = p.A + (int64_t)min(m0 + (u >> 2), p.M - 1) * p.lda;
+        akk[j] = 8 * (u & 3);
+        sh[j] = SH_UNSET;
+    }
+    const u32x4* wsrc[UW];
+#pragma unroll
+    for (int j = 0; j < UW; ++j) {
+        const int v = tid + 256 * j;
+        const int panel = min(n0 / 16 + v / 128, npanel - 1);
+        wsrc[j] = p.W + (int64_t)panel * p.ksteps * 128 + v % 128;
+    }
+    float4 ar[UA][2];
+    u32x4 wr[UW];
+    auto load = [&](int s) {
+#pragma unroll
+        for (int j = 0; j < UA; ++j) {
+            const int k = s * 32 + akk[j];
+            if constexpr (KVEC) {
+                const float* src = arow[j] + min(k, p.K - 8);
+                const float4 x0 = *reinterpret_cast<const float4*>(src);
+                const float4 x1 = *reinterpret_cast<const float4*>(src + 4);
+                const bool ok = k < p.K;
+                ar[j][0] = ok ? x0 : make_float4(0.f, 0.f, 0.f, 0.f);
+                ar[j][1] = ok ? x1 : make_float4(0.f, 0.f, 0.f, 0.f);
+            } else {
+                float tt[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const float xv = arow[j][min(k + e, p.K - 1)];
+                    tt[e] = k + e < p.K ? xv : 0.f;
+                }
+                ar[j][0] = make_float4(tt[0], tt[1], tt[2], tt[3]);
+                ar[j][1] = make_float4(tt[4], tt[5], tt[6], tt[7]);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < UW; ++j) wr[j] = wsrc[j][(int64_t)s * 128];
+    };
+    auto store = [&]() {
+#pragma unroll
+        for (int j = 0; j < UA; ++j) {
+            const int u = tid + 256 * j;
+            const int row = u >> 2, gg = u & 3;
+            const float x[8] = {ar[j][0].x, ar[j][0].y, ar[j][0].z, ar[j][0].w,
+                                ar[j][1].x, ar[j][1].y, ar[j][1].z, ar[j][1].w};
+            float cm = fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3])));
+            cm = fmaxf(cm, fmaxf(fmaxf(fabsf(x[4]), fabsf(x[5])), fmaxf(fabsf(x[6]), fabsf(x[7]))));
+            cm = fmaxf(cm, dppf<0xB1>(cm));              // the row's 4 lanes: quad xor 1, xor 2
+            cm = fmaxf(cm, dppf<0x4E>(cm));
+            if (cm > 0.f && __builtin_amdgcn_frexp_expf(cm) + sh[j] > 15) sh[j] = chunk_shift(cm);
+            const float s = __builtin_ldexpf(1.f, sh[j] == SH_UNSET ? 0 : sh[j]);
+            f16x8 th, tm;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float xs = x[e] * s;
+                const _Float16 h = (_Float16)xs;
+                th[e] = h;
+                tm[e] = (_Float16)(xs - (float)h);
+            }
+            const int r = row ^ (2 * gg);
+            a_lds[(0 * 4 + gg) * BM + r] = __builtin_bit_cast(u32x4, th);
+            a_lds[(1 * 4 + gg) * BM + r] = __builtin_bit_cast(u32x4, tm);
+            if (gg == 0) sh_lds[row] = sh[j];
+        }
+#pragma unroll
+        for (int j = 0; j < UW; ++j) w_lds[tid + 256 * j] = wr[j];
+    };
+
+    f32x4 acc[TN][TM];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    int shr[TM];                                       // scale exponent of this lane's rows
+#pragma unroll
+    for (int i = 0; i < TM; ++i) shr[i] = SH_UNSET;
+
+    const int nk = (p.K + 31) / 32;
+    load(0);
+    for (int s = 0; s < nk; ++s) {
+        __syncthreads();
+        store();
+        __syncthreads();
+        if (s + 1 < nk) load(s + 1);
+        // rows whose scale was lowered this step: rescale their partial sums (exact, rare)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const int shv = sh_lds[wm + 16 * i + c];
+            if (__builtin_amdgcn_ballot_w64(shv != shr[i])) {
+                const float f = (shr[i] == SH_UNSET || shv == shr[i])
+                                    ? 1.f : __builtin_ldexpf(1.f, shv - shr[i]);
+#pragma unroll
+                for (int j = 0; j < TN; ++j) acc[j][i] *= f;
+                shr[i] = shv;
+            }
+        }
+        f16x8 af[TM][2];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const int r = (wm + 16 * i + c) ^ (2 * g);
+            af[i][0] = __builtin_bit_cast(f16x8, a_lds[(0 * 4 + g) * BM + r]);
+            af[i][1] = __builtin_bit_cast(f16x8, a_lds[(1 * 4 + g) * BM + r]);
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int pp = (wn + 16 * j) >> 4;
+            const f16x8 wh = __builtin_bit_cast(f16x8, w_lds[pp * 128 + (0 * 4 + g) * 16 + c]);
+            const f16x8 wl = __builtin_bit_cast(f16x8, w_lds[pp * 128 + (1 * 4 + g) * 16 + c]);
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, af[i][0], acc[j][i], 0, 0, 0);
+                acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, af[i][1], acc[j][i], 0, 0, 0);
+                acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, af[i][0], acc[j][i], 0, 0, 0);
+            }
+        }
+    }
+
+    // epilogue: lane holds C[m = m0 + wm + 16i + c][n = n0 + wn + 16j + 4g + r], r = 0..3
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        const int m = m0 + wm + 16 * i + c;
+        if (m >= p.M) continue;
+        const float rs = __builtin_ldexpf(1.f, -shr[i]);     // 0 for an all-zero row
+        float* crow = p.C + (int64_t)m * p.ldc;
+        const float* rrow = p.R ? p.R + (int64_t)m * p.ldr : nullptr;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int n = n0 + wn + 16 * j + 4 * g;
+            if (n >= p.N) continue;
+            const float4 ws = *reinterpret_cast<const float4*>(p.wsc + n);   // padded to 16
+            float y[4] = {acc[j][i][0] * rs * ws.x, acc[j][i][1] * rs * ws.y,
+                          acc[j][i][2] * rs * ws.z, acc[j][i][3] * rs * ws.w};
+            if (p.vec_out && n + 3 < p.N) {
+                if (p.bias) {
+                    const float4 b = *reinterpret_cast<const float4*>(p.bias + n);
+                    y[0] += b.x; y[1] += b.y; y[2] += b.z; y[3] += b.w;
+                }
+                if (rrow) {
+                    const float4 rv = *reinterpret_cast<const float4*>(rrow + n);
+                    y[0] += rv.x; y[1] += rv.y; y[2] += rv.z; y[3] += rv.w;
+                }
+                if (p.act == FGR_ACT_RELU) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) y[e] = fmaxf(y[e], 0.f);
+                }
+                *reinterpret_cast<float4*>(crow + n) = make_float4(y[0], y[1], y[2], y[3]);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    if (n + e >= p.N) break;
+                    float v = y[e];
+                    if (p.bias) v += p.bias[n + e];
+                    if (rrow) v += rrow[n + e];
+                    if (p.act == FGR_ACT_RELU) v = fmaxf(v, 0.f);
+                    crow[n + e] = v;
+                }
+            }
+        }
+    }
+}
+
+// Row max |w| of W (n x k, element (i, j) at w[i * sn + j * sk]) -> wsc[i] = 2^-e_i with
+// e_i the row scale exponent (max * 2^e_i in [2^14, 2^15)); one wave per row, rows padded
+// to a multiple of 16 get 0.
+__global__ void weight_scale_kernel(const float* __restrict__ w, int n, int k, int64_t sn,
+                                    int64_t sk, int npad, float* __restrict__ wsc) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (row >= npad) return;
+    float mx = 0.f;
+    if (row < n)
+        for (int j = lane; j < k; j += 64) mx = fmaxf(mx, fabsf(w[(int64_t)row * sn + j * sk]));
+    mx = wave_max(mx);
+    if (lane == 0) {
+        const int e = mx > 0.f ? min(15 - __builtin_amdgcn_frexp_expf(mx), 127) : 0;
+        wsc[row] = row < n ? __builtin_ldexpf(1.f, -e) : 0.f;
+    }
+}
+
+// W -> f16x3 image [panel][kstep][term 2][g 4][16 rows] x 16 B (8 k each), rows scaled by
+// 1 / wsc[row] (exact powers of two), zero-padded past n and k.
+__global__ void split_weights_h3_kernel(const float* __restrict__ w, int n, int k, int64_t sn,
+                                        int64_t sk, int ksteps, const float* __restrict__ wsc,
+                                        u32x4* __restrict__ img) {
+    const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t total = (int64_t)((n + 15) / 16) * ksteps * 128;
+    if (u >= total) return;
+    const int i = (int)(u % 16);
+    const int g = (int)((u / 16) % 4);
+    const int t = (int)((u / 64) % 2);
+    const int64_t ps = u / 128;
+    const int s = (int)(ps % ksteps);
+    const int panel = (int)(ps / ksteps);
+    const int row = panel * 16 + i;
+    const float sc = row < n ? 1.f / wsc[row] : 0.f;      // exact: a power of two
+    f16x8 out;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const int col = s * 32 + 8 * g + e;
+        const float x = (row < n && col < k) ? w[(int64_t)row * sn + (int64_t)col * sk] * sc : 0.f;
+        const _Float16 h = (_Float16)x;
+        out[e] = t == 0 ? h : (_Float16)(x - (float)h);
+    }
+    img[u] = __builtin_bit_cast(u32x4, out);
+}
+
+template <int BM, int BN>
+void launch_h3(const GemmH3Args& a, hipStream_t st) {
+    const int nbm = (a.M + BM - 1) / BM, nbn = (a.N + BN - 1) / BN;
+    if (a.K % 8 == 0)
+        hipLaunchKernelGGL((gemm_f16x3_kernel<BM, BN, true>), dim3((unsigned)(nbm * nbn)),
+                           dim3(256), 0, st, a);
+    else
+        hipLaunchKernelGGL((gemm_f16x3_kernel<BM, BN, false>), dim3((unsigned)(nbm * nbn)),
+                           dim3(256), 0, st, a);
+}
+
+size_t image_bytes_h3(int n, int k) {
+    return (size_t)((n + 15) / 16) * ((k + 31) / 32) * 128 * 16;
+}
+
+}  // namespace
+}  // namespace fgr
+
+using namespace fgr;
+
+extern "C" int fgr_split_weights_h3_bytes(int32_t n, int32_t k, size_t* bytes) {
+    FGR_REQUIRE(bytes && n > 0 && k > 0, "fgr_split_weights_h3_bytes: bad arguments");
+    *bytes = image_bytes_h3(n, k) + (size_t)((n + 15) / 16) * 16 * sizeof(float);
+    return FGR_OK;
+}
+
+extern "C" int fgr_split_weights_h3(const float* w, int32_t n, int32_t k, int64_t stride_n,
+                                    int64_t stride_k, void* img, void* stream) {
+    FGR_REQUIRE(w && img && n > 0 && k > 0, "fgr_split_weights_h3: bad arguments");
+    FGR_REQUIRE((reinterpret_cast<uintptr_t>(img) & 15) == 0,
+                "fgr_split_weights_h3: image not 16-B aligned");
+    const int ksteps = (k + 31) / 32;
+    const int npad = (n + 15) / 16 * 16;
+    float* wsc = reinterpret_cast<float*>(static_cast<char*>(img) + image_bytes_h3(n, k));
+    hipStream_t st = as_stream(stream);
+    hipLaunchKernelGGL(weight_scale_kernel, dim3((unsigned)ceil_div(npad, 4)), dim3(256), 0, st, w,
+                       n, k, stride_n, stride_k, npad, wsc);
+    FGR_CHECK_LAUNCH("weight_scale_kernel");
+    const int64_t total = (int64_t)(npad / 16) * ksteps * 128;
+    hipLaunchKernelGGL(split_weights_h3_kernel, dim3((unsigned)ceil_div(total, 256)), dim3(256), 0,
+                       st, w, n, k, stride_n, stride_k, ksteps, wsc, (u32x4*)img);
+    FGR_CHECK_LAUNCH("split_weights_h3_kernel");
+    return FGR_OK;
+}
+
+extern "C" int fgr_gemm_f16x3(const float* a, int64_t lda, const void* w_img, float* c,
+                              int64_t ldc, const float* bias, const float* r, int64_t ldr,
+                              int32_t m, int32_t n, int32_t k, int32_t act, void* stream) {
+    FGR_REQUIRE(a && w_img && c && m >= 0 && n > 0 && k > 0 && lda >= k && ldc >= n &&
+                    (!r || ldr >= n),
+                "fgr_gemm_f16x3: bad arguments (m %d n %d k %d lda %lld)", m, n, k,
+                (long long)lda);
+    const bool vec = (k % 8 == 0) && (lda % 4 == 0) && ((reinterpret_cast<uintptr_t>(a) & 15) == 0);
+    FGR_REQUIRE(vec || (k % 8 != 0), "fgr_gemm_f16x3: A must be 16-B aligned with lda %% 4 == 0");
+    FGR_REQUIRE((reinterpret_cast<uintptr_t>(w_img) & 15) == 0,
+                "fgr_gemm_f16x3: image not 16-B aligned");
+    if (m == 0) return FGR_OK;
+    const bool vo = (ldc % 4 == 0) && ((reinterpret_cast<uintptr_t>(c) & 15) == 0) &&
+                    (!bias || (reinterpret_cast<uintptr_t>(bias) & 15) == 0) &&
+                    (!r || ((ldr % 4 == 0) && (reinterpret_cast<uintptr_t>(r) & 15) == 0));
+    const float* wsc = reinterpret_cast<const float*>(static_cast<const char*>(w_img) +
+                                                      image_bytes_h3(n, k));
+    GemmH3Args g{a, lda, (const u32x4*)w_img, (k + 31) / 32, wsc, c, ldc, bias, r, ldr,
+                 m, n, k, act, vo ? 1 : 0};
+    hipStream_t st = as_stream(stream);
+    // tile BM x BN (activation rows x output channels); FGR_GEMM16_TILE overrides it for
+    // tuning (a = 128x128, b = 64x128, c = 64x64, d = 128x64)
+    const char* force = getenv("FGR_GEMM16_TILE");
+    const char cfg = (force && force[0]) ? force[0] : (n >= 512 && n % 256 == 0) ? 'b' : 'c';
+    if (cfg == 'a')
+        launch_h3<128, 128>(g, st);
+    else if (cfg == 'b')
+        launch_h3<64, 128>(g, st);
+    else if (cfg == 'd')
+        launch_h3<128, 64>(g, st);
+    else
+        launch_h3<64, 64>(g, st);
+    FGR_CHECK_LAUNCH("gemm_f16x3_kernel");
+    return FGR_OK;
+}

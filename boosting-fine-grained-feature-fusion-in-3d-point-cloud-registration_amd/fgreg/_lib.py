@@ -47,6 +47,9 @@ SIGNATURES = {
     'fgr_split_weights3_bytes': [_i32, _i32, ctypes.POINTER(_sz)],
     'fgr_split_weights3': [_vp, _i32, _i32, _i64, _i64, _vp, _vp],
     'fgr_gemm_bf16x6': [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _vp],
+    'fgr_split_weights_h3_bytes': [_i32, _i32, ctypes.POINTER(_sz)],
+    'fgr_split_weights_h3': [_vp, _i32, _i32, _i64, _i64, _vp, _vp],
+    'fgr_gemm_f16x3': [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _vp],
     'fgr_procrustes': [_vp, _vp, _vp, _i64, _i64, _f32, _vp, _vp],
     'fgr_pair_pose': [_vp, _vp, _vp, _i64, _vp, _i32, _i32, _f32, _vp, _vp],
 }

@@ -279,7 +279,7 @@ class my_Bottle2neck(nn.Module):  # noqa: N801 -- reference name (res2net.py:84)
             # one launch for the whole hierarchy + the [.. | x] concat (fgr_res2net_chain)
             cat_in = torch.empty((x.shape[0], w * self.scale + x.shape[1]), dtype=x.dtype,
                                  device=x.device)
-            if lin.MODE == 'bf16x6':
+            if lin.MODE in ('bf16x6', 'f16x3'):
                 ops.res2net_chain(out, w, self.scale, chain[2], chain[1], x, cat_in, split6=True)
             else:
                 ops.res2net_chain(out, w, self.scale, chain[0], chain[1], x, cat_in)

@@ -1,7 +1,10 @@
 """Dense layers of the forward (every Linear / KPConv-weight product goes through
-``linear()``) on the GPU, in one of three precision modes (``FGREG_GEMM`` or ``set_mode``):
+``linear()``) on the GPU, in one of four precision modes (``FGREG_GEMM`` or ``set_mode``):
 
-* ``bf16x6`` (default): fgr_gemm_bf16x6, the fp32-accurate split-bf16 MFMA GEMM (operands
+* ``f16x3`` (default): fgr_gemm_f16x3, the fp32-accurate scaled split-fp16 MFMA GEMM (operands
+  scaled by per-row powers of two and split into two fp16 terms, three term products per
+  step: <= ~3 * 2^-22 relative per product) -- half the matrix-core work of bf16x6.
+* ``bf16x6``: fgr_gemm_bf16x6, the fp32-accurate split-bf16 MFMA GEMM (operands
   split exactly into three bf16 terms, six term products per step: ~2^-27 relative
   residual, below fp32's own rounding). Meets the 1e-4 parity bar on every fixture.
 * ``fp32``: PyTorch's fp32 GEMM (hipBLASLt, fp32 MFMA) -- the A/B baseline.
@@ -17,12 +20,12 @@ import torch
 from . import _lib
 from .ops import ACT_NONE, ACT_RELU, _begin, _dev, _end, _ptr, _stream
 
-MODE = os.environ.get('FGREG_GEMM', 'bf16x6')
+MODE = os.environ.get('FGREG_GEMM', 'f16x3')
 
 
 def set_mode(mode):
     global MODE
-    assert mode in ('fp32', 'bf16x3', 'bf16x6')
+    assert mode in ('fp32', 'bf16x3', 'bf16x6', 'f16x3')
     MODE = mode
 
 
@@ -57,6 +60,21 @@ class SplitWeight3:
         self.src, self.version, self.ptr = src, src._version, src.data_ptr()
 
 
+class SplitWeightH3:
+    """f16x3 image of W (n, k) + per-row scales (fgr_split_weights_h3)."""
+    __slots__ = ('img', 'n', 'k', 'src', 'version', 'ptr')
+
+    def __init__(self, w2: torch.Tensor, n, k, sn, sk, src: torch.Tensor):
+        L = _lib.load()
+        nb = _lib._sz(0)
+        _lib.check(L.fgr_split_weights_h3_bytes(n, k, nb), 'fgr_split_weights_h3_bytes')
+        self.img = torch.empty(nb.value, dtype=torch.uint8, device=w2.device)
+        _lib.check(L.fgr_split_weights_h3(_ptr(w2), n, k, sn, sk, _ptr(self.img), _stream()),
+                   'fgr_split_weights_h3')
+        self.n, self.k = n, k
+        self.src, self.version, self.ptr = src, src._version, src.data_ptr()
+
+
 _CACHE = {}
 
 
@@ -65,16 +83,18 @@ def _valid(ent, w):
             and ent.ptr == w.data_ptr())            # .to() / load_state_dict swap .data
 
 
-def split_weight3(w: torch.Tensor, transpose=False, tag=None) -> SplitWeight3:
-    ck = (id(w), transpose, tag, 3)
+def split_weight3(w: torch.Tensor, transpose=False, tag=None, kind=3):
+    """Cached split image of w (kind 3: bf16x6, kind 'h3': f16x3)."""
+    ck = (id(w), transpose, tag, kind)
     ent = _CACHE.get(ck)
     if not _valid(ent, w):
+        cls = SplitWeight3 if kind == 3 else SplitWeightH3
         if transpose:                    # (K, Cin, Cout) as W[n = cout][k = K*Cin + cin]
             w2 = w.reshape(-1, w.shape[-1]).contiguous()
-            ent = SplitWeight3(w2, w2.shape[1], w2.shape[0], 1, w2.shape[1], w)
+            ent = cls(w2, w2.shape[1], w2.shape[0], 1, w2.shape[1], w)
         else:
             w2 = w.contiguous()
-            ent = SplitWeight3(w2, w2.shape[0], w2.shape[1], w2.shape[1], 1, w)
+            ent = cls(w2, w2.shape[0], w2.shape[1], w2.shape[1], 1, w)
         _CACHE[ck] = ent
     return ent
 
@@ -100,17 +120,22 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act=ACT_NONE, residual=N
         _dev(x)
     if residual is not None:
         assert residual.shape == (x.shape[0], n) and residual.stride(1) == 1
-    if MODE == 'bf16x6' and x.stride(1) == 1 and (k % 8 != 0 or (x.stride(0) % 4 == 0
-                                                             and x.data_ptr() % 16 == 0)):
-        sw = split_weight3(w, transpose, tag)
+    if MODE in ('bf16x6', 'f16x3'):
+        if not (x.stride(1) == 1 and (k % 8 != 0 or (x.stride(0) % 4 == 0
+                                                     and x.data_ptr() % 16 == 0))):
+            x = x.contiguous()                 # the split kernels need 16-B aligned rows
+            if k % 8 == 0 and x.data_ptr() % 16 != 0:
+                x = x.clone()
+        h3 = MODE == 'f16x3'
+        sw = split_weight3(w, transpose, tag, 'h3' if h3 else 3)
         m = x.shape[0]
         if out is None:
             out = torch.empty((m, n), dtype=torch.float32, device=x.device)
+        fn = _lib.load().fgr_gemm_f16x3 if h3 else _lib.load().fgr_gemm_bf16x6
         t0 = _begin('gemm')
-        _lib.check(_lib.load().fgr_gemm_bf16x6(
-            _ptr(x), x.stride(0), _ptr(sw.img), _ptr(out), out.stride(0), _ptr(bias),
-            _ptr(residual), residual.stride(0) if residual is not None else 0, m, n, k, act,
-            _stream()), 'fgr_gemm_bf16x6')
+        _lib.check(fn(_ptr(x), x.stride(0), _ptr(sw.img), _ptr(out), out.stride(0), _ptr(bias),
+                      _ptr(residual), residual.stride(0) if residual is not None else 0, m, n, k,
+                      act, _stream()), 'fgr_gemm_' + MODE)
         _end('gemm', t0, 2 * m * n * k)
         return out
     ok = (MODE == 'bf16x3' and k % 4 == 0 and x.stride(1) == 1

@@ -172,6 +172,22 @@ int fgr_gemm_bf16x6(const float* a, int64_t lda, const void* w_img, float* c, in
                     const float* bias, const float* r, int64_t ldr, int32_t m, int32_t n,
                     int32_t k, int32_t act, void* stream);
 
+/* fp32-accurate scaled split-fp16 GEMM ("f16x3"), same contract as fgr_gemm_bf16x6:
+ *   C[m, n] = act(A[m, :] . W[n, :] + bias[n] (+ R[m, n]))
+ * W rows are scaled by powers of two (row max in [2^14, 2^15)) and A rows on the fly (per
+ * row, lowered only when a later k chunk would overflow fp16, with an exact rescale of the
+ * partial sums); each operand is then split into two fp16 terms (2^-22 relative) and the
+ * three significant term products accumulate in fp32 on v_mfma_f32_16x16x32_f16: <= ~3 *
+ * 2^-22 relative per product, half the matrix-core work of bf16x6. The image (built once by
+ * fgr_split_weights_h3, fgr_split_weights_h3_bytes() bytes, 16-B aligned) holds the split W
+ * in tile order followed by the per-row inverse scales. */
+int fgr_split_weights_h3_bytes(int32_t n, int32_t k, size_t* bytes);
+int fgr_split_weights_h3(const float* w, int32_t n, int32_t k, int64_t stride_n,
+                         int64_t stride_k, void* img, void* stream);
+int fgr_gemm_f16x3(const float* a, int64_t lda, const void* w_img, float* c, int64_t ldc,
+                   const float* bias, const float* r, int64_t ldr, int32_t m, int32_t n,
+                   int32_t k, int32_t act, void* stream);
+
 /* ---- attention ---------------------------------------------------------------------
  * Multi-head scaled-dot-product attention core of nn.MultiheadAttention
  * (transformers.py:95-96, 197-226) on packed, unpadded segments: query segment

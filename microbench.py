@@ -71,27 +71,19 @@ def gemm_shapes():
         if hasattr(m, 'linear'):
             m.linear = orig
     shapes = collections.Counter(calls)
-    tot = {'fp32': 0.0, 'bf16x3': 0.0, 'bf16x6': 0.0, 'lib_bf16_6K': 0.0}
+    modes = ('fp32', 'bf16x6', 'f16x3')
+    tot = {m: 0.0 for m in modes}
     flops = 0
     for (M, N, K, tp, res), cnt in sorted(shapes.items(), key=lambda kv: -kv[0][0] * kv[0][1] * kv[0][2] * kv[1]):
         x = torch.randn(M, K, device=dev)
         w = torch.randn(K, N, device=dev) if tp else torch.randn(N, K, device=dev)
         r = torch.randn(M, N, device=dev) if res else None
         line = f'M={M:6d} N={N:5d} K={K:5d} x{cnt:2d} '
-        for mode in ('fp32', 'bf16x3', 'bf16x6'):
+        for mode in modes:
             lin.set_mode(mode)
             us = timeit(lambda: orig(x, w, None, 0, r, tp), iters=20)
             tot[mode] += us * cnt
             line += f' {mode} {us:7.1f} us ({2 * M * N * K / us / 1e6:6.1f} TF)'
-        # ceiling reference: hipBLASLt bf16 GEMM with K' = 6K and fp32 output
-        try:
-            a6 = torch.randn(M, 6 * K, device=dev).bfloat16()
-            w6 = torch.randn(6 * K, N, device=dev).bfloat16()
-            us = timeit(lambda: torch.mm(a6, w6, out_dtype=torch.float32), iters=20)
-            tot['lib_bf16_6K'] += us * cnt
-            line += f' lib_bf16_6K {us:7.1f} us'
-        except Exception as e:  # noqa: BLE001
-            line += f' lib_bf16_6K n/a ({type(e).__name__})'
         flops += 2 * M * N * K * cnt
         print(line, flush=True)
     lin.set_mode('fp32')
@@ -99,12 +91,15 @@ def gemm_shapes():
           ', '.join(f'{k} {v / 1e3:.3f} ms' for k, v in tot.items()), flush=True)
 
 
-def gemm_tiles():
-    """bf16x6 GEMM per tile configuration (FGR_GEMM6_TILE a=128x128, b=128x64, c=64x64)."""
+def gemm_tiles(mode='bf16x6'):
+    """Split GEMM per tile configuration (bf16x6: FGR_GEMM6_TILE a=128x128, b=128x64,
+    c=64x64, d=64x128; f16x3: FGR_GEMM16_TILE a=128x128, b=64x128, c=64x64, d=128x64)."""
     import os
     import fgreg.linear as lin
     dev = torch.device('cuda:0')
-    lin.set_mode('bf16x6')
+    lin.set_mode(mode)
+    var = 'FGR_GEMM6_TILE' if mode == 'bf16x6' else 'FGR_GEMM16_TILE'
+    print(f'tiles {mode}', flush=True)
     shapes = [(9493, 1024, 2048), (9493, 768, 256), (9493, 256, 3840), (9493, 1024, 256),
               (9493, 256, 1024), (11472, 512, 1024), (9493, 1792, 256), (9493, 256, 256),
               (56958, 256, 256), (11472, 128, 1920), (9493, 512, 1024), (9493, 1024, 512),
@@ -113,12 +108,12 @@ def gemm_tiles():
         x = torch.randn(M, K, device=dev)
         w = torch.randn(N, K, device=dev)
         line = f'M={M:6d} N={N:5d} K={K:5d}'
-        for t in 'acd':
-            os.environ['FGR_GEMM6_TILE'] = t
+        for t in 'abcd':
+            os.environ[var] = t
             us = timeit(lambda: lin.linear(x, w), iters=20)
             line += f'  {t}: {us:7.1f} us ({2 * M * N * K / us / 1e6:6.1f} TF)'
         print(line, flush=True)
-    os.environ['FGR_GEMM6_TILE'] = ''
+    os.environ[var] = ''
 
 
 if __name__ == '__main__':
@@ -131,6 +126,8 @@ if __name__ == '__main__':
         gemm_shapes()
     if 'tiles' in which:
         gemm_tiles()
+    if 'tiles16' in which:
+        gemm_tiles('f16x3')
     if 'gemm1' in which:
         import fgreg.linear as lin
         lin.set_mode('bf16x6')

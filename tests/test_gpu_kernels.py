@@ -272,11 +272,12 @@ def _res2net_case(gpu, cin, cout, my_Bottle2neck, my_res2Net):
 
 @pytest.mark.parametrize('m,n,k', [(11472, 128, 1920), (9200, 1024, 2048), (1000, 3, 256),
                                    (333, 896, 128), (64, 256, 36), (5000, 768, 256)])
-@pytest.mark.parametrize('mode,tol', [('bf16x3', 1e-5), ('bf16x6', 2e-6)])
+@pytest.mark.parametrize('mode,tol', [('bf16x3', 1e-5), ('bf16x6', 2e-6), ('f16x3', 2e-6)])
 def test_gemm_split_vs_fp64(gpu, m, n, k, mode, tol):
     """Split-precision GEMMs vs fp64, bias / ReLU / residual epilogues, strided A, the
     KPConv weight layout. bf16x3 (two terms, 3 products) must be at ~1e-5; bf16x6 (three
-    terms, 6 products) at fp32 level and no worse than 2x torch's fp32 GEMM."""
+    terms, 6 products) and f16x3 (scaled fp16 pairs, 3 products) at fp32 level: no worse
+    than 2x (bf16x6) / 4x (f16x3) torch's fp32 GEMM."""
     from fgreg import linear as fl
     from fgreg import ops
     g = torch.Generator().manual_seed(m + n + k)
@@ -295,6 +296,8 @@ def test_gemm_split_vs_fp64(gpu, m, n, k, mode, tol):
         assert e < tol, (e, e32)
         if mode == 'bf16x6':
             assert e < 2 * e32 + 1e-7, (e, e32)
+        if mode == 'f16x3':
+            assert e < 4 * e32 + 1e-7, (e, e32)
         assert rel_err(fl.linear(X, W, Bb, act=ops.ACT_RELU), ref.clamp_min(0)) < tol
         assert rel_err(fl.linear(X, W, residual=R), ref - b.double() + r.double()) < tol
         # transposed (KPConv weight layout (K, Cin, Cout) used as (K*Cin, Cout))
@@ -302,3 +305,40 @@ def test_gemm_split_vs_fp64(gpu, m, n, k, mode, tol):
         assert rel_err(fl.linear(X, wt.to(gpu), Bb, transpose=True), ref) < tol
     finally:
         fl.set_mode(old)
+
+
+def test_gemm_f16x3_dynamic_range(gpu):
+    """f16x3 row scaling under adversarial magnitudes: rows at 1e-15 .. 1e15 (far outside
+    fp16's range), all-zero rows, rows whose first k chunks are zero, rows that grow by
+    2^40 along k (forces the in-flight rescale of partial sums) and a weight matrix with
+    rows at 1e-10 / 1e10 (outputs stay inside fp32's range). Every output row must match fp64 to 2e-6 of its own scale."""
+    from fgreg import linear as fl
+    g = torch.Generator().manual_seed(7)
+    m, n, k = 700, 96, 320
+    x = torch.randn(m, k, generator=g, dtype=torch.float64)
+    row_scale = torch.tensor([10.0 ** e for e in np.linspace(-15, 15, m)], dtype=torch.float64)
+    x *= row_scale[:, None]
+    x[5] = 0
+    x[17, :200] = 0                                  # first nonzero chunk late
+    ramp = torch.pow(2.0, torch.linspace(0, 40, k, dtype=torch.float64))
+    x[30:60] *= ramp                                 # growing rows: rescales mid-k
+    x[60:90] *= ramp.flip(0)                         # shrinking rows
+    w = torch.randn(n, k, generator=g, dtype=torch.float64) / math.sqrt(k)
+    w[3] *= 1e-10
+    w[4] *= 1e10
+    ref = x @ w.t()
+    X, W = x.float().to(gpu), w.float().to(gpu)
+    ref32 = X.double().cpu() @ W.double().cpu().t()     # fp32-rounded inputs, exact product
+    old = fl.MODE
+    try:
+        fl.set_mode('f16x3')
+        out = fl.linear(X, W).double().cpu()
+    finally:
+        fl.set_mode(old)
+    assert torch.isfinite(out).all()
+    assert (out[5] == 0).all()
+    # per-row normwise error vs the exact product of the fp32 inputs
+    den = (X.double().cpu().abs() @ W.double().cpu().abs().t()).clamp_min(1e-300)
+    err = ((out - ref32).abs() / den).max()
+    assert err < 2e-6, float(err)
+    del ref
