@@ -252,6 +252,228 @@ __global__ void __launch_bounds__(256) gemm_f16x3_kernel(GemmH3Args p) {
     }
 }
 
+// ------------------------------------------------------------------------------------
+// v2: KS k32-steps per staged tile (one row scale per KS*32 chunk, one barrier pair per
+// stage instead of per k32-step) and optionally double-buffered LDS (DBUF: one barrier per
+// stage; the next stage's split + LDS store overlaps other waves' MFMAs).
+// LDS images per stage: A [ks][term 2][g 4][BM rows ^ 2g], W [panel][ks][term 2][g 4][16].
+// ------------------------------------------------------------------------------------
+template <int BM, int BN, int KS, bool DBUF, bool KVEC>
+__global__ void __launch_bounds__(256) gemm_f16x3_v2(GemmH3Args p) {
+    constexpr int TM = BM / 32, TN = BN / 32;
+    constexpr int RU = 4 * KS;                          // units (8 k) of a row per stage
+    constexpr int UA = BM * RU / 256;                   // A units per thread per stage
+    constexpr int UW = 8 * BN * KS / 256;               // W units per thread per stage
+    constexpr int ASZ = 8 * BM * KS, WSZ = 8 * BN * KS; // 16-B units per stage
+    constexpr int NB = DBUF ? 2 : 1;
+    static_assert(UA >= 1 && UW >= 1 && (RU == 4 || RU == 8), "tile");
+    __shared__ u32x4 lds[NB * (ASZ + WSZ)];
+    __shared__ int sh_lds[NB][BM];
+
+    const int nbm = (p.M + BM - 1) / BM, nbn = (p.N + BN - 1) / BN;
+    const int nwg = nbm * nbn;
+    int t = blockIdx.x;
+    {
+        const int q = nwg / 8, r = nwg % 8, x = t % 8, lo = t / 8;
+        t = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + lo;
+    }
+    const int bm = t / nbn, bn = t % nbn;
+    const int m0 = bm * BM, n0 = bn * BN;
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+    const int wn = (wv >> 1) * (BN / 2), wm = (wv & 1) * (BM / 2);
+    const int g = lane >> 4, c = lane & 15;
+    const int npanel = (p.N + 15) / 16;
+
+    const float* arow[UA];
+    int akk[UA], sh[UA];
+#pragma unroll
+    for (int j = 0; j < UA; ++j) {
+        const int u = tid + 256 * j;
+        arow[j] = p.A + (int64_t)min(m0 + u / RU, p.M - 1) * p.lda;
+        akk[j] = 8 * (u % RU);
+        sh[j] = SH_UNSET;
+    }
+    const u32x4* wsrc[UW];
+#pragma unroll
+    for (int j = 0; j < UW; ++j) {
+        const int v = tid + 256 * j;
+        const int panel = min(n0 / 16 + v / (128 * KS), npanel - 1);
+        wsrc[j] = p.W + (int64_t)panel * p.ksteps * 128 + v % (128 * KS);
+    }
+    float4 ar[UA][2];
+    u32x4 wr[UW];
+    auto load = [&](int s) {
+#pragma unroll
+        for (int j = 0; j < UA; ++j) {
+            const int k = s * 32 * KS + akk[j];
+            if constexpr (KVEC) {
+                const float* src = arow[j] + min(k, p.K - 8);
+                const float4 x0 = *reinterpret_cast<const float4*>(src);
+                const float4 x1 = *reinterpret_cast<const float4*>(src + 4);
+                const bool ok = k < p.K;
+                ar[j][0] = ok ? x0 : make_float4(0.f, 0.f, 0.f, 0.f);
+                ar[j][1] = ok ? x1 : make_float4(0.f, 0.f, 0.f, 0.f);
+            } else {
+                float tt[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const float xv = arow[j][min(k + e, p.K - 1)];
+                    tt[e] = k + e < p.K ? xv : 0.f;
+                }
+                ar[j][0] = make_float4(tt[0], tt[1], tt[2], tt[3]);
+                ar[j][1] = make_float4(tt[4], tt[5], tt[6], tt[7]);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < UW; ++j) wr[j] = wsrc[j][(int64_t)s * 128 * KS];
+    };
+    auto store = [&](int b) {
+        u32x4* a_img = lds + b * (ASZ + WSZ);
+        u32x4* w_img = a_img + ASZ;
+#pragma unroll
+        for (int j = 0; j < UA; ++j) {
+            const int u = tid + 256 * j;
+            const int row = u / RU, q = u % RU, ks = q >> 2, gg = q & 3;
+            const float x[8] = {ar[j][0].x, ar[j][0].y, ar[j][0].z, ar[j][0].w,
+                                ar[j][1].x, ar[j][1].y, ar[j][1].z, ar[j][1].w};
+            float cm = fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3])));
+            cm = fmaxf(cm, fmaxf(fmaxf(fabsf(x[4]), fabsf(x[5])), fmaxf(fabsf(x[6]), fabsf(x[7]))));
+            cm = fmaxf(cm, dppf<0xB1>(cm));              // the row's lanes: quad xor 1, xor 2,
+            cm = fmaxf(cm, dppf<0x4E>(cm));
+            if constexpr (RU == 8) cm = fmaxf(cm, dppf<0x141>(cm));   // + half-row mirror
+            if (cm > 0.f && __builtin_amdgcn_frexp_expf(cm) + sh[j] > 15) sh[j] = chunk_shift(cm);
+            const float s = __builtin_ldexpf(1.f, sh[j] == SH_UNSET ? 0 : sh[j]);
+            f16x8 th, tm;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float xs = x[e] * s;
+                const _Float16 h = (_Float16)xs;
+                th[e] = h;
+                tm[e] = (_Float16)(xs - (float)h);
+            }
+            const int r = row ^ (2 * gg);
+            a_img[((ks * 2 + 0) * 4 + gg) * BM + r] = __builtin_bit_cast(u32x4, th);
+            a_img[((ks * 2 + 1) * 4 + gg) * BM + r] = __builtin_bit_cast(u32x4, tm);
+            if (q == 0) sh_lds[b][row] = sh[j];
+        }
+#pragma unroll
+        for (int j = 0; j < UW; ++j) w_img[tid + 256 * j] = wr[j];
+    };
+
+    f32x4 acc[TN][TM];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    int shr[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) shr[i] = SH_UNSET;
+
+    auto compute = [&](int b) {
+        const u32x4* a_img = lds + b * (ASZ + WSZ);
+        const u32x4* w_img = a_img + ASZ;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const int shv = sh_lds[b][wm + 16 * i + c];
+            if (__builtin_amdgcn_ballot_w64(shv != shr[i])) {
+                const float f = (shr[i] == SH_UNSET || shv == shr[i])
+                                    ? 1.f : __builtin_ldexpf(1.f, shv - shr[i]);
+#pragma unroll
+                for (int j = 0; j < TN; ++j) acc[j][i] *= f;
+                shr[i] = shv;
+            }
+        }
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            f16x8 af[TM][2];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const int r = (wm + 16 * i + c) ^ (2 * g);
+                af[i][0] = __builtin_bit_cast(f16x8, a_img[((ks * 2 + 0) * 4 + g) * BM + r]);
+                af[i][1] = __builtin_bit_cast(f16x8, a_img[((ks * 2 + 1) * 4 + g) * BM + r]);
+            }
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int pp = (wn + 16 * j) >> 4;
+                const u32x4* wb = w_img + pp * 128 * KS + ks * 128 + g * 16 + c;
+                const f16x8 wh = __builtin_bit_cast(f16x8, wb[0]);
+                const f16x8 wl = __builtin_bit_cast(f16x8, wb[64]);
+#pragma unroll
+                for (int i = 0; i < TM; ++i) {
+                    acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, af[i][0], acc[j][i], 0, 0, 0);
+                    acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, af[i][1], acc[j][i], 0, 0, 0);
+                    acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, af[i][0], acc[j][i], 0, 0, 0);
+                }
+            }
+        }
+    };
+
+    const int nst = (p.K + 32 * KS - 1) / (32 * KS);
+    if constexpr (DBUF) {
+        load(0);
+        store(0);
+        __syncthreads();
+        if (nst > 1) load(1);
+        for (int s = 0; s < nst; ++s) {
+            compute(s & 1);
+            if (s + 1 < nst) store((s + 1) & 1);
+            if (s + 2 < nst) load(s + 2);
+            __syncthreads();
+        }
+    } else {
+        load(0);
+        for (int s = 0; s < nst; ++s) {
+            __syncthreads();
+            store(0);
+            __syncthreads();
+            if (s + 1 < nst) load(s + 1);
+            compute(0);
+        }
+    }
+
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        const int m = m0 + wm + 16 * i + c;
+        if (m >= p.M) continue;
+        const float rs = __builtin_ldexpf(1.f, -shr[i]);
+        float* crow = p.C + (int64_t)m * p.ldc;
+        const float* rrow = p.R ? p.R + (int64_t)m * p.ldr : nullptr;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int n = n0 + wn + 16 * j + 4 * g;
+            if (n >= p.N) continue;
+            const float4 ws = *reinterpret_cast<const float4*>(p.wsc + n);
+            float y[4] = {acc[j][i][0] * rs * ws.x, acc[j][i][1] * rs * ws.y,
+                          acc[j][i][2] * rs * ws.z, acc[j][i][3] * rs * ws.w};
+            if (p.vec_out && n + 3 < p.N) {
+                if (p.bias) {
+                    const float4 b = *reinterpret_cast<const float4*>(p.bias + n);
+                    y[0] += b.x; y[1] += b.y; y[2] += b.z; y[3] += b.w;
+                }
+                if (rrow) {
+                    const float4 rv = *reinterpret_cast<const float4*>(rrow + n);
+                    y[0] += rv.x; y[1] += rv.y; y[2] += rv.z; y[3] += rv.w;
+                }
+                if (p.act == FGR_ACT_RELU) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) y[e] = fmaxf(y[e], 0.f);
+                }
+                *reinterpret_cast<float4*>(crow + n) = make_float4(y[0], y[1], y[2], y[3]);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    if (n + e >= p.N) break;
+                    float v = y[e];
+                    if (p.bias) v += p.bias[n + e];
+                    if (rrow) v += rrow[n + e];
+                    if (p.act == FGR_ACT_RELU) v = fmaxf(v, 0.f);
+                    crow[n + e] = v;
+                }
+            }
+        }
+    }
+}
+
 // Row max |w| of W (n x k, element (i, j) at w[i * sn + j * sk]) -> wsc[i] = 2^-e_i with
 // e_i the row scale exponent (max * 2^e_i in [2^14, 2^15)); one wave per row, rows padded
 // to a multiple of 16 get 0.
@@ -307,8 +529,22 @@ void launch_h3(const GemmH3Args& a, hipStream_t st) {
                            dim3(256), 0, st, a);
 }
 
+// k32-steps of the image, padded to an even count (v2 stages read 2 per stage)
+int ksteps_h3(int k) { return (k + 63) / 64 * 2; }
+
 size_t image_bytes_h3(int n, int k) {
-    return (size_t)((n + 15) / 16) * ((k + 31) / 32) * 128 * 16;
+    return (size_t)((n + 15) / 16) * ksteps_h3(k) * 128 * 16;
+}
+
+template <int BM, int BN, int KS, bool DBUF>
+void launch_h3v2(const GemmH3Args& a, hipStream_t st) {
+    const int nbm = (a.M + BM - 1) / BM, nbn = (a.N + BN - 1) / BN;
+    if (a.K % 8 == 0)
+        hipLaunchKernelGGL((gemm_f16x3_v2<BM, BN, KS, DBUF, true>), dim3((unsigned)(nbm * nbn)),
+                           dim3(256), 0, st, a);
+    else
+        hipLaunchKernelGGL((gemm_f16x3_v2<BM, BN, KS, DBUF, false>), dim3((unsigned)(nbm * nbn)),
+                           dim3(256), 0, st, a);
 }
 
 }  // namespace
@@ -327,7 +563,7 @@ extern "C" int fgr_split_weights_h3(const float* w, int32_t n, int32_t k, int64_
     FGR_REQUIRE(w && img && n > 0 && k > 0, "fgr_split_weights_h3: bad arguments");
     FGR_REQUIRE((reinterpret_cast<uintptr_t>(img) & 15) == 0,
                 "fgr_split_weights_h3: image not 16-B aligned");
-    const int ksteps = (k + 31) / 32;
+    const int ksteps = ksteps_h3(k);
     const int npad = (n + 15) / 16 * 16;
     float* wsc = reinterpret_cast<float*>(static_cast<char*>(img) + image_bytes_h3(n, k));
     hipStream_t st = as_stream(stream);
@@ -358,13 +594,30 @@ extern "C" int fgr_gemm_f16x3(const float* a, int64_t lda, const void* w_img, fl
                     (!r || ((ldr % 4 == 0) && (reinterpret_cast<uintptr_t>(r) & 15) == 0));
     const float* wsc = reinterpret_cast<const float*>(static_cast<const char*>(w_img) +
                                                       image_bytes_h3(n, k));
-    GemmH3Args g{a, lda, (const u32x4*)w_img, (k + 31) / 32, wsc, c, ldc, bias, r, ldr,
+    GemmH3Args g{a, lda, (const u32x4*)w_img, ksteps_h3(k), wsc, c, ldc, bias, r, ldr,
                  m, n, k, act, vo ? 1 : 0};
     hipStream_t st = as_stream(stream);
     // tile BM x BN (activation rows x output channels); FGR_GEMM16_TILE overrides it for
     // tuning (a = 128x128, b = 64x128, c = 64x64, d = 128x64)
     const char* force = getenv("FGR_GEMM16_TILE");
     const char cfg = (force && force[0]) ? force[0] : (n >= 512 && n % 256 == 0) ? 'b' : 'c';
+    // v2 variants (BM x BN, KS k32-steps per stage, DBUF) for tuning: e..m
+    switch (cfg) {
+        case 'e': launch_h3v2<64, 64, 2, false>(g, st); break;
+        case 'f': launch_h3v2<64, 64, 2, true>(g, st); break;
+        case 'g': launch_h3v2<64, 128, 2, false>(g, st); break;
+        case 'h': launch_h3v2<64, 128, 2, true>(g, st); break;
+        case 'i': launch_h3v2<128, 128, 2, false>(g, st); break;
+        case 'j': launch_h3v2<128, 128, 1, true>(g, st); break;
+        case 'k': launch_h3v2<64, 128, 1, true>(g, st); break;
+        case 'l': launch_h3v2<64, 64, 1, true>(g, st); break;
+        case 'm': launch_h3v2<128, 64, 2, false>(g, st); break;
+        default: break;
+    }
+    if (cfg >= 'e' && cfg <= 'm') {
+        FGR_CHECK_LAUNCH("gemm_f16x3_v2");
+        return FGR_OK;
+    }
     if (cfg == 'a')
         launch_h3<128, 128>(g, st);
     else if (cfg == 'b')

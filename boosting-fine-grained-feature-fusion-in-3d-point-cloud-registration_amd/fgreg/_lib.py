@@ -39,6 +39,9 @@ SIGNATURES = {
     'fgr_attention_bf16x6_workspace': [_i64, _i32, _i32, ctypes.POINTER(_sz)],
     'fgr_attention_bf16x6': [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i32, _i32,
                              _i64, _i32, _i32, _i32, _i32, _f32, _vp, _i64, _vp],
+    'fgr_attention_f16x3_workspace': [_i64, _i32, _i32, ctypes.POINTER(_sz)],
+    'fgr_attention_f16x3': [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i32, _i32,
+                            _i64, _i32, _i32, _i32, _i32, _f32, _vp, _i64, _vp],
     'fgr_res2net_chain': [_vp, _i64, _i32, _i32, _vp, _vp, _vp, _i32, _vp, _i64, _vp],
     'fgr_res2net_chain6': [_vp, _i64, _i32, _i32, _vp, _vp, _vp, _i32, _vp, _i64, _vp],
     'fgr_split_weights': [_vp, _i32, _i32, _i64, _vp, _vp, _vp],

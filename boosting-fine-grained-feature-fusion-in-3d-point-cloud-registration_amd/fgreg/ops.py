@@ -331,9 +331,10 @@ def res2net_chain(h, w, scale, w_frag, bias, x, cat, split6=False):
 # ------------------------------------------------------------------------------------------
 # attention
 # ------------------------------------------------------------------------------------------
-# fgr_attention_bf16x6 (fp32-accurate split-bf16 MFMA) for head_dim 32, fgr_attention (fp32
-# MFMA) otherwise; FGREG_ATTN=fp32 forces the latter (a precision A/B switch, both on the GPU).
-ATTN_MODE = os.environ.get('FGREG_ATTN', 'bf16x6')
+# head_dim 32: fgr_attention_f16x3 (fp32-accurate scaled split-fp16 MFMA, default) or
+# fgr_attention_bf16x6 (split-bf16, 6 products); fgr_attention (fp32 MFMA) otherwise.
+# FGREG_ATTN = f16x3 | bf16x6 | fp32 selects (a precision A/B switch, all on the GPU).
+ATTN_MODE = os.environ.get('FGREG_ATTN', 'f16x3')
 
 
 def attention(q, k, v, q_off, kv_off, kv_seg, max_q_len, n_head, out=None,
@@ -357,19 +358,20 @@ def attention(q, k, v, q_off, kv_off, kv_seg, max_q_len, n_head, out=None,
     assert kv_seg.dtype == torch.int32 and kv_seg.numel() == n_seg
     max_kv_len = max_q_len if max_kv_len is None else max_kv_len
     L = _lib.load()
-    split = (ATTN_MODE == 'bf16x6' and dh == 32
+    split = (ATTN_MODE in ('bf16x6', 'f16x3') and dh == 32
              and all(t.stride(0) % 4 == 0 and t.data_ptr() % 16 == 0 for t in (q, k, v, out)))
     t0 = _begin('attention')
     if split:
+        name = 'fgr_attention_' + ATTN_MODE
         nb = _lib._sz(0)
-        _lib.check(L.fgr_attention_bf16x6_workspace(k.shape[0], n_kv_seg, n_head, nb),
-                   'fgr_attention_bf16x6_workspace')
+        _lib.check(getattr(L, name + '_workspace')(k.shape[0], n_kv_seg, n_head, nb),
+                   name + '_workspace')
         ws = _workspace(q.device, nb.value)
-        _lib.check(L.fgr_attention_bf16x6(
+        _lib.check(getattr(L, name)(
             _ptr(q), q.stride(0), _ptr(k), k.stride(0), _ptr(v), v.stride(0), _ptr(out),
             out.stride(0), _ptr(q_off), _ptr(kv_off), _ptr(kv_seg), n_seg, n_kv_seg, k.shape[0],
             int(max_q_len), int(max_kv_len), n_head, dh, float(math.sqrt(1.0 / float(dh))),
-            _ptr(ws), ws.numel(), _stream()), 'fgr_attention_bf16x6')
+            _ptr(ws), ws.numel(), _stream()), name)
     else:
         _lib.check(L.fgr_attention(_ptr(q), q.stride(0), _ptr(k), k.stride(0), _ptr(v),
                                    v.stride(0), _ptr(out), out.stride(0), _ptr(q_off),

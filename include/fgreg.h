@@ -216,6 +216,21 @@ int fgr_attention_bf16x6(const float* q, int64_t ld_q, const float* k, int64_t l
                          int32_t max_kv_len, int32_t n_head, int32_t head_dim, float scale,
                          void* workspace, int64_t ws_bytes, void* stream);
 
+/* fp32-accurate attention on the fp16 matrix cores (head_dim 32), same semantics and
+ * arguments as fgr_attention_bf16x6: K/V are scaled per (64-key tile, head), Q per query and
+ * P by 2^14 into fp16's normal range (exact powers of two), split into two fp16 terms and
+ * the three significant term products accumulate in fp32 (<= ~3 * 2^-22 per product) at half
+ * the matrix-core work of bf16x6. Workspace: fgr_attention_f16x3_workspace() bytes (split
+ * K/V images + per-tile scale exponents), 16-B aligned. */
+int fgr_attention_f16x3_workspace(int64_t n_kv_rows, int32_t n_kv_seg, int32_t n_head,
+                                  size_t* bytes);
+int fgr_attention_f16x3(const float* q, int64_t ld_q, const float* k, int64_t ld_k,
+                        const float* v, int64_t ld_v, float* o, int64_t ld_o,
+                        const int64_t* q_off, const int64_t* kv_off, const int32_t* kv_seg,
+                        int32_t n_seg, int32_t n_kv_seg, int64_t n_kv_rows, int32_t max_q_len,
+                        int32_t max_kv_len, int32_t n_head, int32_t head_dim, float scale,
+                        void* workspace, int64_t ws_bytes, void* stream);
+
 /* ---- pose ----------------------------------------------------------------------------
  * fast_compute_rigid_transform (utils/se3_torch.py:226-273; threshold < 0 gives the
  * unthresholded compute_rigid_transform, :131-173) on n_batch independent problems

@@ -31,7 +31,7 @@ def attention(lens=(600,) * 16, d=256, nh=8):
     B = len(lens) // 2
     cross = torch.tensor([(c + B) % len(lens) for c in range(len(lens))], dtype=torch.int32, device=dev)
     flops = sum(4 * l * lens[(i + B) % len(lens)] * d for i, l in enumerate(lens))
-    for mode in ('fp32', 'bf16x6'):
+    for mode in ('fp32', 'bf16x6', 'f16x3'):
         ops.ATTN_MODE = mode
         us = timeit(lambda: ops.attention(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], off, off,
                                           cross, max(lens), nh))
@@ -108,7 +108,7 @@ def gemm_tiles(mode='bf16x6'):
         x = torch.randn(M, K, device=dev)
         w = torch.randn(N, K, device=dev)
         line = f'M={M:6d} N={N:5d} K={K:5d}'
-        for t in 'abcd':
+        for t in ('abcd' if mode == 'bf16x6' else 'abcdefghijklm'):
             os.environ[var] = t
             us = timeit(lambda: lin.linear(x, w), iters=20)
             line += f'  {t}: {us:7.1f} us ({2 * M * N * K / us / 1e6:6.1f} TF)'

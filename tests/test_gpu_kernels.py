@@ -157,12 +157,14 @@ def test_attention_vs_torch(gpu, nhead, d):
         assert rel_err(out, ref) < TOL
 
 
-@pytest.mark.parametrize('scale', [1.0, 6.0])
-def test_attention_bf16x6_is_fp32_accurate(gpu, scale):
-    """The split-bf16 attention (fgr_attention_bf16x6, dh = 32) against a float64 reference:
-    its error must be at fp32 level (<= 1e-5 normwise), and no worse than a few times the
+@pytest.mark.parametrize('split', ['bf16x6', 'f16x3'])
+@pytest.mark.parametrize('scale', [1.0, 6.0, 1e-6, 3e3])
+def test_attention_split_is_fp32_accurate(gpu, scale, split):
+    """The split attentions (fgr_attention_bf16x6 / _f16x3, dh = 32) against a float64
+    reference: error at fp32 level (<= 1e-5 normwise) and no worse than a few times the
     fp32-MFMA kernel's own error; separate key segmentation (kv lengths != q lengths,
-    max_kv_len > max_q_len), partial and 1-key tiles, sharp softmax at scale 6."""
+    max_kv_len > max_q_len), partial and 1-key tiles, sharp softmax at scale 6, inputs far
+    outside fp16's range (1e-6: subnormal in fp16 unscaled; 3e3: products past 65504)."""
     import fgreg.ops as ops
     rng = np.random.default_rng(7)
     d, nhead = 256, 8
@@ -171,13 +173,15 @@ def test_attention_bf16x6_is_fp32_accurate(gpu, scale):
     kv_seg = [1, 0, 3, 2]
     q = torch.from_numpy(rng.normal(size=(sum(qlens), d))) * scale
     kv = torch.from_numpy(rng.normal(size=(sum(klens), 2 * d))) * scale
+    if scale > 100:                 # large q and v, small k: scores stay O(1)
+        kv[:, :d] /= scale * scale
     k, v = kv[:, :d], kv[:, d:]
     ref = _attn_ref(q, k, v, qlens, klens, kv_seg, nhead)            # float64
     qg, kvg = q.float().to(gpu), kv.float().to(gpu)
     qo, ko = ops.offsets(qlens, gpu), ops.offsets(klens, gpu)
     seg = torch.tensor(kv_seg, dtype=torch.int32, device=gpu)
     errs = {}
-    for mode in ('bf16x6', 'fp32'):
+    for mode in (split, 'fp32'):
         old = ops.ATTN_MODE
         ops.ATTN_MODE = mode
         try:
@@ -186,8 +190,8 @@ def test_attention_bf16x6_is_fp32_accurate(gpu, scale):
         finally:
             ops.ATTN_MODE = old
         errs[mode] = rel_err(out.double(), ref)
-    assert errs['bf16x6'] < 1e-5, errs
-    assert errs['bf16x6'] < 4 * errs['fp32'] + 1e-7, errs
+    assert errs[split] < 1e-5, errs
+    assert errs[split] < 4 * errs['fp32'] + 1e-7, errs
 
 
 def test_transformer_layer_vs_reference(gpu):
