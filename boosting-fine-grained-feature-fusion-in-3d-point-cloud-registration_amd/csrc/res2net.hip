@@ -239,10 +239,173 @@ res2net_chain6_kernel(const float* __restrict__ h, int64_t n, int scale, int num
     }
 }
 
+// ------------------------------------------------------------------------------------
+// f16x3 variant (scaled two-term fp16 splits, see gemm16.hip): the same hierarchy at half
+// the matrix-core work of bf16x6. Swapped products (C^T = W a^T: W_i fragments as the A
+// operand, activation rows as the B operand) so each lane owns ONE activation row and
+// four output columns. Each step forms a = sp_{i-1} + h_i for the block's 32 rows, takes
+// the row max (LDS atomics: the whole row is on chip, so the scale is exact per row, no
+// online rescaling), scales the row by 2^e (max in [2^14, 2^15)) and splits it into fp16
+// (h, m) images img[t][ks][g][row]; W_i rows come pre-scaled per output column with their
+// inverse scales wsc[i][col] (fgreg.ops.res2net_fragments_h3).
+// ------------------------------------------------------------------------------------
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+template <int KT>
+__global__ void __launch_bounds__(64 * KT)
+res2net_chain_h3_kernel(const float* __restrict__ h, int64_t n, int scale, int nums,
+                        const u32x4* __restrict__ wf, const float* __restrict__ wsc,
+                        const float* __restrict__ bias, const float* __restrict__ x, int cin,
+                        float* __restrict__ cat, int64_t ld) {
+    constexpr int W = 16 * KT, KS = (W + 31) / 32, NU = kRows * KS * 4;   // A units per term
+    constexpr int IT = (NU + 64 * KT - 1) / (64 * KT);                    // build units / thread
+    __shared__ u32x4 img[2 * NU];
+    __shared__ float sp[kRows * W];
+    __shared__ int rmax[kRows];
+    const int tid = threadIdx.x, nth = 64 * KT;
+    const int wv = tid / 64, lane = tid % 64, g = lane >> 4, c = lane & 15;
+    const int64_t r0 = (int64_t)blockIdx.x * kRows;
+    const int64_t hw = (int64_t)scale * W;
+    const int col0 = wv * 16 + 4 * g;                  // this lane's 4 output columns
+
+    for (int i = 0; i < nums; ++i) {
+        const u32x4* wb = wf + (((int64_t)i * KT + wv) * KS) * 128 + lane;
+        u32x4 bq[3][2];                                // ring: k-steps ks, ks+1, ks+2
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+            if (q < KS) {
+#pragma unroll
+                for (int t = 0; t < 2; ++t) bq[q][t] = wb[(q * 2 + t) * 64];
+            }
+        const float4 wsv = *reinterpret_cast<const float4*>(wsc + i * W + col0);
+        const float4 bc = *reinterpret_cast<const float4*>(bias + i * W + col0);
+        if (tid < kRows) rmax[tid] = 0;
+        __syncthreads();
+        // a = sp_{i-1} + h_i: unit u -> (row = u % 32, kg = u / 32), 8 k each
+        float a[IT][8];
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int u = tid + nth * it;
+            const int row = u % kRows, kg = u / kRows, k0 = 8 * kg;
+            const int64_t gr = r0 + row;
+            float cm = 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; e += 4) {
+                float4 hv = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (u < NU && gr < n && k0 + e < W)
+                    hv = *reinterpret_cast<const float4*>(h + gr * hw + (int64_t)i * W + k0 + e);
+                a[it][e] = hv.x; a[it][e + 1] = hv.y; a[it][e + 2] = hv.z; a[it][e + 3] = hv.w;
+            }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                if (i > 0 && u < NU && k0 + e < W) a[it][e] += sp[row * W + k0 + e];
+                cm = fmaxf(cm, fabsf(a[it][e]));
+            }
+            if (u < NU && cm > 0.f) atomicMax(&rmax[row], __float_as_int(cm));
+        }
+        __syncthreads();
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int u = tid + nth * it;
+            if (u >= NU) break;
+            const int row = u % kRows, kg = u / kRows;
+            const float mx = __int_as_float(rmax[row]);
+            const float s = __builtin_ldexpf(1.f, mx > 0.f ? min(15 - __builtin_amdgcn_frexp_expf(mx), 127) : 0);
+            f16x8 th, tm;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float xs = a[it][e] * s;
+                const _Float16 hh = (_Float16)xs;
+                th[e] = hh;
+                tm[e] = (_Float16)(xs - (float)hh);
+            }
+            img[0 * NU + kg * kRows + row] = __builtin_bit_cast(u32x4, th);
+            img[1 * NU + kg * kRows + row] = __builtin_bit_cast(u32x4, tm);
+        }
+        __syncthreads();
+        f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            if (ks + 2 < KS) {
+#pragma unroll
+                for (int t = 0; t < 2; ++t) bq[(ks + 2) % 3][t] = wb[((ks + 2) * 2 + t) * 64];
+            }
+            const f16x8 wh = __builtin_bit_cast(f16x8, bq[ks % 3][0]);
+            const f16x8 wl = __builtin_bit_cast(f16x8, bq[ks % 3][1]);
+            const int base = (ks * 4 + g) * kRows;
+            const f16x8 a0h = __builtin_bit_cast(f16x8, img[0 * NU + base + c]);
+            const f16x8 a0m = __builtin_bit_cast(f16x8, img[1 * NU + base + c]);
+            const f16x8 a1h = __builtin_bit_cast(f16x8, img[0 * NU + base + 16 + c]);
+            const f16x8 a1m = __builtin_bit_cast(f16x8, img[1 * NU + base + 16 + c]);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, a0h, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, a1h, acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, a0m, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, a1m, acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, a0h, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, a1h, acc1, 0, 0, 0);
+        }
+        // epilogue: lane (g, c) holds sp_i[row rg * 16 + c][cols col0 .. col0 + 3]
+#pragma unroll
+        for (int rg = 0; rg < 2; ++rg) {
+            const int row = rg * 16 + c;
+            const float mx = __int_as_float(rmax[row]);
+            const float rs = __builtin_ldexpf(1.f, mx > 0.f ? -min(15 - __builtin_amdgcn_frexp_expf(mx), 127) : 0);
+            const f32x4 av = rg ? acc1 : acc0;
+            float4 y;
+            y.x = fmaxf(av[0] * rs * wsv.x + bc.x, 0.f);
+            y.y = fmaxf(av[1] * rs * wsv.y + bc.y, 0.f);
+            y.z = fmaxf(av[2] * rs * wsv.z + bc.z, 0.f);
+            y.w = fmaxf(av[3] * rs * wsv.w + bc.w, 0.f);
+            if (r0 + row < n)
+                *reinterpret_cast<float4*>(cat + (r0 + row) * ld + (int64_t)i * W + col0) = y;
+            *reinterpret_cast<float4*>(sp + row * W + col0) = y;
+        }
+        __syncthreads();
+    }
+    const int rest = (scale - nums) * W;
+    for (int e = tid; e < kRows * rest; e += nth) {
+        const int row = e / rest, cc = e - row * rest;
+        if (r0 + row < n)
+            cat[(r0 + row) * ld + (int64_t)nums * W + cc] = h[(r0 + row) * hw + (int64_t)nums * W + cc];
+    }
+    if (x) {
+        for (int e = tid; e < kRows * cin; e += nth) {
+            const int row = e / cin, cc = e - row * cin;
+            if (r0 + row < n) cat[(r0 + row) * ld + hw + cc] = x[(r0 + row) * cin + cc];
+        }
+    }
+}
+
 }  // namespace
 }  // namespace fgr
 
 using namespace fgr;
+
+extern "C" int fgr_res2net_chain_h3(const float* h, int64_t n, int32_t w, int32_t scale,
+                                    const void* w_img, const float* w_scale, const float* bias,
+                                    const float* x, int32_t cin, float* cat, int64_t ld_cat,
+                                    void* stream) {
+    FGR_REQUIRE(n >= 0 && scale >= 2 && (w == 112 || w == 224) && cin >= 0,
+                "fgr_res2net_chain_h3: unsupported width %d / scale %d (needs 112 or 224)", w, scale);
+    FGR_REQUIRE(ld_cat >= (int64_t)scale * w + (x ? cin : 0) && ld_cat % 4 == 0,
+                "fgr_res2net_chain_h3: ld_cat too small or not a multiple of 4");
+    FGR_REQUIRE(n == 0 || (h && w_img && w_scale && bias && cat), "fgr_res2net_chain_h3: null pointer");
+    FGR_REQUIRE(((reinterpret_cast<uintptr_t>(h) | reinterpret_cast<uintptr_t>(cat) |
+                  reinterpret_cast<uintptr_t>(w_scale) | reinterpret_cast<uintptr_t>(bias)) & 15) == 0 &&
+                    (scale * w) % 4 == 0,
+                "fgr_res2net_chain_h3: h / cat / w_scale / bias must be 16-B aligned");
+    if (n == 0) return FGR_OK;
+    const dim3 grid((unsigned)ceil_div(n, kRows));
+    hipStream_t st = as_stream(stream);
+    if (w == 112)
+        hipLaunchKernelGGL(res2net_chain_h3_kernel<7>, grid, dim3(64 * 7), 0, st, h, n, scale,
+                           scale - 1, (const u32x4*)w_img, w_scale, bias, x, cin, cat, ld_cat);
+    else
+        hipLaunchKernelGGL(res2net_chain_h3_kernel<14>, grid, dim3(64 * 14), 0, st, h, n, scale,
+                           scale - 1, (const u32x4*)w_img, w_scale, bias, x, cin, cat, ld_cat);
+    FGR_CHECK_LAUNCH("res2net_chain_h3_kernel");
+    return FGR_OK;
+}
 
 extern "C" int fgr_res2net_chain(const float* h, int64_t n, int32_t w, int32_t scale,
                                  const float* w_frag, const float* bias, const float* x,

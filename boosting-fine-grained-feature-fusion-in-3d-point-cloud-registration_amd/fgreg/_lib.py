@@ -44,6 +44,7 @@ SIGNATURES = {
                             _i64, _i32, _i32, _i32, _i32, _f32, _vp, _i64, _vp],
     'fgr_res2net_chain': [_vp, _i64, _i32, _i32, _vp, _vp, _vp, _i32, _vp, _i64, _vp],
     'fgr_res2net_chain6': [_vp, _i64, _i32, _i32, _vp, _vp, _vp, _i32, _vp, _i64, _vp],
+    'fgr_res2net_chain_h3': [_vp, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _i32, _vp, _i64, _vp],
     'fgr_split_weights': [_vp, _i32, _i32, _i64, _vp, _vp, _vp],
     'fgr_gemm_bf16x3': [_vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _vp, _i64, _i32, _i32, _i32,
                         _i32, _vp],

@@ -265,7 +265,8 @@ class my_Bottle2neck(nn.Module):  # noqa: N801 -- reference name (res2net.py:84)
                     wst = torch.stack([wi for wi, _ in ws])
                     chain = (ops.res2net_fragments(wst),
                              torch.stack([bi for _, bi in ws]).contiguous(),
-                             ops.res2net_fragments3(wst))
+                             ops.res2net_fragments3(wst),
+                             ops.res2net_fragments_h3(wst))
             self._folded = (key, w1, b1, ws, w3d, b3d, chain)
         return self._folded[1:]
 
@@ -279,7 +280,11 @@ class my_Bottle2neck(nn.Module):  # noqa: N801 -- reference name (res2net.py:84)
             # one launch for the whole hierarchy + the [.. | x] concat (fgr_res2net_chain)
             cat_in = torch.empty((x.shape[0], w * self.scale + x.shape[1]), dtype=x.dtype,
                                  device=x.device)
-            if lin.MODE in ('bf16x6', 'f16x3'):
+            if lin.MODE == 'f16x3' and w == 112:
+                # (w = 224: the bf16x6 chain measured faster -- fewer barriers per step)
+                ops.res2net_chain(out, w, self.scale, chain[3][0], chain[1], x, cat_in,
+                                  w_scale=chain[3][1])
+            elif lin.MODE in ('bf16x6', 'f16x3'):
                 ops.res2net_chain(out, w, self.scale, chain[2], chain[1], x, cat_in, split6=True)
             else:
                 ops.res2net_chain(out, w, self.scale, chain[0], chain[1], x, cat_in)

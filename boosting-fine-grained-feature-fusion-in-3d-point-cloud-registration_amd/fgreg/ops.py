@@ -308,13 +308,47 @@ def res2net_fragments3(weights: torch.Tensor) -> torch.Tensor:
     return t.permute(1, 2, 4, 0, 5, 3, 6).contiguous()     # [i, jt, ks, t, g, c, e]
 
 
+def res2net_fragments_h3(weights: torch.Tensor):
+    """(nums, w, w) Linear weights (out, in) -> (image, inverse scales) of
+    fgr_res2net_chain_h3: each output row (i, n) scaled by 2^e so its max |w| lies in
+    [2^14, 2^15) (wsc[i, n] = 2^-e), K zero-padded to a multiple of 32, split into two fp16
+    terms (h = f16(x), m = f16(x - h), round to nearest), in 16x16x32 fragment order
+    [i][jt][ks][term][g][c][8] with value W_i[16 jt + c][32 ks + 8 g + e] * 2^e."""
+    nums, w, _ = weights.shape
+    ks = (w + 31) // 32
+    mx = weights.abs().amax(dim=2)                                     # (nums, w)
+    e = torch.where(mx > 0, 15 - torch.frexp(mx).exponent, torch.zeros_like(mx, dtype=torch.int32))
+    e = e.clamp(max=127)
+    sc = torch.ldexp(torch.ones_like(mx), e.float())
+    wp = torch.zeros((nums, w, ks * 32), dtype=torch.float32, device=weights.device)
+    wp[..., :w] = weights * sc[..., None]
+    hi = wp.to(torch.float16)
+    lo = (wp - hi.float()).to(torch.float16)
+    t = torch.stack([hi, lo], 0).reshape(2, nums, w // 16, 16, ks, 4, 8)
+    img = t.permute(1, 2, 4, 0, 5, 3, 6).contiguous()                 # [i, jt, ks, t, g, c, e]
+    return img, (1.0 / sc).contiguous()
+
+
 def res2net_chain_supported(w):
     return w in (112, 224)
 
 
-def res2net_chain(h, w, scale, w_frag, bias, x, cat, split6=False):
+def res2net_chain(h, w, scale, w_frag, bias, x, cat, split6=False, w_scale=None):
     """cat[:, :] = [sp_0..sp_{scale-2} | h_{scale-1} | x] (fgr_res2net_chain, fp32 MFMA;
-    or fgr_res2net_chain6, fp32-accurate split bf16, with w_frag = res2net_fragments3)."""
+    fgr_res2net_chain6, fp32-accurate split bf16, with w_frag = res2net_fragments3; or
+    fgr_res2net_chain_h3, scaled split fp16, with (w_frag, w_scale) = res2net_fragments_h3)."""
+    if w_scale is not None:
+        _dev(h, w_frag, w_scale, bias, x, cat)
+        h = _c(h, torch.float32)
+        n = h.shape[0]
+        assert h.shape[1] == scale * w and cat.shape[0] == n and cat.stride(1) == 1
+        cin = 0 if x is None else x.shape[1]
+        if x is not None:
+            x = _c(x, torch.float32)
+        _lib.check(_lib.load().fgr_res2net_chain_h3(
+            _ptr(h), n, w, scale, _ptr(w_frag), _ptr(w_scale), _ptr(bias), _ptr(x), cin,
+            _ptr(cat), cat.stride(0), _stream()), 'fgr_res2net_chain_h3')
+        return cat
     _dev(h, w_frag, bias, x, cat)
     h = _c(h, torch.float32)
     n = h.shape[0]

@@ -145,6 +145,14 @@ int fgr_res2net_chain6(const float* h, int64_t n, int32_t w, int32_t scale, cons
                        const float* bias, const float* x, int32_t cin, float* cat,
                        int64_t ld_cat, void* stream);
 
+/* fp32-accurate f16x3 variant (scaled two-term fp16 splits, see fgr_gemm_f16x3): rows of
+ * a = sp_{i-1} + h_i scaled exactly per row, W_i rows pre-scaled per output column.
+ * w_img = fgreg.ops.res2net_fragments_h3 image [i][jt][ks][term 2][g][c][8] (fp16), w_scale
+ * (scale-1, w) the inverse column scales; h, cat, w_scale, bias 16-B aligned, ld_cat % 4 == 0. */
+int fgr_res2net_chain_h3(const float* h, int64_t n, int32_t w, int32_t scale, const void* w_img,
+                         const float* w_scale, const float* bias, const float* x, int32_t cin,
+                         float* cat, int64_t ld_cat, void* stream);
+
 /* ---- dense layers ----------------------------------------------------------------------
  * Split-precision GEMM for every Linear / KPConv-weight product of the forward:
  *   C[m, n] = act(A[m, :] . W[n, :] + bias[n] (+ R[m, n]))

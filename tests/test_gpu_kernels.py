@@ -238,12 +238,12 @@ def test_procrustes_vs_reference(gpu, case):
     assert np.array_equal(w_copy.cpu().numpy(), thr)
 
 
-@pytest.mark.parametrize('mode', ['bf16x6', 'fp32'])
+@pytest.mark.parametrize('mode', ['f16x3', 'bf16x6', 'fp32'])
 @pytest.mark.parametrize('cin,cout', [(128, 512), (256, 1024), (8, 32)])
 def test_res2net_block_vs_oracle(gpu, cin, cout, mode):
-    """my_res2Net (res2net.py:84-159, 231-265) in eval: fused fgr_res2net_chain6 (bf16x6)
-    or fgr_res2net_chain (fp32 MFMA) path for widths 112 / 224, torch path for the narrow
-    width, vs the CPU restatement."""
+    """my_res2Net (res2net.py:84-159, 231-265) in eval: fused fgr_res2net_chain_h3 (f16x3),
+    fgr_res2net_chain6 (bf16x6) or fgr_res2net_chain (fp32 MFMA) for widths 112 / 224,
+    torch path for the narrow width, vs the CPU restatement."""
     from fgreg import linear as fl
     from fgreg.backbone import my_Bottle2neck, my_res2Net
     old = fl.MODE
@@ -346,3 +346,25 @@ def test_gemm_f16x3_dynamic_range(gpu):
     err = ((out - ref32).abs() / den).max()
     assert err < 2e-6, float(err)
     del ref
+
+
+@pytest.mark.parametrize('tile', list('abcdefghijklm'))
+def test_gemm_f16x3_tiles(gpu, tile, monkeypatch):
+    """Every f16x3 tile / pipeline variant (FGR_GEMM16_TILE) at fp32 accuracy on ragged
+    shapes (M, N, K not multiples of the tiles; K % 64 != 0, odd k32-step count; N = 3)."""
+    from fgreg import linear as fl
+    monkeypatch.setenv('FGR_GEMM16_TILE', tile)
+    g = torch.Generator().manual_seed(11)
+    old = fl.MODE
+    try:
+        fl.set_mode('f16x3')
+        for m, n, k in ((1000, 200, 1000), (333, 3, 96), (130, 520, 40)):
+            x = torch.randn(m, k, generator=g)
+            w = torch.randn(n, k, generator=g) / math.sqrt(k)
+            b = torch.randn(n, generator=g)
+            r = torch.randn(m, n, generator=g)
+            ref = x.double() @ w.double().t() + b.double() + r.double()
+            out = fl.linear(x.to(gpu), w.to(gpu), b.to(gpu), residual=r.to(gpu))
+            assert rel_err(out, ref) < 2e-6, (tile, m, n, k)
+    finally:
+        fl.set_mode(old)
