@@ -29,7 +29,14 @@ sys.path.insert(0, os.path.join(REPO, 'boosting-fine-grained-feature-fusion-in-3
 
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
 FP32_MFMA_PEAK_TFLOPS = 157.3
-BF16_MFMA_PEAK_TFLOPS = 2500.0   # dense (MI355X_MICROARCH.md); the bf16x6 kernels issue 6 per product
+F16_MFMA_PEAK_TFLOPS = 2500.0    # fp16 / bf16 dense (MI355X_MICROARCH.md)
+# matrix-core products issued per fp32-equivalent product, by precision mode
+PIPE = {'f16x3': 3, 'bf16x6': 6, 'bf16x3': 3, 'fp32': 1}
+PRECISION = {'f16x3': 'fp32-accurate scaled split fp16 (3 fp16 MFMA products per fp32 '
+                      'product, <= ~3 * 2^-22 relative each)',
+             'bf16x6': 'fp32-accurate split bf16 (6 bf16 MFMA products per fp32 product)',
+             'bf16x3': 'split bf16, 3 products (~2^-17 relative)',
+             'fp32': 'fp32 MFMA / hipBLASLt fp32'}
 
 
 def parse():
@@ -56,6 +63,7 @@ def _pmc_traffic():
 def main():
     args = parse()
     import fgreg
+    from fgreg import linear as lin
     from fgreg import ops
     from fgreg.synthetic import make_batch
 
@@ -171,24 +179,29 @@ def main():
                          'algorithmic_bytes_per_launch': g_bytes_launch,
                          'avg_launch_us': g_avg_s * 1e6, 'launches_per_step': len(gather_bytes),
                          'share_of_step': g_ms / (elapsed * 1e3)},
-            'roofline_attention': {'kernel': 'fgr_attention', 'bound': 'mfma',
+            'roofline_attention': {'kernel': f'fgr_attention_{ops.ATTN_MODE}', 'bound': 'mfma',
                                    'achieved': a_achieved, 'peak': FP32_MFMA_PEAK_TFLOPS,
-                                   'unit': 'TFLOP/s', 'frac': a_achieved / FP32_MFMA_PEAK_TFLOPS,
+                                   'unit': 'TFLOP/s (fp32-equivalent)',
+                                   'frac': a_achieved / FP32_MFMA_PEAK_TFLOPS,
                                    'flops_per_step': a_flops_step,
                                    'avg_launch_us': a_ms * 1e3 / max(a_launches, 1),
                                    'share_of_step': a_ms / (elapsed * 1e3),
-                                   'precision': 'fp32-accurate bf16x6 split (6 bf16 MFMA '
-                                                'products per fp32 product)',
-                                   'bf16_pipe_tflops': 6 * a_achieved,
-                                   'bf16_pipe_frac': 6 * a_achieved / BF16_MFMA_PEAK_TFLOPS},
-            'roofline_gemm': {'kernel': 'fgr_gemm_bf16x6 (all dense layers)', 'bound': 'mfma',
+                                   'precision': PRECISION.get(ops.ATTN_MODE, ops.ATTN_MODE),
+                                   'matrix_pipe_tflops': PIPE.get(ops.ATTN_MODE, 1) * a_achieved,
+                                   'matrix_pipe_frac': PIPE.get(ops.ATTN_MODE, 1) * a_achieved /
+                                   (F16_MFMA_PEAK_TFLOPS if ops.ATTN_MODE != 'fp32'
+                                    else FP32_MFMA_PEAK_TFLOPS)},
+            'roofline_gemm': {'kernel': f'fgr_gemm_{lin.MODE} (all dense layers)', 'bound': 'mfma',
                               'achieved': m_achieved, 'peak': FP32_MFMA_PEAK_TFLOPS,
                               'unit': 'TFLOP/s (fp32-equivalent)',
                               'frac': m_achieved / FP32_MFMA_PEAK_TFLOPS,
                               'flops_per_step': m_flops_step,
                               'launches_per_step': len(gemm_flops),
                               'share_of_step': m_ms / (elapsed * 1e3),
-                              'bf16_pipe_frac': 6 * m_achieved / BF16_MFMA_PEAK_TFLOPS},
+                              'precision': PRECISION.get(lin.MODE, lin.MODE),
+                              'matrix_pipe_frac': PIPE.get(lin.MODE, 1) * m_achieved /
+                              (F16_MFMA_PEAK_TFLOPS if lin.MODE != 'fp32'
+                               else FP32_MFMA_PEAK_TFLOPS)},
             'cpu_baseline': cpu,
         }
         print(json.dumps(line), flush=True)

@@ -76,6 +76,15 @@ __device__ __forceinline__ float row16_sum(float v) {
     v += dpp<0x140>(v);
     return v;
 }
+// Sum over all 64 lanes without the LDS crossbar: DPP within each 16-lane row, then
+// v_permlane16/32_swap across the four rows; every lane gets the total.
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+    v = row16_sum(v);
+    auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+    auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
 
 // Index of the segment containing row r, given sorted offsets off[0..n] (off[0] = 0).
 __device__ __forceinline__ int find_segment(const int64_t* off, int n, int64_t r) {

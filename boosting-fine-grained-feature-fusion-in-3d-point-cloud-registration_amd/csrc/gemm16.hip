@@ -73,6 +73,38 @@ __device__ __forceinline__ int chunk_shift(float cm) {
     return min(8 - __builtin_amdgcn_frexp_expf(cm), 127);
 }
 
+// Epilogue of one output: act(y + b + r), or LeakyReLU_0.1(ReLU(y + b) + r) for
+// FGR_ACT_RELU_RES_LEAKY (absent bias / residual come in as 0).
+__device__ __forceinline__ float finish_out(float y, float b, float r, int act) {
+    if (act == FGR_ACT_RELU_RES_LEAKY) {
+        const float t = fmaxf(y + b, 0.f) + r;
+        return t > 0.f ? t : 0.1f * t;
+    }
+    const float t = y + b + r;
+    return act == FGR_ACT_RELU ? fmaxf(t, 0.f) : t;
+}
+
+// Stores one lane's 4 consecutive outputs n..n+3 of a row (16-B accesses when vec and the
+// 4 columns are in range).
+__device__ __forceinline__ void store_out4(const float (&y)[4], const float* bias,
+                                           const float* rrow, float* crow, int n, int N, int act,
+                                           bool vec) {
+    if (vec && n + 3 < N) {
+        float4 b = make_float4(0.f, 0.f, 0.f, 0.f), r = b;
+        if (bias) b = *reinterpret_cast<const float4*>(bias + n);
+        if (rrow) r = *reinterpret_cast<const float4*>(rrow + n);
+        *reinterpret_cast<float4*>(crow + n) =
+            make_float4(finish_out(y[0], b.x, r.x, act), finish_out(y[1], b.y, r.y, act),
+                        finish_out(y[2], b.z, r.z, act), finish_out(y[3], b.w, r.w, act));
+    } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            if (n + e >= N) break;
+            crow[n + e] = finish_out(y[e], bias ? bias[n + e] : 0.f, rrow ? rrow[n + e] : 0.f, act);
+        }
+    }
+}
+
 template <int BM, int BN, bool KVEC>
 __global__ void __launch_bounds__(256) gemm_f16x3_kernel(GemmH3Args p) {
     constexpr int TM = BM / 32, TN = BN / 32;          // 16x16 subtiles per wave (m, n)
@@ -234,33 +266,9 @@ __global__ void __launch_bounds__(256) gemm_f16x3_kernel(GemmH3Args p) {
             const int n = n0 + wn + 16 * j + 4 * g;
             if (n >= p.N) continue;
             const float4 ws = *reinterpret_cast<const float4*>(p.wsc + n);   // padded to 16
-            float y[4] = {acc[j][i][0] * rs * ws.x, acc[j][i][1] * rs * ws.y,
-                          acc[j][i][2] * rs * ws.z, acc[j][i][3] * rs * ws.w};
-            if (p.vec_out && n + 3 < p.N) {
-                if (p.bias) {
-                    const float4 b = *reinterpret_cast<const float4*>(p.bias + n);
-                    y[0] += b.x; y[1] += b.y; y[2] += b.z; y[3] += b.w;
-                }
-                if (rrow) {
-                    const float4 rv = *reinterpret_cast<const float4*>(rrow + n);
-                    y[0] += rv.x; y[1] += rv.y; y[2] += rv.z; y[3] += rv.w;
-                }
-                if (p.act == FGR_ACT_RELU) {
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) y[e] = fmaxf(y[e], 0.f);
-                }
-                *reinterpret_cast<float4*>(crow + n) = make_float4(y[0], y[1], y[2], y[3]);
-            } else {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    if (n + e >= p.N) break;
-                    float v = y[e];
-                    if (p.bias) v += p.bias[n + e];
-                    if (rrow) v += rrow[n + e];
-                    if (p.act == FGR_ACT_RELU) v = fmaxf(v, 0.f);
-                    crow[n + e] = v;
-                }
-            }
+            const float y[4] = {acc[j][i][0] * rs * ws.x, acc[j][i][1] * rs * ws.y,
+                                acc[j][i][2] * rs * ws.z, acc[j][i][3] * rs * ws.w};
+            store_out4(y, p.bias, rrow, crow, n, p.N, p.act, p.vec_out);
         }
     }
 }
@@ -456,33 +464,9 @@ __global__ void __launch_bounds__(256) gemm_f16x3_v2(GemmH3Args p) {
             const int n = n0 + wn + 16 * j + 4 * g;
             if (n >= p.N) continue;
             const float4 ws = *reinterpret_cast<const float4*>(p.wsc + n);
-            float y[4] = {acc[j][i][0] * rs * ws.x, acc[j][i][1] * rs * ws.y,
-                          acc[j][i][2] * rs * ws.z, acc[j][i][3] * rs * ws.w};
-            if (p.vec_out && n + 3 < p.N) {
-                if (p.bias) {
-                    const float4 b = *reinterpret_cast<const float4*>(p.bias + n);
-                    y[0] += b.x; y[1] += b.y; y[2] += b.z; y[3] += b.w;
-                }
-                if (rrow) {
-                    const float4 rv = *reinterpret_cast<const float4*>(rrow + n);
-                    y[0] += rv.x; y[1] += rv.y; y[2] += rv.z; y[3] += rv.w;
-                }
-                if (p.act == FGR_ACT_RELU) {
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) y[e] = fmaxf(y[e], 0.f);
-                }
-                *reinterpret_cast<float4*>(crow + n) = make_float4(y[0], y[1], y[2], y[3]);
-            } else {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    if (n + e >= p.N) break;
-                    float v = y[e];
-                    if (p.bias) v += p.bias[n + e];
-                    if (rrow) v += rrow[n + e];
-                    if (p.act == FGR_ACT_RELU) v = fmaxf(v, 0.f);
-                    crow[n + e] = v;
-                }
-            }
+            const float y[4] = {acc[j][i][0] * rs * ws.x, acc[j][i][1] * rs * ws.y,
+                                acc[j][i][2] * rs * ws.z, acc[j][i][3] * rs * ws.w};
+            store_out4(y, p.bias, rrow, crow, n, p.N, p.act, p.vec_out);
         }
     }
 }
@@ -509,21 +493,33 @@ struct RowsArgs {
     const float* bias;
     const float* R; int64_t ldr;
     int M, N, K, act, vec_out;
+    int nbx;                                            // column-panel blocks (grid = nbx * py)
 };
 
 template <int KT, int BNP, int NW, bool LN>
 __global__ void __launch_bounds__(64 * NW) gemm_rows_f16x3(RowsArgs p) {
     constexpr int NP = BNP / 16;                         // 16-column panels per block
     __shared__ u32x4 wl[NP * KT * 128];
-    __shared__ float lnp[2][KT * 32];
+    __shared__ __attribute__((aligned(16))) float lnp[2][KT * 32];
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
     const int g = lane >> 4, c = lane & 15;
     const int npanel = (p.N + 15) / 16;
-    const int pn0 = blockIdx.x * NP;                     // first 16-col panel of this block
-    // W panel -> LDS (panels past N are clamped; their columns are never stored)
+    // XCD-aware order: the nbx blocks that read the same rows (one per column panel) get
+    // consecutive ids after the remap, i.e. one XCD, so the rows come from its L2 once
+    int t = blockIdx.x;
+    {
+        const int nwg = gridDim.x, q = nwg / 8, r = nwg % 8, x = t % 8, lo = t / 8;
+        t = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + lo;
+    }
+    const int bx = t % p.nbx, by = t / p.nbx, py = gridDim.x / p.nbx;
+    const int pn0 = bx * NP;                             // first 16-col panel of this block
+    // W panel -> LDS (panels past N are clamped; their columns are never stored); k-steps
+    // past the image (KT > ksteps) are zero so the zero A columns meet zeros, not garbage
     for (int u = tid; u < NP * KT * 128; u += 64 * NW) {
         const int pl = u / (KT * 128), rem = u % (KT * 128);
-        wl[u] = p.W[(int64_t)min(pn0 + pl, npanel - 1) * p.ksteps * 128 + rem];
+        wl[u] = rem < p.ksteps * 128
+                    ? p.W[(int64_t)min(pn0 + pl, npanel - 1) * p.ksteps * 128 + rem]
+                    : u32x4{0u, 0u, 0u, 0u};
     }
     if (LN) {
         for (int k = tid; k < KT * 32; k += 64 * NW) {
@@ -534,7 +530,7 @@ __global__ void __launch_bounds__(64 * NW) gemm_rows_f16x3(RowsArgs p) {
     __syncthreads();
 
     const int ntiles = (p.M + 15) / 16;
-    for (int tile = blockIdx.y * NW + wv; tile < ntiles; tile += gridDim.y * NW) {
+    for (int tile = by * NW + wv; tile < ntiles; tile += py * NW) {
         const int row = tile * 16 + c;
         const int64_t rr = min(row, p.M - 1);
         float v[KT][8];
@@ -623,6 +619,9 @@ __global__ void __launch_bounds__(64 * NW) gemm_rows_f16x3(RowsArgs p) {
                 acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, am, acc[j], 0, 0, 0);
                 acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, ah, acc[j], 0, 0, 0);
             }
+            // keep each k-step's LDS fragment loads next to their MFMAs (hoisting all of
+            // them across the unrolled loop is what spilled)
+            __builtin_amdgcn_sched_barrier(0);
         }
         if (row >= p.M) continue;
         const float rs = __builtin_ldexpf(1.f, -sh);
@@ -633,33 +632,9 @@ __global__ void __launch_bounds__(64 * NW) gemm_rows_f16x3(RowsArgs p) {
             const int n = (pn0 + j) * 16 + 4 * g;
             if (n >= p.N) continue;
             const float4 ws = *reinterpret_cast<const float4*>(p.wsc + n);
-            float y[4] = {acc[j][0] * rs * ws.x, acc[j][1] * rs * ws.y,
-                          acc[j][2] * rs * ws.z, acc[j][3] * rs * ws.w};
-            if (p.vec_out && n + 3 < p.N) {
-                if (p.bias) {
-                    const float4 b = *reinterpret_cast<const float4*>(p.bias + n);
-                    y[0] += b.x; y[1] += b.y; y[2] += b.z; y[3] += b.w;
-                }
-                if (rrow) {
-                    const float4 rv = *reinterpret_cast<const float4*>(rrow + n);
-                    y[0] += rv.x; y[1] += rv.y; y[2] += rv.z; y[3] += rv.w;
-                }
-                if (p.act == FGR_ACT_RELU) {
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) y[e] = fmaxf(y[e], 0.f);
-                }
-                *reinterpret_cast<float4*>(crow + n) = make_float4(y[0], y[1], y[2], y[3]);
-            } else {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    if (n + e >= p.N) break;
-                    float vv = y[e];
-                    if (p.bias) vv += p.bias[n + e];
-                    if (rrow) vv += rrow[n + e];
-                    if (p.act == FGR_ACT_RELU) vv = fmaxf(vv, 0.f);
-                    crow[n + e] = vv;
-                }
-            }
+            const float y[4] = {acc[j][0] * rs * ws.x, acc[j][1] * rs * ws.y,
+                                acc[j][2] * rs * ws.z, acc[j][3] * rs * ws.w};
+            store_out4(y, p.bias, rrow, crow, n, p.N, p.act, p.vec_out);
         }
     }
 }
@@ -833,22 +808,31 @@ extern "C" int fgr_gemm_f16x3(const float* a, int64_t lda, const void* w_img, fl
 
 namespace fgr {
 namespace {
+// Grid: nbx column-panel blocks x py row groups, py sized so that the grid fills every CU
+// to its resident-block limit once (each wave then loops over its row tiles).
 template <int KT, int BNP, bool LN>
-void launch_rows(const RowsArgs& a, hipStream_t st, int n_cu) {
+void launch_rows(RowsArgs a, hipStream_t st, int n_cu) {
     constexpr int NW = 8;
-    const int panels = (a.N + BNP - 1) / BNP;
+    static int per_cu = 0;                               // device-properties cache
+    if (per_cu <= 0) {
+        int nb = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                &nb, reinterpret_cast<const void*>(&gemm_rows_f16x3<KT, BNP, NW, LN>), 64 * NW,
+                0) != hipSuccess || nb <= 0)
+            nb = 1;
+        per_cu = nb;
+    }
+    a.nbx = (a.N + BNP - 1) / BNP;
     const int ntiles = (a.M + 15) / 16;
-    int py = (n_cu + panels - 1) / panels;
+    int py = (per_cu * n_cu + a.nbx - 1) / a.nbx;
     py = max(1, min(py, (ntiles + NW - 1) / NW));
-    hipLaunchKernelGGL((gemm_rows_f16x3<KT, BNP, NW, LN>), dim3((unsigned)panels, (unsigned)py),
+    hipLaunchKernelGGL((gemm_rows_f16x3<KT, BNP, NW, LN>), dim3((unsigned)(a.nbx * py)),
                        dim3(64 * NW), 0, st, a);
 }
 template <int KT, bool LN>
 void launch_rows_n(const RowsArgs& a, hipStream_t st, int n_cu) {
     if (a.N <= 16)
         launch_rows<KT, 16, LN>(a, st, n_cu);
-    else if (a.N >= 512)
-        launch_rows<KT, 128, LN>(a, st, n_cu);
     else
         launch_rows<KT, 64, LN>(a, st, n_cu);
 }
@@ -876,9 +860,11 @@ extern "C" int fgr_gemm_rows_f16x3(const float* x, int64_t ldx, const float* ln_
     RowsArgs g{x, ldx, ln_gamma, ln_beta, ln_eps, add, ld_add, (const u32x4*)w_img,
                ksteps_h3(k), wsc, c, ldc, bias, r, ldr, m, n, k, act, vo ? 1 : 0};
     hipStream_t st = as_stream(stream);
-    int dev = 0, n_cu = 256;
-    if (hipGetDevice(&dev) == hipSuccess)
-        hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+    int dev = 0, n_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n_cu <= 0)
+        n_cu = 256;
     const bool ln = ln_gamma != nullptr;
     if (k <= 128) {
         if (ln) launch_rows_n<4, true>(g, st, n_cu); else launch_rows_n<4, false>(g, st, n_cu);

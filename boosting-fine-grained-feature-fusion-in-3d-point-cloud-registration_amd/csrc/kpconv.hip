@@ -81,7 +81,9 @@ row_positive_kernel(const float* __restrict__ x, int64_t ns, unsigned char* __re
 // One wave per query, cin = 64 * VEC, K kernel points (runtime, <= kMaxKp, unrolled by KU).
 // Valid neighbours of each 64-wide chunk are compacted by ballot; their feature rows are
 // then streamed 4 at a time (4 x 16-B loads in flight per lane) into K accumulators.
-template <int VEC, int KU>
+// POSI: the normaliser's "row sum > 0" is taken from the rows as they stream by (a DPP /
+// permlane wave sum per row, no LDS); otherwise from the row_positive_kernel flags.
+template <int VEC, int KU, bool POSI>
 __global__ void __launch_bounds__(64 * kGatherWaves)
 kpconv_gather_wide(const float* __restrict__ q, const float* __restrict__ s, int64_t nq, int64_t ns,
                    const int64_t* __restrict__ idx, int width, const float* __restrict__ x,
@@ -114,7 +116,7 @@ kpconv_gather_wide(const float* __restrict__ q, const float* __restrict__ s, int
         const unsigned long long m = __ballot(valid);
         const int v = __popcll(m);
         if (v == 0) continue;
-        n_pos += __popcll(__ballot(valid && pos[id] != 0));
+        if constexpr (!POSI) n_pos += __popcll(__ballot(valid && pos[id] != 0));
         const int p = __popcll(m & ((1ull << lane) - 1ull));
         if (valid) nb_lds[wv][p] = (int)id;
         if (lane < U) nb_lds[wv][v + lane] = 0;       // pad rows: weight 0, row 0
@@ -137,6 +139,16 @@ kpconv_gather_wide(const float* __restrict__ q, const float* __restrict__ s, int
 #pragma unroll
             for (int u = 0; u < U; ++u)
                 load_vec<VEC>(x + (int64_t)nb_lds[wv][hh + u] * CIN + lane * VEC, xv[u]);
+            if constexpr (POSI) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    float t = 0.f;
+#pragma unroll
+                    for (int j = 0; j < VEC; ++j) t += xv[u][j];
+                    t = wave_sum_dpp(t);
+                    n_pos += (hh + u < v && t > 0.f) ? 1 : 0;
+                }
+            }
 #pragma unroll
             for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -200,6 +212,55 @@ kpconv_gather_narrow(const float* __restrict__ q, const float* __restrict__ s, i
     if (k == 0) nnorm[qi] = (float)(n_pos > 1 ? n_pos : 1);
 }
 
+// cin == 1 (the stem: feats0 = ones, finegrained_regtr.py:126): 16 lanes per query, 4
+// queries per wave. Lane l of a query takes neighbours h = l, l + 16, ... (coalesced index
+// reads), accumulates all K kernel-point sums, and the 16 lanes reduce them with DPP; lane
+// k then writes wf[q, k] (and k + 16), so each neighbour is read once per query instead of
+// once per (query, kernel point).
+template <int KU>
+__global__ void __launch_bounds__(256)
+kpconv_gather_c1(const float* __restrict__ q, const float* __restrict__ s, int64_t nq, int64_t ns,
+                 const int64_t* __restrict__ idx, int width, const float* __restrict__ x,
+                 const float* __restrict__ kp_g, int n_kp, float inv_extent,
+                 float* __restrict__ wf, float* __restrict__ nnorm) {
+    __shared__ float kp[3 * kMaxKp];
+    for (int i = threadIdx.x; i < 3 * n_kp; i += blockDim.x) kp[i] = kp_g[i];
+    __syncthreads();
+    const int64_t qi = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+    const int l = threadIdx.x & 15;
+    const int64_t qc = qi < nq ? qi : nq - 1;          // tail lanes still join the reductions
+    const float qx = q[3 * qc], qy = q[3 * qc + 1], qz = q[3 * qc + 2];
+    float acc[KU];
+#pragma unroll
+    for (int k = 0; k < KU; ++k) acc[k] = 0.f;
+    float n_pos = 0.f;
+    const int64_t* row = idx + qc * width;
+    for (int h = l; h < width; h += 16) {
+        const int64_t id = row[h];
+        if (id < 0 || id >= ns) continue;
+        const float nx = s[3 * id] - qx, ny = s[3 * id + 1] - qy, nz = s[3 * id + 2] - qz;
+        const float xv = x[id];
+        n_pos += xv > 0.f ? 1.f : 0.f;
+#pragma unroll
+        for (int k = 0; k < KU; ++k)
+            if (k < n_kp) acc[k] = fmaf(kp_weight(nx, ny, nz, kp, k, inv_extent), xv, acc[k]);
+    }
+    float mine0 = 0.f, mine1 = 0.f;
+#pragma unroll
+    for (int k = 0; k < KU; ++k) {
+        const float t = row16_sum(acc[k]);
+        if (k == l) mine0 = t;
+        if (k == l + 16) mine1 = t;
+    }
+    n_pos = row16_sum(n_pos);
+    if (qi < nq) {
+        float* out = wf + qi * n_kp;
+        if (l < n_kp) out[l] = mine0;
+        if (KU > 16 && l + 16 < n_kp) out[l + 16] = mine1;
+        if (l == 0) nnorm[qi] = n_pos > 1.f ? n_pos : 1.f;
+    }
+}
+
 template <int CMAX>
 void launch_narrow(const float* q, const float* s, int64_t nq, int64_t ns, const int64_t* idx,
                    int width, const float* x, int cin, const float* kp, int n_kp, float inv_ext,
@@ -209,20 +270,36 @@ void launch_narrow(const float* q, const float* s, int64_t nq, int64_t ns, const
                        st, q, s, nq, ns, idx, width, x, cin, kp, n_kp, inv_ext, wf, nnorm);
 }
 
+template <int VEC, bool POSI>
+void launch_wide_k(const float* q, const float* s, int64_t nq, int64_t ns, const int64_t* idx,
+                   int width, const float* x, unsigned char* pos, const float* kp, int n_kp,
+                   float inv_ext, float* wf, float* nnorm, hipStream_t st) {
+    dim3 grid((unsigned)ceil_div(nq, kGatherWaves));
+    if (n_kp <= 16)
+        hipLaunchKernelGGL((kpconv_gather_wide<VEC, 16, POSI>), grid, dim3(64 * kGatherWaves), 0,
+                           st, q, s, nq, ns, idx, width, x, pos, kp, n_kp, inv_ext, wf, nnorm);
+    else
+        hipLaunchKernelGGL((kpconv_gather_wide<VEC, kMaxKp, POSI>), grid, dim3(64 * kGatherWaves),
+                           0, st, q, s, nq, ns, idx, width, x, pos, kp, n_kp, inv_ext, wf, nnorm);
+}
+
+// Positivity inline (default) or from the per-source-row pre-pass (FGR_GATHER_PREPASS=1,
+// kept for A/B measurements).
 template <int VEC>
 void launch_wide(const float* q, const float* s, int64_t nq, int64_t ns, const int64_t* idx,
                  int width, const float* x, unsigned char* pos, const float* kp, int n_kp,
                  float inv_ext, float* wf, float* nnorm, hipStream_t st) {
-    if (ns > 0)
-        hipLaunchKernelGGL(row_positive_kernel<VEC>, dim3((unsigned)ceil_div(ns, 4)), dim3(256), 0,
-                           st, x, ns, pos);
-    dim3 grid((unsigned)ceil_div(nq, kGatherWaves));
-    if (n_kp <= 16)
-        hipLaunchKernelGGL((kpconv_gather_wide<VEC, 16>), grid, dim3(64 * kGatherWaves), 0, st, q,
-                           s, nq, ns, idx, width, x, pos, kp, n_kp, inv_ext, wf, nnorm);
-    else
-        hipLaunchKernelGGL((kpconv_gather_wide<VEC, kMaxKp>), grid, dim3(64 * kGatherWaves), 0,
-                           st, q, s, nq, ns, idx, width, x, pos, kp, n_kp, inv_ext, wf, nnorm);
+    const char* pre = getenv("FGR_GATHER_PREPASS");
+    if (pre && pre[0] == '1') {
+        if (ns > 0)
+            hipLaunchKernelGGL(row_positive_kernel<VEC>, dim3((unsigned)ceil_div(ns, 4)),
+                               dim3(256), 0, st, x, ns, pos);
+        launch_wide_k<VEC, false>(q, s, nq, ns, idx, width, x, pos, kp, n_kp, inv_ext, wf, nnorm,
+                                  st);
+    } else {
+        launch_wide_k<VEC, true>(q, s, nq, ns, idx, width, x, pos, kp, n_kp, inv_ext, wf, nnorm,
+                                 st);
+    }
 }
 
 // max_pool, one wave per query (c % 64 == 0, VEC floats per lane): valid neighbours are
@@ -317,8 +394,15 @@ extern "C" int fgr_kpconv_gather(const float* q, const float* s, int64_t nq, int
             default: launch_wide<4>(q, s, nq, ns, idx, width, x, pos, kp, n_kp, inv_ext, wf, nnorm, st); break;
         }
     } else if (cin <= 64) {
-        if (cin == 1) launch_narrow<1>(q, s, nq, ns, idx, width, x, cin, kp, n_kp, inv_ext, wf, nnorm, st);
-        else if (cin <= 8) launch_narrow<8>(q, s, nq, ns, idx, width, x, cin, kp, n_kp, inv_ext, wf, nnorm, st);
+        if (cin == 1) {
+            const dim3 grid((unsigned)ceil_div(nq * 16, 256));
+            if (n_kp <= 16)
+                hipLaunchKernelGGL(kpconv_gather_c1<16>, grid, dim3(256), 0, st, q, s, nq, ns, idx,
+                                   width, x, kp, n_kp, inv_ext, wf, nnorm);
+            else
+                hipLaunchKernelGGL(kpconv_gather_c1<kMaxKp>, grid, dim3(256), 0, st, q, s, nq, ns,
+                                   idx, width, x, kp, n_kp, inv_ext, wf, nnorm);
+        } else if (cin <= 8) launch_narrow<8>(q, s, nq, ns, idx, width, x, cin, kp, n_kp, inv_ext, wf, nnorm, st);
         else if (cin <= 16) launch_narrow<16>(q, s, nq, ns, idx, width, x, cin, kp, n_kp, inv_ext, wf, nnorm, st);
         else if (cin <= 32) launch_narrow<32>(q, s, nq, ns, idx, width, x, cin, kp, n_kp, inv_ext, wf, nnorm, st);
         else launch_narrow<64>(q, s, nq, ns, idx, width, x, cin, kp, n_kp, inv_ext, wf, nnorm, st);

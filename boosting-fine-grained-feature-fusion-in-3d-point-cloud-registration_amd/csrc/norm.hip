@@ -308,23 +308,34 @@ layernorm_kernel(float* __restrict__ x, int64_t n, int d, const float* __restric
 //   npf = d // 3 // 2 * 2; dim_t[i] = T ** (2 * (i // 2) / npf);
 //   out[3 * ... ] interleaves sin (even i) / cos (odd i) of xyz_d * scale / dim_t,
 //   grouped per coordinate, then zero padding to d.
-__global__ void sine_pe_kernel(const float* __restrict__ xyz, int64_t n, int d, int npf,
-                               float temperature, float scale, float* __restrict__ out) {
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n * d) return;
-    const int64_t r = t / d;
-    const int col = (int)(t - r * d);
-    float y = 0.f;
-    if (col < 3 * npf) {
-        const int dim = col / npf, i = col - dim * npf;
-        // torch: stack([sin(pd[..., 0::2]), cos(pd[..., 1::2])], -1).reshape -> pairs (sin, cos)
-        const int pair = i >> 1, is_cos = i & 1;
-        const int src_i = 2 * pair + is_cos;   // sin uses even feature 2p, cos odd 2p+1
-        const float dim_t = powf(temperature, (float)(2 * (src_i / 2)) / (float)npf);
-        const float pd = (xyz[r * 3 + dim] * scale) / dim_t;
-        y = is_cos ? cosf(pd) : sinf(pd);
+// kPeRows rows per 256-thread block; the npf/2 distinct dim_t values are computed once per
+// block into LDS (same powf expression, so the same bits as computing them per element).
+constexpr int kPeRows = 8;
+constexpr int kPeMaxPairs = 512;
+
+__global__ void __launch_bounds__(256)
+sine_pe_kernel(const float* __restrict__ xyz, int64_t n, int d, int npf, float temperature,
+               float scale, float* __restrict__ out) {
+    __shared__ float dim_t[kPeMaxPairs];
+    for (int p = threadIdx.x; p < npf / 2; p += blockDim.x)
+        dim_t[p] = powf(temperature, (float)(2 * p) / (float)npf);
+    __syncthreads();
+    const int64_t r0 = (int64_t)blockIdx.x * kPeRows;
+    const int rows = (int)min<int64_t>(kPeRows, n - r0);
+    for (int e = threadIdx.x; e < rows * d; e += blockDim.x) {
+        const int rr = e / d, col = e - rr * d;
+        const int64_t r = r0 + rr;
+        float y = 0.f;
+        if (col < 3 * npf) {
+            const int dim = col / npf, i = col - dim * npf;
+            // torch: stack([sin(pd[..., 0::2]), cos(pd[..., 1::2])], -1).reshape -> (sin, cos)
+            // pairs; sin uses even feature 2p, cos odd 2p+1, both with dim_t[p]
+            const int pair = i >> 1, is_cos = i & 1;
+            const float pd = (xyz[r * 3 + dim] * scale) / dim_t[pair];
+            y = is_cos ? cosf(pd) : sinf(pd);
+        }
+        out[r * d + col] = y;
     }
-    out[t] = y;
 }
 
 }  // namespace
@@ -409,8 +420,8 @@ extern "C" int fgr_sine_pos_embed(const float* xyz, int64_t n, int32_t d_model, 
     FGR_REQUIRE(n == 0 || (xyz && out), "fgr_sine_pos_embed: null pointer");
     if (n == 0) return FGR_OK;
     const int npf = d_model / 3 / 2 * 2;
-    const int64_t tot = n * d_model;
-    hipLaunchKernelGGL(sine_pe_kernel, dim3((unsigned)ceil_div(tot, 256)), dim3(256), 0,
+    FGR_REQUIRE(npf / 2 <= kPeMaxPairs, "fgr_sine_pos_embed: d_model %d too large", d_model);
+    hipLaunchKernelGGL(sine_pe_kernel, dim3((unsigned)ceil_div(n, kPeRows)), dim3(256), 0,
                        as_stream(stream), xyz, n, d_model, npf, temperature, scale, out);
     FGR_CHECK_LAUNCH("sine_pe_kernel");
     return FGR_OK;

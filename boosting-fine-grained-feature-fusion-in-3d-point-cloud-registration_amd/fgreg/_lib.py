@@ -54,12 +54,14 @@ SIGNATURES = {
     'fgr_split_weights_h3_bytes': [_i32, _i32, ctypes.POINTER(_sz)],
     'fgr_split_weights_h3': [_vp, _i32, _i32, _i64, _i64, _vp, _vp],
     'fgr_gemm_f16x3': [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _vp],
+    'fgr_gemm_rows_f16x3': [_vp, _i64, _vp, _vp, _f32, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _i64,
+                            _i32, _i32, _i32, _i32, _vp],
     'fgr_procrustes': [_vp, _vp, _vp, _i64, _i64, _f32, _vp, _vp],
     'fgr_pair_pose': [_vp, _vp, _vp, _i64, _vp, _i32, _i32, _f32, _vp, _vp],
 }
 
 NB_INDEX, NB_DIST = 0, 1
-ACT_NONE, ACT_LEAKY, ACT_RELU = 0, 1, 2
+ACT_NONE, ACT_LEAKY, ACT_RELU, ACT_RELU_RES_LEAKY = 0, 1, 2, 3
 
 _lib = None
 

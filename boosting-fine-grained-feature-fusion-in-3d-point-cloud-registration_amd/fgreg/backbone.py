@@ -270,9 +270,13 @@ class my_Bottle2neck(nn.Module):  # noqa: N801 -- reference name (res2net.py:84)
             self._folded = (key, w1, b1, ws, w3d, b3d, chain)
         return self._folded[1:]
 
-    def forward(self, x):
+    def forward(self, x, shortcut=None):
+        """-> relu(bn3(conv3(cat)) + downsample(x)); with ``shortcut`` (the enclosing
+        bottleneck block's identity shortcut) -> LeakyReLU_0.1(that + shortcut), fused into
+        the last GEMM's epilogue (finegrained_kpconv_blocks.py:715-725)."""
         if self.training:
-            return self._forward_train(x)
+            y = self._forward_train(x)
+            return y if shortcut is None else F.leaky_relu(y + shortcut, 0.1)
         w1, b1, ws, w3d, b3d, chain = self._folded_params()
         out = linear(x, w1, b1, act=ops.ACT_RELU)
         w = self.width
@@ -288,6 +292,8 @@ class my_Bottle2neck(nn.Module):  # noqa: N801 -- reference name (res2net.py:84)
                 ops.res2net_chain(out, w, self.scale, chain[2], chain[1], x, cat_in, split6=True)
             else:
                 ops.res2net_chain(out, w, self.scale, chain[0], chain[1], x, cat_in)
+            if shortcut is not None:
+                return linear(cat_in, w3d, b3d, act=ops.ACT_RELU_RES_LEAKY, residual=shortcut)
             return linear(cat_in, w3d, b3d, act=ops.ACT_RELU)
         cat_in = torch.empty((x.shape[0], w * self.scale + (x.shape[1] if self.downsample is not None else 0)),
                              dtype=x.dtype, device=x.device)
@@ -301,8 +307,10 @@ class my_Bottle2neck(nn.Module):  # noqa: N801 -- reference name (res2net.py:84)
             cat_in[:, self.nums * w:self.scale * w] = out[:, self.nums * w:self.scale * w]
         if self.downsample is not None:
             cat_in[:, self.scale * w:] = x
-            return torch._addmm_activation(b3d, cat_in, w3d.t())
-        return (torch.addmm(b3d, cat_in, w3d.t()) + x).relu_()
+            y = torch._addmm_activation(b3d, cat_in, w3d.t())
+        else:
+            y = (torch.addmm(b3d, cat_in, w3d.t()) + x).relu_()
+        return y if shortcut is None else F.leaky_relu(y + shortcut, 0.1)
 
     def _forward_train(self, x):
         out = F.relu(self.bn1(self.conv1(x)))
@@ -329,8 +337,8 @@ class my_res2Net(nn.Module):  # noqa: N801 -- reference name (res2net.py:231)
         self.layer1 = nn.Sequential(block(in_dim, out_dim, 1, downsample=downsample,
                                           stype='normal', baseWidth=baseWidth, scale=scale))
 
-    def forward(self, x):
-        return self.layer1(x)
+    def forward(self, x, shortcut=None):
+        return self.layer1(x) if shortcut is None else self.layer1[0](x, shortcut)
 
 
 def _level_inputs(block, layer_ind, batch):
@@ -402,13 +410,14 @@ class ResnetBottleneckBlock(nn.Module):
         y, nnorm = self.KPConv.forward_unnormalized(q, s, idx, x)
         y = self.batch_norm_conv(y, off_post, lens_post, row_div=nnorm)
         # res2net ends in ReLU, so the reference's LeakyReLU at :715 is the identity here
-        y = self.res2net(y)
         shortcut = ops.max_pool(features, idx) if 'strided' in self.block_name else features
         if isinstance(self.unary_shortcut, UnaryBlock):
+            y = self.res2net(y)
             # LeakyReLU(y + IN(shortcut @ W^T)) in one kernel (:722-725)
             return self.unary_shortcut(shortcut, off_post, lens_post, residual=y,
                                        post_act=ops.ACT_LEAKY)
-        return F.leaky_relu(y + shortcut, 0.1)
+        # identity shortcut: LeakyReLU(y + shortcut) in the Res2Net's last GEMM epilogue
+        return self.res2net(y, shortcut=shortcut)
 
 
 def block_decider(block_name, radius, in_dim, out_dim, layer_ind, config, flag=False):

@@ -12,15 +12,26 @@
   the 3DMatch fixture's pose misses the 1e-4 bar (1.3e-4), so it is opt-in only.
 Split weights are built once and cached against the fp32 tensor's identity, data pointer
 and version (a checkpoint load, .to() or in-place update invalidates the cache).
+
+In f16x3 mode, short contractions (K <= 256) can run on fgr_gemm_rows_f16x3 instead, which
+keeps a W panel in LDS and whole A rows in registers and fuses the LayerNorm (+ positional
+add) producing A into its row loads (``linear(..., ln=norm, add=pos)``). ``FGREG_ROWS``:
+'1' for the LayerNorm-fused calls, '2' for every eligible call, '0' (default) never (then
+``ln`` / ``add`` run as a separate fgr_layernorm launch). Measured on MI355X it is still
+slower than the LayerNorm launch + tiled GEMM at the transformer's shapes (QKV 9493 x 768 x
+256: 72 vs 37 us), so it is opt-in until it is reworked.
 """
 import os
 
 import torch
+import torch.nn.functional as F
 
 from . import _lib
-from .ops import ACT_NONE, ACT_RELU, _begin, _dev, _end, _ptr, _stream
+from . import ops
+from .ops import ACT_NONE, ACT_RELU, ACT_RELU_RES_LEAKY, _begin, _dev, _end, _ptr, _stream
 
 MODE = os.environ.get('FGREG_GEMM', 'f16x3')
+ROWS = os.environ.get('FGREG_ROWS', '0')
 
 
 def set_mode(mode):
@@ -83,10 +94,11 @@ def _valid(ent, w):
             and ent.ptr == w.data_ptr())            # .to() / load_state_dict swap .data
 
 
-def split_weight3(w: torch.Tensor, transpose=False, tag=None, kind=3):
-    """Cached split image of w (kind 3: bf16x6, kind 'h3': f16x3)."""
+def split_weight3(w: torch.Tensor, transpose=False, tag=None, kind=3, cache=True):
+    """Split image of w (kind 3: bf16x6, kind 'h3': f16x3), cached unless ``cache`` is False
+    (operands that change every call, e.g. the loss's feature matrices)."""
     ck = (id(w), transpose, tag, kind)
-    ent = _CACHE.get(ck)
+    ent = _CACHE.get(ck) if cache else None
     if not _valid(ent, w):
         cls = SplitWeight3 if kind == 3 else SplitWeightH3
         if transpose:                    # (K, Cin, Cout) as W[n = cout][k = K*Cin + cin]
@@ -95,7 +107,8 @@ def split_weight3(w: torch.Tensor, transpose=False, tag=None, kind=3):
         else:
             w2 = w.contiguous()
             ent = cls(w2, w2.shape[0], w2.shape[1], w2.shape[1], 1, w)
-        _CACHE[ck] = ent
+        if cache:
+            _CACHE[ck] = ent
     return ent
 
 
@@ -109,10 +122,37 @@ def split_weight(w: torch.Tensor, transpose=False, tag=None) -> SplitWeight:
     return ent
 
 
+def _rows_ok(x, k, add, act):
+    return (k <= 256 and k % 8 == 0 and act in (ACT_NONE, ACT_RELU, ACT_RELU_RES_LEAKY)
+            and x.stride(1) == 1 and x.stride(0) % 4 == 0 and x.data_ptr() % 16 == 0
+            and (add is None or (add.stride(1) == 1 and add.stride(0) % 4 == 0
+                                 and add.data_ptr() % 16 == 0)))
+
+
+def _linear_rows(x, w, bias, act, residual, tag, out, ln, add, cache):
+    n, k = w.shape
+    sw = split_weight3(w, False, tag, 'h3', cache=cache)
+    m = x.shape[0]
+    if out is None:
+        out = torch.empty((m, n), dtype=torch.float32, device=x.device)
+    g, b, eps = (ln.weight, ln.bias, float(ln.eps)) if ln is not None else (None, None, 0.0)
+    t0 = _begin('gemm')
+    _lib.check(_lib.load().fgr_gemm_rows_f16x3(
+        _ptr(x), x.stride(0), _ptr(g), _ptr(b), eps, _ptr(add),
+        add.stride(0) if add is not None else 0, _ptr(sw.img), _ptr(out), out.stride(0),
+        _ptr(bias), _ptr(residual), residual.stride(0) if residual is not None else 0, m, n, k,
+        act, _stream()), 'fgr_gemm_rows_f16x3')
+    _end('gemm', t0, 2 * m * n * k)
+    return out
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act=ACT_NONE, residual=None,
-           transpose=False, tag=None, out=None) -> torch.Tensor:
-    """act(x @ W^T + bias (+ residual)), W = w (n, k), or W = w.reshape(k, n).t() if
-    transpose (e.g. KPConv weights (K, Cin, Cout) used as (K*Cin, Cout))."""
+           transpose=False, tag=None, out=None, ln=None, add=None, cache=True) -> torch.Tensor:
+    """act(A @ W^T + bias (+ residual)), W = w (n, k), or W = w.reshape(k, n).t() if
+    transpose (e.g. KPConv weights (K, Cin, Cout) used as (K*Cin, Cout)); A = x, or
+    A = ln(x) (+ add) for an nn.LayerNorm ``ln`` and / or an added tensor ``add`` (fused into
+    the GEMM's row loads where fgr_gemm_rows_f16x3 applies). ACT_RELU_RES_LEAKY applies the
+    residual after the ReLU: LeakyReLU_0.1(ReLU(A @ W^T + bias) + residual)."""
     n = w.shape[-1] if transpose else w.shape[0]
     k = w.numel() // n if transpose else w.shape[1]
     assert x.dim() == 2 and x.shape[1] == k and x.dtype == torch.float32
@@ -120,6 +160,19 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act=ACT_NONE, residual=N
         _dev(x)
     if residual is not None:
         assert residual.shape == (x.shape[0], n) and residual.stride(1) == 1
+    if add is not None:
+        assert add.shape == x.shape and add.dtype == torch.float32
+    fused = ln is not None or add is not None
+    if (MODE == 'f16x3' and not transpose and (ROWS == '2' or (fused and ROWS == '1'))
+            and _rows_ok(x, k, add, act)):
+        return _linear_rows(x, w, bias, act, residual, tag, out, ln, add, cache)
+    if fused:
+        x = (ops.layernorm(x.contiguous(), ln.weight, ln.bias, ln.eps, add=add)
+             if ln is not None else x + add)
+    if act == ACT_RELU_RES_LEAKY and MODE != 'f16x3':
+        y = linear(x, w, bias, ACT_RELU, None, transpose, tag, cache=cache)
+        y = F.leaky_relu(y + residual, 0.1)
+        return out.copy_(y) if out is not None else y
     if MODE in ('bf16x6', 'f16x3'):
         if not (x.stride(1) == 1 and (k % 8 != 0 or (x.stride(0) % 4 == 0
                                                      and x.data_ptr() % 16 == 0))):
@@ -127,7 +180,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act=ACT_NONE, residual=N
             if k % 8 == 0 and x.data_ptr() % 16 != 0:
                 x = x.clone()
         h3 = MODE == 'f16x3'
-        sw = split_weight3(w, transpose, tag, 'h3' if h3 else 3)
+        sw = split_weight3(w, transpose, tag, 'h3' if h3 else 3, cache=cache)
         m = x.shape[0]
         if out is None:
             out = torch.empty((m, n), dtype=torch.float32, device=x.device)

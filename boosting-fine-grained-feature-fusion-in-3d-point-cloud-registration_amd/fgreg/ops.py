@@ -13,7 +13,7 @@ from typing import Sequence, Tuple
 import torch
 
 from . import _lib
-from ._lib import ACT_LEAKY, ACT_NONE, ACT_RELU, NB_DIST, NB_INDEX  # noqa: F401
+from ._lib import ACT_LEAKY, ACT_NONE, ACT_RELU, ACT_RELU_RES_LEAKY, NB_DIST, NB_INDEX  # noqa: F401
 
 
 def _ptr(t):

@@ -47,8 +47,10 @@ enum {
                          nearest, ties by index (neighbors.cpp:211-332, :260-261)  */
 };
 
-/* activation codes */
-enum { FGR_ACT_NONE = 0, FGR_ACT_LEAKY = 1, FGR_ACT_RELU = 2 };
+/* activation codes; FGR_ACT_RELU_RES_LEAKY (the f16x3 GEMMs only) applies the residual AFTER
+ * the ReLU: C = LeakyReLU_0.1(ReLU(A.W + bias) + R) -- a Res2Net block output plus its
+ * identity shortcut (finegrained_kpconv_blocks.py:715-725) in one epilogue. */
+enum { FGR_ACT_NONE = 0, FGR_ACT_LEAKY = 1, FGR_ACT_RELU = 2, FGR_ACT_RELU_RES_LEAKY = 3 };
 
 int fgr_abi_version(void);
 const char* fgr_last_error(void);
@@ -195,6 +197,18 @@ int fgr_split_weights_h3(const float* w, int32_t n, int32_t k, int64_t stride_n,
 int fgr_gemm_f16x3(const float* a, int64_t lda, const void* w_img, float* c, int64_t ldc,
                    const float* bias, const float* r, int64_t ldr, int32_t m, int32_t n,
                    int32_t k, int32_t act, void* stream);
+
+/* Row-resident f16x3 GEMM for short contractions (k <= 256, k % 8 == 0) with the LayerNorm
+ * (+ positional add) that produces its input fused into the row loads -- the transformer's
+ * norm -> Linear pairs (transformers.py:193-238: norm1/2 + pos -> in_proj, norm3 -> linear1):
+ *   A = ln_gamma ? LN(x) * ln_gamma + ln_beta (+ add) : x (+ add)   (LN eps ln_eps, biased var)
+ *   C = act(A . W^T + bias (+ R))                                    (act as fgr_gemm_f16x3)
+ * Each A row is scaled by its exact max (no online rescale). w_img from fgr_split_weights_h3;
+ * x, add, w_img 16-B aligned with ldx, ld_add % 4 == 0. */
+int fgr_gemm_rows_f16x3(const float* x, int64_t ldx, const float* ln_gamma, const float* ln_beta,
+                        float ln_eps, const float* add, int64_t ld_add, const void* w_img, float* c,
+                        int64_t ldc, const float* bias, const float* r, int64_t ldr, int32_t m,
+                        int32_t n, int32_t k, int32_t act, void* stream);
 
 /* ---- attention ---------------------------------------------------------------------
  * Multi-head scaled-dot-product attention core of nn.MultiheadAttention

@@ -37,12 +37,17 @@ def test_kpconv_block_vs_reference(gpu):
     assert torch.equal(mp.cpu(), torch.from_numpy(g['maxpool']))
 
 
-@pytest.mark.parametrize('cin', [1, 3, 16, 32, 64, 128, 256])
-def test_kpconv_gather_vs_torch(gpu, cin):
-    """Gather-weight stage vs the fp32 torch restatement (all channel widths in the configs)."""
+@pytest.mark.parametrize('cin,H,prepass', [(1, 50, '0'), (1, 7, '0'), (3, 50, '0'), (16, 50, '0'),
+                                           (32, 50, '0'), (64, 50, '0'), (128, 50, '0'),
+                                           (256, 50, '0'), (128, 50, '1'), (256, 70, '1'),
+                                           (64, 130, '0')])
+def test_kpconv_gather_vs_torch(gpu, cin, H, prepass, monkeypatch):
+    """Gather-weight stage vs the fp32 torch restatement (all channel widths in the configs;
+    the cin = 1 stem kernel; wide kernels with the inline and the pre-pass normaliser)."""
     import fgreg.ops as ops
-    rng = np.random.default_rng(cin)
-    ns, nq, H = 900, 700, 50
+    monkeypatch.setenv('FGR_GATHER_PREPASS', prepass)
+    rng = np.random.default_rng(cin + H)
+    ns, nq = 900, 700
     s = rng.uniform(-1, 1, (ns, 3)).astype(np.float32)
     q = s[rng.choice(ns, nq, replace=False)] + rng.normal(0, 0.01, (nq, 3)).astype(np.float32)
     idx = rng.integers(0, ns, (nq, H))
@@ -194,9 +199,12 @@ def test_attention_split_is_fp32_accurate(gpu, scale, split):
     assert errs[split] < 4 * errs['fp32'] + 1e-7, errs
 
 
-def test_transformer_layer_vs_reference(gpu):
+@pytest.mark.parametrize('rows', ['0', '1'])
+def test_transformer_layer_vs_reference(gpu, rows):
     """One TransformerCrossEncoderLayer.forward_pre (transformers.py:183-244), B = 2 with
-    unequal lengths, against the reference module's output (padded rows excluded)."""
+    unequal lengths, against the reference module's output (padded rows excluded); the
+    deferred-bias path and the LayerNorm-fused row-GEMM path (FGREG_ROWS=1)."""
+    from fgreg import linear as fl
     from fgreg.transformer import Segments, TransformerCrossEncoderLayer
     g = golden('transformer_layer')
     layer = TransformerCrossEncoderLayer(64, 8, 128, 0.0, normalize_before=True,
@@ -212,9 +220,14 @@ def test_transformer_layer_vs_reference(gpu):
     x = torch.from_numpy(np.concatenate(rows)).to(gpu)
     pos = torch.from_numpy(np.concatenate(prow)).to(gpu)
     seg = Segments(ns + nt, gpu)
-    with torch.no_grad():
-        y, pending = layer.forward_packed(x.clone(), pos, seg)
-        y = (y + pending).cpu().numpy()
+    old = fl.ROWS
+    try:
+        fl.ROWS = rows
+        with torch.no_grad():
+            y, pending = layer.forward_packed(x.clone(), pos, seg)
+            y = (y if pending is None else y + pending).cpu().numpy()
+    finally:
+        fl.ROWS = old
     ref = np.concatenate([g['src_out'][:ns[b], b] for b in range(2)] +
                          [g['tgt_out'][:nt[b], b] for b in range(2)])
     assert rel_err(y, ref) < TOL
@@ -368,3 +381,50 @@ def test_gemm_f16x3_tiles(gpu, tile, monkeypatch):
             assert rel_err(out, ref) < 2e-6, (tile, m, n, k)
     finally:
         fl.set_mode(old)
+
+
+@pytest.mark.parametrize('m,n,k', [(1000, 768, 256), (333, 200, 96), (50, 16, 64), (17, 3, 40),
+                                   (2000, 1024, 128), (129, 70, 256)])
+def test_gemm_rows_f16x3(gpu, m, n, k, monkeypatch):
+    """Row-resident f16x3 GEMM (fgr_gemm_rows_f16x3) vs fp64: plain, LayerNorm-fused
+    (+ positional add) with bias / ReLU / residual epilogues, ragged M / N, K below one
+    k-step pair (zero-filled W panel). LayerNorm reference in fp64 from the fp32 inputs."""
+    from fgreg import linear as fl
+    from fgreg import ops
+    g = torch.Generator().manual_seed(m * 7 + n + k)
+    x = torch.randn(m, k, generator=g) * 3 + 1
+    pos = torch.randn(m, k, generator=g)
+    w = torch.randn(n, k, generator=g) / math.sqrt(k)
+    b = torch.randn(n, generator=g)
+    r = torch.randn(m, n, generator=g)
+    ln = torch.nn.LayerNorm(k)
+    with torch.no_grad():
+        ln.weight.copy_(1 + 0.2 * torch.randn(k, generator=g))
+        ln.bias.copy_(0.2 * torch.randn(k, generator=g))
+    xd = x.double()
+    mu = xd.mean(1, keepdim=True)
+    var = ((xd - mu) ** 2).mean(1, keepdim=True)
+    a = (xd - mu) / torch.sqrt(var + ln.eps) * ln.weight.double() + ln.bias.double() + pos.double()
+    ref_ln = a @ w.double().t() + b.double()
+    ref = xd @ w.double().t() + b.double()
+    X, P, W, B, R, LN = x.to(gpu), pos.to(gpu), w.to(gpu), b.to(gpu), r.to(gpu), ln.to(gpu)
+    old_mode, old_rows = fl.MODE, fl.ROWS
+    try:
+        fl.set_mode('f16x3')
+        fl.ROWS = '2'
+        assert rel_err(fl.linear(X, W, B), ref) < 2e-6
+        assert rel_err(fl.linear(X, W, B, act=ops.ACT_RELU), ref.clamp_min(0)) < 2e-6
+        assert rel_err(fl.linear(X, W, B, residual=R), ref + r.double()) < 2e-6
+        assert rel_err(fl.linear(X, W, B, ln=LN, add=P), ref_ln) < 2e-6
+        assert rel_err(fl.linear(X, W, B, act=ops.ACT_RELU, ln=LN, add=P),
+                       ref_ln.clamp_min(0)) < 2e-6
+        lk = torch.nn.functional.leaky_relu(ref.clamp_min(0) + r.double(), 0.1)
+        assert rel_err(fl.linear(X, W, B, act=ops.ACT_RELU_RES_LEAKY, residual=R), lk) < 2e-6
+        fl.ROWS = '0'      # same calls through fgr_layernorm + the tiled GEMM
+        assert rel_err(fl.linear(X, W, B, ln=LN, add=P), ref_ln) < 2e-6
+        assert rel_err(fl.linear(X, W, B, act=ops.ACT_RELU_RES_LEAKY, residual=R), lk) < 2e-6
+        fl.set_mode('bf16x6')   # emulated epilogue in the other modes
+        assert rel_err(fl.linear(X, W, B, act=ops.ACT_RELU_RES_LEAKY, residual=R), lk) < 2e-6
+    finally:
+        fl.set_mode(old_mode)
+        fl.ROWS = old_rows
