@@ -84,7 +84,7 @@ def main():
     np.random.seed(0)
     model = fgreg.RegTR(cfg).to(dev).eval()
     P = args.pairs_per_gpu
-    src, tgt, _ = make_batch('modelnet', P, start=rank * P)     # this rank's shard of pairs
+    src, tgt, pose_gt = make_batch('modelnet', P, start=rank * P)   # this rank's shard of pairs
     batch_src = [torch.from_numpy(s).to(dev) for s in src]
     batch_tgt = [torch.from_numpy(t).to(dev) for t in tgt]
     from fgreg import dist as fdist
@@ -128,6 +128,10 @@ def main():
             step()
         torch.cuda.synchronize()
         ops.TIMER = None
+        # test-step tail: compute_loss + _compute_metrics on the
+        # outputs of one step, outside the timed region
+        tail_ms, tail_inputs = test_tail(model, batch_src, batch_tgt, src, tgt, pose_gt, dev,
+                                          args.steps)
 
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if dist is not None:
@@ -151,7 +155,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_seconds > 0:
-        cpu = cpu_baseline(cfg, model, src, tgt, args.cpu_seconds)
+        cpu = cpu_baseline(cfg, model, src, tgt, args.cpu_seconds, tail_inputs)
 
     if rank == 0:
         pairs = world * P * args.steps
@@ -202,6 +206,9 @@ def main():
                               'matrix_pipe_frac': PIPE.get(lin.MODE, 1) * m_achieved /
                               (F16_MFMA_PEAK_TFLOPS if lin.MODE != 'fp32'
                                else FP32_MFMA_PEAK_TFLOPS)},
+            'test_tail': {'what': 'compute_loss + _compute_metrics of one step (8 pairs: '
+                                  'overlap pyramid, BCE, 2x InfoNCE, CorrCriterion, se3_compare)',
+                          'ms_per_step': tail_ms},
             'cpu_baseline': cpu,
         }
         print(json.dumps(line), flush=True)
@@ -209,7 +216,37 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(cfg, model, src, tgt, budget_s):
+def _overlap_flags(a, b, pose, radius=0.05):
+    """Per-point ground-truth overlap flags of a pair (nearest point of the other cloud
+    under the true pose within radius), the loss input the reference's dataset provides."""
+    from scipy.spatial import cKDTree
+    aw = a @ pose[:, :3].T + pose[:, 3]
+    return ((cKDTree(b).query(aw)[0] < radius).astype(np.float32),
+            (cKDTree(aw).query(b)[0] < radius).astype(np.float32))
+
+
+def test_tail(model, batch_src, batch_tgt, src, tgt, pose_gt, dev, iters):
+    """Times fgreg.loss.compute_loss + compute_metrics on the outputs of one forward."""
+    from fgreg import loss as floss
+    flags = [_overlap_flags(s, t, p) for s, t, p in zip(src, tgt, pose_gt)]
+    with torch.no_grad():
+        batch = {'src_xyz': batch_src, 'tgt_xyz': batch_tgt}
+        out = model(batch)                                  # fills batch['kpconv_meta']
+        batch['pose'] = torch.from_numpy(pose_gt).to(dev)
+        batch['src_overlap'] = [torch.from_numpy(f[0]).to(dev) for f in flags]
+        batch['tgt_overlap'] = [torch.from_numpy(f[1]).to(dev) for f in flags]
+        floss.compute_loss(model, out, batch)               # warm (weight splits)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            floss.compute_loss(model, out, batch)
+            floss.compute_metrics(out, batch)
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) / iters * 1e3
+    return ms, (out, batch)
+
+
+def cpu_baseline(cfg, model, src, tgt, budget_s, tail_inputs=None):
     """CPU restatement (oracle/model_oracle.py, "port") on the same pairs, for ~budget_s."""
     sys.path.insert(0, os.path.join(REPO, 'oracle'))
     import model_oracle as mo
@@ -223,9 +260,24 @@ def cpu_baseline(cfg, model, src, tgt, budget_s):
         t_tot += time.perf_counter() - t0
         n_pairs += 1
         it += 1
-    return {'value': n_pairs / t_tot, 'unit': 'pairs/s', 'cores': threads, 'kind': 'port',
-            'sample': f'{n_pairs} ModelNet-like pairs (B=1 forwards) of the same workload, '
-                      f'{t_tot:.1f} s, torch CPU fp32 with {threads} threads'}
+    res = {'value': n_pairs / t_tot, 'unit': 'pairs/s', 'cores': threads, 'kind': 'port',
+           'sample': f'{n_pairs} ModelNet-like pairs (B=1 forwards) of the same workload, '
+                     f'{t_tot:.1f} s, torch CPU fp32 with {threads} threads'}
+    if tail_inputs is not None:       # the test-step tail on the same outputs (loss_oracle)
+        import loss_oracle as lo
+        out, batch = tail_inputs
+        cpu = lambda v: [t.cpu() for t in v] if isinstance(v, list) else v.cpu()
+        pred = {k: cpu(v) for k, v in out.items()}
+        meta = {k: cpu(batch['kpconv_meta'][k]) for k in ('points', 'pools', 'stack_lengths')}
+        b = {'pose': batch['pose'].cpu(), 'src_overlap': cpu(batch['src_overlap']),
+             'tgt_overlap': cpu(batch['tgt_overlap']), 'kpconv_meta': meta}
+        W = model.feature_criterion.W.detach().cpu()
+        W_un = model.feature_criterion_un.W.detach().cpu()
+        t0 = time.perf_counter()
+        lo.compute_loss(cfg, W, W_un, pred, b)
+        lo.pose_errors(pred['pose'], b['pose'])
+        res['test_tail_ms'] = (time.perf_counter() - t0) * 1e3
+    return res
 
 
 if __name__ == '__main__':

@@ -56,6 +56,13 @@ SIGNATURES = {
     'fgr_gemm_f16x3': [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _vp],
     'fgr_gemm_rows_f16x3': [_vp, _i64, _vp, _vp, _f32, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _i64,
                             _i32, _i32, _i32, _i32, _vp],
+    'fgr_overlap_pool': [_vp, _i64, _vp, _i64, _i32, _vp, _vp],
+    'fgr_bce_logits_mean': [_vp, _i64, _vp, _i64, _vp, _vp],
+    'fgr_transform_points': [_vp, _i64, _vp, _i32, _vp, _i32, _vp, _vp],
+    'fgr_infonce_rows': [_vp, _i64, _vp, _vp, _vp, _vp, _i32, _i64, _f32, _f32, _vp, _vp, _vp],
+    'fgr_infonce_reduce': [_vp, _vp, _vp, _i32, _vp, _vp],
+    'fgr_corr_loss': [_vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp],
+    'fgr_se3_compare': [_vp, _vp, _i32, _i32, _vp, _vp, _vp],
     'fgr_procrustes': [_vp, _vp, _vp, _i64, _i64, _f32, _vp, _vp],
     'fgr_pair_pose': [_vp, _vp, _vp, _i64, _vp, _i32, _i32, _f32, _vp, _vp],
 }

@@ -1,0 +1,185 @@
+"""Test-step tail on libfgreg: the reference's ``compute_loss``
+(models/finegrained_regtr.py:252-309) and ``_compute_metrics`` (generic_reg_model.py:203-215)
+on the packed forward outputs, so ``GenericRegModel.test_step`` runs at GPU speed.
+
+* ``compute_overlaps``  finegrained_kpconv.py:545-571      fgr_overlap_pool per level
+* overlap loss          nn.BCEWithLogitsLoss (mean)          fgr_bce_logits_mean
+* feature loss          InfoNCELossFull (feature_loss.py:246-314): the match logits
+                        A W_sym P^T as two f16x3 GEMMs over all pairs at once (A W_sym, then
+                        against every positive row), the masked log-sum-exp per anchor row
+                        (fgr_infonce_rows) and the per-pair / batch means (fgr_infonce_reduce)
+* correspondence loss   CorrCriterion('mae') both directions  fgr_corr_loss
+* metrics               se3_compare of every layer's pose     fgr_se3_compare
+Same keys, weights (finegrained_regtr.py:94-98) and reduction order as the reference; all
+arithmetic in fp32 on the GPU (no CPU path: the ops raise on CPU tensors).
+"""
+import torch
+
+from . import _lib, ops
+from .linear import linear
+from .ops import _c, _dev, _ptr, _stream
+
+
+def overlap_pool(prev: torch.Tensor, pools: torch.Tensor) -> torch.Tensor:
+    """One compute_overlaps step: (N_prev,) overlaps, (N_q, H) pool table -> (N_q,)."""
+    _dev(prev, pools)
+    prev, pools = _c(prev, torch.float32), _c(pools, torch.int64)
+    out = torch.empty((pools.shape[0],), dtype=torch.float32, device=prev.device)
+    _lib.check(_lib.load().fgr_overlap_pool(_ptr(prev), prev.shape[0], _ptr(pools), pools.shape[0],
+                                            pools.shape[1], _ptr(out), _stream()),
+               'fgr_overlap_pool')
+    return out
+
+
+def compute_overlaps(batch):
+    """finegrained_kpconv.py:545-571: {'pyr_0': cat(src_overlap + tgt_overlap), 'pyr_p': ...}."""
+    meta = batch['kpconv_meta']
+    pyr = {'pyr_0': torch.cat(list(batch['src_overlap']) + list(batch['tgt_overlap']),
+                              dim=0).float()}
+    for p in range(1, len(meta['points'])):
+        pyr[f'pyr_{p}'] = overlap_pool(pyr[f'pyr_{p - 1}'], meta['pools'][p - 1])
+    return pyr
+
+
+def bce_with_logits_mean(x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    _dev(x, y)
+    assert x.dim() == 1 and y.shape == x.shape and x.dtype == torch.float32
+    y = _c(y, torch.float32)
+    out = torch.empty((), dtype=torch.float32, device=x.device)
+    _lib.check(_lib.load().fgr_bce_logits_mean(_ptr(x), x.stride(0), _ptr(y), x.shape[0],
+                                               _ptr(out), _stream()), 'fgr_bce_logits_mean')
+    return out
+
+
+def transform_points(xyz, seg_off, pose, inverse=False) -> torch.Tensor:
+    """se3_transform_list over packed segments (pose (n_seg, 3, 4))."""
+    _dev(xyz, seg_off, pose)
+    xyz, pose = _c(xyz, torch.float32), _c(pose, torch.float32)
+    out = torch.empty_like(xyz)
+    _lib.check(_lib.load().fgr_transform_points(_ptr(xyz), xyz.shape[0], _ptr(seg_off),
+                                                seg_off.numel() - 1, _ptr(pose), int(inverse),
+                                                _ptr(out), _stream()), 'fgr_transform_points')
+    return out
+
+
+_WSYM = {}
+
+
+def _w_sym(W: torch.Tensor) -> torch.Tensor:
+    """triu(W) + triu(W)^T (feature_loss.py:280-281), kept per parameter version so its
+    split image is cached by linear()."""
+    key = id(W)
+    ent = _WSYM.get(key)
+    if ent is None or ent[0] is not W or ent[1] != W._version or ent[2] != W.data_ptr():
+        with torch.no_grad():
+            t = torch.triu(W.detach().float())
+            ent = (W, W._version, W.data_ptr(), (t + t.t()).contiguous())
+        _WSYM[key] = ent
+    return ent[3]
+
+
+def infonce(W, anchor_feat, positive_feat, anchor_xyz, positive_xyz, a_off, p_off, r_p, r_n):
+    """InfoNCELossFull.forward over B pairs packed along rows (pair b: anchor rows
+    a_off[b]..a_off[b+1], positive rows p_off[b]..p_off[b+1]) -> 0-d tensor."""
+    _dev(anchor_feat, positive_feat, anchor_xyz, positive_xyz, a_off, p_off)
+    A = _c(anchor_feat, torch.float32)
+    P = _c(positive_feat, torch.float32)
+    aw = linear(A, _w_sym(W))                          # A W_sym (W_sym symmetric)
+    logits = linear(aw, P, cache=False)                # (N_a, N_p) over all pairs
+    n_a, n_pairs = A.shape[0], a_off.numel() - 1
+    row_loss = torch.empty((n_a,), dtype=torch.float32, device=A.device)
+    row_mask = torch.empty_like(row_loss)
+    L = _lib.load()
+    axyz, pxyz = _c(anchor_xyz, torch.float32), _c(positive_xyz, torch.float32)
+    _lib.check(L.fgr_infonce_rows(_ptr(logits), logits.stride(0), _ptr(axyz), _ptr(pxyz),
+                                  _ptr(a_off), _ptr(p_off), n_pairs, n_a, float(r_p), float(r_n),
+                                  _ptr(row_loss), _ptr(row_mask), _stream()), 'fgr_infonce_rows')
+    out = torch.empty((), dtype=torch.float32, device=A.device)
+    _lib.check(L.fgr_infonce_reduce(_ptr(row_loss), _ptr(row_mask), _ptr(a_off), n_pairs,
+                                    _ptr(out), _stream()), 'fgr_infonce_reduce')
+    return out
+
+
+def corr_loss(xyz, corr, w, seg_off, pose) -> torch.Tensor:
+    """src (pose) + tgt (se3_inv(pose)) CorrCriterion('mae') with overlap weights."""
+    _dev(xyz, corr, w, seg_off, pose)
+    xyz, corr, w, pose = (_c(t, torch.float32) for t in (xyz, corr, w, pose))
+    out = torch.empty((), dtype=torch.float32, device=xyz.device)
+    _lib.check(_lib.load().fgr_corr_loss(_ptr(xyz), _ptr(corr), _ptr(w), _ptr(seg_off),
+                                         pose.shape[0], _ptr(pose), _ptr(out), _stream()),
+               'fgr_corr_loss')
+    return out
+
+
+def se3_compare(pred, gt):
+    """pred (L, B, 3, 4), gt (B, 3, 4) -> {'rot_deg': (L, B), 'trans': (L, B)}."""
+    _dev(pred, gt)
+    pred, gt = _c(pred, torch.float32), _c(gt, torch.float32)
+    n_layers, n_pairs = pred.shape[0], pred.shape[1]
+    rot = torch.empty((n_layers, n_pairs), dtype=torch.float32, device=pred.device)
+    trans = torch.empty_like(rot)
+    _lib.check(_lib.load().fgr_se3_compare(_ptr(pred), _ptr(gt), n_layers, n_pairs, _ptr(rot),
+                                           _ptr(trans), _stream()), 'fgr_se3_compare')
+    return {'rot_deg': rot, 'trans': trans}
+
+
+def weight_dict(cfg):
+    """finegrained_regtr.py:94-98."""
+    wd = {}
+    for k in ['overlap', 'feature', 'corr']:
+        for i in cfg.get(f'{k}_loss_on', [cfg.num_encoder_layers - 1]):
+            wd[f'{k}_{i}'] = cfg.get(f'wt_{k}')
+    wd['feature_un'] = cfg.wt_feature_un
+    return wd
+
+
+def compute_loss(model, pred, batch):
+    """RegTR.compute_loss (finegrained_regtr.py:252-309) -> dict of 0-d tensors with the
+    reference's keys; adds batch['overlap_pyr'] like the reference."""
+    cfg = model.cfg
+    if cfg.get('feature_loss_type', 'infonce') != 'infonce':
+        raise NotImplementedError('only the infonce feature loss is in the reference configs')
+    meta = batch['kpconv_meta']
+    pose_gt = _c(batch['pose'].float(), torch.float32)           # (B, 3, 4)
+    p = len(meta['stack_lengths']) - 1
+    pyr = compute_overlaps(batch)
+    batch['overlap_pyr'] = pyr
+    ov = pyr[f'pyr_{p}']
+    lens = [int(v) for v in meta['stack_lengths'][p].tolist()]
+    B = len(lens) // 2
+    dev = ov.device
+    seg_off = ops.offsets(lens, dev)
+    a_off, p_off = ops.offsets(lens[:B], dev), ops.offsets(lens[B:], dev)
+
+    losses = {}
+    logits = torch.cat(list(pred['src_overlap']) + list(pred['tgt_overlap']), dim=-2)
+    for i in cfg.overlap_loss_on:
+        losses[f'overlap_{i}'] = bce_with_logits_mean(logits[i, :, 0], ov)
+    src_kp, tgt_kp = torch.cat(list(pred['src_kp'])), torch.cat(list(pred['tgt_kp']))
+    axyz = transform_points(src_kp, a_off, pose_gt)
+    for i in cfg.feature_loss_on:
+        losses[f'feature_{i}'] = infonce(
+            model.feature_criterion.W, torch.cat([s[i] for s in pred['src_feat']]),
+            torch.cat([t[i] for t in pred['tgt_feat']]), axyz, tgt_kp, a_off, p_off,
+            cfg.r_p, cfg.r_n)
+    losses['feature_un'] = infonce(
+        model.feature_criterion_un.W, torch.cat(list(pred['src_feat_un'])),
+        torch.cat(list(pred['tgt_feat_un'])), axyz, tgt_kp, a_off, p_off, cfg.r_p, cfg.r_n)
+    xyz = torch.cat([src_kp, tgt_kp])
+    for i in cfg.corr_loss_on:
+        corr = torch.cat([w[i] for w in pred['src_kp_warped']] +
+                         [w[i] for w in pred['tgt_kp_warped']])
+        losses[f'corr_{i}'] = corr_loss(xyz, corr, ov, seg_off, pose_gt)
+    wd = weight_dict(cfg)
+    losses['total'] = torch.sum(torch.stack([losses[k] * wd[k] for k in losses]))
+    return losses
+
+
+def compute_metrics(pred, batch):
+    """GenericRegModel._compute_metrics (generic_reg_model.py:203-215)."""
+    metrics = {}
+    for k in [k for k in pred.keys() if k.startswith('pose')]:
+        err = se3_compare(pred[k], batch['pose'])
+        metrics[f'rot_err_deg{k[4:]}'] = err['rot_deg']
+        metrics[f'trans_err{k[4:]}'] = err['trans']
+    return metrics

@@ -269,6 +269,43 @@ int fgr_pair_pose(const float* xyz, const float* corr, const float* logits, int6
                   const int64_t* seg_off, int32_t n_pairs, int32_t n_layers, float threshold,
                   float* out, void* stream);
 
+/* ---- test-step tail --------------------------------------------
+ * What GenericRegModel.test_step runs after the forward (generic_reg_model.py:128-132),
+ * on packed tensors (clouds src_0..src_{B-1}, tgt_0..tgt_{B-1}):
+ *  fgr_overlap_pool     compute_overlaps, one level (finegrained_kpconv.py:560-569):
+ *                       out[q] = clamp(mean_{h: idx[q,h] < n_prev} prev[idx[q,h]], 0, 1),
+ *                       NaN for a row without valid entries (as the reference);
+ *  fgr_bce_logits_mean  nn.BCEWithLogitsLoss() on x[i * stride_x] vs y[i] (:264-267);
+ *  fgr_transform_points se3_transform_list (se3_torch.py:70-90): rows of segment s get
+ *                       pose[s] (3 x 4), or se3_inv(pose[s]) when inverse != 0;
+ *  fgr_infonce_rows     InfoNCELossFull.compute_infonce (feature_loss.py:268-296) per anchor
+ *                       row, given the match logits (n_anchor, ld) over ALL positive rows
+ *                       (columns of pair b: p_off[b]..p_off[b+1]): nearest positive by
+ *                       torch.cdist's matrix-multiply distance (lowest index on ties),
+ *                       row_mask = (its distance < r_p), points closer than r_n ignored,
+ *                       row_loss = logsumexp - positive logit;
+ *  fgr_infonce_reduce   sum(loss[mask]) / sum(mask) per pair, mean over pairs (:295, 314);
+ *  fgr_corr_loss        CorrCriterion('mae') for src (pose) + tgt (se3_inv(pose)) directions
+ *                       with overlap weights w (corr_loss.py:18-38, finegrained_regtr.py:283-296);
+ *  fgr_se3_compare      se3_compare(pred[l, b], gt[b]) (se3_torch.py:117-129) -> rotation
+ *                       error in degrees and translation error, (n_layers, n_pairs) each.
+ * The single-block reductions are deterministic. */
+int fgr_overlap_pool(const float* prev, int64_t n_prev, const int64_t* idx, int64_t nq,
+                     int32_t width, float* out, void* stream);
+int fgr_bce_logits_mean(const float* x, int64_t stride_x, const float* y, int64_t n, float* out,
+                        void* stream);
+int fgr_transform_points(const float* xyz, int64_t n, const int64_t* seg_off, int32_t n_seg,
+                         const float* pose, int32_t inverse, float* out, void* stream);
+int fgr_infonce_rows(const float* logits, int64_t ld, const float* axyz, const float* pxyz,
+                     const int64_t* a_off, const int64_t* p_off, int32_t n_pairs, int64_t n_anchor,
+                     float r_p, float r_n, float* row_loss, float* row_mask, void* stream);
+int fgr_infonce_reduce(const float* row_loss, const float* row_mask, const int64_t* a_off,
+                       int32_t n_pairs, float* out, void* stream);
+int fgr_corr_loss(const float* xyz, const float* corr, const float* w, const int64_t* seg_off,
+                  int32_t n_pairs, const float* pose, float* out, void* stream);
+int fgr_se3_compare(const float* pred, const float* gt, int32_t n_layers, int32_t n_pairs,
+                    float* rot_deg, float* trans, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -66,3 +66,28 @@ def gpu():
     import fgreg
     fgreg.load()
     return torch.device('cuda:0')
+
+
+OUT_KEYS = ['src_feat_un', 'tgt_feat_un', 'src_feat', 'tgt_feat', 'src_kp', 'tgt_kp',
+            'src_kp_warped', 'tgt_kp_warped', 'src_overlap', 'tgt_overlap']
+
+
+def loss_fixture(device='cpu'):
+    """-> (cfg, pred, batch, losses, metrics, pyr, W, W_un): the reference's forward outputs
+    (forward_modelnet_small) as per-cloud tensors, the loss inputs and the reference's own
+    compute_loss / _compute_metrics results (loss_modelnet_small)."""
+    cfg, _, src, tgt, meta, d = forward_fixture('forward_modelnet_small')
+    g = golden('loss_modelnet_small')
+    B = len(src)
+    T = lambda a: torch.from_numpy(np.asarray(a)).to(device)
+    pred = {k: [T(d[f'out.{k}.{b}']) for b in range(B)] for k in OUT_KEYS}
+    pred['pose'] = T(d['out.pose'])
+    batch = {'src_xyz': [T(s) for s in src], 'tgt_xyz': [T(t) for t in tgt],
+             'kpconv_meta': {k: [t.to(device) for t in v] for k, v in meta.items()},
+             'pose': T(g['pose']),
+             'src_overlap': [T(g[f'src_overlap.{b}']) for b in range(B)],
+             'tgt_overlap': [T(g[f'tgt_overlap.{b}']) for b in range(B)]}
+    losses = {k[5:]: float(g[k]) for k in g.files if k.startswith('loss.')}
+    metrics = {k[7:]: g[k] for k in g.files if k.startswith('metric.')}
+    pyr = {k[12:]: g[k] for k in g.files if k.startswith('overlap_pyr.')}
+    return cfg, pred, batch, losses, metrics, pyr, T(g['W']), T(g['W_un'])

@@ -425,8 +425,56 @@ def make_forward(fr, fk):
     save('forward_3dmatch_small', **pack_forward(model, meta, out, over, [s], [t], 4.0))
 
 
+def make_loss(fr, fk):
+    """Test-step tail fixture: the reference's own RegTR.compute_loss
+    (finegrained_regtr.py:252-309) and GenericRegModel._compute_metrics
+    (generic_reg_model.py:203-215) on the forward of forward_modelnet_small (same seeded
+    model, inputs and kpconv_meta, so the forward outputs are that fixture's out.*), with the
+    pairs' ground-truth poses and per-point overlap flags (nearest point of the other cloud,
+    under the true pose, within 0.05)."""
+    from scipy.spatial import cKDTree
+    cfg = load_cfg('modelnet.yaml', **SMALL_MODELNET)
+    pairs = [modelnet_like_pair(i, n_raw=512) for i in range(2)]
+    src = [p[0] for p in pairs]
+    tgt = [p[1] for p in pairs]
+    pose = np.stack([p[2] for p in pairs]).astype(np.float32)
+    model, meta, out = run_forward(fr, fk, cfg, src, tgt)
+    ref = np.load(os.path.join(HERE, 'forward_modelnet_small.npz'))
+    for b in range(2):          # same forward as the committed fixture
+        assert np.array_equal(out['src_feat'][b].numpy(), ref[f'out.src_feat.{b}'])
+    sov, tov = [], []
+    for b in range(2):
+        sw = src[b] @ pose[b][:, :3].T + pose[b][:, 3]
+        sov.append((cKDTree(tgt[b]).query(sw)[0] < 0.05).astype(np.float32))
+        tov.append((cKDTree(sw).query(tgt[b])[0] < 0.05).astype(np.float32))
+    batch = {'src_xyz': [torch.from_numpy(c) for c in src],
+             'tgt_xyz': [torch.from_numpy(c) for c in tgt],
+             'kpconv_meta': meta, 'pose': torch.from_numpy(pose),
+             'src_overlap': [torch.from_numpy(o) for o in sov],
+             'tgt_overlap': [torch.from_numpy(o) for o in tov]}
+    with torch.no_grad(), cuda_to_cpu():
+        losses = model.compute_loss(out, batch)
+        metrics = model._compute_metrics(out, batch)
+    arrays = {'pose': pose, 'W': model.feature_criterion.W.detach().numpy(),
+              'W_un': model.feature_criterion_un.W.detach().numpy()}
+    for b in range(2):
+        arrays[f'src_overlap.{b}'] = sov[b]
+        arrays[f'tgt_overlap.{b}'] = tov[b]
+    for k, v in batch['overlap_pyr'].items():
+        arrays[f'overlap_pyr.{k}'] = v.numpy()
+    for k, v in losses.items():
+        arrays[f'loss.{k}'] = np.float32(v.item())
+    for k, v in metrics.items():
+        arrays[f'metric.{k}'] = v.numpy()
+    save('loss_modelnet_small', **arrays)
+
+
 if __name__ == '__main__':
     fr, fk = import_reference()
+    if sys.argv[1:] == ['loss']:
+        make_loss(fr, fk)
+        sys.exit(0)
     make_geometry()
     make_modules(fr, fk)
     make_forward(fr, fk)
+    make_loss(fr, fk)

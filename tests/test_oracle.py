@@ -159,3 +159,20 @@ def test_oracle_kpconv_and_instnorm_match_reference():
     assert torch.equal(mo.max_pool(T(g['x']), T(g['pools'].astype(np.int64))), T(g['maxpool']))
     n = golden('instnorm')
     assert rel_err(mo.instance_norm(T(n['x']), T(n['lengths'].astype(np.int64))), n['out']) < 1e-6
+
+
+def test_loss_oracle_matches_reference():
+    """oracle/loss_oracle.py vs the reference's own compute_loss / _compute_metrics on its
+    own forward outputs (tests/golden/loss_modelnet_small.npz)."""
+    import loss_oracle as lo
+    from conftest import loss_fixture
+    cfg, pred, batch, ref_losses, ref_metrics, ref_pyr, W, W_un = loss_fixture()
+    losses, pyr = lo.compute_loss(cfg, W, W_un, pred, batch)
+    assert set(losses) == set(ref_losses)
+    for k, v in ref_losses.items():
+        assert abs(float(losses[k]) - v) <= 1e-5 * max(1.0, abs(v)), (k, float(losses[k]), v)
+    for p, lvl in enumerate(pyr):
+        np.testing.assert_allclose(lvl.numpy(), ref_pyr[f'pyr_{p}'], rtol=1e-6, atol=1e-7)
+    rot, trans = lo.pose_errors(pred['pose'], batch['pose'])
+    np.testing.assert_allclose(rot.numpy(), ref_metrics['rot_err_deg'], atol=1e-3)
+    np.testing.assert_allclose(trans.numpy(), ref_metrics['trans_err'], rtol=1e-5, atol=1e-6)
