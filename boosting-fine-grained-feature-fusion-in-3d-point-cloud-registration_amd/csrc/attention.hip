@@ -666,6 +666,7 @@ extern "C" int fgr_attention(const float* q, int64_t ld_q, const float* k, int64
     if (max_q_len == 0) return FGR_OK;
     dim3 grid((unsigned)ceil_div(max_q_len, kBQ), (unsigned)n_head, (unsigned)n_seg);
     hipStream_t st = as_stream(stream);
+    TimedCall timed_(st);
     switch (head_dim) {
         case 4: launch<4>(grid, st, q, ld_q, k, ld_k, v, ld_v, o, ld_o, q_off, kv_off, kv_seg, scale); break;
         case 8: launch<8>(grid, st, q, ld_q, k, ld_k, v, ld_v, o, ld_o, q_off, kv_off, kv_seg, scale); break;
@@ -717,6 +718,7 @@ extern "C" int fgr_attention_bf16x6(const float* q, int64_t ld_q, const float* k
                 (long long)ws_bytes, (long long)need);
     if (max_q_len == 0 || max_kv_len == 0) return FGR_OK;
     hipStream_t st = as_stream(stream);
+    TimedCall timed_(st);
     hipLaunchKernelGGL(attn_kv_image_kernel,
                        dim3((unsigned)ceil_div(max_kv_len, 64), (unsigned)n_head, (unsigned)n_kv_seg),
                        dim3(256), 0, st, k, ld_k, v, ld_v, kv_off, n_head, (uint4*)workspace);

@@ -339,6 +339,7 @@ extern "C" int fgr_attention_f16x3(const float* q, int64_t ld_q, const float* k,
                 (long long)ws_bytes, (long long)need);
     if (max_q_len == 0 || max_kv_len == 0) return FGR_OK;
     hipStream_t st = as_stream(stream);
+    TimedCall timed_(st);
     uint4* img = static_cast<uint4*>(workspace);
     int2* sc = reinterpret_cast<int2*>(static_cast<char*>(workspace) + nt * kUnits * 16);
     hipLaunchKernelGGL(attn_kv_image16_kernel,

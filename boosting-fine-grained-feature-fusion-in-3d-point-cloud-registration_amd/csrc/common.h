@@ -15,6 +15,24 @@ void set_error(const char* fmt, ...);
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// Opt-in launch timing (fgr_time_next_call): a TimedCall placed right before an entry
+// point's first launch records the armed start event there and the end event when the
+// entry point returns, on the launch stream, then disarms -- so the measured interval
+// holds this call's kernels only, not the caller's host time before the call.
+void timing_arm_take(hipEvent_t* start, hipEvent_t* end);
+struct TimedCall {
+    hipStream_t st;
+    hipEvent_t end = nullptr;
+    explicit TimedCall(hipStream_t s) : st(s) {
+        hipEvent_t start = nullptr;
+        timing_arm_take(&start, &end);
+        if (start) (void)hipEventRecord(start, st);
+    }
+    ~TimedCall() {
+        if (end) (void)hipEventRecord(end, st);
+    }
+};
+
 // Checks a kernel launch / runtime call; on failure records a message and returns.
 #define FGR_CHECK_LAUNCH(what)                                                        \
     do {                                                                              \

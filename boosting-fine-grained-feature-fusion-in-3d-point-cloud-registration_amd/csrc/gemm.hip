@@ -464,6 +464,7 @@ extern "C" int fgr_gemm_bf16x6(const float* a, int64_t lda, const void* w_img, f
     if (m == 0) return FGR_OK;
     Gemm6Args g{a, lda, (const u32x4*)w_img, (k + 31) / 32, c, ldc, bias, r, ldr, m, n, k, act};
     hipStream_t st = as_stream(stream);
+    TimedCall timed_(st);
     // tile choice (measured on the forward's shapes, microbench.py tiles): 64 x 128 for wide
     // outputs (N >= 512, N % 256 == 0), 64 x 64 otherwise -- small tiles at 4-5 blocks per
     // CU hide the 2-barrier staging better than 128 x 128 at 2. FGR_GEMM6_TILE overrides it

@@ -762,6 +762,7 @@ extern "C" int fgr_gemm_f16x3(const float* a, int64_t lda, const void* w_img, fl
     GemmH3Args g{a, lda, (const u32x4*)w_img, ksteps_h3(k), wsc, c, ldc, bias, r, ldr,
                  m, n, k, act, vo ? 1 : 0};
     hipStream_t st = as_stream(stream);
+    TimedCall timed_(st);
     // tile BM x BN (activation rows x output channels); FGR_GEMM16_TILE overrides it for
     // tuning (a = 128x128, b = 64x128, c = 64x64, d = 128x64)
     // Default per shape (measured on the forward's GEMMs, microbench.py tiles16): wide outputs
@@ -860,6 +861,7 @@ extern "C" int fgr_gemm_rows_f16x3(const float* x, int64_t ldx, const float* ln_
     RowsArgs g{x, ldx, ln_gamma, ln_beta, ln_eps, add, ld_add, (const u32x4*)w_img,
                ksteps_h3(k), wsc, c, ldc, bias, r, ldr, m, n, k, act, vo ? 1 : 0};
     hipStream_t st = as_stream(stream);
+    TimedCall timed_(st);
     int dev = 0, n_cu = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||

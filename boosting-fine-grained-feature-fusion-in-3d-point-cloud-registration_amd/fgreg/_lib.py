@@ -9,7 +9,7 @@ import os
 import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, 'libfgreg.so')
+LIB_PATH = os.environ.get('FGREG_LIB_PATH') or os.path.join(HERE, 'libfgreg.so')  # override: A/B builds (tools/)
 CSRC = os.path.join(os.path.dirname(HERE), 'csrc')
 
 _vp = ctypes.c_void_p
@@ -64,6 +64,7 @@ SIGNATURES = {
     'fgr_corr_loss': [_vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp],
     'fgr_se3_compare': [_vp, _vp, _i32, _i32, _vp, _vp, _vp],
     'fgr_procrustes': [_vp, _vp, _vp, _i64, _i64, _f32, _vp, _vp],
+    'fgr_time_next_call': [_vp, _vp],
     'fgr_pair_pose': [_vp, _vp, _vp, _i64, _vp, _i32, _i32, _f32, _vp, _vp],
 }
 

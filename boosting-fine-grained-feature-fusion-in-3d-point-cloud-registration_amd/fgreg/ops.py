@@ -32,18 +32,25 @@ class KernelTimer:
         self.count = False
 
     def begin(self, name):
+        """Creates the event pair of one launch and arms it in libfgreg
+        (fgr_time_next_call), so the events are recorded on the launch stream by the entry
+        point itself, immediately around its kernels: the interval excludes the Python /
+        ctypes time before the launch, during which the GPU may sit idle."""
         if name not in self.names:
             return None
-        ev = torch.cuda.Event(enable_timing=True)
-        ev.record()
-        return ev
+        start = torch.cuda.Event(enable_timing=True)
+        end = torch.cuda.Event(enable_timing=True)
+        start.record()            # materialise both events (re-recorded by the call)
+        end.record()
+        _lib.check(_lib.load().fgr_time_next_call(start.cuda_event, end.cuda_event),
+                   'fgr_time_next_call')
+        return start, end
 
-    def end(self, name, start, work=None):
-        if start is None:
+    def end(self, name, pair, work=None):
+        if pair is None:
             return
-        ev = torch.cuda.Event(enable_timing=True)
-        ev.record()
-        self.events[name].append((start, ev))
+        _lib.load().fgr_time_next_call(None, None)   # disarm if the call launched nothing
+        self.events[name].append(pair)
         if self.count and work is not None:
             self.work[name].append(work() if callable(work) else work)
 

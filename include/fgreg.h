@@ -55,6 +55,14 @@ enum { FGR_ACT_NONE = 0, FGR_ACT_LEAKY = 1, FGR_ACT_RELU = 2, FGR_ACT_RELU_RES_L
 int fgr_abi_version(void);
 const char* fgr_last_error(void);
 
+/* Opt-in instrumentation (bench.py's per-kernel rooflines; not part of the reference's
+ * interface): arms two caller-created hipEvent_t for the NEXT timed entry point called on
+ * this thread (fgr_kpconv_gather, fgr_attention*, fgr_gemm_bf16x6, fgr_gemm_f16x3,
+ * fgr_gemm_rows_f16x3). That call records `start_event` on its stream right before its
+ * first kernel launch and `end_event` after its last one, then disarms; (NULL, NULL)
+ * disarms explicitly. Thread-local like the error string. */
+int fgr_time_next_call(void* start_event, void* end_event);
+
 /* ---- grid subsampling ------------------------------------------------------------
  * Replaces batch_grid_subsampling_kpconv_gpu (finegrained_kpconv.py:218-245; ME
  * UNWEIGHTED_AVERAGE) and its CPU twin subsample_batch
