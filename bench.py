@@ -11,7 +11,9 @@ N GPUs = N processes (torchrun), pairs sharded 8 per rank with no data-path coll
 
 Prints ONE JSON line on rank 0 (contract in the task statement), with
   roofline:     the KPConv gather kernel (HBM-bound): algorithmic bytes per launch /
-                average launch time from HIP events over the timed region;
+                average launch time from HIP events over the timed region (recorded by
+                libfgreg itself around its kernels, fgr_time_next_call, event pairs created
+                before the region);
   cpu_baseline: the CPU restatement (oracle/model_oracle.py, kind "port") timed on the
                 host cores on a bounded sample of the same workload (rank 0, N = 1 only).
 """
@@ -110,6 +112,7 @@ def main():
         timer.count = False
         timer.reset_events()
         timer.names.discard('gemm')       # GEMM events: separate pass below, not in `value`
+        timer.prealloc(args.steps * (len(gather_bytes) + len(attn_flops)))
 
         if dist is not None:
             dist.barrier()
@@ -123,6 +126,7 @@ def main():
         elapsed = time.perf_counter() - t0
         # instrumented pass for the GEMM roofline (every dense layer), outside the timed region
         gtimer = ops.KernelTimer(['gemm'])
+        gtimer.prealloc(args.steps * len(gemm_flops))
         ops.TIMER = gtimer
         for _ in range(args.steps):
             step()

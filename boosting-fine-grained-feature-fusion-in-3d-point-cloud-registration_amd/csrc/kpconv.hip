@@ -93,7 +93,6 @@ kpconv_gather_wide(const float* __restrict__ q, const float* __restrict__ s, int
     constexpr int U = 4;                               // neighbour rows in flight
     __shared__ float w_lds[kGatherWaves][64 + U][KU];
     __shared__ int nb_lds[kGatherWaves][64 + U];
-    __shared__ float c_lds[kGatherWaves][64][3];
     __shared__ float kp[3 * kMaxKp];
     const int wv = threadIdx.x / 64, lane = threadIdx.x % 64;
     for (int i = threadIdx.x; i < 3 * n_kp; i += blockDim.x) kp[i] = kp_g[i];
@@ -119,47 +118,33 @@ kpconv_gather_wide(const float* __restrict__ q, const float* __restrict__ s, int
         if (v == 0) continue;
         if constexpr (!POSI) n_pos += __popcll(__ballot(valid && pos[id] != 0));
         const int p = __popcll(m & ((1ull << lane) - 1ull));
-        // the lane holding a valid neighbour owns its compacted slot p: it writes the id
-        // and the centred neighbour xyz (neighbours are centred first, then compared with
-        // the kernel points, :302, :313) -- one dependent trip (idx -> xyz) instead of
-        // idx -> LDS -> xyz; the influences are then spread over all lanes from LDS
-        if (valid) {
-            nb_lds[wv][p] = (int)id;
-            c_lds[wv][p][0] = s[3 * id] - qx;
-            c_lds[wv][p][1] = s[3 * id + 1] - qy;
-            c_lds[wv][p][2] = s[3 * id + 2] - qz;
-        }
+        if (valid) nb_lds[wv][p] = (int)id;
         if (lane < U) nb_lds[wv][v + lane] = 0;       // pad rows: weight 0, row 0
         __builtin_amdgcn_wave_barrier();
-        // the first U feature rows are in flight while the influences are computed
-        float xa[U][VEC];
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            load_vec<VEC>(x + (int64_t)nb_lds[wv][u] * CIN + lane * VEC, xa[u]);
+        // kernel-point influences of the valid neighbours -> LDS (pad rows get 0)
         for (int t = lane; t < (v + U) * KU; t += 64) {
             const int hh = t / KU, k = t - hh * KU;
             float w = 0.f;
-            if (hh < v && k < n_kp)
-                w = kp_weight(c_lds[wv][hh][0], c_lds[wv][hh][1], c_lds[wv][hh][2], kp, k,
-                              inv_extent);
+            if (hh < v && k < n_kp) {
+                const int sid = nb_lds[wv][hh];
+                // neighbours are centred first, then compared with the kernel points (:302, :313)
+                const float nx = s[3 * sid] - qx, ny = s[3 * sid + 1] - qy, nz = s[3 * sid + 2] - qz;
+                w = kp_weight(nx, ny, nz, kp, k, inv_extent);
+            }
             w_lds[wv][hh][k] = w;
         }
         __builtin_amdgcn_wave_barrier();
         for (int hh = 0; hh < v; hh += U) {
-            // the next U rows are in flight while this group is accumulated (double buffer)
-            const bool more = hh + U < v;
-            float xb[U][VEC];
-            if (more) {
+            float xv[U][VEC];
 #pragma unroll
-                for (int u = 0; u < U; ++u)
-                    load_vec<VEC>(x + (int64_t)nb_lds[wv][hh + U + u] * CIN + lane * VEC, xb[u]);
-            }
+            for (int u = 0; u < U; ++u)
+                load_vec<VEC>(x + (int64_t)nb_lds[wv][hh + u] * CIN + lane * VEC, xv[u]);
             if constexpr (POSI) {
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     float t = 0.f;
 #pragma unroll
-                    for (int j = 0; j < VEC; ++j) t += xa[u][j];
+                    for (int j = 0; j < VEC; ++j) t += xv[u][j];
                     t = wave_sum_dpp(t);
                     n_pos += (hh + u < v && t > 0.f) ? 1 : 0;
                 }
@@ -170,14 +155,8 @@ kpconv_gather_wide(const float* __restrict__ q, const float* __restrict__ s, int
                 for (int k = 0; k < KU; ++k) {
                     const float w = w_lds[wv][hh + u][k];
 #pragma unroll
-                    for (int j = 0; j < VEC; ++j) acc[k][j] = fmaf(w, xa[u][j], acc[k][j]);
+                    for (int j = 0; j < VEC; ++j) acc[k][j] = fmaf(w, xv[u][j], acc[k][j]);
                 }
-            if (more) {
-#pragma unroll
-                for (int u = 0; u < U; ++u)
-#pragma unroll
-                    for (int j = 0; j < VEC; ++j) xa[u][j] = xb[u][j];
-            }
         }
         __builtin_amdgcn_wave_barrier();
     }
@@ -244,7 +223,6 @@ kpconv_gather_c1(const float* __restrict__ q, const float* __restrict__ s, int64
                  const int64_t* __restrict__ idx, int width, const float* __restrict__ x,
                  const float* __restrict__ kp_g, int n_kp, float inv_extent,
                  float* __restrict__ wf, float* __restrict__ nnorm) {
-    constexpr int R = 4;                               // index entries per lane in flight
     __shared__ float kp[3 * kMaxKp];
     for (int i = threadIdx.x; i < 3 * n_kp; i += blockDim.x) kp[i] = kp_g[i];
     __syncthreads();
@@ -257,25 +235,15 @@ kpconv_gather_c1(const float* __restrict__ q, const float* __restrict__ s, int64
     for (int k = 0; k < KU; ++k) acc[k] = 0.f;
     float n_pos = 0.f;
     const int64_t* row = idx + qc * width;
-    for (int h0 = 0; h0 < width; h0 += 16 * R) {
-        // R index loads in flight together, then the valid neighbours' xyz / feature
-        int64_t id[R];
+    for (int h = l; h < width; h += 16) {
+        const int64_t id = row[h];
+        if (id < 0 || id >= ns) continue;
+        const float nx = s[3 * id] - qx, ny = s[3 * id + 1] - qy, nz = s[3 * id + 2] - qz;
+        const float xv = x[id];
+        n_pos += xv > 0.f ? 1.f : 0.f;
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const int h = h0 + l + 16 * r;
-            id[r] = h < width ? row[h] : ns;
-        }
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            if (id[r] < 0 || id[r] >= ns) continue;   // only valid neighbours are read
-            const int64_t sid = id[r];
-            const float nx = s[3 * sid] - qx, ny = s[3 * sid + 1] - qy, nz = s[3 * sid + 2] - qz;
-            const float xv = x[sid];
-            n_pos += xv > 0.f ? 1.f : 0.f;
-#pragma unroll
-            for (int k = 0; k < KU; ++k)
-                if (k < n_kp) acc[k] = fmaf(kp_weight(nx, ny, nz, kp, k, inv_extent), xv, acc[k]);
-        }
+        for (int k = 0; k < KU; ++k)
+            if (k < n_kp) acc[k] = fmaf(kp_weight(nx, ny, nz, kp, k, inv_extent), xv, acc[k]);
     }
     float mine0 = 0.f, mine1 = 0.f;
 #pragma unroll

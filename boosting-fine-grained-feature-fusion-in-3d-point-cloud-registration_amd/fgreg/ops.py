@@ -30,6 +30,7 @@ class KernelTimer:
         self.events = {n: [] for n in names}
         self.work = {n: [] for n in names}
         self.count = False
+        self.pool = []
 
     def begin(self, name):
         """Creates the event pair of one launch and arms it in libfgreg
@@ -38,10 +39,7 @@ class KernelTimer:
         ctypes time before the launch, during which the GPU may sit idle."""
         if name not in self.names:
             return None
-        start = torch.cuda.Event(enable_timing=True)
-        end = torch.cuda.Event(enable_timing=True)
-        start.record()            # materialise both events (re-recorded by the call)
-        end.record()
+        start, end = self.pool.pop() if self.pool else self._pair()
         _lib.check(_lib.load().fgr_time_next_call(start.cuda_event, end.cuda_event),
                    'fgr_time_next_call')
         return start, end
@@ -53,6 +51,18 @@ class KernelTimer:
         self.events[name].append(pair)
         if self.count and work is not None:
             self.work[name].append(work() if callable(work) else work)
+
+    @staticmethod
+    def _pair():
+        start = torch.cuda.Event(enable_timing=True)
+        end = torch.cuda.Event(enable_timing=True)
+        start.record()            # materialise both events (re-recorded by the call)
+        end.record()
+        return start, end
+
+    def prealloc(self, n):
+        """Creates n event pairs up front, so a timed region pays only the arm call."""
+        self.pool.extend(self._pair() for _ in range(n))
 
     def reset_events(self):
         self.events = {n: [] for n in self.names}
