@@ -12,6 +12,7 @@ import numpy as np
 import pytest
 import torch
 
+sys.dont_write_bytecode = True     # never leave bytecode next to /root/reference's sources
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(REPO, 'boosting-fine-grained-feature-fusion-in-3d-point-cloud-registration_amd')
 GOLDEN = os.path.join(REPO, 'tests', 'golden')
