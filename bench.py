@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Benchmark: point-cloud pairs/s of the registration forward on MI355X.
 
-Workload (BASELINE.json configs[1] / configs[3]): ModelNet40-like 2048-pt pairs through
-the reference's test transforms (717 + 717 points per pair, fgreg.synthetic), 8 pairs
+Workload (BASELINE.json configs[1] / configs[3]): ModelNet40-shaped 2048-pt pairs through
+the reference's exact crop test transforms (717 + 717 points per pair,
+fgreg.synthetic.modelnet_reference_pair -> fgreg.transforms), 8 pairs
 per GPU, full RegTR forward (preprocessing, KPConv/Res2Net encoder, 6-layer cross
 encoder, correspondence head, pose) in fp32 with random-init weights of the reference
 ModelNet architecture. One step = one forward over one batch already resident in HBM.
@@ -175,8 +176,10 @@ def main():
             'scaling': 'weak',
             'vs_baseline': None,
             'dtype': 'f32',
-            'data': 'synthetic ModelNet-like pairs (box surfaces, 2048 raw pts -> crop 0.7 -> '
-                    '717+717 pts), random-init weights of the reference ModelNet architecture',
+            'data': 'synthetic ModelNet40-shaped pairs: 2048-pt box-surface raw clouds through '
+                    'the reference crop test transforms (crop 0.7, euler SE3 45deg/0.5, '
+                    'resample 717+717, jitter, shuffle; fgreg/transforms.py), random-init '
+                    'weights of the reference ModelNet architecture',
             'config': {'workload': 'ModelNet40 2048-pt pairs, 8 pairs per GPU (BASELINE configs[1]'
                                    ' at N=1, configs[3] at N=8)',
                        'pairs_per_gpu': P, 'global_batch': P * world, 'points_per_cloud': 717,

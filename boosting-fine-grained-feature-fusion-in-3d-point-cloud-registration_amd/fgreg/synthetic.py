@@ -3,6 +3,10 @@
 No dataset is reachable from this image, so the benchmark and the tests use
 clouds of the same shape as the reference's test inputs:
 
+* ``modelnet_reference_pair(i)`` (``make_batch('modelnet')``, the bench workload) -- the
+  box-surface raw cloud below through the reference's exact crop test pipeline
+  (fgreg/transforms.py, pinned to data_loaders/modelnet_transforms.py);
+
 * ``modelnet_like_pair(i)`` -- a 2048-point raw cloud (uniform samples on the
   faces of a random box, normalised to max|p| = 1) pushed through the steps of
   the reference's ModelNet *test* transforms (data_loaders/modelnet.py:111-117):
@@ -119,9 +123,23 @@ def indoor_like_pair(i, n_points=20000, max_rot_deg=15.0, max_trans=0.3):
     return src.astype(np.float32), tgt.astype(np.float32), pose.astype(np.float32)
 
 
+def modelnet_reference_pair(i, n_raw=2048):
+    """A box-surface raw cloud (seeded by i) through the reference's exact ModelNet crop test
+    pipeline (fgreg.transforms.modelnet_crop_test, sample index i): the bench workload.
+    Returns (src (717,3) f32, tgt (717,3) f32, pose (3,4) f32: src -> tgt)."""
+    from .transforms import modelnet_crop_test
+    raw = _box_surface(np.random.default_rng(1000003 * (i + 1)), n_raw).astype(np.float32)
+    smp = modelnet_crop_test(raw, i)
+    return (smp['src_xyz'].numpy().astype(np.float32), smp['tgt_xyz'].numpy().astype(np.float32),
+            smp['pose'].numpy().astype(np.float32))
+
+
 def make_batch(kind, batch_size, start=0, **kw):
-    """List-of-clouds batch in the reference's collate_pair layout (collate_functions.py:4-22)."""
-    gen = modelnet_like_pair if kind == 'modelnet' else indoor_like_pair
+    """List-of-clouds batch in the reference's collate_pair layout (collate_functions.py:4-22).
+    'modelnet': the reference's crop test pipeline on synthetic raw clouds; 'modelnet_like':
+    the seeded approximation above; otherwise 3DMatch-like fragments."""
+    gen = {'modelnet': modelnet_reference_pair, 'modelnet_like': modelnet_like_pair}.get(
+        kind, indoor_like_pair)
     pairs = [gen(start + b, **kw) for b in range(batch_size)]
     return ([p[0] for p in pairs], [p[1] for p in pairs],
             np.stack([p[2] for p in pairs]).astype(np.float32))
