@@ -42,12 +42,36 @@ PRECISION = {'f16x3': 'fp32-accurate scaled split fp16 (3 fp16 MFMA products per
              'fp32': 'fp32 MFMA / hipBLASLt fp32'}
 
 
+DATA = {
+    'modelnet': 'synthetic ModelNet40-shaped pairs: 2048-pt box-surface raw clouds through the '
+                'reference crop test transforms (crop 0.7, euler SE3 45deg/0.5, resample '
+                '717+717, jitter, shuffle; fgreg/transforms.py), random-init weights of the '
+                'reference ModelNet architecture',
+    '3dmatch': 'synthetic 3DMatch-like fragment pairs: 20k pts on the floor and walls of a room, '
+               '5 mm noise, second fragment rotated <= 15 deg / moved <= 0.3 m '
+               '(fgreg/synthetic.py), random-init weights of the reference 3DMatch architecture',
+}
+METRIC = {
+    'modelnet': 'point-cloud pairs/sec (forward) on ModelNet 2048-pt pairs',
+    '3dmatch': 'point-cloud pairs/sec (forward) on 3DMatch ~20k-pt fragment pairs',
+}
+WORKLOAD = {
+    'modelnet': 'ModelNet40 2048-pt pairs, {P} pairs per GPU (BASELINE configs[1] at N=1, '
+                'configs[3] at N=8)',
+    '3dmatch': '3DMatch ~20k-pt fragment pairs, {P} pair(s) per GPU (BASELINE configs[2])',
+}
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument('--gpus', type=int, default=1)
     p.add_argument('--steps', type=int, default=20)
     p.add_argument('--warmup', type=int, default=5)
-    p.add_argument('--pairs-per-gpu', type=int, default=8)
+    p.add_argument('--pairs-per-gpu', type=int, default=None,
+                   help='default 8 (modelnet) / 1 (3dmatch)')
+    p.add_argument('--workload', choices=('modelnet', '3dmatch'), default='modelnet',
+                   help='modelnet: BASELINE configs[1]/[3] (the headline line); 3dmatch: '
+                        'configs[2], 20k-pt fragment pairs, a parity / stress line')
     p.add_argument('--cpu-seconds', type=float, default=10.0,
                    help='budget of the CPU baseline sample (0 disables it)')
     p.add_argument('--no-cpu-baseline', action='store_true')
@@ -82,12 +106,12 @@ def main():
         import torch.distributed as dist
         dist.init_process_group('nccl', device_id=dev)
 
-    cfg = fgreg.config.get('modelnet')
+    cfg = fgreg.config.get(args.workload)
     torch.manual_seed(0)
     np.random.seed(0)
     model = fgreg.RegTR(cfg).to(dev).eval()
-    P = args.pairs_per_gpu
-    src, tgt, pose_gt = make_batch('modelnet', P, start=rank * P)   # this rank's shard of pairs
+    P = args.pairs_per_gpu or (8 if args.workload == 'modelnet' else 1)
+    src, tgt, pose_gt = make_batch(args.workload, P, start=rank * P)   # this rank's shard of pairs
     batch_src = [torch.from_numpy(s).to(dev) for s in src]
     batch_tgt = [torch.from_numpy(t).to(dev) for t in tgt]
     from fgreg import dist as fdist
@@ -165,7 +189,7 @@ def main():
     if rank == 0:
         pairs = world * P * args.steps
         line = {
-            'metric': 'point-cloud pairs/sec (forward) on ModelNet 2048-pt pairs',
+            'metric': METRIC[args.workload],
             'value': pairs / elapsed,
             'unit': 'pairs/s',
             'n_gpus': world,
@@ -176,13 +200,10 @@ def main():
             'scaling': 'weak',
             'vs_baseline': None,
             'dtype': 'f32',
-            'data': 'synthetic ModelNet40-shaped pairs: 2048-pt box-surface raw clouds through '
-                    'the reference crop test transforms (crop 0.7, euler SE3 45deg/0.5, '
-                    'resample 717+717, jitter, shuffle; fgreg/transforms.py), random-init '
-                    'weights of the reference ModelNet architecture',
-            'config': {'workload': 'ModelNet40 2048-pt pairs, 8 pairs per GPU (BASELINE configs[1]'
-                                   ' at N=1, configs[3] at N=8)',
-                       'pairs_per_gpu': P, 'global_batch': P * world, 'points_per_cloud': 717,
+            'data': DATA[args.workload],
+            'config': {'workload': WORKLOAD[args.workload].format(P=P),
+                       'pairs_per_gpu': P, 'global_batch': P * world,
+                       'points_per_cloud': int(np.mean([len(c) for c in src])),
                        'parallelism': f'pair-sharded dp{world}'},
             'roofline': {'kernel': 'fgr_kpconv_gather', 'bound': 'hbm',
                          'achieved': g_achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
