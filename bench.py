@@ -180,7 +180,7 @@ def main():
     m_ms = gtimer.total_ms('gemm')
     m_flops_step = float(sum(gemm_flops))
     m_achieved = m_flops_step * args.steps / (m_ms / 1e3) / 1e12 if m_ms > 0 else 0.0
-    traffic = _pmc_traffic()
+    traffic = _pmc_traffic() if args.workload == 'modelnet' else None   # PMC pass: modelnet
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_seconds > 0:
@@ -234,7 +234,7 @@ def main():
                               'matrix_pipe_frac': PIPE.get(lin.MODE, 1) * m_achieved /
                               (F16_MFMA_PEAK_TFLOPS if lin.MODE != 'fp32'
                                else FP32_MFMA_PEAK_TFLOPS)},
-            'test_tail': {'what': 'compute_loss + _compute_metrics of one step (8 pairs: '
+            'test_tail': {'what': f'compute_loss + _compute_metrics of one step ({P} pair(s): '
                                   'overlap pyramid, BCE, 2x InfoNCE, CorrCriterion, se3_compare)',
                           'ms_per_step': tail_ms},
             'cpu_baseline': cpu,
@@ -289,7 +289,7 @@ def cpu_baseline(cfg, model, src, tgt, budget_s, tail_inputs=None):
         n_pairs += 1
         it += 1
     res = {'value': n_pairs / t_tot, 'unit': 'pairs/s', 'cores': threads, 'kind': 'port',
-           'sample': f'{n_pairs} ModelNet-like pairs (B=1 forwards) of the same workload, '
+           'sample': f'{n_pairs} pairs (B=1 forwards) of the same workload, '
                      f'{t_tot:.1f} s, torch CPU fp32 with {threads} threads'}
     if tail_inputs is not None:       # the test-step tail on the same outputs (loss_oracle)
         import loss_oracle as lo
