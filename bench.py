@@ -1,26 +1,40 @@
 #!/usr/bin/env python3
 """Benchmark: point-cloud pairs/s of the registration forward on MI355X.
 
-Workload (BASELINE.json configs[1] / configs[3]): ModelNet40-shaped 2048-pt pairs through
-the reference's exact crop test transforms (717 + 717 points per pair,
-fgreg.synthetic.modelnet_reference_pair -> fgreg.transforms), 8 pairs
-per GPU, full RegTR forward (preprocessing, KPConv/Res2Net encoder, 6-layer cross
-encoder, correspondence head, pose) in fp32 with random-init weights of the reference
-ModelNet architecture. One step = one forward over one batch already resident in HBM.
-N GPUs = N processes (torchrun), pairs sharded 8 per rank with no data-path collective
-(weak scaling); each step ends with an RCCL all-gather of the per-pair poses.
+Workloads (``--workload``; BASELINE.json configs):
+  modelnet  (default, configs[1] at N=1 / configs[3] at N=8) ModelNet40-shaped 2048-pt pairs
+            through the reference's exact crop test transforms (717 + 717 points per pair,
+            fgreg.synthetic.modelnet_reference_pair -> fgreg.transforms), 8 pairs per GPU;
+  3dmatch   (configs[2]) 20k + 20k-pt indoor fragment pairs, 1 pair per GPU;
+  raw2048   (SURVEY §8(d) D2 stress) the 2048-pt raw clouds fed directly, 8 pairs per GPU.
+Full RegTR forward (preprocessing, KPConv/Res2Net encoder, 6-layer cross encoder,
+correspondence head, pose) with random-init weights of the reference architecture. One step =
+one forward over one batch already resident in HBM. N GPUs = N processes (torchrun), pairs
+sharded per rank with no data-path collective (weak scaling); each step ends with an RCCL
+all-gather of the per-pair poses.
 
 Prints ONE JSON line on rank 0 (contract in the task statement), with
-  roofline:     the KPConv gather kernel (HBM-bound): algorithmic bytes per launch /
-                average launch time from HIP events over the timed region (recorded by
-                libfgreg itself around its kernels, fgr_time_next_call, event pairs created
-                before the region);
-  cpu_baseline: the CPU restatement (oracle/model_oracle.py, kind "port") timed on the
-                host cores on a bounded sample of the same workload (rank 0, N = 1 only).
+  roofline:            the KPConv gather kernel (the north star's HBM target): algorithmic
+                       bytes per launch / average launch time from HIP events recorded by
+                       libfgreg itself around its kernels inside the timed region;
+  roofline_attention,
+  roofline_gemm,
+  rooflines_other:     every other kernel family (radius search, grid subsampling,
+                       InstanceNorm, LayerNorm, pose) from a separate instrumented replay of
+                       the same steps AFTER the timed region (so `value` carries no
+                       instrumentation but the gather's); MFMA fractions are against the
+                       matrix pipe the kernels actually run on (fp16 MFMA, 3 products per
+                       fp32-equivalent product for f16x3), the fp32-MFMA figure as a note;
+  cpu_baseline:        the CPU restatement (oracle/model_oracle.py, kind "port") timed on the
+                       host cores on a bounded sample of the same workload (rank 0, N = 1).
+``--profile``: warmup + timed steps only (no counting, instrumented, tail or CPU legs), for
+``rocprofv3 --kernel-trace --stats`` runs whose per-step kernel sums must stay within
+ms_per_step (tools/kernel_stats.py).
 """
 import argparse
 import json
 import os
+import platform
 import sys
 import time
 
@@ -40,25 +54,42 @@ PRECISION = {'f16x3': 'fp32-accurate scaled split fp16 (3 fp16 MFMA products per
              'bf16x6': 'fp32-accurate split bf16 (6 bf16 MFMA products per fp32 product)',
              'bf16x3': 'split bf16, 3 products (~2^-17 relative)',
              'fp32': 'fp32 MFMA / hipBLASLt fp32'}
-
+DTYPE = {'f16x3': 'f32 (emulated on the fp16 MFMA pipe: f16x3 split products)',
+         'bf16x6': 'f32 (emulated on the bf16 MFMA pipe: bf16x6 split products)',
+         'fp32': 'f32'}
 
 DATA = {
     'modelnet': 'synthetic ModelNet40-shaped pairs: 2048-pt box-surface raw clouds through the '
                 'reference crop test transforms (crop 0.7, euler SE3 45deg/0.5, resample '
                 '717+717, jitter, shuffle; fgreg/transforms.py), random-init weights of the '
                 'reference ModelNet architecture',
+    'raw2048': 'synthetic ModelNet40-shaped raw clouds: 2048+2048-pt box-surface clouds fed '
+               'directly (no crop / resample; SURVEY D2 stress), random-init weights of the '
+               'reference ModelNet architecture',
     '3dmatch': 'synthetic 3DMatch-like fragment pairs: 20k pts on the floor and walls of a room, '
                '5 mm noise, second fragment rotated <= 15 deg / moved <= 0.3 m '
                '(fgreg/synthetic.py), random-init weights of the reference 3DMatch architecture',
 }
 METRIC = {
     'modelnet': 'point-cloud pairs/sec (forward) on ModelNet 2048-pt pairs',
+    'raw2048': 'point-cloud pairs/sec (forward) on raw 2048+2048-pt pairs',
     '3dmatch': 'point-cloud pairs/sec (forward) on 3DMatch ~20k-pt fragment pairs',
 }
 WORKLOAD = {
     'modelnet': 'ModelNet40 2048-pt pairs, {P} pairs per GPU (BASELINE configs[1] at N=1, '
                 'configs[3] at N=8)',
+    'raw2048': 'raw 2048+2048-pt pairs, {P} pairs per GPU (SURVEY D2 stress input)',
     '3dmatch': '3DMatch ~20k-pt fragment pairs, {P} pair(s) per GPU (BASELINE configs[2])',
+}
+CFG_NAME = {'modelnet': 'modelnet', 'raw2048': 'modelnet', '3dmatch': '3dmatch'}
+PAIRS = {'modelnet': 8, 'raw2048': 8, '3dmatch': 1}
+# D4 byte / flop definitions per timed family
+OTHER = {
+    'radius_search': ('hbm', '12 (Nq + Ns) + 8 Nq K bytes (int64 table)'),
+    'grid_subsample': ('hbm', '12 (N_in + N_out) bytes (count + fill calls)'),
+    'instnorm': ('hbm', '8 N C bytes (+ 4 N C residual, + 4 N row divisor)'),
+    'layernorm': ('hbm', '8 N d bytes (+ 4 N d per add / pre-bias)'),
+    'pose': ('hbm', '28 B per (layer, point) + 48 B per pose'),
 }
 
 
@@ -68,23 +99,40 @@ def parse():
     p.add_argument('--steps', type=int, default=20)
     p.add_argument('--warmup', type=int, default=5)
     p.add_argument('--pairs-per-gpu', type=int, default=None,
-                   help='default 8 (modelnet) / 1 (3dmatch)')
-    p.add_argument('--workload', choices=('modelnet', '3dmatch'), default='modelnet',
+                   help='default 8 (modelnet, raw2048) / 1 (3dmatch)')
+    p.add_argument('--workload', choices=tuple(METRIC), default='modelnet',
                    help='modelnet: BASELINE configs[1]/[3] (the headline line); 3dmatch: '
-                        'configs[2], 20k-pt fragment pairs, a parity / stress line')
+                        'configs[2]; raw2048: the uncropped stress input')
     p.add_argument('--cpu-seconds', type=float, default=10.0,
-                   help='budget of the CPU baseline sample (0 disables it)')
+                   help='budget of the CPU baseline B=1 sample (0 disables it)')
     p.add_argument('--no-cpu-baseline', action='store_true')
+    p.add_argument('--profile', action='store_true',
+                   help='warmup + timed steps only (for rocprofv3 kernel-trace runs)')
     return p.parse_args()
 
 
-def _pmc_traffic():
-    """Per-launch HBM bytes of the gather kernel from the committed PMC summary, if any."""
-    path = os.path.join(REPO, 'profiles', 'pmc_kpconv_gather.json')
+def _pmc_traffic(kernel):
+    """Per-launch HBM bytes of `kernel` from this round's committed PMC summary
+    (tools/pmc_traffic.py output), or None when no summary for the current kernel exists."""
+    path = os.path.join(REPO, 'profiles', 'pmc_kpconv.json')
     if not os.path.exists(path):
-        return None
+        return None, None
     with open(path) as f:
-        return json.load(f).get('hbm_bytes_per_launch')
+        d = json.load(f)
+    if d.get('op') != kernel:
+        return None, None
+    return d.get('hbm_bytes_per_launch'), os.path.relpath(path, REPO)
+
+
+def _cpu_model():
+    try:
+        with open('/proc/cpuinfo') as f:
+            for line in f:
+                if line.startswith('model name'):
+                    return line.split(':', 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or 'unknown'
 
 
 def main():
@@ -106,12 +154,14 @@ def main():
         import torch.distributed as dist
         dist.init_process_group('nccl', device_id=dev)
 
-    cfg = fgreg.config.get(args.workload)
+    wl = args.workload
+    cfg = fgreg.config.get(CFG_NAME[wl])
     torch.manual_seed(0)
     np.random.seed(0)
     model = fgreg.RegTR(cfg).to(dev).eval()
-    P = args.pairs_per_gpu or (8 if args.workload == 'modelnet' else 1)
-    src, tgt, pose_gt = make_batch(args.workload, P, start=rank * P)   # this rank's shard of pairs
+    P = args.pairs_per_gpu or PAIRS[wl]
+    kind = {'raw2048': 'modelnet_raw'}.get(wl, wl)
+    src, tgt, pose_gt = make_batch(kind, P, start=rank * P)   # this rank's shard of pairs
     batch_src = [torch.from_numpy(s).to(dev) for s in src]
     batch_tgt = [torch.from_numpy(t).to(dev) for t in tgt]
     from fgreg import dist as fdist
@@ -122,123 +172,129 @@ def main():
             out['pose_all'] = fdist.gather_pair_results(out['pose'], [P] * world, pair_dim=1)
         return out
 
-    with torch.no_grad():
-        for _ in range(max(args.warmup, 1)):
-            step()
-        # algorithmic work per launch (untimed pass with counting on)
-        timer = ops.KernelTimer(['kpconv_gather', 'attention', 'gemm'])
-        timer.count = True
-        ops.TIMER = timer
-        step()
-        torch.cuda.synchronize()
-        gather_bytes = list(timer.work['kpconv_gather'])
-        attn_flops = list(timer.work['attention'])
-        gemm_flops = list(timer.work['gemm'])
-        timer.count = False
-        timer.reset_events()
-        timer.names.discard('gemm')       # GEMM events: separate pass below, not in `value`
-        timer.prealloc(args.steps * (len(gather_bytes) + len(attn_flops)))
-
+    def timed(n):
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(args.steps):
+        for _ in range(n):
             step()
         torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
-        elapsed = time.perf_counter() - t0
-        # instrumented pass for the GEMM roofline (every dense layer), outside the timed region
-        gtimer = ops.KernelTimer(['gemm'])
-        gtimer.prealloc(args.steps * len(gemm_flops))
-        ops.TIMER = gtimer
-        for _ in range(args.steps):
+        return time.perf_counter() - t0
+
+    with torch.no_grad():
+        for _ in range(max(args.warmup, 1)):
             step()
-        torch.cuda.synchronize()
-        ops.TIMER = None
-        # test-step tail: compute_loss + _compute_metrics on the
-        # outputs of one step, outside the timed region
-        tail_ms, tail_inputs = test_tail(model, batch_src, batch_tgt, src, tgt, pose_gt, dev,
-                                          args.steps)
+        if args.profile:
+            elapsed = timed(args.steps)
+        else:
+            # algorithmic work per launch (untimed pass with counting on)
+            fams = ['kpconv_gather', 'attention', 'gemm'] + list(OTHER)
+            timer = ops.KernelTimer(fams)
+            timer.count = True
+            ops.TIMER = timer
+            step()
+            torch.cuda.synchronize()
+            work = {n: list(timer.work[n]) for n in fams}
+            # timed region: only the gather (the headline roofline kernel) is instrumented
+            timer = ops.KernelTimer(['kpconv_gather'])
+            timer.prealloc(args.steps * len(work['kpconv_gather']))
+            ops.TIMER = timer
+            elapsed = timed(args.steps)
+            # instrumented replay for every other family, outside the timed region
+            rtimer = ops.KernelTimer([n for n in fams if n != 'kpconv_gather'])
+            rtimer.prealloc(args.steps * sum(len(work[n]) + 2 for n in rtimer.names))
+            ops.TIMER = rtimer
+            for _ in range(args.steps):
+                step()
+            torch.cuda.synchronize()
+            ops.TIMER = None
+            # test-step tail: compute_loss + _compute_metrics on the
+            # outputs of one step, outside the timed region
+            tail_ms, tail_inputs = test_tail(model, batch_src, batch_tgt, src, tgt, pose_gt, dev,
+                                              args.steps)
 
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if dist is not None:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
+    step_ms = elapsed / args.steps * 1e3
 
+    line = {
+        'metric': METRIC[wl], 'value': world * P * args.steps / elapsed, 'unit': 'pairs/s',
+        'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': step_ms,
+        'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
+        'dtype': DTYPE.get(lin.MODE, lin.MODE), 'data': DATA[wl],
+        'config': {'workload': WORKLOAD[wl].format(P=P), 'pairs_per_gpu': P,
+                   'global_batch': P * world,
+                   'points_per_cloud': int(np.mean([len(c) for c in src])),
+                   'parallelism': f'pair-sharded dp{world}'},
+    }
+    if args.profile:
+        line['profile'] = 'warmup + timed steps only (rocprofv3 companion run)'
+        if rank == 0:
+            print(json.dumps(line), flush=True)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
+    # ---- rooflines ---------------------------------------------------------------------
+    g_bytes_launch = float(np.mean(work['kpconv_gather'])) if work['kpconv_gather'] else 0.0
     g_ms = timer.total_ms('kpconv_gather')
     g_launches = len(timer.events['kpconv_gather'])
-    a_ms = timer.total_ms('attention')
-    a_launches = len(timer.events['attention'])
-    g_bytes_step = float(sum(gather_bytes))
-    a_flops_step = float(sum(attn_flops))
     g_avg_s = g_ms / 1e3 / max(g_launches, 1)
-    g_bytes_launch = g_bytes_step / max(len(gather_bytes), 1)
     g_achieved = g_bytes_launch / g_avg_s / 1e9 if g_avg_s > 0 else 0.0
-    a_achieved = a_flops_step * args.steps / (a_ms / 1e3) / 1e12 if a_ms > 0 else 0.0
-    m_ms = gtimer.total_ms('gemm')
-    m_flops_step = float(sum(gemm_flops))
-    m_achieved = m_flops_step * args.steps / (m_ms / 1e3) / 1e12 if m_ms > 0 else 0.0
-    traffic = _pmc_traffic() if args.workload == 'modelnet' else None   # PMC pass: modelnet
+    traffic, traffic_src = _pmc_traffic('fgr_kpconv_gather')
+    line['roofline'] = {
+        'kernel': 'fgr_kpconv_gather', 'bound': 'hbm', 'achieved': g_achieved,
+        'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': g_achieved / HBM_PEAK_GBS,
+        'traffic': traffic, 'traffic_source': traffic_src,
+        'algorithmic_bytes_per_launch': g_bytes_launch, 'avg_launch_us': g_avg_s * 1e6,
+        'launches_per_step': len(work['kpconv_gather']), 'share_of_step': g_ms / (elapsed * 1e3)}
 
+    def mfma_family(name, mode, kernel):
+        ms = rtimer.total_ms(name)
+        flops = float(sum(work[name]))
+        ach = flops * args.steps / (ms / 1e3) / 1e12 if ms > 0 else 0.0
+        pipe = PIPE.get(mode, 1)
+        peak = (F16_MFMA_PEAK_TFLOPS / pipe) if mode != 'fp32' else FP32_MFMA_PEAK_TFLOPS
+        return {'kernel': kernel, 'bound': 'mfma', 'achieved': ach, 'peak': peak,
+                'unit': 'TFLOP/s (fp32-equivalent)', 'frac': ach / peak,
+                'peak_note': (f'fp16 dense MFMA {F16_MFMA_PEAK_TFLOPS:.0f} TF / {pipe} products '
+                              f'per fp32-equivalent product; vs the {FP32_MFMA_PEAK_TFLOPS} TF '
+                              f'fp32-MFMA peak this would read {ach / FP32_MFMA_PEAK_TFLOPS:.2f}'
+                              if mode != 'fp32' else 'fp32 MFMA peak'),
+                'flops_per_step': flops, 'launches_per_step': len(work[name]),
+                'avg_launch_us': ms * 1e3 / max(len(rtimer.events[name]), 1),
+                'share_of_step': ms / args.steps / step_ms,
+                'precision': PRECISION.get(mode, mode)}
+
+    line['roofline_attention'] = mfma_family('attention', ops.ATTN_MODE,
+                                             f'fgr_attention_{ops.ATTN_MODE}')
+    line['roofline_gemm'] = mfma_family('gemm', lin.MODE, f'fgr_gemm_{lin.MODE} (all dense layers)')
+    other = {}
+    for name, (bound, what) in OTHER.items():
+        ms = rtimer.total_ms(name)
+        b = float(sum(work[name]))
+        if ms <= 0 or b <= 0:
+            continue
+        ach = b * args.steps / (ms / 1e3) / 1e9
+        other[name] = {'bound': bound, 'achieved': ach, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                       'frac': ach / HBM_PEAK_GBS, 'bytes_per_step': b, 'algorithmic': what,
+                       'calls_per_step': len(work[name]),
+                       'us_per_step': ms * 1e3 / args.steps,
+                       'share_of_step': ms / args.steps / step_ms}
+    line['rooflines_other'] = other
+    line['test_tail'] = {'what': f'compute_loss + _compute_metrics of one step ({P} pair(s): '
+                                 'overlap pyramid, BCE, 2x InfoNCE, CorrCriterion, se3_compare)',
+                         'ms_per_step': tail_ms}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_seconds > 0:
         cpu = cpu_baseline(cfg, model, src, tgt, args.cpu_seconds, tail_inputs)
-
+    line['cpu_baseline'] = cpu
     if rank == 0:
-        pairs = world * P * args.steps
-        line = {
-            'metric': METRIC[args.workload],
-            'value': pairs / elapsed,
-            'unit': 'pairs/s',
-            'n_gpus': world,
-            'steps': args.steps,
-            'warmup': args.warmup,
-            'ms_per_step': elapsed / args.steps * 1e3,
-            'higher_is_better': True,
-            'scaling': 'weak',
-            'vs_baseline': None,
-            'dtype': 'f32',
-            'data': DATA[args.workload],
-            'config': {'workload': WORKLOAD[args.workload].format(P=P),
-                       'pairs_per_gpu': P, 'global_batch': P * world,
-                       'points_per_cloud': int(np.mean([len(c) for c in src])),
-                       'parallelism': f'pair-sharded dp{world}'},
-            'roofline': {'kernel': 'fgr_kpconv_gather', 'bound': 'hbm',
-                         'achieved': g_achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                         'frac': g_achieved / HBM_PEAK_GBS, 'traffic': traffic,
-                         'algorithmic_bytes_per_launch': g_bytes_launch,
-                         'avg_launch_us': g_avg_s * 1e6, 'launches_per_step': len(gather_bytes),
-                         'share_of_step': g_ms / (elapsed * 1e3)},
-            'roofline_attention': {'kernel': f'fgr_attention_{ops.ATTN_MODE}', 'bound': 'mfma',
-                                   'achieved': a_achieved, 'peak': FP32_MFMA_PEAK_TFLOPS,
-                                   'unit': 'TFLOP/s (fp32-equivalent)',
-                                   'frac': a_achieved / FP32_MFMA_PEAK_TFLOPS,
-                                   'flops_per_step': a_flops_step,
-                                   'avg_launch_us': a_ms * 1e3 / max(a_launches, 1),
-                                   'share_of_step': a_ms / (elapsed * 1e3),
-                                   'precision': PRECISION.get(ops.ATTN_MODE, ops.ATTN_MODE),
-                                   'matrix_pipe_tflops': PIPE.get(ops.ATTN_MODE, 1) * a_achieved,
-                                   'matrix_pipe_frac': PIPE.get(ops.ATTN_MODE, 1) * a_achieved /
-                                   (F16_MFMA_PEAK_TFLOPS if ops.ATTN_MODE != 'fp32'
-                                    else FP32_MFMA_PEAK_TFLOPS)},
-            'roofline_gemm': {'kernel': f'fgr_gemm_{lin.MODE} (all dense layers)', 'bound': 'mfma',
-                              'achieved': m_achieved, 'peak': FP32_MFMA_PEAK_TFLOPS,
-                              'unit': 'TFLOP/s (fp32-equivalent)',
-                              'frac': m_achieved / FP32_MFMA_PEAK_TFLOPS,
-                              'flops_per_step': m_flops_step,
-                              'launches_per_step': len(gemm_flops),
-                              'share_of_step': m_ms / (elapsed * 1e3),
-                              'precision': PRECISION.get(lin.MODE, lin.MODE),
-                              'matrix_pipe_frac': PIPE.get(lin.MODE, 1) * m_achieved /
-                              (F16_MFMA_PEAK_TFLOPS if lin.MODE != 'fp32'
-                               else FP32_MFMA_PEAK_TFLOPS)},
-            'test_tail': {'what': f'compute_loss + _compute_metrics of one step ({P} pair(s): '
-                                  'overlap pyramid, BCE, 2x InfoNCE, CorrCriterion, se3_compare)',
-                          'ms_per_step': tail_ms},
-            'cpu_baseline': cpu,
-        }
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
@@ -274,8 +330,17 @@ def test_tail(model, batch_src, batch_tgt, src, tgt, pose_gt, dev, iters):
     return ms, (out, batch)
 
 
+def _calibration():
+    path = os.path.join(REPO, 'profiles', 'cpu_calibration.json')
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f)
+
+
 def cpu_baseline(cfg, model, src, tgt, budget_s, tail_inputs=None):
-    """CPU restatement (oracle/model_oracle.py, "port") on the same pairs, for ~budget_s."""
+    """CPU restatement (oracle/model_oracle.py, "port") on the same pairs: B=1 forwards for
+    ~budget_s, then one B=len(src) forward (BASELINE.md §3 asks for both legs)."""
     sys.path.insert(0, os.path.join(REPO, 'oracle'))
     import model_oracle as mo
     sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
@@ -289,8 +354,19 @@ def cpu_baseline(cfg, model, src, tgt, budget_s, tail_inputs=None):
         n_pairs += 1
         it += 1
     res = {'value': n_pairs / t_tot, 'unit': 'pairs/s', 'cores': threads, 'kind': 'port',
+           'cpu_model': _cpu_model(),
            'sample': f'{n_pairs} pairs (B=1 forwards) of the same workload, '
                      f'{t_tot:.1f} s, torch CPU fp32 with {threads} threads'}
+    if len(src) > 1:
+        t0 = time.perf_counter()
+        mo.forward(cfg, sd, list(src), list(tgt), mode=mo.geom.INDEX)
+        tb = time.perf_counter() - t0
+        res['batch_leg'] = {'pairs_per_batch': len(src), 'value': len(src) / tb,
+                            'unit': 'pairs/s', 'seconds': tb}
+    cal = _calibration()
+    if cal is not None:
+        res['calibration'] = {k: cal[k] for k in ('reference_over_port', 'hardware', 'source')
+                              if k in cal}
     if tail_inputs is not None:       # the test-step tail on the same outputs (loss_oracle)
         import loss_oracle as lo
         out, batch = tail_inputs

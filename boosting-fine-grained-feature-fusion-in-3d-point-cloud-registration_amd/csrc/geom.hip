@@ -339,6 +339,7 @@ extern "C" int fgr_grid_subsample_count(const float* points, const int64_t* off,
                     (points || n_points == 0) && n_points < (1ll << 31),
                 "fgr_grid_subsample_count: bad arguments");
     hipStream_t st = as_stream(stream);
+    TimedCall timed_(st);
     GridWs g;
     size_t tb = cub_temp_bytes(n_points, n_clouds);
     carve(ws, n_points, n_clouds, tb, &g);
@@ -420,6 +421,7 @@ extern "C" int fgr_radius_search(const float* q, const int64_t* q_off, const flo
                 "fgr_radius_search: mode %d / width %d unsupported", mode, width);
     if (nq == 0 || width == 0 || max_q_len == 0) return FGR_OK;
     hipStream_t st = as_stream(stream);
+    TimedCall timed_(st);
     const float r2 = radius * radius;
     if (mode == FGR_NB_INDEX) {
         dim3 grid((unsigned)ceil_div(max_q_len, kWaveQueries), (unsigned)n_clouds);

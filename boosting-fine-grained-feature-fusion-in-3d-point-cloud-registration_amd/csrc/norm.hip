@@ -362,6 +362,7 @@ extern "C" int fgr_instnorm(const float* x, int64_t n, int32_t c, const int64_t*
     const int64_t chunks = ceil_div(max_seg_len, kChunk);
     InArgs a{x, c, seg_off, row_div, eps, act, residual, post_act, out, (float*)ws, (int)chunks};
     hipStream_t st = as_stream(stream);
+    TimedCall timed_(st);
     const unsigned cx = (unsigned)ceil_div(c, 64);
     if (max_seg_len <= kSegRows) {
         hipLaunchKernelGGL(instnorm_seg16_kernel, dim3((unsigned)ceil_div(c, 16), n_seg, 1),
@@ -390,6 +391,7 @@ extern "C" int fgr_layernorm(float* x, int64_t n, int32_t d, const float* gamma,
     if (n == 0) return FGR_OK;
     dim3 grid((unsigned)ceil_div(n, 4));
     hipStream_t st = as_stream(stream);
+    TimedCall timed_(st);
     const bool vec = d % 64 == 0 && d <= 1024 &&
                      ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(out) |
                        reinterpret_cast<uintptr_t>(gamma) | reinterpret_cast<uintptr_t>(beta) |

@@ -229,6 +229,7 @@ extern "C" int fgr_pair_pose(const float* xyz, const float* corr, const float* l
     FGR_REQUIRE(n_pairs > 0 && n_layers > 0 && n_tot >= 0 && seg_off && xyz && corr && logits &&
                     out,
                 "fgr_pair_pose: bad arguments");
+    TimedCall timed_(as_stream(stream));
     hipLaunchKernelGGL(pair_pose_kernel, dim3((unsigned)n_pairs, (unsigned)n_layers),
                        dim3(kPoseThreads), 0, as_stream(stream), xyz, corr, logits, n_tot,
                        seg_off, n_pairs, threshold, out);

@@ -247,8 +247,9 @@ class my_Bottle2neck(nn.Module):  # noqa: N801 -- reference name (res2net.py:84)
         return (lin.weight * s[:, None]).contiguous(), (bn.bias - bn.running_mean * s).contiguous()
 
     def _folded_params(self):
-        key = tuple(p._version for p in self.parameters()) + tuple(
-            b._version for b in self.buffers())
+        # version AND storage pointer: Module.to() / .cuda() swap .data without a version bump
+        key = tuple((p._version, p.data_ptr()) for p in self.parameters()) + tuple(
+            (b._version, b.data_ptr()) for b in self.buffers())
         if self._folded is None or self._folded[0] != key:
             with torch.no_grad():
                 w1, b1 = self._fold(self.conv1, self.bn1)

@@ -88,9 +88,20 @@ def _stream():
 
 
 def _dev(*tensors):
+    """Operands must be GPU tensors on the CURRENT device: launches go to that device's
+    current stream (_stream), so a tensor on another device would hand foreign pointers
+    to the kernels. RegTR.forward enters the inputs' device itself."""
+    cur = None
     for t in tensors:
-        if t is not None and not t.is_cuda:
+        if t is None:
+            continue
+        if not t.is_cuda:
             raise _lib.FgrError('fgreg ops need GPU tensors (no CPU fallback by design)')
+        if cur is None:
+            cur = torch.cuda.current_device()
+        if t.device.index != cur:
+            raise _lib.FgrError(f'operand on {t.device} but the current device is cuda:{cur}: '
+                                f'wrap the call in `with torch.cuda.device({t.device}):`')
 
 
 def _c(t, dtype):
@@ -127,15 +138,19 @@ def grid_subsample(points: torch.Tensor, off: torch.Tensor, lengths: Sequence[in
     ws = torch.empty(ws_bytes.value, dtype=torch.uint8, device=pts.device)
     counts = torch.empty(nc + 1, dtype=torch.int64, device=pts.device)
     st = _stream()
+    t0 = _begin('grid_subsample')
     _lib.check(L.fgr_grid_subsample_count(_ptr(pts), _ptr(off), nc, n, float(dl), _ptr(ws),
                                           ws_bytes.value, _ptr(counts), st),
                'fgr_grid_subsample_count')
+    _end('grid_subsample', t0)
     host = counts.cpu().tolist()  # host sync: output size is data-dependent
     m = host[nc]
     out = torch.empty((m, 3), dtype=torch.float32, device=pts.device)
     keys = torch.empty((m,), dtype=torch.int64, device=pts.device) if return_keys else None
+    t0 = _begin('grid_subsample')
     _lib.check(L.fgr_grid_subsample_fill(n, nc, m, _ptr(ws), ws_bytes.value, _ptr(pts), _ptr(out),
                                          _ptr(keys), st), 'fgr_grid_subsample_fill')
+    _end('grid_subsample', t0, 12 * (n + m))   # D4: 12 (N_in + N_out) bytes
     if return_keys:
         return out, host[:nc], keys
     return out, host[:nc]
@@ -184,9 +199,12 @@ def radius_search(q: torch.Tensor, q_off: torch.Tensor, q_lengths: Sequence[int]
         m = int(mx.item())
         width = m if limit <= 0 else min(m, int(limit))
     out = torch.empty((q.shape[0], width), dtype=torch.int64, device=q.device)
+    t0 = _begin('radius_search')
     _lib.check(L.fgr_radius_search(_ptr(q), _ptr(q_off), _ptr(s), _ptr(s_off), nc, q.shape[0],
                                    s.shape[0], max_q, r, int(mode), width, _ptr(out), st),
                'fgr_radius_search')
+    # D4: 12 (Nq + Ns) + idx_bytes * Nq * K
+    _end('radius_search', t0, 12 * (q.shape[0] + s.shape[0]) + 8 * q.shape[0] * width)
     return out
 
 
@@ -260,9 +278,13 @@ def instnorm(x, seg_off, lengths, row_div=None, act=ACT_NONE, residual=None, pos
     nb = _lib._sz(0)
     _lib.check(L.fgr_instnorm_workspace(max_len, c, n_seg, nb), 'fgr_instnorm_workspace')
     ws = torch.empty(nb.value, dtype=torch.uint8, device=x.device) if nb.value else None
+    t0 = _begin('instnorm')
     _lib.check(L.fgr_instnorm(_ptr(x), n, c, _ptr(seg_off), n_seg, max_len, _ptr(row_div),
                               float(eps), act, _ptr(residual), post_act, _ptr(out), _ptr(ws),
                               nb.value, _stream()), 'fgr_instnorm')
+    # D4: 8 N C (read + write) + 4 N C per residual + 4 N for the row divisor
+    _end('instnorm', t0, n * c * (8 + (4 if residual is not None else 0))
+         + (4 * n if row_div is not None else 0))
     return out
 
 
@@ -280,9 +302,12 @@ def layernorm(x, weight, bias, eps=1e-5, add=None, pre_bias=None, out=None) -> t
     if out is None:
         out = torch.empty_like(x)
     assert out.is_contiguous() and out.shape == x.shape
+    t0 = _begin('layernorm')
     _lib.check(_lib.load().fgr_layernorm(_ptr(x), n, d, _ptr(weight.contiguous()),
                                          _ptr(bias.contiguous()), float(eps), _ptr(add),
                                          _ptr(pre_bias), _ptr(out), _stream()), 'fgr_layernorm')
+    _end('layernorm', t0, n * d * (8 + (4 if add is not None else 0)
+                                   + (4 if pre_bias is not None else 0)))
     return out
 
 
@@ -480,7 +505,10 @@ def pair_pose(xyz, corr, logits, seg_off, n_pairs, threshold=0.85) -> torch.Tens
     assert xyz.shape == (n_tot, 3) and logits.shape == (n_layers, n_tot)
     assert seg_off.numel() == 2 * n_pairs + 1
     out = torch.empty((n_layers, n_pairs, 3, 4), dtype=torch.float32, device=xyz.device)
+    t0 = _begin('pose')
     _lib.check(_lib.load().fgr_pair_pose(_ptr(xyz), _ptr(corr), _ptr(logits), n_tot,
                                          _ptr(seg_off), n_pairs, n_layers, float(threshold),
                                          _ptr(out), _stream()), 'fgr_pair_pose')
+    # D4: per (layer, point) xyz 12 + corr 12 + logit 4 = 28 B, + 48 B per pose
+    _end('pose', t0, n_layers * (28 * n_tot + 48 * n_pairs))
     return out

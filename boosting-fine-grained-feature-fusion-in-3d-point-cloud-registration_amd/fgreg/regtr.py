@@ -129,10 +129,22 @@ class RegTR(nn.Module):
             self.feature_criterion_un = _LossParams(cfg.d_embed)
         self.pose_threshold = 0.85   # hard-coded in fast_compute_rigid_transform (se3_torch.py:226)
 
-    @torch.no_grad()
     def forward(self, batch):
-        if torch.is_grad_enabled() and self.training:
-            raise NotImplementedError('fgreg implements the inference forward only')
+        # The guard runs before entering no_grad (a @torch.no_grad() decorator would make
+        # is_grad_enabled() always False here and the check dead).
+        if self.training and torch.is_grad_enabled():
+            raise NotImplementedError(
+                'fgreg.RegTR.forward is the inference forward (eval(), no autograd); training '
+                'mode with gradients (train.py) is not implemented -- call model.eval() or run '
+                'under torch.no_grad()')
+        dev = batch['src_xyz'][0].device
+        if dev.type != 'cuda':          # the ops raise FgrError on host tensors (no CPU path)
+            with torch.no_grad():
+                return self._forward(batch)
+        with torch.no_grad(), torch.cuda.device(dev):
+            return self._forward(batch)
+
+    def _forward(self, batch):
         B = len(batch['src_xyz'])
         meta = self.preprocessor(list(batch['src_xyz']) + list(batch['tgt_xyz']))
         batch['kpconv_meta'] = meta

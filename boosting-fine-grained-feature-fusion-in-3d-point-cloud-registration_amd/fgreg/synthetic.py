@@ -134,12 +134,30 @@ def modelnet_reference_pair(i, n_raw=2048):
             smp['pose'].numpy().astype(np.float32))
 
 
+def modelnet_raw_pair(i, n_raw=2048, rot_mag=45.0, trans_mag=0.5):
+    """The raw-2048 stress input ("feed the 2048-pt clouds directly"):
+    the box-surface raw cloud of pair i, uncropped and not resampled, as the target, and the
+    same cloud under a random euler SE3 (45 deg, 0.5) plus jitter (0.01, clip 0.05) as the
+    source. Returns (src (n_raw,3) f32, tgt (n_raw,3) f32, pose (3,4) f32: src -> tgt)."""
+    rng = np.random.default_rng(1000003 * (i + 1))
+    raw = _box_surface(rng, n_raw)
+    ang = np.deg2rad(rng.uniform(-rot_mag, rot_mag, 3))
+    R = _euler_rotation(ang)
+    t = rng.uniform(-trans_mag, trans_mag, 3)
+    jit = lambda p: p + np.clip(rng.normal(0.0, 0.01, p.shape), -0.05, 0.05)
+    src = jit(raw @ R.T + t)[rng.permutation(n_raw)]
+    tgt = jit(raw)
+    pose = np.concatenate([R.T, (-R.T @ t)[:, None]], 1)
+    return src.astype(np.float32), tgt.astype(np.float32), pose.astype(np.float32)
+
+
 def make_batch(kind, batch_size, start=0, **kw):
     """List-of-clouds batch in the reference's collate_pair layout (collate_functions.py:4-22).
     'modelnet': the reference's crop test pipeline on synthetic raw clouds; 'modelnet_like':
-    the seeded approximation above; otherwise 3DMatch-like fragments."""
-    gen = {'modelnet': modelnet_reference_pair, 'modelnet_like': modelnet_like_pair}.get(
-        kind, indoor_like_pair)
+    the seeded approximation above; 'modelnet_raw': the uncropped 2048-pt stress input;
+    otherwise 3DMatch-like fragments."""
+    gen = {'modelnet': modelnet_reference_pair, 'modelnet_like': modelnet_like_pair,
+           'modelnet_raw': modelnet_raw_pair}.get(kind, indoor_like_pair)
     pairs = [gen(start + b, **kw) for b in range(batch_size)]
     return ([p[0] for p in pairs], [p[1] for p in pairs],
             np.stack([p[2] for p in pairs]).astype(np.float32))

@@ -62,6 +62,7 @@ class RegTR(GenericRegModel):
         self.weight_dict['feature_un'] = cfg.wt_feature_un
 
     forward = fgreg.RegTR.forward
+    _forward = fgreg.RegTR._forward
 
     def compute_loss(self, pred, batch):
         """finegrained_regtr.py:252-309 on libfgreg (fgreg/loss.py): overlap BCE, InfoNCE

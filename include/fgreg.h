@@ -148,7 +148,7 @@ int fgr_sine_pos_embed(const float* xyz, int64_t n, int32_t d_model, float tempe
 int fgr_res2net_chain(const float* h, int64_t n, int32_t w, int32_t scale, const float* w_frag,
                       const float* bias, const float* x, int32_t cin, float* cat, int64_t ld_cat,
                       void* stream);
-/* fp32-accurate bf16x6 variant (the default): w_img = the (nums, w, w) folded weights
+/* fp32-accurate bf16x6 variant (used for w = 224, where it measured faster): w_img = the (nums, w, w) folded weights
  * K-padded to a multiple of 32, split into three bf16 terms and laid out in 16x16x32
  * fragment order [i][jt][ks][term][g][c][8] (fgreg.ops.res2net_fragments3); h 16-B aligned. */
 int fgr_res2net_chain6(const float* h, int64_t n, int32_t w, int32_t scale, const void* w_img,
@@ -176,7 +176,8 @@ int fgr_gemm_bf16x3(const float* a, int64_t lda, const void* w_hi, const void* w
                     float* c, int64_t ldc, const float* bias, const float* r, int64_t ldr,
                     int32_t m, int32_t n, int32_t k, int32_t act, void* stream);
 
-/* fp32-accurate split GEMM (the default for every dense layer of the forward):
+/* fp32-accurate split-bf16 GEMM ("bf16x6", opt-in FGREG_GEMM=bf16x6; the default is
+ * fgr_gemm_f16x3 below):
  *   C[m, n] = act(A[m, :] . W[n, :] + bias[n] (+ R[m, n]))
  * Operands are split exactly into three bf16 terms (x = h + m + l, residual <= 2^-27 |x|)
  * and the six significant term products accumulate in fp32 on v_mfma_f32_16x16x32_bf16.

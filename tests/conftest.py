@@ -60,6 +60,21 @@ def rel_err(a, b):
     return float((a - b).abs().max() / max(float(b.abs().max()), 1e-30))
 
 
+def elem_err(a, b, floor=1e-2):
+    """Elementwise relative error with an absolute floor:
+    max_i |a_i - b_i| / max(|b_i|, floor * max|b|). Unlike rel_err it does not let a
+    small-magnitude entry hide behind the tensor's largest one; the floor keeps entries
+    that are ~0 by cancellation (where any fp32 path has only absolute accuracy) from
+    dividing by ~0."""
+    a = a.detach().double().cpu() if torch.is_tensor(a) else torch.as_tensor(np.asarray(a, np.float64))
+    b = b.detach().double().cpu() if torch.is_tensor(b) else torch.as_tensor(np.asarray(b, np.float64))
+    assert a.shape == b.shape, (a.shape, b.shape)
+    if b.numel() == 0:
+        return 0.0
+    den = torch.clamp(b.abs(), min=max(floor * float(b.abs().max()), 1e-30))
+    return float(((a - b).abs() / den).max())
+
+
 @pytest.fixture(scope='session')
 def gpu():
     if not torch.cuda.is_available():

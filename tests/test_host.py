@@ -181,3 +181,16 @@ def test_f16x3_split_numerics():
     den = np.abs(x).astype(np.float64) @ np.abs(w).astype(np.float64).T + 1e-300
     assert (got[3] == 0).all()
     assert (np.abs(got - ref) / den).max() < 2e-6
+
+
+def test_training_mode_with_grad_raises_clearly():
+    """model.train() + a forward with autograd on (what train.py does) fails fast with a clear
+    message before any kernel launch; eval() or no_grad() is the supported inference path."""
+    import fgreg
+    import fgreg.config as fc
+    model = fgreg.RegTR(fc.get('modelnet')).train()
+    batch = {'src_xyz': [torch.zeros(8, 3)], 'tgt_xyz': [torch.zeros(8, 3)]}
+    with pytest.raises(NotImplementedError, match='inference forward'):
+        model(batch)
+    with torch.no_grad(), pytest.raises(fgreg.FgrError):   # guard passes; CPU tensors refused
+        model(batch)

@@ -1,15 +1,22 @@
 #!/bin/bash
-# One GPU session: parity tests, bench, kernel-trace profile, PMC traffic passes of the gather.
-# usage (on the GPU box, from the repo root): bash tools/gpu_round.sh <tag>
-# The profiled bench runs 3 warmup + 1 counting + 10 timed + 10 GEMM-instrumented forwards:
-# per-step kernel stats = python tools/kernel_stats.py <kernel_stats.csv> 24
+# One GPU session: parity tests, bench lines, kernel-trace profiles of the timed steps only,
+# PMC traffic passes of the KPConv gather. Every GPU step has its own time limit and the
+# steps are chained: the first failure (fault, abort, timeout) ends the script.
+# usage (on the GPU box, from the repo root): bash tools/gpu_round.sh <tag> [skip-tests]
 set -o pipefail
 tag=${1:-run}
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests -m gpu -q -p no:cacheprovider > gpurun_out/tests_$tag.log 2>&1; echo "EXIT $?" >> gpurun_out/tests_$tag.log
+W=2; K=20          # profiled runs: forwards = W + K (tools/kernel_stats.py)
+if [ "$2" != "skip-tests" ]; then
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+      -p no:cacheprovider > gpurun_out/tests_$tag.log 2>&1 || { echo "TESTS FAILED $?"; tail -30 gpurun_out/tests_$tag.log; exit 1; }
+  tail -3 gpurun_out/tests_$tag.log
+fi
 timeout -k 10 400 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_$tag.json 2> gpurun_out/bench_$tag.err || exit 1
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$tag -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/prof_$tag.log 2>&1 || exit 1
-timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex 'kpconv_gather|row_positive' --output-format csv -d gpurun_out/pmcf_$tag -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/pmcf_$tag.log 2>&1 || exit 1
-timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex 'kpconv_gather|row_positive' --output-format csv -d gpurun_out/pmcw_$tag -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/pmcw_$tag.log 2>&1 || exit 1
+timeout -k 10 400 python bench.py --workload 3dmatch --steps 10 --warmup 3 > gpurun_out/bench3d_$tag.json 2> gpurun_out/bench3d_$tag.err || exit 1
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$tag -- python3 bench.py --profile --steps $K --warmup $W > gpurun_out/prof_$tag.json 2> gpurun_out/prof_$tag.err || exit 1
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof3d_$tag -- python3 bench.py --profile --workload 3dmatch --steps $K --warmup $W > gpurun_out/prof3d_$tag.json 2> gpurun_out/prof3d_$tag.err || exit 1
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex 'kpconv_gather' --output-format csv -d gpurun_out/pmcf_$tag -- python3 bench.py --profile --steps 3 --warmup 1 > gpurun_out/pmcf_$tag.log 2>&1 || exit 1
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex 'kpconv_gather' --output-format csv -d gpurun_out/pmcw_$tag -- python3 bench.py --profile --steps 3 --warmup 1 > gpurun_out/pmcw_$tag.log 2>&1 || exit 1
 echo DONE

@@ -1,42 +1,37 @@
-"""Per-launch HBM traffic of the KPConv gather op from two rocprofv3 PMC passes.
+"""Per-launch HBM traffic of one op from two rocprofv3 PMC passes of `bench.py --profile`.
 
-usage: python tools/pmc_traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv>
-                                   > profiles/pmc_kpconv_gather.json
-(op launches = dispatches of kpconv_gather_* kernels, one per fgr_kpconv_gather call)
+usage: python tools/pmc_traffic.py <op> <kernel-regex> <fetch counter_collection.csv>
+                                   <write counter_collection.csv> > profiles/pmc_kpconv.json
 
-The op fgr_kpconv_gather is two kernels (row_positive_kernel + kpconv_gather_wide, or
-kpconv_gather_narrow alone); both are summed. Corrections per MI355X_MICROARCH.md
-§HBM: FETCH_SIZE reports half the bytes of wide coalesced reads on gfx950 -> x2;
-WRITE_SIZE is exact for 16-B-per-lane stores. FETCH_SIZE / WRITE_SIZE are in KB.
+Every dispatch of a kernel matching <kernel-regex> is one launch of <op> (e.g.
+fgr_kpconv_gather = kpconv_gather_wide / _narrow / _c1). Corrections per
+MI355X_MICROARCH.md §HBM: FETCH_SIZE reports half the bytes of wide coalesced reads on gfx950
+-> x2; WRITE_SIZE is exact for 16-B-per-lane stores. FETCH_SIZE / WRITE_SIZE are in KB.
 """
 import csv
 import json
+import re
 import sys
 
-PATTERNS = ('kpconv_gather', 'row_positive_kernel')
 
-
-def total(path, counter):
-    tot, n, ops = 0.0, 0, set()
+def total(path, counter, rx):
+    tot, ids = 0.0, set()
     for r in csv.DictReader(open(path)):
-        if r['Counter_Name'] == counter and any(p in r['Kernel_Name'] for p in PATTERNS):
+        if r['Counter_Name'] == counter and rx.search(r['Kernel_Name']):
             tot += float(r['Counter_Value'])
-            n += 1
-            if 'kpconv_gather' in r['Kernel_Name']:
-                ops.add(r['Dispatch_Id'])
-    return tot, n, len(ops)
+            ids.add(r['Dispatch_Id'])
+    return tot, len(ids)
 
 
 def main():
-    fetch_csv, write_csv = sys.argv[1], sys.argv[2]
-    f_kb, nf, launches = total(fetch_csv, 'FETCH_SIZE')
-    w_kb, nw, launches_w = total(write_csv, 'WRITE_SIZE')
-    assert launches == launches_w and launches > 0, (launches, launches_w)
-    fetch = 2.0 * f_kb * 1024 / launches
-    write = w_kb * 1024 / launches
+    op, rx, fetch_csv, write_csv = sys.argv[1], re.compile(sys.argv[2]), sys.argv[3], sys.argv[4]
+    f_kb, nf = total(fetch_csv, 'FETCH_SIZE', rx)
+    w_kb, nw = total(write_csv, 'WRITE_SIZE', rx)
+    assert nf == nw and nf > 0, (nf, nw)
+    fetch = 2.0 * f_kb * 1024 / nf
+    write = w_kb * 1024 / nw
     print(json.dumps({
-        'kernel': 'fgr_kpconv_gather (row_positive_kernel + kpconv_gather_*)',
-        'op_launches': launches, 'kernel_dispatches': [nf, nw],
+        'op': op, 'kernel_regex': sys.argv[2], 'launches': nf,
         'fetch_size_kb_total_raw': f_kb, 'write_size_kb_total': w_kb,
         'hbm_read_bytes_per_launch': fetch, 'hbm_write_bytes_per_launch': write,
         'hbm_bytes_per_launch': fetch + write,
