@@ -188,7 +188,12 @@ def main():
         for _ in range(max(args.warmup, 1)):
             step()
         if args.profile:
+            # marker kernels around the timed region: tools/kernel_stats.py sums only the
+            # dispatches between them (torch's spin kernel, ~1 us)
+            torch.cuda._sleep(1000)
             elapsed = timed(args.steps)
+            torch.cuda._sleep(1000)
+            torch.cuda.synchronize()
         else:
             # algorithmic work per launch (untimed pass with counting on)
             fams = ['kpconv_gather', 'attention', 'gemm'] + list(OTHER)

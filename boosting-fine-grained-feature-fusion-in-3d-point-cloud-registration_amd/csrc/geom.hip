@@ -323,23 +323,19 @@ radius_dist_kernel(const float* __restrict__ q, const int64_t* __restrict__ q_of
 
 using namespace fgr;
 
-extern "C" int fgr_grid_subsample_workspace(int64_t n_points, int32_t n_clouds, size_t* bytes) {
-    FGR_REQUIRE(bytes && n_points >= 0 && n_clouds > 0 && n_points < (1ll << 31),
-                "fgr_grid_subsample_workspace: bad arguments");
+namespace fgr {
+
+// The radix-sort path of grid subsampling (hipCUB segmented sort of the voxel keys), used by
+// the entry points in grid.hip when the caller selects it (max_cells < 0): it handles any key
+// space, the dense counting-sort path only those that fit its histogram.
+size_t grid_radix_ws_bytes(int64_t n_points, int32_t n_clouds) {
     GridWs g;
     carve(nullptr, n_points, n_clouds, cub_temp_bytes(n_points, n_clouds), &g);
-    *bytes = g.total;
-    return FGR_OK;
+    return g.total;
 }
 
-extern "C" int fgr_grid_subsample_count(const float* points, const int64_t* off, int32_t n_clouds,
-                                        int64_t n_points, float dl, void* ws, size_t ws_bytes,
-                                        int64_t* counts, void* stream) {
-    FGR_REQUIRE(off && counts && ws && n_clouds > 0 && n_points >= 0 && dl > 0.f &&
-                    (points || n_points == 0) && n_points < (1ll << 31),
-                "fgr_grid_subsample_count: bad arguments");
-    hipStream_t st = as_stream(stream);
-    TimedCall timed_(st);
+int grid_radix_count(const float* points, const int64_t* off, int32_t n_clouds, int64_t n_points,
+                     float dl, void* ws, size_t ws_bytes, int64_t* counts, hipStream_t st) {
     GridWs g;
     size_t tb = cub_temp_bytes(n_points, n_clouds);
     carve(ws, n_points, n_clouds, tb, &g);
@@ -373,11 +369,8 @@ extern "C" int fgr_grid_subsample_count(const float* points, const int64_t* off,
     return FGR_OK;
 }
 
-extern "C" int fgr_grid_subsample_fill(int64_t n_points, int32_t n_clouds, int64_t n_out, void* ws,
-                                       size_t ws_bytes, const float* points, float* out_points,
-                                       int64_t* out_keys, void* stream) {
-    FGR_REQUIRE(ws && n_clouds > 0 && n_out >= 0 && n_out <= n_points && (out_points || n_out == 0),
-                "fgr_grid_subsample_fill: bad arguments");
+int grid_radix_fill(int64_t n_points, int32_t n_clouds, int64_t n_out, void* ws, size_t ws_bytes,
+                    const float* points, float* out_points, int64_t* out_keys, hipStream_t st) {
     GridWs g;
     carve(ws, n_points, n_clouds, cub_temp_bytes(n_points, n_clouds), &g);
     if (g.total > ws_bytes) {
@@ -385,12 +378,13 @@ extern "C" int fgr_grid_subsample_fill(int64_t n_points, int32_t n_clouds, int64
         return FGR_E_WORKSPACE;
     }
     if (n_out == 0) return FGR_OK;
-    hipLaunchKernelGGL(grid_fill_kernel, dim3(ceil_div(n_out, 256)), dim3(256), 0,
-                       as_stream(stream), points, g.svals, g.skeys, g.vstart, n_out, out_points,
-                       out_keys);
+    hipLaunchKernelGGL(grid_fill_kernel, dim3(ceil_div(n_out, 256)), dim3(256), 0, st, points,
+                       g.svals, g.skeys, g.vstart, n_out, out_points, out_keys);
     FGR_CHECK_LAUNCH("grid_fill_kernel");
     return FGR_OK;
 }
+
+}  // namespace fgr
 
 extern "C" int fgr_radius_count(const float* q, const int64_t* q_off, const float* s,
                                 const int64_t* s_off, int32_t n_clouds, int64_t nq,

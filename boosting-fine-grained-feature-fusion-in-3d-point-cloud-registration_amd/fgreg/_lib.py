@@ -20,9 +20,13 @@ _sz = ctypes.c_size_t
 
 # name -> argtypes (all return int status)
 SIGNATURES = {
-    'fgr_grid_subsample_workspace': [_i64, _i32, ctypes.POINTER(_sz)],
-    'fgr_grid_subsample_count': [_vp, _vp, _i32, _i64, _f32, _vp, _sz, _vp, _vp],
-    'fgr_grid_subsample_fill': [_i64, _i32, _i64, _vp, _sz, _vp, _vp, _vp, _vp],
+    'fgr_grid_subsample_workspace': [_i64, _i32, _i64, ctypes.POINTER(_sz)],
+    'fgr_grid_subsample_count': [_vp, _vp, _i32, _i64, _f32, _i64, _vp, _sz, _vp, _vp],
+    'fgr_grid_subsample_fill': [_i64, _i32, _i64, _i64, _vp, _sz, _vp, _vp, _vp, _vp],
+    'fgr_radius_grid_workspace': [_i64, _i32, ctypes.POINTER(_sz)],
+    'fgr_radius_grid_build': [_vp, _vp, _i32, _i64, _f32, _vp, _sz, _vp],
+    'fgr_radius_search_grid': [_vp, _vp, _i32, _i64, _i32, _vp, _vp, _i64, _vp, _sz, _f32, _i32,
+                               _i32, _vp, _vp, _vp, _vp],
     'fgr_radius_count': [_vp, _vp, _vp, _vp, _i32, _i64, _i32, _f32, _vp, _vp, _vp],
     'fgr_radius_search': [_vp, _vp, _vp, _vp, _i32, _i64, _i64, _i32, _f32, _i32, _i32, _vp, _vp],
     'fgr_kpconv_gather_workspace': [_i64, _i32, ctypes.POINTER(_sz)],

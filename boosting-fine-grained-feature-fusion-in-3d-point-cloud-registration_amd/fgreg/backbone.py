@@ -68,9 +68,12 @@ class PreprocessorHIP(nn.Module):
             if any('deformable' in b for b in layer_blocks[:-1]) or 'deformable' in block:
                 raise NotImplementedError('deformable KPConv is not used by the reference configs')
             r = r_normal
+            # one cell grid over this level's points serves the conv and the pool tables
+            # (same supports, same radius); None for small clouds (brute-force scan)
+            grid = ops.radius_grid(points, off, lens, r)
             if layer_blocks:
                 conv_i = ops.radius_search(points, off, lens, points, off, lens, r, limits[layer],
-                                           self.mode)
+                                           self.mode, grid=grid)
             else:
                 conv_i = torch.zeros((0, 1), dtype=torch.int64, device=device)
             if 'pool' in block or 'strided' in block:
@@ -78,9 +81,10 @@ class PreprocessorHIP(nn.Module):
                 pool_p, pool_lens = ops.grid_subsample(points, off, lens, dl)
                 pool_off = ops.offsets(pool_lens, device)
                 pool_i = ops.radius_search(pool_p, pool_off, pool_lens, points, off, lens, r,
-                                           limits[layer], self.mode)
+                                           limits[layer], self.mode, grid=grid)
+                up_grid = ops.radius_grid(pool_p, pool_off, pool_lens, 2 * r)
                 up_i = ops.radius_search(points, off, lens, pool_p, pool_off, pool_lens, 2 * r,
-                                         limits[layer], self.mode)
+                                         limits[layer], self.mode, grid=up_grid)
             else:
                 pool_p = torch.zeros((0, 3), dtype=torch.float32, device=device)
                 pool_lens, pool_off = [], None

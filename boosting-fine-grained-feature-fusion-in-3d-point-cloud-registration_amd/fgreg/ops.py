@@ -121,48 +121,106 @@ def offsets(lengths: Sequence[int], device) -> torch.Tensor:
 # ------------------------------------------------------------------------------------------
 # geometry
 # ------------------------------------------------------------------------------------------
+GRID_RADIX = os.environ.get('FGREG_GRID_SORT', 'dense') == 'radix'   # A/B switch (tests)
+
+
 def grid_subsample(points: torch.Tensor, off: torch.Tensor, lengths: Sequence[int], dl: float,
-                   return_keys=False):
+                   return_keys=False, max_cells=None):
     """Barycentre grid subsampling per cloud (grid_subsampling.cpp semantics).
 
     Returns (sub_points (M,3) f32, sub_lengths List[int][, keys (M,) int64]). One host
-    sync (the voxel counts), as in the reference's own GPU path.
+    sync (the voxel counts), as in the reference's own GPU path. ``max_cells``: the dense
+    voxel-key histogram's capacity (None = the library default, -1 = the radix-sort path);
+    a key space past it is reported by the count call and the count is redone with the
+    needed capacity (or the radix path beyond 2^28 counters).
     """
     _dev(points, off)
     pts = _c(points, torch.float32)
     n, nc = pts.shape[0], len(lengths)
     assert pts.dim() == 2 and pts.shape[1] == 3 and off.numel() == nc + 1
     L = _lib.load()
-    ws_bytes = _lib._sz(0)
-    _lib.check(L.fgr_grid_subsample_workspace(n, nc, ws_bytes), 'fgr_grid_subsample_workspace')
-    ws = torch.empty(ws_bytes.value, dtype=torch.uint8, device=pts.device)
+    cap = (-1 if GRID_RADIX else 0) if max_cells is None else int(max_cells)
     counts = torch.empty(nc + 1, dtype=torch.int64, device=pts.device)
     st = _stream()
-    t0 = _begin('grid_subsample')
-    _lib.check(L.fgr_grid_subsample_count(_ptr(pts), _ptr(off), nc, n, float(dl), _ptr(ws),
-                                          ws_bytes.value, _ptr(counts), st),
-               'fgr_grid_subsample_count')
-    _end('grid_subsample', t0)
-    host = counts.cpu().tolist()  # host sync: output size is data-dependent
+    for _ in range(2):
+        ws_bytes = _lib._sz(0)
+        _lib.check(L.fgr_grid_subsample_workspace(n, nc, cap, ws_bytes),
+                   'fgr_grid_subsample_workspace')
+        ws = torch.empty(ws_bytes.value, dtype=torch.uint8, device=pts.device)
+        t0 = _begin('grid_subsample')
+        _lib.check(L.fgr_grid_subsample_count(_ptr(pts), _ptr(off), nc, n, float(dl), cap,
+                                              _ptr(ws), ws_bytes.value, _ptr(counts), st),
+                   'fgr_grid_subsample_count')
+        _end('grid_subsample', t0)
+        host = counts.cpu().tolist()  # host sync: output size is data-dependent
+        if host[nc] >= 0:
+            break
+        need = -host[nc]           # dense key space past the histogram: retry once
+        cap = need if need <= (1 << 28) else -1
     m = host[nc]
+    assert m >= 0, 'grid subsampling: key space overflow after retry'
     out = torch.empty((m, 3), dtype=torch.float32, device=pts.device)
     keys = torch.empty((m,), dtype=torch.int64, device=pts.device) if return_keys else None
     t0 = _begin('grid_subsample')
-    _lib.check(L.fgr_grid_subsample_fill(n, nc, m, _ptr(ws), ws_bytes.value, _ptr(pts), _ptr(out),
-                                         _ptr(keys), st), 'fgr_grid_subsample_fill')
+    _lib.check(L.fgr_grid_subsample_fill(n, nc, cap, m, _ptr(ws), ws_bytes.value, _ptr(pts),
+                                         _ptr(out), _ptr(keys), st), 'fgr_grid_subsample_fill')
     _end('grid_subsample', t0, 12 * (n + m))   # D4: 12 (N_in + N_out) bytes
     if return_keys:
         return out, host[:nc], keys
     return out, host[:nc]
 
 
-def radius_count(q, q_off, q_lengths, s, s_off, radius) -> Tuple[torch.Tensor, int]:
+# Radius search over a cell grid for clouds of at least this many supports (below it the
+# brute-force index-order scan is faster: fewer launches, the cloud stays in L1/L2).
+GRID_MIN_SUPPORTS = int(os.environ.get('FGREG_RADIUS_GRID_MIN', '4096'))
+GRID_MAX_WIDTH = 256
+
+
+class RadiusGrid:
+    """Supports of a packed batch binned into cells for one radius (fgr_radius_grid_build);
+    serves every radius_search / radius_count over the same supports with radius <= that."""
+
+    def __init__(self, s, s_off, s_lengths, radius):
+        _dev(s, s_off)
+        self.s = _c(s, torch.float32)
+        self.s_off, self.s_lengths = s_off, list(s_lengths)
+        self.radius = float(radius)
+        nc = len(self.s_lengths)
+        L = _lib.load()
+        nb = _lib._sz(0)
+        _lib.check(L.fgr_radius_grid_workspace(self.s.shape[0], nc, nb), 'fgr_radius_grid_workspace')
+        self.ws = torch.empty(max(nb.value, 1), dtype=torch.uint8, device=s.device)
+        self.nbytes = nb.value
+        t0 = _begin('radius_search')
+        _lib.check(L.fgr_radius_grid_build(_ptr(self.s), _ptr(s_off), nc, self.s.shape[0],
+                                           self.radius, _ptr(self.ws), self.nbytes, _stream()),
+                   'fgr_radius_grid_build')
+        _end('radius_search', t0, 12 * self.s.shape[0])
+
+    def serves(self, s, radius):
+        return s.data_ptr() == self.s.data_ptr() and float(radius) <= self.radius
+
+
+def radius_grid(s, s_off, s_lengths, radius):
+    """A RadiusGrid when the clouds are large enough for the cell path, else None."""
+    if not len(s_lengths) or max(s_lengths) < GRID_MIN_SUPPORTS:
+        return None
+    return RadiusGrid(s, s_off, s_lengths, radius)
+
+
+def radius_count(q, q_off, q_lengths, s, s_off, radius, grid=None) -> Tuple[torch.Tensor, int]:
     """Uncapped neighbour counts (int32 per query) and their max (host int, one sync)."""
     _dev(q, q_off, s, s_off)
     q, s = _c(q, torch.float32), _c(s, torch.float32)
     counts = torch.empty(q.shape[0], dtype=torch.int32, device=q.device)
     mx = torch.empty(1, dtype=torch.int32, device=q.device)
     max_q = max(q_lengths) if len(q_lengths) else 0
+    if grid is not None and grid.serves(s, radius):
+        _lib.check(_lib.load().fgr_radius_search_grid(
+            _ptr(q), _ptr(q_off), len(q_lengths), q.shape[0], max_q, _ptr(s), _ptr(s_off),
+            s.shape[0], _ptr(grid.ws), grid.nbytes, float(radius), NB_INDEX, 0, None, _ptr(counts),
+            _ptr(mx), _stream()), 'fgr_radius_search_grid')
+        return counts, int(mx.item())
     _lib.check(_lib.load().fgr_radius_count(_ptr(q), _ptr(q_off), _ptr(s), _ptr(s_off),
                                             len(q_lengths), q.shape[0], max_q, float(radius), _ptr(counts),
                                             _ptr(mx), _stream()), 'fgr_radius_count')
@@ -171,11 +229,13 @@ def radius_count(q, q_off, q_lengths, s, s_off, radius) -> Tuple[torch.Tensor, i
 
 def radius_search(q: torch.Tensor, q_off: torch.Tensor, q_lengths: Sequence[int], s: torch.Tensor,
                   s_off: torch.Tensor, s_lengths: Sequence[int], radius: float, limit: int,
-                  mode: int = NB_INDEX) -> torch.Tensor:
+                  mode: int = NB_INDEX, grid: 'RadiusGrid' = None) -> torch.Tensor:
     """Radius neighbours, (Nq, width) int64 padded with the shadow index Ns_total.
 
     mode NB_INDEX: ball_query semantics, width = limit (no host sync).
     mode NB_DIST:  nanoflann semantics, width = min(max count, limit) (one host sync).
+    ``grid``: a RadiusGrid over these supports (radius_grid()), used when it serves this
+    radius and width <= 256; otherwise the brute-force scan.
     """
     _dev(q, q_off, s, s_off)
     q, s = _c(q, torch.float32), _c(s, torch.float32)
@@ -192,13 +252,17 @@ def radius_search(q: torch.Tensor, q_off: torch.Tensor, q_lengths: Sequence[int]
             raise _lib.FgrError('ball_query semantics need a positive neighbour limit')
         width = int(limit)
     else:
-        counts = torch.empty(q.shape[0], dtype=torch.int32, device=q.device)
-        mx = torch.empty(1, dtype=torch.int32, device=q.device)
-        _lib.check(L.fgr_radius_count(_ptr(q), _ptr(q_off), _ptr(s), _ptr(s_off), nc, q.shape[0],
-                                      max_q, r, _ptr(counts), _ptr(mx), st), 'fgr_radius_count')
-        m = int(mx.item())
+        _, m = radius_count(q, q_off, q_lengths, s, s_off, r, grid)
         width = m if limit <= 0 else min(m, int(limit))
     out = torch.empty((q.shape[0], width), dtype=torch.int64, device=q.device)
+    if grid is not None and grid.serves(s, r) and width <= GRID_MAX_WIDTH:
+        t0 = _begin('radius_search')
+        _lib.check(L.fgr_radius_search_grid(
+            _ptr(q), _ptr(q_off), nc, q.shape[0], max_q, _ptr(s), _ptr(s_off), s.shape[0],
+            _ptr(grid.ws), grid.nbytes, r, int(mode), width, _ptr(out), None, None, st),
+            'fgr_radius_search_grid')
+        _end('radius_search', t0, 12 * q.shape[0] + 8 * q.shape[0] * width)
+        return out
     t0 = _begin('radius_search')
     _lib.check(L.fgr_radius_search(_ptr(q), _ptr(q_off), _ptr(s), _ptr(s_off), nc, q.shape[0],
                                    s.shape[0], max_q, r, int(mode), width, _ptr(out), st),

@@ -58,7 +58,8 @@ const char* fgr_last_error(void);
 /* Opt-in instrumentation (bench.py's per-kernel rooflines; not part of the reference's
  * interface): arms two caller-created hipEvent_t for the NEXT timed entry point called on
  * this thread (fgr_kpconv_gather, fgr_attention*, fgr_gemm_bf16x6, fgr_gemm_f16x3,
- * fgr_gemm_rows_f16x3). That call records `start_event` on its stream right before its
+ * fgr_gemm_rows_f16x3, fgr_grid_subsample_count / _fill, fgr_radius_search,
+ * fgr_radius_grid_build, fgr_radius_search_grid, fgr_instnorm, fgr_layernorm, fgr_pair_pose). That call records `start_event` on its stream right before its
  * first kernel launch and `end_event` after its last one, then disarms; (NULL, NULL)
  * disarms explicitly. Thread-local like the error string. */
 int fgr_time_next_call(void* start_event, void* end_event);
@@ -68,17 +69,24 @@ int fgr_time_next_call(void* start_event, void* end_event);
  * UNWEIGHTED_AVERAGE) and its CPU twin subsample_batch
  * (cpp_subsampling/wrapper.cpp:62-333 -> grid_subsampling.cpp:5-211).
  * Voxel key and barycentre follow grid_subsampling.cpp bit for bit; voxels are
- * emitted in ascending key order per cloud.
+ * emitted in ascending key order per cloud, members summed in ascending point index.
+ * `max_cells` selects the path: > 0 a counting sort over a dense voxel-key histogram of that
+ * many counters (the clouds' key spaces nx*ny*nz laid end to end; 0 = the default
+ * 8 n_points + 2^20), < 0 the radix-sort path (any key space). The same max_cells must be
+ * passed to all three calls.
  * 1) fgr_grid_subsample_count: writes counts[c] (voxels of cloud c) and
- *    counts[n_clouds] (total) as int64; keeps the sorted state in `ws`.
+ *    counts[n_clouds] (total) as int64; keeps the sorted state in `ws`. Dense path only:
+ *    if the key space exceeds max_cells, counts[n_clouds] = -(cells needed) and nothing else
+ *    is valid -- call again with a larger max_cells (or -1).
  * 2) fgr_grid_subsample_fill: writes out_points (total, 3) and optionally the
  *    voxel keys (total) from the same `ws` (must follow the count call). */
-int fgr_grid_subsample_workspace(int64_t n_points, int32_t n_clouds, size_t* bytes);
+int fgr_grid_subsample_workspace(int64_t n_points, int32_t n_clouds, int64_t max_cells,
+                                 size_t* bytes);
 int fgr_grid_subsample_count(const float* points, const int64_t* off, int32_t n_clouds,
-                             int64_t n_points, float dl, void* ws, size_t ws_bytes,
-                             int64_t* counts, void* stream);
-int fgr_grid_subsample_fill(int64_t n_points, int32_t n_clouds, int64_t n_out, void* ws,
-                            size_t ws_bytes, const float* points, float* out_points,
+                             int64_t n_points, float dl, int64_t max_cells, void* ws,
+                             size_t ws_bytes, int64_t* counts, void* stream);
+int fgr_grid_subsample_fill(int64_t n_points, int32_t n_clouds, int64_t max_cells, int64_t n_out,
+                            void* ws, size_t ws_bytes, const float* points, float* out_points,
                             int64_t* out_keys, void* stream);
 
 /* ---- radius neighbour search -----------------------------------------------------
@@ -93,6 +101,22 @@ int fgr_radius_count(const float* q, const int64_t* q_off, const float* s, const
 int fgr_radius_search(const float* q, const int64_t* q_off, const float* s, const int64_t* s_off,
                       int32_t n_clouds, int64_t nq, int64_t ns, int32_t max_q_len, float radius,
                       int32_t mode, int32_t width, int64_t* out, void* stream);
+
+/* Cell-binned radius search for large clouds (same rows as fgr_radius_search, both modes):
+ * fgr_radius_grid_build bins the supports of every cloud into cubic cells of edge
+ * >= 1.0625 * radius (a counting sort; the grid workspace, fgr_radius_grid_workspace() bytes,
+ * depends on ns and n_clouds only); fgr_radius_search_grid then scans the 27 cells around
+ * each query. One grid serves every query set searched with a radius <= the build radius
+ * over the same supports (the conv and pool tables of a pyramid level). width <= 256.
+ * With counts != NULL it writes the uncapped counts + their max instead (fgr_radius_count). */
+int fgr_radius_grid_workspace(int64_t ns, int32_t n_clouds, size_t* bytes);
+int fgr_radius_grid_build(const float* s, const int64_t* s_off, int32_t n_clouds, int64_t ns,
+                          float radius, void* grid, size_t grid_bytes, void* stream);
+int fgr_radius_search_grid(const float* q, const int64_t* q_off, int32_t n_clouds, int64_t nq,
+                           int32_t max_q_len, const float* s, const int64_t* s_off, int64_t ns,
+                           const void* grid, size_t grid_bytes, float radius, int32_t mode,
+                           int32_t width, int64_t* out, int32_t* counts, int32_t* max_count,
+                           void* stream);
 
 /* ---- KPConv ------------------------------------------------------------------------
  * The gather-weight stage of KPConv.forward (finegrained_kpconv_blocks.py:296-381,

@@ -182,3 +182,69 @@ def test_geometry_at_3dmatch_scale(gpu):
     sub, sl = ops.grid_subsample(pd, off, lens, 2 * r / 2.5)
     o_pts, o_lens = og.grid_subsample(P, L, 2 * r / 2.5)
     assert sl == o_lens.tolist() and np.array_equal(sub.cpu().numpy(), o_pts)
+
+
+# ---- counting-sort paths (csrc/grid.hip) -----------------------------------------------------
+def _grid_cases():
+    """(name, points, lengths, radius): the golden inputs, a 3DMatch-size pair, a cloud with
+    600 coincident points (600 hits per query: the LDS rank list overflows -> bisection path)
+    and clouds of 0 / 1 points."""
+    from fgreg.synthetic import indoor_like_pair
+    out = []
+    for case in CASES:
+        g = golden(f'geom_{case}')
+        out.append((case, g['points'], [int(v) for v in g['lengths']], float(g['r0'])))
+    src, tgt, _ = indoor_like_pair(5)
+    out.append(('3dmatch', np.concatenate([src, tgt]), [len(src), len(tgt)], 0.0625))
+    rng = np.random.default_rng(2)
+    dup = np.concatenate([np.full((600, 3), 0.25, np.float32),
+                          rng.uniform(-1, 1, (900, 3)).astype(np.float32)])
+    dup = dup[rng.permutation(len(dup))]
+    one = rng.uniform(-1, 1, (1, 3)).astype(np.float32)
+    out.append(('dup', np.concatenate([dup, one]), [len(dup), 0, 1], 0.2))
+    return out
+
+
+@pytest.mark.parametrize('mode', ['index', 'dist'])
+def test_radius_grid_matches_bruteforce_and_oracle(gpu, mode):
+    """Every row of the cell-grid search equals the brute-force scan (and the oracle) in both
+    semantics, for conv (q = s), shifted queries partly outside the supports' bounding box,
+    widths 40 and 256, and the uncapped counts."""
+    import fgreg.ops as ops
+    m = ops.NB_INDEX if mode == 'index' else ops.NB_DIST
+    om = og.INDEX if mode == 'index' else og.DIST
+    for name, P, L, r in _grid_cases():
+        pd = torch.from_numpy(P).to(gpu)
+        lens, off = _lens_off(L, gpu)
+        grid = ops.RadiusGrid(pd, off, lens, r)
+        Q = (P + np.float32(0.7 * r)).astype(np.float32)          # some queries leave the bbox
+        qd = torch.from_numpy(Q).to(gpu)
+        for q, qt in ((P, pd), (Q, qd)):
+            for K in (40, 256):
+                a = ops.radius_search(qt, off, lens, pd, off, lens, r, K, m, grid=grid)
+                if a.shape[1] <= 64 or m == ops.NB_INDEX:   # brute-force DIST: width <= 64
+                    b = ops.radius_search(qt, off, lens, pd, off, lens, r, K, m)
+                    assert torch.equal(a, b), (name, K)
+                if len(P) <= 5000:
+                    assert np.array_equal(a.cpu().numpy(), og.radius_search(q, L, P, L, r, K, om))
+            c1, m1 = ops.radius_count(qt, off, lens, pd, off, r, grid=grid)
+            c2, m2 = ops.radius_count(qt, off, lens, pd, off, r)
+            assert torch.equal(c1, c2) and m1 == m2, name
+
+
+def test_grid_subsample_dense_matches_radix(gpu):
+    """The dense counting-sort path gives the radix-sort path's voxels bit for bit (order,
+    barycentres, keys), also after a key-space overflow retry (tiny max_cells)."""
+    import fgreg.ops as ops
+    for name, P, L, r in _grid_cases():
+        pd = torch.from_numpy(P).to(gpu)
+        lens, off = _lens_off(L, gpu)
+        for dl in (0.4 * r, 0.8 * r):
+            a = ops.grid_subsample(pd, off, lens, dl, return_keys=True)
+            b = ops.grid_subsample(pd, off, lens, dl, return_keys=True, max_cells=-1)
+            c = ops.grid_subsample(pd, off, lens, dl, return_keys=True, max_cells=16)
+            for x in (b, c):
+                assert x[1] == a[1] and torch.equal(x[0], a[0]) and torch.equal(x[2], a[2]), name
+            o_pts, o_lens, o_keys = og.grid_subsample(P, L, dl, return_keys=True)
+            assert a[1] == o_lens.tolist() and np.array_equal(a[0].cpu().numpy(), o_pts)
+            assert np.array_equal(a[2].cpu().numpy(), o_keys)

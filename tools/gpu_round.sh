@@ -7,7 +7,7 @@ set -o pipefail
 tag=${1:-run}
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-W=2; K=20          # profiled runs: forwards = W + K (tools/kernel_stats.py)
+W=2; K=20          # profiled runs: python tools/kernel_stats.py <kernel_trace.csv> $K <ms_per_step>
 if [ "$2" != "skip-tests" ]; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
       -p no:cacheprovider > gpurun_out/tests_$tag.log 2>&1 || { echo "TESTS FAILED $?"; tail -30 gpurun_out/tests_$tag.log; exit 1; }

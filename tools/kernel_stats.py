@@ -1,40 +1,58 @@
-"""Per-step kernel summary of a rocprofv3 --stats run of `bench.py --profile`.
+"""Per-step kernel summary of the TIMED steps of a `rocprofv3 --kernel-trace` run of
+`bench.py --profile`.
 
-usage: python tools/kernel_stats.py <kernel_stats.csv> <forwards> [<ms_per_step>] [top]
+usage: python tools/kernel_stats.py <kernel_trace.csv> <timed steps> [<ms_per_step>] [top]
 
-<forwards> = warmup + timed steps of the profiled run: every forward launches the same
-kernels, so a kernel's per-step time is its total / forwards. Kernels with fewer calls than
-forwards ran only once (weight splitting on the first forward) and are listed apart, not in
-the per-step sum. With <ms_per_step> (from the same run's JSON line) the script states the
-host / launch gap = ms_per_step - sum of per-step kernel time.
+bench.py --profile launches torch's spin kernel (torch.cuda._sleep) right before and right
+after its timed region; only the dispatches between the last two such markers are summed,
+so warmup forwards and one-time work (weight splitting) are excluded by construction and
+the per-step kernel sum is comparable with the same run's ms_per_step. Also reports the
+GPU-busy time (union of dispatch intervals) per step.
 """
 import csv
 import sys
+from collections import defaultdict
 
 
 def main():
     rows = list(csv.DictReader(open(sys.argv[1])))
-    fwd = float(sys.argv[2])
+    steps = float(sys.argv[2])
     step_ms = float(sys.argv[3]) if len(sys.argv) > 3 else None
     top = int(sys.argv[4]) if len(sys.argv) > 4 else 40
-    per, once = [], []
-    for r in rows:
-        (per if int(r['Calls']) >= fwd else once).append(r)
-    tot = sum(float(r['TotalDurationNs']) for r in per) / 1e6 / fwd
-    for r in sorted(per, key=lambda r: -float(r['TotalDurationNs']))[:top]:
-        ms = float(r['TotalDurationNs']) / 1e6 / fwd
-        print(f"{ms:8.3f} ms/step {100 * ms / tot:6.2f}% n/step={int(r['Calls']) / fwd:6.1f} "
-              f"avg={float(r['AverageNs']) / 1e3:8.1f}us  {r['Name'][:110]}")
-    print(f'sum of per-step kernel time: {tot:.3f} ms/step over {len(per)} kernels '
-          f'({fwd:.0f} forwards)')
+    rows.sort(key=lambda r: int(r['Start_Timestamp']))
+    marks = [i for i, r in enumerate(rows) if 'sleep' in r['Kernel_Name'].lower()
+             or 'spin' in r['Kernel_Name'].lower()]
+    assert len(marks) >= 2, 'no marker kernels in the trace'
+    a, b = marks[-2], marks[-1]
+    sel = rows[a + 1:b]
+    tot_ns, calls = defaultdict(float), defaultdict(int)
+    for r in sel:
+        d = int(r['End_Timestamp']) - int(r['Start_Timestamp'])
+        tot_ns[r['Kernel_Name']] += d
+        calls[r['Kernel_Name']] += 1
+    tot = sum(tot_ns.values()) / 1e6 / steps
+    busy, cur_s, cur_e = 0, None, None
+    for r in sel:
+        s, e = int(r['Start_Timestamp']), int(r['End_Timestamp'])
+        if cur_e is None or s > cur_e:
+            if cur_e is not None:
+                busy += cur_e - cur_s
+            cur_s, cur_e = s, e
+        else:
+            cur_e = max(cur_e, e)
+    if cur_e is not None:
+        busy += cur_e - cur_s
+    span = (int(rows[b]['Start_Timestamp']) - int(rows[a]['End_Timestamp'])) / 1e6 / steps
+    for name in sorted(tot_ns, key=lambda n: -tot_ns[n])[:top]:
+        ms = tot_ns[name] / 1e6 / steps
+        print(f"{ms:8.3f} ms/step {100 * ms / tot:6.2f}% n/step={calls[name] / steps:6.1f} "
+              f"avg={tot_ns[name] / calls[name] / 1e3:8.1f}us  {name[:110]}")
+    print(f'timed region: {len(sel)} dispatches over {steps:.0f} steps; sum of kernel time '
+          f'{tot:.3f} ms/step; GPU busy (union) {busy / 1e6 / steps:.3f} ms/step; '
+          f'marker-to-marker span {span:.3f} ms/step')
     if step_ms is not None:
         print(f'ms_per_step (same run, bench JSON): {step_ms:.3f} -> host/launch gap '
-              f'{step_ms - tot:.3f} ms/step ({100 * (step_ms - tot) / step_ms:.1f} %)')
-    if once:
-        print('one-time kernels (first forward only, not in the sum):')
-        for r in sorted(once, key=lambda r: -float(r['TotalDurationNs'])):
-            print(f"  {float(r['TotalDurationNs']) / 1e6:8.3f} ms total, {r['Calls']} calls  "
-                  f"{r['Name'][:100]}")
+              f'{step_ms - busy / 1e6 / steps:.3f} ms/step')
 
 
 if __name__ == '__main__':
