@@ -1,4 +1,4 @@
-// fp32-accurate attention (head_dim 32) on the fp16 matrix cores with scaled two-term splits
+// fp32-accurate attention (head_dim 32 or 64) on the fp16 matrix cores with scaled two-term splits
 // ("f16x3") -- the same contract as fgr_attention_bf16x6, at half its matrix-core work.
 //
 // Replaces the core of nn.MultiheadAttention in the reference's cross encoder
@@ -21,9 +21,10 @@
 //   O^T[dh][query] += V^T P^T   A = V (LDS, ds_read_b64_tr_b16), B = P (registers)
 // so every softmax row is lane-local; 16x16x32 f16 lane maps (lane l, g = l >> 4,
 // c = l & 15): A[i = c][k = 8g + e], B[k = 8g + e][j = c], C[i = 4g + r][j = c].
-// Per-(tile, head) image, 16 KB, staged into LDS by a flat copy:
-//   K: [term 2][g 4][key 64] x 16 B (8 dims)            ds_read_b128, conflict-free
-//   V: [term 2][key 64][32 dh] f16, 16-B chunk index XOR ((key >> 2) & 1) << 1
+// Per-(tile, head) image, 256 * DH B (16 KB at DH 32, 32 KB at DH 64), staged into LDS by a
+// flat copy:
+//   K: [k-step DH/32][term 2][g 4][key 64] x 16 B (8 dims)   ds_read_b128, conflict-free
+//   V: [term 2][key 64][DH] f16, 16-B chunk index XOR ((key >> 2) & 1) << 1
 // Tile t of kv segment s sits at tile index kv_off[s] / 64 + s + t; the (e_k, e_v) scale
 // exponents of all tiles follow the images.
 #include "common.h"
@@ -36,8 +37,9 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-constexpr int kUnits = 1024;             // 16-B units per (tile, head) image
-constexpr int kUnitV = 512;              // first V unit
+// 16-B units per (tile, head) image and the first V unit, by head dim
+template <int DH> constexpr int units() { return DH * 16 + (DH / 32) * 512; }
+template <int DH> constexpr int unit_v() { return (DH / 32) * 512; }
 constexpr float kPScale = 16384.f;       // 2^14
 
 __device__ __forceinline__ float xg_max16(float v) {   // max over lanes c, c^16, c^32, c^48
@@ -63,28 +65,31 @@ __device__ __forceinline__ void split2(float x, _Float16& h, _Float16& m) {
     m = (_Float16)(x - (float)h);
 }
 
+template <int DH>
 __global__ void __launch_bounds__(256)
 attn_kv_image16_kernel(const float* __restrict__ k, int64_t ld_k, const float* __restrict__ v,
                        int64_t ld_v, const int64_t* __restrict__ kv_off, int n_head,
                        uint4* __restrict__ img, int2* __restrict__ sc) {
+    constexpr int NF = DH / 16;                                  // float4s per thread
+    constexpr int RU = DH / 4;                                   // float4s per key row
     const int s = blockIdx.z, h = blockIdx.y, tt = blockIdx.x;
     const int64_t kb = kv_off[s];
     const int nk = (int)(kv_off[s + 1] - kb);
     if (tt * 64 >= nk) return;                                   // block-uniform
     __shared__ float red[2][4];
     const int64_t tile = (kb / 64 + s + tt) * n_head + h;
-    char* base = reinterpret_cast<char*>(img + tile * kUnits);
-    float kf[2][4], vf[2][4];
+    char* base = reinterpret_cast<char*>(img + tile * units<DH>());
+    float kf[NF][4], vf[NF][4];
     float km = 0.f, vm = 0.f;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int e = threadIdx.x + 256 * i;                     // float4 of the 64 x 32 tile
-        const int key = e >> 3, d0 = (e & 7) * 4;
+    for (int i = 0; i < NF; ++i) {
+        const int e = threadIdx.x + 256 * i;                     // float4 of the 64 x DH tile
+        const int key = e / RU, d0 = (e % RU) * 4;
         const bool ok = tt * 64 + key < nk;
         const int64_t row = kb + tt * 64 + key;
-        const float4 kx = ok ? *reinterpret_cast<const float4*>(k + row * ld_k + h * 32 + d0)
+        const float4 kx = ok ? *reinterpret_cast<const float4*>(k + row * ld_k + h * DH + d0)
                              : make_float4(0.f, 0.f, 0.f, 0.f);
-        const float4 vx = ok ? *reinterpret_cast<const float4*>(v + row * ld_v + h * 32 + d0)
+        const float4 vx = ok ? *reinterpret_cast<const float4*>(v + row * ld_v + h * DH + d0)
                              : make_float4(0.f, 0.f, 0.f, 0.f);
         kf[i][0] = kx.x; kf[i][1] = kx.y; kf[i][2] = kx.z; kf[i][3] = kx.w;
         vf[i][0] = vx.x; vf[i][1] = vx.y; vf[i][2] = vx.z; vf[i][3] = vx.w;
@@ -105,34 +110,39 @@ attn_kv_image16_kernel(const float* __restrict__ k, int64_t ld_k, const float* _
     if (threadIdx.x == 0) sc[tile] = make_int2(ek, ev);
     const float sk = __builtin_ldexpf(1.f, ek), sv = __builtin_ldexpf(1.f, ev);
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NF; ++i) {
         const int e = threadIdx.x + 256 * i;
-        const int key = e >> 3, d0 = (e & 7) * 4;
+        const int key = e / RU, d0 = (e % RU) * 4;
         _Float16 kt[2][4], vt[2][4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             split2(kf[i][j] * sk, kt[0][j], kt[1][j]);
             split2(vf[i][j] * sv, vt[0][j], vt[1][j]);
         }
-        const int g = d0 >> 3, half = (d0 >> 2) & 1;
+        const int ks = d0 >> 5, g = (d0 & 31) >> 3, half = (d0 >> 2) & 1;
         const int vch = (d0 >> 3) ^ (((key >> 2) & 1) << 1);
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
-            *reinterpret_cast<uint2*>(base + ((t * 4 + g) * 64 + key) * 16 + half * 8) =
+            *reinterpret_cast<uint2*>(base + (((ks * 2 + t) * 4 + g) * 64 + key) * 16 + half * 8) =
                 *reinterpret_cast<const uint2*>(kt[t]);
-            *reinterpret_cast<uint2*>(base + kUnitV * 16 + t * 4096 + key * 64 + vch * 16 + half * 8) =
+            *reinterpret_cast<uint2*>(base + unit_v<DH>() * 16 + t * (128 * DH) + key * (2 * DH) +
+                                      vch * 16 + half * 8) =
                 *reinterpret_cast<const uint2*>(vt[t]);
         }
     }
 }
 
+template <int DH>
 __global__ void __launch_bounds__(256, 4)
 attn_f16x3_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __restrict__ img,
                   const int2* __restrict__ sc, float* __restrict__ o, int64_t ld_o,
                   const int64_t* __restrict__ q_off, const int64_t* __restrict__ kv_off,
                   const int32_t* __restrict__ kv_seg, int n_head, int n_seg, int n_qblk,
                   float scale_log2) {
-    __shared__ u32x4 lds[kUnits];
+    constexpr int KD = DH / 32;                                  // k-steps of Q K^T
+    constexpr int TD = DH / 16;                                  // 16-row output tiles (dh)
+    constexpr int UN = units<DH>(), NS = UN / 256;
+    __shared__ u32x4 lds[UN];
     // XCD-aware block order: linear id L runs on XCD L % 8; all q-blocks of one
     // (segment, head) get ids of one residue mod 8, so one XCD's L2 serves its K/V image.
     const int L = blockIdx.x, xcd = L & 7, j0 = L >> 3;
@@ -147,40 +157,51 @@ attn_f16x3_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __rest
     const int nk = (int)(kv_off[ks + 1] - kb);
     const int ntile = (nk + 63) / 64;
     const int64_t tile0 = (kb / 64 + ks) * n_head + head;
-    const u32x4* tiles = reinterpret_cast<const u32x4*>(img) + tile0 * kUnits;
-    const int64_t tile_stride = (int64_t)n_head * kUnits;
+    const u32x4* tiles = reinterpret_cast<const u32x4*>(img) + tile0 * UN;
+    const int64_t tile_stride = (int64_t)n_head * UN;
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
     const int g = lane >> 4, c = lane & 15;
 
-    // Q^T operand (B): lane (g, c) holds q[query c][8g .. 8g+7] * scale * log2(e), scaled
-    // per query into fp16 range and split
+    // Q^T operand (B): lane (g, c) holds q[query c][32 kd + 8g .. +7] * scale * log2(e),
+    // scaled per query into fp16 range and split
     const int64_t qrow = q0 + wv * 16 + c;
-    float x[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (qrow < qe) {
-        const float4* p = reinterpret_cast<const float4*>(q + qrow * ld_q + head * 32 + 8 * g);
-        const float4 a = p[0], b = p[1];
-        x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
-        x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+    float x[KD][8];
+#pragma unroll
+    for (int kd = 0; kd < KD; ++kd) {
+        float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+        if (qrow < qe) {
+            const float4* p = reinterpret_cast<const float4*>(q + qrow * ld_q + head * DH + 32 * kd + 8 * g);
+            a = p[0];
+            b = p[1];
+        }
+        x[kd][0] = a.x; x[kd][1] = a.y; x[kd][2] = a.z; x[kd][3] = a.w;
+        x[kd][4] = b.x; x[kd][5] = b.y; x[kd][6] = b.z; x[kd][7] = b.w;
     }
     float qm = 0.f;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        x[e] *= scale_log2;
-        qm = fmaxf(qm, fabsf(x[e]));
-    }
+    for (int kd = 0; kd < KD; ++kd)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            x[kd][e] *= scale_log2;
+            qm = fmaxf(qm, fabsf(x[kd][e]));
+        }
     const int eq = range_exp(xg_max16(qm));
     const float sq = __builtin_ldexpf(1.f, eq);
-    f16x8 qt[2];
+    f16x8 qt[KD][2];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        _Float16 h, m;
-        split2(x[e] * sq, h, m);
-        qt[0][e] = h; qt[1][e] = m;
-    }
-    f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    for (int kd = 0; kd < KD; ++kd)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            _Float16 h, m;
+            split2(x[kd][e] * sq, h, m);
+            qt[kd][0][e] = h; qt[kd][1][e] = m;
+        }
+    f32x4 acc[TD];
+#pragma unroll
+    for (int t = 0; t < TD; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
     float m_run = -INFINITY, l_run = 0.f;
 
-    u32x4 stage[4];
+    u32x4 stage[NS];
     const char* lbase = reinterpret_cast<const char*>(lds);
     // transposed-read addresses of V: lane c = 4qq + p reads row 4g + qq (+16, +32j),
     // columns 16t + 4p .. +3 (chunk 2t + (p >> 1), swizzled by row bit 2)
@@ -188,30 +209,33 @@ attn_f16x3_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __rest
 
     if (ntile > 0) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) stage[i] = tiles[tid + 256 * i];
+        for (int i = 0; i < NS; ++i) stage[i] = tiles[tid + 256 * i];
     }
     for (int tt = 0; tt < ntile; ++tt) {
         const int2 e2 = sc[tile0 + tt * n_head];
         __syncthreads();
 #pragma unroll
-        for (int i = 0; i < 4; ++i) lds[tid + 256 * i] = stage[i];
+        for (int i = 0; i < NS; ++i) lds[tid + 256 * i] = stage[i];
         __syncthreads();
         if (tt + 1 < ntile) {
             const u32x4* src = tiles + (tt + 1) * tile_stride;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) stage[i] = src[tid + 256 * i];
+            for (int i = 0; i < NS; ++i) stage[i] = src[tid + 256 * i];
         }
         const int valid = nk - tt * 64;
 
         f32x4 s[4];
 #pragma unroll
         for (int n = 0; n < 4; ++n) {
-            const f16x8 kh = __builtin_bit_cast(f16x8, lds[(0 * 4 + g) * 64 + 16 * n + c]);
-            const f16x8 kl = __builtin_bit_cast(f16x8, lds[(1 * 4 + g) * 64 + 16 * n + c]);
             f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f};
-            a = __builtin_amdgcn_mfma_f32_16x16x32_f16(kl, qt[0], a, 0, 0, 0);
-            a = __builtin_amdgcn_mfma_f32_16x16x32_f16(kh, qt[1], a, 0, 0, 0);
-            a = __builtin_amdgcn_mfma_f32_16x16x32_f16(kh, qt[0], a, 0, 0, 0);
+#pragma unroll
+            for (int kd = 0; kd < KD; ++kd) {
+                const f16x8 kh = __builtin_bit_cast(f16x8, lds[((kd * 2 + 0) * 4 + g) * 64 + 16 * n + c]);
+                const f16x8 kl = __builtin_bit_cast(f16x8, lds[((kd * 2 + 1) * 4 + g) * 64 + 16 * n + c]);
+                a = __builtin_amdgcn_mfma_f32_16x16x32_f16(kl, qt[kd][0], a, 0, 0, 0);
+                a = __builtin_amdgcn_mfma_f32_16x16x32_f16(kh, qt[kd][1], a, 0, 0, 0);
+                a = __builtin_amdgcn_mfma_f32_16x16x32_f16(kh, qt[kd][0], a, 0, 0, 0);
+            }
             s[n] = a;
         }
         // s (scaled units) * f = log2-domain score; f > 0 so max commutes with it
@@ -243,7 +267,9 @@ attn_f16x3_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __rest
             }
         l_run = l_run * alpha + rs;
 
-        f32x4 tmp[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+        f32x4 tmp[TD];
+#pragma unroll
+        for (int t = 0; t < TD; ++t) tmp[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             // P^T operand of step j (keys 32j + 4g + {0..3}, 32j + 16 + 4g + {0..3})
@@ -255,16 +281,16 @@ attn_f16x3_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __rest
                 pt[0][e] = h; pt[1][e] = m;
             }
 #pragma unroll
-            for (int t = 0; t < 2; ++t) {
+            for (int t = 0; t < TD; ++t) {
                 f16x8 vf[2];
                 const int r0 = 32 * j + 4 * g + qq, r1 = r0 + 16;
                 const int ch = 2 * t + (pp >> 1);
-                const int off0 = r0 * 64 + ((ch ^ (((r0 >> 2) & 1) << 1)) * 16) + (pp & 1) * 8;
-                const int off1 = r1 * 64 + ((ch ^ (((r1 >> 2) & 1) << 1)) * 16) + (pp & 1) * 8;
+                const int off0 = r0 * (2 * DH) + ((ch ^ (((r0 >> 2) & 1) << 1)) * 16) + (pp & 1) * 8;
+                const int off1 = r1 * (2 * DH) + ((ch ^ (((r1 >> 2) & 1) << 1)) * 16) + (pp & 1) * 8;
 #pragma unroll
                 for (int tm = 0; tm < 2; ++tm) {
                     typedef __attribute__((address_space(3))) s16x4 lds_s4;
-                    const char* vb = lbase + kUnitV * 16 + tm * 4096;
+                    const char* vb = lbase + unit_v<DH>() * 16 + tm * (128 * DH);
                     const s16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
                         (lds_s4*)(uintptr_t)(uint32_t)(uintptr_t)(vb + off0));
                     const s16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
@@ -281,7 +307,7 @@ attn_f16x3_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __rest
         }
         const float fv = __builtin_ldexpf(1.f, -(e2.y + 14));
 #pragma unroll
-        for (int t = 0; t < 2; ++t)
+        for (int t = 0; t < TD; ++t)
 #pragma unroll
             for (int r = 0; r < 4; ++r) acc[t][r] = __builtin_fmaf(tmp[t][r], fv, acc[t][r] * alpha);
     }
@@ -289,11 +315,11 @@ attn_f16x3_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __rest
     const float inv = 1.0f / xg_sum16(l_run);
     if (qrow < qe) {
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
+        for (int t = 0; t < TD; ++t) {
             float4 y;
             y.x = acc[t][0] * inv; y.y = acc[t][1] * inv;
             y.z = acc[t][2] * inv; y.w = acc[t][3] * inv;
-            *reinterpret_cast<float4*>(o + qrow * ld_o + head * 32 + 16 * t + 4 * g) = y;
+            *reinterpret_cast<float4*>(o + qrow * ld_o + head * DH + 16 * t + 4 * g) = y;
         }
     }
 }
@@ -309,8 +335,9 @@ extern "C" int fgr_attention_f16x3_workspace(int64_t n_kv_rows, int32_t n_kv_seg
                                              int32_t n_head, size_t* bytes) {
     FGR_REQUIRE(bytes && n_kv_rows >= 0 && n_kv_seg >= 0 && n_head > 0,
                 "fgr_attention_f16x3_workspace: bad arguments");
+    // sized for the largest supported head dim (64)
     const int64_t nt = n_tiles16(n_kv_rows, n_kv_seg) * n_head;
-    *bytes = (size_t)(nt * kUnits * 16 + nt * 8);
+    *bytes = (size_t)(nt * units<64>() * 16 + nt * 8);
     return FGR_OK;
 }
 
@@ -324,33 +351,45 @@ extern "C" int fgr_attention_f16x3(const float* q, int64_t ld_q, const float* k,
     FGR_REQUIRE(q && k && v && o && q_off && kv_off && kv_seg && workspace && n_seg > 0 &&
                     n_kv_seg > 0 && n_head > 0 && max_q_len >= 0 && max_kv_len >= 0,
                 "fgr_attention_f16x3: bad arguments");
-    FGR_REQUIRE(head_dim == 32, "fgr_attention_f16x3: head_dim %d (only 32)", head_dim);
-    FGR_REQUIRE(ld_q >= n_head * 32 && ld_k >= n_head * 32 && ld_v >= n_head * 32 &&
-                    ld_o >= n_head * 32 && ld_q % 4 == 0 && ld_k % 4 == 0 && ld_v % 4 == 0 &&
+    FGR_REQUIRE(head_dim == 32 || head_dim == 64, "fgr_attention_f16x3: head_dim %d (32 or 64)",
+                head_dim);
+    const int dh = head_dim;
+    FGR_REQUIRE(ld_q >= n_head * dh && ld_k >= n_head * dh && ld_v >= n_head * dh &&
+                    ld_o >= n_head * dh && ld_q % 4 == 0 && ld_k % 4 == 0 && ld_v % 4 == 0 &&
                     ld_o % 4 == 0,
-                "fgr_attention_f16x3: row strides must be >= n_head*32 and multiples of 4");
+                "fgr_attention_f16x3: row strides must be >= n_head*head_dim and multiples of 4");
     FGR_REQUIRE(((reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(k) |
                   reinterpret_cast<uintptr_t>(v) | reinterpret_cast<uintptr_t>(o) |
                   reinterpret_cast<uintptr_t>(workspace)) & 15) == 0,
                 "fgr_attention_f16x3: q/k/v/o/workspace must be 16-B aligned");
     const int64_t nt = n_tiles16(n_kv_rows, n_kv_seg) * n_head;
-    const int64_t need = nt * kUnits * 16 + nt * 8;
+    const int un = dh == 32 ? units<32>() : units<64>();
+    const int64_t need = nt * un * 16 + nt * 8;
     FGR_REQUIRE(ws_bytes >= need, "fgr_attention_f16x3: workspace %lld < %lld bytes",
                 (long long)ws_bytes, (long long)need);
     if (max_q_len == 0 || max_kv_len == 0) return FGR_OK;
     hipStream_t st = as_stream(stream);
     TimedCall timed_(st);
     uint4* img = static_cast<uint4*>(workspace);
-    int2* sc = reinterpret_cast<int2*>(static_cast<char*>(workspace) + nt * kUnits * 16);
-    hipLaunchKernelGGL(attn_kv_image16_kernel,
-                       dim3((unsigned)ceil_div(max_kv_len, 64), (unsigned)n_head, (unsigned)n_kv_seg),
-                       dim3(256), 0, st, k, ld_k, v, ld_v, kv_off, n_head, img, sc);
+    int2* sc = reinterpret_cast<int2*>(static_cast<char*>(workspace) + nt * un * 16);
+    const dim3 kgrid((unsigned)ceil_div(max_kv_len, 64), (unsigned)n_head, (unsigned)n_kv_seg);
+    if (dh == 32)
+        hipLaunchKernelGGL(attn_kv_image16_kernel<32>, kgrid, dim3(256), 0, st, k, ld_k, v, ld_v,
+                           kv_off, n_head, img, sc);
+    else
+        hipLaunchKernelGGL(attn_kv_image16_kernel<64>, kgrid, dim3(256), 0, st, k, ld_k, v, ld_v,
+                           kv_off, n_head, img, sc);
     FGR_CHECK_LAUNCH("attn_kv_image16_kernel");
     const int n_qblk = (int)ceil_div(max_q_len, 64);
     const int64_t n_blocks = ceil_div((int64_t)n_seg * n_head, 8) * 8 * n_qblk;
-    hipLaunchKernelGGL(attn_f16x3_kernel, dim3((unsigned)n_blocks), dim3(256), 0, st, q, ld_q,
-                       (const uint4*)img, (const int2*)sc, o, ld_o, q_off, kv_off, kv_seg, n_head,
-                       n_seg, n_qblk, scale * 1.4426950408889634f);
+    if (dh == 32)
+        hipLaunchKernelGGL(attn_f16x3_kernel<32>, dim3((unsigned)n_blocks), dim3(256), 0, st, q,
+                           ld_q, (const uint4*)img, (const int2*)sc, o, ld_o, q_off, kv_off, kv_seg,
+                           n_head, n_seg, n_qblk, scale * 1.4426950408889634f);
+    else
+        hipLaunchKernelGGL(attn_f16x3_kernel<64>, dim3((unsigned)n_blocks), dim3(256), 0, st, q,
+                           ld_q, (const uint4*)img, (const int2*)sc, o, ld_o, q_off, kv_off, kv_seg,
+                           n_head, n_seg, n_qblk, scale * 1.4426950408889634f);
     FGR_CHECK_LAUNCH("attn_f16x3_kernel");
     return FGR_OK;
 }

@@ -200,6 +200,131 @@ __global__ void __launch_bounds__(64 * kInW) instnorm_seg16_kernel(InArgs a) {
     }
 }
 
+// Segmented instance norm for long segments (> kSegRows rows, e.g. 3DMatch's 20k-row clouds),
+// three launches that keep every CU busy (the register-resident chunk kernel above runs
+// only C/64 x n_seg x rows/768 blocks -- ~100 at 2 x 20k x 64):
+//   1. stats: one 256-thread block per (segment, chunk of kLsIter x kLsRpi rows), 16-B loads
+//      (TPR = C/4 threads per row), shifted sums S = sum(v - K), Q = sum((v - K)^2) with the
+//      segment's first row as the pivot K (no cancellation when |mean| >> std);
+//   2. merge: per (segment, channel) the chunk partials in fp64 -> mean, rstd;
+//   3. apply: the same chunks, (v - mean) * rstd -> act (-> + residual -> post_act), 16-B stores.
+// v = x / row_div (when given) is recomputed identically in passes 1 and 3.
+constexpr int kLsIter = 4;                 // row iterations per block (16 KB of x per block)
+
+struct LsArgs {
+    const float* x;
+    int c, tpr, rpi, rows;                 // channels, threads per row (c/4), rows per iteration, rows per chunk
+    const int64_t* seg_off;
+    int n_chunks;
+    const float* row_div;
+    float eps;
+    int act;
+    const float* residual;
+    int post_act;
+    float* out;
+    float* part;                           // [n_seg][n_chunks][2][c] (S, Q)
+    float* stats;                          // [n_seg][2][c] (mean, rstd)
+};
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+__global__ void __launch_bounds__(256) instnorm_ls_stats_kernel(LsArgs a) {
+    __shared__ float4 red[2][256];
+    const int seg = blockIdx.y, chunk = blockIdx.x;
+    const int64_t b = a.seg_off[seg], e = a.seg_off[seg + 1];
+    const int64_t r0 = b + (int64_t)chunk * a.rows;
+    if (r0 >= e) return;                                   // block-uniform
+    const int64_t r1 = min(e, r0 + a.rows);
+    const int t = threadIdx.x, cg = t % a.tpr, rr = t / a.tpr;
+    const int col = 4 * cg;
+    float4 k = ld4(a.x + b * a.c + col);                   // pivot: the segment's first row
+    if (a.row_div) {
+        const float d = a.row_div[b];
+        k.x = k.x / d; k.y = k.y / d; k.z = k.z / d; k.w = k.w / d;
+    }
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f), q = s;
+    for (int64_t r = r0 + rr; r < r1; r += a.rpi) {
+        float4 v = ld4(a.x + r * a.c + col);
+        if (a.row_div) {
+            const float d = a.row_div[r];
+            v.x = v.x / d; v.y = v.y / d; v.z = v.z / d; v.w = v.w / d;
+        }
+        const float dx = v.x - k.x, dy = v.y - k.y, dz = v.z - k.z, dw = v.w - k.w;
+        s.x += dx; s.y += dy; s.z += dz; s.w += dw;
+        q.x += dx * dx; q.y += dy * dy; q.z += dz * dz; q.w += dw * dw;
+    }
+    red[0][t] = s;
+    red[1][t] = q;
+    __syncthreads();
+    if (rr != 0) return;
+    for (int j = 1; j < a.rpi; ++j) {
+        const float4 s2 = red[0][t + j * a.tpr], q2 = red[1][t + j * a.tpr];
+        s.x += s2.x; s.y += s2.y; s.z += s2.z; s.w += s2.w;
+        q.x += q2.x; q.y += q2.y; q.z += q2.z; q.w += q2.w;
+    }
+    float* pp = a.part + ((int64_t)seg * a.n_chunks + chunk) * 2 * a.c;
+    *reinterpret_cast<float4*>(pp + col) = s;
+    *reinterpret_cast<float4*>(pp + a.c + col) = q;
+}
+
+__global__ void __launch_bounds__(256) instnorm_ls_merge_kernel(LsArgs a) {
+    const int seg = blockIdx.y;
+    const int ch = blockIdx.x * 256 + threadIdx.x;
+    if (ch >= a.c) return;
+    const int64_t b = a.seg_off[seg], e = a.seg_off[seg + 1];
+    if (e <= b) return;
+    const int nch = (int)((e - b + a.rows - 1) / a.rows);
+    double S = 0.0, Q = 0.0;
+    const float* pp = a.part + (int64_t)seg * a.n_chunks * 2 * a.c + ch;
+    for (int k = 0; k < nch; ++k) {
+        S += (double)pp[(int64_t)k * 2 * a.c];
+        Q += (double)pp[(int64_t)k * 2 * a.c + a.c];
+    }
+    float kv = a.x[b * a.c + ch];
+    if (a.row_div) kv = kv / a.row_div[b];
+    const double n = (double)(e - b);
+    const double m = S / n;
+    const double var = fmax(Q / n - m * m, 0.0);          // biased, of the shifted values
+    a.stats[((int64_t)seg * 2) * a.c + ch] = (float)((double)kv + m);
+    a.stats[((int64_t)seg * 2 + 1) * a.c + ch] = 1.0f / sqrtf((float)var + a.eps);
+}
+
+__global__ void __launch_bounds__(256) instnorm_ls_apply_kernel(LsArgs a) {
+    const int seg = blockIdx.y, chunk = blockIdx.x;
+    const int64_t b = a.seg_off[seg], e = a.seg_off[seg + 1];
+    const int64_t r0 = b + (int64_t)chunk * a.rows;
+    if (r0 >= e) return;
+    const int64_t r1 = min(e, r0 + a.rows);
+    const int t = threadIdx.x, cg = t % a.tpr, rr = t / a.tpr;
+    const int col = 4 * cg;
+    const float4 mean = ld4(a.stats + ((int64_t)seg * 2) * a.c + col);
+    const float4 rstd = ld4(a.stats + ((int64_t)seg * 2 + 1) * a.c + col);
+    for (int64_t r = r0 + rr; r < r1; r += a.rpi) {
+        float4 v = ld4(a.x + r * a.c + col);
+        if (a.row_div) {
+            const float d = a.row_div[r];
+            v.x = v.x / d; v.y = v.y / d; v.z = v.z / d; v.w = v.w / d;
+        }
+        float4 y;
+        y.x = act_fn((v.x - mean.x) * rstd.x, a.act);
+        y.y = act_fn((v.y - mean.y) * rstd.y, a.act);
+        y.z = act_fn((v.z - mean.z) * rstd.z, a.act);
+        y.w = act_fn((v.w - mean.w) * rstd.w, a.act);
+        if (a.residual) {
+            const float4 rv = ld4(a.residual + r * a.c + col);
+            y.x = act_fn(y.x + rv.x, a.post_act);
+            y.y = act_fn(y.y + rv.y, a.post_act);
+            y.z = act_fn(y.z + rv.z, a.post_act);
+            y.w = act_fn(y.w + rv.w, a.post_act);
+        }
+        *reinterpret_cast<float4*>(a.out + r * a.c + col) = y;
+    }
+}
+
+// the long-segment path applies when C/4 threads per row tile a 256-thread block
+inline bool ls_ok(int c) { return c % 4 == 0 && c / 4 <= 256 && 256 % (c / 4) == 0; }
+inline int ls_rows(int c) { return (256 / (c / 4)) * kLsIter; }
+
 // LayerNorm, 16 lanes per row (4 rows per wave, 16 per block), d % 64 == 0 and
 // d <= 64 * V: each lane holds V/4 float4 (16-B loads / stores), row reductions on DPP
 // within a 16-lane row (no LDS). `pre_bias` as in layernorm_kernel below.
@@ -346,6 +471,11 @@ using namespace fgr;
 extern "C" int fgr_instnorm_workspace(int64_t max_seg_len, int32_t c, int32_t n_seg,
                                       size_t* bytes) {
     FGR_REQUIRE(bytes && max_seg_len >= 0 && c > 0 && n_seg > 0, "fgr_instnorm_workspace: bad arguments");
+    if (max_seg_len > kSegRows && ls_ok(c)) {
+        const int64_t chunks = ceil_div(max_seg_len, ls_rows(c));
+        *bytes = (size_t)n_seg * (chunks + 1) * 2 * c * sizeof(float);
+        return FGR_OK;
+    }
     const int64_t chunks = ceil_div(max_seg_len, kChunk);
     *bytes = chunks > 1 ? (size_t)n_seg * chunks * 3 * c * sizeof(float) : 0;
     return FGR_OK;
@@ -367,6 +497,25 @@ extern "C" int fgr_instnorm(const float* x, int64_t n, int32_t c, const int64_t*
     if (max_seg_len <= kSegRows) {
         hipLaunchKernelGGL(instnorm_seg16_kernel, dim3((unsigned)ceil_div(c, 16), n_seg, 1),
                            dim3(64 * kInW), 0, st, a);
+    } else if (ls_ok(c)) {
+        const int rows = ls_rows(c);
+        const int64_t lc = ceil_div(max_seg_len, rows);
+        const size_t need = (size_t)n_seg * (lc + 1) * 2 * c * sizeof(float);
+        FGR_REQUIRE(ws && ws_bytes >= need &&
+                        ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(out) |
+                          reinterpret_cast<uintptr_t>(residual) |
+                          reinterpret_cast<uintptr_t>(ws)) & 15) == 0,
+                    "fgr_instnorm: workspace %zu < %zu bytes or operands not 16-B aligned",
+                    ws_bytes, need);
+        float* part = (float*)ws;
+        LsArgs la{x, c, c / 4, 256 / (c / 4), rows, seg_off, (int)lc, row_div, eps, act,
+                  residual, post_act, out, part, part + (size_t)n_seg * lc * 2 * c};
+        hipLaunchKernelGGL(instnorm_ls_stats_kernel, dim3((unsigned)lc, n_seg), dim3(256), 0, st, la);
+        FGR_CHECK_LAUNCH("instnorm_ls_stats_kernel");
+        hipLaunchKernelGGL(instnorm_ls_merge_kernel, dim3((unsigned)ceil_div(c, 256), n_seg), dim3(256),
+                           0, st, la);
+        FGR_CHECK_LAUNCH("instnorm_ls_merge_kernel");
+        hipLaunchKernelGGL(instnorm_ls_apply_kernel, dim3((unsigned)lc, n_seg), dim3(256), 0, st, la);
     } else if (chunks == 1) {
         hipLaunchKernelGGL(instnorm_chunk_kernel<0>, dim3(cx, n_seg, 1), dim3(64 * kInW), 0, st, a);
     } else {

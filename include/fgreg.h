@@ -271,7 +271,8 @@ int fgr_attention_bf16x6(const float* q, int64_t ld_q, const float* k, int64_t l
                          int32_t max_kv_len, int32_t n_head, int32_t head_dim, float scale,
                          void* workspace, int64_t ws_bytes, void* stream);
 
-/* fp32-accurate attention on the fp16 matrix cores (head_dim 32), same semantics and
+/* fp32-accurate attention on the fp16 matrix cores (head_dim 32 -- ModelNet's d 256 / 8 heads --
+ * or 64 -- 3DMatch's d 512 / 8 heads), same semantics and
  * arguments as fgr_attention_bf16x6: K/V are scaled per (64-key tile, head), Q per query and
  * P by 2^14 into fp16's normal range (exact powers of two), split into two fp16 terms and
  * the three significant term products accumulate in fp32 (<= ~3 * 2^-22 per product) at half

@@ -78,12 +78,18 @@ def test_instnorm_vs_reference(gpu):
     assert rel_err(out, g['out']) < TOL
 
 
-@pytest.mark.parametrize('lens', [[700, 1, 33, 512], [1024, 1000, 2], [3000, 5, 1500, 1024, 1025]])
-def test_instnorm_fusions_vs_torch(gpu, lens):
-    """Register path (segments <= 1024 rows) and the two-launch chunked path."""
+@pytest.mark.parametrize('lens,c,mu', [([700, 1, 33, 512], 72, 2.0), ([1024, 1000, 2], 72, 2.0),
+                                       ([3000, 5, 1500, 1024, 1025], 72, 2.0),
+                                       ([3000, 5, 1500, 1024, 1025], 64, 2.0),
+                                       ([20000, 13389], 64, 50.0), ([5483, 1, 2000], 256, 2.0),
+                                       ([1100, 4000], 1024, -30.0)])
+def test_instnorm_fusions_vs_torch(gpu, lens, c, mu):
+    """Register path (segments <= 1024 rows), the two-launch chunked path (C % 4 != 0) and
+    the three-launch long-segment path (C / 4 divides 256), including 3DMatch-size clouds
+    with |mean| >> std (the shifted sums must not cancel)."""
     import fgreg.ops as ops
     rng = np.random.default_rng(5)
-    x = torch.from_numpy(rng.normal(2, 3, (sum(lens), 72)).astype(np.float32))
+    x = torch.from_numpy(rng.normal(mu, 3 if abs(mu) < 10 else 0.5, (sum(lens), c)).astype(np.float32))
     div = torch.from_numpy(rng.integers(1, 9, sum(lens)).astype(np.float32))
     res = torch.from_numpy(rng.normal(size=x.shape).astype(np.float32))
     ref = mo.instance_norm(x / div[:, None], torch.tensor(lens))
@@ -162,17 +168,17 @@ def test_attention_vs_torch(gpu, nhead, d):
         assert rel_err(out, ref) < TOL
 
 
-@pytest.mark.parametrize('split', ['bf16x6', 'f16x3'])
+@pytest.mark.parametrize('split,d', [('bf16x6', 256), ('f16x3', 256), ('f16x3', 512)])
 @pytest.mark.parametrize('scale', [1.0, 6.0, 1e-6, 3e3])
-def test_attention_split_is_fp32_accurate(gpu, scale, split):
-    """The split attentions (fgr_attention_bf16x6 / _f16x3, dh = 32) against a float64
+def test_attention_split_is_fp32_accurate(gpu, scale, split, d):
+    """The split attentions (fgr_attention_bf16x6 dh = 32; _f16x3 dh = 32 and 64) against a float64
     reference: error at fp32 level (<= 1e-5 normwise) and no worse than a few times the
     fp32-MFMA kernel's own error; separate key segmentation (kv lengths != q lengths,
     max_kv_len > max_q_len), partial and 1-key tiles, sharp softmax at scale 6, inputs far
     outside fp16's range (1e-6: subnormal in fp16 unscaled; 3e3: products past 65504)."""
     import fgreg.ops as ops
     rng = np.random.default_rng(7)
-    d, nhead = 256, 8
+    nhead = 8
     qlens = [300, 1, 64, 129]
     klens = [65, 700, 1, 128]
     kv_seg = [1, 0, 3, 2]
