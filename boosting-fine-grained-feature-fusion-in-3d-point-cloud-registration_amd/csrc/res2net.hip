@@ -253,10 +253,12 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 template <int KT>
 __global__ void __launch_bounds__(64 * KT)
-res2net_chain_h3_kernel(const float* __restrict__ h, int64_t n, int scale, int nums,
+res2net_chain_h3_kernel(const float* __restrict__ h, int64_t n, int w, int scale, int nums,
                         const u32x4* __restrict__ wf, const float* __restrict__ wsc,
                         const float* __restrict__ bias, const float* __restrict__ x, int cin,
                         float* __restrict__ cat, int64_t ld) {
+    // W = the width padded to whole 16-column tiles (one wave each); w <= W the real width
+    // (w % 4 == 0): columns past w carry zero weights and are never stored
     constexpr int W = 16 * KT, KS = (W + 31) / 32, NU = kRows * KS * 4;   // A units per term
     constexpr int IT = (NU + 64 * KT - 1) / (64 * KT);                    // build units / thread
     __shared__ u32x4 img[2 * NU];
@@ -265,8 +267,9 @@ res2net_chain_h3_kernel(const float* __restrict__ h, int64_t n, int scale, int n
     const int tid = threadIdx.x, nth = 64 * KT;
     const int wv = tid / 64, lane = tid % 64, g = lane >> 4, c = lane & 15;
     const int64_t r0 = (int64_t)blockIdx.x * kRows;
-    const int64_t hw = (int64_t)scale * W;
+    const int64_t hw = (int64_t)scale * w;
     const int col0 = wv * 16 + 4 * g;                  // this lane's 4 output columns
+    const bool col_ok = col0 < w;
 
     for (int i = 0; i < nums; ++i) {
         const u32x4* wb = wf + (((int64_t)i * KT + wv) * KS) * 128 + lane;
@@ -277,8 +280,9 @@ res2net_chain_h3_kernel(const float* __restrict__ h, int64_t n, int scale, int n
 #pragma unroll
                 for (int t = 0; t < 2; ++t) bq[q][t] = wb[(q * 2 + t) * 64];
             }
-        const float4 wsv = *reinterpret_cast<const float4*>(wsc + i * W + col0);
-        const float4 bc = *reinterpret_cast<const float4*>(bias + i * W + col0);
+        const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 wsv = col_ok ? *reinterpret_cast<const float4*>(wsc + i * w + col0) : z4;
+        const float4 bc = col_ok ? *reinterpret_cast<const float4*>(bias + i * w + col0) : z4;
         if (tid < kRows) rmax[tid] = 0;
         __syncthreads();
         // a = sp_{i-1} + h_i: unit u -> (row = u % 32, kg = u / 32), 8 k each
@@ -292,13 +296,13 @@ res2net_chain_h3_kernel(const float* __restrict__ h, int64_t n, int scale, int n
 #pragma unroll
             for (int e = 0; e < 8; e += 4) {
                 float4 hv = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (u < NU && gr < n && k0 + e < W)
-                    hv = *reinterpret_cast<const float4*>(h + gr * hw + (int64_t)i * W + k0 + e);
+                if (u < NU && gr < n && k0 + e < w)
+                    hv = *reinterpret_cast<const float4*>(h + gr * hw + (int64_t)i * w + k0 + e);
                 a[it][e] = hv.x; a[it][e + 1] = hv.y; a[it][e + 2] = hv.z; a[it][e + 3] = hv.w;
             }
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
-                if (i > 0 && u < NU && k0 + e < W) a[it][e] += sp[row * W + k0 + e];
+                if (i > 0 && u < NU && k0 + e < w) a[it][e] += sp[row * W + k0 + e];
                 cm = fmaxf(cm, fabsf(a[it][e]));
             }
             if (u < NU && cm > 0.f) atomicMax(&rmax[row], __float_as_int(cm));
@@ -356,17 +360,17 @@ res2net_chain_h3_kernel(const float* __restrict__ h, int64_t n, int scale, int n
             y.y = fmaxf(av[1] * rs * wsv.y + bc.y, 0.f);
             y.z = fmaxf(av[2] * rs * wsv.z + bc.z, 0.f);
             y.w = fmaxf(av[3] * rs * wsv.w + bc.w, 0.f);
-            if (r0 + row < n)
-                *reinterpret_cast<float4*>(cat + (r0 + row) * ld + (int64_t)i * W + col0) = y;
+            if (r0 + row < n && col_ok)
+                *reinterpret_cast<float4*>(cat + (r0 + row) * ld + (int64_t)i * w + col0) = y;
             *reinterpret_cast<float4*>(sp + row * W + col0) = y;
         }
         __syncthreads();
     }
-    const int rest = (scale - nums) * W;
+    const int rest = (scale - nums) * w;
     for (int e = tid; e < kRows * rest; e += nth) {
         const int row = e / rest, cc = e - row * rest;
         if (r0 + row < n)
-            cat[(r0 + row) * ld + (int64_t)nums * W + cc] = h[(r0 + row) * hw + (int64_t)nums * W + cc];
+            cat[(r0 + row) * ld + (int64_t)nums * w + cc] = h[(r0 + row) * hw + (int64_t)nums * w + cc];
     }
     if (x) {
         for (int e = tid; e < kRows * cin; e += nth) {
@@ -385,8 +389,9 @@ extern "C" int fgr_res2net_chain_h3(const float* h, int64_t n, int32_t w, int32_
                                     const void* w_img, const float* w_scale, const float* bias,
                                     const float* x, int32_t cin, float* cat, int64_t ld_cat,
                                     void* stream) {
-    FGR_REQUIRE(n >= 0 && scale >= 2 && (w == 112 || w == 224) && cin >= 0,
-                "fgr_res2net_chain_h3: unsupported width %d / scale %d (needs 112 or 224)", w, scale);
+    FGR_REQUIRE(n >= 0 && scale >= 2 && w > 0 && w <= 224 && w % 4 == 0 && cin >= 0,
+                "fgr_res2net_chain_h3: unsupported width %d / scale %d (w %% 4 == 0, <= 224)", w,
+                scale);
     FGR_REQUIRE(ld_cat >= (int64_t)scale * w + (x ? cin : 0) && ld_cat % 4 == 0,
                 "fgr_res2net_chain_h3: ld_cat too small or not a multiple of 4");
     FGR_REQUIRE(n == 0 || (h && w_img && w_scale && bias && cat), "fgr_res2net_chain_h3: null pointer");
@@ -397,12 +402,23 @@ extern "C" int fgr_res2net_chain_h3(const float* h, int64_t n, int32_t w, int32_
     if (n == 0) return FGR_OK;
     const dim3 grid((unsigned)ceil_div(n, kRows));
     hipStream_t st = as_stream(stream);
-    if (w == 112)
-        hipLaunchKernelGGL(res2net_chain_h3_kernel<7>, grid, dim3(64 * 7), 0, st, h, n, scale,
-                           scale - 1, (const u32x4*)w_img, w_scale, bias, x, cin, cat, ld_cat);
-    else
-        hipLaunchKernelGGL(res2net_chain_h3_kernel<14>, grid, dim3(64 * 14), 0, st, h, n, scale,
-                           scale - 1, (const u32x4*)w_img, w_scale, bias, x, cin, cat, ld_cat);
+    const int kt = (w + 15) / 16;
+#define FGR_H3_CASE(KT)                                                                         \
+    case KT:                                                                                    \
+        hipLaunchKernelGGL(res2net_chain_h3_kernel<KT>, grid, dim3(64 * KT), 0, st, h, n, w,    \
+                           scale, scale - 1, (const u32x4*)w_img, w_scale, bias, x, cin, cat,   \
+                           ld_cat);                                                             \
+        break;
+    switch (kt) {
+        FGR_H3_CASE(2)
+        FGR_H3_CASE(4)
+        FGR_H3_CASE(7)
+        FGR_H3_CASE(14)
+        default:
+            set_error("fgr_res2net_chain_h3: width %d has no kernel instance (28, 56, 112, 224)", w);
+            return FGR_E_ARG;
+    }
+#undef FGR_H3_CASE
     FGR_CHECK_LAUNCH("res2net_chain_h3_kernel");
     return FGR_OK;
 }

@@ -266,12 +266,15 @@ class my_Bottle2neck(nn.Module):  # noqa: N801 -- reference name (res2net.py:84)
                 else:
                     w3d, b3d = w3, b3
                 chain = None
-                if w1.is_cuda and ops.res2net_chain_supported(self.width) and self.nums > 0:
+                if w1.is_cuda and self.nums > 0 and (ops.res2net_chain_supported(self.width) or
+                                                     ops.res2net_chain_supported(self.width, True)):
                     wst = torch.stack([wi for wi, _ in ws])
-                    chain = (ops.res2net_fragments(wst),
+                    full = ops.res2net_chain_supported(self.width)
+                    chain = (ops.res2net_fragments(wst) if full else None,
                              torch.stack([bi for _, bi in ws]).contiguous(),
-                             ops.res2net_fragments3(wst),
-                             ops.res2net_fragments_h3(wst))
+                             ops.res2net_fragments3(wst) if full else None,
+                             ops.res2net_fragments_h3(wst)
+                             if ops.res2net_chain_supported(self.width, True) else None)
             self._folded = (key, w1, b1, ws, w3d, b3d, chain)
         return self._folded[1:]
 
@@ -285,15 +288,22 @@ class my_Bottle2neck(nn.Module):  # noqa: N801 -- reference name (res2net.py:84)
         w1, b1, ws, w3d, b3d, chain = self._folded_params()
         out = linear(x, w1, b1, act=ops.ACT_RELU)
         w = self.width
+        use = None
         if chain is not None and self.downsample is not None:
-            # one launch for the whole hierarchy + the [.. | x] concat (fgr_res2net_chain)
+            if lin.MODE == 'f16x3' and chain[3] is not None and (w != 224 or chain[2] is None):
+                use = 'h3'      # (w = 224: the bf16x6 chain measured faster -- fewer barriers)
+            elif lin.MODE in ('bf16x6', 'f16x3') and chain[2] is not None:
+                use = 'bf16x6'
+            elif chain[0] is not None and lin.MODE == 'fp32':
+                use = 'fp32'
+        if use is not None:
+            # one launch for the whole hierarchy + the [.. | x] concat (fgr_res2net_chain*)
             cat_in = torch.empty((x.shape[0], w * self.scale + x.shape[1]), dtype=x.dtype,
                                  device=x.device)
-            if lin.MODE == 'f16x3' and w == 112:
-                # (w = 224: the bf16x6 chain measured faster -- fewer barriers per step)
+            if use == 'h3':
                 ops.res2net_chain(out, w, self.scale, chain[3][0], chain[1], x, cat_in,
                                   w_scale=chain[3][1])
-            elif lin.MODE in ('bf16x6', 'f16x3'):
+            elif use == 'bf16x6':
                 ops.res2net_chain(out, w, self.scale, chain[2], chain[1], x, cat_in, split6=True)
             else:
                 ops.res2net_chain(out, w, self.scale, chain[0], chain[1], x, cat_in)

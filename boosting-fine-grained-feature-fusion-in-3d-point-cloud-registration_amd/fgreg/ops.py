@@ -417,25 +417,31 @@ def res2net_fragments3(weights: torch.Tensor) -> torch.Tensor:
 def res2net_fragments_h3(weights: torch.Tensor):
     """(nums, w, w) Linear weights (out, in) -> (image, inverse scales) of
     fgr_res2net_chain_h3: each output row (i, n) scaled by 2^e so its max |w| lies in
-    [2^14, 2^15) (wsc[i, n] = 2^-e), K zero-padded to a multiple of 32, split into two fp16
-    terms (h = f16(x), m = f16(x - h), round to nearest), in 16x16x32 fragment order
+    [2^14, 2^15) (wsc[i, n] = 2^-e), rows zero-padded to Wp = 16 ceil(w / 16) (one 16-column
+    tile per wave) and K to a multiple of 32, split into two fp16 terms (h = f16(x),
+    m = f16(x - h), round to nearest), in 16x16x32 fragment order
     [i][jt][ks][term][g][c][8] with value W_i[16 jt + c][32 ks + 8 g + e] * 2^e."""
     nums, w, _ = weights.shape
-    ks = (w + 31) // 32
+    wp_rows = (w + 15) // 16 * 16
+    ks = (wp_rows + 31) // 32
     mx = weights.abs().amax(dim=2)                                     # (nums, w)
     e = torch.where(mx > 0, 15 - torch.frexp(mx).exponent, torch.zeros_like(mx, dtype=torch.int32))
     e = e.clamp(max=127)
     sc = torch.ldexp(torch.ones_like(mx), e.float())
-    wp = torch.zeros((nums, w, ks * 32), dtype=torch.float32, device=weights.device)
-    wp[..., :w] = weights * sc[..., None]
+    wp = torch.zeros((nums, wp_rows, ks * 32), dtype=torch.float32, device=weights.device)
+    wp[:, :w, :w] = weights * sc[..., None]
     hi = wp.to(torch.float16)
     lo = (wp - hi.float()).to(torch.float16)
-    t = torch.stack([hi, lo], 0).reshape(2, nums, w // 16, 16, ks, 4, 8)
+    t = torch.stack([hi, lo], 0).reshape(2, nums, wp_rows // 16, 16, ks, 4, 8)
     img = t.permute(1, 2, 4, 0, 5, 3, 6).contiguous()                 # [i, jt, ks, t, g, c, e]
     return img, (1.0 / sc).contiguous()
 
 
-def res2net_chain_supported(w):
+def res2net_chain_supported(w, h3=False):
+    """fp32 / bf16x6 chains: w = 112, 224; the f16x3 chain: any w % 4 == 0 up to 224 whose
+    16-column tile count has a kernel instance (28, 56, 112, 224: every reference width)."""
+    if h3:
+        return w % 4 == 0 and (w + 15) // 16 in (2, 4, 7, 14)
     return w in (112, 224)
 
 

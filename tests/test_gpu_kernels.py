@@ -258,11 +258,12 @@ def test_procrustes_vs_reference(gpu, case):
 
 
 @pytest.mark.parametrize('mode', ['f16x3', 'bf16x6', 'fp32'])
-@pytest.mark.parametrize('cin,cout', [(128, 512), (256, 1024), (8, 32)])
+@pytest.mark.parametrize('cin,cout', [(128, 512), (256, 1024), (32, 128), (64, 256), (8, 32)])
 def test_res2net_block_vs_oracle(gpu, cin, cout, mode):
-    """my_res2Net (res2net.py:84-159, 231-265) in eval: fused fgr_res2net_chain_h3 (f16x3),
-    fgr_res2net_chain6 (bf16x6) or fgr_res2net_chain (fp32 MFMA) for widths 112 / 224,
-    torch path for the narrow width, vs the CPU restatement."""
+    """my_res2Net (res2net.py:84-159, 231-265) in eval: fused fgr_res2net_chain_h3 (f16x3; widths
+    28 / 56 / 112 -- 3DMatch's narrow blocks pad to whole 16-column tiles), fgr_res2net_chain6
+    (bf16x6) or fgr_res2net_chain (fp32 MFMA) for widths 112 / 224, the GEMM loop for the
+    rest (width 7 here), vs the CPU restatement."""
     from fgreg import linear as fl
     from fgreg.backbone import my_Bottle2neck, my_res2Net
     old = fl.MODE
