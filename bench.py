@@ -108,6 +108,9 @@ def parse():
     p.add_argument('--no-cpu-baseline', action='store_true')
     p.add_argument('--profile', action='store_true',
                    help='warmup + timed steps only (for rocprofv3 kernel-trace runs)')
+    p.add_argument('--gemm-table', default=None,
+                   help='write the per-shape GEMM table (M, N, K, launches, us, TFLOP/s, '
+                        'bytes, fractions) of the instrumented replay to this JSON file')
     return p.parse_args()
 
 
@@ -276,6 +279,8 @@ def main():
                 'share_of_step': ms / args.steps / step_ms,
                 'precision': PRECISION.get(mode, mode)}
 
+    if args.gemm_table and rank == 0:
+        write_gemm_table(args.gemm_table, rtimer, args.steps, step_ms, lin.MODE)
     line['roofline_attention'] = mfma_family('attention', ops.ATTN_MODE,
                                              f'fgr_attention_{ops.ATTN_MODE}')
     line['roofline_gemm'] = mfma_family('gemm', lin.MODE, f'fgr_gemm_{lin.MODE} (all dense layers)')
@@ -303,6 +308,35 @@ def main():
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def write_gemm_table(path, rtimer, steps, step_ms, mode):
+    """Per-shape table of the dense layers (bytes, flops, time and the binding
+    roof per shape). bytes = the minimum operand traffic 4 M K (A) + 4 N K (f16x3 image:
+    2 terms x 2 B) + 4 M N (C), assuming every operand is read once."""
+    pipe = PIPE.get(mode, 1)
+    mfma_peak = (F16_MFMA_PEAK_TFLOPS / pipe) if mode != 'fp32' else FP32_MFMA_PEAK_TFLOPS
+    rows = []
+    for (m, n, k), (ms, cnt) in sorted(rtimer.per_label('gemm').items(),
+                                       key=lambda kv: -kv[1][0]):
+        us = ms * 1e3 / cnt
+        flops = 2.0 * m * n * k
+        byt = 4.0 * m * k + 4.0 * n * k + 4.0 * m * n
+        tf = flops / (us * 1e-6) / 1e12
+        gbs = byt / (us * 1e-6) / 1e9
+        t_mfma = flops / (mfma_peak * 1e12) * 1e6
+        t_hbm = byt / (HBM_PEAK_GBS * 1e9) * 1e6
+        rows.append({'M': m, 'N': n, 'K': k, 'launches_per_step': cnt / steps, 'us': us,
+                     'us_per_step': ms * 1e3 / steps, 'gflop': flops / 1e9, 'mbytes': byt / 1e6,
+                     'tflops_fp32_equiv': tf, 'gbs': gbs, 'mfma_frac': tf / mfma_peak,
+                     'hbm_frac': gbs / HBM_PEAK_GBS,
+                     'binding_roof': 'mfma' if t_mfma >= t_hbm else 'hbm',
+                     'roof_frac': max(t_mfma, t_hbm) / us})
+    tot = sum(r['us_per_step'] for r in rows)
+    with open(path, 'w') as f:
+        json.dump({'mode': mode, 'mfma_peak_tflops_fp32_equiv': mfma_peak,
+                   'hbm_peak_gbs': HBM_PEAK_GBS, 'ms_per_step': step_ms,
+                   'gemm_us_per_step': tot, 'shapes': rows}, f, indent=1)
 
 
 def _overlap_flags(a, b, pose, radius=0.05):

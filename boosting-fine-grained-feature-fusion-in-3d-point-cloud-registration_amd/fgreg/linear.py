@@ -185,7 +185,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act=ACT_NONE, residual=N
         if out is None:
             out = torch.empty((m, n), dtype=torch.float32, device=x.device)
         fn = _lib.load().fgr_gemm_f16x3 if h3 else _lib.load().fgr_gemm_bf16x6
-        t0 = _begin('gemm')
+        t0 = _begin('gemm', (m, n, k))
         _lib.check(fn(_ptr(x), x.stride(0), _ptr(sw.img), _ptr(out), out.stride(0), _ptr(bias),
                       _ptr(residual), residual.stride(0) if residual is not None else 0, m, n, k,
                       act, _stream()), 'fgr_gemm_' + MODE)

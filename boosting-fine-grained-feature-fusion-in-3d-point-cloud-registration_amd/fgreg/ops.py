@@ -29,10 +29,11 @@ class KernelTimer:
         self.names = set(names)
         self.events = {n: [] for n in names}
         self.work = {n: [] for n in names}
+        self.labels = {n: [] for n in names}     # optional per-launch label (e.g. GEMM shape)
         self.count = False
         self.pool = []
 
-    def begin(self, name):
+    def begin(self, name, label=None):
         """Creates the event pair of one launch and arms it in libfgreg
         (fgr_time_next_call), so the events are recorded on the launch stream by the entry
         point itself, immediately around its kernels: the interval excludes the Python /
@@ -42,6 +43,7 @@ class KernelTimer:
         start, end = self.pool.pop() if self.pool else self._pair()
         _lib.check(_lib.load().fgr_time_next_call(start.cuda_event, end.cuda_event),
                    'fgr_time_next_call')
+        self.labels[name].append(label)
         return start, end
 
     def end(self, name, pair, work=None):
@@ -66,6 +68,16 @@ class KernelTimer:
 
     def reset_events(self):
         self.events = {n: [] for n in self.names}
+        self.labels = {n: [] for n in self.names}
+
+    def per_label(self, name):
+        """{label: [total ms, launches]} over the recorded launches of `name`."""
+        out = {}
+        for (a, b), lab in zip(self.events[name], self.labels[name]):
+            ent = out.setdefault(lab, [0.0, 0])
+            ent[0] += a.elapsed_time(b)
+            ent[1] += 1
+        return out
 
     def total_ms(self, name):
         return sum(a.elapsed_time(b) for a, b in self.events[name])
@@ -74,8 +86,8 @@ class KernelTimer:
 TIMER = None  # set to a KernelTimer to instrument
 
 
-def _begin(name):
-    return TIMER.begin(name) if TIMER is not None else None
+def _begin(name, label=None):
+    return TIMER.begin(name, label) if TIMER is not None else None
 
 
 def _end(name, start, work=None):
