@@ -267,18 +267,35 @@ __global__ void __launch_bounds__(256) instnorm_ls_stats_kernel(LsArgs a) {
     *reinterpret_cast<float4*>(pp + a.c + col) = q;
 }
 
-__global__ void __launch_bounds__(256) instnorm_ls_merge_kernel(LsArgs a) {
+// one 1024-thread block per (64-channel group, segment): lane = channel, the 16 waves
+// stride over the chunks (coalesced 256-B rows of partials), fp64 sums merged through LDS
+__global__ void __launch_bounds__(1024) instnorm_ls_merge_kernel(LsArgs a) {
+    __shared__ double red[2][16][64];
     const int seg = blockIdx.y;
-    const int ch = blockIdx.x * 256 + threadIdx.x;
-    if (ch >= a.c) return;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int ch = blockIdx.x * 64 + lane;
     const int64_t b = a.seg_off[seg], e = a.seg_off[seg + 1];
-    if (e <= b) return;
+    if (e <= b) return;                                    // block-uniform
     const int nch = (int)((e - b + a.rows - 1) / a.rows);
     double S = 0.0, Q = 0.0;
-    const float* pp = a.part + (int64_t)seg * a.n_chunks * 2 * a.c + ch;
-    for (int k = 0; k < nch; ++k) {
-        S += (double)pp[(int64_t)k * 2 * a.c];
-        Q += (double)pp[(int64_t)k * 2 * a.c + a.c];
+    if (ch < a.c) {
+        const float* pp = a.part + (int64_t)seg * a.n_chunks * 2 * a.c + ch;
+#pragma unroll 4
+        for (int k = wv; k < nch; k += 16) {
+            S += (double)pp[(int64_t)k * 2 * a.c];
+            Q += (double)pp[(int64_t)k * 2 * a.c + a.c];
+        }
+    }
+    red[0][wv][lane] = S;
+    red[1][wv][lane] = Q;
+    __syncthreads();
+    if (wv != 0 || ch >= a.c) return;
+    S = 0.0;
+    Q = 0.0;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) {
+        S += red[0][w][lane];
+        Q += red[1][w][lane];
     }
     float kv = a.x[b * a.c + ch];
     if (a.row_div) kv = kv / a.row_div[b];
@@ -512,7 +529,7 @@ extern "C" int fgr_instnorm(const float* x, int64_t n, int32_t c, const int64_t*
                   residual, post_act, out, part, part + (size_t)n_seg * lc * 2 * c};
         hipLaunchKernelGGL(instnorm_ls_stats_kernel, dim3((unsigned)lc, n_seg), dim3(256), 0, st, la);
         FGR_CHECK_LAUNCH("instnorm_ls_stats_kernel");
-        hipLaunchKernelGGL(instnorm_ls_merge_kernel, dim3((unsigned)ceil_div(c, 256), n_seg), dim3(256),
+        hipLaunchKernelGGL(instnorm_ls_merge_kernel, dim3((unsigned)ceil_div(c, 64), n_seg), dim3(1024),
                            0, st, la);
         FGR_CHECK_LAUNCH("instnorm_ls_merge_kernel");
         hipLaunchKernelGGL(instnorm_ls_apply_kernel, dim3((unsigned)lc, n_seg), dim3(256), 0, st, la);

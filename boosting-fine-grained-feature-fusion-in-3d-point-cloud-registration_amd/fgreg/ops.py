@@ -542,14 +542,18 @@ def attention(q, k, v, q_off, kv_off, kv_seg, max_q_len, n_head, out=None,
 
 
 _WS = {}
+_WS_RETIRED = []
 
 
 def _workspace(device, nbytes):
     """Grow-only scratch buffer per device, reused by consecutive launches on the current
-    stream (stream order serialises the reuse)."""
+    stream (stream order serialises the reuse). Outgrown buffers are kept alive: a captured
+    HIP graph may still point at them."""
     key = (device, torch.cuda.current_stream(device).cuda_stream)
     buf = _WS.get(key)
     if buf is None or buf.numel() < nbytes:
+        if buf is not None:
+            _WS_RETIRED.append(buf)
         buf = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
         _WS[key] = buf
     return buf

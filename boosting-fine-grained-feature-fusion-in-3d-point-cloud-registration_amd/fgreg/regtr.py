@@ -12,6 +12,9 @@ the forward is re-laid out for the GPU:
 The returned per-cloud lists are views into the packed tensors.
 """
 import logging
+import os
+import weakref
+from collections import OrderedDict
 
 import torch
 import torch.nn as nn
@@ -149,24 +152,17 @@ class RegTR(nn.Module):
         meta = self.preprocessor(list(batch['src_xyz']) + list(batch['tgt_xyz']))
         batch['kpconv_meta'] = meta
         n_lvl = len(meta['points'])
-        slens_c, off_c = host_layout(meta, n_lvl - 1)
-        pts0 = meta['points'][0]
-        feats0 = torch.ones((pts0.shape[0], 1), dtype=torch.float32, device=pts0.device)
-
-        feats_un, _ = self.kpf_encoder(feats0, meta)
-        both = linear(feats_un, self.feat_proj.weight, self.feat_proj.bias)
+        slens_c, _ = host_layout(meta, n_lvl - 1)
+        for lvl in range(n_lvl):                     # device offsets of every level, eagerly
+            host_layout(meta, lvl)
         xyz_c = meta['points'][-1]
-        pe = self.pos_embed(xyz_c)
-        seg = Segments(slens_c, xyz_c.device)
-        pos = pe if self.cfg.transformer_encoder_has_pos_emb else None
-        if pos is None:
-            pos = torch.zeros_like(both)
-        feats = self.transformer_encoder.forward_packed(both, pos, seg)        # (L, N, d)
-        if isinstance(self.correspondence_decoder, CorrespondenceRegressor):
-            corr, logits = self.correspondence_decoder.forward_packed(feats)
+        core = None
+        if GRAPHS and xyz_c.is_cuda and ops.TIMER is None:
+            core = _graph_for(self, meta, slens_c, B)
+        if core is not None:
+            both, feats, corr, logits, pose = core.run(meta)
         else:
-            corr, logits = self.correspondence_decoder.forward_packed(feats, xyz_c, pe, seg)
-        pose = ops.pair_pose(xyz_c, corr, logits[..., 0], seg.off, B, self.pose_threshold)
+            both, feats, corr, logits, pose = self._core(meta, Segments(slens_c, xyz_c.device), B)
 
         offs = [0]
         for n in slens_c:
@@ -186,3 +182,107 @@ class RegTR(nn.Module):
             'pose': pose,
         }
         return outputs
+
+    def _core(self, meta, seg, B):
+        """The post-preprocessing forward (finegrained_regtr.py:126-218): encoder, feat_proj,
+        positional embedding, cross encoder, correspondence head, pose. Pure device work on
+        the kpconv_meta tensors and their precomputed host layout -- no host sync, no host
+        -> device copy -- so it can be captured in a HIP graph (_CoreGraph)."""
+        pts0 = meta['points'][0]
+        feats0 = torch.ones((pts0.shape[0], 1), dtype=torch.float32, device=pts0.device)
+        feats_un, _ = self.kpf_encoder(feats0, meta)
+        both = linear(feats_un, self.feat_proj.weight, self.feat_proj.bias)
+        xyz_c = meta['points'][-1]
+        pe = self.pos_embed(xyz_c)
+        pos = pe if self.cfg.transformer_encoder_has_pos_emb else None
+        if pos is None:
+            pos = torch.zeros_like(both)
+        feats = self.transformer_encoder.forward_packed(both, pos, seg)        # (L, N, d)
+        if isinstance(self.correspondence_decoder, CorrespondenceRegressor):
+            corr, logits = self.correspondence_decoder.forward_packed(feats)
+        else:
+            corr, logits = self.correspondence_decoder.forward_packed(feats, xyz_c, pe, seg)
+        pose = ops.pair_pose(xyz_c, corr, logits[..., 0], seg.off, B, self.pose_threshold)
+        return both, feats, corr, logits, pose
+
+    def _apply(self, fn, *args, **kwargs):
+        _GRAPHS.pop(self, None)        # .to() / .cuda() move the weights the graphs point at
+        return super()._apply(fn, *args, **kwargs)
+
+
+# ------------------------------------------------------------------------------------------
+# HIP-graph replay of the post-preprocessing forward
+# ------------------------------------------------------------------------------------------
+# The preprocessing has one host sync per pyramid level (voxel counts) and data-dependent
+# sizes, so it always runs eagerly. Everything after it is a fixed sequence of ~130-300
+# launches whose shapes are set by the pyramid's per-cloud lengths: for a batch whose
+# lengths (the "signature") were seen before, that sequence is captured once into a HIP graph
+# (torch.cuda.CUDAGraph = hipGraph on ROCm) and replayed, removing the host launch cost
+# (ctypes, Python) between kernels. The graph reads the kpconv_meta through static copies
+# (refreshed by device copies before each replay) and its outputs are cloned, so callers
+# never see a buffer that the next replay overwrites. Signatures are captured on their
+# SECOND occurrence (one-off shapes stay eager), at most GRAPH_CACHE per model; a parameter
+# update (version change), load_state_dict or .to() drops the model's graphs.
+# FGREG_GRAPHS=0 disables the path (A/B).
+GRAPHS = os.environ.get('FGREG_GRAPHS', '1') != '0'
+GRAPH_CACHE = 8
+_GRAPHS = weakref.WeakKeyDictionary()        # model -> {'ver', 'seen', 'graphs'}
+_META_IN = ('points', 'neighbors', 'pools')  # what the core reads (upsamples: decoder only)
+
+
+class _CoreGraph:
+    def __init__(self, model, meta, slens_c, B):
+        self.meta = {k: [t.clone() for t in meta[k]] for k in _META_IN}
+        self.meta['stack_lengths'] = list(meta['stack_lengths'])
+        self.meta['_host'] = {'lengths': meta['_host']['lengths'],
+                              'offsets': [o.clone() for o in meta['_host']['offsets']]}
+        self.seg = Segments(slens_c, meta['points'][-1].device)
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):                 # warm-up outside the capture
+            model._core(self.meta, self.seg, B)
+        torch.cuda.current_stream().wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.out = model._core(self.meta, self.seg, B)
+
+    def run(self, meta):
+        for k in _META_IN:
+            for dst, src in zip(self.meta[k], meta[k]):
+                dst.copy_(src)
+        self.graph.replay()
+        return tuple(t.clone() for t in self.out)
+
+
+def _params_version(model):
+    st = _GRAPHS.get(model)
+    plist = st['params'] if st is not None else list(model.parameters()) + list(model.buffers())
+    return sum(p._version for p in plist), plist
+
+
+def _graph_for(model, meta, slens_c, B):
+    ver, plist = _params_version(model)
+    st = _GRAPHS.get(model)
+    if st is None or st['ver'] != ver:
+        st = {'ver': ver, 'params': plist, 'seen': {}, 'graphs': OrderedDict()}
+        _GRAPHS[model] = st
+    sig = (B, tuple(tuple(l) for l in meta['_host']['lengths']),
+           tuple(tuple(t.shape) for t in meta['neighbors']), tuple(tuple(t.shape) for t in meta['pools']))
+    g = st['graphs'].get(sig)
+    if g is not None:
+        st['graphs'].move_to_end(sig)
+        return g
+    n = st['seen'].get(sig, 0)
+    st['seen'][sig] = n + 1
+    if n == 0 or len(st['seen']) > 4096:
+        return None
+    try:
+        g = _CoreGraph(model, meta, slens_c, B)
+    except RuntimeError as e:                          # capture unsupported here: stay eager
+        _logger.warning('fgreg: HIP graph capture failed (%s); running eagerly', e)
+        st['seen'][sig] = -(1 << 30)
+        return None
+    st['graphs'][sig] = g
+    while len(st['graphs']) > GRAPH_CACHE:
+        st['graphs'].popitem(last=False)
+    return g

@@ -135,3 +135,46 @@ def test_forward_full_config_vs_oracle(gpu, kind, B, n_points):
     for k, v in worst.items():
         assert v < ELEM_TOL, (k, v)
     assert np.abs(out['pose'].cpu().numpy() - ref['pose'].numpy()).max() < TOL
+
+
+def test_graph_replay_matches_eager(gpu):
+    """The HIP-graph replay of the post-preprocessing forward (fgreg.regtr._CoreGraph) gives
+    the eager forward's outputs bit for bit, also for a DIFFERENT batch with the same shape
+    signature (points permuted within each cloud: same per-level lengths and table shapes,
+    different kpconv_meta contents), and its outputs are not aliased by the next replay."""
+    import fgreg.config as fc
+    import fgreg.regtr as rt
+    from fgreg.synthetic import make_batch
+    model = _random_model(fc.get('modelnet'), 5).to(gpu)
+    src, tgt, _ = make_batch('modelnet', 2)
+    rng = np.random.default_rng(0)
+    src2 = [s[rng.permutation(len(s))] for s in src]
+    tgt2 = [t[rng.permutation(len(t))] for t in tgt]
+    old = rt.GRAPHS
+    try:
+        rt.GRAPHS = False
+        e1 = model(_batch(src, tgt, gpu))
+        e2 = model(_batch(src2, tgt2, gpu))
+        rt.GRAPHS = True
+        model(_batch(src, tgt, gpu))
+        model(_batch(src, tgt, gpu))                  # second sighting: captured
+        assert len(rt._GRAPHS[model]['graphs']) == 1
+        g1 = model(_batch(src, tgt, gpu))
+        g2 = model(_batch(src2, tgt2, gpu))
+        assert len(rt._GRAPHS[model]['graphs']) == 1  # same signature: replayed, not recaptured
+    finally:
+        rt.GRAPHS = old
+    for ref, got in ((e1, g1), (e2, g2)):
+        for k in KEYS:
+            for b in range(2):
+                assert torch.equal(got[k][b], ref[k][b]), k
+        assert torch.equal(got['pose'], ref['pose'])
+    # a parameter update invalidates the captured graphs
+    with torch.no_grad():
+        model.feat_proj.bias.add_(0.0)
+    rt.GRAPHS = True
+    try:
+        model(_batch(src, tgt, gpu))
+        assert len(rt._GRAPHS[model]['graphs']) == 0
+    finally:
+        rt.GRAPHS = old
