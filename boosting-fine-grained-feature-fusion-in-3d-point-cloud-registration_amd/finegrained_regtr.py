@@ -63,6 +63,11 @@ class RegTR(GenericRegModel):
 
     forward = fgreg.RegTR.forward
     _forward = fgreg.RegTR._forward
+    _core = fgreg.RegTR._core
+
+    def _apply(self, fn, *args, **kwargs):
+        fgreg.regtr._GRAPHS.pop(self, None)   # captured graphs point at the old weights
+        return super()._apply(fn, *args, **kwargs)
 
     def compute_loss(self, pred, batch):
         """finegrained_regtr.py:252-309 on libfgreg (fgreg/loss.py): overlap BCE, InfoNCE
