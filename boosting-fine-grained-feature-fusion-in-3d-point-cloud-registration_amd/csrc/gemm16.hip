@@ -472,6 +472,201 @@ __global__ void __launch_bounds__(256) gemm_f16x3_v2(GemmH3Args p) {
 }
 
 // ------------------------------------------------------------------------------------
+// v3: the v2 stage layout (KS k32-steps per stage, double-buffered LDS, one barrier per
+// stage) with a two-deep REGISTER ring: while stage s is multiplied, the global loads of
+// stages s+1 and s+2 are in flight (v2 keeps only s+1 in flight, so every stage waits out
+// most of an L2/HBM round trip). Stage s+1 is split and written to the idle LDS buffer after
+// the MFMAs of stage s, then its registers are refilled with stage s+3. The loop is unrolled
+// by two so every ring index is a compile-time constant (no scratch).
+// ------------------------------------------------------------------------------------
+template <int BM, int BN, int KS, bool KVEC>
+__global__ void __launch_bounds__(256) gemm_f16x3_v3(GemmH3Args p) {
+    constexpr int TM = BM / 32, TN = BN / 32;
+    constexpr int RU = 4 * KS;                          // units (8 k) of a row per stage
+    constexpr int UA = BM * RU / 256;                   // A units per thread per stage
+    constexpr int UW = 8 * BN * KS / 256;               // W units per thread per stage
+    constexpr int ASZ = 8 * BM * KS, WSZ = 8 * BN * KS; // 16-B units per stage
+    static_assert(UA >= 1 && UW >= 1 && (RU == 4 || RU == 8), "tile");
+    __shared__ u32x4 lds[2 * (ASZ + WSZ)];
+    __shared__ int sh_lds[2][BM];
+
+    const int nbm = (p.M + BM - 1) / BM, nbn = (p.N + BN - 1) / BN;
+    const int nwg = nbm * nbn;
+    int t = blockIdx.x;
+    {
+        const int q = nwg / 8, r = nwg % 8, x = t % 8, lo = t / 8;
+        t = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + lo;
+    }
+    const int bm = t / nbn, bn = t % nbn;
+    const int m0 = bm * BM, n0 = bn * BN;
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+    const int wn = (wv >> 1) * (BN / 2), wm = (wv & 1) * (BM / 2);
+    const int g = lane >> 4, c = lane & 15;
+    const int npanel = (p.N + 15) / 16;
+
+    const float* arow[UA];
+    int akk[UA], sh[UA];
+#pragma unroll
+    for (int j = 0; j < UA; ++j) {
+        const int u = tid + 256 * j;
+        arow[j] = p.A + (int64_t)min(m0 + u / RU, p.M - 1) * p.lda;
+        akk[j] = 8 * (u % RU);
+        sh[j] = SH_UNSET;
+    }
+    const u32x4* wsrc[UW];
+#pragma unroll
+    for (int j = 0; j < UW; ++j) {
+        const int v = tid + 256 * j;
+        const int panel = min(n0 / 16 + v / (128 * KS), npanel - 1);
+        wsrc[j] = p.W + (int64_t)panel * p.ksteps * 128 + v % (128 * KS);
+    }
+    float4 ar0[UA][2], ar1[UA][2];
+    u32x4 wr0[UW], wr1[UW];
+    auto load = [&](int s, float4 (&ar)[UA][2], u32x4 (&wr)[UW]) {
+#pragma unroll
+        for (int j = 0; j < UA; ++j) {
+            const int k = s * 32 * KS + akk[j];
+            if constexpr (KVEC) {
+                const float* src = arow[j] + min(k, p.K - 8);
+                const float4 x0 = *reinterpret_cast<const float4*>(src);
+                const float4 x1 = *reinterpret_cast<const float4*>(src + 4);
+                const bool ok = k < p.K;
+                ar[j][0] = ok ? x0 : make_float4(0.f, 0.f, 0.f, 0.f);
+                ar[j][1] = ok ? x1 : make_float4(0.f, 0.f, 0.f, 0.f);
+            } else {
+                float tt[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const float xv = arow[j][min(k + e, p.K - 1)];
+                    tt[e] = k + e < p.K ? xv : 0.f;
+                }
+                ar[j][0] = make_float4(tt[0], tt[1], tt[2], tt[3]);
+                ar[j][1] = make_float4(tt[4], tt[5], tt[6], tt[7]);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < UW; ++j) wr[j] = wsrc[j][(int64_t)s * 128 * KS];
+    };
+    auto store = [&](int b, const float4 (&ar)[UA][2], const u32x4 (&wr)[UW]) {
+        u32x4* a_img = lds + b * (ASZ + WSZ);
+        u32x4* w_img = a_img + ASZ;
+#pragma unroll
+        for (int j = 0; j < UA; ++j) {
+            const int u = tid + 256 * j;
+            const int row = u / RU, q = u % RU, ks = q >> 2, gg = q & 3;
+            const float x[8] = {ar[j][0].x, ar[j][0].y, ar[j][0].z, ar[j][0].w,
+                                ar[j][1].x, ar[j][1].y, ar[j][1].z, ar[j][1].w};
+            float cm = fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3])));
+            cm = fmaxf(cm, fmaxf(fmaxf(fabsf(x[4]), fabsf(x[5])), fmaxf(fabsf(x[6]), fabsf(x[7]))));
+            cm = fmaxf(cm, dppf<0xB1>(cm));
+            cm = fmaxf(cm, dppf<0x4E>(cm));
+            if constexpr (RU == 8) cm = fmaxf(cm, dppf<0x141>(cm));
+            if (cm > 0.f && __builtin_amdgcn_frexp_expf(cm) + sh[j] > 15) sh[j] = chunk_shift(cm);
+            const float sc = __builtin_ldexpf(1.f, sh[j] == SH_UNSET ? 0 : sh[j]);
+            f16x8 th, tm;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float xs = x[e] * sc;
+                const _Float16 h = (_Float16)xs;
+                th[e] = h;
+                tm[e] = (_Float16)(xs - (float)h);
+            }
+            const int r = row ^ (2 * gg);
+            a_img[((ks * 2 + 0) * 4 + gg) * BM + r] = __builtin_bit_cast(u32x4, th);
+            a_img[((ks * 2 + 1) * 4 + gg) * BM + r] = __builtin_bit_cast(u32x4, tm);
+            if (q == 0) sh_lds[b][row] = sh[j];
+        }
+#pragma unroll
+        for (int j = 0; j < UW; ++j) w_img[tid + 256 * j] = wr[j];
+    };
+
+    f32x4 acc[TN][TM];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    int shr[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) shr[i] = SH_UNSET;
+
+    auto compute = [&](int b) {
+        const u32x4* a_img = lds + b * (ASZ + WSZ);
+        const u32x4* w_img = a_img + ASZ;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const int shv = sh_lds[b][wm + 16 * i + c];
+            if (__builtin_amdgcn_ballot_w64(shv != shr[i])) {
+                const float f = (shr[i] == SH_UNSET || shv == shr[i])
+                                    ? 1.f : __builtin_ldexpf(1.f, shv - shr[i]);
+#pragma unroll
+                for (int j = 0; j < TN; ++j) acc[j][i] *= f;
+                shr[i] = shv;
+            }
+        }
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            f16x8 af[TM][2];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const int r = (wm + 16 * i + c) ^ (2 * g);
+                af[i][0] = __builtin_bit_cast(f16x8, a_img[((ks * 2 + 0) * 4 + g) * BM + r]);
+                af[i][1] = __builtin_bit_cast(f16x8, a_img[((ks * 2 + 1) * 4 + g) * BM + r]);
+            }
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int pp = (wn + 16 * j) >> 4;
+                const u32x4* wb = w_img + pp * 128 * KS + ks * 128 + g * 16 + c;
+                const f16x8 wh = __builtin_bit_cast(f16x8, wb[0]);
+                const f16x8 wl = __builtin_bit_cast(f16x8, wb[64]);
+#pragma unroll
+                for (int i = 0; i < TM; ++i) {
+                    acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, af[i][0], acc[j][i], 0, 0, 0);
+                    acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, af[i][1], acc[j][i], 0, 0, 0);
+                    acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, af[i][0], acc[j][i], 0, 0, 0);
+                }
+            }
+        }
+    };
+
+    const int nst = (p.K + 32 * KS - 1) / (32 * KS);
+    load(0, ar0, wr0);
+    if (nst > 1) load(1, ar1, wr1);
+    store(0, ar0, wr0);
+    __syncthreads();
+    if (nst > 2) load(2, ar0, wr0);
+    // iteration s: multiply buffer s&1, stage s+1 from ring (s+1)&1, refill it with s+3
+    for (int s = 0; s < nst; s += 2) {
+        compute(0);
+        if (s + 1 < nst) store(1, ar1, wr1);
+        if (s + 3 < nst) load(s + 3, ar1, wr1);
+        __syncthreads();
+        if (s + 1 >= nst) break;
+        compute(1);
+        if (s + 2 < nst) store(0, ar0, wr0);
+        if (s + 4 < nst) load(s + 4, ar0, wr0);
+        __syncthreads();
+    }
+
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        const int m = m0 + wm + 16 * i + c;
+        if (m >= p.M) continue;
+        const float rs = __builtin_ldexpf(1.f, -shr[i]);
+        float* crow = p.C + (int64_t)m * p.ldc;
+        const float* rrow = p.R ? p.R + (int64_t)m * p.ldr : nullptr;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int n = n0 + wn + 16 * j + 4 * g;
+            if (n >= p.N) continue;
+            const float4 ws = *reinterpret_cast<const float4*>(p.wsc + n);
+            const float y[4] = {acc[j][i][0] * rs * ws.x, acc[j][i][1] * rs * ws.y,
+                                acc[j][i][2] * rs * ws.z, acc[j][i][3] * rs * ws.w};
+            store_out4(y, p.bias, rrow, crow, n, p.N, p.act, p.vec_out);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
 // Row-resident f16x3 GEMM for short contractions (K <= 256), optionally fused with the
 // LayerNorm (+ positional-embedding add) that produces its input:
 //   A = LN(X) * gamma + beta (+ P)      (or A = X),    C = act(A W^T + bias (+ R))
@@ -701,6 +896,17 @@ size_t image_bytes_h3(int n, int k) {
     return (size_t)((n + 15) / 16) * ksteps_h3(k) * 128 * 16;
 }
 
+template <int BM, int BN, int KS>
+void launch_h3v3(const GemmH3Args& a, hipStream_t st) {
+    const int nbm = (a.M + BM - 1) / BM, nbn = (a.N + BN - 1) / BN;
+    if (a.K % 8 == 0)
+        hipLaunchKernelGGL((gemm_f16x3_v3<BM, BN, KS, true>), dim3((unsigned)(nbm * nbn)),
+                           dim3(256), 0, st, a);
+    else
+        hipLaunchKernelGGL((gemm_f16x3_v3<BM, BN, KS, false>), dim3((unsigned)(nbm * nbn)),
+                           dim3(256), 0, st, a);
+}
+
 template <int BM, int BN, int KS, bool DBUF>
 void launch_h3v2(const GemmH3Args& a, hipStream_t st) {
     const int nbm = (a.M + BM - 1) / BM, nbn = (a.N + BN - 1) / BN;
@@ -789,9 +995,16 @@ extern "C" int fgr_gemm_f16x3(const float* a, int64_t lda, const void* w_img, fl
         case 'k': launch_h3v2<64, 128, 1, true>(g, st); break;
         case 'l': launch_h3v2<64, 64, 1, true>(g, st); break;
         case 'm': launch_h3v2<128, 64, 2, false>(g, st); break;
+        // v3 (two-deep register ring): n..s
+        case 'n': launch_h3v3<64, 64, 2>(g, st); break;
+        case 'o': launch_h3v3<64, 128, 1>(g, st); break;
+        case 'p': launch_h3v3<64, 128, 2>(g, st); break;
+        case 'q': launch_h3v3<128, 64, 1>(g, st); break;
+        case 'r': launch_h3v3<128, 128, 1>(g, st); break;
+        case 's': launch_h3v3<128, 64, 2>(g, st); break;
         default: break;
     }
-    if (cfg >= 'e' && cfg <= 'm') {
+    if (cfg >= 'e' && cfg <= 's') {
         FGR_CHECK_LAUNCH("gemm_f16x3_v2");
         return FGR_OK;
     }

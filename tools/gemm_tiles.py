@@ -1,0 +1,58 @@
+"""GEMM tile sweep (development tool, GPU): times fgr_gemm_f16x3 per tile configuration
+(FGR_GEMM16_TILE) on the forward's shapes and checks every variant against an fp64 product.
+usage: python tools/gemm_tiles.py [configs] > gpurun_out/gemm_tiles.txt"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                'boosting-fine-grained-feature-fusion-in-3d-point-cloud-registration_amd'))
+import fgreg.linear as lin  # noqa: E402
+
+SHAPES = [(9544, 768, 256), (9544, 1024, 2048), (9544, 256, 1024), (9544, 256, 3840),
+          (9544, 256, 256), (9544, 1024, 256), (11472, 512, 1024), (11472, 128, 1920),
+          (9544, 1792, 256), (57264, 256, 256), (11472, 896, 128), (2120, 1536, 512),
+          (2120, 512, 1024), (2120, 512, 512), (26778, 256, 512), (40000, 128, 256)]
+
+
+def timeit(fn, iters=30):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(iters):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / iters * 1e3
+
+
+def main():
+    cfgs = sys.argv[1] if len(sys.argv) > 1 else 'befknopqrs'
+    dev = torch.device('cuda:0')
+    lin.set_mode('f16x3')
+    g = torch.Generator(device=dev).manual_seed(0)
+    for (M, N, K) in SHAPES:
+        x = torch.randn(M, K, device=dev, generator=g)
+        w = torch.randn(N, K, device=dev, generator=g) * 0.05
+        ref = (x.double() @ w.double().t())
+        line = f'M={M:6d} N={N:5d} K={K:5d}'
+        best = None
+        for t in cfgs:
+            os.environ['FGR_GEMM16_TILE'] = t
+            y = lin.linear(x, w)
+            err = float((y.double() - ref).abs().max() / ref.abs().max())
+            us = timeit(lambda: lin.linear(x, w))
+            tf = 2 * M * N * K / us / 1e6
+            line += f' | {t} {us:6.1f}us {tf:5.0f}TF{"" if err < 1e-5 else " ERR%.1e" % err}'
+            if best is None or us < best[1]:
+                best = (t, us)
+        os.environ['FGR_GEMM16_TILE'] = ''
+        us0 = timeit(lambda: lin.linear(x, w))
+        print(line + f' || default {us0:6.1f}us best {best[0]}', flush=True)
+
+
+if __name__ == '__main__':
+    main()
