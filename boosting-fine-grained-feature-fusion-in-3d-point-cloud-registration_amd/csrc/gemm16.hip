@@ -667,6 +667,196 @@ __global__ void __launch_bounds__(256) gemm_f16x3_v3(GemmH3Args p) {
 }
 
 // ------------------------------------------------------------------------------------
+// v4: W fragments straight from the image into registers. The f16x3 W image is stored in
+// MFMA fragment order ([panel][kstep][term][g][16] x 16 B), so one wave-load of a panel's
+// term is 1 KB contiguous in lane order -- no LDS round trip for W. The waves split the
+// block's BN output channels (BN/4 each: TN = BN/64 16-column tiles) and each covers all
+// BM activation rows, so no W byte is loaded twice per block; only A is staged (split in
+// registers -> double-buffered LDS, one barrier per k32 step). W fragments of step s+1 are
+// loaded while step s multiplies (register double buffer, loop unrolled by two).
+// Motivation (VERDICT r1 / microbench): v1-v3 stage W through LDS with ds_write_b128, whose
+// transfer cost (~13 cycles per wave-instruction) plus the fragment reads exceeds the
+// MFMA time of a 64 x 128 step -- they are LDS-bound.
+// ------------------------------------------------------------------------------------
+template <int BM, int BN, bool KVEC>
+__global__ void __launch_bounds__(256) gemm_f16x3_v4(GemmH3Args p) {
+    constexpr int TM = BM / 16, TN = BN / 64;          // per wave: TM row tiles x TN col tiles
+    constexpr int UA = BM * 4 / 256;                    // A units (8 k) per thread per step
+    constexpr int ASZ = 8 * BM;                         // 16-B units of one A stage
+    static_assert(UA >= 1 && TN >= 1, "tile");
+    __shared__ u32x4 a_lds[2 * ASZ];
+    __shared__ int sh_lds[2][BM];
+
+    const int nbm = (p.M + BM - 1) / BM, nbn = (p.N + BN - 1) / BN;
+    const int nwg = nbm * nbn;
+    int t = blockIdx.x;
+    {
+        const int q = nwg / 8, r = nwg % 8, x = t % 8, lo = t / 8;
+        t = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + lo;
+    }
+    const int bm = t / nbn, bn = t % nbn;
+    const int m0 = bm * BM, n0 = bn * BN;
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+    const int g = lane >> 4, c = lane & 15;
+    const int npanel = (p.N + 15) / 16;
+    const int wn = wv * (BN / 4);                       // this wave's first output channel
+
+    const float* arow[UA];
+    int akk[UA], sh[UA];
+#pragma unroll
+    for (int j = 0; j < UA; ++j) {
+        const int u = tid + 256 * j;
+        arow[j] = p.A + (int64_t)min(m0 + (u >> 2), p.M - 1) * p.lda;
+        akk[j] = 8 * (u & 3);
+        sh[j] = SH_UNSET;
+    }
+    // W fragment pointers: panel of tile j, lane's unit within a (kstep, term) block of 64
+    const u32x4* wp[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int panel = min((n0 + wn) / 16 + j, npanel - 1);
+        wp[j] = p.W + (int64_t)panel * p.ksteps * 128 + lane;
+    }
+    float4 ar[UA][2];
+    auto load_a = [&](int s) {
+#pragma unroll
+        for (int j = 0; j < UA; ++j) {
+            const int k = s * 32 + akk[j];
+            if constexpr (KVEC) {
+                const float* src = arow[j] + min(k, p.K - 8);
+                const float4 x0 = *reinterpret_cast<const float4*>(src);
+                const float4 x1 = *reinterpret_cast<const float4*>(src + 4);
+                const bool ok = k < p.K;
+                ar[j][0] = ok ? x0 : make_float4(0.f, 0.f, 0.f, 0.f);
+                ar[j][1] = ok ? x1 : make_float4(0.f, 0.f, 0.f, 0.f);
+            } else {
+                float tt[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const float xv = arow[j][min(k + e, p.K - 1)];
+                    tt[e] = k + e < p.K ? xv : 0.f;
+                }
+                ar[j][0] = make_float4(tt[0], tt[1], tt[2], tt[3]);
+                ar[j][1] = make_float4(tt[4], tt[5], tt[6], tt[7]);
+            }
+        }
+    };
+    auto store_a = [&](int b) {
+        u32x4* a_img = a_lds + b * ASZ;
+#pragma unroll
+        for (int j = 0; j < UA; ++j) {
+            const int u = tid + 256 * j;
+            const int row = u >> 2, gg = u & 3;
+            const float x[8] = {ar[j][0].x, ar[j][0].y, ar[j][0].z, ar[j][0].w,
+                                ar[j][1].x, ar[j][1].y, ar[j][1].z, ar[j][1].w};
+            float cm = fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3])));
+            cm = fmaxf(cm, fmaxf(fmaxf(fabsf(x[4]), fabsf(x[5])), fmaxf(fabsf(x[6]), fabsf(x[7]))));
+            cm = fmaxf(cm, dppf<0xB1>(cm));
+            cm = fmaxf(cm, dppf<0x4E>(cm));
+            if (cm > 0.f && __builtin_amdgcn_frexp_expf(cm) + sh[j] > 15) sh[j] = chunk_shift(cm);
+            const float sc = __builtin_ldexpf(1.f, sh[j] == SH_UNSET ? 0 : sh[j]);
+            f16x8 th, tm;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float xs = x[e] * sc;
+                const _Float16 h = (_Float16)xs;
+                th[e] = h;
+                tm[e] = (_Float16)(xs - (float)h);
+            }
+            const int r = row ^ (2 * gg);
+            a_img[(0 * 4 + gg) * BM + r] = __builtin_bit_cast(u32x4, th);
+            a_img[(1 * 4 + gg) * BM + r] = __builtin_bit_cast(u32x4, tm);
+            if (gg == 0) sh_lds[b][row] = sh[j];
+        }
+    };
+    u32x4 w0[TN][2], w1[TN][2];
+    auto load_w = [&](int s, u32x4 (&w)[TN][2]) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            w[j][0] = wp[j][(int64_t)s * 128];
+            w[j][1] = wp[j][(int64_t)s * 128 + 64];
+        }
+    };
+
+    f32x4 acc[TN][TM];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    int shr[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) shr[i] = SH_UNSET;
+
+    auto compute = [&](int b, const u32x4 (&w)[TN][2]) {
+        const u32x4* a_img = a_lds + b * ASZ;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const int shv = sh_lds[b][16 * i + c];
+            if (__builtin_amdgcn_ballot_w64(shv != shr[i])) {
+                const float f = (shr[i] == SH_UNSET || shv == shr[i])
+                                    ? 1.f : __builtin_ldexpf(1.f, shv - shr[i]);
+#pragma unroll
+                for (int j = 0; j < TN; ++j) acc[j][i] *= f;
+                shr[i] = shv;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const int r = (16 * i + c) ^ (2 * g);
+            const f16x8 ah = __builtin_bit_cast(f16x8, a_img[(0 * 4 + g) * BM + r]);
+            const f16x8 am = __builtin_bit_cast(f16x8, a_img[(1 * 4 + g) * BM + r]);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const f16x8 wh = __builtin_bit_cast(f16x8, w[j][0]);
+                const f16x8 wl = __builtin_bit_cast(f16x8, w[j][1]);
+                acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, ah, acc[j][i], 0, 0, 0);
+                acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, am, acc[j][i], 0, 0, 0);
+                acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, ah, acc[j][i], 0, 0, 0);
+            }
+        }
+    };
+
+    const int nk = (p.K + 31) / 32;
+    load_a(0);
+    load_w(0, w0);
+    for (int s = 0; s < nk; s += 2) {
+        store_a(0);
+        __syncthreads();
+        if (s + 1 < nk) {
+            load_a(s + 1);
+            load_w(s + 1, w1);
+        }
+        compute(0, w0);
+        if (s + 1 >= nk) break;
+        store_a(1);
+        __syncthreads();
+        if (s + 2 < nk) {
+            load_a(s + 2);
+            load_w(s + 2, w0);
+        }
+        compute(1, w1);
+    }
+
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        const int m = m0 + 16 * i + c;
+        if (m >= p.M) continue;
+        const float rs = __builtin_ldexpf(1.f, -shr[i]);
+        float* crow = p.C + (int64_t)m * p.ldc;
+        const float* rrow = p.R ? p.R + (int64_t)m * p.ldr : nullptr;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int n = n0 + wn + 16 * j + 4 * g;
+            if (n >= p.N) continue;
+            const float4 ws = *reinterpret_cast<const float4*>(p.wsc + n);
+            const float y[4] = {acc[j][i][0] * rs * ws.x, acc[j][i][1] * rs * ws.y,
+                                acc[j][i][2] * rs * ws.z, acc[j][i][3] * rs * ws.w};
+            store_out4(y, p.bias, rrow, crow, n, p.N, p.act, p.vec_out);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
 // Row-resident f16x3 GEMM for short contractions (K <= 256), optionally fused with the
 // LayerNorm (+ positional-embedding add) that produces its input:
 //   A = LN(X) * gamma + beta (+ P)      (or A = X),    C = act(A W^T + bias (+ R))
@@ -896,6 +1086,17 @@ size_t image_bytes_h3(int n, int k) {
     return (size_t)((n + 15) / 16) * ksteps_h3(k) * 128 * 16;
 }
 
+template <int BM, int BN>
+void launch_h3v4(const GemmH3Args& a, hipStream_t st) {
+    const int nbm = (a.M + BM - 1) / BM, nbn = (a.N + BN - 1) / BN;
+    if (a.K % 8 == 0)
+        hipLaunchKernelGGL((gemm_f16x3_v4<BM, BN, true>), dim3((unsigned)(nbm * nbn)), dim3(256),
+                           0, st, a);
+    else
+        hipLaunchKernelGGL((gemm_f16x3_v4<BM, BN, false>), dim3((unsigned)(nbm * nbn)), dim3(256),
+                           0, st, a);
+}
+
 template <int BM, int BN, int KS>
 void launch_h3v3(const GemmH3Args& a, hipStream_t st) {
     const int nbm = (a.M + BM - 1) / BM, nbn = (a.N + BN - 1) / BN;
@@ -1002,9 +1203,15 @@ extern "C" int fgr_gemm_f16x3(const float* a, int64_t lda, const void* w_img, fl
         case 'q': launch_h3v3<128, 64, 1>(g, st); break;
         case 'r': launch_h3v3<128, 128, 1>(g, st); break;
         case 's': launch_h3v3<128, 64, 2>(g, st); break;
+        // v4 (W fragments straight to registers): t..x
+        case 't': launch_h3v4<64, 64>(g, st); break;
+        case 'u': launch_h3v4<64, 128>(g, st); break;
+        case 'v': launch_h3v4<128, 64>(g, st); break;
+        case 'w': launch_h3v4<128, 128>(g, st); break;
+        case 'x': launch_h3v4<64, 256>(g, st); break;
         default: break;
     }
-    if (cfg >= 'e' && cfg <= 's') {
+    if (cfg >= 'e' && cfg <= 'x') {
         FGR_CHECK_LAUNCH("gemm_f16x3_v2");
         return FGR_OK;
     }
