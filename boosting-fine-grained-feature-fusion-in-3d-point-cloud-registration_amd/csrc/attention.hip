@@ -733,3 +733,117 @@ extern "C" int fgr_attention_bf16x6(const float* q, int64_t ld_q, const float* k
     FGR_CHECK_LAUNCH("attn_bf16x6_kernel");
     return FGR_OK;
 }
+
+// ------------------------------------------------------------------------------------------
+// CorrespondenceDecoder.simple_attention (finegrained_regtr.py:328-363), the soft
+// correspondence head used with direct_regress_coor: False: one head of width d whose values
+// are the partner cloud's coordinates (3 columns),
+//   corr[q] = sum_j softmax_j((q . k_j) * scale) * xyz[j],
+// for every (layer, cloud) query segment in ONE launch (segment i attends to key segment
+// kv_seg[i]; the reference's key padding mask is the segment end). fp32 throughout: a block
+// holds 32 queries x 8 lanes (each lane a d/8 slice of the dot product, reduced over its 8
+// lanes with DPP), key rows are staged 32 at a time through LDS, and the softmax is online
+// (running max / sum, the 3 value sums rescaled on each new max).
+// ------------------------------------------------------------------------------------------
+namespace fgr {
+namespace {
+
+constexpr int kCaQ = 32;      // queries per block
+constexpr int kCaK = 32;      // keys per LDS tile
+
+template <int D>
+__global__ void __launch_bounds__(256)
+corr_attention_kernel(const float* __restrict__ q, int64_t ld_q, const float* __restrict__ k,
+                      int64_t ld_k, const float* __restrict__ xyz, float* __restrict__ out,
+                      const int64_t* __restrict__ q_off, const int64_t* __restrict__ kv_off,
+                      const int32_t* __restrict__ kv_seg, const int64_t* __restrict__ v_off,
+                      float scale) {
+    constexpr int DL = D / 8;                              // dims per lane
+    __shared__ float kt[kCaK][D + 4];
+    __shared__ float vt[kCaK][3];
+    const int seg = blockIdx.y;
+    const int64_t qb = q_off[seg], qe = q_off[seg + 1];
+    const int64_t q0 = qb + (int64_t)blockIdx.x * kCaQ;
+    if (q0 >= qe) return;                                  // block-uniform
+    const int ks = kv_seg[seg];
+    const int64_t kb = kv_off[ks], ke = kv_off[ks + 1];
+    const int64_t vb = v_off[ks];                          // value rows of key segment ks
+    const int tid = threadIdx.x, qi = tid >> 3, sl = tid & 7;
+    const int64_t row = q0 + qi;
+    const bool active = row < qe;
+    float qv[DL];
+#pragma unroll
+    for (int e = 0; e < DL; ++e) qv[e] = active ? q[row * ld_q + sl * DL + e] * scale : 0.f;
+    float m = -INFINITY, l = 0.f, a0 = 0.f, a1 = 0.f, a2 = 0.f;
+    for (int64_t j0 = kb; j0 < ke; j0 += kCaK) {
+        const int nk = (int)min((int64_t)kCaK, ke - j0);
+        __syncthreads();
+        for (int e = tid; e < kCaK * D; e += 256) {
+            const int r = e / D, cc = e - r * D;
+            kt[r][cc] = r < nk ? k[(j0 + r) * ld_k + cc] : 0.f;
+        }
+        if (tid < kCaK * 3) {
+            const int r = tid / 3, cc = tid - r * 3;
+            vt[r][cc] = r < nk ? xyz[(vb + (j0 - kb) + r) * 3 + cc] : 0.f;
+        }
+        __syncthreads();
+        for (int r = 0; r < nk; ++r) {
+            float s = 0.f;
+#pragma unroll
+            for (int e = 0; e < DL; ++e) s = fmaf(qv[e], kt[r][sl * DL + e], s);
+            s += dpp<0xB1>(s);                             // the 8 lanes of this query
+            s += dpp<0x4E>(s);
+            s += dpp<0x141>(s);
+            if (s > m) {
+                const float f = __expf(m - s);
+                l *= f; a0 *= f; a1 *= f; a2 *= f;
+                m = s;
+            }
+            const float p = __expf(s - m);
+            l += p;
+            a0 = fmaf(p, vt[r][0], a0);
+            a1 = fmaf(p, vt[r][1], a1);
+            a2 = fmaf(p, vt[r][2], a2);
+        }
+    }
+    if (active && sl == 0) {
+        const float inv = 1.0f / l;
+        out[row * 3 + 0] = a0 * inv;
+        out[row * 3 + 1] = a1 * inv;
+        out[row * 3 + 2] = a2 * inv;
+    }
+}
+
+}  // namespace
+}  // namespace fgr
+
+extern "C" int fgr_corr_attention(const float* q, int64_t ld_q, const float* k, int64_t ld_k,
+                                  const float* xyz, float* out, const int64_t* q_off,
+                                  const int64_t* kv_off, const int32_t* kv_seg,
+                                  const int64_t* v_off, int32_t n_seg, int32_t max_q_len,
+                                  int32_t d, float scale, void* stream) {
+    FGR_REQUIRE(q && k && xyz && out && q_off && kv_off && kv_seg && v_off && n_seg > 0 &&
+                    max_q_len >= 0 && ld_q >= d && ld_k >= d,
+                "fgr_corr_attention: bad arguments");
+    FGR_REQUIRE(d == 32 || d == 64 || d == 128 || d == 256 || d == 512,
+                "fgr_corr_attention: d %d unsupported (32, 64, 128, 256, 512)", d);
+    if (max_q_len == 0) return FGR_OK;
+    hipStream_t st = as_stream(stream);
+    TimedCall timed_(st);
+    const dim3 grid((unsigned)ceil_div(max_q_len, kCaQ), (unsigned)n_seg);
+#define FGR_CA(DD)                                                                              \
+    case DD:                                                                                    \
+        hipLaunchKernelGGL(corr_attention_kernel<DD>, grid, dim3(256), 0, st, q, ld_q, k, ld_k, \
+                           xyz, out, q_off, kv_off, kv_seg, v_off, scale);                      \
+        break;
+    switch (d) {
+        FGR_CA(32)
+        FGR_CA(64)
+        FGR_CA(128)
+        FGR_CA(256)
+        FGR_CA(512)
+    }
+#undef FGR_CA
+    FGR_CHECK_LAUNCH("corr_attention_kernel");
+    return FGR_OK;
+}

@@ -67,6 +67,8 @@ SIGNATURES = {
     'fgr_infonce_reduce': [_vp, _vp, _vp, _i32, _vp, _vp],
     'fgr_corr_loss': [_vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp],
     'fgr_se3_compare': [_vp, _vp, _i32, _i32, _vp, _vp, _vp],
+    'fgr_corr_attention': [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32,
+                           _f32, _vp],
     'fgr_procrustes': [_vp, _vp, _vp, _i64, _i64, _f32, _vp, _vp],
     'fgr_time_next_call': [_vp, _vp],
     'fgr_pair_pose': [_vp, _vp, _vp, _i64, _vp, _i32, _i32, _f32, _vp, _vp],

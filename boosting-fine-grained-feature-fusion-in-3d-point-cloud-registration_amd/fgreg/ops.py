@@ -566,6 +566,26 @@ def attention_flops(q_off, kv_off, kv_seg, d):
     return sum(4 * (qo[i + 1] - qo[i]) * (ko[ks[i] + 1] - ko[ks[i]]) * d for i in range(len(ks)))
 
 
+def corr_attention(q, k, xyz, q_off, kv_off, kv_seg, v_off, max_q_len, scale) -> torch.Tensor:
+    """CorrespondenceDecoder.simple_attention over packed (layer, cloud) segments
+    (fgr_corr_attention): -> (rows, 3) softmax-weighted partner coordinates."""
+    _dev(q, k, xyz, q_off, kv_off, kv_seg, v_off)
+    for t in (q, k):
+        assert t.dtype == torch.float32 and t.dim() == 2 and t.stride(1) == 1
+    xyz = _c(xyz, torch.float32)
+    d = q.shape[1]
+    assert k.shape[1] == d and xyz.dim() == 2 and xyz.shape[1] == 3
+    assert kv_seg.dtype == torch.int32 and kv_seg.numel() == q_off.numel() - 1
+    out = torch.empty((q.shape[0], 3), dtype=torch.float32, device=q.device)
+    t0 = _begin('attention')
+    _lib.check(_lib.load().fgr_corr_attention(
+        _ptr(q), q.stride(0), _ptr(k), k.stride(0), _ptr(xyz), _ptr(out), _ptr(q_off),
+        _ptr(kv_off), _ptr(kv_seg), _ptr(v_off), q_off.numel() - 1, int(max_q_len), d,
+        float(scale), _stream()), 'fgr_corr_attention')
+    _end('attention', t0, lambda: attention_flops(q_off, kv_off, kv_seg, d) // 2)
+    return out
+
+
 # ------------------------------------------------------------------------------------------
 # pose
 # ------------------------------------------------------------------------------------------

@@ -12,6 +12,7 @@ the forward is re-laid out for the GPU:
 The returned per-cloud lists are views into the packed tensors.
 """
 import logging
+import math
 import os
 import weakref
 from collections import OrderedDict
@@ -52,8 +53,10 @@ class CorrespondenceRegressor(nn.Module):
 
 class CorrespondenceDecoder(nn.Module):
     """finegrained_regtr.py:312-408 (direct_regress_coor: False): single-head attention
-    whose values are the other cloud's coordinates. Parameter layout of the reference;
-    evaluated with the fused attention kernel per layer (values zero-padded to width d)."""
+    whose values are the other cloud's coordinates. Parameter layout of the reference. The
+    q / k projections run once over all L layers' rows (f16x3 GEMMs) and the attention of
+    every (layer, cloud) segment is ONE fgr_corr_attention launch (values = the partner's 3
+    coordinates, no padding to width d)."""
 
     def __init__(self, d_embed, use_pos_emb, pos_embed=None, num_neighbors=0):
         super().__init__()
@@ -69,20 +72,15 @@ class CorrespondenceDecoder(nn.Module):
 
     def forward_packed(self, feats, xyz, pos, seg: Segments):
         L, N, d = feats.shape
-        f = feats + pos.unsqueeze(0) if self.use_pos_emb else feats
-        q = torch.addmm(self.q_proj.bias, f.reshape(L * N, d), self.q_proj.weight.t())
-        k = torch.addmm(self.k_proj.bias, f.reshape(L * N, d), self.k_proj.weight.t())
-        # one head of width d; the 3 value columns ride in a zero-padded width-d value matrix
-        vfull = torch.zeros((N, d), dtype=feats.dtype, device=feats.device)
-        vfull[:, :3] = xyz
-        corr = torch.empty((L, N, 3), dtype=feats.dtype, device=feats.device)
-        for l in range(L):
-            ql, kl = q[l * N:(l + 1) * N], k[l * N:(l + 1) * N]
-            o = ops.attention(ql, kl, vfull, seg.off, seg.off, seg.cross_seg, seg.max_len, 1)
-            corr[l] = o[:, :3]
-        logits = torch.addmm(self.conf_logits_decoder.bias, feats.reshape(L * N, d),
-                             self.conf_logits_decoder.weight.t())
-        return corr, logits.view(L, N, 1)
+        f = (feats + pos.unsqueeze(0) if self.use_pos_emb else feats).reshape(L * N, d)
+        q = linear(f, self.q_proj.weight, self.q_proj.bias)
+        k = linear(f, self.k_proj.weight, self.k_proj.bias)
+        q_off, kv_seg, v_off = seg.layer_tables
+        corr = ops.corr_attention(q, k, xyz, q_off, q_off, kv_seg, v_off, seg.max_len,
+                                  1.0 / math.sqrt(d))        # q_proj(query) / sqrt(D) (:344)
+        logits = linear(feats.reshape(L * N, d), self.conf_logits_decoder.weight,
+                        self.conf_logits_decoder.bias)
+        return corr.view(L, N, 3), logits.view(L, N, 1)
 
 
 class _LossParams(nn.Module):
@@ -162,7 +160,7 @@ class RegTR(nn.Module):
         if core is not None:
             both, feats, corr, logits, pose = core.run(meta)
         else:
-            both, feats, corr, logits, pose = self._core(meta, Segments(slens_c, xyz_c.device), B)
+            both, feats, corr, logits, pose = self._core(meta, self._segments(slens_c, xyz_c), B)
 
         offs = [0]
         for n in slens_c:
@@ -182,6 +180,11 @@ class RegTR(nn.Module):
             'pose': pose,
         }
         return outputs
+
+    def _segments(self, slens_c, xyz_c):
+        n_layers = (0 if isinstance(self.correspondence_decoder, CorrespondenceRegressor)
+                    else len(self.transformer_encoder.layers))
+        return Segments(slens_c, xyz_c.device, n_layers)
 
     def _core(self, meta, seg, B):
         """The post-preprocessing forward (finegrained_regtr.py:126-218): encoder, feat_proj,
@@ -236,7 +239,7 @@ class _CoreGraph:
         self.meta['stack_lengths'] = list(meta['stack_lengths'])
         self.meta['_host'] = {'lengths': meta['_host']['lengths'],
                               'offsets': [o.clone() for o in meta['_host']['offsets']]}
-        self.seg = Segments(slens_c, meta['points'][-1].device)
+        self.seg = model._segments(slens_c, meta['points'][-1])
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):                 # warm-up outside the capture

@@ -30,9 +30,10 @@ from .linear import linear
 
 
 class Segments:
-    """Device-side segment tables of one packed batch of 2B clouds."""
+    """Device-side segment tables of one packed batch of 2B clouds (built before any graph
+    capture: they are host -> device copies)."""
 
-    def __init__(self, lengths, device):
+    def __init__(self, lengths, device, n_layers=0):
         self.lengths = [int(n) for n in lengths]
         n = len(self.lengths)
         assert n % 2 == 0
@@ -42,6 +43,18 @@ class Segments:
         self.cross_seg = torch.tensor([(c + self.B) % n for c in range(n)], dtype=torch.int32,
                                       device=device)
         self.max_len = max(self.lengths) if n else 0
+        self.layer_tables = None
+        if n_layers:
+            # (layer, cloud) segments of the L stacked layer outputs (L * N rows): segment
+            # l * 2B + c attends to l * 2B + partner(c); value rows = the partner's xyz rows
+            N = sum(self.lengths)
+            q_off = [l * N + o for l in range(n_layers) for o in self.off.tolist()[:-1]]
+            q_off.append(n_layers * N)
+            kv_seg = [l * n + (c + self.B) % n for l in range(n_layers) for c in range(n)]
+            v_off = self.off.tolist()[:-1] * n_layers
+            self.layer_tables = (torch.tensor(q_off, dtype=torch.int64, device=device),
+                                 torch.tensor(kv_seg, dtype=torch.int32, device=device),
+                                 torch.tensor(v_off, dtype=torch.int64, device=device))
 
 
 class TransformerCrossEncoderLayer(nn.Module):

@@ -64,6 +64,7 @@ class RegTR(GenericRegModel):
     forward = fgreg.RegTR.forward
     _forward = fgreg.RegTR._forward
     _core = fgreg.RegTR._core
+    _segments = fgreg.RegTR._segments
 
     def _apply(self, fn, *args, **kwargs):
         fgreg.regtr._GRAPHS.pop(self, None)   # captured graphs point at the old weights

@@ -287,6 +287,17 @@ int fgr_attention_f16x3(const float* q, int64_t ld_q, const float* k, int64_t ld
                         int32_t max_kv_len, int32_t n_head, int32_t head_dim, float scale,
                         void* workspace, int64_t ws_bytes, void* stream);
 
+/* CorrespondenceDecoder.simple_attention (finegrained_regtr.py:328-363; the soft
+ * correspondence head of direct_regress_coor: False): single-head attention of width d whose
+ * values are the partner cloud's coordinates, for all (layer, cloud) segments in one launch:
+ *   out[r] = sum_j softmax_j(scale * q[r] . k[j]) * xyz[v_off[s'] + (j - kv_off[s'])]
+ * for query row r of segment s (rows q_off[s]..q_off[s+1]), s' = kv_seg[s], keys j in
+ * kv_off[s']..kv_off[s'+1]. fp32; d in {32, 64, 128, 256, 512}; out (rows, 3). */
+int fgr_corr_attention(const float* q, int64_t ld_q, const float* k, int64_t ld_k,
+                       const float* xyz, float* out, const int64_t* q_off, const int64_t* kv_off,
+                       const int32_t* kv_seg, const int64_t* v_off, int32_t n_seg,
+                       int32_t max_q_len, int32_t d, float scale, void* stream);
+
 /* ---- pose ----------------------------------------------------------------------------
  * fast_compute_rigid_transform (utils/se3_torch.py:226-273; threshold < 0 gives the
  * unthresholded compute_rigid_transform, :131-173) on n_batch independent problems

@@ -307,7 +307,23 @@ def forward(cfg, sd, src_xyz, tgt_xyz, meta=None, mode=geom.INDEX):
         return (x @ sd['correspondence_decoder.conf_logits_decoder.weight'].t()
                 + sd['correspondence_decoder.conf_logits_decoder.bias'])
 
-    s_corr, t_corr = corr_mlp(s_cond), corr_mlp(t_cond)
+    def simple_attention(query, key, value, kmask):                          # :328-363
+        q = (query @ sd['correspondence_decoder.q_proj.weight'].t()
+             + sd['correspondence_decoder.q_proj.bias']) / math.sqrt(query.shape[-1])
+        k = key @ sd['correspondence_decoder.k_proj.weight'].t() + sd['correspondence_decoder.k_proj.bias']
+        attn = torch.einsum('...qbd,...sbd->...bqs', q, k)
+        attn = attn.masked_fill(kmask[:, None, :], float('-inf'))
+        return torch.einsum('...bqs,...sbd->...qbd', torch.softmax(attn, -1), value)
+
+    if cfg.get('direct_regress_coor', False):
+        s_corr, t_corr = corr_mlp(s_cond), corr_mlp(t_cond)
+    else:                                       # CorrespondenceDecoder (:312-408), pos emb on
+        s2 = s_cond + spos if cfg.get('corr_decoder_has_pos_emb', True) else s_cond
+        t2 = t_cond + tpos if cfg.get('corr_decoder_has_pos_emb', True) else t_cond
+        sx, _ = _pad(src_xyz_c)
+        tx, _ = _pad(tgt_xyz_c)
+        s_corr = simple_attention(s2, t2, tx, tmask)
+        t_corr = simple_attention(t2, s2, sx, smask)
     s_ov, t_ov = conf(s_cond), conf(t_cond)
     ns, nt = slens_c[:B], slens_c[B:]
     out = {

@@ -425,6 +425,20 @@ def make_forward(fr, fk):
     save('forward_3dmatch_small', **pack_forward(model, meta, out, over, [s], [t], 4.0))
 
 
+def make_forward_decoder(fr, fk):
+    """(3) the soft-correspondence head: the reduced ModelNet config with
+    direct_regress_coor: False, i.e. the reference's CorrespondenceDecoder
+    (finegrained_regtr.py:312-408) instead of the regressor -- inactive in the shipped configs,
+    pinned here for API completeness."""
+    over = dict(SMALL_MODELNET, direct_regress_coor=False)
+    cfg = load_cfg('modelnet.yaml', **over)
+    pairs = [modelnet_like_pair(i + 5, n_raw=512) for i in range(2)]
+    src = [p[0] for p in pairs]
+    tgt = [p[1] for p in pairs]
+    model, meta, out = run_forward(fr, fk, cfg, src, tgt, seed=7)
+    save('forward_modelnet_decoder', **pack_forward(model, meta, out, over, src, tgt, 4.0))
+
+
 def make_loss(fr, fk):
     """Test-step tail fixture: the reference's own RegTR.compute_loss
     (finegrained_regtr.py:252-309) and GenericRegModel._compute_metrics
@@ -474,7 +488,11 @@ if __name__ == '__main__':
     if sys.argv[1:] == ['loss']:
         make_loss(fr, fk)
         sys.exit(0)
+    if sys.argv[1:] == ['decoder']:
+        make_forward_decoder(fr, fk)
+        sys.exit(0)
     make_geometry()
     make_modules(fr, fk)
     make_forward(fr, fk)
+    make_forward_decoder(fr, fk)
     make_loss(fr, fk)

@@ -63,7 +63,8 @@ def test_oracle_radius_boundary():
     assert np.array_equal(mine, g['nb'].astype(np.int64))
 
 
-@pytest.mark.parametrize('name', ['forward_modelnet_small', 'forward_3dmatch_small'])
+@pytest.mark.parametrize('name', ['forward_modelnet_small', 'forward_3dmatch_small',
+                                  'forward_modelnet_decoder'])
 def test_oracle_forward_matches_reference(name):
     cfg, sd, src, tgt, meta, d = forward_fixture(name)
     out = mo.forward(cfg, sd, src, tgt, meta=meta)
