@@ -1172,19 +1172,23 @@ extern "C" int fgr_gemm_f16x3(const float* a, int64_t lda, const void* w_img, fl
     TimedCall timed_(st);
     // tile BM x BN (activation rows x output channels); FGR_GEMM16_TILE overrides it for
     // tuning (a = 128x128, b = 64x128, c = 64x64, d = 128x64)
-    // Default per shape (measured on the forward's GEMMs, microbench.py tiles16): wide outputs
-    // take 64 x 128 tiles (double-buffered v2 when K >= 512), narrow ones 64 x 64 v2 stages of
-    // 64 k (double-buffered for long K at N <= 128), very tall ones 64 x 128.
+    // Default per shape (measured on the forward's GEMMs, tools/gemm_tiles.py,
+    // profiles/r02_gemm_tiles.txt): wide outputs take 64 x 128 tiles (v4 -- W fragments
+    // straight to registers -- for K >= 1024, double-buffered v2 for K >= 512), narrow ones the
+    // 64 x 64 v4 (K <= 1024) or v2 stages of 64 k (double-buffered for long K at N <= 128),
+    // very tall ones 64 x 128.
     const char* force = getenv("FGR_GEMM16_TILE");
     char cfg;
     if (force && force[0])
         cfg = force[0];
     else if (n >= 512)
-        cfg = k >= 512 ? 'k' : 'b';
+        cfg = k >= 1024 ? 'u' : (k >= 512 ? 'k' : 'b');
     else if ((int64_t)ceil_div(m, 64) * ceil_div(n, 64) >= 2048)
         cfg = 'b';
+    else if (n <= 128 && k >= 1024)
+        cfg = 'f';
     else
-        cfg = (n <= 128 && k >= 1024) ? 'f' : 'e';
+        cfg = k <= 1024 ? 't' : 'e';
     // v2 variants (BM x BN, KS k32-steps per stage, DBUF) for tuning: e..m
     switch (cfg) {
         case 'e': launch_h3v2<64, 64, 2, false>(g, st); break;
