@@ -6,7 +6,11 @@ Workloads (``--workload``; BASELINE.json configs):
             through the reference's exact crop test transforms (717 + 717 points per pair,
             fgreg.synthetic.modelnet_reference_pair -> fgreg.transforms), 8 pairs per GPU;
   3dmatch   (configs[2]) 20k + 20k-pt indoor fragment pairs, 1 pair per GPU;
-  raw2048   (SURVEY §8(d) D2 stress) the 2048-pt raw clouds fed directly, 8 pairs per GPU.
+  raw2048   (SURVEY §8(d) D2 stress) the 2048-pt raw clouds fed directly, 8 pairs per GPU;
+  3dlomatch (configs[4]) 20k + 20k-pt low-overlap (10-30%) fragment pairs, 1 pair per GPU, in
+            the bf16 compute mode (fgreg.set_precision('bf16'): bf16 MFMA GEMMs + attention).
+``--precision fp32|bf16`` overrides the workload's default compute mode (bf16 for 3dlomatch,
+fp32-accurate f16x3 otherwise).
 Full RegTR forward (preprocessing, KPConv/Res2Net encoder, 6-layer cross encoder,
 correspondence head, pose) with random-init weights of the reference architecture. One step =
 one forward over one batch already resident in HBM. N GPUs = N processes (torchrun), pairs
@@ -48,14 +52,18 @@ HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md, chip tabl
 FP32_MFMA_PEAK_TFLOPS = 157.3
 F16_MFMA_PEAK_TFLOPS = 2500.0    # fp16 / bf16 dense (MI355X_MICROARCH.md)
 # matrix-core products issued per fp32-equivalent product, by precision mode
-PIPE = {'f16x3': 3, 'bf16x6': 6, 'bf16x3': 3, 'fp32': 1}
+PIPE = {'f16x3': 3, 'bf16x6': 6, 'bf16x3': 3, 'bf16': 1, 'fp32': 1}
 PRECISION = {'f16x3': 'fp32-accurate scaled split fp16 (3 fp16 MFMA products per fp32 '
                       'product, <= ~3 * 2^-22 relative each)',
              'bf16x6': 'fp32-accurate split bf16 (6 bf16 MFMA products per fp32 product)',
              'bf16x3': 'split bf16, 3 products (~2^-17 relative)',
+             'bf16': 'bf16 (one bf16 MFMA product per product, fp32 accumulation, ~2^-9 '
+                     'relative per product)',
              'fp32': 'fp32 MFMA / hipBLASLt fp32'}
 DTYPE = {'f16x3': 'f32 (emulated on the fp16 MFMA pipe: f16x3 split products)',
          'bf16x6': 'f32 (emulated on the bf16 MFMA pipe: bf16x6 split products)',
+         'bf16': 'bf16 (bf16 MFMA GEMMs + attention; fp32 accumulation, storage, norms, '
+                 'geometry and pose)',
          'fp32': 'f32'}
 
 DATA = {
@@ -69,20 +77,29 @@ DATA = {
     '3dmatch': 'synthetic 3DMatch-like fragment pairs: 20k pts on the floor and walls of a room, '
                '5 mm noise, second fragment rotated <= 15 deg / moved <= 0.3 m '
                '(fgreg/synthetic.py), random-init weights of the reference 3DMatch architecture',
+    '3dlomatch': 'synthetic 3DLoMatch-like fragment pairs: 20k + 20k pts cut from opposite ends '
+                 'of a 6 x 3 x 2.5 m room with 10-30% shared extent, 5 mm noise, rotated <= 15 '
+                 'deg / moved <= 0.3 m (fgreg/synthetic.py lowoverlap_pair), random-init '
+                 'weights of the reference 3DMatch architecture',
 }
 METRIC = {
     'modelnet': 'point-cloud pairs/sec (forward) on ModelNet 2048-pt pairs',
     'raw2048': 'point-cloud pairs/sec (forward) on raw 2048+2048-pt pairs',
     '3dmatch': 'point-cloud pairs/sec (forward) on 3DMatch ~20k-pt fragment pairs',
+    '3dlomatch': 'point-cloud pairs/sec (forward) on 3DLoMatch low-overlap ~20k-pt fragment pairs',
 }
 WORKLOAD = {
     'modelnet': 'ModelNet40 2048-pt pairs, {P} pairs per GPU (BASELINE configs[1] at N=1, '
                 'configs[3] at N=8)',
     'raw2048': 'raw 2048+2048-pt pairs, {P} pairs per GPU (SURVEY D2 stress input)',
     '3dmatch': '3DMatch ~20k-pt fragment pairs, {P} pair(s) per GPU (BASELINE configs[2])',
+    '3dlomatch': '3DLoMatch low-overlap ~20k-pt fragment pairs, bf16 features/attention, {P} '
+                 'pair(s) per GPU (BASELINE configs[4])',
 }
-CFG_NAME = {'modelnet': 'modelnet', 'raw2048': 'modelnet', '3dmatch': '3dmatch'}
-PAIRS = {'modelnet': 8, 'raw2048': 8, '3dmatch': 1}
+CFG_NAME = {'modelnet': 'modelnet', 'raw2048': 'modelnet', '3dmatch': '3dmatch',
+            '3dlomatch': '3dlomatch'}
+PAIRS = {'modelnet': 8, 'raw2048': 8, '3dmatch': 1, '3dlomatch': 1}
+PRECISION_DEFAULT = {'3dlomatch': 'bf16'}
 # D4 byte / flop definitions per timed family
 OTHER = {
     'radius_search': ('hbm', '12 (Nq + Ns) + 8 Nq K bytes (int64 table)'),
@@ -102,7 +119,10 @@ def parse():
                    help='default 8 (modelnet, raw2048) / 1 (3dmatch)')
     p.add_argument('--workload', choices=tuple(METRIC), default='modelnet',
                    help='modelnet: BASELINE configs[1]/[3] (the headline line); 3dmatch: '
-                        'configs[2]; raw2048: the uncropped stress input')
+                        'configs[2]; 3dlomatch: configs[4] (bf16); raw2048: the uncropped '
+                        'stress input')
+    p.add_argument('--precision', choices=('fp32', 'bf16'), default=None,
+                   help='compute mode (default: bf16 for 3dlomatch, fp32-accurate otherwise)')
     p.add_argument('--cpu-seconds', type=float, default=10.0,
                    help='budget of the CPU baseline B=1 sample (0 disables it)')
     p.add_argument('--no-cpu-baseline', action='store_true')
@@ -158,6 +178,7 @@ def main():
         dist.init_process_group('nccl', device_id=dev)
 
     wl = args.workload
+    fgreg.set_precision(args.precision or PRECISION_DEFAULT.get(wl, 'fp32'))
     cfg = fgreg.config.get(CFG_NAME[wl])
     torch.manual_seed(0)
     np.random.seed(0)
@@ -243,6 +264,7 @@ def main():
                    'global_batch': P * world,
                    'points_per_cloud': int(np.mean([len(c) for c in src])),
                    'parallelism': f'pair-sharded dp{world}',
+                   'precision': fgreg.precision(),
                    'hip_graph': ('post-preprocessing forward replayed from the shape-keyed graph '
                                  'cache; preprocessing eager' if fregtr.GRAPHS else 'off')},
     }
@@ -322,15 +344,17 @@ def main():
 def write_gemm_table(path, rtimer, steps, step_ms, mode):
     """Per-shape table of the dense layers (bytes, flops, time and the binding
     roof per shape). bytes = the minimum operand traffic 4 M K (A) + 4 N K (f16x3 image:
-    2 terms x 2 B) + 4 M N (C), assuming every operand is read once."""
+    2 terms x 2 B; 2 N K for the single-term bf16 image) + 4 M N (C), assuming every operand
+    is read once."""
     pipe = PIPE.get(mode, 1)
+    wb = 2.0 if mode == 'bf16' else 4.0
     mfma_peak = (F16_MFMA_PEAK_TFLOPS / pipe) if mode != 'fp32' else FP32_MFMA_PEAK_TFLOPS
     rows = []
     for (m, n, k), (ms, cnt) in sorted(rtimer.per_label('gemm').items(),
                                        key=lambda kv: -kv[1][0]):
         us = ms * 1e3 / cnt
         flops = 2.0 * m * n * k
-        byt = 4.0 * m * k + 4.0 * n * k + 4.0 * m * n
+        byt = 4.0 * m * k + wb * n * k + 4.0 * m * n
         tf = flops / (us * 1e-6) / 1e12
         gbs = byt / (us * 1e-6) / 1e9
         t_mfma = flops / (mfma_peak * 1e12) * 1e6

@@ -46,6 +46,9 @@ SIGNATURES = {
     'fgr_attention_f16x3_workspace': [_i64, _i32, _i32, ctypes.POINTER(_sz)],
     'fgr_attention_f16x3': [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i32, _i32,
                             _i64, _i32, _i32, _i32, _i32, _f32, _vp, _i64, _vp],
+    'fgr_attention_bf16_workspace': [_i64, _i32, _i32, ctypes.POINTER(_sz)],
+    'fgr_attention_bf16': [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i32, _i32,
+                           _i64, _i32, _i32, _i32, _i32, _f32, _vp, _i64, _vp],
     'fgr_res2net_chain': [_vp, _i64, _i32, _i32, _vp, _vp, _vp, _i32, _vp, _i64, _vp],
     'fgr_res2net_chain6': [_vp, _i64, _i32, _i32, _vp, _vp, _vp, _i32, _vp, _i64, _vp],
     'fgr_res2net_chain_h3': [_vp, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _i32, _vp, _i64, _vp],
@@ -58,6 +61,9 @@ SIGNATURES = {
     'fgr_split_weights_h3_bytes': [_i32, _i32, ctypes.POINTER(_sz)],
     'fgr_split_weights_h3': [_vp, _i32, _i32, _i64, _i64, _vp, _vp],
     'fgr_gemm_f16x3': [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _vp],
+    'fgr_split_weights_bf16_bytes': [_i32, _i32, ctypes.POINTER(_sz)],
+    'fgr_split_weights_bf16': [_vp, _i32, _i32, _i64, _i64, _vp, _vp],
+    'fgr_gemm_bf16': [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _vp],
     'fgr_gemm_rows_f16x3': [_vp, _i64, _vp, _vp, _f32, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _i64,
                             _i32, _i32, _i32, _i32, _vp],
     'fgr_overlap_pool': [_vp, _i64, _vp, _i64, _i32, _vp, _vp],

@@ -70,7 +70,8 @@ THREEDMATCH = Cfg(_COMMON, dataset='3dmatch', num_layers=4, neighborhood_limits=
 
 
 def get(name, **overrides):
-    base = {'modelnet': MODELNET, '3dmatch': THREEDMATCH}[name]
+    # 3DLoMatch is the 3DMatch model on the low-overlap benchmark pairs (same conf/3dmatch.yaml)
+    base = {'modelnet': MODELNET, '3dmatch': THREEDMATCH, '3dlomatch': THREEDMATCH}[name]
     cfg = Cfg(copy.deepcopy(dict(base)))
     cfg.update(overrides)
     return cfg

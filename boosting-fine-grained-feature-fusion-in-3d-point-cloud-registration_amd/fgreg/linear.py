@@ -1,5 +1,5 @@
 """Dense layers of the forward (every Linear / KPConv-weight product goes through
-``linear()``) on the GPU, in one of four precision modes (``FGREG_GEMM`` or ``set_mode``):
+``linear()``) on the GPU, in one of five precision modes (``FGREG_GEMM`` or ``set_mode``):
 
 * ``f16x3`` (default): fgr_gemm_f16x3, the fp32-accurate scaled split-fp16 MFMA GEMM (operands
   scaled by per-row powers of two and split into two fp16 terms, three term products per
@@ -7,6 +7,9 @@
 * ``bf16x6``: fgr_gemm_bf16x6, the fp32-accurate split-bf16 MFMA GEMM (operands
   split exactly into three bf16 terms, six term products per step: ~2^-27 relative
   residual, below fp32's own rounding). Meets the 1e-4 parity bar on every fixture.
+* ``bf16``: fgr_gemm_bf16, one bf16 MFMA product per fp32 product (operands rounded to bf16,
+  fp32 accumulation: ~2^-9 relative per product) -- the BASELINE configs[4] (3DLoMatch)
+  compute mode, 3x fewer matrix-core cycles than f16x3; tolerance in DESIGN.md.
 * ``fp32``: PyTorch's fp32 GEMM (hipBLASLt, fp32 MFMA) -- the A/B baseline.
 * ``bf16x3``: fgr_gemm_bf16x3, two-term split (~2^-17 relative per product); faster, but
   the 3DMatch fixture's pose misses the 1e-4 bar (1.3e-4), so it is opt-in only.
@@ -36,7 +39,7 @@ ROWS = os.environ.get('FGREG_ROWS', '0')
 
 def set_mode(mode):
     global MODE
-    assert mode in ('fp32', 'bf16x3', 'bf16x6', 'f16x3')
+    assert mode in ('fp32', 'bf16x3', 'bf16x6', 'f16x3', 'bf16')
     MODE = mode
 
 
@@ -86,7 +89,23 @@ class SplitWeightH3:
         self.src, self.version, self.ptr = src, src._version, src.data_ptr()
 
 
+class SplitWeightBF:
+    """Single-term bf16 image of W (n, k) (fgr_split_weights_bf16)."""
+    __slots__ = ('img', 'n', 'k', 'src', 'version', 'ptr')
+
+    def __init__(self, w2: torch.Tensor, n, k, sn, sk, src: torch.Tensor):
+        L = _lib.load()
+        nb = _lib._sz(0)
+        _lib.check(L.fgr_split_weights_bf16_bytes(n, k, nb), 'fgr_split_weights_bf16_bytes')
+        self.img = torch.empty(nb.value, dtype=torch.uint8, device=w2.device)
+        _lib.check(L.fgr_split_weights_bf16(_ptr(w2), n, k, sn, sk, _ptr(self.img), _stream()),
+                   'fgr_split_weights_bf16')
+        self.n, self.k = n, k
+        self.src, self.version, self.ptr = src, src._version, src.data_ptr()
+
+
 _CACHE = {}
+_IMAGE = {3: SplitWeight3, 'h3': SplitWeightH3, 'bf16': SplitWeightBF}
 
 
 def _valid(ent, w):
@@ -95,12 +114,12 @@ def _valid(ent, w):
 
 
 def split_weight3(w: torch.Tensor, transpose=False, tag=None, kind=3, cache=True):
-    """Split image of w (kind 3: bf16x6, kind 'h3': f16x3), cached unless ``cache`` is False
+    """Split image of w (kind 3: bf16x6, kind 'h3': f16x3, 'bf16': single bf16), cached unless ``cache`` is False
     (operands that change every call, e.g. the loss's feature matrices)."""
     ck = (id(w), transpose, tag, kind)
     ent = _CACHE.get(ck) if cache else None
     if not _valid(ent, w):
-        cls = SplitWeight3 if kind == 3 else SplitWeightH3
+        cls = _IMAGE[kind]
         if transpose:                    # (K, Cin, Cout) as W[n = cout][k = K*Cin + cin]
             w2 = w.reshape(-1, w.shape[-1]).contiguous()
             ent = cls(w2, w2.shape[1], w2.shape[0], 1, w2.shape[1], w)
@@ -169,22 +188,22 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act=ACT_NONE, residual=N
     if fused:
         x = (ops.layernorm(x.contiguous(), ln.weight, ln.bias, ln.eps, add=add)
              if ln is not None else x + add)
-    if act == ACT_RELU_RES_LEAKY and MODE != 'f16x3':
+    if act == ACT_RELU_RES_LEAKY and MODE not in ('f16x3', 'bf16'):
         y = linear(x, w, bias, ACT_RELU, None, transpose, tag, cache=cache)
         y = F.leaky_relu(y + residual, 0.1)
         return out.copy_(y) if out is not None else y
-    if MODE in ('bf16x6', 'f16x3'):
+    if MODE in ('bf16x6', 'f16x3', 'bf16'):
         if not (x.stride(1) == 1 and (k % 8 != 0 or (x.stride(0) % 4 == 0
                                                      and x.data_ptr() % 16 == 0))):
             x = x.contiguous()                 # the split kernels need 16-B aligned rows
             if k % 8 == 0 and x.data_ptr() % 16 != 0:
                 x = x.clone()
-        h3 = MODE == 'f16x3'
-        sw = split_weight3(w, transpose, tag, 'h3' if h3 else 3, cache=cache)
+        kind = {'f16x3': 'h3', 'bf16x6': 3, 'bf16': 'bf16'}[MODE]
+        sw = split_weight3(w, transpose, tag, kind, cache=cache)
         m = x.shape[0]
         if out is None:
             out = torch.empty((m, n), dtype=torch.float32, device=x.device)
-        fn = _lib.load().fgr_gemm_f16x3 if h3 else _lib.load().fgr_gemm_bf16x6
+        fn = getattr(_lib.load(), 'fgr_gemm_' + MODE)
         t0 = _begin('gemm', (m, n, k))
         _lib.check(fn(_ptr(x), x.stride(0), _ptr(sw.img), _ptr(out), out.stride(0), _ptr(bias),
                       _ptr(residual), residual.stride(0) if residual is not None else 0, m, n, k,

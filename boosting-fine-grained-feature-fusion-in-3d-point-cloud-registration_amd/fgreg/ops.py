@@ -491,8 +491,9 @@ def res2net_chain(h, w, scale, w_frag, bias, x, cat, split6=False, w_scale=None)
 # ------------------------------------------------------------------------------------------
 # head_dim 32 / 64: fgr_attention_f16x3 (fp32-accurate scaled split-fp16 MFMA, default);
 # head_dim 32: fgr_attention_bf16x6 (split-bf16, 6 products); fgr_attention (fp32 MFMA)
-# otherwise.
-# FGREG_ATTN = f16x3 | bf16x6 | fp32 selects (a precision A/B switch, all on the GPU).
+# otherwise; 'bf16' (head_dim 32 / 64): fgr_attention_bf16, one bf16 product per fp32 product
+# (the BASELINE configs[4] compute mode, set together with linear.MODE by set_precision).
+# FGREG_ATTN = f16x3 | bf16x6 | bf16 | fp32 selects (a precision A/B switch, all on the GPU).
 ATTN_MODE = os.environ.get('FGREG_ATTN', 'f16x3')
 
 
@@ -517,7 +518,8 @@ def attention(q, k, v, q_off, kv_off, kv_seg, max_q_len, n_head, out=None,
     assert kv_seg.dtype == torch.int32 and kv_seg.numel() == n_seg
     max_kv_len = max_q_len if max_kv_len is None else max_kv_len
     L = _lib.load()
-    split = (((ATTN_MODE == 'f16x3' and dh in (32, 64)) or (ATTN_MODE == 'bf16x6' and dh == 32))
+    split = (((ATTN_MODE in ('f16x3', 'bf16') and dh in (32, 64))
+              or (ATTN_MODE == 'bf16x6' and dh == 32))
              and all(t.stride(0) % 4 == 0 and t.data_ptr() % 16 == 0 for t in (q, k, v, out)))
     t0 = _begin('attention')
     if split:

@@ -269,7 +269,8 @@ def _graph_for(model, meta, slens_c, B):
     if st is None or st['ver'] != ver:
         st = {'ver': ver, 'params': plist, 'seen': {}, 'graphs': OrderedDict()}
         _GRAPHS[model] = st
-    sig = (B, tuple(tuple(l) for l in meta['_host']['lengths']),
+    from . import linear as _lin
+    sig = (B, _lin.MODE, ops.ATTN_MODE, tuple(tuple(l) for l in meta['_host']['lengths']),
            tuple(tuple(t.shape) for t in meta['neighbors']), tuple(tuple(t.shape) for t in meta['pools']))
     g = st['graphs'].get(sig)
     if g is not None:

@@ -20,6 +20,9 @@ clouds of the same shape as the reference's test inputs:
   and four walls of a 3 x 3 x 2.5 m room with 5 mm noise; the second fragment
   is an independent sample under a random rotation <= 15 deg and translation
   <= 0.3 m.
+* ``lowoverlap_pair(i)`` -- a 3DLoMatch-like pair (BASELINE configs[4]): two fragments cut
+  from opposite ends of a 6 x 3 x 2.5 m room so that 10-30% of each fragment lies in the
+  shared strip, each sampled independently with N points, plus the same random motion.
 """
 import math
 
@@ -123,6 +126,40 @@ def indoor_like_pair(i, n_points=20000, max_rot_deg=15.0, max_trans=0.3):
     return src.astype(np.float32), tgt.astype(np.float32), pose.astype(np.float32)
 
 
+def _strip(rng, n, size, lo, hi):
+    """n room-surface samples with lo <= x < hi (rejection sampling)."""
+    out, have = [], 0
+    while have < n:
+        p = _room(rng, 3 * n, size)
+        p = p[(p[:, 0] >= lo) & (p[:, 0] < hi)]
+        out.append(p)
+        have += len(p)
+    return np.concatenate(out)[:n]
+
+
+def lowoverlap_pair(i, n_points=20000, overlap=(0.1, 0.3), max_rot_deg=15.0, max_trans=0.3):
+    """3DLoMatch-like pair: the target covers x in [-L/2, -L/2 + W) of an L = 6 m room, the
+    source x in [L/2 - W, L/2), W = L / (2 - f) so a fraction f in ``overlap`` of each
+    fragment's extent is shared. Returns (src (N,3) f32, tgt (N,3) f32, pose (3,4) f32:
+    src -> tgt, overlap fraction f)."""
+    rng = np.random.default_rng(104729 * (i + 1))
+    size = (6.0, 3.0, 2.5)
+    f = rng.uniform(*overlap)
+    L = size[0]
+    W = L / (2.0 - f)
+    tgt = _strip(rng, n_points, size, -L / 2, -L / 2 + W)
+    src0 = _strip(rng, n_points, size, L / 2 - W, L / 2)
+    axis = rng.normal(size=3)
+    axis /= np.linalg.norm(axis)
+    ang = np.deg2rad(rng.uniform(0, max_rot_deg))
+    K = np.array([[0, -axis[2], axis[1]], [axis[2], 0, -axis[0]], [-axis[1], axis[0], 0]])
+    R = np.eye(3) + math.sin(ang) * K + (1 - math.cos(ang)) * K @ K
+    t = rng.uniform(-max_trans, max_trans, 3)
+    src = (src0 - t) @ R
+    pose = np.concatenate([R, t[:, None]], 1)
+    return src.astype(np.float32), tgt.astype(np.float32), pose.astype(np.float32), f
+
+
 def modelnet_reference_pair(i, n_raw=2048):
     """A box-surface raw cloud (seeded by i) through the reference's exact ModelNet crop test
     pipeline (fgreg.transforms.modelnet_crop_test, sample index i): the bench workload.
@@ -155,9 +192,9 @@ def make_batch(kind, batch_size, start=0, **kw):
     """List-of-clouds batch in the reference's collate_pair layout (collate_functions.py:4-22).
     'modelnet': the reference's crop test pipeline on synthetic raw clouds; 'modelnet_like':
     the seeded approximation above; 'modelnet_raw': the uncropped 2048-pt stress input;
-    otherwise 3DMatch-like fragments."""
+    '3dlomatch': low-overlap fragments; otherwise 3DMatch-like fragments."""
     gen = {'modelnet': modelnet_reference_pair, 'modelnet_like': modelnet_like_pair,
-           'modelnet_raw': modelnet_raw_pair}.get(kind, indoor_like_pair)
+           'modelnet_raw': modelnet_raw_pair, '3dlomatch': lowoverlap_pair}.get(kind, indoor_like_pair)
     pairs = [gen(start + b, **kw) for b in range(batch_size)]
     return ([p[0] for p in pairs], [p[1] for p in pairs],
             np.stack([p[2] for p in pairs]).astype(np.float32))

@@ -58,8 +58,9 @@ const char* fgr_last_error(void);
 /* Opt-in instrumentation (bench.py's per-kernel rooflines; not part of the reference's
  * interface): arms two caller-created hipEvent_t for the NEXT timed entry point called on
  * this thread (fgr_kpconv_gather, fgr_attention*, fgr_gemm_bf16x6, fgr_gemm_f16x3,
- * fgr_gemm_rows_f16x3, fgr_grid_subsample_count / _fill, fgr_radius_search,
- * fgr_radius_grid_build, fgr_radius_search_grid, fgr_instnorm, fgr_layernorm, fgr_pair_pose). That call records `start_event` on its stream right before its
+ * fgr_gemm_bf16, fgr_gemm_rows_f16x3, fgr_grid_subsample_count / _fill, fgr_radius_search,
+ * fgr_radius_grid_build, fgr_radius_search_grid, fgr_instnorm, fgr_layernorm,
+ * fgr_pair_pose). That call records `start_event` on its stream right before its
  * first kernel launch and `end_event` after its last one, then disarms; (NULL, NULL)
  * disarms explicitly. Thread-local like the error string. */
 int fgr_time_next_call(void* start_event, void* end_event);
@@ -231,6 +232,22 @@ int fgr_gemm_f16x3(const float* a, int64_t lda, const void* w_img, float* c, int
                    const float* bias, const float* r, int64_t ldr, int32_t m, int32_t n,
                    int32_t k, int32_t act, void* stream);
 
+/* bf16 GEMM (the bf16 compute mode, BASELINE configs[4] -- 3DLoMatch with bf16 features),
+ * same contract as fgr_gemm_f16x3 (act includes FGR_ACT_RELU_RES_LEAKY):
+ *   C[m, n] = act(bf16(A[m, :]) . bf16(W[n, :]) + bias[n] (+ R[m, n]))
+ * One v_mfma_f32_16x16x32_bf16 product per product: operands rounded to bf16 (RNE, ~2^-9
+ * relative), fp32 accumulation, fp32 epilogue and output. Replaces the same nn.Linear /
+ * KPConv-weight products as fgr_gemm_f16x3 (finegrained_regtr.py:47-105 via its layers) at a
+ * third of the matrix-core work. W image built once by fgr_split_weights_bf16
+ * (fgr_split_weights_bf16_bytes() bytes, 16-B aligned; element (i, j) read from
+ * w[i * stride_n + j * stride_k]); A 16-B aligned with lda % 4 == 0 when k % 8 == 0. */
+int fgr_split_weights_bf16_bytes(int32_t n, int32_t k, size_t* bytes);
+int fgr_split_weights_bf16(const float* w, int32_t n, int32_t k, int64_t stride_n,
+                           int64_t stride_k, void* img, void* stream);
+int fgr_gemm_bf16(const float* a, int64_t lda, const void* w_img, float* c, int64_t ldc,
+                  const float* bias, const float* r, int64_t ldr, int32_t m, int32_t n, int32_t k,
+                  int32_t act, void* stream);
+
 /* Row-resident f16x3 GEMM for short contractions (k <= 256, k % 8 == 0) with the LayerNorm
  * (+ positional add) that produces its input fused into the row loads -- the transformer's
  * norm -> Linear pairs (transformers.py:193-238: norm1/2 + pos -> in_proj, norm3 -> linear1):
@@ -286,6 +303,20 @@ int fgr_attention_f16x3(const float* q, int64_t ld_q, const float* k, int64_t ld
                         int32_t n_seg, int32_t n_kv_seg, int64_t n_kv_rows, int32_t max_q_len,
                         int32_t max_kv_len, int32_t n_head, int32_t head_dim, float scale,
                         void* workspace, int64_t ws_bytes, void* stream);
+
+/* bf16 attention (the bf16 compute mode; head_dim 32 or 64), same semantics and arguments as
+ * fgr_attention_f16x3: q * scale * log2(e), K, V and the softmax numerators P rounded to bf16
+ * (RNE) where they enter v_mfma_f32_16x16x32_bf16; scores, the online softmax, accumulation
+ * and the output stay fp32. Workspace: fgr_attention_bf16_workspace() bytes (bf16 K/V
+ * images), 16-B aligned. */
+int fgr_attention_bf16_workspace(int64_t n_kv_rows, int32_t n_kv_seg, int32_t n_head,
+                                 size_t* bytes);
+int fgr_attention_bf16(const float* q, int64_t ld_q, const float* k, int64_t ld_k,
+                       const float* v, int64_t ld_v, float* o, int64_t ld_o,
+                       const int64_t* q_off, const int64_t* kv_off, const int32_t* kv_seg,
+                       int32_t n_seg, int32_t n_kv_seg, int64_t n_kv_rows, int32_t max_q_len,
+                       int32_t max_kv_len, int32_t n_head, int32_t head_dim, float scale,
+                       void* workspace, int64_t ws_bytes, void* stream);
 
 /* CorrespondenceDecoder.simple_attention (finegrained_regtr.py:328-363; the soft
  * correspondence head of direct_regress_coor: False): single-head attention of width d whose
