@@ -398,11 +398,14 @@ attn_bf16_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __restr
     }
 }
 
-int ksteps_bf(int k) { return (k + 31) / 32; }
+int ksteps_bf(int k) { return (k + 63) / 64 * 2; }     // even: g5 stages read 2 k32-steps
 size_t image_bytes_bf(int n, int k) { return (size_t)((n + 15) / 16) * ksteps_bf(k) * 64 * 16; }
 int64_t n_tiles_bf(int64_t n_kv_rows, int32_t n_kv_seg) { return n_kv_rows / 64 + n_kv_seg + 1; }
 
 }  // namespace
+bool gemm_g5_bf16(char cfg, const float* A, int64_t lda, const void* W, int ksteps, float* C,
+                  int64_t ldc, const float* bias, const float* R, int64_t ldr, int M, int N, int K,
+                  int act, int vec_out, hipStream_t st);
 }  // namespace fgr
 
 using namespace fgr;
@@ -441,6 +444,17 @@ extern "C" int fgr_gemm_bf16(const float* a, int64_t lda, const void* w_img, flo
                  vo ? 1 : 0};
     hipStream_t st = as_stream(stream);
     TimedCall timed_(st);
+    // narrow outputs with long contractions: the 64 x 64 LDS-DMA g5 ('I', gemm5.hip; measured
+    // 1.2-1.5x faster there), otherwise the register-staged kernel below (FGR_GEMM_BF16_TILE
+    // A..R forces a g5 variant, anything else this kernel)
+    const char* force = getenv("FGR_GEMM_BF16_TILE");
+    const char cfg = force && force[0] ? force[0] : (n <= 256 && k >= 1000 ? 'I' : 'z');
+    if (cfg >= 'A' && cfg <= 'R' && k % 8 == 0) {
+        gemm_g5_bf16(cfg, a, lda, w_img, ksteps_bf(k), c, ldc, bias, r, ldr, m, n, k, act,
+                     vo ? 1 : 0, st);
+        FGR_CHECK_LAUNCH("gemm_g5 (bf16)");
+        return FGR_OK;
+    }
     const int bm = 64, bn = n >= 128 ? 128 : 64;
     const unsigned nblk = (unsigned)(ceil_div(m, bm) * ceil_div(n, bn));
     if (bn == 128) {

@@ -32,6 +32,9 @@
 #include "common.h"
 
 namespace fgr {
+bool gemm_g5_f16x3(char cfg, const float* A, int64_t lda, const void* W, int ksteps,
+                   const float* wsc, float* C, int64_t ldc, const float* bias, const float* R,
+                   int64_t ldr, int M, int N, int K, int act, int vec_out, hipStream_t st);
 namespace {
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
@@ -1171,24 +1174,36 @@ extern "C" int fgr_gemm_f16x3(const float* a, int64_t lda, const void* w_img, fl
     hipStream_t st = as_stream(stream);
     TimedCall timed_(st);
     // tile BM x BN (activation rows x output channels); FGR_GEMM16_TILE overrides it for
-    // tuning (a = 128x128, b = 64x128, c = 64x64, d = 128x64)
-    // Default per shape (measured on the forward's GEMMs, tools/gemm_tiles.py,
-    // profiles/r02_gemm_tiles.txt): wide outputs take 64 x 128 tiles (v4 -- W fragments
-    // straight to registers -- for K >= 1024, double-buffered v2 for K >= 512), narrow ones the
-    // 64 x 64 v4 (K <= 1024) or v2 stages of 64 k (double-buffered for long K at N <= 128),
-    // very tall ones 64 x 128.
+    // tuning (a = 128x128, b = 64x128, c = 64x64, d = 128x64, e..x: v2-v4 variants, A..R: g5)
+    // Default per shape (measured on the forward's GEMMs with tools/gemm_tiles.py, device
+    // time from HIP-graph replays; profiles/r02_gemm_tiles*.txt): wide outputs take 64 x 128
+    // tiles (v4 -- W fragments straight to registers -- for K >= 1024, double-buffered v2
+    // for K >= 512), very tall ones 64 x 128; narrow outputs (N <= 256) and short row counts
+    // (M <= 4096, N <= 512) the 64 x 64 LDS-DMA g5 ('I') when K % 8 == 0, else the 64 x 64 v4.
     const char* force = getenv("FGR_GEMM16_TILE");
+    const bool g5ok = k % 8 == 0;
     char cfg;
     if (force && force[0])
         cfg = force[0];
+    else if (g5ok && m <= 4096 && n <= 512)
+        cfg = 'I';
     else if (n >= 512)
         cfg = k >= 1024 ? 'u' : (k >= 512 ? 'k' : 'b');
     else if ((int64_t)ceil_div(m, 64) * ceil_div(n, 64) >= 2048)
         cfg = 'b';
+    else if (g5ok && (k >= 512 || m <= 16384))
+        cfg = 'I';
     else if (n <= 128 && k >= 1024)
         cfg = 'f';
     else
         cfg = k <= 1024 ? 't' : 'e';
+    // g5 (gemm5.hip: LDS-DMA pipeline, A split after the read): A..J, K % 8 == 0 only
+    if (cfg >= 'A' && cfg <= 'R' && k % 8 == 0) {
+        gemm_g5_f16x3(cfg, a, lda, w_img, ksteps_h3(k), wsc, c, ldc, bias, r, ldr, m, n, k, act,
+                      vo ? 1 : 0, st);
+        FGR_CHECK_LAUNCH("gemm_g5");
+        return FGR_OK;
+    }
     // v2 variants (BM x BN, KS k32-steps per stage, DBUF) for tuning: e..m
     switch (cfg) {
         case 'e': launch_h3v2<64, 64, 2, false>(g, st); break;

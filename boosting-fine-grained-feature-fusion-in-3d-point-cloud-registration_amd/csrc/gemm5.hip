@@ -1,0 +1,416 @@
+// "g5" GEMM structure for the dense layers (f16x3 and bf16 modes):
+//
+//   C[M, N] = act(A[M, K] . W[N, K]^T + bias[N] (+ R[M, N]))
+//
+// Why a new structure. The forward's GEMMs are short and skinny (M ~ 2k-57k activation rows,
+// K = 64..3840, N = 64..1792); at K = 256 a block runs 8 k32-steps. The register-staged
+// kernels of gemm16.hip split A once per block into an LDS image and keep one k-step in
+// flight, so each k-step waits a full HBM / L2 round trip (~1-2 us under load) and the
+// ds_write_b128 pass of the split image (13 cycles per wave-instruction) sits on the
+// critical path: 9544 x 768 x 256 ran at 27 us where the fp16 pipe needs 4.5 us.
+//
+// Structure:
+//   * both operands travel global -> LDS by LDS-DMA (global_load_lds_dwordx4, no VGPR
+//     destination), S stages in flight (counted vmcnt, raw s_barrier: one barrier per stage),
+//     KS k32-steps per stage;
+//   * A is staged as raw fp32 (full 128-B row lines, 16-B chunks XOR-swizzled by row bits 1
+//     and 3 on the SOURCE address so the fragment reads are bank-conflict-free) and split
+//     into fp16 terms in registers after the read. Every wave owns BM / 4 distinct rows, so
+//     each A element is read and split exactly once per block (no LDS write pass at all);
+//   * W images (fgr_split_weights_h3 / _bf16) are DMA'd as they lie (already in fragment
+//     order) and shared by the 4 waves;
+//   * swapped orientation as gemm16.hip: W fragments are the MFMA A operand, activations the
+//     B operand, so each lane's 4 accumulators belong to ONE activation row -- the f16x3
+//     per-row scale (and its rare in-flight lowering) is lane-local, the epilogue stores
+//     16-B float4s.
+// f16x3 precision contract: identical to gemm16.hip (row scales chosen per 32-wide chunk
+// into [2^7, 2^8) and lowered only on overflow risk, two fp16 terms per operand, the three
+// significant products hh, hm, mh in fp32 accumulation).
+// Lane maps of v_mfma_f32_16x16x32_{f16,bf16} (lane l, g = l >> 4, c = l & 15): A[i = c][k =
+// 8g + e], B[k = 8g + e][j = c], C[i = 4g + r][j = c].
+#include "common.h"
+
+namespace fgr {
+namespace {
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
+
+constexpr int SH_UNSET = 0x3fff;
+
+// 16 zero bytes: the DMA source of A chunks past K (the LDS image gets exact zeros, so no
+// register-side masking is needed)
+__device__ __attribute__((aligned(16))) float g5_zero[4];
+
+struct G5Args {
+    const float* A; int64_t lda;
+    const u32x4* W; int ksteps;       // image [panel][kstep][term][g 4][16] x 16 B
+    const float* wsc;                 // f16x3: per n 2^-e_n (padded to 16); bf16: unused
+    float* C; int64_t ldc;
+    const float* bias;
+    const float* R; int64_t ldr;
+    int M, N, K, act, vec_out;
+};
+
+// chunk swizzle of A row r (16-B chunk q of a 128-B row line lands at q ^ swz(r)): rows
+// {0-3, 12-15} and {4-11} of one ds_read_b128 lane group hit 16 distinct 16-B bank slots
+__device__ __forceinline__ int swz(int r) { return (r >> 1) & 5; }
+
+// s_waitcnt vmcnt(n) (expcnt / lgkmcnt: no wait) -- gfx9 encoding
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    static_assert(N >= 0 && N < 64, "vmcnt");
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+// s_waitcnt vmcnt(n) lgkmcnt(0)
+template <int N>
+__device__ __forceinline__ void wait_vm_lgkm0() {
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4));
+}
+
+__device__ __forceinline__ float xg_max(float v) {        // max over lanes c, c^16, c^32, c^48
+    auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+    auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+
+__device__ __forceinline__ float finish5(float y, float b, float r, int act) {
+    if (act == FGR_ACT_RELU_RES_LEAKY) {
+        const float t = fmaxf(y + b, 0.f) + r;
+        return t > 0.f ? t : 0.1f * t;
+    }
+    const float t = y + b + r;
+    return act == FGR_ACT_RELU ? fmaxf(t, 0.f) : t;
+}
+
+// TERMS 2: f16x3 (W image with hi / lo terms + row scales); 1: bf16 (single-term image)
+template <int BM, int BN, int KS, int S, int TERMS, bool PIPE>
+__global__ void __launch_bounds__(256) gemm_g5(G5Args p) {
+    constexpr int WR = BM / 4;                 // rows per wave
+    constexpr int TM = WR / 16;                // 16-row fragments per wave
+    constexpr int TN = BN / 16;                // W panels per block
+    constexpr int A_UNITS = BM * 8 * KS;       // [ks][row][8 chunks] x 16 B
+    constexpr int W_PANEL = TERMS * 64;        // units of one (panel, kstep)
+    constexpr int W_UNITS = TN * KS * W_PANEL;
+    constexpr int ST = A_UNITS + W_UNITS;      // units per stage
+    constexpr int NP = ST / 64;                // DMA wave-instructions per stage
+    constexpr int A_PIECES = A_UNITS / 64;
+    static_assert(TM >= 1 && NP % 4 == 0, "tile");
+    constexpr int P = NP / 4;                  // per wave per stage
+    __shared__ u32x4 lds[S * ST];
+
+    const int nbm = (p.M + BM - 1) / BM, nbn = (p.N + BN - 1) / BN;
+    const int nwg = nbm * nbn;
+    int t = blockIdx.x;
+    {   // XCD-aware bijective remap: consecutive tiles (n fastest) on one XCD
+        const int q = nwg / 8, r = nwg % 8, x = t % 8, lo = t / 8;
+        t = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + lo;
+    }
+    const int bm = t / nbn, bn = t % nbn;
+    const int m0 = bm * BM, n0 = bn * BN;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably wave-uniform
+    const int g = lane >> 4, c = lane & 15;
+    const int npanel = (p.N + 15) / 16;
+    const int nk = (p.K + 32 * KS - 1) / (32 * KS);          // stages
+
+    // ---- DMA sources of this wave's P pieces (per stage: + stage * KS * 32 floats / units)
+    // (A_PIECES % 4 == 0: piece j of every wave is an A piece iff j < A_PIECES / 4)
+    static_assert(A_PIECES % 4 == 0, "A pieces");
+    const float* asrc[P];
+    int akoff[P];                                            // k offset of the chunk in its step
+    const u32x4* wsrc[P];
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+        const int q = wv + 4 * j;
+        if (j < A_PIECES / 4) {
+            const int ks = q / (BM / 8);
+            const int row = (q % (BM / 8)) * 8 + (lane >> 3);
+            const int ch = (lane & 7) ^ swz(row);
+            akoff[j] = ks * 32 + 4 * ch;
+            asrc[j] = p.A + (int64_t)min(m0 + row, p.M - 1) * p.lda + akoff[j];
+            wsrc[j] = nullptr;
+        } else {
+            const int w = q - A_PIECES;
+            const int panel = w / (KS * TERMS), rem = w % (KS * TERMS);
+            const int ks = rem / TERMS, term = rem % TERMS;
+            const int pg = min(n0 / 16 + panel, npanel - 1);
+            wsrc[j] = p.W + ((int64_t)pg * p.ksteps + ks) * W_PANEL + term * 64 + lane;
+            asrc[j] = nullptr;
+            akoff[j] = 0;
+        }
+    }
+    auto issue = [&](int s) {
+        lds_void* base = (lds_void*)(lds + (s % S) * ST);
+        const int k0 = s * KS * 32;
+        const bool full = k0 + KS * 32 <= p.K;                  // wave-uniform
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            const int q = wv + 4 * j;
+            lds_void* dst = (lds_void*)((__attribute__((address_space(3))) char*)base + q * 1024);
+            const void* src;
+            if (j < A_PIECES / 4) {
+                src = (full || k0 + akoff[j] < p.K) ? (const void*)(asrc[j] + k0)
+                                                    : (const void*)g5_zero;
+            } else {
+                src = wsrc[j] + (int64_t)s * KS * W_PANEL;
+            }
+            __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
+        }
+    };
+
+    f32x4 acc[TN][TM];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    int sh[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) sh[i] = SH_UNSET;
+
+    // fragment reads of one k32-step: W panels (A operand), this wave's raw fp32 rows
+    auto read_frags = [&](const u32x4* st, int ks, u32x4 (&ua)[TM][2], u32x4 (&wf)[TN][TERMS]) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int tt = 0; tt < TERMS; ++tt)
+                wf[j][tt] = st[A_UNITS + (j * KS + ks) * W_PANEL + tt * 64 + lane];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const int row = wv * WR + 16 * i + c;
+            const u32x4* ar = st + (ks * BM + row) * 8;
+            ua[i][0] = ar[(2 * g) ^ swz(row)];
+            ua[i][1] = ar[(2 * g + 1) ^ swz(row)];
+        }
+    };
+    // activation fragments (B operand): f16x3 row scaling + two-term split, or bf16 rounding
+    auto convert = [&](const u32x4 (&ua)[TM][2], u32x4 (&bh)[TM], u32x4 (&bl)[TM]) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const u32x4 u0 = ua[i][0], u1 = ua[i][1];
+            const float x[8] = {__uint_as_float(u0[0]), __uint_as_float(u0[1]),
+                                __uint_as_float(u0[2]), __uint_as_float(u0[3]),
+                                __uint_as_float(u1[0]), __uint_as_float(u1[1]),
+                                __uint_as_float(u1[2]), __uint_as_float(u1[3])};
+            if constexpr (TERMS == 2) {
+                float cm = fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3])));
+                cm = fmaxf(cm, fmaxf(fmaxf(fabsf(x[4]), fabsf(x[5])), fmaxf(fabsf(x[6]), fabsf(x[7]))));
+                cm = xg_max(cm);
+                const bool lower = cm > 0.f && __builtin_amdgcn_frexp_expf(cm) + sh[i] > 15;
+                if (__builtin_amdgcn_ballot_w64(lower)) {
+                    const int nsh = lower ? min(8 - __builtin_amdgcn_frexp_expf(cm), 127) : sh[i];
+                    const float f = (sh[i] == SH_UNSET || !lower) ? 1.f
+                                                                   : __builtin_ldexpf(1.f, nsh - sh[i]);
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) acc[j][i] *= f;
+                    sh[i] = nsh;
+                }
+                const float sc = __builtin_ldexpf(1.f, sh[i] == SH_UNSET ? 0 : sh[i]);
+                f16x8 h, m;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const float xs = x[e] * sc;
+                    const _Float16 hv = (_Float16)xs;
+                    h[e] = hv;
+                    m[e] = (_Float16)(xs - (float)hv);
+                }
+                bh[i] = __builtin_bit_cast(u32x4, h);
+                bl[i] = __builtin_bit_cast(u32x4, m);
+            } else {
+                bf16x8 h;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) h[e] = (__bf16)x[e];
+                bh[i] = __builtin_bit_cast(u32x4, h);
+                bl[i] = bh[i];
+            }
+        }
+    };
+    auto mma = [&](const u32x4 (&wf)[TN][TERMS], const u32x4 (&bh)[TM], const u32x4 (&bl)[TM]) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            if constexpr (TERMS == 2) {
+                const f16x8 wh = __builtin_bit_cast(f16x8, wf[j][0]);
+                const f16x8 wl = __builtin_bit_cast(f16x8, wf[j][1]);
+#pragma unroll
+                for (int i = 0; i < TM; ++i) {
+                    const f16x8 ah = __builtin_bit_cast(f16x8, bh[i]);
+                    const f16x8 al = __builtin_bit_cast(f16x8, bl[i]);
+                    acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, ah, acc[j][i], 0, 0, 0);
+                    acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, al, acc[j][i], 0, 0, 0);
+                    acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, ah, acc[j][i], 0, 0, 0);
+                }
+            } else {
+                const bf16x8 wb = __builtin_bit_cast(bf16x8, wf[j][0]);
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+                    acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                        wb, __builtin_bit_cast(bf16x8, bh[i]), acc[j][i], 0, 0, 0);
+            }
+        }
+    };
+
+#pragma unroll
+    for (int s = 0; s < S - 1; ++s)
+        if (s < nk) issue(s);
+
+    if constexpr (!PIPE) {
+        for (int s = 0; s < nk; ++s) {
+            // this wave's DMAs of stage s retired (later stages may stay in flight), then the
+            // barrier makes every wave's pieces visible and retires all reads of the buffer
+            // that is refilled next
+            const int ahead = min(S - 2, nk - 1 - s);
+            if constexpr (S >= 4) {
+                if (ahead >= 2) wait_vm_lgkm0<2 * P>();
+                else if (ahead == 1) wait_vm_lgkm0<P>();
+                else wait_vm_lgkm0<0>();
+            } else {
+                if (ahead >= 1) wait_vm_lgkm0<P>();
+                else wait_vm_lgkm0<0>();
+            }
+            __builtin_amdgcn_s_barrier();
+            if (s + S - 1 < nk) issue(s + S - 1);
+            const u32x4* st = lds + (s % S) * ST;
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                u32x4 ua[TM][2], wf[TN][TERMS], bh[TM], bl[TM];
+                read_frags(st, ks, ua, wf);
+                convert(ua, bh, bl);
+                mma(wf, bh, bl);
+            }
+        }
+    } else {
+        // software-pipelined (KS == 1): the fragments of stage s + 1 are read and split while
+        // the MFMAs of stage s run from registers
+        static_assert(KS == 1 && S >= 3, "pipelined g5: one k32-step per stage, >= 3 stages");
+        {
+            const int ahead = min(S - 2, nk - 1);
+            if (ahead >= 2) wait_vm_lgkm0<2 * P>();
+            else if (ahead == 1) wait_vm_lgkm0<P>();
+            else wait_vm_lgkm0<0>();
+        }
+        __builtin_amdgcn_s_barrier();
+        u32x4 ua[TM][2], wf[TN][TERMS], bh[TM], bl[TM];
+        read_frags(lds, 0, ua, wf);
+        convert(ua, bh, bl);
+        for (int s = 0; s < nk; ++s) {
+            if (s + 1 < nk) {
+                // stage s + 1 landed (stages up to s + S - 2 were issued; keep the later ones
+                // in flight); the barrier also retires every wave's reads of stage s
+                const int ahead = min(S - 3, nk - 2 - s);
+                if constexpr (S >= 5) {
+                    if (ahead >= 2) wait_vm_lgkm0<2 * P>();
+                    else if (ahead == 1) wait_vm_lgkm0<P>();
+                    else wait_vm_lgkm0<0>();
+                } else if constexpr (S == 4) {
+                    if (ahead >= 1) wait_vm_lgkm0<P>();
+                    else wait_vm_lgkm0<0>();
+                } else {
+                    wait_vm_lgkm0<0>();
+                }
+                __builtin_amdgcn_s_barrier();
+                if (s + S - 1 < nk) issue(s + S - 1);
+                u32x4 ua2[TM][2], wf2[TN][TERMS];
+                read_frags(lds + ((s + 1) % S) * ST, 0, ua2, wf2);
+                mma(wf, bh, bl);
+                convert(ua2, bh, bl);
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+#pragma unroll
+                    for (int tt = 0; tt < TERMS; ++tt) wf[j][tt] = wf2[j][tt];
+            } else {
+                mma(wf, bh, bl);
+            }
+        }
+    }
+
+    // epilogue: lane holds C[m = m0 + wv WR + 16i + c][n = n0 + 16j + 4g + r], r = 0..3
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        const int m = m0 + wv * WR + 16 * i + c;
+        if (m >= p.M) continue;
+        const float rs = TERMS == 2 ? __builtin_ldexpf(1.f, -sh[i]) : 1.f;   // 0: all-zero row
+        float* crow = p.C + (int64_t)m * p.ldc;
+        const float* rrow = p.R ? p.R + (int64_t)m * p.ldr : nullptr;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int n = n0 + 16 * j + 4 * g;
+            if (n >= p.N) continue;
+            float4 ws = make_float4(1.f, 1.f, 1.f, 1.f);
+            if constexpr (TERMS == 2) ws = *reinterpret_cast<const float4*>(p.wsc + n);
+            const float y[4] = {acc[j][i][0] * rs * ws.x, acc[j][i][1] * rs * ws.y,
+                                acc[j][i][2] * rs * ws.z, acc[j][i][3] * rs * ws.w};
+            if (p.vec_out && n + 3 < p.N) {
+                float4 bb = make_float4(0.f, 0.f, 0.f, 0.f), rr = bb;
+                if (p.bias) bb = *reinterpret_cast<const float4*>(p.bias + n);
+                if (rrow) rr = *reinterpret_cast<const float4*>(rrow + n);
+                *reinterpret_cast<float4*>(crow + n) =
+                    make_float4(finish5(y[0], bb.x, rr.x, p.act), finish5(y[1], bb.y, rr.y, p.act),
+                                finish5(y[2], bb.z, rr.z, p.act), finish5(y[3], bb.w, rr.w, p.act));
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    if (n + e >= p.N) break;
+                    crow[n + e] = finish5(y[e], p.bias ? p.bias[n + e] : 0.f,
+                                          rrow ? rrow[n + e] : 0.f, p.act);
+                }
+            }
+        }
+    }
+}
+
+template <int BM, int BN, int KS, int S, int TERMS, bool PIPE = false>
+void launch_g5(const G5Args& a, hipStream_t st) {
+    const int nbm = (a.M + BM - 1) / BM, nbn = (a.N + BN - 1) / BN;
+    hipLaunchKernelGGL((gemm_g5<BM, BN, KS, S, TERMS, PIPE>), dim3((unsigned)(nbm * nbn)),
+                       dim3(256), 0, st, a);
+}
+
+template <int TERMS>
+bool dispatch_g5(char cfg, const G5Args& a, hipStream_t st) {
+    switch (cfg) {
+        case 'A': launch_g5<64, 64, 1, 4, TERMS>(a, st); break;
+        case 'B': launch_g5<64, 128, 1, 3, TERMS>(a, st); break;
+        case 'C': launch_g5<64, 64, 2, 3, TERMS>(a, st); break;
+        case 'D': launch_g5<64, 128, 2, 3, TERMS>(a, st); break;
+        case 'E': launch_g5<128, 64, 1, 4, TERMS>(a, st); break;
+        case 'F': launch_g5<128, 128, 1, 3, TERMS>(a, st); break;
+        case 'G': launch_g5<64, 256, 1, 3, TERMS>(a, st); break;
+        case 'H': launch_g5<128, 128, 2, 2, TERMS>(a, st); break;
+        case 'I': launch_g5<64, 64, 1, 3, TERMS>(a, st); break;
+        case 'J': launch_g5<128, 64, 2, 3, TERMS>(a, st); break;
+        // software-pipelined: K..R
+        case 'K': launch_g5<64, 64, 1, 4, TERMS, true>(a, st); break;
+        case 'L': launch_g5<64, 128, 1, 4, TERMS, true>(a, st); break;
+        case 'M': launch_g5<64, 64, 1, 5, TERMS, true>(a, st); break;
+        case 'N': launch_g5<128, 64, 1, 4, TERMS, true>(a, st); break;
+        case 'O': launch_g5<128, 128, 1, 3, TERMS, true>(a, st); break;
+        case 'P': launch_g5<64, 256, 1, 3, TERMS, true>(a, st); break;
+        case 'Q': launch_g5<64, 128, 1, 3, TERMS, true>(a, st); break;
+        case 'R': launch_g5<128, 128, 1, 4, TERMS, true>(a, st); break;
+        default: return false;
+    }
+    return true;
+}
+
+}  // namespace
+
+// A 16-B aligned with lda % 4 == 0 and K % 8 == 0 (checked by the callers).
+bool gemm_g5_f16x3(char cfg, const float* A, int64_t lda, const void* W, int ksteps,
+                   const float* wsc, float* C, int64_t ldc, const float* bias, const float* R,
+                   int64_t ldr, int M, int N, int K, int act, int vec_out, hipStream_t st) {
+    G5Args a{A, lda, (const u32x4*)W, ksteps, wsc, C, ldc, bias, R, ldr, M, N, K, act, vec_out};
+    return dispatch_g5<2>(cfg, a, st);
+}
+
+bool gemm_g5_bf16(char cfg, const float* A, int64_t lda, const void* W, int ksteps, float* C,
+                  int64_t ldc, const float* bias, const float* R, int64_t ldr, int M, int N, int K,
+                  int act, int vec_out, hipStream_t st) {
+    G5Args a{A, lda, (const u32x4*)W, ksteps, nullptr, C, ldc, bias, R, ldr, M, N, K, act, vec_out};
+    return dispatch_g5<1>(cfg, a, st);
+}
+
+}  // namespace fgr

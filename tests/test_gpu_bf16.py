@@ -45,14 +45,17 @@ def bf16_mode():
     fgreg.set_precision(old)
 
 
+@pytest.mark.parametrize('tile', ['', 'z', 'A', 'B', 'I', 'K', 'O', 'D'])
 @pytest.mark.parametrize('m,n,k', [(11472, 128, 1920), (9200, 1024, 2048), (1000, 3, 256),
                                    (333, 896, 128), (64, 256, 36), (5000, 768, 256), (1, 64, 7),
                                    (4097, 130, 1000)])
-def test_gemm_bf16_rounding_points(gpu, bf16_mode, m, n, k):
+def test_gemm_bf16_rounding_points(gpu, bf16_mode, m, n, k, tile, monkeypatch):
     """fgr_gemm_bf16 = fp32 accumulation of bf16(A) bf16(W) products: vs the same rounded
     operands in fp64 within 1e-5 (accumulation order only); vs exact fp64 at bf16 level; bias /
-    ReLU / residual / fused-leaky epilogues, strided A, the KPConv weight layout."""
+    ReLU / residual / fused-leaky epilogues, strided A, the KPConv weight layout; every kernel
+    variant (FGR_GEMM_BF16_TILE: '' default dispatch, 'z' register-staged, A..R the LDS-DMA g5)."""
     from fgreg import linear as fl
+    monkeypatch.setenv('FGR_GEMM_BF16_TILE', tile)
     from fgreg import ops
     g = torch.Generator().manual_seed(m + n + k)
     x = torch.randn(m, k + 4, generator=g)[:, :k]

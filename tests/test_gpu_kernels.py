@@ -331,11 +331,13 @@ def test_gemm_split_vs_fp64(gpu, m, n, k, mode, tol):
         fl.set_mode(old)
 
 
-def test_gemm_f16x3_dynamic_range(gpu):
-    """f16x3 row scaling under adversarial magnitudes: rows at 1e-15 .. 1e15 (far outside
-    fp16's range), all-zero rows, rows whose first k chunks are zero, rows that grow by
+@pytest.mark.parametrize('tile', ['', 'b', 'I', 'K', 'O'])
+def test_gemm_f16x3_dynamic_range(gpu, tile, monkeypatch):
+    """f16x3 row scaling (tile: '' the default dispatch, else FGR_GEMM16_TILE) under
+    adversarial magnitudes: rows at 1e-15 .. 1e15 (far outside fp16's range), all-zero rows, rows whose first k chunks are zero, rows that grow by
     2^40 along k (forces the in-flight rescale of partial sums) and a weight matrix with
     rows at 1e-10 / 1e10 (outputs stay inside fp32's range). Every output row must match fp64 to 2e-6 of its own scale."""
+    monkeypatch.setenv('FGR_GEMM16_TILE', tile)
     from fgreg import linear as fl
     g = torch.Generator().manual_seed(7)
     m, n, k = 700, 96, 320
@@ -368,17 +370,19 @@ def test_gemm_f16x3_dynamic_range(gpu):
     del ref
 
 
-@pytest.mark.parametrize('tile', list('abcdefghijklm'))
+@pytest.mark.parametrize('tile', list('abcdefghijklmnopqrstuvwx') + list('ABCDEFGHIJKLMNOPQR'))
 def test_gemm_f16x3_tiles(gpu, tile, monkeypatch):
-    """Every f16x3 tile / pipeline variant (FGR_GEMM16_TILE) at fp32 accuracy on ragged
-    shapes (M, N, K not multiples of the tiles; K % 64 != 0, odd k32-step count; N = 3)."""
+    """Every f16x3 tile / pipeline variant (FGR_GEMM16_TILE; A..R: the LDS-DMA g5 kernels of
+    gemm5.hip) at fp32 accuracy on ragged shapes (M, N, K not multiples of the tiles; K % 64
+    != 0, odd k32-step count; N = 3; K % 8 != 0 takes the register-staged fallback)."""
     from fgreg import linear as fl
     monkeypatch.setenv('FGR_GEMM16_TILE', tile)
     g = torch.Generator().manual_seed(11)
     old = fl.MODE
     try:
         fl.set_mode('f16x3')
-        for m, n, k in ((1000, 200, 1000), (333, 3, 96), (130, 520, 40)):
+        for m, n, k in ((1000, 200, 1000), (333, 3, 96), (130, 520, 40), (77, 50, 36),
+                        (4099, 272, 264)):
             x = torch.randn(m, k, generator=g)
             w = torch.randn(n, k, generator=g) / math.sqrt(k)
             b = torch.randn(n, generator=g)

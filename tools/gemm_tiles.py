@@ -1,6 +1,7 @@
 """GEMM tile sweep (development tool, GPU): times fgr_gemm_f16x3 per tile configuration
 (FGR_GEMM16_TILE) on the forward's shapes and checks every variant against an fp64 product.
-usage: python tools/gemm_tiles.py [configs] > gpurun_out/gemm_tiles.txt"""
+usage: python tools/gemm_tiles.py [configs] [bf16] > gpurun_out/gemm_tiles.txt
+(bf16: fgr_gemm_bf16 with FGR_GEMM_BF16_TILE, checked against bf16-rounded operands)"""
 import os
 import sys
 
@@ -13,44 +14,59 @@ import fgreg.linear as lin  # noqa: E402
 SHAPES = [(9544, 768, 256), (9544, 1024, 2048), (9544, 256, 1024), (9544, 256, 3840),
           (9544, 256, 256), (9544, 1024, 256), (11472, 512, 1024), (11472, 128, 1920),
           (9544, 1792, 256), (57264, 256, 256), (11472, 896, 128), (2120, 1536, 512),
-          (2120, 512, 1024), (2120, 512, 512), (26778, 256, 512), (40000, 128, 256)]
+          (2120, 512, 1024), (2120, 512, 512), (26778, 256, 512), (40000, 128, 256),
+          (9543, 130, 1000), (333, 896, 128)]
 
 
-def timeit(fn, iters=30):
+def timeit(fn, iters=20):
+    """Device time per call: `iters` calls captured in one HIP graph (the forward replays its
+    GEMMs from a graph too), so host launch overhead does not enter small shapes."""
     for _ in range(3):
         fn()
     torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        for _ in range(iters):
+            fn()
+    graph.replay()
+    torch.cuda.synchronize()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
-    for _ in range(iters):
-        fn()
+    for _ in range(3):
+        graph.replay()
     b.record()
     torch.cuda.synchronize()
-    return a.elapsed_time(b) / iters * 1e3
+    return a.elapsed_time(b) / (3 * iters) * 1e3
 
 
 def main():
-    cfgs = sys.argv[1] if len(sys.argv) > 1 else 'befknopqrs'
+    cfgs = sys.argv[1] if len(sys.argv) > 1 else 'btukABCDEFGHIJ'
+    bf = len(sys.argv) > 2 and sys.argv[2] == 'bf16'
+    env = 'FGR_GEMM_BF16_TILE' if bf else 'FGR_GEMM16_TILE'
     dev = torch.device('cuda:0')
-    lin.set_mode('f16x3')
+    lin.set_mode('bf16' if bf else 'f16x3')
     g = torch.Generator(device=dev).manual_seed(0)
     for (M, N, K) in SHAPES:
         x = torch.randn(M, K, device=dev, generator=g)
         w = torch.randn(N, K, device=dev, generator=g) * 0.05
-        ref = (x.double() @ w.double().t())
+        if bf:
+            ref = x.bfloat16().double() @ w.bfloat16().double().t()
+        else:
+            ref = (x.double() @ w.double().t())
         line = f'M={M:6d} N={N:5d} K={K:5d}'
         best = None
         for t in cfgs:
-            os.environ['FGR_GEMM16_TILE'] = t
-            y = lin.linear(x, w)
+            os.environ[env] = t
+            out = torch.empty(M, N, device=dev)
+            y = lin.linear(x, w, out=out)
             err = float((y.double() - ref).abs().max() / ref.abs().max())
-            us = timeit(lambda: lin.linear(x, w))
+            us = timeit(lambda: lin.linear(x, w, out=out))
             tf = 2 * M * N * K / us / 1e6
             line += f' | {t} {us:6.1f}us {tf:5.0f}TF{"" if err < 1e-5 else " ERR%.1e" % err}'
             if best is None or us < best[1]:
                 best = (t, us)
-        os.environ['FGR_GEMM16_TILE'] = ''
-        us0 = timeit(lambda: lin.linear(x, w))
+        os.environ[env] = ''
+        us0 = timeit(lambda: lin.linear(x, w, out=out))
         print(line + f' || default {us0:6.1f}us best {best[0]}', flush=True)
 
 
