@@ -167,6 +167,89 @@ kpconv_gather_wide(const float* __restrict__ q, const float* __restrict__ s, int
     if (lane == 0) nnorm[qi] = (float)(n_pos > 1 ? n_pos : 1);
 }
 
+// cin = 16 / 32 (3DMatch's first bottleneck convs run at 128 / 4 = 32 channels): one wave per
+// query, lanes = (kernel-point group kg, channel quad): every lane owns 4 channels (one 16-B
+// load per neighbour row; the wave reads each row as one 64- / 128-B line) of KPL kernel
+// points k = kg, kg + KG, .... Valid neighbours are compacted by ballot and their K kernel-
+// point influences computed once into LDS (as kpconv_gather_wide); the row-sum positivity
+// of the normaliser is a DPP reduction over the QUADS lanes that hold the row.
+template <int QUADS, int KPL>
+__global__ void __launch_bounds__(256)
+kpconv_gather_quads(const float* __restrict__ q, const float* __restrict__ s, int64_t nq,
+                    int64_t ns, const int64_t* __restrict__ idx, int width,
+                    const float* __restrict__ x, const float* __restrict__ kp_g, int n_kp,
+                    float inv_extent, float* __restrict__ wf, float* __restrict__ nnorm) {
+    constexpr int CIN = 4 * QUADS, KG = 64 / QUADS, U = 4, KW = 16;
+    static_assert(KG * KPL >= KW, "kernel points per lane");
+    __shared__ float w_lds[4][64 + U][KW];
+    __shared__ int nb_lds[4][64 + U];
+    __shared__ float kp[3 * kMaxKp];
+    const int wv = threadIdx.x / 64, lane = threadIdx.x % 64;
+    const int quad = lane % QUADS, kg = lane / QUADS;
+    for (int i = threadIdx.x; i < 3 * n_kp; i += blockDim.x) kp[i] = kp_g[i];
+    __syncthreads();
+    const int64_t qi = (int64_t)blockIdx.x * 4 + wv;
+    if (qi >= nq) return;
+    const float qx = q[3 * qi], qy = q[3 * qi + 1], qz = q[3 * qi + 2];
+    float4 acc[KPL];
+#pragma unroll
+    for (int j = 0; j < KPL; ++j) acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    int n_pos = 0;
+    const int64_t* row = idx + qi * width;
+    for (int h0 = 0; h0 < width; h0 += 64) {
+        const int h = h0 + lane;
+        const int64_t id = h < width ? row[h] : ns;
+        const bool valid = id >= 0 && id < ns;
+        const unsigned long long m = __ballot(valid);
+        const int v = __popcll(m);
+        if (v == 0) continue;
+        if (valid) nb_lds[wv][__popcll(m & ((1ull << lane) - 1ull))] = (int)id;
+        if (lane < U) nb_lds[wv][v + lane] = 0;        // pad rows: weight 0, row 0
+        __builtin_amdgcn_wave_barrier();
+        for (int t = lane; t < (v + U) * KW; t += 64) {
+            const int hh = t / KW, k = t % KW;
+            float w = 0.f;
+            if (hh < v && k < n_kp) {
+                const int sid = nb_lds[wv][hh];
+                const float nx = s[3 * sid] - qx, ny = s[3 * sid + 1] - qy, nz = s[3 * sid + 2] - qz;
+                w = kp_weight(nx, ny, nz, kp, k, inv_extent);
+            }
+            w_lds[wv][hh][k] = w;
+        }
+        __builtin_amdgcn_wave_barrier();
+        for (int hh = 0; hh < v; hh += U) {
+            float4 xv[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                xv[u] = *reinterpret_cast<const float4*>(x + (int64_t)nb_lds[wv][hh + u] * CIN + 4 * quad);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                float rs = (xv[u].x + xv[u].y) + (xv[u].z + xv[u].w);
+                rs += dpp<0xB1>(rs);                     // quad_perm xor 1
+                rs += dpp<0x4E>(rs);                     // quad_perm xor 2
+                if constexpr (QUADS == 8) rs += dpp<0x141>(rs);   // row_half_mirror: 8 lanes
+                n_pos += (hh + u < v && rs > 0.f) ? 1 : 0;
+#pragma unroll
+                for (int j = 0; j < KPL; ++j) {
+                    const float w = w_lds[wv][hh + u][kg + KG * j];
+                    acc[j].x = fmaf(w, xv[u].x, acc[j].x);
+                    acc[j].y = fmaf(w, xv[u].y, acc[j].y);
+                    acc[j].z = fmaf(w, xv[u].z, acc[j].z);
+                    acc[j].w = fmaf(w, xv[u].w, acc[j].w);
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    float* out = wf + qi * (int64_t)n_kp * CIN + 4 * quad;
+#pragma unroll
+    for (int j = 0; j < KPL; ++j) {
+        const int k = kg + KG * j;
+        if (k < n_kp) *reinterpret_cast<float4*>(out + (int64_t)k * CIN) = acc[j];
+    }
+    if (lane == 0) nnorm[qi] = (float)(n_pos > 1 ? n_pos : 1);
+}
+
 // One thread per (query, kernel point); cin <= 64 (narrow layers, incl. the cin = 1 stem).
 template <int CMAX>
 __global__ void __launch_bounds__(256)
@@ -402,6 +485,16 @@ extern "C" int fgr_kpconv_gather(const float* q, const float* s, int64_t nq, int
                                    width, x, kp, n_kp, inv_ext, wf, nnorm);
             else
                 hipLaunchKernelGGL(kpconv_gather_c1<kMaxKp>, grid, dim3(256), 0, st, q, s, nq, ns,
+                                   idx, width, x, kp, n_kp, inv_ext, wf, nnorm);
+        } else if ((cin == 16 || cin == 32) && n_kp <= 16 &&
+                   (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
+                   (reinterpret_cast<uintptr_t>(wf) & 15) == 0) {
+            const dim3 grid((unsigned)ceil_div(nq, 4));
+            if (cin == 32)
+                hipLaunchKernelGGL((kpconv_gather_quads<8, 2>), grid, dim3(256), 0, st, q, s, nq, ns,
+                                   idx, width, x, kp, n_kp, inv_ext, wf, nnorm);
+            else
+                hipLaunchKernelGGL((kpconv_gather_quads<4, 1>), grid, dim3(256), 0, st, q, s, nq, ns,
                                    idx, width, x, kp, n_kp, inv_ext, wf, nnorm);
         } else if (cin <= 8) launch_narrow<8>(q, s, nq, ns, idx, width, x, cin, kp, n_kp, inv_ext, wf, nnorm, st);
         else if (cin <= 16) launch_narrow<16>(q, s, nq, ns, idx, width, x, cin, kp, n_kp, inv_ext, wf, nnorm, st);

@@ -40,10 +40,12 @@ def test_kpconv_block_vs_reference(gpu):
 @pytest.mark.parametrize('cin,H,prepass', [(1, 50, '0'), (1, 7, '0'), (3, 50, '0'), (16, 50, '0'),
                                            (32, 50, '0'), (64, 50, '0'), (128, 50, '0'),
                                            (256, 50, '0'), (128, 50, '1'), (256, 70, '1'),
-                                           (64, 130, '0')])
+                                           (64, 130, '0'), (32, 130, '0'), (32, 5, '0'),
+                                           (16, 70, '0')])
 def test_kpconv_gather_vs_torch(gpu, cin, H, prepass, monkeypatch):
     """Gather-weight stage vs the fp32 torch restatement (all channel widths in the configs;
-    the cin = 1 stem kernel; wide kernels with the inline and the pre-pass normaliser)."""
+    the cin = 1 stem kernel; the quad-lane kernel of cin 16 / 32 incl. widths past one
+    64-neighbour chunk; wide kernels with the inline and the pre-pass normaliser)."""
     import fgreg.ops as ops
     monkeypatch.setenv('FGR_GATHER_PREPASS', prepass)
     rng = np.random.default_rng(cin + H)
