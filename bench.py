@@ -134,10 +134,10 @@ def parse():
     return p.parse_args()
 
 
-def _pmc_traffic(kernel):
-    """Per-launch HBM bytes of `kernel` from this round's committed PMC summary
-    (tools/pmc_traffic.py output), or None when no summary for the current kernel exists."""
-    path = os.path.join(REPO, 'profiles', 'pmc_kpconv.json')
+def _pmc_traffic(kernel, workload):
+    """Per-launch HBM bytes of `kernel` on `workload` from this round's committed PMC summary
+    (tools/pmc_traffic.py output, tools/gpu_round.sh), or None when there is none."""
+    path = os.path.join(REPO, 'profiles', f'pmc_kpconv_{workload}.json')
     if not os.path.exists(path):
         return None, None
     with open(path) as f:
@@ -282,7 +282,7 @@ def main():
     g_launches = len(timer.events['kpconv_gather'])
     g_avg_s = g_ms / 1e3 / max(g_launches, 1)
     g_achieved = g_bytes_launch / g_avg_s / 1e9 if g_avg_s > 0 else 0.0
-    traffic, traffic_src = _pmc_traffic('fgr_kpconv_gather')
+    traffic, traffic_src = _pmc_traffic('fgr_kpconv_gather', wl)
     line['roofline'] = {
         'kernel': 'fgr_kpconv_gather', 'bound': 'hbm', 'achieved': g_achieved,
         'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': g_achieved / HBM_PEAK_GBS,

@@ -291,9 +291,9 @@ class my_Bottle2neck(nn.Module):  # noqa: N801 -- reference name (res2net.py:84)
         use = None
         if chain is not None and self.downsample is not None:
             if (lin.MODE in ('f16x3', 'bf16') and chain[3] is not None
-                    and (w != 224 or chain[2] is None or lin.MODE == 'bf16')):
+                    and (w != 224 or chain[2] is None)):
                 use = 'h3'      # (w = 224: the bf16x6 chain measured faster -- fewer barriers)
-            elif lin.MODE in ('bf16x6', 'f16x3') and chain[2] is not None:
+            elif lin.MODE in ('bf16x6', 'f16x3', 'bf16') and chain[2] is not None:
                 use = 'bf16x6'
             elif chain[0] is not None and lin.MODE == 'fp32':
                 use = 'fp32'
