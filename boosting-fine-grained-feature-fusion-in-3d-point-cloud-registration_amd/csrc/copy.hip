@@ -1,0 +1,69 @@
+// Batched device-to-device copies: up to kMaxCopies (src, dst, bytes) triples in ONE launch.
+// The HIP-graph replay of the forward (fgreg/regtr.py) refreshes its static kpconv_meta inputs
+// and clones its outputs every step -- ~10-30 small copies, each a separate blit dispatch
+// (~4-5 us apiece in the trace) -- so they go through this kernel instead.
+#include "common.h"
+
+namespace fgr {
+namespace {
+
+constexpr int kMaxCopies = 32;
+
+struct CopyBatch {
+    const char* src[kMaxCopies];
+    char* dst[kMaxCopies];
+    int64_t bytes[kMaxCopies];
+};
+
+// grid (x: chunks of 256 threads x 4 x 16 B, y: copy); 16-B accesses when both ends allow
+__global__ void __launch_bounds__(256) copy_batch_kernel(CopyBatch b) {
+    const int k = blockIdx.y;
+    const char* s = b.src[k];
+    char* d = b.dst[k];
+    const int64_t n = b.bytes[k];
+    const int64_t chunk = (int64_t)blockIdx.x * 256 * 64;
+    if (chunk >= n) return;
+    const bool vec = ((reinterpret_cast<uintptr_t>(s) | reinterpret_cast<uintptr_t>(d)) & 15) == 0;
+    if (vec) {
+        const int64_t n16 = n / 16;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t i = chunk / 16 + threadIdx.x + 256 * u;
+            if (i < n16)
+                reinterpret_cast<uint4*>(d)[i] = reinterpret_cast<const uint4*>(s)[i];
+        }
+        const int64_t tail = n16 * 16;
+        if (blockIdx.x == 0 && threadIdx.x < n - tail) d[tail + threadIdx.x] = s[tail + threadIdx.x];
+    } else {
+        for (int64_t i = chunk + threadIdx.x; i < min(n, chunk + 256 * 64); i += 256) d[i] = s[i];
+    }
+}
+
+}  // namespace
+}  // namespace fgr
+
+using namespace fgr;
+
+extern "C" int fgr_copy_batch(int32_t n, const void* const* src, void* const* dst,
+                              const int64_t* bytes, void* stream) {
+    FGR_REQUIRE(n >= 0 && (n == 0 || (src && dst && bytes)), "fgr_copy_batch: bad arguments");
+    hipStream_t st = as_stream(stream);
+    for (int32_t i0 = 0; i0 < n; i0 += kMaxCopies) {
+        const int m = n - i0 < kMaxCopies ? n - i0 : kMaxCopies;
+        CopyBatch b{};
+        int64_t mx = 0;
+        for (int j = 0; j < m; ++j) {
+            FGR_REQUIRE(bytes[i0 + j] >= 0 && (bytes[i0 + j] == 0 || (src[i0 + j] && dst[i0 + j])),
+                        "fgr_copy_batch: copy %d: bad pointer / size", i0 + j);
+            b.src[j] = static_cast<const char*>(src[i0 + j]);
+            b.dst[j] = static_cast<char*>(dst[i0 + j]);
+            b.bytes[j] = bytes[i0 + j];
+            mx = bytes[i0 + j] > mx ? bytes[i0 + j] : mx;
+        }
+        if (mx == 0) continue;
+        hipLaunchKernelGGL(copy_batch_kernel, dim3((unsigned)ceil_div(mx, 256 * 64), (unsigned)m),
+                           dim3(256), 0, st, b);
+        FGR_CHECK_LAUNCH("copy_batch_kernel");
+    }
+    return FGR_OK;
+}

@@ -155,19 +155,31 @@ int launch_scan(int* io, int* ord, const int64_t* n_dev, int64_t n_max, int2* ti
 }
 
 // per-cloud min / max of xyz (256 threads, one block per cloud); valid in thread 0
+// bounding box of pts[b, e) over the whole block (<= 1024 threads); every thread keeps 4
+// points' loads in flight per round (the loop is latency-bound: one block per cloud)
 __device__ __forceinline__ void block_bbox(const float* __restrict__ pts, int64_t b, int64_t e,
                                            float mn[3], float mx[3]) {
     mn[0] = mn[1] = mn[2] = INFINITY;
     mx[0] = mx[1] = mx[2] = -INFINITY;
-    for (int64_t i = b + threadIdx.x; i < e; i += blockDim.x) {
+    const int64_t bs = blockDim.x;
+    for (int64_t i0 = b + threadIdx.x; i0 < e; i0 += 4 * bs) {
+        float v[4][3];
 #pragma unroll
-        for (int d = 0; d < 3; ++d) {
-            const float v = pts[3 * i + d];
-            mn[d] = fminf(mn[d], v);
-            mx[d] = fmaxf(mx[d], v);
+        for (int u = 0; u < 4; ++u) {
+            const int64_t i = i0 + u * bs;
+            const int64_t ic = i < e ? i : i0;              // i0 < e: always a valid point
+#pragma unroll
+            for (int d = 0; d < 3; ++d) v[u][d] = pts[3 * ic + d];
         }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int d = 0; d < 3; ++d) {
+                mn[d] = fminf(mn[d], v[u][d]);
+                mx[d] = fmaxf(mx[d], v[u][d]);
+            }
     }
-    __shared__ float red[2][3][4];
+    __shared__ float red[2][3][16];
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
         for (int o = 32; o > 0; o >>= 1) {
@@ -175,14 +187,18 @@ __device__ __forceinline__ void block_bbox(const float* __restrict__ pts, int64_
             mx[d] = fmaxf(mx[d], __shfl_xor(mx[d], o, kWave));
         }
     }
-    const int w = threadIdx.x / kWave, l = threadIdx.x % kWave;
+    const int w = threadIdx.x / kWave, l = threadIdx.x % kWave, nw = (int)(bs / kWave);
     if (l == 0)
         for (int d = 0; d < 3; ++d) { red[0][d][w] = mn[d]; red[1][d][w] = mx[d]; }
     __syncthreads();
     if (threadIdx.x == 0)
         for (int d = 0; d < 3; ++d) {
-            mn[d] = fminf(fminf(red[0][d][0], red[0][d][1]), fminf(red[0][d][2], red[0][d][3]));
-            mx[d] = fmaxf(fmaxf(red[1][d][0], red[1][d][1]), fmaxf(red[1][d][2], red[1][d][3]));
+            mn[d] = red[0][d][0];
+            mx[d] = red[1][d][0];
+            for (int k = 1; k < nw; ++k) {
+                mn[d] = fminf(mn[d], red[0][d][k]);
+                mx[d] = fmaxf(mx[d], red[1][d][k]);
+            }
         }
 }
 
@@ -198,7 +214,7 @@ struct DGrid {
 
 constexpr long long kHuge = 1ll << 62;
 
-__global__ void __launch_bounds__(256) dgrid_bbox_kernel(const float* __restrict__ pts,
+__global__ void __launch_bounds__(1024) dgrid_bbox_kernel(const float* __restrict__ pts,
                                                          const int64_t* __restrict__ off, float dl,
                                                          DGrid* __restrict__ grids) {
     const int c = blockIdx.x;
@@ -389,7 +405,7 @@ struct RGrid {
 
 __host__ __device__ inline long long rgrid_cap(int64_t n_c) { return 4 * n_c + 1024; }
 
-__global__ void __launch_bounds__(256) rgrid_bbox_kernel(const float* __restrict__ s,
+__global__ void __launch_bounds__(1024) rgrid_bbox_kernel(const float* __restrict__ s,
                                                          const int64_t* __restrict__ s_off,
                                                          float radius, RGrid* __restrict__ grids) {
     const int c = blockIdx.x;
@@ -644,7 +660,7 @@ extern "C" int fgr_grid_subsample_count(const float* points, const int64_t* off,
         set_error("fgr_grid_subsample_count: workspace %zu < %zu bytes", ws_bytes, g.total);
         return FGR_E_WORKSPACE;
     }
-    hipLaunchKernelGGL(dgrid_bbox_kernel, dim3(n_clouds), dim3(256), 0, st, points, off, dl,
+    hipLaunchKernelGGL(dgrid_bbox_kernel, dim3(n_clouds), dim3(1024), 0, st, points, off, dl,
                        g.grids);
     FGR_CHECK_LAUNCH("dgrid_bbox_kernel");
     hipLaunchKernelGGL(dgrid_base_kernel, dim3(1), dim3(64), 0, st, g.grids, n_clouds,
@@ -715,7 +731,7 @@ extern "C" int fgr_radius_grid_build(const float* s, const int64_t* s_off, int32
     hipStream_t st = as_stream(stream);
     TimedCall timed_(st);
     const int64_t cap = 4 * ns + 1024ll * n_clouds;
-    hipLaunchKernelGGL(rgrid_bbox_kernel, dim3(n_clouds), dim3(256), 0, st, s, s_off, radius,
+    hipLaunchKernelGGL(rgrid_bbox_kernel, dim3(n_clouds), dim3(1024), 0, st, s, s_off, radius,
                        g.grids);
     FGR_CHECK_LAUNCH("rgrid_bbox_kernel");
     FGR_CHECK_HIP(hipMemsetAsync(g.start, 0, 4 * (cap + 1), st));

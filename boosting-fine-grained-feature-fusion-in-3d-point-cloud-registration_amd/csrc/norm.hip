@@ -342,61 +342,77 @@ __global__ void __launch_bounds__(256) instnorm_ls_apply_kernel(LsArgs a) {
 inline bool ls_ok(int c) { return c % 4 == 0 && c / 4 <= 256 && 256 % (c / 4) == 0; }
 inline int ls_rows(int c) { return (256 / (c / 4)) * kLsIter; }
 
-// LayerNorm, 16 lanes per row (4 rows per wave, 16 per block), d % 64 == 0 and
-// d <= 64 * V: each lane holds V/4 float4 (16-B loads / stores), row reductions on DPP
-// within a 16-lane row (no LDS). `pre_bias` as in layernorm_kernel below.
-template <int V>
+// LayerNorm, LPR lanes per row (16 / 32 / 64: 16 / 8 / 4 rows per 256-thread block), d % 64
+// == 0 and d <= 4 * LPR * NV: each lane holds NV float4 (16-B loads / stores). Every load of
+// the row (x, pre_bias, gamma, beta, add) is issued before the reductions, so a row costs
+// one memory round trip; row sums on DPP within 16-lane rows, then permlane16 / 32 swaps.
+// `pre_bias` as in layernorm_kernel below.
+template <int LPR>
+__device__ __forceinline__ float lpr_sum(float v) {
+    v = row16_sum(v);
+    if constexpr (LPR >= 32) {
+        auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+        v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+    }
+    if constexpr (LPR >= 64) {
+        auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+        v = __uint_as_float(b[0]) + __uint_as_float(b[1]);
+    }
+    return v;
+}
+
+template <int LPR, int NV>
 __global__ void __launch_bounds__(256)
-layernorm16_kernel(float* __restrict__ x, int64_t n, int d, const float* __restrict__ g,
-                   const float* __restrict__ bta, float eps, const float* __restrict__ add,
-                   const float* __restrict__ pre_bias, float* __restrict__ out) {
-    const int64_t r = (int64_t)blockIdx.x * 16 + threadIdx.x / 16;
-    const int l = threadIdx.x & 15;
+layernorm_lpr_kernel(float* __restrict__ x, int64_t n, int d, const float* __restrict__ g,
+                     const float* __restrict__ bta, float eps, const float* __restrict__ add,
+                     const float* __restrict__ pre_bias, float* __restrict__ out) {
+    constexpr int RPB = 256 / LPR;
+    const int64_t r = (int64_t)blockIdx.x * RPB + threadIdx.x / LPR;
+    const int l = threadIdx.x % LPR;
     const bool ok = r < n;                               // keep all lanes for the DPP sums
     const int64_t rr = ok ? r : n - 1;
-    float4 v[V / 4];
+    float4 v[NV], gg[NV], bb[NV], ad[NV];
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+        const int col = 4 * (l + LPR * j);
+        const bool in = col < d;
+        v[j] = in ? *reinterpret_cast<const float4*>(x + rr * d + col) : z;
+        gg[j] = in ? *reinterpret_cast<const float4*>(g + col) : z;
+        bb[j] = in ? *reinterpret_cast<const float4*>(bta + col) : z;
+        ad[j] = (in && add) ? *reinterpret_cast<const float4*>(add + rr * d + col) : z;
+    }
     float s = 0.f;
 #pragma unroll
-    for (int j = 0; j < V / 4; ++j) {
-        const int col = 4 * (l + 16 * j);
-        float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (col < d) {
-            t = *reinterpret_cast<const float4*>(x + rr * d + col);
-            if (pre_bias) {
-                const float4 pb = *reinterpret_cast<const float4*>(pre_bias + col);
-                t.x += pb.x; t.y += pb.y; t.z += pb.z; t.w += pb.w;
-                if (ok) *reinterpret_cast<float4*>(x + rr * d + col) = t;
-            }
+    for (int j = 0; j < NV; ++j) {
+        const int col = 4 * (l + LPR * j);
+        if (pre_bias && col < d) {
+            const float4 pb = *reinterpret_cast<const float4*>(pre_bias + col);
+            v[j].x += pb.x; v[j].y += pb.y; v[j].z += pb.z; v[j].w += pb.w;
+            if (ok) *reinterpret_cast<float4*>(x + rr * d + col) = v[j];
         }
-        v[j] = t;
-        s += (t.x + t.y) + (t.z + t.w);
+        s += (v[j].x + v[j].y) + (v[j].z + v[j].w);
     }
-    const float mean = row16_sum(s) / (float)d;
+    const float mean = lpr_sum<LPR>(s) / (float)d;
     float sq = 0.f;
 #pragma unroll
-    for (int j = 0; j < V / 4; ++j) {
-        if (4 * (l + 16 * j) < d) {
+    for (int j = 0; j < NV; ++j) {
+        if (4 * (l + LPR * j) < d) {
             const float a0 = v[j].x - mean, a1 = v[j].y - mean, a2 = v[j].z - mean, a3 = v[j].w - mean;
             sq += (a0 * a0 + a1 * a1) + (a2 * a2 + a3 * a3);
         }
     }
-    const float rstd = 1.0f / sqrtf(row16_sum(sq) / (float)d + eps);
+    const float rstd = 1.0f / sqrtf(lpr_sum<LPR>(sq) / (float)d + eps);
     if (!ok) return;
 #pragma unroll
-    for (int j = 0; j < V / 4; ++j) {
-        const int col = 4 * (l + 16 * j);
+    for (int j = 0; j < NV; ++j) {
+        const int col = 4 * (l + LPR * j);
         if (col < d) {
-            const float4 gg = *reinterpret_cast<const float4*>(g + col);
-            const float4 bb = *reinterpret_cast<const float4*>(bta + col);
             float4 y;
-            y.x = (v[j].x - mean) * rstd * gg.x + bb.x;
-            y.y = (v[j].y - mean) * rstd * gg.y + bb.y;
-            y.z = (v[j].z - mean) * rstd * gg.z + bb.z;
-            y.w = (v[j].w - mean) * rstd * gg.w + bb.w;
-            if (add) {
-                const float4 ad = *reinterpret_cast<const float4*>(add + r * d + col);
-                y.x += ad.x; y.y += ad.y; y.z += ad.z; y.w += ad.w;
-            }
+            y.x = (v[j].x - mean) * rstd * gg[j].x + bb[j].x + ad[j].x;
+            y.y = (v[j].y - mean) * rstd * gg[j].y + bb[j].y + ad[j].y;
+            y.z = (v[j].z - mean) * rstd * gg[j].z + bb[j].z + ad[j].z;
+            y.w = (v[j].w - mean) * rstd * gg[j].w + bb[j].w + ad[j].w;
             *reinterpret_cast<float4*>(out + r * d + col) = y;
         }
     }
@@ -563,13 +579,16 @@ extern "C" int fgr_layernorm(float* x, int64_t n, int32_t d, const float* gamma,
                        reinterpret_cast<uintptr_t>(gamma) | reinterpret_cast<uintptr_t>(beta) |
                        reinterpret_cast<uintptr_t>(add) | reinterpret_cast<uintptr_t>(pre_bias)) & 15) == 0;
     if (vec) {
-        const dim3 g16((unsigned)ceil_div(n, 16));
+        // lanes per row sized so each lane holds at most 4 float4 (rows stay in flight)
         if (d <= 256)
-            hipLaunchKernelGGL(layernorm16_kernel<16>, g16, dim3(256), 0, st, x, n, d, gamma, beta, eps, add, pre_bias, out);
+            hipLaunchKernelGGL((layernorm_lpr_kernel<16, 4>), dim3((unsigned)ceil_div(n, 16)),
+                               dim3(256), 0, st, x, n, d, gamma, beta, eps, add, pre_bias, out);
         else if (d <= 512)
-            hipLaunchKernelGGL(layernorm16_kernel<32>, g16, dim3(256), 0, st, x, n, d, gamma, beta, eps, add, pre_bias, out);
+            hipLaunchKernelGGL((layernorm_lpr_kernel<32, 4>), dim3((unsigned)ceil_div(n, 8)),
+                               dim3(256), 0, st, x, n, d, gamma, beta, eps, add, pre_bias, out);
         else
-            hipLaunchKernelGGL(layernorm16_kernel<64>, g16, dim3(256), 0, st, x, n, d, gamma, beta, eps, add, pre_bias, out);
+            hipLaunchKernelGGL((layernorm_lpr_kernel<64, 4>), dim3((unsigned)ceil_div(n, 4)),
+                               dim3(256), 0, st, x, n, d, gamma, beta, eps, add, pre_bias, out);
     } else if (d <= 64)
         hipLaunchKernelGGL(layernorm_kernel<1>, grid, dim3(256), 0, st, x, n, d, gamma, beta, eps, add, pre_bias, out);
     else if (d <= 256)

@@ -6,6 +6,7 @@ outputs with the torch caching allocator and launches on torch's current stream.
 There is deliberately no CPU path: on a tensor that is not on a GPU, or without
 libfgreg.so, these raise.
 """
+import ctypes
 import math
 import os
 from typing import Sequence, Tuple
@@ -541,6 +542,22 @@ def attention(q, k, v, q_off, kv_off, kv_seg, max_q_len, n_head, out=None,
                    'fgr_attention')
     _end('attention', t0, lambda: attention_flops(q_off, kv_off, kv_seg, d))
     return out
+
+
+def copy_batch(srcs, dsts):
+    """dst.copy_(src) for every pair (same shape / dtype, contiguous, device tensors) in one
+    fgr_copy_batch launch per 32 pairs."""
+    n = len(srcs)
+    if n == 0:
+        return
+    for a, b in zip(srcs, dsts):
+        assert a.shape == b.shape and a.dtype == b.dtype and a.is_contiguous() and b.is_contiguous()
+    _dev(*srcs, *dsts)
+    arr = ctypes.c_void_p * n
+    src = arr(*[t.data_ptr() for t in srcs])
+    dst = arr(*[t.data_ptr() for t in dsts])
+    nb = (ctypes.c_int64 * n)(*[t.numel() * t.element_size() for t in srcs])
+    _lib.check(_lib.load().fgr_copy_batch(n, src, dst, nb, _stream()), 'fgr_copy_batch')
 
 
 _WS = {}

@@ -250,11 +250,17 @@ class _CoreGraph:
             self.out = model._core(self.meta, self.seg, B)
 
     def run(self, meta):
+        srcs, dsts = [], []
         for k in _META_IN:
             for dst, src in zip(self.meta[k], meta[k]):
-                dst.copy_(src)
+                srcs.append(src.contiguous())
+                dsts.append(dst)
+        ops.copy_batch(srcs, dsts)                  # one dispatch for all static inputs
         self.graph.replay()
-        return tuple(t.clone() for t in self.out)
+        outs = [torch.empty_like(t) if t.is_contiguous() else t.clone() for t in self.out]
+        pairs = [(t, o) for t, o in zip(self.out, outs) if t.is_contiguous()]
+        ops.copy_batch([t for t, _ in pairs], [o for _, o in pairs])   # the clones, one dispatch
+        return tuple(outs)
 
 
 def _params_version(model):

@@ -329,6 +329,13 @@ int fgr_corr_attention(const float* q, int64_t ld_q, const float* k, int64_t ld_
                        const int32_t* kv_seg, const int64_t* v_off, int32_t n_seg,
                        int32_t max_q_len, int32_t d, float scale, void* stream);
 
+/* Batched device-to-device copies: n (src[i] -> dst[i], bytes[i]) triples (host arrays of device
+ * pointers) in one launch per 32 copies; 16-B accesses where both ends are 16-B aligned. Not a
+ * reference interface: the HIP-graph replay of the forward refreshes its static inputs and
+ * clones its outputs with it (one dispatch instead of one blit per tensor). */
+int fgr_copy_batch(int32_t n, const void* const* src, void* const* dst, const int64_t* bytes,
+                   void* stream);
+
 /* ---- pose ----------------------------------------------------------------------------
  * fast_compute_rigid_transform (utils/se3_torch.py:226-273; threshold < 0 gives the
  * unthresholded compute_rigid_transform, :131-173) on n_batch independent problems
