@@ -333,7 +333,7 @@ def main():
                          'ms_per_step': tail_ms}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_seconds > 0:
-        cpu = cpu_baseline(cfg, model, src, tgt, args.cpu_seconds, tail_inputs)
+        cpu = cpu_baseline(cfg, model, src, tgt, args.cpu_seconds, tail_inputs, wl)
     line['cpu_baseline'] = cpu
     if rank == 0:
         print(json.dumps(line), flush=True)
@@ -410,7 +410,7 @@ def _calibration():
         return json.load(f)
 
 
-def cpu_baseline(cfg, model, src, tgt, budget_s, tail_inputs=None):
+def cpu_baseline(cfg, model, src, tgt, budget_s, tail_inputs=None, workload='modelnet'):
     """CPU restatement (oracle/model_oracle.py, "port") on the same pairs: B=1 forwards for
     ~budget_s, then one B=len(src) forward (BASELINE.md §3 asks for both legs)."""
     sys.path.insert(0, os.path.join(REPO, 'oracle'))
@@ -437,8 +437,13 @@ def cpu_baseline(cfg, model, src, tgt, budget_s, tail_inputs=None):
                             'unit': 'pairs/s', 'seconds': tb}
     cal = _calibration()
     if cal is not None:
-        res['calibration'] = {k: cal[k] for k in ('reference_over_port', 'hardware', 'source')
-                              if k in cal}
+        # the ratio measured on this workload's architecture / cloud size (3DLoMatch: 3DMatch's)
+        key = {'raw2048': 'modelnet', '3dlomatch': '3dmatch'}.get(workload, workload)
+        per = cal.get('per_workload', {}).get(key)
+        ratio = per['reference_over_port'] if per else cal.get('reference_over_port')
+        res['calibration'] = {'reference_over_port': ratio, 'workload': key if per else 'modelnet',
+                              'hardware': cal.get('hardware'), 'source': cal.get('source'),
+                              'reference_estimate_pairs_per_s': res['value'] * ratio}
     if tail_inputs is not None:       # the test-step tail on the same outputs (loss_oracle)
         import loss_oracle as lo
         out, batch = tail_inputs
