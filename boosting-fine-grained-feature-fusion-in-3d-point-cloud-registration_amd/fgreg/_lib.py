@@ -66,6 +66,9 @@ SIGNATURES = {
     'fgr_gemm_bf16': [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _vp],
     'fgr_gemm_rows_f16x3': [_vp, _i64, _vp, _vp, _f32, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _i64,
                             _i32, _i32, _i32, _i32, _vp],
+    'fgr_split_rows_h3_bytes': [_i32, _i32, ctypes.POINTER(_sz)],
+    'fgr_split_rows_h3': [_vp, _i64, _i32, _i32, _vp, _vp],
+    'fgr_gemm_h3_presplit': [_vp, _vp, _vp, _i64, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _vp],
     'fgr_copy_batch': [_i32, _vp, _vp, _vp, _vp],
     'fgr_overlap_pool': [_vp, _i64, _vp, _i64, _i32, _vp, _vp],
     'fgr_bce_logits_mean': [_vp, _i64, _vp, _i64, _vp, _vp],

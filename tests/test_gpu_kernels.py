@@ -441,3 +441,30 @@ def test_gemm_rows_f16x3(gpu, m, n, k, monkeypatch):
     finally:
         fl.set_mode(old_mode)
         fl.ROWS = old_rows
+
+
+@pytest.mark.parametrize('tile', list('abcdefgh'))
+def test_gemm_h3_presplit(gpu, tile, monkeypatch):
+    """fgr_split_rows_h3 + fgr_gemm_h3_presplit (both operands pre-split images, per-(row,
+    k32 step) activation scales) vs fp64: ragged M / N / K (K % 32 != 0, M not a multiple of
+    any tile), rows spanning 1e-12 .. 1e12, zero rows, bias / residual epilogues."""
+    from fgreg import linear as fl
+    monkeypatch.setenv('FGR_GEMM_G6_TILE', tile)
+    g = torch.Generator().manual_seed(3)
+    for m, n, k in ((1000, 200, 1000), (333, 3, 96), (130, 520, 40), (4099, 272, 264)):
+        x = torch.randn(m, k, generator=g, dtype=torch.float64)
+        x *= torch.tensor([10.0 ** e for e in np.linspace(-12, 12, m)], dtype=torch.float64)[:, None]
+        x[7] = 0
+        w = torch.randn(n, k, generator=g) / math.sqrt(k)
+        b = torch.randn(n, generator=g)
+        r = torch.randn(m, n, generator=g)
+        X = x.float()
+        ref = X.double() @ w.double().t()
+        a = fl.split_rows(X.to(gpu))
+        out = fl.linear_presplit(a, w.to(gpu)).double().cpu()
+        den = (X.double().abs() @ w.double().abs().t()).clamp_min(1e-300)
+        assert float(((out - ref).abs() / den).max()) < 2e-6, (tile, m, n, k)
+        assert (out[7] == 0).all()
+        out = fl.linear_presplit(a, w.to(gpu), b.to(gpu), residual=r.to(gpu)).double().cpu()
+        full = ref + b.double() + r.double()
+        assert rel_err(out, full) < 2e-6, (tile, m, n, k)
