@@ -53,7 +53,7 @@ struct G6Args {
     int M, N, K, act, vec_out;
 };
 
-template <int BM, int BN, int S>
+template <int BM, int BN, int S, bool PROBE = false>
 __global__ void __launch_bounds__(256) gemm_g6(G6Args p) {
     constexpr int TM = BM / 32, TN = BN / 32;          // 16 x 16 fragments per wave
     constexpr int A_UNITS = (BM / 16) * 128;           // [panel][term][g][16]
@@ -145,8 +145,10 @@ __global__ void __launch_bounds__(256) gemm_g6(G6Args p) {
             else wait_vm_lgkm0_6<0>();
         }
         __builtin_amdgcn_s_barrier();
-        if (s + S - 1 < nk) issue(s + S - 1);
-        const u32x4* st = lds + (s % S) * ST;
+        // PROBE (timing experiment only, wrong results): no DMA after the prologue, so the
+        // loop's cost without any global traffic is measured
+        if (!PROBE && s + S - 1 < nk) issue(s + S - 1);
+        const u32x4* st = lds + (PROBE ? 0 : (s % S) * ST);
         const float* sc = reinterpret_cast<const float*>(st + A_UNITS + W_UNITS);
         u32x4 af[TM][2], wf[TN][2];
         float sa[TM];
@@ -264,10 +266,10 @@ __global__ void __launch_bounds__(256) split_rows_h3_kernel(const float* __restr
     if (g == 0) sA[(int64_t)s * ld_s + m] = __builtin_ldexpf(1.f, -e);
 }
 
-template <int BM, int BN, int S>
+template <int BM, int BN, int S, bool PROBE = false>
 void launch_g6(const G6Args& a, hipStream_t st) {
     const int nbm = (a.M + BM - 1) / BM, nbn = (a.N + BN - 1) / BN;
-    hipLaunchKernelGGL((gemm_g6<BM, BN, S>), dim3((unsigned)(nbm * nbn)), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((gemm_g6<BM, BN, S, PROBE>), dim3((unsigned)(nbm * nbn)), dim3(256), 0, st, a);
 }
 
 int ksteps6(int k) { return (k + 63) / 64 * 2; }
@@ -335,6 +337,8 @@ extern "C" int fgr_gemm_h3_presplit(const void* a_img, const void* w_img, float*
         case 'f': launch_g6<64, 64, 3>(g, st); break;
         case 'g': launch_g6<128, 256, 2>(g, st); break;
         case 'h': launch_g6<256, 128, 2>(g, st); break;
+        case 'y': launch_g6<64, 64, 3, true>(g, st); break;     // timing probes (wrong results)
+        case 'z': launch_g6<128, 128, 3, true>(g, st); break;
         default: launch_g6<64, 64, 4>(g, st); break;
     }
     FGR_CHECK_LAUNCH("gemm_g6");
