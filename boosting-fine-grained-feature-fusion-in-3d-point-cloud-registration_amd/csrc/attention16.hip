@@ -132,8 +132,19 @@ attn_kv_image16_kernel(const float* __restrict__ k, int64_t ld_k, const float* _
     }
 }
 
-template <int DH>
-__global__ void __launch_bounds__(256, 4)
+// GLDS: the K/V tile images go global -> LDS by LDS-DMA into two buffers (tile t + 1 in
+// flight while tile t is computed; one barrier per tile, no staging registers, no ds_write
+// pass), with the per-tile scale exponents preloaded into the same LDS array (a plain load
+// inside the loop would make the compiler wait for the DMA). Needs <= kMaxTilesLds tiles.
+constexpr int kMaxTilesLds = 256;
+
+template <int N>
+__device__ __forceinline__ void wait_vm_lgkm0_a() {
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4));
+}
+
+template <int DH, bool GLDS>
+__global__ void __launch_bounds__(256, (GLDS && DH == 64) ? 2 : 4)
 attn_f16x3_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __restrict__ img,
                   const int2* __restrict__ sc, float* __restrict__ o, int64_t ld_o,
                   const int64_t* __restrict__ q_off, const int64_t* __restrict__ kv_off,
@@ -142,7 +153,8 @@ attn_f16x3_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __rest
     constexpr int KD = DH / 32;                                  // k-steps of Q K^T
     constexpr int TD = DH / 16;                                  // 16-row output tiles (dh)
     constexpr int UN = units<DH>(), NS = UN / 256;
-    __shared__ u32x4 lds[UN];
+    constexpr int EXU = GLDS ? kMaxTilesLds * 8 / 16 : 0;       // 16-B units of exponents
+    __shared__ u32x4 lds[(GLDS ? 2 : 1) * UN + EXU];
     // XCD-aware block order: linear id L runs on XCD L % 8; all q-blocks of one
     // (segment, head) get ids of one residue mod 8, so one XCD's L2 serves its K/V image.
     const int L = blockIdx.x, xcd = L & 7, j0 = L >> 3;
@@ -201,27 +213,55 @@ attn_f16x3_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __rest
     for (int t = 0; t < TD; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
     float m_run = -INFINITY, l_run = 0.f;
 
-    u32x4 stage[NS];
-    const char* lbase = reinterpret_cast<const char*>(lds);
+    u32x4 stage[GLDS ? 1 : NS];
     // transposed-read addresses of V: lane c = 4qq + p reads row 4g + qq (+16, +32j),
     // columns 16t + 4p .. +3 (chunk 2t + (p >> 1), swizzled by row bit 2)
     const int qq = c >> 2, pp = c & 3;
-
-    if (ntile > 0) {
+    int2* ex_lds = reinterpret_cast<int2*>(lds + (GLDS ? 2 * UN : 0));
+    constexpr int PW = UN / 64 / 4;                              // DMA pieces per wave per tile
+    auto dma = [&](int t) {                                      // tile t -> buffer t & 1
+        const u32x4* src = tiles + t * tile_stride;
+        __attribute__((address_space(3))) char* dst =
+            (__attribute__((address_space(3))) char*)(lds + (t & 1) * UN);
+#pragma unroll
+        for (int j = 0; j < PW; ++j) {
+            const int piece = wv + 4 * j;
+            __builtin_amdgcn_global_load_lds((const void*)(src + piece * 64 + lane),
+                                             (__attribute__((address_space(3))) void*)(dst + piece * 1024),
+                                             16, 0, 0);
+        }
+    };
+    if constexpr (GLDS) {
+        for (int t = tid; t < ntile; t += 256) ex_lds[t] = sc[tile0 + t * n_head];
+        __syncthreads();
+        if (ntile > 0) dma(0);
+    } else if (ntile > 0) {
 #pragma unroll
         for (int i = 0; i < NS; ++i) stage[i] = tiles[tid + 256 * i];
     }
     for (int tt = 0; tt < ntile; ++tt) {
-        const int2 e2 = sc[tile0 + tt * n_head];
-        __syncthreads();
+        int2 e2;
+        const u32x4* tbuf;
+        if constexpr (GLDS) {
+            wait_vm_lgkm0_a<0>();           // this wave's pieces of tile tt landed
+            __builtin_amdgcn_s_barrier();   // everyone's landed; buffer (tt+1)&1 no longer read
+            if (tt + 1 < ntile) dma(tt + 1);
+            tbuf = lds + (tt & 1) * UN;
+            e2 = ex_lds[tt];
+        } else {
+            e2 = sc[tile0 + tt * n_head];
+            __syncthreads();
 #pragma unroll
-        for (int i = 0; i < NS; ++i) lds[tid + 256 * i] = stage[i];
-        __syncthreads();
-        if (tt + 1 < ntile) {
-            const u32x4* src = tiles + (tt + 1) * tile_stride;
+            for (int i = 0; i < NS; ++i) lds[tid + 256 * i] = stage[i];
+            __syncthreads();
+            if (tt + 1 < ntile) {
+                const u32x4* src = tiles + (tt + 1) * tile_stride;
 #pragma unroll
-            for (int i = 0; i < NS; ++i) stage[i] = src[tid + 256 * i];
+                for (int i = 0; i < NS; ++i) stage[i] = src[tid + 256 * i];
+            }
+            tbuf = lds;
         }
+        const char* lbase = reinterpret_cast<const char*>(tbuf);
         const int valid = nk - tt * 64;
 
         f32x4 s[4];
@@ -230,8 +270,8 @@ attn_f16x3_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __rest
             f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int kd = 0; kd < KD; ++kd) {
-                const f16x8 kh = __builtin_bit_cast(f16x8, lds[((kd * 2 + 0) * 4 + g) * 64 + 16 * n + c]);
-                const f16x8 kl = __builtin_bit_cast(f16x8, lds[((kd * 2 + 1) * 4 + g) * 64 + 16 * n + c]);
+                const f16x8 kh = __builtin_bit_cast(f16x8, tbuf[((kd * 2 + 0) * 4 + g) * 64 + 16 * n + c]);
+                const f16x8 kl = __builtin_bit_cast(f16x8, tbuf[((kd * 2 + 1) * 4 + g) * 64 + 16 * n + c]);
                 a = __builtin_amdgcn_mfma_f32_16x16x32_f16(kl, qt[kd][0], a, 0, 0, 0);
                 a = __builtin_amdgcn_mfma_f32_16x16x32_f16(kh, qt[kd][1], a, 0, 0, 0);
                 a = __builtin_amdgcn_mfma_f32_16x16x32_f16(kh, qt[kd][0], a, 0, 0, 0);
@@ -382,14 +422,29 @@ extern "C" int fgr_attention_f16x3(const float* q, int64_t ld_q, const float* k,
     FGR_CHECK_LAUNCH("attn_kv_image16_kernel");
     const int n_qblk = (int)ceil_div(max_q_len, 64);
     const int64_t n_blocks = ceil_div((int64_t)n_seg * n_head, 8) * 8 * n_qblk;
-    if (dh == 32)
-        hipLaunchKernelGGL(attn_f16x3_kernel<32>, dim3((unsigned)n_blocks), dim3(256), 0, st, q,
-                           ld_q, (const uint4*)img, (const int2*)sc, o, ld_o, q_off, kv_off, kv_seg,
-                           n_head, n_seg, n_qblk, scale * 1.4426950408889634f);
+    // LDS-DMA K/V staging (measured: head dim 64 57 -> 42 us per launch on the 3DMatch
+    // forward although its 2 x 32-KB buffers halve the blocks per CU; head dim 32 on par)
+    // when every key segment fits the preloaded exponent table; FGR_ATTN_GLDS=0 selects the
+    // register-staged loop (A/B)
+    const char* gl = getenv("FGR_ATTN_GLDS");
+    const bool glds = !(gl && gl[0] == '0') && ceil_div(max_kv_len, 64) <= kMaxTilesLds;
+    const float sl2 = scale * 1.4426950408889634f;
+    if (dh == 32 && glds)
+        hipLaunchKernelGGL((attn_f16x3_kernel<32, true>), dim3((unsigned)n_blocks), dim3(256), 0, st,
+                           q, ld_q, (const uint4*)img, (const int2*)sc, o, ld_o, q_off, kv_off,
+                           kv_seg, n_head, n_seg, n_qblk, sl2);
+    else if (dh == 32)
+        hipLaunchKernelGGL((attn_f16x3_kernel<32, false>), dim3((unsigned)n_blocks), dim3(256), 0,
+                           st, q, ld_q, (const uint4*)img, (const int2*)sc, o, ld_o, q_off, kv_off,
+                           kv_seg, n_head, n_seg, n_qblk, sl2);
+    else if (glds)
+        hipLaunchKernelGGL((attn_f16x3_kernel<64, true>), dim3((unsigned)n_blocks), dim3(256), 0, st,
+                           q, ld_q, (const uint4*)img, (const int2*)sc, o, ld_o, q_off, kv_off,
+                           kv_seg, n_head, n_seg, n_qblk, sl2);
     else
-        hipLaunchKernelGGL(attn_f16x3_kernel<64>, dim3((unsigned)n_blocks), dim3(256), 0, st, q,
-                           ld_q, (const uint4*)img, (const int2*)sc, o, ld_o, q_off, kv_off, kv_seg,
-                           n_head, n_seg, n_qblk, scale * 1.4426950408889634f);
+        hipLaunchKernelGGL((attn_f16x3_kernel<64, false>), dim3((unsigned)n_blocks), dim3(256), 0,
+                           st, q, ld_q, (const uint4*)img, (const int2*)sc, o, ld_o, q_off, kv_off,
+                           kv_seg, n_head, n_seg, n_qblk, sl2);
     FGR_CHECK_LAUNCH("attn_f16x3_kernel");
     return FGR_OK;
 }

@@ -18,6 +18,7 @@ statistics as in the reference, but no custom backward exists for the KPConv
 kernels.
 """
 import math
+import os
 from typing import List
 
 import numpy as np
@@ -165,6 +166,12 @@ def init_kernel_points(radius, n_kp, rng=np.random):
 # ------------------------------------------------------------------------------------------
 # Blocks
 # ------------------------------------------------------------------------------------------
+# Res2Net hierarchy kernel where both fp32-accurate chains exist (w = 112, 224): the bf16x6
+# chain at w = 224 (measured faster), the f16x3 chain otherwise; FGREG_R2N = h3 | bf16x6
+# forces one (A/B switch)
+R2N = os.environ.get('FGREG_R2N', 'auto')
+
+
 class KPConv(nn.Module):
     """Rigid KPConv (finegrained_kpconv_blocks.py:171-401): linear influence, sum mode."""
 
@@ -290,8 +297,9 @@ class my_Bottle2neck(nn.Module):  # noqa: N801 -- reference name (res2net.py:84)
         w = self.width
         use = None
         if chain is not None and self.downsample is not None:
+            prefer6 = R2N == 'bf16x6' or (R2N == 'auto' and w == 224)
             if (lin.MODE in ('f16x3', 'bf16') and chain[3] is not None
-                    and (w != 224 or chain[2] is None)):
+                    and (not prefer6 or chain[2] is None)):
                 use = 'h3'      # (w = 224: the bf16x6 chain measured faster -- fewer barriers)
             elif lin.MODE in ('bf16x6', 'f16x3', 'bf16') and chain[2] is not None:
                 use = 'bf16x6'
