@@ -268,8 +268,8 @@ attn_bf16_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __restr
                  const int64_t* __restrict__ kv_off, const int32_t* __restrict__ kv_seg,
                  int n_head, int n_seg, int n_qblk, float scale_log2) {
     constexpr int KD = DH / 32, TD = DH / 16;
-    constexpr int UN = bf_units<DH>(), NS = UN / 256;
-    __shared__ u32x4 lds[UN];
+    constexpr int UN = bf_units<DH>();
+    __shared__ u32x4 lds[2 * UN];
     const int L = blockIdx.x, xcd = L & 7, j0 = L >> 3;
     const int pair = (j0 / n_qblk) * 8 + xcd, qblk = j0 % n_qblk;
     if (pair >= n_seg * n_head) return;
@@ -305,23 +305,29 @@ attn_bf16_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __restr
 #pragma unroll
     for (int t = 0; t < TD; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
     float m_run = -INFINITY, l_run = 0.f;
-    u32x4 stage[NS];
-    const char* lbase = reinterpret_cast<const char*>(lds);
+    // K/V tiles by LDS-DMA into two buffers: tile t + 1 in flight while tile t is computed,
+    // one barrier per tile (as attention16.hip's f16x3 loop)
     const int qq = c >> 2, pp = c & 3;
-    if (ntile > 0) {
+    constexpr int PW = UN / 64 / 4;                              // DMA pieces per wave per tile
+    auto dma = [&](int t) {
+        const u32x4* src = tiles + t * tile_stride;
+        __attribute__((address_space(3))) char* dst =
+            (__attribute__((address_space(3))) char*)(lds + (t & 1) * UN);
 #pragma unroll
-        for (int i = 0; i < NS; ++i) stage[i] = tiles[tid + 256 * i];
-    }
-    for (int tt = 0; tt < ntile; ++tt) {
-        __syncthreads();
-#pragma unroll
-        for (int i = 0; i < NS; ++i) lds[tid + 256 * i] = stage[i];
-        __syncthreads();
-        if (tt + 1 < ntile) {
-            const u32x4* src = tiles + (tt + 1) * tile_stride;
-#pragma unroll
-            for (int i = 0; i < NS; ++i) stage[i] = src[tid + 256 * i];
+        for (int j = 0; j < PW; ++j) {
+            const int piece = wv + 4 * j;
+            __builtin_amdgcn_global_load_lds((const void*)(src + piece * 64 + lane),
+                                             (__attribute__((address_space(3))) void*)(dst + piece * 1024),
+                                             16, 0, 0);
         }
+    };
+    if (ntile > 0) dma(0);
+    for (int tt = 0; tt < ntile; ++tt) {
+        __builtin_amdgcn_s_waitcnt((7 << 4));                    // vmcnt(0) lgkmcnt(0)
+        __builtin_amdgcn_s_barrier();
+        if (tt + 1 < ntile) dma(tt + 1);
+        const u32x4* tbuf = lds + (tt & 1) * UN;
+        const char* lbase = reinterpret_cast<const char*>(tbuf);
         const int valid = nk - tt * 64;
         f32x4 s[4];
 #pragma unroll
@@ -330,7 +336,7 @@ attn_bf16_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __restr
 #pragma unroll
             for (int kd = 0; kd < KD; ++kd)
                 a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                    __builtin_bit_cast(bf16x8, lds[(kd * 4 + g) * 64 + 16 * n + c]), qt[kd], a, 0, 0, 0);
+                    __builtin_bit_cast(bf16x8, tbuf[(kd * 4 + g) * 64 + 16 * n + c]), qt[kd], a, 0, 0, 0);
             s[n] = a;
         }
         if (valid < 64) {
