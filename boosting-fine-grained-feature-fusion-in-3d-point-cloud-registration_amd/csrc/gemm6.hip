@@ -53,17 +53,18 @@ struct G6Args {
     int M, N, K, act, vec_out;
 };
 
-template <int BM, int BN, int S, bool PROBE = false>
+template <int BM, int BN, int S, bool PROBE = false, int REP = 1, int KS = 1>
 __global__ void __launch_bounds__(256) gemm_g6(G6Args p) {
     constexpr int TM = BM / 32, TN = BN / 32;          // 16 x 16 fragments per wave
-    constexpr int A_UNITS = (BM / 16) * 128;           // [panel][term][g][16]
+    constexpr int A_UNITS = (BM / 16) * 128;           // [panel][term][g][16] of one k32 step
     constexpr int W_UNITS = (BN / 16) * 128;
     constexpr int S_UNITS = 64;                        // 4 pieces x 256 B of scales (BM <= 256)
-    constexpr int ST = A_UNITS + W_UNITS + S_UNITS;
+    constexpr int ST1 = A_UNITS + W_UNITS + S_UNITS;   // one k32 step
+    constexpr int ST = KS * ST1;                       // one stage = KS k32 steps
     constexpr int A_PIECES = A_UNITS / 64, W_PIECES = W_UNITS / 64;
-    constexpr int NP = A_PIECES + W_PIECES + 4;
-    static_assert(NP % 4 == 0 && BM <= 256, "tile");
-    constexpr int P = NP / 4;
+    constexpr int NP1 = A_PIECES + W_PIECES + 4;
+    static_assert(NP1 % 4 == 0 && BM <= 256, "tile");
+    constexpr int P1 = NP1 / 4, P = P1 * KS;           // DMA pieces per wave per k-step / stage
     __shared__ u32x4 lds[S * ST];
 
     const int nbm = (p.M + BM - 1) / BM, nbn = (p.N + BN - 1) / BN;
@@ -80,16 +81,16 @@ __global__ void __launch_bounds__(256) gemm_g6(G6Args p) {
     const int wm = (wv & 1) * (BM / 2), wn = (wv >> 1) * (BN / 2);
     const int g = lane >> 4, c = lane & 15;
     const int npanel_w = (p.N + 15) / 16;
-    const int nk = (p.K + 31) / 32;
+    const int nst = (p.K + 32 * KS - 1) / (32 * KS);  // stages (images padded to even k32 steps)
 
-    // DMA sources: piece q = wv + 4 j of a stage. A panels are padded to whole blocks
+    // DMA sources of one k32 step: piece q = wv + 4 j. A panels are padded to whole blocks
     // (fgr_split_rows_h3 allocates ceil(M / 256) * 16 panels), W panels are clamped.
     // (A_PIECES, W_PIECES multiples of 4: piece j's kind is the same in every wave)
     static_assert(A_PIECES % 4 == 0 && W_PIECES % 4 == 0, "pieces");
     constexpr int JA = A_PIECES / 4, JW = (A_PIECES + W_PIECES) / 4;
-    const u32x4* src0[P];
+    const u32x4* src0[P1];
 #pragma unroll
-    for (int j = 0; j < P; ++j) {
+    for (int j = 0; j < P1; ++j) {
         const int q = wv + 4 * j;
         if (j < JA) {
             const int panel = q / 2, term = q % 2;
@@ -105,21 +106,25 @@ __global__ void __launch_bounds__(256) gemm_g6(G6Args p) {
         }
     }
     auto issue = [&](int s) {
-        __attribute__((address_space(3))) char* base =
-            (__attribute__((address_space(3))) char*)(lds + (s % S) * ST);
 #pragma unroll
-        for (int j = 0; j < P; ++j) {
-            const int q = wv + 4 * j;
-            if (j >= JW) {
-                const float* src = reinterpret_cast<const float*>(src0[j]) + (int64_t)s * p.ld_sA;
-                __builtin_amdgcn_global_load_lds((const void*)src,
-                                                 (lds_void*)(base + (A_UNITS + W_UNITS) * 16 +
-                                                             (q - A_PIECES - W_PIECES) * 256),
-                                                 4, 0, 0);
-            } else {
-                const u32x4* src = src0[j] + (int64_t)s * 128;
-                __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(base + q * 1024), 16,
-                                                 0, 0);
+        for (int ks = 0; ks < KS; ++ks) {
+            const int k = s * KS + ks;                                  // k32 step
+            __attribute__((address_space(3))) char* base =
+                (__attribute__((address_space(3))) char*)(lds + (s % S) * ST + ks * ST1);
+#pragma unroll
+            for (int j = 0; j < P1; ++j) {
+                const int q = wv + 4 * j;
+                if (j >= JW) {
+                    const float* src = reinterpret_cast<const float*>(src0[j]) + (int64_t)k * p.ld_sA;
+                    __builtin_amdgcn_global_load_lds((const void*)src,
+                                                     (lds_void*)(base + (A_UNITS + W_UNITS) * 16 +
+                                                                 (q - A_PIECES - W_PIECES) * 256),
+                                                     4, 0, 0);
+                } else {
+                    const u32x4* src = src0[j] + (int64_t)k * 128;
+                    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(base + q * 1024),
+                                                     16, 0, 0);
+                }
             }
         }
     };
@@ -132,23 +137,29 @@ __global__ void __launch_bounds__(256) gemm_g6(G6Args p) {
 
 #pragma unroll
     for (int s = 0; s < S - 1; ++s)
-        if (s < nk) issue(s);
+        if (s < nst) issue(s);
 
-    for (int s = 0; s < nk; ++s) {
-        const int ahead = min(S - 2, nk - 1 - s);
+    for (int s = 0; s < nst; ++s) {
+        const int ahead = min(S - 2, nst - 1 - s);
         if constexpr (S >= 4) {
             if (ahead >= 2) wait_vm_lgkm0_6<2 * P>();
             else if (ahead == 1) wait_vm_lgkm0_6<P>();
             else wait_vm_lgkm0_6<0>();
-        } else {
+        } else if constexpr (S == 3) {
             if (ahead >= 1) wait_vm_lgkm0_6<P>();
             else wait_vm_lgkm0_6<0>();
+        } else {
+            wait_vm_lgkm0_6<0>();
         }
         __builtin_amdgcn_s_barrier();
         // PROBE (timing experiment only, wrong results): no DMA after the prologue, so the
         // loop's cost without any global traffic is measured
-        if (!PROBE && s + S - 1 < nk) issue(s + S - 1);
-        const u32x4* st = lds + (PROBE ? 0 : (s % S) * ST);
+        if (!PROBE && s + S - 1 < nst) issue(s + S - 1);
+#pragma unroll 1
+        for (int rep = 0; rep < REP; ++rep) {       // REP > 1: timing probe only
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+        const u32x4* st = lds + (PROBE ? 0 : (s % S) * ST) + ks * ST1;
         const float* sc = reinterpret_cast<const float*>(st + A_UNITS + W_UNITS);
         u32x4 af[TM][2], wf[TN][2];
         float sa[TM];
@@ -180,6 +191,8 @@ __global__ void __launch_bounds__(256) gemm_g6(G6Args p) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) acc[j][i][r] = __builtin_fmaf(tt[r], sa[i], acc[j][i][r]);
             }
+        }
+        }
         }
     }
 
@@ -266,10 +279,11 @@ __global__ void __launch_bounds__(256) split_rows_h3_kernel(const float* __restr
     if (g == 0) sA[(int64_t)s * ld_s + m] = __builtin_ldexpf(1.f, -e);
 }
 
-template <int BM, int BN, int S, bool PROBE = false>
+template <int BM, int BN, int S, bool PROBE = false, int REP = 1, int KS = 1>
 void launch_g6(const G6Args& a, hipStream_t st) {
     const int nbm = (a.M + BM - 1) / BM, nbn = (a.N + BN - 1) / BN;
-    hipLaunchKernelGGL((gemm_g6<BM, BN, S, PROBE>), dim3((unsigned)(nbm * nbn)), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((gemm_g6<BM, BN, S, PROBE, REP, KS>), dim3((unsigned)(nbm * nbn)),
+                       dim3(256), 0, st, a);
 }
 
 int ksteps6(int k) { return (k + 63) / 64 * 2; }
@@ -339,6 +353,16 @@ extern "C" int fgr_gemm_h3_presplit(const void* a_img, const void* w_img, float*
         case 'h': launch_g6<256, 128, 2>(g, st); break;
         case 'y': launch_g6<64, 64, 3, true>(g, st); break;     // timing probes (wrong results)
         case 'z': launch_g6<128, 128, 3, true>(g, st); break;
+        case 'w': launch_g6<64, 64, 3, true, 2>(g, st); break;
+        case 'x': launch_g6<64, 64, 3, true, 4>(g, st); break;
+        // two / four k32 steps per stage
+        case 'i': launch_g6<64, 64, 2, false, 1, 2>(g, st); break;
+        case 'j': launch_g6<64, 64, 3, false, 1, 2>(g, st); break;
+        case 'k': launch_g6<64, 64, 2, false, 1, 4>(g, st); break;
+        case 'l': launch_g6<128, 128, 2, false, 1, 2>(g, st); break;
+        case 'm': launch_g6<64, 128, 2, false, 1, 2>(g, st); break;
+        case 'n': launch_g6<128, 64, 2, false, 1, 2>(g, st); break;
+        case 'o': launch_g6<64, 64, 3, true, 1, 2>(g, st); break;     // probe, 2 steps / stage
         default: launch_g6<64, 64, 4>(g, st); break;
     }
     FGR_CHECK_LAUNCH("gemm_g6");
