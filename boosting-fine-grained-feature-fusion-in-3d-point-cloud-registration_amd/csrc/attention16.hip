@@ -27,6 +27,8 @@
 //   V: [term 2][key 64][DH] f16, 16-B chunk index XOR ((key >> 2) & 1) << 1
 // Tile t of kv segment s sits at tile index kv_off[s] / 64 + s + t; the (e_k, e_v) scale
 // exponents of all tiles follow the images.
+#include <type_traits>
+
 #include "common.h"
 
 namespace fgr {
@@ -239,7 +241,22 @@ attn_f16x3_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __rest
 #pragma unroll
         for (int i = 0; i < NS; ++i) stage[i] = tiles[tid + 256 * i];
     }
-    for (int tt = 0; tt < ntile; ++tt) {
+    // transposed V read offsets (byte, within the V part of a tile image): tile-invariant
+    int voff[2][TD][2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int t = 0; t < TD; ++t) {
+            const int r0 = 32 * j + 4 * g + qq, r1 = r0 + 16;
+            const int ch = 2 * t + (pp >> 1);
+            voff[j][t][0] = unit_v<DH>() * 16 + r0 * (2 * DH) +
+                            ((ch ^ (((r0 >> 2) & 1) << 1)) * 16) + (pp & 1) * 8;
+            voff[j][t][1] = unit_v<DH>() * 16 + r1 * (2 * DH) +
+                            ((ch ^ (((r1 >> 2) & 1) << 1)) * 16) + (pp & 1) * 8;
+        }
+    // one key tile; MASK only for the last, partial tile (no per-key selects elsewhere)
+    auto tile = [&](int tt, auto mask_tag) {
+        constexpr bool MASK = decltype(mask_tag)::value;
         int2 e2;
         const u32x4* tbuf;
         if constexpr (GLDS) {
@@ -261,7 +278,7 @@ attn_f16x3_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __rest
             }
             tbuf = lds;
         }
-        const char* lbase = reinterpret_cast<const char*>(tbuf);
+        const uint32_t lb32 = (uint32_t)(uintptr_t)tbuf;
         const int valid = nk - tt * 64;
 
         f32x4 s[4];
@@ -280,7 +297,7 @@ attn_f16x3_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __rest
         }
         // s (scaled units) * f = log2-domain score; f > 0 so max commutes with it
         const float f = __builtin_ldexpf(1.f, -(e2.x + eq));
-        if (valid < 64) {
+        if constexpr (MASK) {
 #pragma unroll
             for (int n = 0; n < 4; ++n)
 #pragma unroll
@@ -323,18 +340,15 @@ attn_f16x3_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __rest
 #pragma unroll
             for (int t = 0; t < TD; ++t) {
                 f16x8 vf[2];
-                const int r0 = 32 * j + 4 * g + qq, r1 = r0 + 16;
-                const int ch = 2 * t + (pp >> 1);
-                const int off0 = r0 * (2 * DH) + ((ch ^ (((r0 >> 2) & 1) << 1)) * 16) + (pp & 1) * 8;
-                const int off1 = r1 * (2 * DH) + ((ch ^ (((r1 >> 2) & 1) << 1)) * 16) + (pp & 1) * 8;
 #pragma unroll
                 for (int tm = 0; tm < 2; ++tm) {
                     typedef __attribute__((address_space(3))) s16x4 lds_s4;
-                    const char* vb = lbase + unit_v<DH>() * 16 + tm * (128 * DH);
+                    // 32-bit LDS byte addresses (no 64-bit pointer arithmetic per read)
+                    const uint32_t vb = lb32 + tm * (128 * DH);
                     const s16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                        (lds_s4*)(uintptr_t)(uint32_t)(uintptr_t)(vb + off0));
+                        (lds_s4*)(uintptr_t)(vb + voff[j][t][0]));
                     const s16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                        (lds_s4*)(uintptr_t)(uint32_t)(uintptr_t)(vb + off1));
+                        (lds_s4*)(uintptr_t)(vb + voff[j][t][1]));
                     const s16x8 w8 = __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7);
                     vf[tm] = __builtin_bit_cast(f16x8, w8);
                 }
@@ -350,7 +364,11 @@ attn_f16x3_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __rest
         for (int t = 0; t < TD; ++t)
 #pragma unroll
             for (int r = 0; r < 4; ++r) acc[t][r] = __builtin_fmaf(tmp[t][r], fv, acc[t][r] * alpha);
-    }
+    };
+    const int nfull = nk / 64;                       // tiles with 64 valid keys
+    for (int tt = 0; tt < nfull; ++tt) tile(tt, std::false_type{});
+    if (nfull < ntile) tile(nfull, std::true_type{});
+
     // O^T (dh 16t + 4g + r, query c) / l
     const float inv = 1.0f / xg_sum16(l_run);
     if (qrow < qe) {
