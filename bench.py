@@ -170,12 +170,19 @@ def main():
     local_rank = int(os.environ.get('LOCAL_RANK', '0'))
     if world != args.gpus:
         raise SystemExit(f'--gpus {args.gpus} but WORLD_SIZE={world}')
-    torch.cuda.set_device(local_rank)
-    dev = torch.device('cuda', local_rank)
+    # one rank per GPU; FGREG_DIST_BACKEND=gloo runs the multi-rank path on fewer GPUs than
+    # ranks (ranks share devices round-robin) for a hardware rehearsal of the N > 1 code
+    backend = os.environ.get('FGREG_DIST_BACKEND', 'nccl')
+    local_dev = local_rank % max(torch.cuda.device_count(), 1) if backend == 'gloo' else local_rank
+    torch.cuda.set_device(local_dev)
+    dev = torch.device('cuda', local_dev)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group('nccl', device_id=dev)
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=dev)      # RCCL over xGMI
+        else:
+            dist.init_process_group(backend)
 
     wl = args.workload
     fgreg.set_precision(args.precision or PRECISION_DEFAULT.get(wl, 'fp32'))
@@ -249,7 +256,8 @@ def main():
             tail_ms, tail_inputs = test_tail(model, batch_src, batch_tgt, src, tgt, pose_gt, dev,
                                               args.steps)
 
-    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    el = torch.tensor([elapsed], dtype=torch.float64,
+                      device=dev if backend == 'nccl' else 'cpu')
     if dist is not None:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())

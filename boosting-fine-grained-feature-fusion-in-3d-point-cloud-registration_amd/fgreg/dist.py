@@ -37,6 +37,8 @@ def gather_pair_results(local: torch.Tensor, counts: Sequence[int], pair_dim: in
     numbers of pairs (`counts[r]`). Returns the concatenation in rank order."""
     world = dist.get_world_size()
     assert len(counts) == world
+    if local.is_cuda and dist.get_backend() == 'gloo':     # gloo: exchange host copies
+        return gather_pair_results(local.cpu(), counts, pair_dim).to(local.device)
     mx = max(counts)
     shape = list(local.shape)
     shape[pair_dim] = mx
