@@ -99,9 +99,10 @@ def _random_model(cfg, seed):
 
 # (kind, B, n_points): the two bench lines at their own sizes -- ModelNet B = 8 (the
 # headline bench batch, BASELINE configs[1]) and 3DMatch 20k + 20k, B = 1 (configs[2]) --
-# plus the smaller cases kept from round 1.
+# plus the smaller cases kept from round 1 and the uncropped 2048 + 2048-point stress input.
 FULL_CASES = [('modelnet', 2, None), ('modelnet', 8, None), ('3dmatch', 1, 8000),
-              ('3dmatch', 1, 20000)]
+              ('3dmatch', 1, 20000), ('modelnet_raw', 2, None)]
+CFG_OF = {'modelnet_raw': 'modelnet'}     # the raw-2048 stress input on ModelNet
 # elementwise bound (floor 1e-2 of the tensor's max magnitude): every entry of every
 # output, not only the largest ones, within 1e-3 relative
 ELEM_TOL, ELEM_FLOOR = 1e-3, 1e-2
@@ -111,7 +112,7 @@ ELEM_TOL, ELEM_FLOOR = 1e-3, 1e-2
 def test_forward_full_config_vs_oracle(gpu, kind, B, n_points):
     import fgreg.config as fc
     from fgreg.synthetic import make_batch
-    cfg = fc.get(kind)
+    cfg = fc.get(CFG_OF.get(kind, kind))
     model = _random_model(cfg, 11)
     sd = {k: v.clone() for k, v in model.state_dict().items()}
     kw = {} if n_points is None else {'n_points': n_points}

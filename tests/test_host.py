@@ -194,3 +194,16 @@ def test_training_mode_with_grad_raises_clearly():
         model(batch)
     with torch.no_grad(), pytest.raises(fgreg.FgrError):   # guard passes; CPU tensors refused
         model(batch)
+
+
+def test_load_fragment_formats(tmp_path):
+    """fgreg.data.load_fragment: numpy arrays in a .pth (the reference's fragment files, read
+    with torch.load(weights_only=True) + numpy allow-list), .npy and .npz (no pickle)."""
+    import os
+    from fgreg.data import load_fragment
+    a = np.random.default_rng(0).normal(size=(50, 3))
+    torch.save(a, os.path.join(tmp_path, 'a.pth'))
+    np.save(os.path.join(tmp_path, 'a.npy'), a)
+    np.savez(os.path.join(tmp_path, 'a.npz'), xyz=a)
+    for f in ('a.pth', 'a.npy', 'a.npz'):
+        assert np.array_equal(load_fragment(os.path.join(tmp_path, f)), a)
