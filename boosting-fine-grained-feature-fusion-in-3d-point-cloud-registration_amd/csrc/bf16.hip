@@ -451,11 +451,21 @@ extern "C" int fgr_gemm_bf16(const float* a, int64_t lda, const void* w_img, flo
     hipStream_t st = as_stream(stream);
     TimedCall timed_(st);
     // narrow outputs with long contractions: the 64 x 64 LDS-DMA g5 ('I', gemm5.hip; measured
-    // 1.2-1.5x faster there), otherwise the register-staged kernel below (FGR_GEMM_BF16_TILE
-    // A..R forces a g5 variant, anything else this kernel)
+    // 1.2-1.5x faster there); few tiles (<= 400 of 64 x 64) with K >= 512 and the short-M
+    // K >= 2048 layers: the two-k-group g5 ('S', 'T', 'W'); otherwise the register-staged
+    // kernel below (FGR_GEMM_BF16_TILE A..W forces a g5 variant, anything else this kernel)
     const char* force = getenv("FGR_GEMM_BF16_TILE");
-    const char cfg = force && force[0] ? force[0] : (n <= 256 && k >= 1000 ? 'I' : 'z');
-    if (cfg >= 'A' && cfg <= 'R' && k % 8 == 0) {
+    const int64_t tiles64 = (int64_t)ceil_div(m, 64) * ceil_div(n, 64);
+    char cfg;
+    if (force && force[0])
+        cfg = force[0];
+    else if (tiles64 <= 400 && k >= 512 && n >= 32)
+        cfg = (k >= 2048 || n <= 64) ? 'S' : ((n <= 128 && k >= 1024 && tiles64 > 256) ? 'T' : 'W');
+    else if (m <= 4096 && k >= 2048)
+        cfg = 'W';
+    else
+        cfg = n <= 256 && k >= 1000 ? 'I' : 'z';
+    if (cfg >= 'A' && cfg <= 'W' && k % 8 == 0) {
         gemm_g5_bf16(cfg, a, lda, w_img, ksteps_bf(k), c, ldc, bias, r, ldr, m, n, k, act,
                      vo ? 1 : 0, st);
         FGR_CHECK_LAUNCH("gemm_g5 (bf16)");

@@ -1180,16 +1180,22 @@ extern "C" int fgr_gemm_f16x3(const float* a, int64_t lda, const void* w_img, fl
     // tiles (v4 -- W fragments straight to registers -- for K >= 1024, double-buffered v2
     // for K >= 512), very tall ones 64 x 128; narrow outputs (N <= 256) and short row counts
     // (M <= 4096, N <= 512) the 64 x 64 LDS-DMA g5 ('I') when K % 8 == 0, else the 64 x 64 v4.
+    // Few tiles (<= 400 of 64 x 64, e.g. the 3DMatch transformer's 2 x 1060 tokens) with
+    // K >= 512: the two-k-group g5 ('W', 'T'; 8 waves per block) -- 1.1-1.45x there
+    // (profiles/r02_gemm_tiles_splitk*.txt).
     const char* force = getenv("FGR_GEMM16_TILE");
     const bool g5ok = k % 8 == 0;
+    const int64_t tiles64 = (int64_t)ceil_div(m, 64) * ceil_div(n, 64);
     char cfg;
     if (force && force[0])
         cfg = force[0];
-    else if (g5ok && m <= 4096 && n <= 512)
-        cfg = 'I';
+    else if (g5ok && tiles64 <= 400 && k >= 512 && n >= 32)
+        cfg = (n <= 128 && k >= 1024 && tiles64 > 256) ? 'T' : 'W';
+    else if (g5ok && m <= 4096)
+        cfg = (n <= 512 || (n <= 1024 && k <= 512)) ? 'I' : 'B';
     else if (n >= 512)
         cfg = k >= 1024 ? 'u' : (k >= 512 ? 'k' : 'b');
-    else if ((int64_t)ceil_div(m, 64) * ceil_div(n, 64) >= 2048)
+    else if (tiles64 >= 2048)
         cfg = 'b';
     else if (g5ok && (k >= 512 || m <= 16384))
         cfg = 'I';
@@ -1197,8 +1203,8 @@ extern "C" int fgr_gemm_f16x3(const float* a, int64_t lda, const void* w_img, fl
         cfg = 'f';
     else
         cfg = k <= 1024 ? 't' : 'e';
-    // g5 (gemm5.hip: LDS-DMA pipeline, A split after the read): A..J, K % 8 == 0 only
-    if (cfg >= 'A' && cfg <= 'R' && k % 8 == 0) {
+    // g5 (gemm5.hip: LDS-DMA pipeline, A split after the read): A..W, K % 8 == 0 only
+    if (cfg >= 'A' && cfg <= 'W' && k % 8 == 0) {
         gemm_g5_f16x3(cfg, a, lda, w_img, ksteps_h3(k), wsc, c, ldc, bias, r, ldr, m, n, k, act,
                       vo ? 1 : 0, st);
         FGR_CHECK_LAUNCH("gemm_g5");

@@ -87,9 +87,14 @@ __device__ __forceinline__ float finish5(float y, float b, float r, int act) {
     return act == FGR_ACT_RELU ? fmaxf(t, 0.f) : t;
 }
 
-// TERMS 2: f16x3 (W image with hi / lo terms + row scales); 1: bf16 (single-term image)
-template <int BM, int BN, int KS, int S, int TERMS, bool PIPE>
-__global__ void __launch_bounds__(256) gemm_g5(G5Args p) {
+// TERMS 2: f16x3 (W image with hi / lo terms + row scales); 1: bf16 (single-term image).
+// KW k-groups of 4 waves (intra-block split-K): group h computes the k32-steps ks = h, h + KW,
+// ... of every stage for the same rows, so a block of a short-M GEMM (~1 block per CU) keeps
+// KW waves per SIMD and one wave's convert / LDS-read VALU work overlaps another's MFMAs; the
+// groups' accumulators are merged through LDS at the end (fixed order, deterministic).
+template <int BM, int BN, int KS, int S, int TERMS, bool PIPE, int KW = 1>
+__global__ void __launch_bounds__(256 * KW) gemm_g5(G5Args p) {
+    constexpr int NW = 4 * KW;                 // waves per block
     constexpr int WR = BM / 4;                 // rows per wave
     constexpr int TM = WR / 16;                // 16-row fragments per wave
     constexpr int TN = BN / 16;                // W panels per block
@@ -99,8 +104,9 @@ __global__ void __launch_bounds__(256) gemm_g5(G5Args p) {
     constexpr int ST = A_UNITS + W_UNITS;      // units per stage
     constexpr int NP = ST / 64;                // DMA wave-instructions per stage
     constexpr int A_PIECES = A_UNITS / 64;
-    static_assert(TM >= 1 && NP % 4 == 0, "tile");
-    constexpr int P = NP / 4;                  // per wave per stage
+    static_assert(TM >= 1 && NP % NW == 0 && KS % KW == 0, "tile");
+    static_assert(!PIPE || KW == 1, "pipelined g5: one k-group");
+    constexpr int P = NP / NW;                 // per wave per stage
     __shared__ u32x4 lds[S * ST];
 
     const int nbm = (p.M + BM - 1) / BM, nbn = (p.N + BN - 1) / BN;
@@ -114,20 +120,21 @@ __global__ void __launch_bounds__(256) gemm_g5(G5Args p) {
     const int m0 = bm * BM, n0 = bn * BN;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably wave-uniform
+    const int rw = wv & 3, kg = wv >> 2;                     // row slice, k-group
     const int g = lane >> 4, c = lane & 15;
     const int npanel = (p.N + 15) / 16;
     const int nk = (p.K + 32 * KS - 1) / (32 * KS);          // stages
 
     // ---- DMA sources of this wave's P pieces (per stage: + stage * KS * 32 floats / units)
-    // (A_PIECES % 4 == 0: piece j of every wave is an A piece iff j < A_PIECES / 4)
-    static_assert(A_PIECES % 4 == 0, "A pieces");
+    // (A_PIECES % NW == 0: piece j of every wave is an A piece iff j < A_PIECES / NW)
+    static_assert(A_PIECES % NW == 0, "A pieces");
     const float* asrc[P];
     int akoff[P];                                            // k offset of the chunk in its step
     const u32x4* wsrc[P];
 #pragma unroll
     for (int j = 0; j < P; ++j) {
-        const int q = wv + 4 * j;
-        if (j < A_PIECES / 4) {
+        const int q = wv + NW * j;
+        if (j < A_PIECES / NW) {
             const int ks = q / (BM / 8);
             const int row = (q % (BM / 8)) * 8 + (lane >> 3);
             const int ch = (lane & 7) ^ swz(row);
@@ -150,10 +157,10 @@ __global__ void __launch_bounds__(256) gemm_g5(G5Args p) {
         const bool full = k0 + KS * 32 <= p.K;                  // wave-uniform
 #pragma unroll
         for (int j = 0; j < P; ++j) {
-            const int q = wv + 4 * j;
+            const int q = wv + NW * j;
             lds_void* dst = (lds_void*)((__attribute__((address_space(3))) char*)base + q * 1024);
             const void* src;
-            if (j < A_PIECES / 4) {
+            if (j < A_PIECES / NW) {
                 src = (full || k0 + akoff[j] < p.K) ? (const void*)(asrc[j] + k0)
                                                     : (const void*)g5_zero;
             } else {
@@ -181,7 +188,7 @@ __global__ void __launch_bounds__(256) gemm_g5(G5Args p) {
                 wf[j][tt] = st[A_UNITS + (j * KS + ks) * W_PANEL + tt * 64 + lane];
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
-            const int row = wv * WR + 16 * i + c;
+            const int row = rw * WR + 16 * i + c;
             const u32x4* ar = st + (ks * BM + row) * 8;
             ua[i][0] = ar[(2 * g) ^ swz(row)];
             ua[i][1] = ar[(2 * g + 1) ^ swz(row)];
@@ -275,7 +282,8 @@ __global__ void __launch_bounds__(256) gemm_g5(G5Args p) {
             if (s + S - 1 < nk) issue(s + S - 1);
             const u32x4* st = lds + (s % S) * ST;
 #pragma unroll
-            for (int ks = 0; ks < KS; ++ks) {
+            for (int kk = 0; kk < KS / KW; ++kk) {
+                const int ks = kk * KW + kg;
                 u32x4 ua[TM][2], wf[TN][TERMS], bh[TM], bl[TM];
                 read_frags(st, ks, ua, wf);
                 convert(ua, bh, bl);
@@ -327,10 +335,51 @@ __global__ void __launch_bounds__(256) gemm_g5(G5Args p) {
         }
     }
 
-    // epilogue: lane holds C[m = m0 + wv WR + 16i + c][n = n0 + 16j + 4g + r], r = 0..3
+    if constexpr (KW == 2) {
+        // merge the k-groups: group 1 parks its accumulators (+ f16x3 row exponents) in the
+        // drained stage buffers, group 0 adds them at the common (smaller) row scale; every
+        // DMA retired at the last stage (vmcnt 0), the barrier retires every stage read
+        static_assert(S * ST * 16 >= 4 * TN * TM * 64 * 16 + 4 * TM * 64 * 4, "merge space");
+        __syncthreads();
+        f32x4* xa = reinterpret_cast<f32x4*>(lds);
+        int* xs = reinterpret_cast<int*>(xa + 4 * TN * TM * 64);
+        if (kg == 1) {
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int i = 0; i < TM; ++i) xa[((rw * TN + j) * TM + i) * 64 + lane] = acc[j][i];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) xs[(rw * TM + i) * 64 + lane] = sh[i];
+        }
+        __syncthreads();
+        if (kg == 1) return;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            float f0 = 1.f, f1 = 1.f;
+            if constexpr (TERMS == 2) {
+                // an unset exponent means that group saw only zeros (its accumulators are 0)
+                const int s1 = xs[(rw * TM + i) * 64 + lane];
+                if (s1 != SH_UNSET) {
+                    if (sh[i] == SH_UNSET) {
+                        sh[i] = s1;
+                    } else {
+                        const int s0 = min(sh[i], s1);
+                        f0 = __builtin_ldexpf(1.f, s0 - sh[i]);
+                        f1 = __builtin_ldexpf(1.f, s0 - s1);
+                        sh[i] = s0;
+                    }
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+                acc[j][i] = acc[j][i] * f0 + xa[((rw * TN + j) * TM + i) * 64 + lane] * f1;
+        }
+    }
+
+    // epilogue: lane holds C[m = m0 + rw WR + 16i + c][n = n0 + 16j + 4g + r], r = 0..3
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
-        const int m = m0 + wv * WR + 16 * i + c;
+        const int m = m0 + rw * WR + 16 * i + c;
         if (m >= p.M) continue;
         const float rs = TERMS == 2 ? __builtin_ldexpf(1.f, -sh[i]) : 1.f;   // 0: all-zero row
         float* crow = p.C + (int64_t)m * p.ldc;
@@ -362,11 +411,11 @@ __global__ void __launch_bounds__(256) gemm_g5(G5Args p) {
     }
 }
 
-template <int BM, int BN, int KS, int S, int TERMS, bool PIPE = false>
+template <int BM, int BN, int KS, int S, int TERMS, bool PIPE = false, int KW = 1>
 void launch_g5(const G5Args& a, hipStream_t st) {
     const int nbm = (a.M + BM - 1) / BM, nbn = (a.N + BN - 1) / BN;
-    hipLaunchKernelGGL((gemm_g5<BM, BN, KS, S, TERMS, PIPE>), dim3((unsigned)(nbm * nbn)),
-                       dim3(256), 0, st, a);
+    hipLaunchKernelGGL((gemm_g5<BM, BN, KS, S, TERMS, PIPE, KW>), dim3((unsigned)(nbm * nbn)),
+                       dim3(256 * KW), 0, st, a);
 }
 
 template <int TERMS>
@@ -391,6 +440,12 @@ bool dispatch_g5(char cfg, const G5Args& a, hipStream_t st) {
         case 'P': launch_g5<64, 256, 1, 3, TERMS, true>(a, st); break;
         case 'Q': launch_g5<64, 128, 1, 3, TERMS, true>(a, st); break;
         case 'R': launch_g5<128, 128, 1, 4, TERMS, true>(a, st); break;
+        // two k-groups (512 threads): S..W
+        case 'S': launch_g5<64, 64, 2, 3, TERMS, false, 2>(a, st); break;
+        case 'T': launch_g5<64, 128, 2, 3, TERMS, false, 2>(a, st); break;
+        case 'U': launch_g5<64, 64, 2, 4, TERMS, false, 2>(a, st); break;
+        case 'V': launch_g5<128, 64, 2, 3, TERMS, false, 2>(a, st); break;
+        case 'W': launch_g5<64, 64, 2, 2, TERMS, false, 2>(a, st); break;
         default: return false;
     }
     return true;

@@ -336,7 +336,7 @@ def test_gemm_split_vs_fp64(gpu, m, n, k, mode, tol):
         fl.set_mode(old)
 
 
-@pytest.mark.parametrize('tile', ['', 'b', 'I', 'K', 'O'])
+@pytest.mark.parametrize('tile', ['', 'b', 'I', 'K', 'O', 'S'])
 def test_gemm_f16x3_dynamic_range(gpu, tile, monkeypatch):
     """f16x3 row scaling (tile: '' the default dispatch, else FGR_GEMM16_TILE) under
     adversarial magnitudes: rows at 1e-15 .. 1e15 (far outside fp16's range), all-zero rows, rows whose first k chunks are zero, rows that grow by
@@ -375,7 +375,7 @@ def test_gemm_f16x3_dynamic_range(gpu, tile, monkeypatch):
     del ref
 
 
-@pytest.mark.parametrize('tile', list('abcdefghijklmnopqrstuvwx') + list('ABCDEFGHIJKLMNOPQR'))
+@pytest.mark.parametrize('tile', list('abcdefghijklmnopqrstuvwx') + list('ABCDEFGHIJKLMNOPQRSTUVW'))
 def test_gemm_f16x3_tiles(gpu, tile, monkeypatch):
     """Every f16x3 tile / pipeline variant (FGR_GEMM16_TILE; A..R: the LDS-DMA g5 kernels of
     gemm5.hip) at fp32 accuracy on ragged shapes (M, N, K not multiples of the tiles; K % 64

@@ -1,6 +1,6 @@
 """GEMM tile sweep (development tool, GPU): times fgr_gemm_f16x3 per tile configuration
 (FGR_GEMM16_TILE) on the forward's shapes and checks every variant against an fp64 product.
-usage: python tools/gemm_tiles.py [configs] [bf16] > gpurun_out/gemm_tiles.txt
+usage: python tools/gemm_tiles.py [configs] [bf16] [3d] > gpurun_out/gemm_tiles.txt
 (bf16: fgr_gemm_bf16 with FGR_GEMM_BF16_TILE, checked against bf16-rounded operands)"""
 import os
 import sys
@@ -16,6 +16,11 @@ SHAPES = [(9544, 768, 256), (9544, 1024, 2048), (9544, 256, 1024), (9544, 256, 3
           (9544, 1792, 256), (57264, 256, 256), (11472, 896, 128), (2120, 1536, 512),
           (2120, 512, 1024), (2120, 512, 512), (26778, 256, 512), (40000, 128, 256),
           (9543, 130, 1000), (333, 896, 128)]
+# the 3DMatch / 3DLoMatch transformer and head shapes (2 x 1060 tokens) and its decoder
+SHAPES_3D = [(2120, 1536, 512), (2120, 512, 1024), (2120, 512, 512), (2120, 1024, 512),
+             (2120, 1024, 2048), (2120, 256, 3840), (2120, 128, 1920), (2120, 256, 1024),
+             (2120, 256, 512), (2120, 896, 128), (2120, 1792, 256), (10967, 128, 1920),
+             (10967, 512, 1024), (12720, 512, 512), (10967, 256, 512), (10967, 64, 960)]
 
 
 def timeit(fn, iters=20):
@@ -41,12 +46,13 @@ def timeit(fn, iters=20):
 
 def main():
     cfgs = sys.argv[1] if len(sys.argv) > 1 else 'btukABCDEFGHIJ'
-    bf = len(sys.argv) > 2 and sys.argv[2] == 'bf16'
+    bf = 'bf16' in sys.argv[2:]
+    shapes = SHAPES_3D if '3d' in sys.argv[2:] else SHAPES
     env = 'FGR_GEMM_BF16_TILE' if bf else 'FGR_GEMM16_TILE'
     dev = torch.device('cuda:0')
     lin.set_mode('bf16' if bf else 'f16x3')
     g = torch.Generator(device=dev).manual_seed(0)
-    for (M, N, K) in SHAPES:
+    for (M, N, K) in shapes:
         x = torch.randn(M, K, device=dev, generator=g)
         w = torch.randn(N, K, device=dev, generator=g) * 0.05
         if bf:
