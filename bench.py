@@ -113,8 +113,8 @@ OTHER = {
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument('--gpus', type=int, default=1)
-    p.add_argument('--steps', type=int, default=20)
-    p.add_argument('--warmup', type=int, default=5)
+    p.add_argument('--steps', type=int, default=50)
+    p.add_argument('--warmup', type=int, default=10)
     p.add_argument('--pairs-per-gpu', type=int, default=None,
                    help='default 8 (modelnet, raw2048) / 1 (3dmatch)')
     p.add_argument('--workload', choices=tuple(METRIC), default='modelnet',

@@ -1190,11 +1190,11 @@ extern "C" int fgr_gemm_f16x3(const float* a, int64_t lda, const void* w_img, fl
     if (force && force[0])
         cfg = force[0];
     else if (g5ok && tiles64 <= 400 && k >= 512 && n >= 32)
-        cfg = (n <= 128 && k >= 1024 && tiles64 > 256) ? 'T' : 'W';
+        cfg = (k >= 2048 || n <= 64) ? 'S' : ((n <= 128 && k >= 1024 && tiles64 > 256) ? 'T' : 'W');
     else if (g5ok && m <= 4096)
         cfg = (n <= 512 || (n <= 1024 && k <= 512)) ? 'I' : 'B';
     else if (n >= 512)
-        cfg = k >= 1024 ? 'u' : (k >= 512 ? 'k' : 'b');
+        cfg = k >= 1024 ? 'u' : (k >= 512 ? (g5ok ? 'B' : 'k') : 'b');
     else if (tiles64 >= 2048)
         cfg = 'b';
     else if (g5ok && (k >= 512 || m <= 16384))
@@ -1204,9 +1204,10 @@ extern "C" int fgr_gemm_f16x3(const float* a, int64_t lda, const void* w_img, fl
     else
         cfg = k <= 1024 ? 't' : 'e';
     // g5 (gemm5.hip: LDS-DMA pipeline, A split after the read): A..W, K % 8 == 0 only
-    if (cfg >= 'A' && cfg <= 'W' && k % 8 == 0) {
-        gemm_g5_f16x3(cfg, a, lda, w_img, ksteps_h3(k), wsc, c, ldc, bias, r, ldr, m, n, k, act,
-                      vo ? 1 : 0, st);
+    if (((cfg >= 'A' && cfg <= 'W') || (cfg >= '0' && cfg <= '7')) && k % 8 == 0) {
+        FGR_REQUIRE(gemm_g5_f16x3(cfg, a, lda, w_img, ksteps_h3(k), wsc, c, ldc, bias, r, ldr, m, n, k, act,
+                      vo ? 1 : 0, st),
+                    "fgr_gemm_f16x3: g5 variant %c unavailable", cfg);
         FGR_CHECK_LAUNCH("gemm_g5");
         return FGR_OK;
     }

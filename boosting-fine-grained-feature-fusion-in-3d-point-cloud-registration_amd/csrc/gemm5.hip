@@ -47,6 +47,7 @@ __device__ __attribute__((aligned(16))) float g5_zero[4];
 
 struct G5Args {
     const float* A; int64_t lda;
+    const float* zero;                // g5_zero's device address (no GOT load in the loop)
     const u32x4* W; int ksteps;       // image [panel][kstep][term][g 4][16] x 16 B
     const float* wsc;                 // f16x3: per n 2^-e_n (padded to 16); bf16: unused
     float* C; int64_t ldc;
@@ -78,6 +79,29 @@ __device__ __forceinline__ float xg_max(float v) {        // max over lanes c, c
     return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
 }
 
+// max(|a|, |b|, |c|) in one v_max3_f32 (no NaN canonicalisation: finite activations)
+__device__ __forceinline__ float max3_abs(float a, float b, float c) {
+    float r;
+    asm("v_max3_f32 %0, |%1|, |%2|, |%3|" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+// packed f16 (hi terms) of a sc, b sc: v_fma_mixlo / mixhi (round to nearest even, as a
+// v_cvt_f16_f32 of the exact product)
+__device__ __forceinline__ unsigned split_hi2(float a, float b, float sc) {
+    unsigned d;
+    asm("v_fma_mixlo_f16 %0, %1, %2, 0" : "=v"(d) : "v"(a), "v"(sc));
+    asm("v_fma_mixhi_f16 %0, %1, %2, 0" : "+v"(d) : "v"(b), "v"(sc));
+    return d;
+}
+// packed f16 (lo terms) of a sc - hi_a, b sc - hi_b (hi from split_hi2: f16 halves of h)
+__device__ __forceinline__ unsigned split_lo2(float a, float b, float sc, unsigned h) {
+    unsigned d;
+    asm("v_fma_mixlo_f16 %0, %1, %2, -%3 op_sel_hi:[0,0,1]" : "=v"(d) : "v"(a), "v"(sc), "v"(h));
+    asm("v_fma_mixhi_f16 %0, %1, %2, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+        : "+v"(d) : "v"(b), "v"(sc), "v"(h));
+    return d;
+}
+
 __device__ __forceinline__ float finish5(float y, float b, float r, int act) {
     if (act == FGR_ACT_RELU_RES_LEAKY) {
         const float t = fmaxf(y + b, 0.f) + r;
@@ -92,19 +116,24 @@ __device__ __forceinline__ float finish5(float y, float b, float r, int act) {
 // ... of every stage for the same rows, so a block of a short-M GEMM (~1 block per CU) keeps
 // KW waves per SIMD and one wave's convert / LDS-read VALU work overlaps another's MFMAs; the
 // groups' accumulators are merged through LDS at the end (fixed order, deterministic).
-template <int BM, int BN, int KS, int S, int TERMS, bool PIPE, int KW = 1>
+// WC waves across the columns (1: every wave owns BM / 4 rows x all BN columns; 2: a 2 x 2
+// layout, BM / 2 rows x BN / 2 columns per wave -- a third less LDS read traffic per MFMA,
+// each A row split by the two waves that share it).
+template <int BM, int BN, int KS, int S, int TERMS, bool PIPE, int KW = 1, int WC = 1>
 __global__ void __launch_bounds__(256 * KW) gemm_g5(G5Args p) {
     constexpr int NW = 4 * KW;                 // waves per block
-    constexpr int WR = BM / 4;                 // rows per wave
+    constexpr int RW = 4 / WC;                 // waves across the rows
+    constexpr int WR = BM / RW;                // rows per wave
     constexpr int TM = WR / 16;                // 16-row fragments per wave
     constexpr int TN = BN / 16;                // W panels per block
+    constexpr int TNW = TN / WC;               // W panels per wave
     constexpr int A_UNITS = BM * 8 * KS;       // [ks][row][8 chunks] x 16 B
     constexpr int W_PANEL = TERMS * 64;        // units of one (panel, kstep)
     constexpr int W_UNITS = TN * KS * W_PANEL;
     constexpr int ST = A_UNITS + W_UNITS;      // units per stage
     constexpr int NP = ST / 64;                // DMA wave-instructions per stage
     constexpr int A_PIECES = A_UNITS / 64;
-    static_assert(TM >= 1 && NP % NW == 0 && KS % KW == 0, "tile");
+    static_assert(TM >= 1 && TNW >= 1 && TN % WC == 0 && NP % NW == 0 && KS % KW == 0, "tile");
     static_assert(!PIPE || KW == 1, "pipelined g5: one k-group");
     constexpr int P = NP / NW;                 // per wave per stage
     __shared__ u32x4 lds[S * ST];
@@ -120,7 +149,8 @@ __global__ void __launch_bounds__(256 * KW) gemm_g5(G5Args p) {
     const int m0 = bm * BM, n0 = bn * BN;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably wave-uniform
-    const int rw = wv & 3, kg = wv >> 2;                     // row slice, k-group
+    const int w4 = wv & 3, kg = wv >> 2;                     // wave in its k-group, k-group
+    const int rw = w4 / WC, cw = w4 % WC;                    // row slice, column slice
     const int g = lane >> 4, c = lane & 15;
     const int npanel = (p.N + 15) / 16;
     const int nk = (p.K + 32 * KS - 1) / (32 * KS);          // stages
@@ -154,38 +184,51 @@ __global__ void __launch_bounds__(256 * KW) gemm_g5(G5Args p) {
     auto issue = [&](int s) {
         lds_void* base = (lds_void*)(lds + (s % S) * ST);
         const int k0 = s * KS * 32;
-        const bool full = k0 + KS * 32 <= p.K;                  // wave-uniform
+        if (k0 + KS * 32 <= p.K) {                              // wave-uniform: no K tail
 #pragma unroll
-        for (int j = 0; j < P; ++j) {
-            const int q = wv + NW * j;
-            lds_void* dst = (lds_void*)((__attribute__((address_space(3))) char*)base + q * 1024);
-            const void* src;
-            if (j < A_PIECES / NW) {
-                src = (full || k0 + akoff[j] < p.K) ? (const void*)(asrc[j] + k0)
-                                                    : (const void*)g5_zero;
-            } else {
-                src = wsrc[j] + (int64_t)s * KS * W_PANEL;
+            for (int j = 0; j < P; ++j) {
+                const int q = wv + NW * j;
+                lds_void* dst = (lds_void*)((__attribute__((address_space(3))) char*)base + q * 1024);
+                const void* src = j < A_PIECES / NW ? (const void*)(asrc[j] + k0)
+                                                    : (const void*)(wsrc[j] + (int64_t)s * KS * W_PANEL);
+                __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
             }
-            __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
+        } else {
+#pragma unroll
+            for (int j = 0; j < P; ++j) {
+                const int q = wv + NW * j;
+                lds_void* dst = (lds_void*)((__attribute__((address_space(3))) char*)base + q * 1024);
+                const void* src;
+                if (j < A_PIECES / NW) {
+                    src = k0 + akoff[j] < p.K ? (const void*)(asrc[j] + k0) : (const void*)p.zero;
+                } else {
+                    src = wsrc[j] + (int64_t)s * KS * W_PANEL;
+                }
+                __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
+            }
         }
     };
 
-    f32x4 acc[TN][TM];
+    f32x4 acc[TNW][TM];
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
+    for (int j = 0; j < TNW; ++j)
 #pragma unroll
         for (int i = 0; i < TM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
     int sh[TM];
+    float scv[TM];                             // 2^sh (1 while unset)
 #pragma unroll
-    for (int i = 0; i < TM; ++i) sh[i] = SH_UNSET;
+    for (int i = 0; i < TM; ++i) {
+        sh[i] = SH_UNSET;
+        scv[i] = 1.f;
+    }
 
-    // fragment reads of one k32-step: W panels (A operand), this wave's raw fp32 rows
-    auto read_frags = [&](const u32x4* st, int ks, u32x4 (&ua)[TM][2], u32x4 (&wf)[TN][TERMS]) {
+    // fragment reads of one k32-step: this wave's W panels (A operand) and raw fp32 rows
+    auto read_frags = [&](const u32x4* st, int ks, u32x4 (&ua)[TM][2], u32x4 (&wf)[TNW][TERMS]) {
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
+        for (int j = 0; j < TNW; ++j)
 #pragma unroll
             for (int tt = 0; tt < TERMS; ++tt)
-                wf[j][tt] = st[A_UNITS + (j * KS + ks) * W_PANEL + tt * 64 + lane];
+                wf[j][tt] = st[A_UNITS + ((cw * TNW + j) * KS + ks) * W_PANEL + tt * 64 + lane];
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
             const int row = rw * WR + 16 * i + c;
@@ -204,29 +247,35 @@ __global__ void __launch_bounds__(256 * KW) gemm_g5(G5Args p) {
                                 __uint_as_float(u1[0]), __uint_as_float(u1[1]),
                                 __uint_as_float(u1[2]), __uint_as_float(u1[3])};
             if constexpr (TERMS == 2) {
-                float cm = fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3])));
-                cm = fmaxf(cm, fmaxf(fmaxf(fabsf(x[4]), fabsf(x[5])), fmaxf(fabsf(x[6]), fabsf(x[7]))));
-                cm = xg_max(cm);
-                const bool lower = cm > 0.f && __builtin_amdgcn_frexp_expf(cm) + sh[i] > 15;
-                if (__builtin_amdgcn_ballot_w64(lower)) {
+                // the lowering test is monotone in the row max, so a lane whose own 8 values
+                // do not trigger it cannot make the row trigger: the exact row max (2
+                // permlane swaps) is only formed when some lane's values do (first chunk of
+                // a row, or a chunk that grows past the current scale)
+                float cm = max3_abs(x[0], x[1], x[2]);
+                cm = max3_abs(x[3], x[4], cm);
+                cm = fmaxf(cm, max3_abs(x[5], x[6], x[7]));
+                const bool may = cm > 0.f && __builtin_amdgcn_frexp_expf(cm) + sh[i] > 15;
+                if (__builtin_amdgcn_ballot_w64(may)) {
+                    cm = xg_max(cm);
+                    const bool lower = cm > 0.f && __builtin_amdgcn_frexp_expf(cm) + sh[i] > 15;
                     const int nsh = lower ? min(8 - __builtin_amdgcn_frexp_expf(cm), 127) : sh[i];
                     const float f = (sh[i] == SH_UNSET || !lower) ? 1.f
                                                                    : __builtin_ldexpf(1.f, nsh - sh[i]);
 #pragma unroll
-                    for (int j = 0; j < TN; ++j) acc[j][i] *= f;
+                    for (int j = 0; j < TNW; ++j) acc[j][i] *= f;
                     sh[i] = nsh;
+                    scv[i] = __builtin_ldexpf(1.f, sh[i] == SH_UNSET ? 0 : sh[i]);
                 }
-                const float sc = __builtin_ldexpf(1.f, sh[i] == SH_UNSET ? 0 : sh[i]);
-                f16x8 h, m;
+                // hi = f16(x sc), lo = f16(x sc - hi) by v_fma_mix (x sc exact: power of two;
+                // x sc - hi exact in fp32): one VALU per term and element
+                u32x4 hh, mm;
 #pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    const float xs = x[e] * sc;
-                    const _Float16 hv = (_Float16)xs;
-                    h[e] = hv;
-                    m[e] = (_Float16)(xs - (float)hv);
+                for (int e = 0; e < 4; ++e) {
+                    hh[e] = split_hi2(x[2 * e], x[2 * e + 1], scv[i]);
+                    mm[e] = split_lo2(x[2 * e], x[2 * e + 1], scv[i], hh[e]);
                 }
-                bh[i] = __builtin_bit_cast(u32x4, h);
-                bl[i] = __builtin_bit_cast(u32x4, m);
+                bh[i] = hh;
+                bl[i] = mm;
             } else {
                 bf16x8 h;
 #pragma unroll
@@ -236,9 +285,9 @@ __global__ void __launch_bounds__(256 * KW) gemm_g5(G5Args p) {
             }
         }
     };
-    auto mma = [&](const u32x4 (&wf)[TN][TERMS], const u32x4 (&bh)[TM], const u32x4 (&bl)[TM]) {
+    auto mma = [&](const u32x4 (&wf)[TNW][TERMS], const u32x4 (&bh)[TM], const u32x4 (&bl)[TM]) {
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
+        for (int j = 0; j < TNW; ++j) {
             if constexpr (TERMS == 2) {
                 const f16x8 wh = __builtin_bit_cast(f16x8, wf[j][0]);
                 const f16x8 wl = __builtin_bit_cast(f16x8, wf[j][1]);
@@ -284,7 +333,7 @@ __global__ void __launch_bounds__(256 * KW) gemm_g5(G5Args p) {
 #pragma unroll
             for (int kk = 0; kk < KS / KW; ++kk) {
                 const int ks = kk * KW + kg;
-                u32x4 ua[TM][2], wf[TN][TERMS], bh[TM], bl[TM];
+                u32x4 ua[TM][2], wf[TNW][TERMS], bh[TM], bl[TM];
                 read_frags(st, ks, ua, wf);
                 convert(ua, bh, bl);
                 mma(wf, bh, bl);
@@ -301,7 +350,7 @@ __global__ void __launch_bounds__(256 * KW) gemm_g5(G5Args p) {
             else wait_vm_lgkm0<0>();
         }
         __builtin_amdgcn_s_barrier();
-        u32x4 ua[TM][2], wf[TN][TERMS], bh[TM], bl[TM];
+        u32x4 ua[TM][2], wf[TNW][TERMS], bh[TM], bl[TM];
         read_frags(lds, 0, ua, wf);
         convert(ua, bh, bl);
         for (int s = 0; s < nk; ++s) {
@@ -321,12 +370,12 @@ __global__ void __launch_bounds__(256 * KW) gemm_g5(G5Args p) {
                 }
                 __builtin_amdgcn_s_barrier();
                 if (s + S - 1 < nk) issue(s + S - 1);
-                u32x4 ua2[TM][2], wf2[TN][TERMS];
+                u32x4 ua2[TM][2], wf2[TNW][TERMS];
                 read_frags(lds + ((s + 1) % S) * ST, 0, ua2, wf2);
                 mma(wf, bh, bl);
                 convert(ua2, bh, bl);
 #pragma unroll
-                for (int j = 0; j < TN; ++j)
+                for (int j = 0; j < TNW; ++j)
 #pragma unroll
                     for (int tt = 0; tt < TERMS; ++tt) wf[j][tt] = wf2[j][tt];
             } else {
@@ -339,17 +388,17 @@ __global__ void __launch_bounds__(256 * KW) gemm_g5(G5Args p) {
         // merge the k-groups: group 1 parks its accumulators (+ f16x3 row exponents) in the
         // drained stage buffers, group 0 adds them at the common (smaller) row scale; every
         // DMA retired at the last stage (vmcnt 0), the barrier retires every stage read
-        static_assert(S * ST * 16 >= 4 * TN * TM * 64 * 16 + 4 * TM * 64 * 4, "merge space");
+        static_assert(S * ST * 16 >= 4 * TNW * TM * 64 * 16 + 4 * TM * 64 * 4, "merge space");
         __syncthreads();
         f32x4* xa = reinterpret_cast<f32x4*>(lds);
-        int* xs = reinterpret_cast<int*>(xa + 4 * TN * TM * 64);
+        int* xs = reinterpret_cast<int*>(xa + 4 * TNW * TM * 64);
         if (kg == 1) {
 #pragma unroll
-            for (int j = 0; j < TN; ++j)
+            for (int j = 0; j < TNW; ++j)
 #pragma unroll
-                for (int i = 0; i < TM; ++i) xa[((rw * TN + j) * TM + i) * 64 + lane] = acc[j][i];
+                for (int i = 0; i < TM; ++i) xa[((w4 * TNW + j) * TM + i) * 64 + lane] = acc[j][i];
 #pragma unroll
-            for (int i = 0; i < TM; ++i) xs[(rw * TM + i) * 64 + lane] = sh[i];
+            for (int i = 0; i < TM; ++i) xs[(w4 * TM + i) * 64 + lane] = sh[i];
         }
         __syncthreads();
         if (kg == 1) return;
@@ -358,7 +407,7 @@ __global__ void __launch_bounds__(256 * KW) gemm_g5(G5Args p) {
             float f0 = 1.f, f1 = 1.f;
             if constexpr (TERMS == 2) {
                 // an unset exponent means that group saw only zeros (its accumulators are 0)
-                const int s1 = xs[(rw * TM + i) * 64 + lane];
+                const int s1 = xs[(w4 * TM + i) * 64 + lane];
                 if (s1 != SH_UNSET) {
                     if (sh[i] == SH_UNSET) {
                         sh[i] = s1;
@@ -371,12 +420,12 @@ __global__ void __launch_bounds__(256 * KW) gemm_g5(G5Args p) {
                 }
             }
 #pragma unroll
-            for (int j = 0; j < TN; ++j)
-                acc[j][i] = acc[j][i] * f0 + xa[((rw * TN + j) * TM + i) * 64 + lane] * f1;
+            for (int j = 0; j < TNW; ++j)
+                acc[j][i] = acc[j][i] * f0 + xa[((w4 * TNW + j) * TM + i) * 64 + lane] * f1;
         }
     }
 
-    // epilogue: lane holds C[m = m0 + rw WR + 16i + c][n = n0 + 16j + 4g + r], r = 0..3
+    // epilogue: lane holds C[m = m0 + rw WR + 16i + c][n = n0 + 16 (cw TNW + j) + 4g + r]
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
         const int m = m0 + rw * WR + 16 * i + c;
@@ -385,8 +434,8 @@ __global__ void __launch_bounds__(256 * KW) gemm_g5(G5Args p) {
         float* crow = p.C + (int64_t)m * p.ldc;
         const float* rrow = p.R ? p.R + (int64_t)m * p.ldr : nullptr;
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            const int n = n0 + 16 * j + 4 * g;
+        for (int j = 0; j < TNW; ++j) {
+            const int n = n0 + 16 * (cw * TNW + j) + 4 * g;
             if (n >= p.N) continue;
             float4 ws = make_float4(1.f, 1.f, 1.f, 1.f);
             if constexpr (TERMS == 2) ws = *reinterpret_cast<const float4*>(p.wsc + n);
@@ -411,15 +460,24 @@ __global__ void __launch_bounds__(256 * KW) gemm_g5(G5Args p) {
     }
 }
 
-template <int BM, int BN, int KS, int S, int TERMS, bool PIPE = false, int KW = 1>
+template <int BM, int BN, int KS, int S, int TERMS, bool PIPE = false, int KW = 1, int WC = 1>
 void launch_g5(const G5Args& a, hipStream_t st) {
     const int nbm = (a.M + BM - 1) / BM, nbn = (a.N + BN - 1) / BN;
-    hipLaunchKernelGGL((gemm_g5<BM, BN, KS, S, TERMS, PIPE, KW>), dim3((unsigned)(nbm * nbn)),
+    hipLaunchKernelGGL((gemm_g5<BM, BN, KS, S, TERMS, PIPE, KW, WC>), dim3((unsigned)(nbm * nbn)),
                        dim3(256 * KW), 0, st, a);
+}
+
+const float* g5_zero_ptr() {
+    static const float* z = [] {
+        void* p = nullptr;
+        return hipGetSymbolAddress(&p, HIP_SYMBOL(g5_zero)) == hipSuccess ? (const float*)p : nullptr;
+    }();
+    return z;
 }
 
 template <int TERMS>
 bool dispatch_g5(char cfg, const G5Args& a, hipStream_t st) {
+    if (!a.zero) return false;
     switch (cfg) {
         case 'A': launch_g5<64, 64, 1, 4, TERMS>(a, st); break;
         case 'B': launch_g5<64, 128, 1, 3, TERMS>(a, st); break;
@@ -446,6 +504,15 @@ bool dispatch_g5(char cfg, const G5Args& a, hipStream_t st) {
         case 'U': launch_g5<64, 64, 2, 4, TERMS, false, 2>(a, st); break;
         case 'V': launch_g5<128, 64, 2, 3, TERMS, false, 2>(a, st); break;
         case 'W': launch_g5<64, 64, 2, 2, TERMS, false, 2>(a, st); break;
+        // 2 x 2 wave layout: 0..7
+        case '0': launch_g5<64, 128, 1, 3, TERMS, false, 1, 2>(a, st); break;
+        case '1': launch_g5<64, 64, 1, 3, TERMS, false, 1, 2>(a, st); break;
+        case '2': launch_g5<128, 128, 1, 3, TERMS, false, 1, 2>(a, st); break;
+        case '3': launch_g5<128, 64, 1, 3, TERMS, false, 1, 2>(a, st); break;
+        case '4': launch_g5<64, 128, 2, 3, TERMS, false, 2, 2>(a, st); break;
+        case '5': launch_g5<64, 64, 2, 2, TERMS, false, 2, 2>(a, st); break;
+        case '6': launch_g5<64, 256, 1, 3, TERMS, false, 1, 2>(a, st); break;
+        case '7': launch_g5<128, 128, 1, 4, TERMS, false, 1, 2>(a, st); break;
         default: return false;
     }
     return true;
@@ -457,14 +524,16 @@ bool dispatch_g5(char cfg, const G5Args& a, hipStream_t st) {
 bool gemm_g5_f16x3(char cfg, const float* A, int64_t lda, const void* W, int ksteps,
                    const float* wsc, float* C, int64_t ldc, const float* bias, const float* R,
                    int64_t ldr, int M, int N, int K, int act, int vec_out, hipStream_t st) {
-    G5Args a{A, lda, (const u32x4*)W, ksteps, wsc, C, ldc, bias, R, ldr, M, N, K, act, vec_out};
+    G5Args a{A, lda, g5_zero_ptr(), (const u32x4*)W, ksteps, wsc, C, ldc, bias, R, ldr, M, N, K,
+             act, vec_out};
     return dispatch_g5<2>(cfg, a, st);
 }
 
 bool gemm_g5_bf16(char cfg, const float* A, int64_t lda, const void* W, int ksteps, float* C,
                   int64_t ldc, const float* bias, const float* R, int64_t ldr, int M, int N, int K,
                   int act, int vec_out, hipStream_t st) {
-    G5Args a{A, lda, (const u32x4*)W, ksteps, nullptr, C, ldc, bias, R, ldr, M, N, K, act, vec_out};
+    G5Args a{A, lda, g5_zero_ptr(), (const u32x4*)W, ksteps, nullptr, C, ldc, bias, R, ldr, M, N,
+             K, act, vec_out};
     return dispatch_g5<1>(cfg, a, st);
 }
 

@@ -45,7 +45,7 @@ def bf16_mode():
     fgreg.set_precision(old)
 
 
-@pytest.mark.parametrize('tile', ['', 'z', 'A', 'B', 'I', 'K', 'O', 'D', 'S', 'T'])
+@pytest.mark.parametrize('tile', ['', 'z', 'A', 'B', 'I', 'K', 'O', 'D', 'S', 'T', '0', '2', '5'])
 @pytest.mark.parametrize('m,n,k', [(11472, 128, 1920), (9200, 1024, 2048), (1000, 3, 256),
                                    (333, 896, 128), (64, 256, 36), (5000, 768, 256), (1, 64, 7),
                                    (4097, 130, 1000)])

@@ -375,7 +375,7 @@ def test_gemm_f16x3_dynamic_range(gpu, tile, monkeypatch):
     del ref
 
 
-@pytest.mark.parametrize('tile', list('abcdefghijklmnopqrstuvwx') + list('ABCDEFGHIJKLMNOPQRSTUVW'))
+@pytest.mark.parametrize('tile', list('abcdefghijklmnopqrstuvwx') + list('ABCDEFGHIJKLMNOPQRSTUVW01234567'))
 def test_gemm_f16x3_tiles(gpu, tile, monkeypatch):
     """Every f16x3 tile / pipeline variant (FGR_GEMM16_TILE; A..R: the LDS-DMA g5 kernels of
     gemm5.hip) at fp32 accuracy on ragged shapes (M, N, K not multiples of the tiles; K % 64

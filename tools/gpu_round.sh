@@ -20,9 +20,9 @@ for wl in modelnet 3dmatch; do
   timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex 'kpconv_gather' --output-format csv -d gpurun_out/pmcw_${wl}_$tag -- python3 bench.py --profile --workload $wl --steps 3 --warmup 1 > gpurun_out/pmcw_${wl}_$tag.log 2>&1 || exit 1
   python3 tools/pmc_traffic.py fgr_kpconv_gather kpconv_gather $(ls gpurun_out/pmcf_${wl}_$tag/*/*counter_collection.csv) $(ls gpurun_out/pmcw_${wl}_$tag/*/*counter_collection.csv) > profiles/pmc_kpconv_$wl.json || exit 1
 done
-timeout -k 10 400 python bench.py --steps 20 --warmup 5 --gemm-table gpurun_out/gemm_$tag.json > gpurun_out/bench_$tag.json 2> gpurun_out/bench_$tag.err || exit 1
-timeout -k 10 400 python bench.py --workload 3dmatch --steps 10 --warmup 3 --gemm-table gpurun_out/gemm3d_$tag.json > gpurun_out/bench3d_$tag.json 2> gpurun_out/bench3d_$tag.err || exit 1
-timeout -k 10 400 python bench.py --workload 3dlomatch --steps 10 --warmup 3 --gemm-table gpurun_out/gemmlo_$tag.json > gpurun_out/benchlo_$tag.json 2> gpurun_out/benchlo_$tag.err || exit 1
+timeout -k 10 400 python bench.py --steps 50 --warmup 10 --gemm-table gpurun_out/gemm_$tag.json > gpurun_out/bench_$tag.json 2> gpurun_out/bench_$tag.err || exit 1
+timeout -k 10 400 python bench.py --workload 3dmatch --steps 50 --warmup 10 --gemm-table gpurun_out/gemm3d_$tag.json > gpurun_out/bench3d_$tag.json 2> gpurun_out/bench3d_$tag.err || exit 1
+timeout -k 10 400 python bench.py --workload 3dlomatch --steps 50 --warmup 10 --gemm-table gpurun_out/gemmlo_$tag.json > gpurun_out/benchlo_$tag.json 2> gpurun_out/benchlo_$tag.err || exit 1
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$tag -- python3 bench.py --profile --steps $K --warmup $W > gpurun_out/prof_$tag.json 2> gpurun_out/prof_$tag.err || exit 1
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof3d_$tag -- python3 bench.py --profile --workload 3dmatch --steps $K --warmup $W > gpurun_out/prof3d_$tag.json 2> gpurun_out/prof3d_$tag.err || exit 1
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/proflo_$tag -- python3 bench.py --profile --workload 3dlomatch --steps $K --warmup $W > gpurun_out/proflo_$tag.json 2> gpurun_out/proflo_$tag.err || exit 1
