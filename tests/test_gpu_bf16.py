@@ -133,6 +133,7 @@ def test_attention_bf16(gpu, bf16_mode, d, scale):
 def _random_model(cfg, seed):
     import fgreg
     torch.manual_seed(seed)
+    np.random.seed(seed)          # init_kernel_points draws from numpy's global generator
     m = fgreg.RegTR(cfg)
     g = torch.Generator().manual_seed(seed)
     with torch.no_grad():

@@ -84,9 +84,11 @@ def test_instnorm_vs_reference(gpu):
                                        ([3000, 5, 1500, 1024, 1025], 72, 2.0),
                                        ([3000, 5, 1500, 1024, 1025], 64, 2.0),
                                        ([20000, 13389], 64, 50.0), ([5483, 1, 2000], 256, 2.0),
-                                       ([1100, 4000], 1024, -30.0)])
+                                       ([1100, 4000], 1024, -30.0), ([596] * 16, 1024, 2.0),
+                                       ([1, 1024, 300, 7] * 4, 576, -20.0)])
 def test_instnorm_fusions_vs_torch(gpu, lens, c, mu):
-    """Register path (segments <= 1024 rows), the two-launch chunked path (C % 4 != 0) and
+    """Register paths (segments <= 1024 rows: 16-channel blocks, or 64-channel blocks with
+    16-B accesses when C % 4 == 0 and there are >= 128 of them), the two-launch chunked path (C % 4 != 0) and
     the three-launch long-segment path (C / 4 divides 256), including 3DMatch-size clouds
     with |mean| >> std (the shifted sums must not cancel)."""
     import fgreg.ops as ops
@@ -375,7 +377,7 @@ def test_gemm_f16x3_dynamic_range(gpu, tile, monkeypatch):
     del ref
 
 
-@pytest.mark.parametrize('tile', list('abcdefghijklmnopqrstuvwx') + list('ABCDEFGHIJKLMNOPQRSTUVW01234567'))
+@pytest.mark.parametrize('tile', list('abcdefghijklmnopqrstuvwx') + list('ABCDEFGHIJKLMNOPQRSTUVW0123456789'))
 def test_gemm_f16x3_tiles(gpu, tile, monkeypatch):
     """Every f16x3 tile / pipeline variant (FGR_GEMM16_TILE; A..R: the LDS-DMA g5 kernels of
     gemm5.hip) at fp32 accuracy on ragged shapes (M, N, K not multiples of the tiles; K % 64
