@@ -214,103 +214,6 @@ __global__ void __launch_bounds__(64 * kInW) instnorm_seg16_kernel(InArgs a) {
     }
 }
 
-// seg16 with 16-B accesses: lane (rl, cc) owns channels 4 cc .. 4 cc + 3 of a 64-channel
-// group (full 256-B row slices instead of 64-B ones, ~2x the bytes per request); rows and
-// the reduction order per channel are seg16's, so the results are bit-identical. For
-// C % 4 == 0, 16-B aligned operands and enough (64-channel group, segment) blocks.
-__global__ void __launch_bounds__(64 * kInW) instnorm_seg64_kernel(InArgs a) {
-    __shared__ float4 red[kInW][16];
-    const int seg = blockIdx.y;
-    const int wv = threadIdx.x / 64, lane = threadIdx.x % 64;
-    const int rl = lane >> 4, cc = lane & 15;
-    const int ch = blockIdx.x * 64 + 4 * cc;
-    const bool cok = ch < a.c;
-    const int64_t b = a.seg_off[seg], e = a.seg_off[seg + 1];
-    const int nrow = (int)(e - b);
-    if (nrow <= 0) return;
-    const int r0 = wv * 4 + rl;
-    const int chc = cok ? ch : 0;
-    float4 v[kSegRpl];
-    float dv[kSegRpl];
-#pragma unroll
-    for (int j = 0; j < kSegRpl; ++j) {
-        const int rr = min(r0 + 64 * j, nrow - 1);
-        v[j] = *reinterpret_cast<const float4*>(a.x + (b + rr) * a.c + chc);
-        dv[j] = a.row_div ? a.row_div[b + rr] : 1.f;
-    }
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int j = 0; j < kSegRpl; ++j) {
-        const bool ok = r0 + 64 * j < nrow && cok;
-        float4 t = v[j];
-        if (a.row_div) {
-            t.x = t.x / dv[j]; t.y = t.y / dv[j]; t.z = t.z / dv[j]; t.w = t.w / dv[j];
-        }
-        v[j] = ok ? t : make_float4(0.f, 0.f, 0.f, 0.f);
-        s.x += v[j].x; s.y += v[j].y; s.z += v[j].z; s.w += v[j].w;
-    }
-    s.x = xg16_32_sum(s.x); s.y = xg16_32_sum(s.y); s.z = xg16_32_sum(s.z); s.w = xg16_32_sum(s.w);
-    if (rl == 0) red[wv][cc] = s;
-    __syncthreads();
-    float4 tot = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int w = 0; w < kInW; ++w) {
-        const float4 r = red[w][cc];
-        tot.x += r.x; tot.y += r.y; tot.z += r.z; tot.w += r.w;
-    }
-    const float cnt = (float)nrow;
-    const float4 mean = make_float4(tot.x / cnt, tot.y / cnt, tot.z / cnt, tot.w / cnt);
-    __syncthreads();
-    float4 sq = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int j = 0; j < kSegRpl; ++j) {
-        if (r0 + 64 * j < nrow) {
-            const float dx = v[j].x - mean.x, dy = v[j].y - mean.y, dz = v[j].z - mean.z,
-                        dw = v[j].w - mean.w;
-            sq.x += dx * dx; sq.y += dy * dy; sq.z += dz * dz; sq.w += dw * dw;
-        } else {
-            sq.x += 0.f; sq.y += 0.f; sq.z += 0.f; sq.w += 0.f;
-        }
-    }
-    sq.x = xg16_32_sum(sq.x); sq.y = xg16_32_sum(sq.y); sq.z = xg16_32_sum(sq.z); sq.w = xg16_32_sum(sq.w);
-    if (rl == 0) red[wv][cc] = sq;
-    __syncthreads();
-    float4 m2 = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int w = 0; w < kInW; ++w) {
-        const float4 r = red[w][cc];
-        m2.x += r.x; m2.y += r.y; m2.z += r.z; m2.w += r.w;
-    }
-    const float4 rstd = make_float4(1.0f / sqrtf(m2.x / cnt + a.eps), 1.0f / sqrtf(m2.y / cnt + a.eps),
-                                    1.0f / sqrtf(m2.z / cnt + a.eps), 1.0f / sqrtf(m2.w / cnt + a.eps));
-    if (!cok) return;
-    float4 rv[kSegRpl];
-    if (a.residual) {
-#pragma unroll
-        for (int j = 0; j < kSegRpl; ++j)
-            rv[j] = *reinterpret_cast<const float4*>(a.residual + (b + min(r0 + 64 * j, nrow - 1)) * a.c + ch);
-    }
-#pragma unroll
-    for (int j = 0; j < kSegRpl; ++j) {
-        const int rr = r0 + 64 * j;
-        if (rr < nrow) {
-            const int64_t o = (b + rr) * a.c + ch;
-            float4 y;
-            y.x = act_fn((v[j].x - mean.x) * rstd.x, a.act);
-            y.y = act_fn((v[j].y - mean.y) * rstd.y, a.act);
-            y.z = act_fn((v[j].z - mean.z) * rstd.z, a.act);
-            y.w = act_fn((v[j].w - mean.w) * rstd.w, a.act);
-            if (a.residual) {
-                y.x = act_fn(y.x + rv[j].x, a.post_act);
-                y.y = act_fn(y.y + rv[j].y, a.post_act);
-                y.z = act_fn(y.z + rv[j].z, a.post_act);
-                y.w = act_fn(y.w + rv[j].w, a.post_act);
-            }
-            *reinterpret_cast<float4*>(a.out + o) = y;
-        }
-    }
-}
-
 // Segmented instance norm for long segments (> kSegRows rows, e.g. 3DMatch's 20k-row clouds),
 // three launches that keep every CU busy (the register-resident chunk kernel above runs
 // only C/64 x n_seg x rows/768 blocks -- ~100 at 2 x 20k x 64):
@@ -660,12 +563,7 @@ extern "C" int fgr_instnorm(const float* x, int64_t n, int32_t c, const int64_t*
     hipStream_t st = as_stream(stream);
     TimedCall timed_(st);
     const unsigned cx = (unsigned)ceil_div(c, 64);
-    const bool al16 = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(out) |
-                        reinterpret_cast<uintptr_t>(residual)) & 15) == 0;
-    if (max_seg_len <= kSegRows && c % 4 == 0 && al16 && (int64_t)ceil_div(c, 64) * n_seg >= 128) {
-        hipLaunchKernelGGL(instnorm_seg64_kernel, dim3((unsigned)ceil_div(c, 64), n_seg, 1),
-                           dim3(64 * kInW), 0, st, a);
-    } else if (max_seg_len <= kSegRows) {
+    if (max_seg_len <= kSegRows) {
         hipLaunchKernelGGL(instnorm_seg16_kernel, dim3((unsigned)ceil_div(c, 16), n_seg, 1),
                            dim3(64 * kInW), 0, st, a);
     } else if (ls_ok(c)) {

@@ -87,8 +87,8 @@ def test_instnorm_vs_reference(gpu):
                                        ([1100, 4000], 1024, -30.0), ([596] * 16, 1024, 2.0),
                                        ([1, 1024, 300, 7] * 4, 576, -20.0)])
 def test_instnorm_fusions_vs_torch(gpu, lens, c, mu):
-    """Register paths (segments <= 1024 rows: 16-channel blocks, or 64-channel blocks with
-    16-B accesses when C % 4 == 0 and there are >= 128 of them), the two-launch chunked path (C % 4 != 0) and
+    """Register path (segments <= 1024 rows, incl. ModelNet's 16 x 596 x 1024 and ragged
+    16-cloud batches), the two-launch chunked path (C % 4 != 0) and
     the three-launch long-segment path (C / 4 divides 256), including 3DMatch-size clouds
     with |mean| >> std (the shifted sums must not cancel)."""
     import fgreg.ops as ops
