@@ -465,7 +465,7 @@ extern "C" int fgr_gemm_bf16(const float* a, int64_t lda, const void* w_img, flo
         cfg = 'W';
     else
         cfg = n <= 256 && k >= 1000 ? 'I' : 'z';
-    if (((cfg >= 'A' && cfg <= 'W') || (cfg >= '0' && cfg <= '7')) && k % 8 == 0) {
+    if (((cfg >= 'A' && cfg <= 'W') || (cfg >= '0' && cfg <= '9')) && k % 8 == 0) {
         FGR_REQUIRE(gemm_g5_bf16(cfg, a, lda, w_img, ksteps_bf(k), c, ldc, bias, r, ldr, m, n, k, act,
                      vo ? 1 : 0, st),
                     "fgr_gemm_bf16: g5 variant %c unavailable", cfg);

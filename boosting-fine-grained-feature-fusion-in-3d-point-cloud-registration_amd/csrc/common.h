@@ -116,4 +116,29 @@ __device__ __forceinline__ int find_segment(const int64_t* off, int n, int64_t r
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// Two-term fp16 splits and 3-way max by single VALU instructions (gfx950), shared by the
+// f16x3 GEMM and attention loops.
+// max(|a|, |b|, |c|) in one v_max3_f32 (no NaN canonicalisation: finite activations)
+__device__ __forceinline__ float max3_abs(float a, float b, float c) {
+    float r;
+    asm("v_max3_f32 %0, |%1|, |%2|, |%3|" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+// packed f16 (hi terms) of a sc, b sc: v_fma_mixlo / mixhi (round to nearest even, as a
+// v_cvt_f16_f32 of the exact product)
+__device__ __forceinline__ unsigned split_hi2(float a, float b, float sc) {
+    unsigned d;
+    asm("v_fma_mixlo_f16 %0, %1, %2, 0" : "=v"(d) : "v"(a), "v"(sc));
+    asm("v_fma_mixhi_f16 %0, %1, %2, 0" : "+v"(d) : "v"(b), "v"(sc));
+    return d;
+}
+// packed f16 (lo terms) of a sc - hi_a, b sc - hi_b (hi from split_hi2: f16 halves of h)
+__device__ __forceinline__ unsigned split_lo2(float a, float b, float sc, unsigned h) {
+    unsigned d;
+    asm("v_fma_mixlo_f16 %0, %1, %2, -%3 op_sel_hi:[0,0,1]" : "=v"(d) : "v"(a), "v"(sc), "v"(h));
+    asm("v_fma_mixhi_f16 %0, %1, %2, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+        : "+v"(d) : "v"(b), "v"(sc), "v"(h));
+    return d;
+}
+
 }  // namespace fgr

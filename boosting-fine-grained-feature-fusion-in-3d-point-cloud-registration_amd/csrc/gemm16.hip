@@ -1204,7 +1204,7 @@ extern "C" int fgr_gemm_f16x3(const float* a, int64_t lda, const void* w_img, fl
     else
         cfg = k <= 1024 ? 't' : 'e';
     // g5 (gemm5.hip: LDS-DMA pipeline, A split after the read): A..W, K % 8 == 0 only
-    if (((cfg >= 'A' && cfg <= 'W') || (cfg >= '0' && cfg <= '7')) && k % 8 == 0) {
+    if (((cfg >= 'A' && cfg <= 'W') || (cfg >= '0' && cfg <= '9')) && k % 8 == 0) {
         FGR_REQUIRE(gemm_g5_f16x3(cfg, a, lda, w_img, ksteps_h3(k), wsc, c, ldc, bias, r, ldr, m, n, k, act,
                       vo ? 1 : 0, st),
                     "fgr_gemm_f16x3: g5 variant %c unavailable", cfg);

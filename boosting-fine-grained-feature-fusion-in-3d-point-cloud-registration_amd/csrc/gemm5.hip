@@ -79,29 +79,6 @@ __device__ __forceinline__ float xg_max(float v) {        // max over lanes c, c
     return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
 }
 
-// max(|a|, |b|, |c|) in one v_max3_f32 (no NaN canonicalisation: finite activations)
-__device__ __forceinline__ float max3_abs(float a, float b, float c) {
-    float r;
-    asm("v_max3_f32 %0, |%1|, |%2|, |%3|" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
-}
-// packed f16 (hi terms) of a sc, b sc: v_fma_mixlo / mixhi (round to nearest even, as a
-// v_cvt_f16_f32 of the exact product)
-__device__ __forceinline__ unsigned split_hi2(float a, float b, float sc) {
-    unsigned d;
-    asm("v_fma_mixlo_f16 %0, %1, %2, 0" : "=v"(d) : "v"(a), "v"(sc));
-    asm("v_fma_mixhi_f16 %0, %1, %2, 0" : "+v"(d) : "v"(b), "v"(sc));
-    return d;
-}
-// packed f16 (lo terms) of a sc - hi_a, b sc - hi_b (hi from split_hi2: f16 halves of h)
-__device__ __forceinline__ unsigned split_lo2(float a, float b, float sc, unsigned h) {
-    unsigned d;
-    asm("v_fma_mixlo_f16 %0, %1, %2, -%3 op_sel_hi:[0,0,1]" : "=v"(d) : "v"(a), "v"(sc), "v"(h));
-    asm("v_fma_mixhi_f16 %0, %1, %2, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
-        : "+v"(d) : "v"(b), "v"(sc), "v"(h));
-    return d;
-}
-
 __device__ __forceinline__ float finish5(float y, float b, float r, int act) {
     if (act == FGR_ACT_RELU_RES_LEAKY) {
         const float t = fmaxf(y + b, 0.f) + r;
@@ -513,6 +490,9 @@ bool dispatch_g5(char cfg, const G5Args& a, hipStream_t st) {
         case '5': launch_g5<64, 64, 2, 2, TERMS, false, 2, 2>(a, st); break;
         case '6': launch_g5<64, 256, 1, 3, TERMS, false, 1, 2>(a, st); break;
         case '7': launch_g5<128, 128, 1, 4, TERMS, false, 1, 2>(a, st); break;
+        // 128 x 128, deeper pipelines (L2 / MALL traffic per MFMA halves vs 64 x 64): 8, 9
+        case '8': launch_g5<128, 128, 1, 4, TERMS, false>(a, st); break;
+        case '9': launch_g5<128, 128, 1, 5, TERMS, false>(a, st); break;
         default: return false;
     }
     return true;
