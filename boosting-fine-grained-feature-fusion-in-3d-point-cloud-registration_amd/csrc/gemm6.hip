@@ -53,16 +53,19 @@ struct G6Args {
     int M, N, K, act, vec_out;
 };
 
-template <int BM, int BN, int S, bool PROBE = false, int REP = 1, int KS = 1>
+// RS: one scale per ROW for the whole K (fgr_split_rows_h3_rs, or a producer that sees full
+// rows): the three products accumulate straight into acc (no per-step temporaries, no
+// scale DMA) and the row scale is applied once in the epilogue.
+template <int BM, int BN, int S, bool PROBE = false, int REP = 1, int KS = 1, bool RS = false>
 __global__ void __launch_bounds__(256) gemm_g6(G6Args p) {
     constexpr int TM = BM / 32, TN = BN / 32;          // 16 x 16 fragments per wave
     constexpr int A_UNITS = (BM / 16) * 128;           // [panel][term][g][16] of one k32 step
     constexpr int W_UNITS = (BN / 16) * 128;
-    constexpr int S_UNITS = 64;                        // 4 pieces x 256 B of scales (BM <= 256)
+    constexpr int S_UNITS = RS ? 0 : 64;               // 4 pieces x 256 B of scales (BM <= 256)
     constexpr int ST1 = A_UNITS + W_UNITS + S_UNITS;   // one k32 step
     constexpr int ST = KS * ST1;                       // one stage = KS k32 steps
     constexpr int A_PIECES = A_UNITS / 64, W_PIECES = W_UNITS / 64;
-    constexpr int NP1 = A_PIECES + W_PIECES + 4;
+    constexpr int NP1 = A_PIECES + W_PIECES + (RS ? 0 : 4);
     static_assert(NP1 % 4 == 0 && BM <= 256, "tile");
     constexpr int P1 = NP1 / 4, P = P1 * KS;           // DMA pieces per wave per k-step / stage
     __shared__ u32x4 lds[S * ST];
@@ -168,7 +171,7 @@ __global__ void __launch_bounds__(256) gemm_g6(G6Args p) {
             const int panel = (wm >> 4) + i;
             af[i][0] = st[panel * 128 + lane];
             af[i][1] = st[panel * 128 + 64 + lane];
-            sa[i] = sc[wm + 16 * i + c];
+            if constexpr (!RS) sa[i] = sc[wm + 16 * i + c];
         }
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
@@ -184,12 +187,18 @@ __global__ void __launch_bounds__(256) gemm_g6(G6Args p) {
             for (int i = 0; i < TM; ++i) {
                 const f16x8 ah = __builtin_bit_cast(f16x8, af[i][0]);
                 const f16x8 al = __builtin_bit_cast(f16x8, af[i][1]);
-                f32x4 tt = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, ah, f32x4{0.f, 0.f, 0.f, 0.f},
-                                                                  0, 0, 0);
-                tt = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, al, tt, 0, 0, 0);
-                tt = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, ah, tt, 0, 0, 0);
+                if constexpr (RS) {
+                    acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, ah, acc[j][i], 0, 0, 0);
+                    acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, al, acc[j][i], 0, 0, 0);
+                    acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, ah, acc[j][i], 0, 0, 0);
+                } else {
+                    f32x4 tt = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, ah, f32x4{0.f, 0.f, 0.f, 0.f},
+                                                                      0, 0, 0);
+                    tt = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, al, tt, 0, 0, 0);
+                    tt = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, ah, tt, 0, 0, 0);
 #pragma unroll
-                for (int r = 0; r < 4; ++r) acc[j][i][r] = __builtin_fmaf(tt[r], sa[i], acc[j][i][r]);
+                    for (int r = 0; r < 4; ++r) acc[j][i][r] = __builtin_fmaf(tt[r], sa[i], acc[j][i][r]);
+                }
             }
         }
         }
@@ -201,6 +210,7 @@ __global__ void __launch_bounds__(256) gemm_g6(G6Args p) {
     for (int i = 0; i < TM; ++i) {
         const int m = m0 + wm + 16 * i + c;
         if (m >= p.M) continue;
+        const float rsc = RS ? p.sA[m] : 1.f;
         float* crow = p.C + (int64_t)m * p.ldc;
         const float* rrow = p.R ? p.R + (int64_t)m * p.ldr : nullptr;
 #pragma unroll
@@ -208,8 +218,8 @@ __global__ void __launch_bounds__(256) gemm_g6(G6Args p) {
             const int n = n0 + wn + 16 * j + 4 * g;
             if (n >= p.N) continue;
             const float4 ws = *reinterpret_cast<const float4*>(p.wsc + n);
-            const float y[4] = {acc[j][i][0] * ws.x, acc[j][i][1] * ws.y, acc[j][i][2] * ws.z,
-                                acc[j][i][3] * ws.w};
+            const float y[4] = {acc[j][i][0] * rsc * ws.x, acc[j][i][1] * rsc * ws.y,
+                                acc[j][i][2] * rsc * ws.z, acc[j][i][3] * rsc * ws.w};
             if (p.vec_out && n + 3 < p.N) {
                 float4 bb = make_float4(0.f, 0.f, 0.f, 0.f), rr = bb;
                 if (p.bias) bb = *reinterpret_cast<const float4*>(p.bias + n);
@@ -279,10 +289,65 @@ __global__ void __launch_bounds__(256) split_rows_h3_kernel(const float* __restr
     if (g == 0) sA[(int64_t)s * ld_s + m] = __builtin_ldexpf(1.f, -e);
 }
 
-template <int BM, int BN, int S, bool PROBE = false, int REP = 1, int KS = 1>
+// fp32 rows -> A image with ONE exponent per row (the row's max over all of K into
+// [2^14, 2^15); all-zero row: 0): one wave per 16-row panel; lane (g, c) walks row c's
+// k-steps (8 values each), first for the max, then splitting with v_fma_mix. sA[m] = 2^-e.
+__global__ void __launch_bounds__(256) split_rows_rs_kernel(const float* __restrict__ x,
+                                                            int64_t ldx, int M, int K, int ksteps,
+                                                            u32x4* __restrict__ img,
+                                                            float* __restrict__ sA, int64_t n_panels) {
+    const int64_t panel = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (panel >= n_panels) return;
+    const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+    const int64_t m = panel * 16 + c;
+    const bool vec = (K % 4) == 0;
+    auto load8 = [&](int s, float (&v)[8]) {
+        const int k0 = s * 32 + 8 * g;
+        if (m < M && k0 + 8 <= K && vec) {
+            const float4 a = *reinterpret_cast<const float4*>(x + m * ldx + k0);
+            const float4 b = *reinterpret_cast<const float4*>(x + m * ldx + k0 + 4);
+            v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+        } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = (m < M && k0 + e < K) ? x[m * ldx + k0 + e] : 0.f;
+        }
+    };
+    float cm = 0.f;
+    for (int s = 0; s < ksteps; ++s) {
+        float v[8];
+        load8(s, v);
+        cm = fmaxf(cm, max3_abs(v[0], v[1], v[2]));
+        cm = fmaxf(cm, max3_abs(v[3], v[4], v[5]));
+        cm = fmaxf(cm, fmaxf(fabsf(v[6]), fabsf(v[7])));
+    }
+    {
+        auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(cm), __float_as_uint(cm), false, false);
+        cm = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+        auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(cm), __float_as_uint(cm), false, false);
+        cm = fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+    }
+    const int e = cm > 0.f ? min(15 - __builtin_amdgcn_frexp_expf(cm), 127) : 0;
+    const float sc = __builtin_ldexpf(1.f, e);
+    for (int s = 0; s < ksteps; ++s) {
+        float v[8];
+        load8(s, v);
+        u32x4 hh, ll;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            hh[q] = split_hi2(v[2 * q], v[2 * q + 1], sc);
+            ll[q] = split_lo2(v[2 * q], v[2 * q + 1], sc, hh[q]);
+        }
+        u32x4* dst = img + (panel * ksteps + s) * 128;
+        dst[lane] = hh;
+        dst[64 + lane] = ll;
+    }
+    if (g == 0 && m < M) sA[m] = __builtin_ldexpf(1.f, -e);
+}
+
+template <int BM, int BN, int S, bool PROBE = false, int REP = 1, int KS = 1, bool RS = false>
 void launch_g6(const G6Args& a, hipStream_t st) {
     const int nbm = (a.M + BM - 1) / BM, nbn = (a.N + BN - 1) / BN;
-    hipLaunchKernelGGL((gemm_g6<BM, BN, S, PROBE, REP, KS>), dim3((unsigned)(nbm * nbn)),
+    hipLaunchKernelGGL((gemm_g6<BM, BN, S, PROBE, REP, KS, RS>), dim3((unsigned)(nbm * nbn)),
                        dim3(256), 0, st, a);
 }
 
@@ -314,8 +379,13 @@ extern "C" int fgr_split_rows_h3(const float* x, int64_t ldx, int32_t m, int32_t
     float* sA = reinterpret_cast<float*>(im + units * 128);
     hipStream_t st = as_stream(stream);
     TimedCall timed_(st);
-    hipLaunchKernelGGL(split_rows_h3_kernel, dim3((unsigned)ceil_div(units, 4)), dim3(256), 0, st, x,
-                       ldx, m, k, ks, ld_scales6(m), im, sA, units);
+    const char* rs = getenv("FGR_SPLIT_RS");     // experiment: one scale per row (RS GEMMs A..H)
+    if (rs && rs[0] == '1')
+        hipLaunchKernelGGL(split_rows_rs_kernel, dim3((unsigned)ceil_div(panels6(m), 4)), dim3(256), 0,
+                           st, x, ldx, m, k, ks, im, sA, panels6(m));
+    else
+        hipLaunchKernelGGL(split_rows_h3_kernel, dim3((unsigned)ceil_div(units, 4)), dim3(256), 0, st, x,
+                           ldx, m, k, ks, ld_scales6(m), im, sA, units);
     FGR_CHECK_LAUNCH("split_rows_h3_kernel");
     return FGR_OK;
 }
@@ -363,6 +433,15 @@ extern "C" int fgr_gemm_h3_presplit(const void* a_img, const void* w_img, float*
         case 'm': launch_g6<64, 128, 2, false, 1, 2>(g, st); break;
         case 'n': launch_g6<128, 64, 2, false, 1, 2>(g, st); break;
         case 'o': launch_g6<64, 64, 3, true, 1, 2>(g, st); break;     // probe, 2 steps / stage
+        // one scale per row (FGR_SPLIT_RS=1 images): A..H as a..h
+        case 'A': launch_g6<64, 64, 4, false, 1, 1, true>(g, st); break;
+        case 'B': launch_g6<128, 128, 3, false, 1, 1, true>(g, st); break;
+        case 'C': launch_g6<64, 128, 4, false, 1, 1, true>(g, st); break;
+        case 'D': launch_g6<128, 64, 4, false, 1, 1, true>(g, st); break;
+        case 'E': launch_g6<128, 128, 4, false, 1, 1, true>(g, st); break;
+        case 'F': launch_g6<64, 64, 3, false, 1, 1, true>(g, st); break;
+        case 'G': launch_g6<128, 256, 2, false, 1, 1, true>(g, st); break;
+        case 'H': launch_g6<256, 128, 2, false, 1, 1, true>(g, st); break;
         default: launch_g6<64, 64, 4>(g, st); break;
     }
     FGR_CHECK_LAUNCH("gemm_g6");

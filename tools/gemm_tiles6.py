@@ -15,6 +15,9 @@ from gemm_tiles import SHAPES, timeit  # noqa: E402
 
 def main():
     cfgs = sys.argv[1] if len(sys.argv) > 1 else 'abcdefgh'
+    # upper-case configs: one scale per row (FGR_SPLIT_RS=1 split); do not mix with lower case
+    if cfgs.isupper():
+        os.environ['FGR_SPLIT_RS'] = '1'
     dev = torch.device('cuda:0')
     lin.set_mode('f16x3')
     g = torch.Generator(device=dev).manual_seed(0)
