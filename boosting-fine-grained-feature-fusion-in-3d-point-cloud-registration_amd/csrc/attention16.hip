@@ -136,9 +136,9 @@ attn_kv_image16_kernel(const float* __restrict__ k, int64_t ld_k, const float* _
 
 // GLDS: the K/V tile images go global -> LDS by LDS-DMA into two buffers (tile t + 1 in
 // flight while tile t is computed; one barrier per tile, no staging registers, no ds_write
-// pass), with the per-tile scale exponents preloaded into the same LDS array (a plain load
-// inside the loop would make the compiler wait for the DMA). Needs <= kMaxTilesLds tiles.
-constexpr int kMaxTilesLds = 256;
+// pass). The per-tile scale exponents come by scalar loads (block-uniform address: s_load,
+// counted by lgkmcnt, so the loop never waits on the DMA's vmcnt for them); no limit on the
+// key count, 32 KB of LDS at head dim 32 (5 blocks per CU).
 
 template <int N>
 __device__ __forceinline__ void wait_vm_lgkm0_a() {
@@ -146,7 +146,7 @@ __device__ __forceinline__ void wait_vm_lgkm0_a() {
 }
 
 template <int DH, bool GLDS>
-__global__ void __launch_bounds__(256, (GLDS && DH == 64) ? 2 : 4)
+__global__ void __launch_bounds__(256, (GLDS && DH == 64) ? 2 : (GLDS ? 5 : 4))
 attn_f16x3_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __restrict__ img,
                   const int2* __restrict__ sc, float* __restrict__ o, int64_t ld_o,
                   const int64_t* __restrict__ q_off, const int64_t* __restrict__ kv_off,
@@ -155,8 +155,7 @@ attn_f16x3_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __rest
     constexpr int KD = DH / 32;                                  // k-steps of Q K^T
     constexpr int TD = DH / 16;                                  // 16-row output tiles (dh)
     constexpr int UN = units<DH>(), NS = UN / 256;
-    constexpr int EXU = GLDS ? kMaxTilesLds * 8 / 16 : 0;       // 16-B units of exponents
-    __shared__ u32x4 lds[(GLDS ? 2 : 1) * UN + EXU];
+    __shared__ u32x4 lds[(GLDS ? 2 : 1) * UN];
     // XCD-aware block order: linear id L runs on XCD L % 8; all q-blocks of one
     // (segment, head) get ids of one residue mod 8, so one XCD's L2 serves its K/V image.
     const int L = blockIdx.x, xcd = L & 7, j0 = L >> 3;
@@ -219,7 +218,7 @@ attn_f16x3_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __rest
     // transposed-read addresses of V: lane c = 4qq + p reads row 4g + qq (+16, +32j),
     // columns 16t + 4p .. +3 (chunk 2t + (p >> 1), swizzled by row bit 2)
     const int qq = c >> 2, pp = c & 3;
-    int2* ex_lds = reinterpret_cast<int2*>(lds + (GLDS ? 2 * UN : 0));
+
     constexpr int PW = UN / 64 / 4;                              // DMA pieces per wave per tile
     auto dma = [&](int t) {                                      // tile t -> buffer t & 1
         const u32x4* src = tiles + t * tile_stride;
@@ -234,8 +233,6 @@ attn_f16x3_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __rest
         }
     };
     if constexpr (GLDS) {
-        for (int t = tid; t < ntile; t += 256) ex_lds[t] = sc[tile0 + t * n_head];
-        __syncthreads();
         if (ntile > 0) dma(0);
     } else if (ntile > 0) {
 #pragma unroll
@@ -264,7 +261,8 @@ attn_f16x3_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __rest
             __builtin_amdgcn_s_barrier();   // everyone's landed; buffer (tt+1)&1 no longer read
             if (tt + 1 < ntile) dma(tt + 1);
             tbuf = lds + (tt & 1) * UN;
-            e2 = ex_lds[tt];
+            // block-uniform address: a scalar load (lgkmcnt), no wait on the DMA's vmcnt
+            e2 = sc[tile0 + (int64_t)__builtin_amdgcn_readfirstlane(tt) * n_head];
         } else {
             e2 = sc[tile0 + tt * n_head];
             __syncthreads();
@@ -442,10 +440,10 @@ extern "C" int fgr_attention_f16x3(const float* q, int64_t ld_q, const float* k,
     const int64_t n_blocks = ceil_div((int64_t)n_seg * n_head, 8) * 8 * n_qblk;
     // LDS-DMA K/V staging (measured: head dim 64 57 -> 42 us per launch on the 3DMatch
     // forward although its 2 x 32-KB buffers halve the blocks per CU; head dim 32 on par)
-    // when every key segment fits the preloaded exponent table; FGR_ATTN_GLDS=0 selects the
+    // FGR_ATTN_GLDS=0 selects the
     // register-staged loop (A/B)
     const char* gl = getenv("FGR_ATTN_GLDS");
-    const bool glds = !(gl && gl[0] == '0') && ceil_div(max_kv_len, 64) <= kMaxTilesLds;
+    const bool glds = !(gl && gl[0] == '0');
     const float sl2 = scale * 1.4426950408889634f;
     if (dh == 32 && glds)
         hipLaunchKernelGGL((attn_f16x3_kernel<32, true>), dim3((unsigned)n_blocks), dim3(256), 0, st,
