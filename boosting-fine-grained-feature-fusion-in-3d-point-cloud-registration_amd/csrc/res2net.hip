@@ -127,17 +127,20 @@ __device__ __forceinline__ void split3(float x, __bf16& h, __bf16& m, __bf16& l)
     l = (__bf16)(r - (float)m);
 }
 
-template <int KT>   // KT = w / 16 column tiles (= waves); KS = ceil(w / 32) k-steps
+// R rows per block (16, 32 or 48: R / 16 row fragments per wave; 48 puts ModelNet's 9544
+// rows in 199 blocks -- one round of one 14-wave block per CU -- instead of 256 + 43, 16
+// spreads 3DMatch's ~2k rows over twice the CUs)
+template <int KT, int R = kRows>   // KT = w / 16 column tiles (= waves); KS = ceil(w / 32) k-steps
 __global__ void __launch_bounds__(64 * KT)
 res2net_chain6_kernel(const float* __restrict__ h, int64_t n, int scale, int nums,
                       const u32x4* __restrict__ wf, const float* __restrict__ bias,
                       const float* __restrict__ x, int cin, float* __restrict__ cat, int64_t ld) {
-    constexpr int W = 16 * KT, KS = (W + 31) / 32, NU = kRows * KS * 4;   // A units per term
+    constexpr int W = 16 * KT, KS = (W + 31) / 32, NU = R * KS * 4;   // A units per term
     __shared__ u32x4 img[3 * NU];
-    __shared__ float sp[kRows * W];
+    __shared__ float sp[R * W];
     const int tid = threadIdx.x, nth = 64 * KT;
     const int wv = tid / 64, lane = tid % 64, g = lane >> 4, c = lane & 15;
-    const int64_t r0 = (int64_t)blockIdx.x * kRows;
+    const int64_t r0 = (int64_t)blockIdx.x * R;
     const int64_t hw = (int64_t)scale * W;
     const int col = wv * 16 + c;
 
@@ -153,7 +156,7 @@ res2net_chain6_kernel(const float* __restrict__ h, int64_t n, int scale, int num
         const float bc = bias[i * W + col];
         // build the split A images: unit u -> (row = u % 32, kg = u / 32), 8 k each
         for (int u = tid; u < NU; u += nth) {
-            const int row = u % kRows, kg = u / kRows;       // kg = 4 ks + g'
+            const int row = u % R, kg = u / R;       // kg = 4 ks + g'
             const int k0 = 8 * kg;
             float a[8];
             const int64_t gr = r0 + row;
@@ -176,12 +179,15 @@ res2net_chain6_kernel(const float* __restrict__ h, int64_t n, int scale, int num
                 split3(a[e], hh, mm, ll);
                 th[e] = hh; tm[e] = mm; tl[e] = ll;
             }
-            img[0 * NU + kg * kRows + row] = __builtin_bit_cast(u32x4, th);
-            img[1 * NU + kg * kRows + row] = __builtin_bit_cast(u32x4, tm);
-            img[2 * NU + kg * kRows + row] = __builtin_bit_cast(u32x4, tl);
+            img[0 * NU + kg * R + row] = __builtin_bit_cast(u32x4, th);
+            img[1 * NU + kg * R + row] = __builtin_bit_cast(u32x4, tm);
+            img[2 * NU + kg * R + row] = __builtin_bit_cast(u32x4, tl);
         }
         __syncthreads();
-        f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+        constexpr int RF = R / 16;
+        f32x4 acc[RF];
+#pragma unroll
+        for (int f = 0; f < RF; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
             if (ks + 2 < KS) {
@@ -191,34 +197,36 @@ res2net_chain6_kernel(const float* __restrict__ h, int64_t n, int scale, int num
             const bf16x8 bh = __builtin_bit_cast(bf16x8, bq[ks % 3][0]);
             const bf16x8 bm = __builtin_bit_cast(bf16x8, bq[ks % 3][1]);
             const bf16x8 bl = __builtin_bit_cast(bf16x8, bq[ks % 3][2]);
-            const int base = (ks * 4 + g) * kRows;
-            const bf16x8 a0h = __builtin_bit_cast(bf16x8, img[0 * NU + base + c]);
-            const bf16x8 a0m = __builtin_bit_cast(bf16x8, img[1 * NU + base + c]);
-            const bf16x8 a0l = __builtin_bit_cast(bf16x8, img[2 * NU + base + c]);
-            const bf16x8 a1h = __builtin_bit_cast(bf16x8, img[0 * NU + base + 16 + c]);
-            const bf16x8 a1m = __builtin_bit_cast(bf16x8, img[1 * NU + base + 16 + c]);
-            const bf16x8 a1l = __builtin_bit_cast(bf16x8, img[2 * NU + base + 16 + c]);
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0m, bm, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1m, bm, acc1, 0, 0, 0);
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0l, bh, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1l, bh, acc1, 0, 0, 0);
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0h, bl, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1h, bl, acc1, 0, 0, 0);
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0m, bh, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1m, bh, acc1, 0, 0, 0);
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0h, bm, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1h, bm, acc1, 0, 0, 0);
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0h, bh, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1h, bh, acc1, 0, 0, 0);
+            const int base = (ks * 4 + g) * R;
+            bf16x8 ah[RF], am[RF], al[RF];
+#pragma unroll
+            for (int f = 0; f < RF; ++f) {
+                ah[f] = __builtin_bit_cast(bf16x8, img[0 * NU + base + 16 * f + c]);
+                am[f] = __builtin_bit_cast(bf16x8, img[1 * NU + base + 16 * f + c]);
+                al[f] = __builtin_bit_cast(bf16x8, img[2 * NU + base + 16 * f + c]);
+            }
+            // the six products of three-term bf16 splits, smallest first
+#pragma unroll
+            for (int f = 0; f < RF; ++f) acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[f], bm, acc[f], 0, 0, 0);
+#pragma unroll
+            for (int f = 0; f < RF; ++f) acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[f], bh, acc[f], 0, 0, 0);
+#pragma unroll
+            for (int f = 0; f < RF; ++f) acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[f], bl, acc[f], 0, 0, 0);
+#pragma unroll
+            for (int f = 0; f < RF; ++f) acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[f], bh, acc[f], 0, 0, 0);
+#pragma unroll
+            for (int f = 0; f < RF; ++f) acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[f], bm, acc[f], 0, 0, 0);
+#pragma unroll
+            for (int f = 0; f < RF; ++f) acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[f], bh, acc[f], 0, 0, 0);
         }
         // epilogue: sp_i -> cat and the fp32 LDS tile (read by the next step's build,
         // which starts after the barrier below)
 #pragma unroll
-        for (int rg = 0; rg < 2; ++rg) {
+        for (int rg = 0; rg < RF; ++rg) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int row = rg * 16 + 4 * g + r;
-                const float y = fmaxf((rg ? acc1[r] : acc0[r]) + bc, 0.f);
+                const float y = fmaxf(acc[rg][r] + bc, 0.f);
                 if (r0 + row < n) cat[(r0 + row) * ld + (int64_t)i * W + col] = y;
                 sp[row * W + col] = y;
             }
@@ -226,13 +234,13 @@ res2net_chain6_kernel(const float* __restrict__ h, int64_t n, int scale, int num
         __syncthreads();
     }
     const int rest = (scale - nums) * W;
-    for (int e = tid; e < kRows * rest; e += nth) {
+    for (int e = tid; e < R * rest; e += nth) {
         const int row = e / rest, cc = e - row * rest;
         if (r0 + row < n)
             cat[(r0 + row) * ld + (int64_t)nums * W + cc] = h[(r0 + row) * hw + (int64_t)nums * W + cc];
     }
     if (x) {
-        for (int e = tid; e < kRows * cin; e += nth) {
+        for (int e = tid; e < R * cin; e += nth) {
             const int row = e / cin, cc = e - row * cin;
             if (r0 + row < n) cat[(r0 + row) * ld + hw + cc] = x[(r0 + row) * cin + cc];
         }
@@ -453,14 +461,31 @@ extern "C" int fgr_res2net_chain6(const float* h, int64_t n, int32_t w, int32_t 
     FGR_REQUIRE(((reinterpret_cast<uintptr_t>(h) & 15) == 0) && (scale * w) % 4 == 0,
                 "fgr_res2net_chain6: h must be 16-B aligned");
     if (n == 0) return FGR_OK;
-    const dim3 grid((unsigned)ceil_div(n, kRows));
     hipStream_t st = as_stream(stream);
+    // w = 224 (one 14-wave block per CU): 48-row blocks when that saves a round of blocks
+    // over 32-row ones (rounds x rows per block; 256 CUs); FGR_R2N_ROWS=32 forces 32 (A/B)
+    const char* rr = getenv("FGR_R2N_ROWS");
+    int rows = 32;
+    if (w == 224 && !(rr && rr[0] == '3')) {       // min over R of rounds(R) x R, larger R on ties
+        int64_t best = ceil_div(ceil_div(n, 32), 256) * 32;
+        for (int r : {48, 16}) {
+            const int64_t cost = ceil_div(ceil_div(n, r), 256) * r;
+            if (cost < best) { best = cost; rows = r; }
+        }
+    }
+    const int64_t b32 = ceil_div(n, 32);
     if (w == 112)
-        hipLaunchKernelGGL(res2net_chain6_kernel<7>, grid, dim3(64 * 7), 0, st, h, n, scale,
-                           scale - 1, (const u32x4*)w_img, bias, x, cin, cat, ld_cat);
+        hipLaunchKernelGGL(res2net_chain6_kernel<7>, dim3((unsigned)b32), dim3(64 * 7), 0, st, h, n,
+                           scale, scale - 1, (const u32x4*)w_img, bias, x, cin, cat, ld_cat);
+    else if (rows == 48)
+        hipLaunchKernelGGL((res2net_chain6_kernel<14, 48>), dim3((unsigned)ceil_div(n, 48)), dim3(64 * 14),
+                           0, st, h, n, scale, scale - 1, (const u32x4*)w_img, bias, x, cin, cat, ld_cat);
+    else if (rows == 16)
+        hipLaunchKernelGGL((res2net_chain6_kernel<14, 16>), dim3((unsigned)ceil_div(n, 16)), dim3(64 * 14),
+                           0, st, h, n, scale, scale - 1, (const u32x4*)w_img, bias, x, cin, cat, ld_cat);
     else
-        hipLaunchKernelGGL(res2net_chain6_kernel<14>, grid, dim3(64 * 14), 0, st, h, n, scale,
-                           scale - 1, (const u32x4*)w_img, bias, x, cin, cat, ld_cat);
+        hipLaunchKernelGGL(res2net_chain6_kernel<14>, dim3((unsigned)b32), dim3(64 * 14), 0, st, h, n,
+                           scale, scale - 1, (const u32x4*)w_img, bias, x, cin, cat, ld_cat);
     FGR_CHECK_LAUNCH("res2net_chain6_kernel");
     return FGR_OK;
 }

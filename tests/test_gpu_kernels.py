@@ -281,6 +281,28 @@ def test_res2net_block_vs_oracle(gpu, cin, cout, mode):
         fl.set_mode(old)
 
 
+@pytest.mark.parametrize('n', [1500, 9544])
+def test_res2net_chain6_rows_bitexact(gpu, n, monkeypatch):
+    """fgr_res2net_chain6 at width 224 picks 16- / 48-row blocks by row count (1500 -> 16,
+    ModelNet's 9544 -> 48); every accumulator sees the same MFMA sequence as with the 32-row
+    blocks (FGR_R2N_ROWS=32), so the outputs are bit-identical."""
+    from fgreg import linear as fl
+    from fgreg.backbone import my_Bottle2neck, my_res2Net
+    old = fl.MODE
+    fl.set_mode('bf16x6')
+    try:
+        torch.manual_seed(3)
+        m = my_res2Net(my_Bottle2neck, 256, 1024, baseWidth=14, scale=8).to(gpu).eval()
+        x = torch.randn(n, 256, device=gpu)
+        with torch.no_grad():
+            a = m(x).clone()
+            monkeypatch.setenv('FGR_R2N_ROWS', '32')
+            b = m(x).clone()
+        assert torch.equal(a, b)
+    finally:
+        fl.set_mode(old)
+
+
 def _res2net_case(gpu, cin, cout, my_Bottle2neck, my_res2Net):
     torch.manual_seed(cout)
     m = my_res2Net(my_Bottle2neck, cin, cout, baseWidth=14, scale=8)
