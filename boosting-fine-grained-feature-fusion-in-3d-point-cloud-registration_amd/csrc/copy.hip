@@ -67,3 +67,34 @@ extern "C" int fgr_copy_batch(int32_t n, const void* const* src, void* const* ds
     }
     return FGR_OK;
 }
+
+namespace fgr {
+namespace {
+// off[0] = 0, off[i + 1] = off[i] + len[i]: one wave, a running sum over 64-entry chunks
+__global__ void __launch_bounds__(64) lengths_to_offsets_kernel(const int64_t* __restrict__ len,
+                                                                int n, int64_t* __restrict__ off) {
+    const int lane = threadIdx.x;
+    int64_t carry = 0;
+    if (lane == 0) off[0] = 0;
+    for (int b = 0; b < n; b += 64) {
+        int64_t v = b + lane < n ? len[b + lane] : 0;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {                 // inclusive scan over the wave
+            const int64_t u = __shfl_up(v, d, 64);
+            if (lane >= d) v += u;
+        }
+        if (b + lane < n) off[b + lane + 1] = carry + v;
+        carry += __shfl(v, 63, 64);
+    }
+}
+}  // namespace
+}  // namespace fgr
+
+extern "C" int fgr_lengths_to_offsets(const int64_t* lengths, int32_t n, int64_t* offsets,
+                                      void* stream) {
+    FGR_REQUIRE(n >= 0 && offsets && (n == 0 || lengths), "fgr_lengths_to_offsets: bad arguments");
+    hipLaunchKernelGGL(lengths_to_offsets_kernel, dim3(1), dim3(64), 0, as_stream(stream), lengths, n,
+                       offsets);
+    FGR_CHECK_LAUNCH("lengths_to_offsets_kernel");
+    return FGR_OK;
+}

@@ -214,10 +214,18 @@ struct DGrid {
 
 constexpr long long kHuge = 1ll << 62;
 
+// blocks >= n_clouds zero the histogram (4096 counters each) -- one launch instead of a
+// bbox launch plus a memset
 __global__ void __launch_bounds__(1024) dgrid_bbox_kernel(const float* __restrict__ pts,
                                                          const int64_t* __restrict__ off, float dl,
-                                                         DGrid* __restrict__ grids) {
+                                                         DGrid* __restrict__ grids, int n_clouds,
+                                                         int* __restrict__ zero, int64_t n_zero) {
     const int c = blockIdx.x;
+    if (c >= n_clouds) {                                   // block-uniform
+        const int64_t z0 = (int64_t)(c - n_clouds) * 4096;
+        for (int64_t i = z0 + threadIdx.x; i < min(z0 + 4096, n_zero); i += 1024) zero[i] = 0;
+        return;
+    }
     const int64_t b = off[c], e = off[c + 1];
     float mn[3], mx[3];
     block_bbox(pts, b, e, mn, mx);
@@ -405,10 +413,18 @@ struct RGrid {
 
 __host__ __device__ inline long long rgrid_cap(int64_t n_c) { return 4 * n_c + 1024; }
 
+// blocks >= n_clouds zero the cell starts (4096 each), as dgrid_bbox_kernel
 __global__ void __launch_bounds__(1024) rgrid_bbox_kernel(const float* __restrict__ s,
                                                          const int64_t* __restrict__ s_off,
-                                                         float radius, RGrid* __restrict__ grids) {
+                                                         float radius, RGrid* __restrict__ grids,
+                                                         int n_clouds, int* __restrict__ zero,
+                                                         int64_t n_zero) {
     const int c = blockIdx.x;
+    if (c >= n_clouds) {                                   // block-uniform
+        const int64_t z0 = (int64_t)(c - n_clouds) * 4096;
+        for (int64_t i = z0 + threadIdx.x; i < min(z0 + 4096, n_zero); i += 1024) zero[i] = 0;
+        return;
+    }
     const int64_t b = s_off[c], e = s_off[c + 1];
     float mn[3], mx[3];
     block_bbox(s, b, e, mn, mx);
@@ -660,13 +676,13 @@ extern "C" int fgr_grid_subsample_count(const float* points, const int64_t* off,
         set_error("fgr_grid_subsample_count: workspace %zu < %zu bytes", ws_bytes, g.total);
         return FGR_E_WORKSPACE;
     }
-    hipLaunchKernelGGL(dgrid_bbox_kernel, dim3(n_clouds), dim3(1024), 0, st, points, off, dl,
-                       g.grids);
+    hipLaunchKernelGGL(dgrid_bbox_kernel, dim3((unsigned)(n_clouds + ceil_div(cap + 1, 4096))),
+                       dim3(1024), 0, st, points, off, dl, g.grids, n_clouds, g.hist,
+                       (int64_t)(cap + 1));
     FGR_CHECK_LAUNCH("dgrid_bbox_kernel");
     hipLaunchKernelGGL(dgrid_base_kernel, dim3(1), dim3(64), 0, st, g.grids, n_clouds,
                        (long long)cap, g.ctl);
     FGR_CHECK_LAUNCH("dgrid_base_kernel");
-    FGR_CHECK_HIP(hipMemsetAsync(g.hist, 0, 4 * (cap + 1), st));
     const unsigned nb = (unsigned)ceil_div(n_points > 0 ? n_points : 1, 256);
     hipLaunchKernelGGL(dgrid_key_kernel, dim3(nb), dim3(256), 0, st, points, off, n_clouds,
                        n_points, dl, g.grids, g.ctl, g.hist, g.cellof, g.slot, g.keys);
@@ -731,10 +747,10 @@ extern "C" int fgr_radius_grid_build(const float* s, const int64_t* s_off, int32
     hipStream_t st = as_stream(stream);
     TimedCall timed_(st);
     const int64_t cap = 4 * ns + 1024ll * n_clouds;
-    hipLaunchKernelGGL(rgrid_bbox_kernel, dim3(n_clouds), dim3(1024), 0, st, s, s_off, radius,
-                       g.grids);
+    hipLaunchKernelGGL(rgrid_bbox_kernel, dim3((unsigned)(n_clouds + ceil_div(cap + 1, 4096))),
+                       dim3(1024), 0, st, s, s_off, radius, g.grids, n_clouds, g.start,
+                       (int64_t)(cap + 1));
     FGR_CHECK_LAUNCH("rgrid_bbox_kernel");
-    FGR_CHECK_HIP(hipMemsetAsync(g.start, 0, 4 * (cap + 1), st));
     if (ns > 0) {
         hipLaunchKernelGGL(rgrid_key_kernel, dim3((unsigned)ceil_div(ns, 256)), dim3(256), 0, st, s,
                            s_off, n_clouds, ns, g.grids, g.start, g.cellof, g.slot);

@@ -56,6 +56,9 @@ class PreprocessorHIP(nn.Module):
         lens = [int(p.shape[0]) for p in pts]
         points = torch.cat([p.float() for p in pts], 0).contiguous()
         off = ops.offsets(lens, device)
+        # device copies of the level's lengths: level 0 from the host list, deeper levels
+        # straight from the voxel counts (no host -> device copy, no extra sync)
+        len_dev = torch.tensor(lens, dtype=torch.int64, device=device)
         meta = {'points': [], 'neighbors': [], 'pools': [], 'upsamples': [], 'stack_lengths': []}
         host = {'lengths': [], 'offsets': []}
         layer_blocks, layer = [], 0
@@ -79,8 +82,8 @@ class PreprocessorHIP(nn.Module):
                 conv_i = torch.zeros((0, 1), dtype=torch.int64, device=device)
             if 'pool' in block or 'strided' in block:
                 dl = 2 * r_normal / cfg.conv_radius
-                pool_p, pool_lens = ops.grid_subsample(points, off, lens, dl)
-                pool_off = ops.offsets(pool_lens, device)
+                pool_p, pool_lens, pool_len_dev, pool_off = ops.grid_subsample(points, off, lens, dl,
+                                                                               device_layout=True)
                 pool_i = ops.radius_search(pool_p, pool_off, pool_lens, points, off, lens, r,
                                            limits[layer], self.mode, grid=grid)
                 up_grid = ops.radius_grid(pool_p, pool_off, pool_lens, 2 * r)
@@ -88,17 +91,17 @@ class PreprocessorHIP(nn.Module):
                                          limits[layer], self.mode, grid=up_grid)
             else:
                 pool_p = torch.zeros((0, 3), dtype=torch.float32, device=device)
-                pool_lens, pool_off = [], None
+                pool_lens, pool_off, pool_len_dev = [], None, None
                 pool_i = torch.zeros((0, 1), dtype=torch.int64, device=device)
                 up_i = torch.zeros((0, 1), dtype=torch.int64, device=device)
             meta['points'].append(points)
             meta['neighbors'].append(conv_i)
             meta['pools'].append(pool_i)
             meta['upsamples'].append(up_i)
-            meta['stack_lengths'].append(torch.tensor(lens, dtype=torch.int64, device=device))
+            meta['stack_lengths'].append(len_dev)
             host['lengths'].append(lens)
             host['offsets'].append(off)
-            points, lens, off = pool_p, pool_lens, pool_off
+            points, lens, off, len_dev = pool_p, pool_lens, pool_off, pool_len_dev
             r_normal *= 2
             layer += 1
             layer_blocks = []

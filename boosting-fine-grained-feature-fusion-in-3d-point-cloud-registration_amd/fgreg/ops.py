@@ -138,14 +138,16 @@ GRID_RADIX = os.environ.get('FGREG_GRID_SORT', 'dense') == 'radix'   # A/B switc
 
 
 def grid_subsample(points: torch.Tensor, off: torch.Tensor, lengths: Sequence[int], dl: float,
-                   return_keys=False, max_cells=None):
+                   return_keys=False, max_cells=None, device_layout=False):
     """Barycentre grid subsampling per cloud (grid_subsampling.cpp semantics).
 
     Returns (sub_points (M,3) f32, sub_lengths List[int][, keys (M,) int64]). One host
     sync (the voxel counts), as in the reference's own GPU path. ``max_cells``: the dense
     voxel-key histogram's capacity (None = the library default, -1 = the radix-sort path);
     a key space past it is reported by the count call and the count is redone with the
-    needed capacity (or the radix path beyond 2^28 counters).
+    needed capacity (or the radix path beyond 2^28 counters). ``device_layout``: also return
+    the sub-clouds' lengths (nc,) and row offsets (nc + 1,) as device int64 tensors, built on
+    the device from the counts (no host -> device copy): (sub, lengths, len_dev, off_dev).
     """
     _dev(points, off)
     pts = _c(points, torch.float32)
@@ -178,9 +180,25 @@ def grid_subsample(points: torch.Tensor, off: torch.Tensor, lengths: Sequence[in
     _lib.check(L.fgr_grid_subsample_fill(n, nc, cap, m, _ptr(ws), ws_bytes.value, _ptr(pts),
                                          _ptr(out), _ptr(keys), st), 'fgr_grid_subsample_fill')
     _end('grid_subsample', t0, 12 * (n + m))   # D4: 12 (N_in + N_out) bytes
+    if device_layout:
+        assert not return_keys
+        len_dev = counts[:nc]
+        off_dev = lengths_to_offsets(len_dev)
+        return out, host[:nc], len_dev, off_dev
     if return_keys:
         return out, host[:nc], keys
     return out, host[:nc]
+
+
+def lengths_to_offsets(len_dev: torch.Tensor) -> torch.Tensor:
+    """Device int64 lengths (n,) -> device row offsets (n + 1,), one launch, no host copy."""
+    _dev(len_dev)
+    assert len_dev.dtype == torch.int64 and len_dev.dim() == 1
+    n = len_dev.numel()
+    out = torch.empty(n + 1, dtype=torch.int64, device=len_dev.device)
+    _lib.check(_lib.load().fgr_lengths_to_offsets(_ptr(len_dev.contiguous()), n, _ptr(out), _stream()),
+               'fgr_lengths_to_offsets')
+    return out
 
 
 # Radius search over a cell grid for clouds of at least this many supports (below it the

@@ -347,6 +347,13 @@ int fgr_corr_attention(const float* q, int64_t ld_q, const float* k, int64_t ld_
 int fgr_copy_batch(int32_t n, const void* const* src, void* const* dst, const int64_t* bytes,
                    void* stream);
 
+/* Device-side row offsets from device-side lengths (int64, n entries -> n + 1 offsets,
+ * offsets[0] = 0), so a pyramid level's segment table is built without a host round trip
+ * (replaces the host-list -> device copy of fgreg.ops.offsets after grid subsampling;
+ * reference: the stack_lengths / batch offsets of PreprocessorGPU,
+ * finegrained_kpconv.py:422-542). One launch, asynchronous. */
+int fgr_lengths_to_offsets(const int64_t* lengths, int32_t n, int64_t* offsets, void* stream);
+
 /* ---- pose ----------------------------------------------------------------------------
  * fast_compute_rigid_transform (utils/se3_torch.py:226-273; threshold < 0 gives the
  * unthresholded compute_rigid_transform, :131-173) on n_batch independent problems

@@ -248,3 +248,15 @@ def test_grid_subsample_dense_matches_radix(gpu):
             o_pts, o_lens, o_keys = og.grid_subsample(P, L, dl, return_keys=True)
             assert a[1] == o_lens.tolist() and np.array_equal(a[0].cpu().numpy(), o_pts)
             assert np.array_equal(a[2].cpu().numpy(), o_keys)
+
+
+@pytest.mark.parametrize('n', [0, 1, 2, 16, 64, 65, 300])
+def test_lengths_to_offsets(gpu, n):
+    """fgr_lengths_to_offsets (device lengths -> device row offsets, the per-level segment
+    table of the preprocessing) equals the host prefix sum, across 64-entry chunk borders."""
+    import fgreg.ops as ops
+    rng = np.random.default_rng(n)
+    lens = rng.integers(0, 5000, n).astype(np.int64)
+    off = ops.lengths_to_offsets(torch.from_numpy(lens).to(gpu)).cpu().numpy()
+    assert off.shape == (n + 1,)
+    assert np.array_equal(off, np.concatenate([[0], np.cumsum(lens)]))
