@@ -47,6 +47,21 @@ class PreprocessorHIP(nn.Module):
         self.cfg = cfg
         self.mode = {'ball_query': ops.NB_INDEX, 'nanoflann': ops.NB_DIST}[neighbor_mode]
 
+    def _lengths_to_device(self, lens, device):
+        if device.type != 'cuda':
+            return torch.tensor(lens, dtype=torch.int64, device=device)
+        buf = getattr(self, '_pin', None)
+        if buf is None or buf.numel() < len(lens):
+            buf = torch.empty(max(64, len(lens)), dtype=torch.int64, pin_memory=True)
+            self._pin, self._pin_ev = buf, None
+        if self._pin_ev is not None:
+            self._pin_ev.synchronize()       # the previous copy out of the buffer is done
+        buf[:len(lens)].copy_(torch.tensor(lens, dtype=torch.int64))
+        out = buf[:len(lens)].to(device, non_blocking=True)
+        self._pin_ev = torch.cuda.Event()
+        self._pin_ev.record()
+        return out
+
     def forward(self, pts: List[torch.Tensor]):
         cfg = self.cfg
         limits = cfg.neighborhood_limits
@@ -55,10 +70,14 @@ class PreprocessorHIP(nn.Module):
         arch = cfg.architecture
         lens = [int(p.shape[0]) for p in pts]
         points = torch.cat([p.float() for p in pts], 0).contiguous()
-        off = ops.offsets(lens, device)
-        # device copies of the level's lengths: level 0 from the host list, deeper levels
-        # straight from the voxel counts (no host -> device copy, no extra sync)
-        len_dev = torch.tensor(lens, dtype=torch.int64, device=device)
+        # device lengths / offsets of every level without a synchronising copy: level 0's
+        # lengths by an asynchronous copy from a pinned staging buffer (reused: the previous
+        # forward's copy completed at its voxel-count readback), offsets by
+        # fgr_lengths_to_offsets; deeper levels straight from the voxel counts. So nothing in
+        # the forward waits on the GPU before the first count readback, and those launches
+        # queue behind the previous step's work.
+        len_dev = self._lengths_to_device(lens, device)
+        off = ops.lengths_to_offsets(len_dev)
         meta = {'points': [], 'neighbors': [], 'pools': [], 'upsamples': [], 'stack_lengths': []}
         host = {'lengths': [], 'offsets': []}
         layer_blocks, layer = [], 0
