@@ -116,6 +116,8 @@ __device__ __forceinline__ int find_segment(const int64_t* off, int n, int64_t r
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
 // Two-term fp16 splits and 3-way max by single VALU instructions (gfx950), shared by the
 // f16x3 GEMM and attention loops.
 // max(|a|, |b|, |c|) in one v_max3_f32 (no NaN canonicalisation: finite activations)
@@ -124,21 +126,37 @@ __device__ __forceinline__ float max3_abs(float a, float b, float c) {
     asm("v_max3_f32 %0, |%1|, |%2|, |%3|" : "=v"(r) : "v"(a), "v"(b), "v"(c));
     return r;
 }
-// packed f16 (hi terms) of a sc, b sc: v_fma_mixlo / mixhi (round to nearest even, as a
-// v_cvt_f16_f32 of the exact product)
-__device__ __forceinline__ unsigned split_hi2(float a, float b, float sc) {
-    unsigned d;
-    asm("v_fma_mixlo_f16 %0, %1, %2, 0" : "=v"(d) : "v"(a), "v"(sc));
-    asm("v_fma_mixhi_f16 %0, %1, %2, 0" : "+v"(d) : "v"(b), "v"(sc));
-    return d;
-}
-// packed f16 (lo terms) of a sc - hi_a, b sc - hi_b (hi from split_hi2: f16 halves of h)
-__device__ __forceinline__ unsigned split_lo2(float a, float b, float sc, unsigned h) {
-    unsigned d;
-    asm("v_fma_mixlo_f16 %0, %1, %2, -%3 op_sel_hi:[0,0,1]" : "=v"(d) : "v"(a), "v"(sc), "v"(h));
-    asm("v_fma_mixhi_f16 %0, %1, %2, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
-        : "+v"(d) : "v"(b), "v"(sc), "v"(h));
-    return d;
+// Eight values x[0..7] times a power of two sc, split into packed fp16 hi terms
+// h = f16(x sc) and lo terms l = f16(x sc - h): 16 v_fma_mix{lo,hi}_f16 (one per term and
+// element; x sc is exact and so is x sc - h in fp32, so the bits equal the two-step split)
+// in ONE asm statement that ends with `s_nop 1`: hipcc pads nothing inside asm and only one
+// state after it, while a VGPR written by VALU and read as an MFMA operand needs two
+// (cdna_hip_programming.md 5.7 item 2) -- without the pad an MFMA issued right after can
+// read stale fragments. Outputs are early-clobber (written while inputs are still read).
+__device__ __forceinline__ void split8_f16(const float (&x)[8], float sc, u32x4& h, u32x4& l) {
+    unsigned h0, h1, h2, h3, l0, l1, l2, l3;
+    asm("v_fma_mixlo_f16 %0, %8, %16, 0\n\t"
+        "v_fma_mixlo_f16 %1, %10, %16, 0\n\t"
+        "v_fma_mixlo_f16 %2, %12, %16, 0\n\t"
+        "v_fma_mixlo_f16 %3, %14, %16, 0\n\t"
+        "v_fma_mixhi_f16 %0, %9, %16, 0\n\t"
+        "v_fma_mixhi_f16 %1, %11, %16, 0\n\t"
+        "v_fma_mixhi_f16 %2, %13, %16, 0\n\t"
+        "v_fma_mixhi_f16 %3, %15, %16, 0\n\t"
+        "v_fma_mixlo_f16 %4, %8, %16, -%0 op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixlo_f16 %5, %10, %16, -%1 op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixlo_f16 %6, %12, %16, -%2 op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixlo_f16 %7, %14, %16, -%3 op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixhi_f16 %4, %9, %16, -%0 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixhi_f16 %5, %11, %16, -%1 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixhi_f16 %6, %13, %16, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixhi_f16 %7, %15, %16, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+        "s_nop 1"
+        : "=&v"(h0), "=&v"(h1), "=&v"(h2), "=&v"(h3), "=&v"(l0), "=&v"(l1), "=&v"(l2), "=&v"(l3)
+        : "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(x[4]), "v"(x[5]), "v"(x[6]), "v"(x[7]),
+          "v"(sc));
+    h = u32x4{h0, h1, h2, h3};
+    l = u32x4{l0, l1, l2, l3};
 }
 
 }  // namespace fgr

@@ -245,14 +245,7 @@ __global__ void __launch_bounds__(256 * KW) gemm_g5(G5Args p) {
                 }
                 // hi = f16(x sc), lo = f16(x sc - hi) by v_fma_mix (x sc exact: power of two;
                 // x sc - hi exact in fp32): one VALU per term and element
-                u32x4 hh, mm;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    hh[e] = split_hi2(x[2 * e], x[2 * e + 1], scv[i]);
-                    mm[e] = split_lo2(x[2 * e], x[2 * e + 1], scv[i], hh[e]);
-                }
-                bh[i] = hh;
-                bl[i] = mm;
+                split8_f16(x, scv[i], bh[i], bl[i]);
             } else {
                 bf16x8 h;
 #pragma unroll

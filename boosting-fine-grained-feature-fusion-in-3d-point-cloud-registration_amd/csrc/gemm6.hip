@@ -332,11 +332,7 @@ __global__ void __launch_bounds__(256) split_rows_rs_kernel(const float* __restr
         float v[8];
         load8(s, v);
         u32x4 hh, ll;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            hh[q] = split_hi2(v[2 * q], v[2 * q + 1], sc);
-            ll[q] = split_lo2(v[2 * q], v[2 * q + 1], sc, hh[q]);
-        }
+        split8_f16(v, sc, hh, ll);
         u32x4* dst = img + (panel * ksteps + s) * 128;
         dst[lane] = hh;
         dst[64 + lane] = ll;
