@@ -616,7 +616,20 @@ extern "C" int fgr_layernorm(float* x, int64_t n, int32_t d, const float* gamma,
                        reinterpret_cast<uintptr_t>(add) | reinterpret_cast<uintptr_t>(pre_bias)) & 15) == 0;
     if (vec) {
         // lanes per row sized so each lane holds at most 4 float4 (rows stay in flight)
-        if (d <= 256)
+        // d <= 256: 32 lanes per row (2 float4 each; measured 6-7 % faster than 16 lanes x 4 at
+        // 9544 x 256, tools/ln_bench.py); FGR_LN_LPR = 16 / 64 selects the others (A/B)
+        const char* lp = getenv("FGR_LN_LPR");
+        const int lpr = (lp && lp[0]) ? atoi(lp) : 32;
+        if (d <= 128 && lpr == 32)
+            hipLaunchKernelGGL((layernorm_lpr_kernel<32, 1>), dim3((unsigned)ceil_div(n, 8)),
+                               dim3(256), 0, st, x, n, d, gamma, beta, eps, add, pre_bias, out);
+        else if (d <= 256 && lpr == 32)
+            hipLaunchKernelGGL((layernorm_lpr_kernel<32, 2>), dim3((unsigned)ceil_div(n, 8)),
+                               dim3(256), 0, st, x, n, d, gamma, beta, eps, add, pre_bias, out);
+        else if (d <= 256 && lpr == 64)
+            hipLaunchKernelGGL((layernorm_lpr_kernel<64, 1>), dim3((unsigned)ceil_div(n, 4)),
+                               dim3(256), 0, st, x, n, d, gamma, beta, eps, add, pre_bias, out);
+        else if (d <= 256)
             hipLaunchKernelGGL((layernorm_lpr_kernel<16, 4>), dim3((unsigned)ceil_div(n, 16)),
                                dim3(256), 0, st, x, n, d, gamma, beta, eps, add, pre_bias, out);
         else if (d <= 512)

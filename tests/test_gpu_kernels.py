@@ -122,7 +122,7 @@ def test_sine_pos_embed_vs_reference(gpu, d):
 def test_layernorm_vs_torch(gpu):
     import fgreg.ops as ops
     rng = np.random.default_rng(1)
-    for d in (32, 96, 256, 512, 1024):
+    for d in (32, 64, 96, 128, 192, 256, 512, 1024):
         x = torch.from_numpy(rng.normal(1, 2, (333, d)).astype(np.float32))
         w = torch.from_numpy(rng.normal(1, 0.1, d).astype(np.float32))
         b = torch.from_numpy(rng.normal(0, 0.1, d).astype(np.float32))
