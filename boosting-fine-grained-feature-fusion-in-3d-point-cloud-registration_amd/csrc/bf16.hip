@@ -464,8 +464,8 @@ extern "C" int fgr_gemm_bf16(const float* a, int64_t lda, const void* w_img, flo
     else if (m <= 4096 && k >= 2048)
         cfg = 'W';
     else
-        cfg = n <= 256 && k >= 1000 ? 'I' : 'z';
-    if (((cfg >= 'A' && cfg <= 'W') || (cfg >= '0' && cfg <= '9')) && k % 8 == 0) {
+        cfg = n <= 256 && k >= 1000 ? 'X' : 'z';
+    if (((cfg >= 'A' && cfg <= 'Z') || (cfg >= '0' && cfg <= '9')) && k % 8 == 0) {
         FGR_REQUIRE(gemm_g5_bf16(cfg, a, lda, w_img, ksteps_bf(k), c, ldc, bias, r, ldr, m, n, k, act,
                      vo ? 1 : 0, st),
                     "fgr_gemm_bf16: g5 variant %c unavailable", cfg);

@@ -1180,6 +1180,7 @@ extern "C" int fgr_gemm_f16x3(const float* a, int64_t lda, const void* w_img, fl
     // tiles (v4 -- W fragments straight to registers -- for K >= 1024, double-buffered v2
     // for K >= 512), very tall ones 64 x 128; narrow outputs (N <= 256) and short row counts
     // (M <= 4096, N <= 512) the 64 x 64 LDS-DMA g5 ('I') when K % 8 == 0, else the 64 x 64 v4.
+    // X / Y are I / B with the row-major staged epilogue (3-7 % faster; r02_gemm_tiles_epi.txt).
     // Few tiles (<= 400 of 64 x 64, e.g. the 3DMatch transformer's 2 x 1060 tokens) with
     // K >= 512: the two-k-group g5 ('W', 'T'; 8 waves per block) -- 1.1-1.45x there
     // (profiles/r02_gemm_tiles_splitk*.txt).
@@ -1192,19 +1193,19 @@ extern "C" int fgr_gemm_f16x3(const float* a, int64_t lda, const void* w_img, fl
     else if (g5ok && tiles64 <= 400 && k >= 512 && n >= 32)
         cfg = (k >= 2048 || n <= 64) ? 'S' : ((n <= 128 && k >= 1024 && tiles64 > 256) ? 'T' : 'W');
     else if (g5ok && m <= 4096)
-        cfg = (n <= 512 || (n <= 1024 && k <= 512)) ? 'I' : 'B';
+        cfg = (n <= 512 || (n <= 1024 && k <= 512)) ? 'X' : 'Y';
     else if (n >= 512)
-        cfg = k >= 1024 ? 'u' : (k >= 512 ? (g5ok ? 'B' : 'k') : 'b');
+        cfg = k >= 1024 ? 'u' : (k >= 512 ? (g5ok ? 'Y' : 'k') : 'b');
     else if (tiles64 >= 2048)
         cfg = 'b';
     else if (g5ok && (k >= 512 || m <= 16384))
-        cfg = 'I';
+        cfg = 'X';
     else if (n <= 128 && k >= 1024)
         cfg = 'f';
     else
         cfg = k <= 1024 ? 't' : 'e';
     // g5 (gemm5.hip: LDS-DMA pipeline, A split after the read): A..W, K % 8 == 0 only
-    if (((cfg >= 'A' && cfg <= 'W') || (cfg >= '0' && cfg <= '9')) && k % 8 == 0) {
+    if (((cfg >= 'A' && cfg <= 'Z') || (cfg >= '0' && cfg <= '9')) && k % 8 == 0) {
         FGR_REQUIRE(gemm_g5_f16x3(cfg, a, lda, w_img, ksteps_h3(k), wsc, c, ldc, bias, r, ldr, m, n, k, act,
                       vo ? 1 : 0, st),
                     "fgr_gemm_f16x3: g5 variant %c unavailable", cfg);

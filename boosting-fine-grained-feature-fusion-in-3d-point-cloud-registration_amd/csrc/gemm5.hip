@@ -96,7 +96,8 @@ __device__ __forceinline__ float finish5(float y, float b, float r, int act) {
 // WC waves across the columns (1: every wave owns BM / 4 rows x all BN columns; 2: a 2 x 2
 // layout, BM / 2 rows x BN / 2 columns per wave -- a third less LDS read traffic per MFMA,
 // each A row split by the two waves that share it).
-template <int BM, int BN, int KS, int S, int TERMS, bool PIPE, int KW = 1, int WC = 1>
+template <int BM, int BN, int KS, int S, int TERMS, bool PIPE, int KW = 1, int WC = 1,
+          bool EPI_LDS = false>
 __global__ void __launch_bounds__(256 * KW) gemm_g5(G5Args p) {
     constexpr int NW = 4 * KW;                 // waves per block
     constexpr int RW = 4 / WC;                 // waves across the rows
@@ -395,6 +396,62 @@ __global__ void __launch_bounds__(256 * KW) gemm_g5(G5Args p) {
         }
     }
 
+    if constexpr (KW == 1 && WC == 1) {
+        if (p.vec_out && EPI_LDS) {
+            // staged epilogue: each wave parks its scaled WR x BN tile in the drained stage
+            // buffers and writes it back row-major, 16-B per lane over whole 256 / 512-B row
+            // slices (the MFMA layout stores 64-B pieces of 16 rows per instruction); bias,
+            // residual and activation applied in the row-major pass (coalesced R reads)
+            constexpr int RS_ = BN + 4;                         // padded row stride (floats)
+            static_assert(S * ST * 16 >= 4 * WR * RS_ * 4, "epilogue staging space");
+            __syncthreads();                                    // every stage read retired
+            float* buf = reinterpret_cast<float*>(lds) + wv * (WR * RS_);
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const float rs = TERMS == 2 ? __builtin_ldexpf(1.f, -sh[i]) : 1.f;
+#pragma unroll
+                for (int j = 0; j < TNW; ++j) {
+                    const int n = min(n0 + 16 * j + 4 * g, ((p.N + 15) / 16) * 16 - 4);
+                    float4 ws = make_float4(1.f, 1.f, 1.f, 1.f);
+                    if constexpr (TERMS == 2) ws = *reinterpret_cast<const float4*>(p.wsc + n);
+                    *reinterpret_cast<float4*>(buf + (16 * i + c) * RS_ + 16 * j + 4 * g) =
+                        make_float4(acc[j][i][0] * rs * ws.x, acc[j][i][1] * rs * ws.y,
+                                    acc[j][i][2] * rs * ws.z, acc[j][i][3] * rs * ws.w);
+                }
+            }
+            __syncthreads();
+            constexpr int LPRW = BN / 4, RPI = 64 / LPRW;       // lanes per row, rows per pass
+            const int col = 4 * (lane % LPRW);
+            const int n = n0 + col;
+#pragma unroll
+            for (int it = 0; it < WR / RPI; ++it) {
+                const int row = it * RPI + lane / LPRW;
+                const int m = m0 + rw * WR + row;
+                if (m >= p.M || n >= p.N) continue;
+                const float4 y = *reinterpret_cast<const float4*>(buf + row * RS_ + col);
+                float* crow = p.C + (int64_t)m * p.ldc;
+                const float* rrow = p.R ? p.R + (int64_t)m * p.ldr : nullptr;
+                if (n + 3 < p.N) {
+                    float4 bb = make_float4(0.f, 0.f, 0.f, 0.f), rr = bb;
+                    if (p.bias) bb = *reinterpret_cast<const float4*>(p.bias + n);
+                    if (rrow) rr = *reinterpret_cast<const float4*>(rrow + n);
+                    *reinterpret_cast<float4*>(crow + n) =
+                        make_float4(finish5(y.x, bb.x, rr.x, p.act), finish5(y.y, bb.y, rr.y, p.act),
+                                    finish5(y.z, bb.z, rr.z, p.act), finish5(y.w, bb.w, rr.w, p.act));
+                } else {
+                    const float yv[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        if (n + e >= p.N) break;
+                        crow[n + e] = finish5(yv[e], p.bias ? p.bias[n + e] : 0.f,
+                                              rrow ? rrow[n + e] : 0.f, p.act);
+                    }
+                }
+            }
+            return;
+        }
+    }
+
     // epilogue: lane holds C[m = m0 + rw WR + 16i + c][n = n0 + 16 (cw TNW + j) + 4g + r]
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -430,10 +487,11 @@ __global__ void __launch_bounds__(256 * KW) gemm_g5(G5Args p) {
     }
 }
 
-template <int BM, int BN, int KS, int S, int TERMS, bool PIPE = false, int KW = 1, int WC = 1>
+template <int BM, int BN, int KS, int S, int TERMS, bool PIPE = false, int KW = 1, int WC = 1,
+          bool EPI = false>
 void launch_g5(const G5Args& a, hipStream_t st) {
     const int nbm = (a.M + BM - 1) / BM, nbn = (a.N + BN - 1) / BN;
-    hipLaunchKernelGGL((gemm_g5<BM, BN, KS, S, TERMS, PIPE, KW, WC>), dim3((unsigned)(nbm * nbn)),
+    hipLaunchKernelGGL((gemm_g5<BM, BN, KS, S, TERMS, PIPE, KW, WC, EPI>), dim3((unsigned)(nbm * nbn)),
                        dim3(256 * KW), 0, st, a);
 }
 
@@ -486,6 +544,10 @@ bool dispatch_g5(char cfg, const G5Args& a, hipStream_t st) {
         // 128 x 128, deeper pipelines (L2 / MALL traffic per MFMA halves vs 64 x 64): 8, 9
         case '8': launch_g5<128, 128, 1, 4, TERMS, false>(a, st); break;
         case '9': launch_g5<128, 128, 1, 5, TERMS, false>(a, st); break;
+        // staged (row-major) epilogue: X, Y, Z = I, B, G with it
+        case 'X': launch_g5<64, 64, 1, 3, TERMS, false, 1, 1, true>(a, st); break;
+        case 'Y': launch_g5<64, 128, 1, 3, TERMS, false, 1, 1, true>(a, st); break;
+        case 'Z': launch_g5<64, 256, 1, 3, TERMS, false, 1, 1, true>(a, st); break;
         default: return false;
     }
     return true;
