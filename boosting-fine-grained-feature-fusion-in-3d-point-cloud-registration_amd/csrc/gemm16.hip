@@ -108,14 +108,20 @@ __device__ __forceinline__ void store_out4(const float (&y)[4], const float* bia
     }
 }
 
-template <int BM, int BN, bool KVEC>
+// EPI: staged epilogue -- each wave's scaled (BM/2) x (BN/2) tile parked in LDS (sharing the
+// A / W image space) and written row-major, 16 B per lane over whole row slices.
+template <int BM, int BN, bool KVEC, bool EPI = false>
 __global__ void __launch_bounds__(256) gemm_f16x3_kernel(GemmH3Args p) {
     constexpr int TM = BM / 32, TN = BN / 32;          // 16x16 subtiles per wave (m, n)
     constexpr int UA = BM * 4 / 256;                    // A units (8 k of one row) per thread
     constexpr int UW = 8 * BN / 256;                    // W image units per thread
     static_assert(UA >= 1 && UW >= 1, "tile");
-    __shared__ u32x4 a_lds[2 * 4 * BM];
-    __shared__ u32x4 w_lds[8 * BN];
+    constexpr int ERS = BN / 2 + 4;                     // staged row stride (floats)
+    constexpr int IMG_U = 2 * 4 * BM + 8 * BN;          // A + W images (16-B units)
+    constexpr int EPI_U = EPI ? (4 * (BM / 2) * ERS * 4 + 15) / 16 : 0;
+    __shared__ u32x4 img_lds[IMG_U > EPI_U ? IMG_U : EPI_U];
+    u32x4* a_lds = img_lds;
+    u32x4* w_lds = img_lds + 2 * 4 * BM;
     __shared__ int sh_lds[BM];
 
     // XCD-aware order: hardware dispatches block b to XCD b % 8; remap (bijectively) so that
@@ -256,6 +262,39 @@ __global__ void __launch_bounds__(256) gemm_f16x3_kernel(GemmH3Args p) {
         }
     }
 
+    if constexpr (EPI) {
+        if (p.vec_out) {
+            __syncthreads();                                    // image reads retired
+            float* buf = reinterpret_cast<float*>(img_lds) + wv * ((BM / 2) * ERS);
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const float rs = __builtin_ldexpf(1.f, -shr[i]);
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    const int n = min(n0 + wn + 16 * j + 4 * g, ((p.N + 15) / 16) * 16 - 4);
+                    const float4 ws = *reinterpret_cast<const float4*>(p.wsc + n);
+                    *reinterpret_cast<float4*>(buf + (16 * i + c) * ERS + 16 * j + 4 * g) =
+                        make_float4(acc[j][i][0] * rs * ws.x, acc[j][i][1] * rs * ws.y,
+                                    acc[j][i][2] * rs * ws.z, acc[j][i][3] * rs * ws.w);
+                }
+            }
+            __syncthreads();
+            constexpr int LPRW = BN / 8, RPI = 64 / LPRW;       // lanes per row, rows per pass
+            const int col = 4 * (lane % LPRW);
+            const int n = n0 + wn + col;
+#pragma unroll
+            for (int it = 0; it < (BM / 2) / RPI; ++it) {
+                const int row = it * RPI + lane / LPRW;
+                const int m = m0 + wm + row;
+                if (m >= p.M || n >= p.N) continue;
+                const float4 yv = *reinterpret_cast<const float4*>(buf + row * ERS + col);
+                const float y[4] = {yv.x, yv.y, yv.z, yv.w};
+                store_out4(y, p.bias, p.R ? p.R + (int64_t)m * p.ldr : nullptr,
+                           p.C + (int64_t)m * p.ldc, n, p.N, p.act, true);
+            }
+            return;
+        }
+    }
     // epilogue: lane holds C[m = m0 + wm + 16i + c][n = n0 + wn + 16j + 4g + r], r = 0..3
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -1071,14 +1110,14 @@ __global__ void split_weights_h3_kernel(const float* __restrict__ w, int n, int 
     img[u] = __builtin_bit_cast(u32x4, out);
 }
 
-template <int BM, int BN>
+template <int BM, int BN, bool EPI = false>
 void launch_h3(const GemmH3Args& a, hipStream_t st) {
     const int nbm = (a.M + BM - 1) / BM, nbn = (a.N + BN - 1) / BN;
     if (a.K % 8 == 0)
-        hipLaunchKernelGGL((gemm_f16x3_kernel<BM, BN, true>), dim3((unsigned)(nbm * nbn)),
+        hipLaunchKernelGGL((gemm_f16x3_kernel<BM, BN, true, EPI>), dim3((unsigned)(nbm * nbn)),
                            dim3(256), 0, st, a);
     else
-        hipLaunchKernelGGL((gemm_f16x3_kernel<BM, BN, false>), dim3((unsigned)(nbm * nbn)),
+        hipLaunchKernelGGL((gemm_f16x3_kernel<BM, BN, false, EPI>), dim3((unsigned)(nbm * nbn)),
                            dim3(256), 0, st, a);
 }
 
@@ -1180,7 +1219,8 @@ extern "C" int fgr_gemm_f16x3(const float* a, int64_t lda, const void* w_img, fl
     // tiles (v4 -- W fragments straight to registers -- for K >= 1024, double-buffered v2
     // for K >= 512), very tall ones 64 x 128; narrow outputs (N <= 256) and short row counts
     // (M <= 4096, N <= 512) the 64 x 64 LDS-DMA g5 ('I') when K % 8 == 0, else the 64 x 64 v4.
-    // X / Y are I / B with the row-major staged epilogue (3-7 % faster; r02_gemm_tiles_epi.txt).
+    // X / Y are I / B and y is b with the row-major staged epilogue (3-8 % faster;
+    // profiles/r02_gemm_tiles_epi.txt, r02_gemm_tiles_by.txt).
     // Few tiles (<= 400 of 64 x 64, e.g. the 3DMatch transformer's 2 x 1060 tokens) with
     // K >= 512: the two-k-group g5 ('W', 'T'; 8 waves per block) -- 1.1-1.45x there
     // (profiles/r02_gemm_tiles_splitk*.txt).
@@ -1195,9 +1235,9 @@ extern "C" int fgr_gemm_f16x3(const float* a, int64_t lda, const void* w_img, fl
     else if (g5ok && m <= 4096)
         cfg = (n <= 512 || (n <= 1024 && k <= 512)) ? 'X' : 'Y';
     else if (n >= 512)
-        cfg = k >= 1024 ? 'u' : (k >= 512 ? (g5ok ? 'Y' : 'k') : 'b');
+        cfg = k >= 1024 ? 'u' : (k >= 512 ? (g5ok ? 'Y' : 'k') : 'y');
     else if (tiles64 >= 2048)
-        cfg = 'b';
+        cfg = 'y';
     else if (g5ok && (k >= 512 || m <= 16384))
         cfg = 'X';
     else if (n <= 128 && k >= 1024)
@@ -1246,6 +1286,8 @@ extern "C" int fgr_gemm_f16x3(const float* a, int64_t lda, const void* w_img, fl
         launch_h3<128, 128>(g, st);
     else if (cfg == 'b')
         launch_h3<64, 128>(g, st);
+    else if (cfg == 'y')                                   // 'b' with the staged epilogue
+        launch_h3<64, 128, true>(g, st);
     else if (cfg == 'd')
         launch_h3<128, 64>(g, st);
     else
