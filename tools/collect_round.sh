@@ -1,0 +1,14 @@
+#!/bin/bash
+# Copies one gpu_round.sh run's summaries from gpurun_out/ into profiles/ under <tag>:
+# bench lines, per-shape GEMM tables, rocprofv3 --stats summaries and the per-step kernel
+# table of the timed region. usage: bash tools/collect_round.sh <tag>
+set -e
+tag=$1
+for pair in "modelnet:bench:gemm:prof" "3dmatch:bench3d:gemm3d:prof3d" "3dlomatch:benchlo:gemmlo:proflo"; do
+  IFS=: read wl b g p <<< "$pair"
+  cp gpurun_out/${b}_$tag.json profiles/${tag}_${wl}_bench.json
+  cp gpurun_out/${g}_$tag.json profiles/${tag}_${wl}_gemm_table.json
+  cp gpurun_out/${p}_$tag/*/*_kernel_stats.csv profiles/${tag}_${wl}_kernel_stats.csv
+  ms=$(python3 -c "import json;print(json.loads(open('gpurun_out/${p}_$tag.json').read().strip().splitlines()[-1])['ms_per_step'])")
+  python3 tools/kernel_stats.py gpurun_out/${p}_$tag/*/*_kernel_trace.csv 20 $ms > profiles/${tag}_${wl}_kernel_stats_per_step.txt
+done
