@@ -230,7 +230,7 @@ def main():
             torch.cuda.synchronize()
         else:
             # algorithmic work per launch (untimed pass with counting on)
-            fams = ['kpconv_gather', 'attention', 'gemm'] + list(OTHER)
+            fams = ['kpconv_gather', 'kpconv_fused', 'attention', 'gemm'] + list(OTHER)
             timer = ops.KernelTimer(fams)
             timer.count = True
             ops.TIMER = timer

@@ -33,6 +33,11 @@ SIGNATURES = {
     'fgr_kpconv_gather': [_vp, _vp, _i64, _i64, _vp, _i32, _vp, _i32, _vp, _i32, _f32, _vp, _vp,
                           _vp, _sz, _vp],
     'fgr_max_pool': [_vp, _i64, _i32, _vp, _i64, _i32, _vp, _vp],
+    'fgr_kpconv_fused_weights_bytes': [_i32, _i32, _i32, _i32, ctypes.POINTER(_sz)],
+    'fgr_kpconv_fused_weights': [_vp, _i32, _i32, _i32, _i32, _vp, _vp],
+    'fgr_kpconv_fused_workspace': [_i64, ctypes.POINTER(_sz)],
+    'fgr_kpconv_fused': [_vp, _vp, _i64, _i64, _vp, _i32, _vp, _i32, _vp, _i32, _f32, _vp, _i32,
+                         _i32, _vp, _i64, _vp, _vp, _sz, _vp],
     'fgr_instnorm_workspace': [_i64, _i32, _i32, ctypes.POINTER(_sz)],
     'fgr_instnorm': [_vp, _i64, _i32, _vp, _i32, _i64, _vp, _f32, _i32, _vp, _i32, _vp, _vp, _sz,
                      _vp],
@@ -87,6 +92,7 @@ SIGNATURES = {
 
 NB_INDEX, NB_DIST = 0, 1
 ACT_NONE, ACT_LEAKY, ACT_RELU, ACT_RELU_RES_LEAKY = 0, 1, 2, 3
+KPF_F16X3, KPF_BF16 = 0, 1
 
 _lib = None
 

@@ -26,6 +26,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import _lib
 from . import ops
 from . import linear as lin
 from .linear import linear
@@ -194,6 +195,16 @@ def init_kernel_points(radius, n_kp, rng=np.random):
 R2N = os.environ.get('FGREG_R2N', 'auto')
 
 
+# Fused KPConv dispatch (FGREG_KPF): '1' every eligible layer, '0' never (gather + GEMM)
+KPF = os.environ.get('FGREG_KPF', '0')
+
+
+def _kpf_mode(cin, n_kp):
+    if KPF != '1' or cin % 32 != 0 or n_kp > 15:
+        return None
+    return {'f16x3': _lib.KPF_F16X3, 'bf16': _lib.KPF_BF16}.get(lin.MODE)
+
+
 class KPConv(nn.Module):
     """Rigid KPConv (finegrained_kpconv_blocks.py:171-401): linear influence, sum mode."""
 
@@ -213,7 +224,13 @@ class KPConv(nn.Module):
 
     def forward_unnormalized(self, q_pts, s_pts, neighb_inds, x):
         """-> (sum_k WF_k @ W_k (Nq, Cout), nnorm (Nq,)). The reference divides the first
-        by the second (:395-399); callers fuse that division into the next kernel."""
+        by the second (:395-399); callers fuse that division into the next kernel.
+        Fused (fgr_kpconv_fused: gather + weight GEMM in one launch, wf never written) where
+        the channel width allows it (Cin % 32 == 0) in the f16x3 / bf16 modes; ``KPF``."""
+        mode = _kpf_mode(x.shape[1], self.K)
+        if mode is not None:
+            return ops.kpconv_fused(q_pts, s_pts, neighb_inds, x, self.kernel_points,
+                                    self.KP_extent, self.weights, mode)
         wf, nnorm = ops.kpconv_gather(q_pts, s_pts, neighb_inds, x, self.kernel_points,
                                       self.KP_extent)
         out = linear(wf.view(wf.shape[0], -1), self.weights, transpose=True)

@@ -339,6 +339,73 @@ def gather_bytes(idx, ns, cin, n_kp):
     return nq * (8 * H + 12 + 4 * n_kp * cin + 4) + v * (12 + 4 * cin)
 
 
+class KPFusedWeight:
+    """fgr_kpconv_fused_weights image of a KPConv weight (K, Cin, Cout) for one mode, cached
+    against the tensor's identity / version / data pointer (as linear.split_weight3)."""
+    __slots__ = ('img', 'mode', 'src', 'version', 'ptr')
+
+    def __init__(self, w, mode):
+        L = _lib.load()
+        K, cin, cout = w.shape
+        nb = _lib._sz(0)
+        _lib.check(L.fgr_kpconv_fused_weights_bytes(K, cin, cout, mode, nb),
+                   'fgr_kpconv_fused_weights_bytes')
+        self.img = torch.empty(nb.value, dtype=torch.uint8, device=w.device)
+        wc = w.detach().contiguous()
+        _lib.check(L.fgr_kpconv_fused_weights(_ptr(wc), K, cin, cout, mode, _ptr(self.img),
+                                              _stream()), 'fgr_kpconv_fused_weights')
+        self.mode, self.src, self.version, self.ptr = mode, w, w._version, w.data_ptr()
+
+
+_KPF_CACHE = {}
+
+
+def kpconv_fused_weight(w, mode) -> KPFusedWeight:
+    ent = _KPF_CACHE.get((id(w), mode))
+    if not (ent is not None and ent.src is w and ent.version == w._version
+            and ent.ptr == w.data_ptr()):
+        ent = KPFusedWeight(w, mode)
+        _KPF_CACHE[(id(w), mode)] = ent
+    return ent
+
+
+def kpconv_fused(q, s, idx, x, kernel_points, extent, w, mode=_lib.KPF_F16X3):
+    """-> (out (Nq, Cout) = sum_k wf_k @ W_k, nnorm (Nq,)) by fgr_kpconv_fused: the gather and
+    the weight GEMM in one launch (finegrained_kpconv_blocks.py:296-399 up to the division)."""
+    _dev(q, s, idx, x, kernel_points, w)
+    q, s, x = _c(q, torch.float32), _c(s, torch.float32), _c(x, torch.float32)
+    idx = _c(idx, torch.int64)
+    kp = _c(kernel_points, torch.float32)
+    nq, ns = q.shape[0], s.shape[0]
+    K, cin, cout = w.shape
+    assert idx.dim() == 2 and idx.shape[0] == nq and x.dim() == 2 and x.shape == (ns, cin)
+    assert kp.shape == (K, 3)
+    if x.data_ptr() % 16:
+        x = x.clone()
+    img = kpconv_fused_weight(w, mode)
+    out = torch.empty((nq, cout), dtype=torch.float32, device=q.device)
+    nnorm = torch.empty((nq,), dtype=torch.float32, device=q.device)
+    L = _lib.load()
+    nb = _lib._sz(0)
+    _lib.check(L.fgr_kpconv_fused_workspace(ns, nb), 'fgr_kpconv_fused_workspace')
+    ws = _workspace(q.device, nb.value)
+    t0 = _begin('kpconv_fused', (nq, cout, K * cin))
+    _lib.check(L.fgr_kpconv_fused(_ptr(q), _ptr(s), nq, ns, _ptr(idx), idx.shape[1], _ptr(x), cin,
+                                  _ptr(kp), K, float(extent), _ptr(img.img), cout, mode, _ptr(out),
+                                  out.stride(0), _ptr(nnorm), _ptr(ws), nb.value, _stream()),
+               'fgr_kpconv_fused')
+    _end('kpconv_fused', t0, lambda: fused_bytes(idx, ns, cin, cout))
+    return out, nnorm
+
+
+def fused_bytes(idx, ns, cin, cout):
+    """Algorithmic HBM bytes of one fgr_kpconv_fused launch (SURVEY.md §8(d) D4 with the wf
+    term replaced by the output row): sum_q [8*H + 12 + v_q*(12 + 4*cin) + 4*cout + 4]."""
+    nq, H = idx.shape
+    v = int((idx < ns).sum().item())
+    return nq * (8 * H + 12 + 4 * cout + 4) + v * (12 + 4 * cin)
+
+
 def max_pool(x, idx) -> torch.Tensor:
     _dev(x, idx)
     x, idx = _c(x, torch.float32), _c(idx, torch.int64)

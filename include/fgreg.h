@@ -132,6 +132,27 @@ int fgr_kpconv_gather(const float* q, const float* s, int64_t nq, int64_t ns, co
                       float extent, float* wf, float* nnorm, void* workspace, size_t ws_bytes,
                       void* stream);
 
+/* Fused KPConv: the gather-weight stage above and the weight GEMM in ONE
+ * launch, wf never written (finegrained_kpconv_blocks.py:296-399 up to the division):
+ *   out[q, n] = sum_{k, c} wf[q, k, c] W[k, c, n]   (out: nq x cout, row stride ldo),
+ *   nnorm[q]  = as fgr_kpconv_gather;  the caller divides (or fuses out / nnorm downstream).
+ * mode FGR_KPF_F16X3: fp32-accurate (f16x3 split MFMA, the contract of fgr_gemm_f16x3);
+ * FGR_KPF_BF16: wf rounded to bf16 where it enters the MFMA (the bf16 compute mode).
+ * W (n_kp, cin, cout) fp32 contiguous -> image by fgr_kpconv_fused_weights (built once per
+ * weight, fgr_kpconv_fused_weights_bytes() bytes, 16-B aligned; the contraction order of the
+ * fused kernel). cin % 32 == 0, n_kp <= 15; x, w_img, out 16-B aligned.
+ * workspace: fgr_kpconv_fused_workspace() bytes (per-source-row flags of the normaliser). */
+enum { FGR_KPF_F16X3 = 0, FGR_KPF_BF16 = 1 };
+int fgr_kpconv_fused_weights_bytes(int32_t n_kp, int32_t cin, int32_t cout, int32_t mode,
+                                   size_t* bytes);
+int fgr_kpconv_fused_weights(const float* w, int32_t n_kp, int32_t cin, int32_t cout,
+                             int32_t mode, void* img, void* stream);
+int fgr_kpconv_fused_workspace(int64_t ns, size_t* bytes);
+int fgr_kpconv_fused(const float* q, const float* s, int64_t nq, int64_t ns, const int64_t* idx,
+                     int32_t width, const float* x, int32_t cin, const float* kp, int32_t n_kp,
+                     float extent, const void* w_img, int32_t cout, int32_t mode, float* out,
+                     int64_t ldo, float* nnorm, void* workspace, size_t ws_bytes, void* stream);
+
 /* max_pool (finegrained_kpconv_blocks.py:125-141): out[q, c] = max over the row of
  * x[idx[q, h], c], shadow entries contributing 0 (the appended zero row). */
 int fgr_max_pool(const float* x, int64_t ns, int32_t c, const int64_t* idx, int64_t nq,
