@@ -285,21 +285,39 @@ def main():
         return
 
     # ---- rooflines ---------------------------------------------------------------------
-    g_bytes_launch = float(np.mean(work['kpconv_gather'])) if work['kpconv_gather'] else 0.0
-    g_ms = timer.total_ms('kpconv_gather')
-    g_launches = len(timer.events['kpconv_gather'])
-    g_avg_s = g_ms / 1e3 / max(g_launches, 1)
-    g_achieved = g_bytes_launch / g_avg_s / 1e9 if g_avg_s > 0 else 0.0
-    traffic, traffic_src = _pmc_traffic('fgr_kpconv_gather', wl)
-    line['roofline'] = {
-        'kernel': 'fgr_kpconv_gather', 'bound': 'hbm', 'achieved': g_achieved,
-        'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': g_achieved / HBM_PEAK_GBS,
-        'traffic': traffic, 'traffic_source': traffic_src,
-        'algorithmic_bytes_per_launch': g_bytes_launch, 'avg_launch_us': g_avg_s * 1e6,
-        'launches_per_step': len(work['kpconv_gather']),
-        'share_of_step': g_ms / args.steps / step_ms,
-        'timing': 'HIP events recorded by libfgreg around each launch (fgr_time_next_call), eager '
-                  'replay of the timed steps'}
+    def kpconv_roofline(name, kernel):
+        b_launch = float(np.mean(work[name])) if work[name] else 0.0
+        ms = timer.total_ms(name)
+        avg_s = ms / 1e3 / max(len(timer.events[name]), 1)
+        ach = b_launch / avg_s / 1e9 if avg_s > 0 else 0.0
+        traffic, traffic_src = _pmc_traffic(kernel, wl)
+        return {
+            'kernel': kernel, 'bound': 'hbm', 'achieved': ach,
+            'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': ach / HBM_PEAK_GBS,
+            'traffic': traffic, 'traffic_source': traffic_src,
+            'algorithmic_bytes_per_launch': b_launch, 'avg_launch_us': avg_s * 1e6,
+            'launches_per_step': len(work[name]),
+            'share_of_step': ms / args.steps / step_ms,
+            'timing': 'HIP events recorded by libfgreg around each launch (fgr_time_next_call), '
+                      'eager replay of the timed steps'}
+
+    # the KPConv stage: the fused gather + GEMM kernel where it runs (D4 bytes with the wf
+    # write replaced by the 4 Cout output row), else the gather-weight kernel
+    fused = bool(work['kpconv_fused'])
+    if fused:
+        line['roofline'] = kpconv_roofline('kpconv_fused', 'fgr_kpconv_fused')
+        fl = float(sum(2.0 * m * n * k for (m, n, k) in rtimer.labels['kpconv_fused']))
+        ms_f = rtimer.total_ms('kpconv_fused')
+        pipe = PIPE.get(lin.MODE, 1)
+        mpk = F16_MFMA_PEAK_TFLOPS / pipe
+        ach_tf = fl / (ms_f / 1e3) / 1e12 if ms_f > 0 else 0.0
+        line['roofline']['mfma'] = {
+            'flops_per_step': fl / args.steps, 'achieved': ach_tf, 'peak': mpk,
+            'unit': 'TFLOP/s (fp32-equivalent)', 'frac': ach_tf / mpk,
+            'note': 'the weight contraction 2 Nq K Cin Cout of the same launches'}
+    if work['kpconv_gather']:
+        line['roofline' if not fused else 'roofline_kpconv_gather'] = kpconv_roofline(
+            'kpconv_gather', 'fgr_kpconv_gather')
 
     def mfma_family(name, mode, kernel):
         ms = rtimer.total_ms(name)

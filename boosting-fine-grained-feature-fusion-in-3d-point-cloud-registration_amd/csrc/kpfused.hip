@@ -7,22 +7,25 @@
 //
 // Structure (one 256-thread block = 64 queries x BN output channels; wave w owns queries
 // 16w .. 16w + 15):
-//   * the contraction index runs over (32-channel chunk cc, k32-step t, lane group g,
-//     element e) with kernel point k = g + 4 (e >> 1) and channel c = 32 cc + 2 t + (e & 1)
+//   * the block's neighbour table goes to LDS once (int32 ids, -1 for shadows; per query the
+//     last valid position and the normaliser count, from kpf_row_positive_kernel's per-row
+//     flags), so the gather never waits on an index load;
+//   * the contraction index runs over (16-channel chunk cc, k32-step t, lane group g,
+//     element e) with kernel point k = g + 4 (e >> 1) and channel c = 16 cc + 2 t + (e & 1)
 //     (kernel-point slot 15 is zero padding) -- the KPConv weight is stored once in THAT order
 //     as an f16x3 / bf16 MFMA image (fgr_kpconv_fused_weights);
 //   * so lane (g, c16) of a wave gathers, for ITS query c16 and ITS four kernel points
-//     g, g + 4, g + 8, g + 12, all 32 channels of the chunk: 4 influences per neighbour (no
-//     influence is computed twice inside a chunk), one 128-B read of the neighbour's row chunk,
-//     128 FMAs. When the chunk is done, the lane's registers ARE the MFMA B fragments of the
-//     chunk's 16 k32-steps (B[k = 8g + e][j = c16]) -- no LDS pass, no HBM round trip;
+//     g, g + 4, g + 8, g + 12, the 16 channels of the chunk: 4 influences per neighbour (none
+//     computed twice inside a chunk); each lane loads only its 16-B quarter of the neighbour's
+//     64-B row chunk and the other quarters arrive from the column's sibling lanes by
+//     permlane16 / permlane32 swaps; neighbours go in batches of 4 with the next batch's loads
+//     in flight. When the chunk is done the lane's 64 registers ARE the MFMA B fragments of
+//     the chunk's 8 k32-steps (B[k = 8g + e][j = c16]) -- no LDS pass, no HBM round trip;
 //   * W fragments (the MFMA A operand) travel global -> LDS by LDS-DMA through an S-stage ring
 //     shared by the 4 waves; the stages of the next chunk are in flight while it is gathered;
 //   * f16x3: the query's row scale is set / lowered per chunk from the chunk's exact max over
 //     the query's 4 lanes (the g5 policy, gemm5.hip), then each step's 8 values are split by
-//     v_fma_mix (split8_f16); bf16: rounded once;
-//   * the normaliser counts valid neighbours whose source row has a positive sum, from the
-//     per-row flags of kpf_row_positive_kernel (one pass over x per call).
+//     v_fma_mix (split8_f16); bf16: rounded once.
 // Lane maps of v_mfma_f32_16x16x32_{f16,bf16} (lane l, g = l >> 4, c = l & 15): A[i = c][k =
 // 8g + e], B[k = 8g + e][j = c], C[i = 4g + r][j = c].
 #include "common.h"
@@ -38,7 +41,7 @@ typedef __attribute__((address_space(3))) void lds_void;
 constexpr int kKpMax = 15;          // kernel points of the fused path (slot 15 = padding)
 constexpr int SH_UNSET = 0x3fff;
 
-// k32-steps of the fused contraction (16 kernel-point slots x cin entries)
+// k32-steps of the fused contraction (16 kernel-point slots x cin channels / 32)
 __host__ __device__ inline int kf_ksteps(int cin) { return cin / 2; }
 size_t kf_image_bytes(int cout, int cin, int terms) {
     return (size_t)((cout + 15) / 16) * kf_ksteps(cin) * terms * 64 * 16;
@@ -74,12 +77,12 @@ __global__ void kf_split_weights_kernel(const float* __restrict__ w, int nk, int
     const int s = (int)(ps % ksteps);
     const int panel = (int)(ps / ksteps);
     const int n = panel * 16 + i;
-    const int cc = s / 16, t = s % 16;
+    const int cc = s / 8, t = s % 8;
     const float sc = (terms == 2 && n < cout) ? 1.f / wsc[n] : 1.f;   // exact: a power of two
     float v[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-        const int k = g + 4 * (e >> 1), c = 32 * cc + 2 * t + (e & 1);
+        const int k = g + 4 * (e >> 1), c = 16 * cc + 2 * t + (e & 1);
         v[e] = (n < cout && k < nk) ? w[((int64_t)k * cin + c) * cout + n] * sc : 0.f;
     }
     if (terms == 2) {
@@ -130,7 +133,7 @@ __device__ __forceinline__ float kf_xg_max(float v) {  // max over lanes c, c^16
 
 struct KFArgs {
     const float* q; const float* s; int64_t nq, ns;
-    const int64_t* idx; int width;
+    const int64_t* idx; int width, wpad;
     const float* x; int cin;
     const unsigned char* pos;
     const float* kp; int n_kp; float inv_ext;
@@ -138,15 +141,44 @@ struct KFArgs {
     float* out; int64_t ldo; float* nnorm; int N;
 };
 
-template <int BN, int TERMS, int S>
-__global__ void __launch_bounds__(256, 2) kpconv_fused_kernel(KFArgs p) {
+// lane (g, c) holds piece v of row g of its 16-lane column c; returns all four rows' pieces
+// (r[j] = piece of row j) by one permlane16 and two permlane32 swaps (no LDS)
+__device__ __forceinline__ void kf_col_gather(float v, float (&r)[4]) {
+    auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    // a[0] = row (g & ~1), a[1] = row (g | 1)
+    auto e = __builtin_amdgcn_permlane32_swap(a[0], a[0], false, false);    // rows 0, 2
+    auto o = __builtin_amdgcn_permlane32_swap(a[1], a[1], false, false);    // rows 1, 3
+    r[0] = __uint_as_float(e[0]); r[2] = __uint_as_float(e[1]);
+    r[1] = __uint_as_float(o[0]); r[3] = __uint_as_float(o[1]);
+}
+
+// s_waitcnt vmcnt(ahead * P): the W stages issued after the one about to be read may stay
+// in flight
+template <int P, int S>
+__device__ __forceinline__ void kf_wait_ahead(int ahead) {
+    switch (S >= 8 ? ahead : min(ahead, S - 2)) {
+        case 0: kf_wait_vm<0>(); break;
+        case 1: kf_wait_vm<P>(); break;
+        case 2: kf_wait_vm<(S >= 4 ? 2 : 1) * P>(); break;
+        case 3: kf_wait_vm<(S >= 5 ? 3 : 1) * P>(); break;
+        case 4: kf_wait_vm<(S >= 6 ? 4 : 1) * P>(); break;
+        case 5: kf_wait_vm<(S >= 7 ? 5 : 1) * P>(); break;
+        default: kf_wait_vm<(S >= 8 ? 6 : 1) * P>(); break;
+    }
+}
+
+template <int BN, int TERMS, int S, int NB, int OCC>
+__global__ void __launch_bounds__(256, OCC) kpconv_fused_kernel(KFArgs p) {
     constexpr int TN = BN / 16;                // W panels per block (every wave: all of them)
     constexpr int W_PANEL = TERMS * 64;        // 16-B units of one (panel, k32-step)
     constexpr int ST = TN * W_PANEL;           // units per stage (one k32-step)
     constexpr int NP = ST / 64;                // DMA wave-instructions per stage
     static_assert(NP % 4 == 0, "stage pieces per wave");
     constexpr int P = NP / 4;
+    static_assert(S * P <= 63 && S <= 8, "vmcnt range");
     __shared__ u32x4 lds[S * ST];
+    __shared__ int hlast[64], npos[64];
+    extern __shared__ int ids[];               // [64 queries][wpad]: neighbour id or -1
 
     const int nbm = (int)((p.nq + 63) / 64), nbn = (p.N + BN - 1) / BN;
     const int nwg = nbm * nbn;
@@ -158,6 +190,7 @@ __global__ void __launch_bounds__(256, 2) kpconv_fused_kernel(KFArgs p) {
     }
     const int bm = tb / nbn, bn = tb % nbn;
     const int n0 = bn * BN;
+    const int64_t m0 = (int64_t)bm * 64;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int g = lane >> 4, c = lane & 15;
@@ -187,8 +220,32 @@ __global__ void __launch_bounds__(256, 2) kpconv_fused_kernel(KFArgs p) {
     for (int st = 0; st < S - 1; ++st)
         if (st < nk) issue(st);
 
+    // ---- the block's neighbour table -> LDS (int32, -1 = shadow / past the row), the last
+    // valid position and the normaliser count per query (every row read once per block)
+    if (tid < 64) { hlast[tid] = 0; npos[tid] = 0; }
+    __syncthreads();
+    {
+        const int64_t nrow = min((int64_t)64, p.nq - m0);
+        const int64_t tot = 64 * (int64_t)p.wpad;
+        for (int64_t e = tid; e < tot; e += 256) {
+            const int qq = (int)(e / p.wpad), h = (int)(e % p.wpad);
+            int id = -1;
+            if (qq < nrow && h < p.width) {
+                const int64_t v = p.idx[(m0 + qq) * p.width + h];
+                if (v >= 0 && v < p.ns) id = (int)v;
+            }
+            ids[e] = id;
+            if (id >= 0) {
+                atomicMax(&hlast[qq], h + 1);
+                if (p.pos[id]) atomicAdd(&npos[qq], 1);
+            }
+        }
+    }
+    __syncthreads();
+
     // ---- this lane's query and kernel points
-    const int64_t qi = (int64_t)bm * 64 + wv * 16 + c;
+    const int ql = wv * 16 + c;
+    const int64_t qi = m0 + ql;
     const bool qok = qi < p.nq;
     const int64_t qs = qok ? qi : 0;
     const float qx = p.q[3 * qs], qy = p.q[3 * qs + 1], qz = p.q[3 * qs + 2];
@@ -201,50 +258,79 @@ __global__ void __launch_bounds__(256, 2) kpconv_fused_kernel(KFArgs p) {
         const int kk = kv[j] ? k : 0;
         kx[j] = p.kp[3 * kk]; ky[j] = p.kp[3 * kk + 1]; kz[j] = p.kp[3 * kk + 2];
     }
-    const int64_t* row = p.idx + qs * p.width;
+    // neighbour positions to scan: the wave's largest last-valid position, in whole batches
+    const int hmax = (int)row16_max((float)hlast[ql]);
+    const int nbatch = (hmax + NB - 1) / NB;
+    const int* myids = ids + ql * p.wpad;
 
     f32x4 acc[TN];
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
     int sh = SH_UNSET;
     float scv = 1.f;
-    int n_pos = 0;
 
-    const int nchunks = p.cin / 32;
+    // one batch of NB neighbours: ids (one 16-B LDS read), this lane's 16-B quarter of each
+    // row chunk (16 channels), the neighbour positions
+    struct Batch { int id[NB]; float4 xq[NB]; float sx[NB], sy[NB], sz[NB]; };
+    auto load_batch = [&](int b, int cc, Batch& B) {
+#pragma unroll
+        for (int u = 0; u < NB; ++u) B.id[u] = myids[b * NB + u];
+#pragma unroll
+        for (int u = 0; u < NB; ++u) {
+            const int64_t sid = B.id[u] >= 0 ? B.id[u] : 0;
+            B.xq[u] = *reinterpret_cast<const float4*>(p.x + sid * p.cin + 16 * cc + 4 * g);
+            B.sx[u] = p.s[3 * sid]; B.sy[u] = p.s[3 * sid + 1]; B.sz[u] = p.s[3 * sid + 2];
+        }
+    };
+
+    const int nchunks = p.cin / 16;
     for (int cc = 0; cc < nchunks; ++cc) {
-        // ---- gather: ga[j][ch] = wf[q, g + 4 j, 32 cc + ch]
-        float ga[4][32];
+        // ---- gather: ga[j][ch] = wf[q, g + 4 j, 16 cc + ch]
+        float ga[4][16];
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
-            for (int e = 0; e < 32; ++e) ga[j][e] = 0.f;
-        for (int h = 0; h < p.width; ++h) {
-            const int64_t id = qok ? row[h] : -1;
-            const bool valid = id >= 0 && id < p.ns;
-            if (!__builtin_amdgcn_ballot_w64(valid)) continue;       // wave-uniform skip
-            const int64_t sid = valid ? id : 0;                      // invalid: weight 0
-            if (cc == 0 && valid && p.pos[sid]) ++n_pos;
-            const float nx = p.s[3 * sid] - qx, ny = p.s[3 * sid + 1] - qy,
-                        nz = p.s[3 * sid + 2] - qz;
-            float w[4];
+            for (int e = 0; e < 16; ++e) ga[j][e] = 0.f;
+        Batch cur, nxt;
+        if (nbatch > 0) load_batch(0, cc, cur);
+        for (int b = 0; b < nbatch; ++b) {
+            if (b + 1 < nbatch) load_batch(b + 1, cc, nxt);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                // neighbours are centred first, then compared with the kernel points (:302, :313)
-                const float dx = nx - kx[j], dy = ny - ky[j], dz = nz - kz[j];
-                const float d2 = dx * dx + dy * dy + dz * dz;
-                w[j] = (valid && kv[j]) ? fmaxf(1.0f - sqrtf(d2) * p.inv_ext, 0.0f) : 0.f;
+            for (int u = 0; u < NB; ++u) {
+                const bool valid = cur.id[u] >= 0;
+                const float nx = cur.sx[u] - qx, ny = cur.sy[u] - qy, nz = cur.sz[u] - qz;
+                float w[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    // neighbours are centred first, then compared with the kernel points
+                    // (:302, :313)
+                    const float dx = nx - kx[j], dy = ny - ky[j], dz = nz - kz[j];
+                    const float d2 = dx * dx + dy * dy + dz * dz;
+                    w[j] = (valid && kv[j]) ? fmaxf(1.0f - sqrtf(d2) * p.inv_ext, 0.0f) : 0.f;
+                }
+                // the row's 16 channels: quarter r of the chunk comes from row r of the column
+                float xv[16];
+                {
+                    float t[4];
+                    kf_col_gather(cur.xq[u].x, t);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) xv[4 * r] = t[r];
+                    kf_col_gather(cur.xq[u].y, t);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) xv[4 * r + 1] = t[r];
+                    kf_col_gather(cur.xq[u].z, t);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) xv[4 * r + 2] = t[r];
+                    kf_col_gather(cur.xq[u].w, t);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) xv[4 * r + 3] = t[r];
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) ga[j][e] = fmaf(w[j], xv[e], ga[j][e]);
             }
-            const float4* xr = reinterpret_cast<const float4*>(p.x + sid * p.cin + 32 * cc);
-            float xv[32];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const float4 v = xr[e];
-                xv[4 * e] = v.x; xv[4 * e + 1] = v.y; xv[4 * e + 2] = v.z; xv[4 * e + 3] = v.w;
-            }
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-#pragma unroll
-                for (int e = 0; e < 32; ++e) ga[j][e] = fmaf(w[j], xv[e], ga[j][e]);
+            if (b + 1 < nbatch) cur = nxt;
         }
         // ---- f16x3 row scale: set by the first non-zero chunk (max into [2^7, 2^8)), lowered
         // with the partial sums rescaled when a chunk would pass 2^15
@@ -253,7 +339,7 @@ __global__ void __launch_bounds__(256, 2) kpconv_fused_kernel(KFArgs p) {
 #pragma unroll
             for (int j = 0; j < 4; ++j)
 #pragma unroll
-                for (int e = 0; e < 32; ++e) cm = fmaxf(cm, fabsf(ga[j][e]));
+                for (int e = 0; e < 16; ++e) cm = fmaxf(cm, fabsf(ga[j][e]));
             cm = kf_xg_max(cm);
             const bool lower = cm > 0.f && (sh == SH_UNSET ||
                                             __builtin_amdgcn_frexp_expf(cm) + sh > 15);
@@ -266,19 +352,11 @@ __global__ void __launch_bounds__(256, 2) kpconv_fused_kernel(KFArgs p) {
                 scv = __builtin_ldexpf(1.f, sh);
             }
         }
-        // ---- the chunk's 16 k32-steps: B fragments from ga, W fragments from the ring
+        // ---- the chunk's 8 k32-steps: B fragments from ga, W fragments from the ring
 #pragma unroll
-        for (int t = 0; t < 16; ++t) {
-            const int st = cc * 16 + t;
-            const int ahead = min(S - 2, nk - 1 - st);
-            if constexpr (S >= 4) {
-                if (ahead >= 2) kf_wait_vm<2 * P>();
-                else if (ahead == 1) kf_wait_vm<P>();
-                else kf_wait_vm<0>();
-            } else {
-                if (ahead >= 1) kf_wait_vm<P>();
-                else kf_wait_vm<0>();
-            }
+        for (int t = 0; t < 8; ++t) {
+            const int st = cc * 8 + t;
+            kf_wait_ahead<P, S>(min(S - 2, nk - 1 - st));
             __builtin_amdgcn_s_barrier();
             if (st + S - 1 < nk) issue(st + S - 1);
             const u32x4* sb = lds + (st % S) * ST;
@@ -329,15 +407,15 @@ __global__ void __launch_bounds__(256, 2) kpconv_fused_kernel(KFArgs p) {
                     if (n + e < p.N) orow[n + e] = y[e];
             }
         }
-        if (bn == 0 && g == 0) p.nnorm[qi] = (float)(n_pos > 1 ? n_pos : 1);
+        if (bn == 0 && g == 0) p.nnorm[qi] = (float)(npos[ql] > 1 ? npos[ql] : 1);
     }
 }
 
-template <int BN, int TERMS, int S>
+template <int BN, int TERMS, int S, int NB, int OCC>
 void launch_kf(const KFArgs& a, hipStream_t st) {
     const int nbm = (int)((a.nq + 63) / 64), nbn = (a.N + BN - 1) / BN;
-    hipLaunchKernelGGL((kpconv_fused_kernel<BN, TERMS, S>), dim3((unsigned)(nbm * nbn)), dim3(256),
-                       0, st, a);
+    hipLaunchKernelGGL((kpconv_fused_kernel<BN, TERMS, S, NB, OCC>), dim3((unsigned)(nbm * nbn)), dim3(256),
+                       (size_t)64 * a.wpad * sizeof(int), st, a);
 }
 
 }  // namespace
@@ -347,7 +425,7 @@ using namespace fgr;
 
 extern "C" int fgr_kpconv_fused_weights_bytes(int32_t n_kp, int32_t cin, int32_t cout,
                                               int32_t mode, size_t* bytes) {
-    FGR_REQUIRE(bytes && n_kp > 0 && n_kp <= kKpMax && cin > 0 && cin % 32 == 0 && cout > 0 &&
+    FGR_REQUIRE(bytes && n_kp > 0 && n_kp <= kKpMax && cin > 0 && cin % 16 == 0 && cout > 0 &&
                     (mode == FGR_KPF_F16X3 || mode == FGR_KPF_BF16),
                 "fgr_kpconv_fused_weights_bytes: bad arguments (n_kp %d cin %d cout %d mode %d)",
                 n_kp, cin, cout, mode);
@@ -387,7 +465,7 @@ extern "C" int fgr_kpconv_fused(const float* q, const float* s, int64_t nq, int6
                                 const float* kp, int32_t n_kp, float extent, const void* w_img,
                                 int32_t cout, int32_t mode, float* out, int64_t ldo, float* nnorm,
                                 void* workspace, size_t ws_bytes, void* stream) {
-    FGR_REQUIRE(nq >= 0 && ns >= 0 && width >= 0 && cin > 0 && cin % 32 == 0 && n_kp > 0 &&
+    FGR_REQUIRE(nq >= 0 && ns >= 0 && width >= 0 && cin > 0 && cin % 16 == 0 && n_kp > 0 &&
                     n_kp <= kKpMax && extent > 0.f && cout > 0 && ldo >= cout &&
                     (mode == FGR_KPF_F16X3 || mode == FGR_KPF_BF16),
                 "fgr_kpconv_fused: bad arguments (cin %d n_kp %d cout %d mode %d)", cin, n_kp,
@@ -412,17 +490,29 @@ extern "C" int fgr_kpconv_fused(const float* q, const float* s, int64_t nq, int6
     const int terms = mode == FGR_KPF_F16X3 ? 2 : 1;
     const float* wsc = reinterpret_cast<const float*>(static_cast<const char*>(w_img) +
                                                       kf_image_bytes(cout, cin, terms));
-    KFArgs a{q, s, nq, ns, idx, width, x, cin, pos, kp, n_kp, 1.0f / extent,
+    const int wpad = (width + 3) / 4 * 4;
+    KFArgs a{q, s, nq, ns, idx, width, wpad, x, cin, pos, kp, n_kp, 1.0f / extent,
              static_cast<const u32x4*>(w_img), kf_ksteps(cin), wsc, out, ldo, nnorm, cout};
-    // N tile: 128 output channels (64 for narrow outputs); FGR_KPF_TILE = '6' / '1' forces 64 / 128
+    // variants (FGR_KPF_TILE): '1' 128 columns, 3 W stages, 2-neighbour batches, 2 blocks per
+    // CU; '2' 128 / 8 stages / 4 / 1; '3' 64 / 8 / 4 / 1; '4' 128 / 6 / 8 / 1; '6' 64 / 4 / 2 / 2
     const char* force = getenv("FGR_KPF_TILE");
-    const bool wide = force && force[0] ? force[0] == '1' : cout > 64;
+    const char v = force && force[0] ? force[0] : (cout > 64 ? '1' : '6');
     if (terms == 2) {
-        if (wide) launch_kf<128, 2, 3>(a, st);
-        else launch_kf<64, 2, 4>(a, st);
+        switch (v) {
+            case '2': launch_kf<128, 2, 8, 4, 1>(a, st); break;
+            case '3': launch_kf<64, 2, 8, 4, 1>(a, st); break;
+            case '4': launch_kf<128, 2, 6, 8, 1>(a, st); break;
+            case '6': launch_kf<64, 2, 4, 2, 2>(a, st); break;
+            default: launch_kf<128, 2, 3, 2, 2>(a, st); break;
+        }
     } else {
-        if (wide) launch_kf<128, 1, 4>(a, st);
-        else launch_kf<64, 1, 4>(a, st);
+        switch (v) {
+            case '2': launch_kf<128, 1, 8, 4, 1>(a, st); break;
+            case '3': launch_kf<64, 1, 8, 4, 1>(a, st); break;
+            case '4': launch_kf<128, 1, 8, 8, 1>(a, st); break;
+            case '6': launch_kf<64, 1, 4, 2, 2>(a, st); break;
+            default: launch_kf<128, 1, 4, 2, 2>(a, st); break;
+        }
     }
     FGR_CHECK_LAUNCH("kpconv_fused_kernel");
     return FGR_OK;

@@ -200,7 +200,7 @@ KPF = os.environ.get('FGREG_KPF', '0')
 
 
 def _kpf_mode(cin, n_kp):
-    if KPF != '1' or cin % 32 != 0 or n_kp > 15:
+    if KPF != '1' or cin % 16 != 0 or n_kp > 15:
         return None
     return {'f16x3': _lib.KPF_F16X3, 'bf16': _lib.KPF_BF16}.get(lin.MODE)
 
@@ -226,7 +226,7 @@ class KPConv(nn.Module):
         """-> (sum_k WF_k @ W_k (Nq, Cout), nnorm (Nq,)). The reference divides the first
         by the second (:395-399); callers fuse that division into the next kernel.
         Fused (fgr_kpconv_fused: gather + weight GEMM in one launch, wf never written) where
-        the channel width allows it (Cin % 32 == 0) in the f16x3 / bf16 modes; ``KPF``."""
+        the channel width allows it (Cin % 16 == 0) in the f16x3 / bf16 modes; ``KPF``."""
         mode = _kpf_mode(x.shape[1], self.K)
         if mode is not None:
             return ops.kpconv_fused(q_pts, s_pts, neighb_inds, x, self.kernel_points,

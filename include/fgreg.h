@@ -140,7 +140,7 @@ int fgr_kpconv_gather(const float* q, const float* s, int64_t nq, int64_t ns, co
  * FGR_KPF_BF16: wf rounded to bf16 where it enters the MFMA (the bf16 compute mode).
  * W (n_kp, cin, cout) fp32 contiguous -> image by fgr_kpconv_fused_weights (built once per
  * weight, fgr_kpconv_fused_weights_bytes() bytes, 16-B aligned; the contraction order of the
- * fused kernel). cin % 32 == 0, n_kp <= 15; x, w_img, out 16-B aligned.
+ * fused kernel). cin % 16 == 0, n_kp <= 15; x, w_img, out 16-B aligned.
  * workspace: fgr_kpconv_fused_workspace() bytes (per-source-row flags of the normaliser). */
 enum { FGR_KPF_F16X3 = 0, FGR_KPF_BF16 = 1 };
 int fgr_kpconv_fused_weights_bytes(int32_t n_kp, int32_t cin, int32_t cout, int32_t mode,

@@ -16,9 +16,11 @@ fi
 # PMC passes first (their summaries feed the bench lines' roofline.traffic): FETCH_SIZE and
 # WRITE_SIZE in separate runs, gather kernels only, per workload
 for wl in modelnet 3dmatch; do
-  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex 'kpconv_gather' --output-format csv -d gpurun_out/pmcf_${wl}_$tag -- python3 bench.py --profile --workload $wl --steps 3 --warmup 1 > gpurun_out/pmcf_${wl}_$tag.log 2>&1 || exit 1
-  timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex 'kpconv_gather' --output-format csv -d gpurun_out/pmcw_${wl}_$tag -- python3 bench.py --profile --workload $wl --steps 3 --warmup 1 > gpurun_out/pmcw_${wl}_$tag.log 2>&1 || exit 1
-  python3 tools/pmc_traffic.py fgr_kpconv_gather kpconv_gather $(ls gpurun_out/pmcf_${wl}_$tag/*/*counter_collection.csv) $(ls gpurun_out/pmcw_${wl}_$tag/*/*counter_collection.csv) > profiles/pmc_kpconv_$wl.json || exit 1
+  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex 'kpconv_gather|kpconv_fused_kernel' --output-format csv -d gpurun_out/pmcf_${wl}_$tag -- python3 bench.py --profile --workload $wl --steps 3 --warmup 1 > gpurun_out/pmcf_${wl}_$tag.log 2>&1 || exit 1
+  timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex 'kpconv_gather|kpconv_fused_kernel' --output-format csv -d gpurun_out/pmcw_${wl}_$tag -- python3 bench.py --profile --workload $wl --steps 3 --warmup 1 > gpurun_out/pmcw_${wl}_$tag.log 2>&1 || exit 1
+  # the KPConv stage's op: the fused kernel when it ran (FGREG_KPF), else the gather
+  if grep -q kpconv_fused gpurun_out/pmcf_${wl}_$tag/*/*counter_collection.csv; then op=fgr_kpconv_fused; rx=kpconv_fused_kernel; else op=fgr_kpconv_gather; rx=kpconv_gather; fi
+  python3 tools/pmc_traffic.py $op $rx $(ls gpurun_out/pmcf_${wl}_$tag/*/*counter_collection.csv) $(ls gpurun_out/pmcw_${wl}_$tag/*/*counter_collection.csv) > profiles/pmc_kpconv_$wl.json || exit 1
 done
 timeout -k 10 400 python bench.py --steps 50 --warmup 10 --gemm-table gpurun_out/gemm_$tag.json > gpurun_out/bench_$tag.json 2> gpurun_out/bench_$tag.err || exit 1
 timeout -k 10 400 python bench.py --workload 3dmatch --steps 50 --warmup 10 --gemm-table gpurun_out/gemm3d_$tag.json > gpurun_out/bench3d_$tag.json 2> gpurun_out/bench3d_$tag.err || exit 1

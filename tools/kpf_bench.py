@@ -2,7 +2,7 @@
 forward of the bench workload (real neighbour tables and feature widths), then times
 fgr_kpconv_fused against the unfused gather + weight GEMM on each call (device time from
 HIP-graph replays) and prints the error of each against the other.
-usage: python tools/kpf_bench.py [modelnet|3dmatch|3dlomatch]"""
+usage: python tools/kpf_bench.py [modelnet|3dmatch|3dlomatch] [variants, e.g. 1236]"""
 import os
 import sys
 
@@ -41,7 +41,9 @@ def main():
         model({'src_xyz': [torch.from_numpy(a).to(dev) for a in src],
                'tgt_xyz': [torch.from_numpy(a).to(dev) for a in tgt]})
     backbone.KPConv.forward_unnormalized = orig
-    tot_f = tot_u = 0.0
+    tot_u = 0.0
+    tot_f = {}
+    variants = sys.argv[2] if len(sys.argv) > 2 else '1'
     with torch.no_grad():
         for conv, q, s, idx, x in calls:
             cin, cout = x.shape[1], conv.out_channels
@@ -57,17 +59,23 @@ def main():
                 return ops.kpconv_fused(q, s, idx, x, conv.kernel_points, conv.KP_extent,
                                         conv.weights, mode)
             a, na = unfused()
-            b, nb = fused()
-            err = float((a - b).abs().max() / a.abs().max().clamp_min(1e-30))
-            tu, tf = timeit(unfused), timeit(fused)
+            tu = timeit(unfused)
             tot_u += tu
-            tot_f += tf
             v = float((idx < s.shape[0]).float().sum(1).mean())
+            msg = []
+            for var in variants:
+                os.environ['FGR_KPF_TILE'] = var
+                b, nb = fused()
+                err = float((a - b).abs().max() / a.abs().max().clamp_min(1e-30))
+                tf = timeit(fused)
+                tot_f[var] = tot_f.get(var, 0.0) + tf
+                msg.append(f'{var}: {tf:6.1f} ({tf / tu:.2f}x, {err:.0e}'
+                           f'{"" if torch.equal(na, nb) else " NNORM DIFF"})')
             print(f'nq {q.shape[0]:6d} ns {s.shape[0]:6d} H {idx.shape[1]:3d} v {v:5.1f} '
-                  f'cin {cin:4d} cout {cout:4d}: unfused {tu:7.1f} us  fused {tf:7.1f} us  '
-                  f'({tf / tu:.2f}x)  diff {err:.1e}  nnorm equal {bool(torch.equal(na, nb))}',
+                  f'cin {cin:4d} cout {cout:4d}: unfused {tu:6.1f} us | ' + '  '.join(msg),
                   flush=True)
-    print(f'total: unfused {tot_u:.1f} us  fused {tot_f:.1f} us  ({tot_f / max(tot_u, 1e-9):.2f}x)')
+    print(f'total: unfused {tot_u:.1f} us | ' + '  '.join(
+        f'{k}: {t:.1f} ({t / max(tot_u, 1e-9):.2f}x)' for k, t in tot_f.items()))
 
 
 if __name__ == '__main__':
