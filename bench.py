@@ -126,6 +126,9 @@ def parse():
     p.add_argument('--cpu-seconds', type=float, default=10.0,
                    help='budget of the CPU baseline B=1 sample (0 disables it)')
     p.add_argument('--no-cpu-baseline', action='store_true')
+    p.add_argument('--no-pipeline', action='store_true',
+                   help='time back-to-back model(batch) calls instead of fgreg.pipeline (which '
+                        'preprocesses step i + 1 on a side stream while step i\'s core runs)')
     p.add_argument('--profile', action='store_true',
                    help='warmup + timed steps only (for rocprofv3 kernel-trace runs)')
     p.add_argument('--gemm-table', default=None,
@@ -197,19 +200,31 @@ def main():
     batch_tgt = [torch.from_numpy(t).to(dev) for t in tgt]
     from fgreg import dist as fdist
 
-    def step():
-        out = model({'src_xyz': batch_src, 'tgt_xyz': batch_tgt})
+    def finish(out):
         if dist is not None:   # the one exchange: per-pair poses of every rank (RCCL)
             out['pose_all'] = fdist.gather_pair_results(out['pose'], [P] * world, pair_dim=1)
         return out
+
+    def step():
+        return finish(model({'src_xyz': batch_src, 'tgt_xyz': batch_tgt}))
+
+    def run(n):
+        """n full forwards of the batch: pipelined (fgreg.pipeline: step i + 1's
+        preprocessing on a side stream during step i's core) unless --no-pipeline"""
+        if args.no_pipeline:
+            for _ in range(n):
+                step()
+            return
+        batches = ({'src_xyz': batch_src, 'tgt_xyz': batch_tgt} for _ in range(n))
+        for out in fgreg.pipeline(model, batches):
+            finish(out)
 
     def timed(n):
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(n):
-            step()
+        run(n)
         torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
@@ -219,8 +234,7 @@ def main():
     with torch.no_grad():
         # >= 2 warmup steps: the second sighting of the batch's shape signature captures the
         # HIP graph of the post-preprocessing forward (fgreg/regtr.py), replayed from then on
-        for _ in range(max(args.warmup, 2)):
-            step()
+        run(max(args.warmup, 2))
         if args.profile:
             # marker kernels around the timed region: tools/kernel_stats.py sums only the
             # dispatches between them (torch's spin kernel, ~1 us)
@@ -274,7 +288,10 @@ def main():
                    'parallelism': f'pair-sharded dp{world}',
                    'precision': fgreg.precision(),
                    'hip_graph': ('post-preprocessing forward replayed from the shape-keyed graph '
-                                 'cache; preprocessing eager' if fregtr.GRAPHS else 'off')},
+                                 'cache; preprocessing eager' if fregtr.GRAPHS else 'off'),
+                   'pipeline': ('off: back-to-back model(batch) calls' if args.no_pipeline else
+                                'fgreg.pipeline: every step is a full forward; step i + 1\'s '
+                                'preprocessing runs on a side stream while step i\'s core runs')},
     }
     if args.profile:
         line['profile'] = 'warmup + timed steps only (rocprofv3 companion run)'

@@ -8,6 +8,7 @@ from ._lib import FgrError, build, load  # noqa: F401
 from .backbone import FixedMetaPreprocessor, KPFEncoder, PreprocessorHIP  # noqa: F401
 from .pose import compute_rigid_transform, fast_compute_rigid_transform  # noqa: F401
 from .regtr import RegTR  # noqa: F401
+from .pipeline import pipeline  # noqa: F401
 
 PRECISIONS = ('fp32', 'bf16')
 

@@ -145,14 +145,23 @@ class RegTR(nn.Module):
         with torch.no_grad(), torch.cuda.device(dev):
             return self._forward(batch)
 
-    def _forward(self, batch):
-        B = len(batch['src_xyz'])
+    def _prepare(self, batch):
+        """The preprocessing (kpconv_meta, with every level's host lengths and device
+        offsets): the eager part of the forward, with its host syncs."""
         meta = self.preprocessor(list(batch['src_xyz']) + list(batch['tgt_xyz']))
+        for lvl in range(len(meta['points'])):       # device offsets of every level, eagerly
+            host_layout(meta, lvl)
+        return meta
+
+    def _forward(self, batch, meta=None):
+        """meta: a kpconv_meta already prepared for this batch (fgreg.pipeline), else built
+        here."""
+        B = len(batch['src_xyz'])
+        if meta is None:
+            meta = self._prepare(batch)
         batch['kpconv_meta'] = meta
         n_lvl = len(meta['points'])
         slens_c, _ = host_layout(meta, n_lvl - 1)
-        for lvl in range(n_lvl):                     # device offsets of every level, eagerly
-            host_layout(meta, lvl)
         xyz_c = meta['points'][-1]
         core = None
         if GRAPHS and xyz_c.is_cuda and ops.TIMER is None:
