@@ -411,7 +411,38 @@ int64_t n_tiles_bf(int64_t n_kv_rows, int32_t n_kv_seg) { return n_kv_rows / 64 
 }  // namespace
 bool gemm_g5_bf16(char cfg, const float* A, int64_t lda, const void* W, int ksteps, float* C,
                   int64_t ldc, const float* bias, const float* R, int64_t ldr, int M, int N, int K,
-                  int act, int vec_out, hipStream_t st);
+                  int act, int vec_out, hipStream_t st, int ksplit, float* part);
+bool g5_tile(char cfg, int* bm, int* bn);
+int g5_ksplit(int M, int N, int K, int BM, int BN);
+inline bool splitk_shape(int m, int n, int k) {        // as gemm16.hip
+    return k >= 1920 && n <= 256 && (int64_t)((m + 63) / 64) * ((n + 63) / 64) <= 160;
+}
+
+// narrow outputs with long contractions: the 64 x 64 LDS-DMA g5 ('X', gemm5.hip; measured
+// 1.2-1.5x faster there); few tiles (<= 400 of 64 x 64) with K >= 512 and the short-M
+// K >= 2048 layers: the two-k-group g5 ('S', 'T', 'W'); otherwise the register-staged
+// kernel below ('z'; FGR_GEMM_BF16_TILE A..Z forces a g5 variant, anything else it)
+char bf16_tile(int m, int n, int k) {
+    const char* force = getenv("FGR_GEMM_BF16_TILE");
+    if (force && force[0]) return force[0];
+    const int64_t tiles64 = (int64_t)ceil_div(m, 64) * ceil_div(n, 64);
+    if (k % 8 == 0 && splitk_shape(m, n, k)) return k >= 2048 ? 'X' : 'S';   // split-K
+    if (tiles64 <= 400 && k >= 512 && n >= 32)
+        return (k >= 2048 || n <= 64) ? 'S' : ((n <= 128 && k >= 1024 && tiles64 > 256) ? 'T' : 'W');
+    if (m <= 4096 && k >= 2048) return 'W';
+    return n <= 256 && k >= 1000 ? 'X' : 'z';
+}
+
+int bf16_ksplit(char cfg, int m, int n, int k) {
+    int bm, bn;
+    if (k % 8 != 0 || !g5_tile(cfg, &bm, &bn)) return 1;
+    const char* on = getenv("FGR_GEMM_SPLITK");
+    const char* f = getenv("FGR_GEMM_KSPLIT");
+    if (f && f[0]) return g5_ksplit(m, n, k, bm, bn);
+    if (on && on[0] == '0') return 1;
+    if (on && on[0] == '1') return g5_ksplit(m, n, k, bm, bn);
+    return splitk_shape(m, n, k) ? (k >= 2048 ? 4 : 2) : 1;
+}
 }  // namespace fgr
 
 using namespace fgr;
@@ -433,9 +464,9 @@ extern "C" int fgr_split_weights_bf16(const float* w, int32_t n, int32_t k, int6
     return FGR_OK;
 }
 
-extern "C" int fgr_gemm_bf16(const float* a, int64_t lda, const void* w_img, float* c, int64_t ldc,
-                             const float* bias, const float* r, int64_t ldr, int32_t m, int32_t n,
-                             int32_t k, int32_t act, void* stream) {
+static int gemm_bf16_impl(const float* a, int64_t lda, const void* w_img, float* c, int64_t ldc,
+                          const float* bias, const float* r, int64_t ldr, int32_t m, int32_t n,
+                          int32_t k, int32_t act, void* ws, size_t ws_bytes, void* stream) {
     FGR_REQUIRE(a && w_img && c && m >= 0 && n > 0 && k > 0 && lda >= k && ldc >= n &&
                     (!r || ldr >= n),
                 "fgr_gemm_bf16: bad arguments (m %d n %d k %d)", m, n, k);
@@ -450,24 +481,14 @@ extern "C" int fgr_gemm_bf16(const float* a, int64_t lda, const void* w_img, flo
                  vo ? 1 : 0};
     hipStream_t st = as_stream(stream);
     TimedCall timed_(st);
-    // narrow outputs with long contractions: the 64 x 64 LDS-DMA g5 ('I', gemm5.hip; measured
-    // 1.2-1.5x faster there); few tiles (<= 400 of 64 x 64) with K >= 512 and the short-M
-    // K >= 2048 layers: the two-k-group g5 ('S', 'T', 'W'); otherwise the register-staged
-    // kernel below (FGR_GEMM_BF16_TILE A..W forces a g5 variant, anything else this kernel)
-    const char* force = getenv("FGR_GEMM_BF16_TILE");
-    const int64_t tiles64 = (int64_t)ceil_div(m, 64) * ceil_div(n, 64);
-    char cfg;
-    if (force && force[0])
-        cfg = force[0];
-    else if (tiles64 <= 400 && k >= 512 && n >= 32)
-        cfg = (k >= 2048 || n <= 64) ? 'S' : ((n <= 128 && k >= 1024 && tiles64 > 256) ? 'T' : 'W');
-    else if (m <= 4096 && k >= 2048)
-        cfg = 'W';
-    else
-        cfg = n <= 256 && k >= 1000 ? 'X' : 'z';
+    const char cfg = bf16_tile(m, n, k);
     if (((cfg >= 'A' && cfg <= 'Z') || (cfg >= '0' && cfg <= '9')) && k % 8 == 0) {
+        int ks = bf16_ksplit(cfg, m, n, k);
+        if (ks > 1 && (!ws || ws_bytes < (size_t)ks * m * n * sizeof(float) ||
+                       (reinterpret_cast<uintptr_t>(ws) & 15) != 0))
+            ks = 1;                                     // no room for the parts: no split
         FGR_REQUIRE(gemm_g5_bf16(cfg, a, lda, w_img, ksteps_bf(k), c, ldc, bias, r, ldr, m, n, k, act,
-                     vo ? 1 : 0, st),
+                     vo ? 1 : 0, st, ks, static_cast<float*>(ws)),
                     "fgr_gemm_bf16: g5 variant %c unavailable", cfg);
         FGR_CHECK_LAUNCH("gemm_g5 (bf16)");
         return FGR_OK;
@@ -483,6 +504,19 @@ extern "C" int fgr_gemm_bf16(const float* a, int64_t lda, const void* w_img, flo
     }
     FGR_CHECK_LAUNCH("gemm_bf16_kernel");
     return FGR_OK;
+}
+
+extern "C" int fgr_gemm_bf16(const float* a, int64_t lda, const void* w_img, float* c, int64_t ldc,
+                             const float* bias, const float* r, int64_t ldr, int32_t m, int32_t n,
+                             int32_t k, int32_t act, void* stream) {
+    return gemm_bf16_impl(a, lda, w_img, c, ldc, bias, r, ldr, m, n, k, act, nullptr, 0, stream);
+}
+
+extern "C" int fgr_gemm_bf16_ws(const float* a, int64_t lda, const void* w_img, float* c,
+                                int64_t ldc, const float* bias, const float* r, int64_t ldr,
+                                int32_t m, int32_t n, int32_t k, int32_t act, void* ws,
+                                size_t ws_bytes, void* stream) {
+    return gemm_bf16_impl(a, lda, w_img, c, ldc, bias, r, ldr, m, n, k, act, ws, ws_bytes, stream);
 }
 
 extern "C" int fgr_attention_bf16_workspace(int64_t n_kv_rows, int32_t n_kv_seg, int32_t n_head,

@@ -34,7 +34,16 @@
 namespace fgr {
 bool gemm_g5_f16x3(char cfg, const float* A, int64_t lda, const void* W, int ksteps,
                    const float* wsc, float* C, int64_t ldc, const float* bias, const float* R,
-                   int64_t ldr, int M, int N, int K, int act, int vec_out, hipStream_t st);
+                   int64_t ldr, int M, int N, int K, int act, int vec_out, hipStream_t st,
+                   int ksplit, float* part);
+bool g5_tile(char cfg, int* bm, int* bn);
+int g5_ksplit(int M, int N, int K, int BM, int BN);
+char bf16_tile(int m, int n, int k);
+int bf16_ksplit(char cfg, int m, int n, int k);
+// few 64 x 64 tiles, narrow output, long contraction: split-K pays (measured)
+inline bool splitk_shape(int m, int n, int k) {
+    return k >= 1920 && n <= 256 && (int64_t)((m + 63) / 64) * ((n + 63) / 64) <= 160;
+}
 namespace {
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
@@ -1191,9 +1200,66 @@ extern "C" int fgr_split_weights_h3(const float* w, int32_t n, int32_t k, int64_
     return FGR_OK;
 }
 
-extern "C" int fgr_gemm_f16x3(const float* a, int64_t lda, const void* w_img, float* c,
-                              int64_t ldc, const float* bias, const float* r, int64_t ldr,
-                              int32_t m, int32_t n, int32_t k, int32_t act, void* stream) {
+namespace fgr {
+// The tile variant the f16x3 dispatcher picks for a shape (FGR_GEMM16_TILE overrides it).
+// Default per shape (measured on the forward's GEMMs with tools/gemm_tiles.py, device
+// time from HIP-graph replays; profiles/r02_gemm_tiles*.txt): wide outputs take 64 x 128
+// tiles (v4 -- W fragments straight to registers -- for K >= 1024, double-buffered v2
+// for K >= 512), very tall ones 64 x 128; narrow outputs (N <= 256) and short row counts
+// (M <= 4096, N <= 512) the 64 x 64 LDS-DMA g5 ('I') when K % 8 == 0, else the 64 x 64 v4.
+// X / Y are I / B and y is b with the row-major staged epilogue (3-8 % faster;
+// profiles/r02_gemm_tiles_epi.txt, r02_gemm_tiles_by.txt).
+// Few tiles (<= 400 of 64 x 64, e.g. the 3DMatch transformer's 2 x 1060 tokens) with
+// K >= 512: the two-k-group g5 ('W', 'T'; 8 waves per block) -- 1.1-1.45x there
+// (profiles/r02_gemm_tiles_splitk*.txt).
+char h3_tile(int m, int n, int k) {
+    const char* force = getenv("FGR_GEMM16_TILE");
+    if (force && force[0]) return force[0];
+    const bool g5ok = k % 8 == 0;
+    const int64_t tiles64 = (int64_t)ceil_div(m, 64) * ceil_div(n, 64);
+    // very few tiles with a long K (3DMatch's 2120 x 256 x 3840, 2120 x 128 x 1920 KPConv
+    // products): split-K over 64 x 64 tiles (h3_ksplit; profiles/r02_gemm_splitk_sweep.txt)
+    if (g5ok && splitk_shape(m, n, k)) return k >= 2048 ? 'X' : 'W';
+    if (g5ok && tiles64 <= 400 && k >= 512 && n >= 32)
+        return (k >= 2048 || n <= 64) ? 'S' : ((n <= 128 && k >= 1024 && tiles64 > 256) ? 'T' : 'W');
+    if (g5ok && m <= 4096)
+        return (n <= 512 || (n <= 1024 && k <= 512)) ? 'X' : 'Y';
+    if (n >= 512)
+        return k >= 1024 ? 'u' : (k >= 512 ? (g5ok ? 'Y' : 'k') : 'y');
+    if (tiles64 >= 2048) return 'y';
+    if (g5ok && (k >= 512 || m <= 16384)) return 'X';
+    if (n <= 128 && k >= 1024) return 'f';
+    return k <= 1024 ? 't' : 'e';
+}
+
+// split-K parts for a g5 variant (1 = none): by default only the measured shapes
+// (splitk_shape; 4 parts at K >= 2048, else 2), FGR_GEMM_SPLITK=0 never, =1 the automatic
+// factor (g5_ksplit) for any g5 variant; FGR_GEMM_KSPLIT forces one
+int h3_ksplit(char cfg, int m, int n, int k) {
+    int bm, bn;
+    if (k % 8 != 0 || !g5_tile(cfg, &bm, &bn)) return 1;
+    const char* on = getenv("FGR_GEMM_SPLITK");
+    const char* f = getenv("FGR_GEMM_KSPLIT");
+    if (f && f[0]) return g5_ksplit(m, n, k, bm, bn);
+    if (on && on[0] == '0') return 1;
+    if (on && on[0] == '1') return g5_ksplit(m, n, k, bm, bn);
+    return splitk_shape(m, n, k) ? (k >= 2048 ? 4 : 2) : 1;
+}
+}  // namespace fgr
+
+extern "C" int fgr_gemm_workspace(int32_t m, int32_t n, int32_t k, int32_t mode, size_t* bytes) {
+    FGR_REQUIRE(bytes && m >= 0 && n > 0 && k > 0 && (mode == 0 || mode == 1),
+                "fgr_gemm_workspace: bad arguments");
+    const char cfg = mode == 0 ? h3_tile(m, n, k) : bf16_tile(m, n, k);
+    const int ks = mode == 0 ? h3_ksplit(cfg, m, n, k) : bf16_ksplit(cfg, m, n, k);
+    *bytes = ks > 1 ? (size_t)ks * m * n * sizeof(float) : 0;
+    return FGR_OK;
+}
+
+static int gemm_f16x3_impl(const float* a, int64_t lda, const void* w_img, float* c,
+                           int64_t ldc, const float* bias, const float* r, int64_t ldr,
+                           int32_t m, int32_t n, int32_t k, int32_t act, void* ws,
+                           size_t ws_bytes, void* stream) {
     FGR_REQUIRE(a && w_img && c && m >= 0 && n > 0 && k > 0 && lda >= k && ldc >= n &&
                     (!r || ldr >= n),
                 "fgr_gemm_f16x3: bad arguments (m %d n %d k %d lda %lld)", m, n, k,
@@ -1212,42 +1278,18 @@ extern "C" int fgr_gemm_f16x3(const float* a, int64_t lda, const void* w_img, fl
                  m, n, k, act, vo ? 1 : 0};
     hipStream_t st = as_stream(stream);
     TimedCall timed_(st);
-    // tile BM x BN (activation rows x output channels); FGR_GEMM16_TILE overrides it for
-    // tuning (a = 128x128, b = 64x128, c = 64x64, d = 128x64, e..x: v2-v4 variants, A..R: g5)
-    // Default per shape (measured on the forward's GEMMs with tools/gemm_tiles.py, device
-    // time from HIP-graph replays; profiles/r02_gemm_tiles*.txt): wide outputs take 64 x 128
-    // tiles (v4 -- W fragments straight to registers -- for K >= 1024, double-buffered v2
-    // for K >= 512), very tall ones 64 x 128; narrow outputs (N <= 256) and short row counts
-    // (M <= 4096, N <= 512) the 64 x 64 LDS-DMA g5 ('I') when K % 8 == 0, else the 64 x 64 v4.
-    // X / Y are I / B and y is b with the row-major staged epilogue (3-8 % faster;
-    // profiles/r02_gemm_tiles_epi.txt, r02_gemm_tiles_by.txt).
-    // Few tiles (<= 400 of 64 x 64, e.g. the 3DMatch transformer's 2 x 1060 tokens) with
-    // K >= 512: the two-k-group g5 ('W', 'T'; 8 waves per block) -- 1.1-1.45x there
-    // (profiles/r02_gemm_tiles_splitk*.txt).
-    const char* force = getenv("FGR_GEMM16_TILE");
-    const bool g5ok = k % 8 == 0;
-    const int64_t tiles64 = (int64_t)ceil_div(m, 64) * ceil_div(n, 64);
-    char cfg;
-    if (force && force[0])
-        cfg = force[0];
-    else if (g5ok && tiles64 <= 400 && k >= 512 && n >= 32)
-        cfg = (k >= 2048 || n <= 64) ? 'S' : ((n <= 128 && k >= 1024 && tiles64 > 256) ? 'T' : 'W');
-    else if (g5ok && m <= 4096)
-        cfg = (n <= 512 || (n <= 1024 && k <= 512)) ? 'X' : 'Y';
-    else if (n >= 512)
-        cfg = k >= 1024 ? 'u' : (k >= 512 ? (g5ok ? 'Y' : 'k') : 'y');
-    else if (tiles64 >= 2048)
-        cfg = 'y';
-    else if (g5ok && (k >= 512 || m <= 16384))
-        cfg = 'X';
-    else if (n <= 128 && k >= 1024)
-        cfg = 'f';
-    else
-        cfg = k <= 1024 ? 't' : 'e';
+    // tile BM x BN (activation rows x output channels): h3_tile; FGR_GEMM16_TILE overrides it
+    // for tuning (a = 128x128, b = 64x128, c = 64x64, d = 128x64, e..x: v2-v4 variants, A..Z,
+    // 0..9: g5)
+    const char cfg = h3_tile(m, n, k);
     // g5 (gemm5.hip: LDS-DMA pipeline, A split after the read): A..W, K % 8 == 0 only
     if (((cfg >= 'A' && cfg <= 'Z') || (cfg >= '0' && cfg <= '9')) && k % 8 == 0) {
+        int ks = h3_ksplit(cfg, m, n, k);
+        if (ks > 1 && (!ws || ws_bytes < (size_t)ks * m * n * sizeof(float) ||
+                       (reinterpret_cast<uintptr_t>(ws) & 15) != 0))
+            ks = 1;                                     // no room for the parts: no split
         FGR_REQUIRE(gemm_g5_f16x3(cfg, a, lda, w_img, ksteps_h3(k), wsc, c, ldc, bias, r, ldr, m, n, k, act,
-                      vo ? 1 : 0, st),
+                      vo ? 1 : 0, st, ks, static_cast<float*>(ws)),
                     "fgr_gemm_f16x3: g5 variant %c unavailable", cfg);
         FGR_CHECK_LAUNCH("gemm_g5");
         return FGR_OK;
@@ -1294,6 +1336,19 @@ extern "C" int fgr_gemm_f16x3(const float* a, int64_t lda, const void* w_img, fl
         launch_h3<64, 64>(g, st);
     FGR_CHECK_LAUNCH("gemm_f16x3_kernel");
     return FGR_OK;
+}
+
+extern "C" int fgr_gemm_f16x3(const float* a, int64_t lda, const void* w_img, float* c,
+                              int64_t ldc, const float* bias, const float* r, int64_t ldr,
+                              int32_t m, int32_t n, int32_t k, int32_t act, void* stream) {
+    return gemm_f16x3_impl(a, lda, w_img, c, ldc, bias, r, ldr, m, n, k, act, nullptr, 0, stream);
+}
+
+extern "C" int fgr_gemm_f16x3_ws(const float* a, int64_t lda, const void* w_img, float* c,
+                                 int64_t ldc, const float* bias, const float* r, int64_t ldr,
+                                 int32_t m, int32_t n, int32_t k, int32_t act, void* ws,
+                                 size_t ws_bytes, void* stream) {
+    return gemm_f16x3_impl(a, lda, w_img, c, ldc, bias, r, ldr, m, n, k, act, ws, ws_bytes, stream);
 }
 
 namespace fgr {

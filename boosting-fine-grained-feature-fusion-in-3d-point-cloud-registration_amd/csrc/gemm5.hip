@@ -54,6 +54,7 @@ struct G5Args {
     const float* bias;
     const float* R; int64_t ldr;
     int M, N, K, act, vec_out;
+    int ksplit; float* part;          // split-K: partials [ksplit][M][N] (scaled, no epilogue)
 };
 
 // chunk swizzle of A row r (16-B chunk q of a 128-B row line lands at q ^ swz(r)): rows
@@ -117,12 +118,14 @@ __global__ void __launch_bounds__(256 * KW) gemm_g5(G5Args p) {
     __shared__ u32x4 lds[S * ST];
 
     const int nbm = (p.M + BM - 1) / BM, nbn = (p.N + BN - 1) / BN;
-    const int nwg = nbm * nbn;
+    const int nwg = nbm * nbn, ntot = nwg * p.ksplit;
     int t = blockIdx.x;
     {   // XCD-aware bijective remap: consecutive tiles (n fastest) on one XCD
-        const int q = nwg / 8, r = nwg % 8, x = t % 8, lo = t / 8;
+        const int q = ntot / 8, r = ntot % 8, x = t % 8, lo = t / 8;
         t = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + lo;
     }
+    const int kz = t / nwg;                    // split-K part (0 without split)
+    t %= nwg;
     const int bm = t / nbn, bn = t % nbn;
     const int m0 = bm * BM, n0 = bn * BN;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -131,7 +134,10 @@ __global__ void __launch_bounds__(256 * KW) gemm_g5(G5Args p) {
     const int rw = w4 / WC, cw = w4 % WC;                    // row slice, column slice
     const int g = lane >> 4, c = lane & 15;
     const int npanel = (p.N + 15) / 16;
-    const int nk = (p.K + 32 * KS - 1) / (32 * KS);          // stages
+    // stages: [sb, sb + nk) of the K range (split-K: this block's share)
+    const int nk_all = (p.K + 32 * KS - 1) / (32 * KS);
+    const int sb = (int)((int64_t)kz * nk_all / p.ksplit);
+    const int nk = (int)((int64_t)(kz + 1) * nk_all / p.ksplit) - sb;
 
     // ---- DMA sources of this wave's P pieces (per stage: + stage * KS * 32 floats / units)
     // (A_PIECES % NW == 0: piece j of every wave is an A piece iff j < A_PIECES / NW)
@@ -159,8 +165,9 @@ __global__ void __launch_bounds__(256 * KW) gemm_g5(G5Args p) {
             akoff[j] = 0;
         }
     }
-    auto issue = [&](int s) {
-        lds_void* base = (lds_void*)(lds + (s % S) * ST);
+    auto issue = [&](int sl) {
+        lds_void* base = (lds_void*)(lds + (sl % S) * ST);
+        const int s = sb + sl;                                 // global stage
         const int k0 = s * KS * 32;
         if (k0 + KS * 32 <= p.K) {                              // wave-uniform: no K tail
 #pragma unroll
@@ -396,6 +403,36 @@ __global__ void __launch_bounds__(256 * KW) gemm_g5(G5Args p) {
         }
     }
 
+    if (p.ksplit > 1) {
+        // split-K: this part's scaled product, no bias / residual / activation (applied by
+        // g5_splitk_reduce after summing the parts in order)
+        float* pk = p.part + (int64_t)kz * p.M * p.N;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const int m = m0 + rw * WR + 16 * i + c;
+            if (m >= p.M) continue;
+            const float rs = TERMS == 2 ? __builtin_ldexpf(1.f, -sh[i]) : 1.f;
+#pragma unroll
+            for (int j = 0; j < TNW; ++j) {
+                const int n = n0 + 16 * (cw * TNW + j) + 4 * g;
+                if (n >= p.N) continue;
+                float4 ws = make_float4(1.f, 1.f, 1.f, 1.f);
+                if constexpr (TERMS == 2) ws = *reinterpret_cast<const float4*>(p.wsc + n);
+                const float y[4] = {acc[j][i][0] * rs * ws.x, acc[j][i][1] * rs * ws.y,
+                                    acc[j][i][2] * rs * ws.z, acc[j][i][3] * rs * ws.w};
+                float* prow = pk + (int64_t)m * p.N;
+                if ((p.N & 3) == 0 && n + 3 < p.N) {
+                    *reinterpret_cast<float4*>(prow + n) = make_float4(y[0], y[1], y[2], y[3]);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if (n + e < p.N) prow[n + e] = y[e];
+                }
+            }
+        }
+        return;
+    }
+
     if constexpr (KW == 1 && WC == 1) {
         if (p.vec_out && EPI_LDS) {
             // staged epilogue: each wave parks its scaled WR x BN tile in the drained stage
@@ -491,8 +528,40 @@ template <int BM, int BN, int KS, int S, int TERMS, bool PIPE = false, int KW = 
           bool EPI = false>
 void launch_g5(const G5Args& a, hipStream_t st) {
     const int nbm = (a.M + BM - 1) / BM, nbn = (a.N + BN - 1) / BN;
-    hipLaunchKernelGGL((gemm_g5<BM, BN, KS, S, TERMS, PIPE, KW, WC, EPI>), dim3((unsigned)(nbm * nbn)),
-                       dim3(256 * KW), 0, st, a);
+    hipLaunchKernelGGL((gemm_g5<BM, BN, KS, S, TERMS, PIPE, KW, WC, EPI>),
+                       dim3((unsigned)(nbm * nbn * a.ksplit)), dim3(256 * KW), 0, st, a);
+}
+
+// split-K epilogue: C = act(sum_z part[z] + bias (+ R)), parts summed in order z = 0, 1, ...
+// (deterministic); 4 columns per thread
+__global__ void __launch_bounds__(256) g5_splitk_reduce(G5Args p) {
+    const int nq = (p.N + 3) / 4;
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= (int64_t)p.M * nq) return;
+    const int m = (int)(t / nq), n = (int)(t % nq) * 4;
+    const int64_t mn = (int64_t)p.M * p.N;
+    const float* pp = p.part + (int64_t)m * p.N + n;
+    float* crow = p.C + (int64_t)m * p.ldc;
+    const float* rrow = p.R ? p.R + (int64_t)m * p.ldr : nullptr;
+    if ((p.N & 3) == 0 && p.vec_out) {
+        float4 y = *reinterpret_cast<const float4*>(pp);
+        for (int z = 1; z < p.ksplit; ++z) {
+            const float4 v = *reinterpret_cast<const float4*>(pp + z * mn);
+            y.x += v.x; y.y += v.y; y.z += v.z; y.w += v.w;
+        }
+        float4 bb = make_float4(0.f, 0.f, 0.f, 0.f), rr = bb;
+        if (p.bias) bb = *reinterpret_cast<const float4*>(p.bias + n);
+        if (rrow) rr = *reinterpret_cast<const float4*>(rrow + n);
+        *reinterpret_cast<float4*>(crow + n) =
+            make_float4(finish5(y.x, bb.x, rr.x, p.act), finish5(y.y, bb.y, rr.y, p.act),
+                        finish5(y.z, bb.z, rr.z, p.act), finish5(y.w, bb.w, rr.w, p.act));
+        return;
+    }
+    for (int e = 0; e < 4 && n + e < p.N; ++e) {
+        float y = pp[e];
+        for (int z = 1; z < p.ksplit; ++z) y += pp[z * mn + e];
+        crow[n + e] = finish5(y, p.bias ? p.bias[n + e] : 0.f, rrow ? rrow[n + e] : 0.f, p.act);
+    }
 }
 
 const float* g5_zero_ptr() {
@@ -504,8 +573,21 @@ const float* g5_zero_ptr() {
 }
 
 template <int TERMS>
+bool dispatch_g5_tile(char cfg, const G5Args& a, hipStream_t st);
+
+template <int TERMS>
 bool dispatch_g5(char cfg, const G5Args& a, hipStream_t st) {
     if (!a.zero) return false;
+    if (!dispatch_g5_tile<TERMS>(cfg, a, st)) return false;
+    if (a.ksplit > 1) {
+        const int64_t nthr = (int64_t)a.M * ((a.N + 3) / 4);
+        hipLaunchKernelGGL(g5_splitk_reduce, dim3((unsigned)ceil_div(nthr, 256)), dim3(256), 0, st, a);
+    }
+    return true;
+}
+
+template <int TERMS>
+bool dispatch_g5_tile(char cfg, const G5Args& a, hipStream_t st) {
     switch (cfg) {
         case 'A': launch_g5<64, 64, 1, 4, TERMS>(a, st); break;
         case 'B': launch_g5<64, 128, 1, 3, TERMS>(a, st); break;
@@ -556,20 +638,56 @@ bool dispatch_g5(char cfg, const G5Args& a, hipStream_t st) {
 }  // namespace
 
 // A 16-B aligned with lda % 4 == 0 and K % 8 == 0 (checked by the callers).
+// ksplit > 1: split-K over ksplit parts with `part` = ksplit * M * N floats of workspace
 bool gemm_g5_f16x3(char cfg, const float* A, int64_t lda, const void* W, int ksteps,
                    const float* wsc, float* C, int64_t ldc, const float* bias, const float* R,
-                   int64_t ldr, int M, int N, int K, int act, int vec_out, hipStream_t st) {
+                   int64_t ldr, int M, int N, int K, int act, int vec_out, hipStream_t st,
+                   int ksplit, float* part) {
     G5Args a{A, lda, g5_zero_ptr(), (const u32x4*)W, ksteps, wsc, C, ldc, bias, R, ldr, M, N, K,
-             act, vec_out};
+             act, vec_out, ksplit > 1 && part ? ksplit : 1, part};
     return dispatch_g5<2>(cfg, a, st);
 }
 
 bool gemm_g5_bf16(char cfg, const float* A, int64_t lda, const void* W, int ksteps, float* C,
                   int64_t ldc, const float* bias, const float* R, int64_t ldr, int M, int N, int K,
-                  int act, int vec_out, hipStream_t st) {
+                  int act, int vec_out, hipStream_t st, int ksplit, float* part) {
     G5Args a{A, lda, g5_zero_ptr(), (const u32x4*)W, ksteps, nullptr, C, ldc, bias, R, ldr, M, N,
-             K, act, vec_out};
+             K, act, vec_out, ksplit > 1 && part ? ksplit : 1, part};
     return dispatch_g5<1>(cfg, a, st);
+}
+
+// tile of a g5 variant (BM x BN), false for an unknown variant
+bool g5_tile(char cfg, int* bm, int* bn) {
+    static const char* k64x64 = "ACIKMSUW15X";
+    static const char* k64x128 = "BDLQT04Y";
+    static const char* k128x64 = "EJNV3";
+    static const char* k128x128 = "FHOR2789";
+    static const char* k64x256 = "GP6Z";
+    auto in = [cfg](const char* set) { for (; *set; ++set) if (*set == cfg) return true; return false; };
+    if (in(k64x64)) { *bm = 64; *bn = 64; }
+    else if (in(k64x128)) { *bm = 64; *bn = 128; }
+    else if (in(k128x64)) { *bm = 128; *bn = 64; }
+    else if (in(k128x128)) { *bm = 128; *bn = 128; }
+    else if (in(k64x256)) { *bm = 64; *bn = 256; }
+    else return false;
+    return true;
+}
+
+// split-K factor for an M x N x K g5 GEMM on BM x BN tiles: enough blocks to fill the chip
+// twice when the tile grid alone does not (<= 8 parts, >= 4 k32-steps each); FGR_GEMM_KSPLIT
+// forces a factor (tuning)
+int g5_ksplit(int M, int N, int K, int BM, int BN) {
+    const char* f = getenv("FGR_GEMM_KSPLIT");
+    const int64_t tiles = (int64_t)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+    const int kst = (K + 31) / 32;
+    int ks;
+    if (f && f[0]) {
+        ks = atoi(f);
+    } else {
+        ks = 1;
+        while (ks < 8 && tiles * ks < 512 && kst / (2 * ks) >= 4) ks *= 2;
+    }
+    return ks < 1 ? 1 : (ks > kst ? kst : ks);
 }
 
 }  // namespace fgr

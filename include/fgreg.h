@@ -262,6 +262,20 @@ int fgr_gemm_f16x3(const float* a, int64_t lda, const void* w_img, float* c, int
  * third of the matrix-core work. W image built once by fgr_split_weights_bf16
  * (fgr_split_weights_bf16_bytes() bytes, 16-B aligned; element (i, j) read from
  * w[i * stride_n + j * stride_k]); A 16-B aligned with lda % 4 == 0 when k % 8 == 0. */
+/* Split-K forms of fgr_gemm_f16x3 / fgr_gemm_bf16 (same contract plus a caller workspace):
+ * where the tile grid alone cannot fill the chip (few activation rows, long K) the g5 kernel
+ * runs ksplit parts over disjoint k ranges into the workspace and one launch sums them in a
+ * fixed order and applies the epilogue (deterministic). fgr_gemm_workspace (mode 0 = f16x3,
+ * 1 = bf16) returns the bytes the dispatcher wants for a shape (0: no split); a smaller or
+ * NULL workspace runs unsplit. */
+int fgr_gemm_workspace(int32_t m, int32_t n, int32_t k, int32_t mode, size_t* bytes);
+int fgr_gemm_f16x3_ws(const float* a, int64_t lda, const void* w_img, float* c, int64_t ldc,
+                      const float* bias, const float* r, int64_t ldr, int32_t m, int32_t n,
+                      int32_t k, int32_t act, void* ws, size_t ws_bytes, void* stream);
+int fgr_gemm_bf16_ws(const float* a, int64_t lda, const void* w_img, float* c, int64_t ldc,
+                     const float* bias, const float* r, int64_t ldr, int32_t m, int32_t n,
+                     int32_t k, int32_t act, void* ws, size_t ws_bytes, void* stream);
+
 int fgr_split_weights_bf16_bytes(int32_t n, int32_t k, size_t* bytes);
 int fgr_split_weights_bf16(const float* w, int32_t n, int32_t k, int64_t stride_n,
                            int64_t stride_k, void* img, void* stream);

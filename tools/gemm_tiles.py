@@ -1,6 +1,6 @@
 """GEMM tile sweep (development tool, GPU): times fgr_gemm_f16x3 per tile configuration
 (FGR_GEMM16_TILE) on the forward's shapes and checks every variant against an fp64 product.
-usage: python tools/gemm_tiles.py [configs] [bf16] [3d] > gpurun_out/gemm_tiles.txt
+usage: python tools/gemm_tiles.py [configs] [bf16] [3d] [ks] > gpurun_out/gemm_tiles.txt
 (bf16: fgr_gemm_bf16 with FGR_GEMM_BF16_TILE, checked against bf16-rounded operands)"""
 import os
 import sys
@@ -44,8 +44,15 @@ def timeit(fn, iters=20):
     return a.elapsed_time(b) / (3 * iters) * 1e3
 
 
+# split-K factors swept per tile ('' = the dispatcher's own choice): `ks` in argv sweeps 1/2/4/8
+KSPLITS = ['']
+
+
 def main():
+    global KSPLITS
     cfgs = sys.argv[1] if len(sys.argv) > 1 else 'btukABCDEFGHIJ'
+    if 'ks' in sys.argv[2:]:
+        KSPLITS = ['1', '2', '4', '8']
     bf = 'bf16' in sys.argv[2:]
     shapes = SHAPES_3D if '3d' in sys.argv[2:] else SHAPES
     env = 'FGR_GEMM_BF16_TILE' if bf else 'FGR_GEMM16_TILE'
@@ -61,17 +68,21 @@ def main():
             ref = (x.double() @ w.double().t())
         line = f'M={M:6d} N={N:5d} K={K:5d}'
         best = None
-        for t in cfgs:
+        variants = [(t, ks) for t in cfgs for ks in KSPLITS]
+        for t, ks in variants:
             os.environ[env] = t
+            os.environ['FGR_GEMM_KSPLIT'] = ks
             out = torch.empty(M, N, device=dev)
             y = lin.linear(x, w, out=out)
             err = float((y.double() - ref).abs().max() / ref.abs().max())
             us = timeit(lambda: lin.linear(x, w, out=out))
             tf = 2 * M * N * K / us / 1e6
-            line += f' | {t} {us:6.1f}us {tf:5.0f}TF{"" if err < 1e-5 else " ERR%.1e" % err}'
+            tag = t + (f'/{ks}' if ks else '')
+            line += f' | {tag} {us:6.1f}us {tf:5.0f}TF{"" if err < 1e-5 else " ERR%.1e" % err}'
             if best is None or us < best[1]:
-                best = (t, us)
+                best = (tag, us)
         os.environ[env] = ''
+        os.environ['FGR_GEMM_KSPLIT'] = ''
         us0 = timeit(lambda: lin.linear(x, w, out=out))
         print(line + f' || default {us0:6.1f}us best {best[0]}', flush=True)
 
