@@ -62,6 +62,7 @@ class RegTR(GenericRegModel):
         self.weight_dict['feature_un'] = cfg.wt_feature_un
 
     forward = fgreg.RegTR.forward
+    _prepare = fgreg.RegTR._prepare
     _forward = fgreg.RegTR._forward
     _core = fgreg.RegTR._core
     _segments = fgreg.RegTR._segments
