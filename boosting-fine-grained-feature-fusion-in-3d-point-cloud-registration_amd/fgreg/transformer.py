@@ -98,9 +98,10 @@ class TransformerCrossEncoderLayer(nn.Module):
     def forward_packed(self, x, pos, seg: Segments, pending_bias=None):
         """x (N_tot, d) packed clouds -> (x, pending bias) (forward_pre, transformers.py:183-244).
 
-        Each residual GEMM adds its product into x without the Linear's bias; that bias is
-        returned as 'pending' and folded into the next LayerNorm launch (which writes the
-        biased x back), saving one elementwise pass per residual branch."""
+        Every residual GEMM adds its Linear's bias and the residual in its epilogue, so each
+        LayerNorm only reads x (no in-place bias pass writing x back); ``pending_bias`` (a
+        bias still to be added to x by the first LayerNorm) is accepted for callers that
+        defer one, and the returned pending bias is None."""
         if (pending_bias is None and lin.MODE == 'f16x3' and lin.ROWS != '0'
                 and self.sa_val_has_pos_emb and self.ca_val_has_pos_emb and x.shape[1] <= 256):
             return self._forward_rows(x, pos, seg)
@@ -110,19 +111,18 @@ class TransformerCrossEncoderLayer(nn.Module):
         h0 = None if self.sa_val_has_pos_emb else ops.layernorm(x, self.norm1.weight,
                                                                  self.norm1.bias, self.norm1.eps)
         o = self._attend(self.self_attn, h, h0, self.sa_val_has_pos_emb, seg, seg.self_seg)
-        x = linear(o, self.self_attn.out_proj.weight, residual=x)
+        x = linear(o, self.self_attn.out_proj.weight, self.self_attn.out_proj.bias, residual=x)
         # cross-attention, both directions at once (:212-229)
-        h = ops.layernorm(x, self.norm2.weight, self.norm2.bias, self.norm2.eps, add=pos,
-                          pre_bias=self.self_attn.out_proj.bias)
+        h = ops.layernorm(x, self.norm2.weight, self.norm2.bias, self.norm2.eps, add=pos)
         h0 = None if self.ca_val_has_pos_emb else ops.layernorm(x, self.norm2.weight,
                                                                  self.norm2.bias, self.norm2.eps)
         o = self._attend(self.multihead_attn, h, h0, self.ca_val_has_pos_emb, seg, seg.cross_seg)
-        x = linear(o, self.multihead_attn.out_proj.weight, residual=x)
+        x = linear(o, self.multihead_attn.out_proj.weight, self.multihead_attn.out_proj.bias,
+                   residual=x)
         # position-wise feed-forward (:231-238)
-        h = ops.layernorm(x, self.norm3.weight, self.norm3.bias, self.norm3.eps,
-                          pre_bias=self.multihead_attn.out_proj.bias)
+        h = ops.layernorm(x, self.norm3.weight, self.norm3.bias, self.norm3.eps)
         h = linear(h, self.linear1.weight, self.linear1.bias, act=ops.ACT_RELU)
-        return linear(h, self.linear2.weight, residual=x), self.linear2.bias
+        return linear(h, self.linear2.weight, self.linear2.bias, residual=x), None
 
     def _forward_rows(self, x, pos, seg: Segments):
         """forward_pre with each LayerNorm (+ pos) fused into the GEMM that consumes it
