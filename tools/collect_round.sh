@@ -12,3 +12,6 @@ for pair in "modelnet:bench:gemm:prof" "3dmatch:bench3d:gemm3d:prof3d" "3dlomatc
   ms=$(python3 -c "import json;print(json.loads(open('gpurun_out/${p}_$tag.json').read().strip().splitlines()[-1])['ms_per_step'])")
   python3 tools/kernel_stats.py gpurun_out/${p}_$tag/*/*_kernel_trace.csv 20 $ms > profiles/${tag}_${wl}_kernel_stats_per_step.txt
 done
+for wl in modelnet 3dmatch; do
+  [ -f gpurun_out/pmc_kpconv_${wl}_$tag.json ] && cp gpurun_out/pmc_kpconv_${wl}_$tag.json profiles/pmc_kpconv_$wl.json
+done
