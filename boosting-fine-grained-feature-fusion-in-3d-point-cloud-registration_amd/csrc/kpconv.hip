@@ -93,6 +93,7 @@ kpconv_gather_wide(const float* __restrict__ q, const float* __restrict__ s, int
     constexpr int U = 4;                               // neighbour rows in flight
     __shared__ float w_lds[kGatherWaves][64 + U][KU];
     __shared__ int nb_lds[kGatherWaves][64 + U];
+    __shared__ float3 p_lds[kGatherWaves][64];
     __shared__ float kp[3 * kMaxKp];
     const int wv = threadIdx.x / 64, lane = threadIdx.x % 64;
     for (int i = threadIdx.x; i < 3 * n_kp; i += blockDim.x) kp[i] = kp_g[i];
@@ -118,7 +119,13 @@ kpconv_gather_wide(const float* __restrict__ q, const float* __restrict__ s, int
         if (v == 0) continue;
         if constexpr (!POSI) n_pos += __popcll(__ballot(valid && pos[id] != 0));
         const int p = __popcll(m & ((1ull << lane) - 1ull));
-        if (valid) nb_lds[wv][p] = (int)id;
+        if (valid) {
+            // the lane that holds a valid neighbour loads its position once (one memory round
+            // trip for the whole chunk; the influence loop below then reads LDS only)
+            nb_lds[wv][p] = (int)id;
+            // neighbours are centred first, then compared with the kernel points (:302, :313)
+            p_lds[wv][p] = make_float3(s[3 * id] - qx, s[3 * id + 1] - qy, s[3 * id + 2] - qz);
+        }
         if (lane < U) nb_lds[wv][v + lane] = 0;       // pad rows: weight 0, row 0
         __builtin_amdgcn_wave_barrier();
         // kernel-point influences of the valid neighbours -> LDS (pad rows get 0)
@@ -126,10 +133,8 @@ kpconv_gather_wide(const float* __restrict__ q, const float* __restrict__ s, int
             const int hh = t / KU, k = t - hh * KU;
             float w = 0.f;
             if (hh < v && k < n_kp) {
-                const int sid = nb_lds[wv][hh];
-                // neighbours are centred first, then compared with the kernel points (:302, :313)
-                const float nx = s[3 * sid] - qx, ny = s[3 * sid + 1] - qy, nz = s[3 * sid + 2] - qz;
-                w = kp_weight(nx, ny, nz, kp, k, inv_extent);
+                const float3 d = p_lds[wv][hh];
+                w = kp_weight(d.x, d.y, d.z, kp, k, inv_extent);
             }
             w_lds[wv][hh][k] = w;
         }
@@ -183,6 +188,7 @@ kpconv_gather_quads(const float* __restrict__ q, const float* __restrict__ s, in
     static_assert(KG * KPL >= KW, "kernel points per lane");
     __shared__ float w_lds[4][64 + U][KW];
     __shared__ int nb_lds[4][64 + U];
+    __shared__ float3 p_lds[4][64];
     __shared__ float kp[3 * kMaxKp];
     const int wv = threadIdx.x / 64, lane = threadIdx.x % 64;
     const int quad = lane % QUADS, kg = lane / QUADS;
@@ -203,16 +209,19 @@ kpconv_gather_quads(const float* __restrict__ q, const float* __restrict__ s, in
         const unsigned long long m = __ballot(valid);
         const int v = __popcll(m);
         if (v == 0) continue;
-        if (valid) nb_lds[wv][__popcll(m & ((1ull << lane) - 1ull))] = (int)id;
+        if (valid) {
+            const int p = __popcll(m & ((1ull << lane) - 1ull));
+            nb_lds[wv][p] = (int)id;
+            p_lds[wv][p] = make_float3(s[3 * id] - qx, s[3 * id + 1] - qy, s[3 * id + 2] - qz);
+        }
         if (lane < U) nb_lds[wv][v + lane] = 0;        // pad rows: weight 0, row 0
         __builtin_amdgcn_wave_barrier();
         for (int t = lane; t < (v + U) * KW; t += 64) {
             const int hh = t / KW, k = t % KW;
             float w = 0.f;
             if (hh < v && k < n_kp) {
-                const int sid = nb_lds[wv][hh];
-                const float nx = s[3 * sid] - qx, ny = s[3 * sid + 1] - qy, nz = s[3 * sid + 2] - qz;
-                w = kp_weight(nx, ny, nz, kp, k, inv_extent);
+                const float3 d = p_lds[wv][hh];
+                w = kp_weight(d.x, d.y, d.z, kp, k, inv_extent);
             }
             w_lds[wv][hh][k] = w;
         }
