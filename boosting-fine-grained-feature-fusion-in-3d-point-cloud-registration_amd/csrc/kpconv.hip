@@ -21,6 +21,9 @@ namespace {
 
 constexpr int kMaxKp = 32;         // kernel points supported (configs use 15)
 constexpr int kGatherWaves = 4;    // waves (= queries) per block, wide kernel
+#ifndef GATHER_U
+#define GATHER_U 4                 // neighbour rows in flight per wave (8 measured 10 % slower)
+#endif
 
 template <int VEC>
 __device__ __forceinline__ void load_vec(const float* p, float (&v)[VEC]) {
@@ -90,7 +93,7 @@ kpconv_gather_wide(const float* __restrict__ q, const float* __restrict__ s, int
                    const unsigned char* __restrict__ pos, const float* __restrict__ kp_g, int n_kp,
                    float inv_extent, float* __restrict__ wf, float* __restrict__ nnorm) {
     constexpr int CIN = 64 * VEC;
-    constexpr int U = 4;                               // neighbour rows in flight
+    constexpr int U = GATHER_U;                        // neighbour rows in flight
     __shared__ float w_lds[kGatherWaves][64 + U][KU];
     __shared__ int nb_lds[kGatherWaves][64 + U];
     __shared__ float3 p_lds[kGatherWaves][64];
@@ -184,7 +187,7 @@ kpconv_gather_quads(const float* __restrict__ q, const float* __restrict__ s, in
                     int64_t ns, const int64_t* __restrict__ idx, int width,
                     const float* __restrict__ x, const float* __restrict__ kp_g, int n_kp,
                     float inv_extent, float* __restrict__ wf, float* __restrict__ nnorm) {
-    constexpr int CIN = 4 * QUADS, KG = 64 / QUADS, U = 4, KW = 16;
+    constexpr int CIN = 4 * QUADS, KG = 64 / QUADS, U = GATHER_U, KW = 16;
     static_assert(KG * KPL >= KW, "kernel points per lane");
     __shared__ float w_lds[4][64 + U][KW];
     __shared__ int nb_lds[4][64 + U];
