@@ -21,6 +21,43 @@
 namespace fgr {
 namespace {
 
+// dst[r0 + row][0..cols) = src[r0 + row][0..cols) for row < rows (rows past n skipped): the
+// concatenation tail of the chain kernels. 16-B accesses when every row start is 16-B aligned,
+// four of them in flight per thread (the element-wise loop exposed one memory round trip per
+// element: ~55 per thread for a 1024-channel x)
+__device__ __forceinline__ void copy_rows(float* __restrict__ dst, int64_t ldd,
+                                          const float* __restrict__ src, int64_t lds, int64_t r0,
+                                          int rows, int64_t n, int cols, int tid, int nth) {
+    const bool v4 = ((cols | (int)(ldd & 3) | (int)(lds & 3)) & 3) == 0 &&
+                    ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15) == 0;
+    if (v4) {
+        const int c4 = cols / 4, tot = rows * c4;
+        for (int e0 = tid; e0 < tot; e0 += 4 * nth) {
+            float4 v[4];
+            int64_t so[4], dof[4];
+            bool ok[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int e = e0 + u * nth;
+                const int row = e / c4, cc = (e - row * c4) * 4;
+                ok[u] = e < tot && r0 + row < n;
+                so[u] = (r0 + row) * lds + cc;
+                dof[u] = (r0 + row) * ldd + cc;
+                if (ok[u]) v[u] = *reinterpret_cast<const float4*>(src + so[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (ok[u]) *reinterpret_cast<float4*>(dst + dof[u]) = v[u];
+        }
+        return;
+    }
+    for (int e = tid; e < rows * cols; e += nth) {
+        const int row = e / cols, cc = e - row * cols;
+        if (r0 + row < n) dst[(r0 + row) * ldd + cc] = src[(r0 + row) * lds + cc];
+    }
+}
+
+
 using f32x4 = __attribute__((ext_vector_type(4))) float;
 
 constexpr int kRows = 32;
@@ -92,18 +129,9 @@ res2net_chain_kernel(const float* __restrict__ h, int64_t n, int scale, int nums
         __syncthreads();
     }
     // untouched chunks and the block input (downsample operand) into the cat buffer
-    const int rest = (scale - nums) * W;
-    for (int e = tid; e < kRows * rest; e += nth) {
-        const int row = e / rest, cc = e - row * rest;
-        if (r0 + row < n)
-            cat[(r0 + row) * ld + (int64_t)nums * W + cc] = h[(r0 + row) * hw + (int64_t)nums * W + cc];
-    }
-    if (x) {
-        for (int e = tid; e < kRows * cin; e += nth) {
-            const int row = e / cin, cc = e - row * cin;
-            if (r0 + row < n) cat[(r0 + row) * ld + hw + cc] = x[(r0 + row) * cin + cc];
-        }
-    }
+    copy_rows(cat + (int64_t)nums * W, ld, h + (int64_t)nums * W, hw, r0, kRows, n,
+              (scale - nums) * W, tid, nth);
+    if (x) copy_rows(cat + hw, ld, x, cin, r0, kRows, n, cin, tid, nth);
 }
 
 
@@ -233,18 +261,9 @@ res2net_chain6_kernel(const float* __restrict__ h, int64_t n, int scale, int num
         }
         __syncthreads();
     }
-    const int rest = (scale - nums) * W;
-    for (int e = tid; e < R * rest; e += nth) {
-        const int row = e / rest, cc = e - row * rest;
-        if (r0 + row < n)
-            cat[(r0 + row) * ld + (int64_t)nums * W + cc] = h[(r0 + row) * hw + (int64_t)nums * W + cc];
-    }
-    if (x) {
-        for (int e = tid; e < R * cin; e += nth) {
-            const int row = e / cin, cc = e - row * cin;
-            if (r0 + row < n) cat[(r0 + row) * ld + hw + cc] = x[(r0 + row) * cin + cc];
-        }
-    }
+    copy_rows(cat + (int64_t)nums * W, ld, h + (int64_t)nums * W, hw, r0, R, n,
+              (scale - nums) * W, tid, nth);
+    if (x) copy_rows(cat + hw, ld, x, cin, r0, R, n, cin, tid, nth);
 }
 
 // ------------------------------------------------------------------------------------
@@ -374,18 +393,9 @@ res2net_chain_h3_kernel(const float* __restrict__ h, int64_t n, int w, int scale
         }
         __syncthreads();
     }
-    const int rest = (scale - nums) * w;
-    for (int e = tid; e < kRows * rest; e += nth) {
-        const int row = e / rest, cc = e - row * rest;
-        if (r0 + row < n)
-            cat[(r0 + row) * ld + (int64_t)nums * w + cc] = h[(r0 + row) * hw + (int64_t)nums * w + cc];
-    }
-    if (x) {
-        for (int e = tid; e < kRows * cin; e += nth) {
-            const int row = e / cin, cc = e - row * cin;
-            if (r0 + row < n) cat[(r0 + row) * ld + hw + cc] = x[(r0 + row) * cin + cc];
-        }
-    }
+    copy_rows(cat + (int64_t)nums * w, ld, h + (int64_t)nums * w, hw, r0, kRows, n,
+              (scale - nums) * w, tid, nth);
+    if (x) copy_rows(cat + hw, ld, x, cin, r0, kRows, n, cin, tid, nth);
 }
 
 }  // namespace
