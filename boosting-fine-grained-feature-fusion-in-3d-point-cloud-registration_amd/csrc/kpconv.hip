@@ -131,6 +131,14 @@ kpconv_gather_wide(const float* __restrict__ q, const float* __restrict__ s, int
         }
         if (lane < U) nb_lds[wv][v + lane] = 0;       // pad rows: weight 0, row 0
         __builtin_amdgcn_wave_barrier();
+        // the first U rows are requested before the influences are computed (both need only
+        // the compacted ids), so their memory round trip overlaps the influence loop; with
+        // VEC <= 2 every later batch is also requested one batch ahead
+        constexpr bool DB = VEC <= 2;
+        float xn[U][VEC];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            load_vec<VEC>(x + (int64_t)nb_lds[wv][u] * CIN + lane * VEC, xn[u]);
         // kernel-point influences of the valid neighbours -> LDS (pad rows get 0)
         for (int t = lane; t < (v + U) * KU; t += 64) {
             const int hh = t / KU, k = t - hh * KU;
@@ -144,9 +152,24 @@ kpconv_gather_wide(const float* __restrict__ q, const float* __restrict__ s, int
         __builtin_amdgcn_wave_barrier();
         for (int hh = 0; hh < v; hh += U) {
             float xv[U][VEC];
+            if (hh == 0 || DB) {
 #pragma unroll
-            for (int u = 0; u < U; ++u)
-                load_vec<VEC>(x + (int64_t)nb_lds[wv][hh + u] * CIN + lane * VEC, xv[u]);
+                for (int u = 0; u < U; ++u)
+#pragma unroll
+                    for (int j = 0; j < VEC; ++j) xv[u][j] = xn[u][j];
+            } else {
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    load_vec<VEC>(x + (int64_t)nb_lds[wv][hh + u] * CIN + lane * VEC, xv[u]);
+            }
+            if (DB && hh + U < v) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    // rows past v + U read pad entries (row 0) only when v + U > 64: clamp
+                    const int e = min(hh + U + u, v + U - 1);
+                    load_vec<VEC>(x + (int64_t)nb_lds[wv][e] * CIN + lane * VEC, xn[u]);
+                }
+            }
             if constexpr (POSI) {
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
