@@ -93,6 +93,10 @@ SIGNATURES = {
     'fgr_procrustes': [_vp, _vp, _vp, _i64, _i64, _f32, _vp, _vp],
     'fgr_time_next_call': [_vp, _vp],
     'fgr_pair_pose': [_vp, _vp, _vp, _i64, _vp, _i32, _i32, _f32, _vp, _vp],
+    'fgr_crop_max_points': [ctypes.POINTER(_i32)],
+    'fgr_crop_pairs_mask': [_vp, _i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    'fgr_crop_pairs_assemble': [_vp, _i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp,
+                                _vp, _vp],
 }
 
 NB_INDEX, NB_DIST = 0, 1

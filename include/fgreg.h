@@ -442,6 +442,36 @@ int fgr_corr_loss(const float* xyz, const float* corr, const float* w, const int
 int fgr_se3_compare(const float* pred, const float* gt, int32_t n_layers, int32_t n_pairs,
                     float* rot_deg, float* trans, void* stream);
 
+/* ---- Input side: the ModelNet crop test pipeline on the GPU ----------
+ * Replaces, for a batch of samples, the geometry of data_loaders/modelnet_transforms.py
+ * RandomCrop (:176-246), RandomTransformSE3_euler (:300-355), Resampler (:92-148),
+ * RandomJitter (:151-173) and ShufflePoints (:374-397) as chained by
+ * data_loaders/modelnet.py:111-117; the random draws stay in NumPy's stream on the host
+ * (fgreg/transforms_gpu.py). Pair b's raw cloud is rows [offsets[b], offsets[b+1]) of `raw`
+ * (ld floats per row, xyz first; at most fgr_crop_max_points rows); cloud 0 = source,
+ * 1 = reference.
+ *  fgr_crop_pairs_mask      per (pair, cloud): d = (p - mean(p)) . dirs[b, c] and the
+ *                           percentile threshold (order statistics crop_k[b], crop_k[b]+1 of d,
+ *                           NumPy's lerp with gamma[b]; crop_k[b] < 0: threshold 0, the
+ *                           p_keep = 0.5 rule) -> mask (2, Ntot) u8, keep (2, Ntot) i32 (kept
+ *                           raw indices, in order, at the pair's offset) and count (n_pairs, 2).
+ *  fgr_crop_pairs_assemble  per pair: output row i of cloud c is raw row keep[c][sel[b, c, i]]
+ *                           (Resampler's choice composed with ShufflePoints' permutation by
+ *                           the host), the source moved by rt[b] (3x4 float32), plus
+ *                           noise[b, c, i] (float64, clipped); overlap[b, c, i] = the other
+ *                           cloud's mask at that raw index; corr (2, Ntot) i64 gets the
+ *                           correspondence pairs (raw-index order) at the pair's offset and
+ *                           n_corr[b] their count. sel must hold distinct values < count.
+ * Outputs equal fgreg.transforms.modelnet_crop_test bit for bit (tests/test_gpu_transforms.py). */
+int fgr_crop_max_points(int32_t* n_max);
+int fgr_crop_pairs_mask(const float* raw, int32_t ld, const int64_t* offsets, int32_t n_pairs,
+                        const double* dirs, const int32_t* crop_k, const double* gamma,
+                        uint8_t* mask, int32_t* keep, int32_t* count, void* stream);
+int fgr_crop_pairs_assemble(const float* raw, int32_t ld, const int64_t* offsets, int32_t n_pairs,
+                            const uint8_t* mask, const int32_t* keep, const int32_t* sel,
+                            const double* noise, const float* rt, int32_t m, float* xyz,
+                            uint8_t* overlap, int64_t* corr, int32_t* n_corr, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -83,3 +83,20 @@ def test_crop_pipeline_matches_reference(i, normals, monkeypatch):
     np.testing.assert_array_equal(got['correspondences'].numpy(), sample['correspondences'])
     np.testing.assert_array_equal(got['src_overlap'].numpy(), sample['src_overlap'])
     np.testing.assert_array_equal(got['tgt_overlap'].numpy(), sample['ref_overlap'])
+
+
+@pytest.mark.parametrize('n', [2, 1100, 2048, 4096])
+@pytest.mark.parametrize('p', [0.7, 0.55, 0.9])
+def test_crop_rank_reproduces_percentile(n, p):
+    """transforms_gpu._crop_rank: NumPy's own (k, gamma) of the 'linear' percentile, so the
+    GPU threshold _lerp(s_k, s_k+1, gamma) equals np.percentile (with ties, too)."""
+    from fgreg.transforms_gpu import _crop_rank
+    rng = np.random.default_rng(n)
+    p = np.float32(p)
+    k, g = _crop_rank(n, p)
+    for d in (rng.standard_normal(n), np.round(rng.standard_normal(n), 1)):
+        s = np.sort(d)
+        a, b = s[k], s[min(k + 1, n - 1)]
+        diff = b - a
+        th = b - diff * (1.0 - g) if g >= 0.5 else a + diff * g
+        assert th == np.percentile(d, (1.0 - p) * 100)
