@@ -33,6 +33,25 @@ def _ptr(t):
     return t.data_ptr()
 
 
+def _upload(dev, *arrays):
+    """One host-to-device copy for several small tables: packs the arrays (16-B aligned) into
+    one byte buffer and returns typed device views of it."""
+    offs, pos = [], 0
+    for a in arrays:
+        offs.append(pos)
+        pos += (a.nbytes + 15) // 16 * 16
+    buf = np.zeros(max(pos, 16), dtype=np.uint8)
+    for a, o in zip(arrays, offs):
+        buf[o:o + a.nbytes] = np.ascontiguousarray(a).view(np.uint8).ravel()
+    dbuf = torch.from_numpy(buf).to(dev)
+    return [dbuf[o:o + a.nbytes].view(_TORCH_DT[a.dtype]).view(a.shape)
+            for a, o in zip(arrays, offs)]
+
+
+_TORCH_DT = {np.dtype(np.int64): torch.int64, np.dtype(np.int32): torch.int32,
+             np.dtype(np.float64): torch.float64, np.dtype(np.float32): torch.float32}
+
+
 def _crop_rank(n, p_keep):
     """(k, gamma) of np.percentile(d, (1 - p) * 100) over n values, method 'linear': the
     threshold is NumPy's _lerp(s_k, s_k+1, gamma). Both come from NumPy itself on proxies, so
@@ -86,10 +105,9 @@ def modelnet_crop_test_gpu(points_list, idx_list, p_keep=(0.7, 0.7), rot_mag=45.
         np.random.seed(idx)
         dirs[b, 0] = _uniform_s2()
         dirs[b, 1] = _uniform_s2()
-    off = torch.from_numpy(off_h).to(dev)
-    dirs_d = torch.from_numpy(dirs).to(dev)
-    k_d = torch.tensor([r[0] for r in ranks], dtype=torch.int32).to(dev)
-    g_d = torch.tensor([r[1] for r in ranks], dtype=torch.float64).to(dev)
+    off, dirs_d, k_d, g_d = _upload(dev, off_h, dirs,
+                                    np.array([r[0] for r in ranks], dtype=np.int32),
+                                    np.array([r[1] for r in ranks], dtype=np.float64))
     mask = torch.empty((2, ntot), dtype=torch.uint8, device=dev)
     keep = torch.empty((2, ntot), dtype=torch.int32, device=dev)
     count = torch.empty((B, 2), dtype=torch.int32, device=dev)
@@ -124,9 +142,7 @@ def modelnet_crop_test_gpu(points_list, idx_list, p_keep=(0.7, 0.7), rot_mag=45.
         s_perm = np.random.permutation(m)
         sel[b, 0], sel[b, 1] = s_idx[s_perm], r_idx[r_perm]
         noise[b, 0], noise[b, 1] = nz[0][s_perm], nz[1][r_perm]
-    sel_d = torch.from_numpy(sel).to(dev)
-    noise_d = torch.from_numpy(noise).to(dev)
-    rt_d = torch.from_numpy(rt).to(dev)
+    sel_d, noise_d, rt_d, poses_d = _upload(dev, sel, noise, rt, poses)
     xyz = torch.empty((B, 2, m, 3), dtype=torch.float32, device=dev)
     ov = torch.empty((B, 2, m), dtype=torch.uint8, device=dev)
     corr = torch.empty((2, ntot), dtype=torch.int64, device=dev)
@@ -138,7 +154,6 @@ def modelnet_crop_test_gpu(points_list, idx_list, p_keep=(0.7, 0.7), rot_mag=45.
     nc = n_corr.cpu().numpy()                        # readback 2: correspondence counts
     if (nc < 0).any():
         raise _lib.FgrError('fgr_crop_pairs_assemble: raw cloud size out of range')
-    poses_d = torch.from_numpy(poses).to(dev)
     ovb = ov.bool()
     out = []
     for b, idx in enumerate(idx_list):
