@@ -100,3 +100,16 @@ def test_crop_rank_reproduces_percentile(n, p):
         diff = b - a
         th = b - diff * (1.0 - g) if g >= 0.5 else a + diff * g
         assert th == np.percentile(d, (1.0 - p) * 100)
+
+
+def test_gpu_crop_upload_packing():
+    """transforms_gpu._upload: several tables in one host-to-device copy, typed views intact
+    (run on the CPU device here; the GPU tests use it on cuda)."""
+    from fgreg.transforms_gpu import _upload
+    rng = np.random.default_rng(0)
+    arrs = (np.arange(5, dtype=np.int64), rng.random((2, 2, 3)), np.array([1, 2, 3], np.int32),
+            rng.random((3, 3, 4)).astype(np.float32))
+    out = _upload(torch.device('cpu'), *arrs)
+    for o, a in zip(out, arrs):
+        assert o.shape == a.shape and torch.equal(o, torch.from_numpy(a))
+        assert o.data_ptr() % 16 == 0
