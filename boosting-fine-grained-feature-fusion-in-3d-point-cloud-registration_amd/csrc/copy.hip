@@ -9,19 +9,25 @@ namespace {
 
 constexpr int kMaxCopies = 32;
 
+constexpr int64_t kChunk = 256 * 64;   // bytes per block: 256 threads x 4 x 16 B
+
 struct CopyBatch {
     const char* src[kMaxCopies];
     char* dst[kMaxCopies];
     int64_t bytes[kMaxCopies];
+    int first[kMaxCopies + 1];         // copy k owns blocks [first[k], first[k + 1])
+    int m;
 };
 
-// grid (x: chunks of 256 threads x 4 x 16 B, y: copy); 16-B accesses when both ends allow
+// one flat grid over every copy's chunks (no idle blocks for the short copies); 16-B
+// accesses when both ends allow
 __global__ void __launch_bounds__(256) copy_batch_kernel(CopyBatch b) {
-    const int k = blockIdx.y;
+    int k = 0;
+    while (k + 1 < b.m && b.first[k + 1] <= (int)blockIdx.x) ++k;     // block-uniform
     const char* s = b.src[k];
     char* d = b.dst[k];
     const int64_t n = b.bytes[k];
-    const int64_t chunk = (int64_t)blockIdx.x * 256 * 64;
+    const int64_t chunk = (int64_t)(blockIdx.x - b.first[k]) * kChunk;
     if (chunk >= n) return;
     const bool vec = ((reinterpret_cast<uintptr_t>(s) | reinterpret_cast<uintptr_t>(d)) & 15) == 0;
     if (vec) {
@@ -33,9 +39,9 @@ __global__ void __launch_bounds__(256) copy_batch_kernel(CopyBatch b) {
                 reinterpret_cast<uint4*>(d)[i] = reinterpret_cast<const uint4*>(s)[i];
         }
         const int64_t tail = n16 * 16;
-        if (blockIdx.x == 0 && threadIdx.x < n - tail) d[tail + threadIdx.x] = s[tail + threadIdx.x];
+        if (chunk == 0 && threadIdx.x < n - tail) d[tail + threadIdx.x] = s[tail + threadIdx.x];
     } else {
-        for (int64_t i = chunk + threadIdx.x; i < min(n, chunk + 256 * 64); i += 256) d[i] = s[i];
+        for (int64_t i = chunk + threadIdx.x; i < min(n, chunk + kChunk); i += 256) d[i] = s[i];
     }
 }
 
@@ -51,18 +57,21 @@ extern "C" int fgr_copy_batch(int32_t n, const void* const* src, void* const* ds
     for (int32_t i0 = 0; i0 < n; i0 += kMaxCopies) {
         const int m = n - i0 < kMaxCopies ? n - i0 : kMaxCopies;
         CopyBatch b{};
-        int64_t mx = 0;
+        int64_t nblk = 0;
         for (int j = 0; j < m; ++j) {
             FGR_REQUIRE(bytes[i0 + j] >= 0 && (bytes[i0 + j] == 0 || (src[i0 + j] && dst[i0 + j])),
                         "fgr_copy_batch: copy %d: bad pointer / size", i0 + j);
             b.src[j] = static_cast<const char*>(src[i0 + j]);
             b.dst[j] = static_cast<char*>(dst[i0 + j]);
             b.bytes[j] = bytes[i0 + j];
-            mx = bytes[i0 + j] > mx ? bytes[i0 + j] : mx;
+            b.first[j] = (int)nblk;
+            nblk += ceil_div(bytes[i0 + j], kChunk);
         }
-        if (mx == 0) continue;
-        hipLaunchKernelGGL(copy_batch_kernel, dim3((unsigned)ceil_div(mx, 256 * 64), (unsigned)m),
-                           dim3(256), 0, st, b);
+        FGR_REQUIRE(nblk < (int64_t)1 << 30, "fgr_copy_batch: %lld blocks", (long long)nblk);
+        b.first[m] = (int)nblk;
+        b.m = m;
+        if (nblk == 0) continue;
+        hipLaunchKernelGGL(copy_batch_kernel, dim3((unsigned)nblk), dim3(256), 0, st, b);
         FGR_CHECK_LAUNCH("copy_batch_kernel");
     }
     return FGR_OK;
