@@ -74,6 +74,14 @@ def modelnet_crop_test_gpu(points_list, idx_list, p_keep=(0.7, 0.7), rot_mag=45.
 
     points_list: raw (N_b, 3 or 6) float32 clouds (numpy or torch, any device; all with the
     same column count); idx_list: the sample indices (the per-sample seeds)."""
+    dev = torch.device(device)
+    if dev.type != 'cuda':
+        raise ValueError('modelnet_crop_test_gpu: a GPU device is required (no CPU fallback)')
+    with torch.cuda.device(dev):                    # launches go to this device's stream
+        return _crop_batch(points_list, idx_list, p_keep, rot_mag, trans_mag, jitter, dev)
+
+
+def _crop_batch(points_list, idx_list, p_keep, rot_mag, trans_mag, jitter, dev):
     L = _lib.load()
     B = len(points_list)
     if B == 0 or B != len(idx_list):
@@ -83,7 +91,6 @@ def modelnet_crop_test_gpu(points_list, idx_list, p_keep=(0.7, 0.7), rot_mag=45.
         raise NotImplementedError('GPU crop pipeline: the two-cloud crop (partial: [p, p]) only')
     if np.all(p_keep == 1.0):
         raise NotImplementedError('uncropped pipeline: use the "clean"/"jitter" variant')
-    dev = torch.device(device)
     raws = [torch.as_tensor(np.asarray(p) if not torch.is_tensor(p) else p) for p in points_list]
     ld = raws[0].shape[1]
     if any(r.dim() != 2 or r.shape[1] != ld or ld < 3 for r in raws):
