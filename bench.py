@@ -195,14 +195,28 @@ def main():
     model = fgreg.RegTR(cfg).to(dev).eval()
     P = args.pairs_per_gpu or PAIRS[wl]
     kind = {'raw2048': 'modelnet_raw'}.get(wl, wl)
-    src, tgt, pose_gt = make_batch(kind, P, start=rank * P)   # this rank's shard of pairs
+    from fgreg import dist as fdist
+    if wl in ('3dmatch', '3dlomatch') and world > 1:
+        # variable-size fragments: the global batch of P * world pairs is assigned to ranks by
+        # point count (fgreg.dist.balanced_shards); every rank draws the same
+        # global batch (seeded per pair index) and keeps its shard
+        g_src, g_tgt, g_pose = make_batch(kind, P * world)
+        shards = fdist.balanced_shards([len(a) + len(b) for a, b in zip(g_src, g_tgt)], world)
+        mine = shards[rank]
+        src, tgt, pose_gt = [g_src[i] for i in mine], [g_tgt[i] for i in mine], g_pose[mine]
+        counts = [len(sh) for sh in shards]
+        sharding = 'balanced_shards (greedy by points per pair)'
+    else:
+        src, tgt, pose_gt = make_batch(kind, P, start=rank * P)   # this rank's block of pairs
+        counts = [P] * world
+        sharding = 'contiguous blocks (shard_range)'
+    P = len(src)
     batch_src = [torch.from_numpy(s).to(dev) for s in src]
     batch_tgt = [torch.from_numpy(t).to(dev) for t in tgt]
-    from fgreg import dist as fdist
 
     def finish(out):
         if dist is not None:   # the one exchange: per-pair poses of every rank (RCCL)
-            out['pose_all'] = fdist.gather_pair_results(out['pose'], [P] * world, pair_dim=1)
+            out['pose_all'] = fdist.gather_pair_results(out['pose'], counts, pair_dim=1)
         return out
 
     def step():
@@ -254,6 +268,14 @@ def main():
             ops.TIMER = None
             # timed region: nothing instrumented (graph replay of the core forward)
             elapsed = timed(args.steps)
+            # the same steps with the HIP-graph cache off (every launch eager): what inputs
+            # whose shape signature never repeats get, reported beside `value`
+            fregtr.GRAPHS = False
+            try:
+                run(2)
+                elapsed_eager = timed(args.steps)
+            finally:
+                fregtr.GRAPHS = True
             # per-launch HIP events for every kernel family: an eager replay of the same
             # steps right after the timed region (a graph replay has no per-launch hook); the
             # rocprofv3 trace of the timed region (profiles/) cross-checks the durations
@@ -270,22 +292,24 @@ def main():
             tail_ms, tail_inputs = test_tail(model, batch_src, batch_tgt, src, tgt, pose_gt, dev,
                                               args.steps)
 
-    el = torch.tensor([elapsed], dtype=torch.float64,
+    el = torch.tensor([elapsed, elapsed_eager if not args.profile else 0.0], dtype=torch.float64,
                       device=dev if backend == 'nccl' else 'cpu')
     if dist is not None:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed = float(el.item())
+    elapsed, elapsed_eager = float(el[0].item()), float(el[1].item())
     step_ms = elapsed / args.steps * 1e3
+    n_total = sum(counts)
 
     line = {
-        'metric': METRIC[wl], 'value': world * P * args.steps / elapsed, 'unit': 'pairs/s',
+        'metric': METRIC[wl], 'value': n_total * args.steps / elapsed, 'unit': 'pairs/s',
         'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': step_ms,
         'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
         'dtype': DTYPE.get(lin.MODE, lin.MODE), 'data': DATA[wl],
         'config': {'workload': WORKLOAD[wl].format(P=P), 'pairs_per_gpu': P,
-                   'global_batch': P * world,
+                   'global_batch': n_total,
                    'points_per_cloud': int(np.mean([len(c) for c in src])),
                    'parallelism': f'pair-sharded dp{world}',
+                   'sharding': sharding, 'pairs_per_rank': counts,
                    'precision': fgreg.precision(),
                    'hip_graph': ('post-preprocessing forward replayed from the shape-keyed graph '
                                  'cache; preprocessing eager' if fregtr.GRAPHS else 'off'),
@@ -293,6 +317,12 @@ def main():
                                 'fgreg.pipeline: every step is a full forward; step i + 1\'s '
                                 'preprocessing runs on a side stream while step i\'s core runs')},
     }
+    if not args.profile:
+        line['eager'] = {
+            'value': n_total * args.steps / elapsed_eager, 'unit': 'pairs/s',
+            'ms_per_step': elapsed_eager / args.steps * 1e3,
+            'what': 'the same timed steps with the HIP-graph cache off (FGREG_GRAPHS=0: every '
+                    'launch eager), i.e. inputs whose shape signature never repeats'}
     if args.profile:
         line['profile'] = 'warmup + timed steps only (rocprofv3 companion run)'
         if rank == 0:

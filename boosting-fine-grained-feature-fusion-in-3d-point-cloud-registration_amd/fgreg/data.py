@@ -23,7 +23,6 @@ import numpy as np
 import torch
 
 from . import ops
-from .loss import transform_points
 
 
 def _safe_numpy_globals():
@@ -105,8 +104,12 @@ class ThreeDMatchPairs(torch.utils.data.Dataset):
         if self.pairs is not None and item in self.pairs:
             sm, tm, corr = (torch.as_tensor(np.asarray(v)) for v in self.pairs[item])
         else:
-            off = torch.tensor([0, src.shape[0]], dtype=torch.int64, device=self.device)
-            src_w = transform_points(src, off, pose_t.to(self.device).unsqueeze(0))
+            # the reference applies the float64 pose to the points before its (float64)
+            # Open3D search (threedmatch.py:80-84, se3_numpy.se3_transform): same here, the
+            # result rounded once to float32 for the radius kernel (whose d^2 < r^2 test is
+            # float32 -- DESIGN.md "input side")
+            p64 = torch.from_numpy(pose).to(self.device)
+            src_w = (src_xyz.to(self.device, torch.float64) @ p64[:, :3].T + p64[:, 3]).float()
             sm, tm, corr = compute_overlap(src_w, tgt, self.radius)
         return {'src_xyz': src, 'tgt_xyz': tgt, 'src_overlap': sm, 'tgt_overlap': tm,
                 'correspondences': corr, 'pose': pose_t, 'idx': item,

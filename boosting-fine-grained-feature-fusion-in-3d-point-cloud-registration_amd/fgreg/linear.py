@@ -43,6 +43,24 @@ def set_mode(mode):
     MODE = mode
 
 
+class mode_scope:  # noqa: N801 -- used as a context manager
+    """``with mode_scope('f16x3'):`` runs the enclosed linear() calls in another mode (e.g.
+    the pose-sensitive correspondence head of the bf16 forward in f16x3, regtr.py)."""
+
+    def __init__(self, mode):
+        self.mode, self.prev = mode, None
+
+    def __enter__(self):
+        global MODE
+        self.prev, MODE = MODE, (self.mode or MODE)
+        return self
+
+    def __exit__(self, *exc):
+        global MODE
+        MODE = self.prev
+        return False
+
+
 class SplitWeight:
     __slots__ = ('hi', 'lo', 'ldw', 'n', 'k', 'src', 'version', 'ptr')
 

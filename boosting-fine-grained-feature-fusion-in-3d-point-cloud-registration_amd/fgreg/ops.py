@@ -647,12 +647,47 @@ def copy_batch(srcs, dsts):
 
 _WS = {}
 _WS_RETIRED = []
+_WS_SCOPE = None      # a PrivateWorkspace while one is entered (HIP-graph warm-up / capture)
+
+
+class PrivateWorkspace:
+    """Scratch buffers owned by one client (a captured HIP graph, fgreg/regtr.py _CoreGraph):
+    while entered (``with ws:``), every ``_workspace`` request is served from this object
+    instead of the shared per-(device, stream) buffers, so the graph bakes in scratch memory
+    no other graph and no eager launch ever touches, whatever stream it is replayed on.
+    Outgrown buffers stay referenced (a capture may point at them)."""
+
+    def __init__(self):
+        self.bufs, self.retired, self._prev = {}, [], []
+
+    def get(self, device, nbytes):
+        buf = self.bufs.get(device)
+        if buf is None or buf.numel() < nbytes:
+            if buf is not None:
+                self.retired.append(buf)
+            buf = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
+            self.bufs[device] = buf
+        return buf
+
+    def __enter__(self):
+        global _WS_SCOPE
+        self._prev.append(_WS_SCOPE)
+        _WS_SCOPE = self
+        return self
+
+    def __exit__(self, *exc):
+        global _WS_SCOPE
+        _WS_SCOPE = self._prev.pop()
+        return False
 
 
 def _workspace(device, nbytes):
     """Grow-only scratch buffer per device, reused by consecutive launches on the current
     stream (stream order serialises the reuse). Outgrown buffers are kept alive: a captured
-    HIP graph may still point at them."""
+    HIP graph may still point at them. Inside a ``PrivateWorkspace`` scope the buffer is that
+    scope's own (each captured graph has one)."""
+    if _WS_SCOPE is not None:
+        return _WS_SCOPE.get(device, nbytes)
     key = (device, torch.cuda.current_stream(device).cuda_stream)
     buf = _WS.get(key)
     if buf is None or buf.numel() < nbytes:

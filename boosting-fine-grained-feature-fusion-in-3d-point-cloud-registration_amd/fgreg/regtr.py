@@ -20,6 +20,7 @@ from collections import OrderedDict
 import torch
 import torch.nn as nn
 
+from . import linear as lin
 from . import ops
 from .linear import linear
 from .backbone import KPFEncoder, PreprocessorHIP, host_layout
@@ -27,6 +28,10 @@ from .transformer import (PositionEmbeddingCoordsSine, Segments, TransformerCros
                           TransformerCrossEncoderLayer)
 
 _logger = logging.getLogger(__name__)
+
+# compute mode of the correspondence head's GEMMs when the forward runs in bf16 (None: bf16
+# like the rest); FGREG_BF16_HEAD=f16x3 keeps the pose-sensitive head fp32-accurate
+HEAD_MODE = os.environ.get('FGREG_BF16_HEAD') or None
 
 
 class CorrespondenceRegressor(nn.Module):
@@ -40,14 +45,16 @@ class CorrespondenceRegressor(nn.Module):
         self.conf_logits_decoder = nn.Linear(d_embed, 1)
 
     def forward_packed(self, feats):
-        """feats (L, N, d) -> corr (L, N, 3), logits (L, N, 1)."""
+        """feats (L, N, d) -> corr (L, N, 3), logits (L, N, 1). In the bf16 mode the head
+        runs in ``HEAD_MODE`` (the pose reads its outputs directly; DESIGN.md "bf16 mode")."""
         L, N, d = feats.shape
         f = feats.reshape(L * N, d)
         m = self.coor_mlp
-        h = linear(f, m[0].weight, m[0].bias, act=ops.ACT_RELU)
-        h = linear(h, m[2].weight, m[2].bias, act=ops.ACT_RELU)
-        corr = linear(h, m[4].weight, m[4].bias)
-        logits = linear(f, self.conf_logits_decoder.weight, self.conf_logits_decoder.bias)
+        with lin.mode_scope(HEAD_MODE if lin.MODE == 'bf16' else None):
+            h = linear(f, m[0].weight, m[0].bias, act=ops.ACT_RELU)
+            h = linear(h, m[2].weight, m[2].bias, act=ops.ACT_RELU)
+            corr = linear(h, m[4].weight, m[4].bias)
+            logits = linear(f, self.conf_logits_decoder.weight, self.conf_logits_decoder.bias)
         return corr.view(L, N, 3), logits.view(L, N, 1)
 
 
@@ -238,6 +245,7 @@ class RegTR(nn.Module):
 # FGREG_GRAPHS=0 disables the path (A/B).
 GRAPHS = os.environ.get('FGREG_GRAPHS', '1') != '0'
 GRAPH_CACHE = 8
+SEEN_CACHE = 4096        # signatures remembered for the capture-on-second-sighting rule (LRU)
 _GRAPHS = weakref.WeakKeyDictionary()        # model -> {'ver', 'seen', 'graphs'}
 _META_IN = ('points', 'neighbors', 'pools')  # what the core reads (upsamples: decoder only)
 
@@ -249,13 +257,18 @@ class _CoreGraph:
         self.meta['_host'] = {'lengths': meta['_host']['lengths'],
                               'offsets': [o.clone() for o in meta['_host']['offsets']]}
         self.seg = model._segments(slens_c, meta['points'][-1])
+        # scratch buffers of this graph alone (split-K partials, attention K/V images, gather
+        # flags): a replay never shares them with another graph or an eager launch, on
+        # whatever stream it runs (replays of ONE graph are ordered by the caller's stream,
+        # like its static inputs and outputs)
+        self.ws = ops.PrivateWorkspace()
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):                 # warm-up outside the capture
+        with torch.cuda.stream(side), self.ws:       # warm-up outside the capture
             model._core(self.meta, self.seg, B)
         torch.cuda.current_stream().wait_stream(side)
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        with torch.cuda.graph(self.graph), self.ws:
             self.out = model._core(self.meta, self.seg, B)
 
     def run(self, meta):
@@ -282,18 +295,21 @@ def _graph_for(model, meta, slens_c, B):
     ver, plist = _params_version(model)
     st = _GRAPHS.get(model)
     if st is None or st['ver'] != ver:
-        st = {'ver': ver, 'params': plist, 'seen': {}, 'graphs': OrderedDict()}
+        st = {'ver': ver, 'params': plist, 'seen': OrderedDict(), 'graphs': OrderedDict()}
         _GRAPHS[model] = st
     from . import linear as _lin
-    sig = (B, _lin.MODE, ops.ATTN_MODE, tuple(tuple(l) for l in meta['_host']['lengths']),
+    sig = (B, _lin.MODE, HEAD_MODE, ops.ATTN_MODE, tuple(tuple(l) for l in meta['_host']['lengths']),
            tuple(tuple(t.shape) for t in meta['neighbors']), tuple(tuple(t.shape) for t in meta['pools']))
     g = st['graphs'].get(sig)
     if g is not None:
         st['graphs'].move_to_end(sig)
         return g
-    n = st['seen'].get(sig, 0)
-    st['seen'][sig] = n + 1
-    if n == 0 or len(st['seen']) > 4096:
+    seen = st['seen']
+    n = seen.pop(sig, 0)
+    seen[sig] = n + 1                 # LRU of signatures: most recent last
+    while len(seen) > SEEN_CACHE:
+        seen.popitem(last=False)
+    if n <= 0:
         return None
     try:
         g = _CoreGraph(model, meta, slens_c, B)

@@ -47,11 +47,15 @@ class Segments:
         if n_layers:
             # (layer, cloud) segments of the L stacked layer outputs (L * N rows): segment
             # l * 2B + c attends to l * 2B + partner(c); value rows = the partner's xyz rows
+            # built from the host lengths (reading self.off back would sync the stream)
             N = sum(self.lengths)
-            q_off = [l * N + o for l in range(n_layers) for o in self.off.tolist()[:-1]]
+            host_off = [0]
+            for ln in self.lengths[:-1]:
+                host_off.append(host_off[-1] + ln)
+            q_off = [l * N + o for l in range(n_layers) for o in host_off]
             q_off.append(n_layers * N)
             kv_seg = [l * n + (c + self.B) % n for l in range(n_layers) for c in range(n)]
-            v_off = self.off.tolist()[:-1] * n_layers
+            v_off = host_off * n_layers
             self.layer_tables = (torch.tensor(q_off, dtype=torch.int64, device=device),
                                  torch.tensor(kv_seg, dtype=torch.int32, device=device),
                                  torch.tensor(v_off, dtype=torch.int64, device=device))

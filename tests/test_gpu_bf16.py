@@ -19,14 +19,17 @@ from conftest import rel_err
 
 pytestmark = pytest.mark.gpu
 
-# stated tolerances of the bf16 forward against the fp32 oracle (DESIGN.md "bf16 mode")
-# (measured on MI355X: features 1.0-2.5e-2, scores 3-6e-3, rotation 1.0-1.2 deg, translation
-# 2-3 mm). The pose bounds are 1/5 of the reference's own registration-success thresholds
-# (conf reg_success_thresh_rot 10 deg / _trans 0.1 m): with random-init weights the predicted
-# correspondences collapse toward the centroids and the Procrustes rotation is ill-conditioned,
-# so the bf16 feature error shows up amplified there (the fp32-accurate mode stays at 1e-4).
-BF16_FEAT_TOL = 3e-2        # normwise relative, every per-pair output tensor
-BF16_ROT_DEG = 2.0          # rotation difference of the predicted poses, degrees
+# stated tolerances of the bf16 forward against the fp32 oracle (DESIGN.md "bf16 mode"), set
+# from a sweep over 10 random models (profiles/r03_bf16_sweep.jsonl, tools/bf16_sweep.py: seeds
+# 0-7 at 6k points, 20-21 at 20k): worst case measured 3.4e-2 normwise (a warped-keypoint
+# tensor; features <= 2.2e-2, overlap scores <= 7.9e-3), rotation 2.85 deg, translation 7.4 mm.
+# The pose bounds are half of the reference's own registration-success thresholds (conf
+# reg_success_thresh_rot 10 deg / _trans 0.1 m is 5x the translation bound): with random-init
+# weights the predicted correspondences collapse toward the centroids and the Procrustes rotation
+# is ill-conditioned, so the ~2 % bf16 feature error shows up amplified there (the fp32-accurate
+# mode stays at 1e-4 on the same cases).
+BF16_FEAT_TOL = 5e-2        # normwise relative, every per-pair output tensor
+BF16_ROT_DEG = 5.0          # rotation difference of the predicted poses, degrees
 BF16_TRANS = 0.02           # translation difference, metres
 KEYS = ['src_feat_un', 'tgt_feat_un', 'src_feat', 'tgt_feat', 'src_kp_warped', 'tgt_kp_warped',
         'src_overlap', 'tgt_overlap']
@@ -150,16 +153,17 @@ def _rot_deg(a, b):
     return math.degrees(math.acos(max(-1.0, min(1.0, (np.trace(r) - 1) / 2))))
 
 
-@pytest.mark.parametrize('n_points', [6000, 20000])
-def test_bf16_forward_3dlomatch_vs_oracle(gpu, bf16_mode, n_points):
-    """The configs[4] forward in bf16 on low-overlap pairs against the fp32 CPU oracle:
-    geometry bit-exact, outputs within the stated bf16 tolerance."""
+@pytest.mark.parametrize('seed,n_points', [(s, 6000) for s in range(8)] + [(20, 20000), (21, 20000)])
+def test_bf16_forward_3dlomatch_vs_oracle(gpu, bf16_mode, seed, n_points):
+    """The configs[4] forward in bf16 on low-overlap pairs against the fp32 CPU oracle, over
+    10 random models and input pairs (seeded per case; no hand-picked seed): geometry
+    bit-exact, outputs within the stated bf16 tolerance."""
     import fgreg.config as fc
     from fgreg.synthetic import make_batch
     cfg = fc.get('3dlomatch')
-    model = _random_model(cfg, 13)
+    model = _random_model(cfg, seed)
     sd = {k: v.clone() for k, v in model.state_dict().items()}
-    src, tgt, _ = make_batch('3dlomatch', 1, n_points=n_points)
+    src, tgt, _ = make_batch('3dlomatch', 1, start=seed, n_points=n_points)
     model = model.to(gpu)
     batch = {'src_xyz': [torch.from_numpy(s).to(gpu) for s in src],
              'tgt_xyz': [torch.from_numpy(t).to(gpu) for t in tgt]}
@@ -171,8 +175,9 @@ def test_bf16_forward_3dlomatch_vs_oracle(gpu, bf16_mode, n_points):
     errs = {k: rel_err(out[k][0], ref[k][0]) for k in KEYS}
     p, pr = out['pose'].cpu().numpy()[-1, 0], ref['pose'].numpy()[-1, 0]
     rot, trans = _rot_deg(p, pr), float(np.linalg.norm(p[:, 3] - pr[:, 3]))
-    print(f'\nbf16 3dlomatch n={n_points}: rel errs', {k: f'{v:.2e}' for k, v in errs.items()},
-          f'rot {rot:.3e} deg trans {trans:.3e} m')
+    print(f'\nbf16 3dlomatch seed={seed} n={n_points}: rel errs',
+          {k: f'{v:.2e}' for k, v in errs.items()}, f'rot {rot:.3e} deg trans {trans:.3e} m')
     for k, v in errs.items():
         assert v < BF16_FEAT_TOL, (k, v)
     assert rot < BF16_ROT_DEG and trans < BF16_TRANS, (rot, trans)
+    assert max(errs.values()) > 1e-4            # really the bf16 mode, not the fp32-accurate path

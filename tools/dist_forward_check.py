@@ -2,8 +2,8 @@
 every rank runs fgreg.RegTR.forward on its shard of a ModelNet batch (fgreg.dist.shard_range),
 the per-pair poses are all-gathered (fgreg.dist.gather_pair_results, the bench's exchange),
 and rank 0 compares them with a single forward over the whole batch on the same weights.
-FGREG_DIST_BACKEND=gloo lets the ranks share one GPU (the 1-GPU box); nccl needs one GPU per
-rank. Exit status 0 = match."""
+FGREG_DIST_BACKEND=gloo lets the ranks share one GPU (the 1-GPU box); nccl (RCCL) needs one GPU
+per rank (tests/test_gpu_dist.py runs it at world size 1 on the 1-GPU box). Exit status 0 = match."""
 import os
 import sys
 
@@ -36,12 +36,16 @@ def main():
     T = lambda cl: [torch.from_numpy(c).to(dev) for c in cl]
     out = model({'src_xyz': T(src[b0:b1]), 'tgt_xyz': T(tgt[b0:b1])})
     poses = fdist.gather_pair_results(out['pose'], counts, pair_dim=1)
-    ok = torch.ones(1)
+    # the bench's other collective: max-over-ranks of the elapsed time (device tensor on RCCL)
+    el = torch.tensor([float(rank)], dtype=torch.float64, device=dev if backend == 'nccl' else 'cpu')
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    assert float(el.item()) == world - 1
+    ok = torch.ones(1, device=dev if backend == 'nccl' else 'cpu')
     if rank == 0:
         full = model({'src_xyz': T(src), 'tgt_xyz': T(tgt)})['pose']
         err = float((poses.cpu() - full.cpu()).abs().max())
-        print(f'world {world} backend {backend}: {B} pairs, shards {counts}, max |pose diff| {err:.3e}',
-              flush=True)
+        print(f'world {world} backend {dist.get_backend()}: {B} pairs, shards {counts}, '
+              f'gathered on {poses.device}, max |pose diff| {err:.3e}', flush=True)
         ok[0] = 1.0 if err < 1e-5 and poses.shape == full.shape else 0.0
     dist.broadcast(ok, 0)
     dist.destroy_process_group()
