@@ -731,7 +731,7 @@ extern "C" int fgr_layernorm_bwd_workspace(int64_t n, int32_t d, size_t* bytes) 
 extern "C" int fgr_layernorm_bwd(const float* x, int64_t n, int32_t d, const float* gamma, float eps,
                                  const float* dy, float* dx, float* dgamma_dbeta, void* ws,
                                  size_t ws_bytes, void* stream) {
-    FGR_REQUIRE(n >= 0 && d > 0 && d <= 1024 && d % 64 == 0, "fgr_layernorm_bwd: bad arguments (d %% 64 == 0, <= 1024)");
+    FGR_REQUIRE(n >= 0 && d > 0 && d <= 1024, "fgr_layernorm_bwd: bad arguments (0 < d <= 1024)");
     FGR_REQUIRE(gamma && dgamma_dbeta && ws && (n == 0 || (x && dy && dx)), "fgr_layernorm_bwd: null pointer");
     size_t need = 0;
     fgr_layernorm_bwd_workspace(n, d, &need);
@@ -745,12 +745,13 @@ extern "C" int fgr_layernorm_bwd(const float* x, int64_t n, int32_t d, const flo
     if (n == 0) {
         FGR_CHECK_HIP(hipMemsetAsync(part, 0, (size_t)2 * d * sizeof(float), st));
     } else {
-        const int per = d / 64;
+        int per = 1;
+        while (64 * per < d) per *= 2;
         switch (per) {
 #define LNB(P) case P: hipLaunchKernelGGL(layernorm_bwd_kernel<P>, dim3((unsigned)nb), dim3(256), 0, st, x, n, d, gamma, eps, dy, dx, part); break;
             LNB(1) LNB(2) LNB(4) LNB(8) LNB(16)
 #undef LNB
-            default: FGR_REQUIRE(false, "fgr_layernorm_bwd: d / 64 must be 1, 2, 4, 8 or 16");
+            default: FGR_REQUIRE(false, "fgr_layernorm_bwd: unsupported d");
         }
         FGR_CHECK_LAUNCH("layernorm_bwd_kernel");
     }
@@ -770,8 +771,9 @@ extern "C" int fgr_attention_bwd(const float* q, int64_t ldq, const float* k, in
                                  const int32_t* kv_seg, int32_t n_seg, int32_t n_kv_seg, int64_t nq,
                                  int64_t max_q_len, int64_t max_kv_len, int32_t nhead, int32_t dh,
                                  float scale, void* ws, size_t ws_bytes, void* stream) {
-    FGR_REQUIRE(n_seg > 0 && n_kv_seg > 0 && nhead > 0 && (dh == 32 || dh == 64) && nq >= 0,
-                "fgr_attention_bwd: bad arguments (head dim 32 / 64)");
+    FGR_REQUIRE(n_seg > 0 && n_kv_seg > 0 && nhead > 0 && nq >= 0 &&
+                    (dh == 4 || dh == 8 || dh == 16 || dh == 32 || dh == 64),
+                "fgr_attention_bwd: bad arguments (head dim 4 / 8 / 16 / 32 / 64)");
     FGR_REQUIRE(q && k && v && o && dout && dq && dk && dv && q_off && kv_off && kv_seg && ws,
                 "fgr_attention_bwd: null pointer");
     size_t need = 0;
@@ -783,14 +785,14 @@ extern "C" int fgr_attention_bwd(const float* q, int64_t ldq, const float* k, in
               (float*)ws + std::max<int64_t>(nq, 1) * nhead};
     hipStream_t st = as_stream(stream);
     dim3 g1((unsigned)(n_seg * a.q_blocks), nhead), g2((unsigned)(n_kv_seg * a.kv_blocks), nhead);
-    if (dh == 32) {
-        hipLaunchKernelGGL(attn_bwd_dq_kernel<32>, g1, dim3(64), 0, st, a);
-        FGR_CHECK_LAUNCH("attn_bwd_dq_kernel");
-        hipLaunchKernelGGL(attn_bwd_dkdv_kernel<32>, g2, dim3(64), 0, st, a);
-    } else {
-        hipLaunchKernelGGL(attn_bwd_dq_kernel<64>, g1, dim3(64), 0, st, a);
-        FGR_CHECK_LAUNCH("attn_bwd_dq_kernel");
-        hipLaunchKernelGGL(attn_bwd_dkdv_kernel<64>, g2, dim3(64), 0, st, a);
+    switch (dh) {
+#define ATB(D) case D: \
+        hipLaunchKernelGGL(attn_bwd_dq_kernel<D>, g1, dim3(64), 0, st, a); \
+        FGR_CHECK_LAUNCH("attn_bwd_dq_kernel"); \
+        hipLaunchKernelGGL(attn_bwd_dkdv_kernel<D>, g2, dim3(64), 0, st, a); \
+        break;
+        ATB(4) ATB(8) ATB(16) ATB(32) ATB(64)
+#undef ATB
     }
     FGR_CHECK_LAUNCH("attn_bwd_dkdv_kernel");
     return FGR_OK;

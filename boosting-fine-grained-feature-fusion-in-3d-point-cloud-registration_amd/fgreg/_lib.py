@@ -93,6 +93,22 @@ SIGNATURES = {
     'fgr_procrustes': [_vp, _vp, _vp, _i64, _i64, _f32, _vp, _vp],
     'fgr_time_next_call': [_vp, _vp],
     'fgr_pair_pose': [_vp, _vp, _vp, _i64, _vp, _i32, _i32, _f32, _vp, _vp],
+    'fgr_kpconv_scatter': [_vp, _vp, _i64, _i64, _vp, _i32, _vp, _i32, _vp, _i32, _f32, _vp, _vp],
+    'fgr_max_pool_bwd': [_vp, _i64, _i32, _vp, _i64, _i32, _vp, _vp, _vp],
+    'fgr_segnorm_workspace': [_i64, _i32, _i32, ctypes.POINTER(_sz)],
+    'fgr_segnorm_stats': [_vp, _i64, _i32, _vp, _i32, _i64, _vp, _f32, _vp, _vp, _vp, _vp, _sz, _vp],
+    'fgr_segnorm_apply': [_vp, _i64, _i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _i32, _vp,
+                          _vp],
+    'fgr_segnorm_bwd': [_vp, _i64, _i32, _vp, _i32, _i64, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32,
+                        _vp, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp],
+    'fgr_colsum_workspace': [_i64, _i32, ctypes.POINTER(_sz)],
+    'fgr_colsum': [_vp, _i64, _i32, _i64, _vp, _vp, _sz, _vp],
+    'fgr_layernorm_bwd_workspace': [_i64, _i32, ctypes.POINTER(_sz)],
+    'fgr_layernorm_bwd': [_vp, _i64, _i32, _vp, _f32, _vp, _vp, _vp, _vp, _sz, _vp],
+    'fgr_attention_bwd_workspace': [_i64, _i32, ctypes.POINTER(_sz)],
+    'fgr_attention_bwd': [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64,
+                          _vp, _i64, _vp, _vp, _vp, _i32, _i32, _i64, _i64, _i64, _i32, _i32, _f32,
+                          _vp, _sz, _vp],
     'fgr_crop_max_points': [ctypes.POINTER(_i32)],
     'fgr_crop_pairs_mask': [_vp, _i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     'fgr_crop_pairs_assemble': [_vp, _i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp,

@@ -1,0 +1,310 @@
+"""Differentiable ops of the training forward (train.py's
+``training_step`` -> ``loss.backward()`` -> ``clip_grad_norm_``, trainer.py:110-125).
+
+Each op is a ``torch.autograd.Function`` whose forward AND backward run in libfgreg:
+
+* ``linear_t``      y = act(x W^T + b) (+ residual): forward on fgr_gemm_f16x3 (bf16 in the
+                    bf16 mode); backward dX = dY W on the same GEMM with the transposed weight
+                    image, dW = dY^T X on the GEMM with X as the (transposed) weight image,
+                    db = fgr_colsum(dY);
+* ``kpconv_t``      the KPConv gather-weight + weight product (finegrained_kpconv_blocks.py:
+                    265-399 up to the division, which the following norm applies): backward
+                    d_wf = dout W2^T (GEMM), dW = wf^T dout (GEMM; wf regathered, not kept),
+                    dx = fgr_kpconv_scatter(d_wf) (the scatter-add of the reference's
+                    ``gather(method=2)``, :66-97);
+* ``segnorm_t``     per-(segment, channel) normalisation with batch statistics
+                    (fgr_segnorm_*): InstanceNorm per cloud (BatchNormBlock, :462-518) and the
+                    Res2Net BatchNorm1d in train() (res2net.py:126-159, one segment + affine,
+                    running statistics updated like nn.BatchNorm1d);
+* ``layernorm_t``   nn.LayerNorm (+ the positional add) -> fgr_layernorm / fgr_layernorm_bwd;
+* ``attention_t``   the packed-segment MHA core on the fused QKV tensor -> fgr_attention_f16x3
+                    forward, fgr_attention_bwd backward;
+* ``max_pool_t``    max_pool (:125-141) -> fgr_max_pool / fgr_max_pool_bwd.
+Elementwise glue between them (ReLU masks, the bottleneck's LeakyReLU(x + shortcut),
+concatenation) is torch on the same device. No CPU path: every op raises on host tensors.
+"""
+import math
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib, ops
+from .linear import linear
+from .ops import ACT_LEAKY, ACT_NONE, ACT_RELU, _c, _dev, _ptr, _stream
+
+
+def colsum(x: torch.Tensor) -> torch.Tensor:
+    """Column sums of a (n, c) tensor with unit column stride (fgr_colsum, fp64 partials)."""
+    _dev(x)
+    assert x.dim() == 2 and x.stride(1) == 1 and x.dtype == torch.float32
+    n, c = x.shape
+    out = torch.empty((c,), dtype=torch.float32, device=x.device)
+    L = _lib.load()
+    nb = _lib._sz(0)
+    _lib.check(L.fgr_colsum_workspace(n, c, nb), 'fgr_colsum_workspace')
+    ws = torch.empty(nb.value, dtype=torch.uint8, device=x.device)
+    _lib.check(L.fgr_colsum(_ptr(x), n, c, max(x.stride(0), c), _ptr(out), _ptr(ws), nb.value,
+                            _stream()), 'fgr_colsum')
+    return out
+
+
+def _relu_mask(dy, y):
+    return torch.where(y > 0, dy, torch.zeros_like(dy))
+
+
+# ------------------------------------------------------------------------------------------
+# dense layers
+# ------------------------------------------------------------------------------------------
+class _LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, residual, act):
+        assert act in (ACT_NONE, ACT_RELU)
+        y = linear(x, w, b, act=act, residual=residual)
+        ctx.act, ctx.has_b, ctx.has_r = act, b is not None, residual is not None
+        ctx.save_for_backward(x, w, y if act == ACT_RELU else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, y = ctx.saved_tensors
+        dy = dy.contiguous()
+        if ctx.act == ACT_RELU:
+            dy = _relu_mask(dy, y)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = linear(dy, w, transpose=True, tag='bwd_dx')          # dY W
+        if ctx.needs_input_grad[1]:
+            dw = linear(dy.t().contiguous(), x, transpose=True, cache=False)   # dY^T X
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            db = colsum(dy)
+        dres = dy if ctx.has_r and ctx.needs_input_grad[3] else None
+        return dx, dw, db, dres, None
+
+
+def linear_t(x, w, b=None, act=ACT_NONE, residual=None):
+    """act(x W^T + b) (+ residual after the activation is NOT supported: residual is added
+    before, as the transformer's out-projection / FFN epilogues use it with act NONE)."""
+    assert residual is None or act == ACT_NONE
+    return _LinearFn.apply(x, w, b, residual, act)
+
+
+# ------------------------------------------------------------------------------------------
+# KPConv
+# ------------------------------------------------------------------------------------------
+class _KPConvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, W, q, s, idx, kp, extent):
+        wf, nnorm = ops.kpconv_gather(q, s, idx, x, kp, extent)
+        out = linear(wf.view(wf.shape[0], -1), W, transpose=True)
+        ctx.extent = float(extent)
+        ctx.save_for_backward(x, W, q, s, idx, kp)
+        ctx.mark_non_differentiable(nnorm)
+        return out, nnorm
+
+    @staticmethod
+    def backward(ctx, dout, _dnnorm):
+        x, W, q, s, idx, kp = ctx.saved_tensors
+        dout = dout.contiguous()
+        nq = q.shape[0]
+        K, cin, cout = W.shape
+        dx = dW = None
+        if ctx.needs_input_grad[0]:
+            dwf = linear(dout, W, transpose='flat', tag='bwd_dwf')           # (nq, K * cin)
+            dx = torch.zeros_like(x)
+            _dev(q, s, idx, dwf, kp, dx)
+            _lib.check(_lib.load().fgr_kpconv_scatter(
+                _ptr(_c(q, torch.float32)), _ptr(_c(s, torch.float32)), nq, s.shape[0],
+                _ptr(_c(idx, torch.int64)), idx.shape[1], _ptr(dwf), cin, _ptr(_c(kp, torch.float32)),
+                K, ctx.extent, _ptr(dx), _stream()), 'fgr_kpconv_scatter')
+        if ctx.needs_input_grad[1]:
+            wf, _ = ops.kpconv_gather(q, s, idx, x, kp, ctx.extent)          # regathered
+            dWt = linear(dout.t().contiguous(), wf.view(nq, K * cin), transpose=True, cache=False)
+            dW = dWt.t().reshape(K, cin, cout)                               # (dout^T wf)^T
+        return dx, dW, None, None, None, None, None
+
+
+def kpconv_t(conv, q, s, idx, x):
+    """-> (sum_k WF_k W_k (Nq, Cout), nnorm (Nq,)) of a fgreg.backbone.KPConv, differentiable in
+    x and the weights (kernel points are fixed, as requires_grad=False in the reference)."""
+    return _KPConvFn.apply(x, conv.weights, q, s, idx, conv.kernel_points, conv.KP_extent)
+
+
+class _MaxPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, idx):
+        ctx.save_for_backward(x, idx)
+        return ops.max_pool(x, idx)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, idx = ctx.saved_tensors
+        dy = dy.contiguous()
+        dx = torch.zeros_like(x)
+        _lib.check(_lib.load().fgr_max_pool_bwd(_ptr(x.contiguous()), x.shape[0], x.shape[1],
+                                                _ptr(idx.contiguous()), idx.shape[0], idx.shape[1],
+                                                _ptr(dy), _ptr(dx), _stream()), 'fgr_max_pool_bwd')
+        return dx, None
+
+
+def max_pool_t(x, idx):
+    return _MaxPoolFn.apply(x, idx)
+
+
+# ------------------------------------------------------------------------------------------
+# normalisation
+# ------------------------------------------------------------------------------------------
+def _seg_ws(max_len, c, n_seg, extra=0, device=None):
+    nb = _lib._sz(0)
+    _lib.check(_lib.load().fgr_segnorm_workspace(max_len, c, n_seg, nb), 'fgr_segnorm_workspace')
+    return torch.empty(nb.value + extra, dtype=torch.uint8, device=device)
+
+
+class _SegNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, residual, row_div, seg_off, lengths, act, post_act, eps, stats):
+        x = _c(x, torch.float32)
+        _dev(x, gamma, beta, residual, row_div, seg_off)
+        n, c = x.shape
+        n_seg = len(lengths)
+        max_len = max(lengths) if n_seg else 0
+        assert seg_off.numel() == n_seg + 1 and sum(lengths) == n
+        L = _lib.load()
+        mean = torch.empty((n_seg, c), dtype=torch.float32, device=x.device)
+        rstd, var = torch.empty_like(mean), torch.empty_like(mean)
+        ws = _seg_ws(max_len, c, n_seg, device=x.device)
+        rd = _c(row_div, torch.float32) if row_div is not None else None
+        _lib.check(L.fgr_segnorm_stats(_ptr(x), n, c, _ptr(seg_off), n_seg, max_len, _ptr(rd),
+                                       float(eps), _ptr(mean), _ptr(rstd), _ptr(var), _ptr(ws),
+                                       ws.numel(), _stream()), 'fgr_segnorm_stats')
+        res = _c(residual, torch.float32) if residual is not None else None
+        y = torch.empty_like(x)
+        _lib.check(L.fgr_segnorm_apply(_ptr(x), n, c, _ptr(seg_off), n_seg, _ptr(rd), _ptr(mean),
+                                       _ptr(rstd), _ptr(gamma), _ptr(beta), act, _ptr(res), post_act,
+                                       _ptr(y), _stream()), 'fgr_segnorm_apply')
+        if stats is not None:
+            stats.append((mean, var, n))
+        ctx.meta = (n, c, n_seg, max_len, act, post_act, residual is not None, gamma is not None)
+        ctx.save_for_backward(x, gamma, beta, rd, seg_off, mean, rstd, y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, gamma, beta, rd, seg_off, mean, rstd, y = ctx.saved_tensors
+        n, c, n_seg, max_len, act, post_act, has_r, affine = ctx.meta
+        dy = _c(dy, torch.float32)
+        dx = torch.empty_like(x)
+        dres = torch.empty_like(x) if has_r else None
+        dg = torch.empty((c,), dtype=torch.float32, device=x.device) if affine else None
+        db = torch.empty_like(dg) if affine else None
+        ws = _seg_ws(max_len, c, n_seg, extra=8 * n_seg * c, device=x.device)
+        _lib.check(_lib.load().fgr_segnorm_bwd(
+            _ptr(x), n, c, _ptr(seg_off), n_seg, max_len, _ptr(rd), _ptr(mean), _ptr(rstd),
+            _ptr(gamma), _ptr(beta), act, int(has_r), post_act, _ptr(y), _ptr(dy), _ptr(dx),
+            _ptr(dres), _ptr(dg), _ptr(db), _ptr(ws), ws.numel(), _stream()), 'fgr_segnorm_bwd')
+        return dx, dg, db, dres, None, None, None, None, None, None, None
+
+
+def segnorm_t(x, off, lengths, row_div=None, act=ACT_NONE, residual=None, post_act=ACT_NONE,
+              gamma=None, beta=None, eps=1e-5, stats=None):
+    """post(act((x / row_div - mean) rstd (* gamma + beta)) + residual), statistics per segment
+    of the current batch; ``stats`` (a list) receives (mean, biased var, rows)."""
+    return _SegNormFn.apply(x, gamma, beta, residual, row_div, off, list(lengths), act, post_act,
+                            eps, stats)
+
+
+def batchnorm_t(bn, x, act=ACT_NONE, residual=None, post_act=ACT_NONE):
+    """nn.BatchNorm1d ``bn`` in training mode on (N, C) rows (batch statistics over all rows,
+    running statistics updated in place as torch does: momentum, unbiased variance)."""
+    n = x.shape[0]
+    off = torch.tensor([0, n], dtype=torch.int64, device=x.device)
+    stats = [] if bn.track_running_stats else None
+    y = segnorm_t(x, off, [n], act=act, residual=residual, post_act=post_act, gamma=bn.weight,
+                  beta=bn.bias, eps=bn.eps, stats=stats)
+    if stats:
+        mean, var, rows = stats[0]
+        with torch.no_grad():
+            bn.num_batches_tracked.add_(1)
+            m = bn.momentum if bn.momentum is not None else 1.0 / float(bn.num_batches_tracked)
+            unbiased = var[0] * (rows / max(rows - 1, 1))
+            bn.running_mean.mul_(1 - m).add_(mean[0], alpha=m)
+            bn.running_var.mul_(1 - m).add_(unbiased, alpha=m)
+    return y
+
+
+class _LayerNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, add, eps):
+        x = _c(x, torch.float32)
+        y = ops.layernorm(x, gamma, beta, eps, add=add)
+        ctx.eps = float(eps)
+        ctx.has_add = add is not None
+        ctx.save_for_backward(x, gamma)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, gamma = ctx.saved_tensors
+        dy = _c(dy, torch.float32)
+        n, d = x.shape
+        dx = torch.empty_like(x)
+        dgb = torch.empty((2 * d,), dtype=torch.float32, device=x.device)
+        L = _lib.load()
+        nb = _lib._sz(0)
+        _lib.check(L.fgr_layernorm_bwd_workspace(n, d, nb), 'fgr_layernorm_bwd_workspace')
+        ws = torch.empty(nb.value, dtype=torch.uint8, device=x.device)
+        _lib.check(L.fgr_layernorm_bwd(_ptr(x), n, d, _ptr(gamma.contiguous()), ctx.eps, _ptr(dy),
+                                       _ptr(dx), _ptr(dgb), _ptr(ws), nb.value, _stream()),
+                   'fgr_layernorm_bwd')
+        dadd = dy if ctx.has_add and ctx.needs_input_grad[3] else None
+        return dx, dgb[:d], dgb[d:], dadd, None
+
+
+def layernorm_t(x, norm, add=None):
+    """nn.LayerNorm ``norm`` of x (+ add, e.g. the positional embedding)."""
+    return _LayerNormFn.apply(x, norm.weight, norm.bias, add, norm.eps)
+
+
+# ------------------------------------------------------------------------------------------
+# attention
+# ------------------------------------------------------------------------------------------
+class _AttentionFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, off, kv_seg, max_len, nhead):
+        qkv = _c(qkv, torch.float32)
+        d = qkv.shape[1] // 3
+        o = ops.attention(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], off, off, kv_seg, max_len,
+                          nhead)
+        ctx.meta = (d, int(max_len), int(nhead))
+        ctx.save_for_backward(qkv, o, off, kv_seg)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, o, off, kv_seg = ctx.saved_tensors
+        d, max_len, nhead = ctx.meta
+        do = _c(do, torch.float32)
+        n = qkv.shape[0]
+        dh = d // nhead
+        dqkv = torch.empty_like(qkv)
+        L = _lib.load()
+        nb = _lib._sz(0)
+        _lib.check(L.fgr_attention_bwd_workspace(n, nhead, nb), 'fgr_attention_bwd_workspace')
+        ws = torch.empty(nb.value, dtype=torch.uint8, device=qkv.device)
+        p, dp, ld = qkv.data_ptr(), dqkv.data_ptr(), qkv.stride(0)
+        n_seg = off.numel() - 1
+        _lib.check(L.fgr_attention_bwd(
+            p, ld, p + 4 * d, ld, p + 8 * d, ld, _ptr(o), o.stride(0), _ptr(do), do.stride(0),
+            dp, ld, dp + 4 * d, ld, dp + 8 * d, ld, _ptr(off), _ptr(off), _ptr(kv_seg), n_seg,
+            n_seg, n, max_len, max_len, nhead, dh, float(math.sqrt(1.0 / float(dh))), _ptr(ws),
+            nb.value, _stream()), 'fgr_attention_bwd')
+        return dqkv, None, None, None, None
+
+
+def attention_t(qkv, off, kv_seg, max_len, nhead):
+    """Packed-segment MHA core on a fused (N, 3d) [q | k | v] tensor: query segment i attends
+    to key segment kv_seg[i] (self- or cross-attention over one segmentation)."""
+    return _AttentionFn.apply(qkv, off, kv_seg, max_len, nhead)
+
+
+def leaky(x):
+    return F.leaky_relu(x, 0.1)

@@ -13,9 +13,9 @@ The compute path is:
 * ``BatchNormBlock``    -- fgr_instnorm (per-cloud InstanceNorm1d, fused act/residual);
 * ``my_res2Net``        -- BatchNorm folded into the Linear weights (eval) + GEMMs.
 
-Forward only (inference). In training mode the Res2Net BatchNorms use batch
-statistics as in the reference, but no custom backward exists for the KPConv
-kernels.
+This module holds the inference forward; the training forward (Res2Net BatchNorm on batch
+statistics, every op differentiable on libfgreg's backward kernels) composes the same modules
+in fgreg/training.py.
 """
 import math
 import os
@@ -328,8 +328,9 @@ class my_Bottle2neck(nn.Module):  # noqa: N801 -- reference name (res2net.py:84)
         """-> relu(bn3(conv3(cat)) + downsample(x)); with ``shortcut`` (the enclosing
         bottleneck block's identity shortcut) -> LeakyReLU_0.1(that + shortcut), fused into
         the last GEMM's epilogue (finegrained_kpconv_blocks.py:715-725)."""
-        if self.training:
-            y = self._forward_train(x)
+        if self.training:       # batch statistics, differentiable (fgreg/training.py)
+            from .training import bottle2neck_train
+            y = bottle2neck_train(self, x)
             return y if shortcut is None else F.leaky_relu(y + shortcut, 0.1)
         w1, b1, ws, w3d, b3d, chain = self._folded_params()
         out = linear(x, w1, b1, act=ops.ACT_RELU)
@@ -374,20 +375,6 @@ class my_Bottle2neck(nn.Module):  # noqa: N801 -- reference name (res2net.py:84)
         else:
             y = (torch.addmm(b3d, cat_in, w3d.t()) + x).relu_()
         return y if shortcut is None else F.leaky_relu(y + shortcut, 0.1)
-
-    def _forward_train(self, x):
-        out = F.relu(self.bn1(self.conv1(x)))
-        spx = torch.split(out, self.width, 1)
-        outs, sp = [], None
-        for i in range(self.nums):
-            sp = spx[i] if i == 0 else sp + spx[i]
-            sp = F.relu(self.bns[i](self.convs[i](sp)))
-            outs.append(sp)
-        if self.scale != 1:
-            outs.append(spx[self.nums])
-        out = self.bn3(self.conv3(torch.cat(outs, 1)))
-        residual = self.downsample(x) if self.downsample is not None else x
-        return F.relu(out + residual)
 
 
 class my_res2Net(nn.Module):  # noqa: N801 -- reference name (res2net.py:231)

@@ -138,7 +138,10 @@ def split_weight3(w: torch.Tensor, transpose=False, tag=None, kind=3, cache=True
     ent = _CACHE.get(ck) if cache else None
     if not _valid(ent, w):
         cls = _IMAGE[kind]
-        if transpose:                    # (K, Cin, Cout) as W[n = cout][k = K*Cin + cin]
+        if transpose == 'flat':          # (..., k) as W[n = leading index][k = last index]
+            w2 = w.reshape(-1, w.shape[-1]).contiguous()
+            ent = cls(w2, w2.shape[0], w2.shape[1], w2.shape[1], 1, w)
+        elif transpose:                  # (K, Cin, Cout) as W[n = cout][k = K*Cin + cin]
             w2 = w.reshape(-1, w.shape[-1]).contiguous()
             ent = cls(w2, w2.shape[1], w2.shape[0], 1, w2.shape[1], w)
         else:
@@ -186,12 +189,17 @@ def _linear_rows(x, w, bias, act, residual, tag, out, ln, add, cache):
 def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act=ACT_NONE, residual=None,
            transpose=False, tag=None, out=None, ln=None, add=None, cache=True) -> torch.Tensor:
     """act(A @ W^T + bias (+ residual)), W = w (n, k), or W = w.reshape(k, n).t() if
-    transpose (e.g. KPConv weights (K, Cin, Cout) used as (K*Cin, Cout)); A = x, or
+    transpose (e.g. KPConv weights (K, Cin, Cout) used as (K*Cin, Cout)), or W =
+    w.reshape(-1, w.shape[-1]) if transpose == 'flat' (the backward's d_wf = dout W2^T); A = x, or
     A = ln(x) (+ add) for an nn.LayerNorm ``ln`` and / or an added tensor ``add`` (fused into
     the GEMM's row loads where fgr_gemm_rows_f16x3 applies). ACT_RELU_RES_LEAKY applies the
     residual after the ReLU: LeakyReLU_0.1(ReLU(A @ W^T + bias) + residual)."""
-    n = w.shape[-1] if transpose else w.shape[0]
-    k = w.numel() // n if transpose else w.shape[1]
+    if transpose == 'flat':
+        k = w.shape[-1]
+        n = w.numel() // k
+    else:
+        n = w.shape[-1] if transpose else w.shape[0]
+        k = w.numel() // n if transpose else w.shape[1]
     assert x.dim() == 2 and x.shape[1] == k and x.dtype == torch.float32
     if not x.is_cuda:
         _dev(x)
@@ -211,6 +219,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act=ACT_NONE, residual=N
         y = F.leaky_relu(y + residual, 0.1)
         return out.copy_(y) if out is not None else y
     if MODE in ('bf16x6', 'f16x3', 'bf16'):
+        if x.shape[0] == 1 and x.stride(1) == 1 and x.stride(0) != k:
+            x = x.as_strided(x.shape, (k, 1))      # a 1-row view's row stride is arbitrary
         if not (x.stride(1) == 1 and (k % 8 != 0 or (x.stride(0) % 4 == 0
                                                      and x.data_ptr() % 16 == 0))):
             x = x.contiguous()                 # the split kernels need 16-B aligned rows
@@ -240,10 +250,10 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act=ACT_NONE, residual=N
                 _stream()), 'fgr_gemm_' + MODE)
         _end('gemm', t0, 2 * m * n * k)
         return out
-    ok = (MODE == 'bf16x3' and k % 4 == 0 and x.stride(1) == 1
+    ok = (MODE == 'bf16x3' and transpose != 'flat' and k % 4 == 0 and x.stride(1) == 1
           and x.stride(0) % 4 == 0 and x.data_ptr() % 16 == 0)
     if not ok:
-        W = w.reshape(k, n) if transpose else w.t()
+        W = w.reshape(n, k).t() if transpose == 'flat' else (w.reshape(k, n) if transpose else w.t())
         if residual is not None:
             y = torch.addmm(residual, x, W)
             if bias is not None:

@@ -138,15 +138,17 @@ class RegTR(nn.Module):
         self.pose_threshold = 0.85   # hard-coded in fast_compute_rigid_transform (se3_torch.py:226)
 
     def forward(self, batch):
-        # The guard runs before entering no_grad (a @torch.no_grad() decorator would make
-        # is_grad_enabled() always False here and the check dead).
-        if self.training and torch.is_grad_enabled():
-            raise NotImplementedError(
-                'fgreg.RegTR.forward is the inference forward (eval(), no autograd); training '
-                'mode with gradients (train.py) is not implemented -- call model.eval() or run '
-                'under torch.no_grad()')
+        """eval(): the inference forward (no autograd, HIP-graph replay of the core).
+        train(): the training forward (fgreg/training.py): Res2Net BatchNorm on batch
+        statistics and, with autograd enabled, differentiable end to end on libfgreg's forward
+        and backward kernels (train.py's loss.backward())."""
         dev = batch['src_xyz'][0].device
-        if dev.type != 'cuda':          # the ops raise FgrError on host tensors (no CPU path)
+        if self.training:
+            if dev.type != 'cuda':      # the ops raise FgrError on host tensors (no CPU path)
+                return self._forward(batch, train=True)
+            with torch.cuda.device(dev):
+                return self._forward(batch, train=True)
+        if dev.type != 'cuda':
             with torch.no_grad():
                 return self._forward(batch)
         with torch.no_grad(), torch.cuda.device(dev):
@@ -160,23 +162,26 @@ class RegTR(nn.Module):
             host_layout(meta, lvl)
         return meta
 
-    def _forward(self, batch, meta=None):
+    def _forward(self, batch, meta=None, train=False):
         """meta: a kpconv_meta already prepared for this batch (fgreg.pipeline), else built
-        here."""
+        here. train: the training-mode core (fgreg/training.py) instead of the inference one."""
         B = len(batch['src_xyz'])
         if meta is None:
-            meta = self._prepare(batch)
+            with torch.no_grad():
+                meta = self._prepare(batch)
         batch['kpconv_meta'] = meta
         n_lvl = len(meta['points'])
         slens_c, _ = host_layout(meta, n_lvl - 1)
         xyz_c = meta['points'][-1]
-        core = None
-        if GRAPHS and xyz_c.is_cuda and ops.TIMER is None:
-            core = _graph_for(self, meta, slens_c, B)
-        if core is not None:
-            both, feats, corr, logits, pose = core.run(meta)
+        if train:
+            from .training import core_train
+            res = core_train(self, meta, self._segments(slens_c, xyz_c), B)
         else:
-            both, feats, corr, logits, pose = self._core(meta, self._segments(slens_c, xyz_c), B)
+            core = (_graph_for(self, meta, slens_c, B)
+                    if GRAPHS and xyz_c.is_cuda and ops.TIMER is None else None)
+            res = core.run(meta) if core is not None else self._core(
+                meta, self._segments(slens_c, xyz_c), B)
+        both, feats, corr, logits, pose = res
 
         offs = [0]
         for n in slens_c:

@@ -472,6 +472,64 @@ int fgr_crop_pairs_assemble(const float* raw, int32_t ld, const int64_t* offsets
                             const double* noise, const float* rt, int32_t m, float* xyz,
                             uint8_t* overlap, int64_t* corr, int32_t* n_corr, void* stream);
 
+/* ---- Training backward (train.py -> trainer.py:110-125 backward) -------
+ * The dense products' gradients run on the GEMM entry points above with transposed weight
+ * images (fgreg/autograd.py); these cover the rest. The two scatters add with fp32 global
+ * atomics (exact up to fp32 rounding, order may vary between runs); every reduction is
+ * deterministic (fixed-order fp64 partials).
+ *  fgr_kpconv_scatter   KPConv gather-weight backward: dx[idx[q,h], c] += sum_k w(q,h,k)
+ *                       dwf[q,k,c] with the forward's influences (finegrained_kpconv_blocks.py:
+ *                       296-381; the reference's gather(method=2), :66-97). dx is accumulated.
+ *  fgr_max_pool_bwd     max_pool (:125-141): dx[arg, c] += dy[q, c], arg = the row's first
+ *                       maximum (shadow entries read 0 and receive nothing). dx is accumulated.
+ *  fgr_segnorm_stats    per-(segment, channel) mean / rstd / biased var of v = x / row_div:
+ *                       InstanceNorm1d per cloud (:498-507) or BatchNorm1d batch statistics
+ *                       (one segment, res2net.py:126-159 in train()); workspace
+ *                       fgr_segnorm_workspace bytes.
+ *  fgr_segnorm_apply    out = post(act((v - mean) rstd (* gamma + beta)) + residual).
+ *  fgr_segnorm_bwd      its backward from (y = out, dy): dx, dres (= d residual), dgamma / dbeta
+ *                       (NULL without gamma); workspace fgr_segnorm_workspace + 8 n_seg c bytes.
+ *  fgr_layernorm_bwd    nn.LayerNorm backward (transformers.py:105-107): dx, and
+ *                       dgamma_dbeta[0..d) = sum dy xhat, [d..2d) = sum dy; d <= 1024.
+ *  fgr_colsum           out[c] = sum_r x[r, c] (fp64 partials; bias gradients).
+ *  fgr_attention_bwd    softmax attention backward over packed segments (the layout of
+ *                       fgr_attention*): dq, dk, dv (each may alias column slices of one
+ *                       tensor), head dim 4 / 8 / 16 / 32 / 64, fp32; key segments may be attended by any
+ *                       number of query segments. */
+int fgr_kpconv_scatter(const float* q, const float* s, int64_t nq, int64_t ns, const int64_t* idx,
+                       int32_t width, const float* dwf, int32_t cin, const float* kernel_points,
+                       int32_t n_kp, float extent, float* dx, void* stream);
+int fgr_max_pool_bwd(const float* x, int64_t ns, int32_t c, const int64_t* idx, int64_t nq,
+                     int32_t width, const float* dy, float* dx, void* stream);
+int fgr_segnorm_workspace(int64_t max_seg_len, int32_t c, int32_t n_seg, size_t* bytes);
+int fgr_segnorm_stats(const float* x, int64_t n, int32_t c, const int64_t* seg_off, int32_t n_seg,
+                      int64_t max_seg_len, const float* row_div, float eps, float* mean, float* rstd,
+                      float* var, void* ws, size_t ws_bytes, void* stream);
+int fgr_segnorm_apply(const float* x, int64_t n, int32_t c, const int64_t* seg_off, int32_t n_seg,
+                      const float* row_div, const float* mean, const float* rstd, const float* gamma,
+                      const float* beta, int32_t act, const float* residual, int32_t post_act,
+                      float* out, void* stream);
+int fgr_segnorm_bwd(const float* x, int64_t n, int32_t c, const int64_t* seg_off, int32_t n_seg,
+                    int64_t max_seg_len, const float* row_div, const float* mean, const float* rstd,
+                    const float* gamma, const float* beta, int32_t act, int32_t has_residual,
+                    int32_t post_act, const float* y, const float* dy, float* dx, float* dres,
+                    float* dgamma, float* dbeta, void* ws, size_t ws_bytes, void* stream);
+int fgr_colsum_workspace(int64_t n, int32_t c, size_t* bytes);
+int fgr_colsum(const float* x, int64_t n, int32_t c, int64_t ldx, float* out, void* ws,
+               size_t ws_bytes, void* stream);
+int fgr_layernorm_bwd_workspace(int64_t n, int32_t d, size_t* bytes);
+int fgr_layernorm_bwd(const float* x, int64_t n, int32_t d, const float* gamma, float eps,
+                      const float* dy, float* dx, float* dgamma_dbeta, void* ws, size_t ws_bytes,
+                      void* stream);
+int fgr_attention_bwd_workspace(int64_t nq, int32_t nhead, size_t* bytes);
+int fgr_attention_bwd(const float* q, int64_t ldq, const float* k, int64_t ldk, const float* v,
+                      int64_t ldv, const float* o, int64_t ldo, const float* dout, int64_t lddo,
+                      float* dq, int64_t lddq, float* dk, int64_t lddk, float* dv, int64_t lddv,
+                      const int64_t* q_off, const int64_t* kv_off, const int32_t* kv_seg,
+                      int32_t n_seg, int32_t n_kv_seg, int64_t nq, int64_t max_q_len,
+                      int64_t max_kv_len, int32_t nhead, int32_t dh, float scale, void* ws,
+                      size_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -21,6 +21,33 @@ import torch.nn.functional as F
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import geom  # noqa: E402
 
+# Optional trace of the distance of every activation input to its kink (ReLU / LeakyReLU at 0,
+# max-pool: gap between a row's two largest entries), relative to the tensor's max |value|:
+# a list to append (site, margin) to, or None. Gradients are discontinuous at those points,
+# so gradient parity between two fp32 implementations is only defined away from them
+# (tests/test_gpu_train.py).
+ACT_TRACE = None
+
+
+def _trace(site, z):
+    # exact zeros (an upstream ReLU's output, shadow rows) are excluded: every implementation
+    # produces them exactly and takes the same branch there
+    if ACT_TRACE is not None and z.numel():
+        za = z.detach().abs()
+        nz = za[za > 0]
+        if nz.numel():
+            ACT_TRACE.append((site, float(nz.min() / za.max())))
+
+
+def _relu(z, site='relu'):
+    _trace(site, z)
+    return F.relu(z)
+
+
+def _leaky(z, site='leaky'):
+    _trace(site, z)
+    return F.leaky_relu(z, 0.1)
+
 
 # ----------------------------------------------------------------------------------------
 # Preprocessing (models/backbone_kpconv/finegrained_kpconv.py:296-542)
@@ -95,7 +122,21 @@ def kpconv(q, s, idx, x, W, kp, extent):
 def max_pool(x, idx):
     """blocks:125-141: gather with an appended zero row, max over the row."""
     x = torch.cat([x, torch.zeros_like(x[:1])], 0)
-    return x[idx].max(1)[0]
+    g = x[idx]
+    if ACT_TRACE is not None and g.shape[1] > 1:
+        # candidates: the real entries and ONE zero standing for all shadow entries (ties
+        # among shadows carry no gradient); margin = gap between the two largest candidates
+        real = idx < x.shape[0] - 1
+        gd = g.detach()
+        cand = torch.where(real.unsqueeze(-1), gd, torch.full_like(gd, -math.inf))
+        shadow = torch.where((~real).any(1, keepdim=True), torch.zeros_like(gd[:, :1]),
+                             torch.full_like(gd[:, :1], -math.inf))
+        top = torch.cat([cand, shadow], 1).topk(2, dim=1)[0]
+        gap = torch.nan_to_num(top[:, 0] - top[:, 1], nan=math.inf)
+        gap = gap[gap > 0]                  # exact ties: the first entry wins everywhere
+        if gap.numel():
+            ACT_TRACE.append(('max_pool', float(gap.min() / gd.abs().max().clamp_min(1e-30))))
+    return g.max(1)[0]
 
 
 def instance_norm(x, lens, eps=1e-5):
@@ -110,7 +151,13 @@ def instance_norm(x, lens, eps=1e-5):
     return torch.cat(outs, 0)
 
 
-def _bn(sd, p, x, eps=1e-5):
+def _bn(sd, p, x, eps=1e-5, train=False):
+    """BatchNorm1d: eval on running statistics; train on the batch's (biased variance, all
+    rows of all clouds -- nn.BatchNorm1d.train(), res2net.py:126-159 in train.py)."""
+    if train:
+        mu = x.mean(0)
+        var = ((x - mu) ** 2).mean(0)
+        return (x - mu) / torch.sqrt(var + eps) * sd[p + '.weight'] + sd[p + '.bias']
     return ((x - sd[p + '.running_mean']) / torch.sqrt(sd[p + '.running_var'] + eps)
             * sd[p + '.weight'] + sd[p + '.bias'])
 
@@ -118,28 +165,30 @@ def _bn(sd, p, x, eps=1e-5):
 def unary(sd, p, x, lens, relu=True):
     """UnaryBlock (blocks:521-555): Linear(no bias) -> InstanceNorm -> LeakyReLU(0.1)."""
     x = instance_norm(x @ sd[p + '.mlp.weight'].t(), lens)
-    return F.leaky_relu(x, 0.1) if relu else x
+    return _leaky(x, p) if relu else x
 
 
-def res2net(sd, p, x, scale=8):
-    """my_res2Net / my_Bottle2neck, eval BatchNorm (res2net.py:126-159, 231-265)."""
+def res2net(sd, p, x, scale=8, train=False):
+    """my_res2Net / my_Bottle2neck (res2net.py:126-159, 231-265); BatchNorm on running
+    statistics (eval) or batch statistics (train)."""
     p = p + '.layer1.0'
-    out = F.relu(_bn(sd, p + '.bn1', x @ sd[p + '.conv1.weight'].t()))
+    out = _relu(_bn(sd, p + '.bn1', x @ sd[p + '.conv1.weight'].t(), train=train), p + '.bn1')
     width = sd[p + '.convs.0.weight'].shape[0]
     spx = torch.split(out, width, 1)
     outs = []
     sp = None
     for i in range(scale - 1):
         sp = spx[i] if i == 0 else sp + spx[i]
-        sp = F.relu(_bn(sd, f'{p}.bns.{i}', sp @ sd[f'{p}.convs.{i}.weight'].t()))
+        sp = _relu(_bn(sd, f'{p}.bns.{i}', sp @ sd[f'{p}.convs.{i}.weight'].t(), train=train),
+                   f'{p}.bns.{i}')
         outs.append(sp)
     outs.append(spx[scale - 1])
-    out = _bn(sd, p + '.bn3', torch.cat(outs, 1) @ sd[p + '.conv3.weight'].t())
-    res = _bn(sd, p + '.downsample.1', x @ sd[p + '.downsample.0.weight'].t())
-    return F.relu(out + res)
+    out = _bn(sd, p + '.bn3', torch.cat(outs, 1) @ sd[p + '.conv3.weight'].t(), train=train)
+    res = _bn(sd, p + '.downsample.1', x @ sd[p + '.downsample.0.weight'].t(), train=train)
+    return _relu(out + res, p + '.out')
 
 
-def encoder(cfg, sd, meta, feats0):
+def encoder(cfg, sd, meta, feats0, train=False):
     """KPFEncoder.forward (finegrained_kpconv.py:22-95) with block_decider's blocks."""
     r = cfg['first_subsampling_dl'] * cfg['conv_radius']
     layer = 0
@@ -158,17 +207,17 @@ def encoder(cfg, sd, meta, feats0):
         if block.startswith('simple'):                                         # blocks:620-634
             y = kpconv(q, s, idx, x, sd[p + '.KPConv.weights'], sd[p + '.KPConv.kernel_points'],
                        extent)
-            x = F.leaky_relu(instance_norm(y, lens_post), 0.1)
+            x = _leaky(instance_norm(y, lens_post), p)
         elif block.startswith('resnetb'):                                      # blocks:692-727
             y = unary(sd, p + '.unary1', x, lens_pre) if p + '.unary1.mlp.weight' in sd else x
             y = kpconv(q, s, idx, y, sd[p + '.KPConv.weights'], sd[p + '.KPConv.kernel_points'],
                        extent)
             y = instance_norm(y, lens_post)
-            y = F.leaky_relu(res2net(sd, p + '.res2net', y), 0.1)
+            y = _leaky(res2net(sd, p + '.res2net', y, train=train), p + '.res2net')
             sc = max_pool(x, idx) if strided else x
             if p + '.unary_shortcut.mlp.weight' in sd:
                 sc = unary(sd, p + '.unary_shortcut', sc, lens_post, relu=False)
-            x = F.leaky_relu(y + sc, 0.1)
+            x = _leaky(y + sc, p + '.out')
         else:
             raise NotImplementedError(block)
         if strided:
@@ -184,7 +233,7 @@ def sine_pos_embed(xyz, d_model, temperature=10000, scale=1.0):
     """PositionEmbeddingCoordsSine.forward (position_embedding.py:29-49), n_dim=3."""
     npf = d_model // 3 // 2 * 2
     pad = d_model - npf * 3
-    dim_t = torch.arange(npf, dtype=torch.float32)
+    dim_t = torch.arange(npf, dtype=xyz.dtype)
     dim_t = temperature ** (2 * torch.div(dim_t, 2, rounding_mode='trunc') / npf)
     pd = (xyz * (scale * 2 * math.pi)).unsqueeze(-1) / dim_t
     emb = torch.stack([pd[..., 0::2].sin(), pd[..., 1::2].cos()], -1).reshape(*xyz.shape[:-1], -1)
@@ -206,7 +255,7 @@ def mha(sd, p, q, k, v, kmask, nhead):
     qh = qp.reshape(Lq, B * nhead, dh).transpose(0, 1) * (1.0 / math.sqrt(dh))
     kh = kp_.reshape(Lk, B * nhead, dh).transpose(0, 1)
     vh = vp.reshape(Lk, B * nhead, dh).transpose(0, 1)
-    mask = torch.zeros(B, Lk).masked_fill(kmask, float('-inf'))
+    mask = torch.zeros(B, Lk, dtype=q.dtype).masked_fill(kmask, float('-inf'))
     mask = mask.repeat_interleave(nhead, 0).unsqueeze(1)
     att = torch.softmax(torch.baddbmm(mask, qh, kh.transpose(1, 2)), -1)
     o = torch.bmm(att, vh).transpose(0, 1).reshape(Lq, B, d)
@@ -230,14 +279,15 @@ def cross_encoder_layer(sd, p, src, tgt, smask, tmask, spos, tpos, nhead):
     src, tgt = src + s3, tgt + t3
 
     def ffn(x):
-        h = F.relu(_ln(sd, p + '.norm3', x) @ sd[p + '.linear1.weight'].t() + sd[p + '.linear1.bias'])
+        h = _relu(_ln(sd, p + '.norm3', x) @ sd[p + '.linear1.weight'].t() + sd[p + '.linear1.bias'],
+                  p + '.ffn')
         return x + h @ sd[p + '.linear2.weight'].t() + sd[p + '.linear2.bias']
     return ffn(src), ffn(tgt)
 
 
 def _pad(seqs):
     n = max(len(s) for s in seqs)
-    out = torch.zeros(n, len(seqs), seqs[0].shape[-1])
+    out = torch.zeros(n, len(seqs), seqs[0].shape[-1], dtype=seqs[0].dtype)
     mask = torch.ones(len(seqs), n, dtype=torch.bool)
     for b, s in enumerate(seqs):
         out[:len(s), b] = s
@@ -271,12 +321,24 @@ def weighted_procrustes(a, b, w, threshold=0.85):
 # ----------------------------------------------------------------------------------------
 @torch.no_grad()
 def forward(cfg, sd, src_xyz, tgt_xyz, meta=None, mode=geom.INDEX):
+    """The inference forward (eval(), no autograd)."""
+    return _forward(cfg, sd, src_xyz, tgt_xyz, meta, mode, train=False)
+
+
+def forward_train(cfg, sd, src_xyz, tgt_xyz, meta=None, mode=geom.INDEX):
+    """The training-mode forward (model.train(), autograd on): Res2Net BatchNorm on batch
+    statistics; differentiable in every state_dict tensor that requires grad (the pose is
+    computed without gradients, as no loss reads it, finegrained_regtr.py:252-309)."""
+    return _forward(cfg, sd, src_xyz, tgt_xyz, meta, mode, train=True)
+
+
+def _forward(cfg, sd, src_xyz, tgt_xyz, meta, mode, train):
     B = len(src_xyz)
     if meta is None:
         meta = preprocess(cfg, [np.asarray(c) for c in list(src_xyz) + list(tgt_xyz)], mode)
     slens_c = meta['stack_lengths'][-1].tolist()
     feats0 = torch.ones_like(meta['points'][0][:, :1])                         # :126
-    feats_un = encoder(cfg, sd, meta, feats0)
+    feats_un = encoder(cfg, sd, meta, feats0, train=train)
     both = feats_un @ sd['feat_proj.weight'].t() + sd['feat_proj.bias']       # :149
     src_f, tgt_f = torch.split(both, slens_c)[:B], torch.split(both, slens_c)[B:]
     xyz_c = meta['points'][-1]
@@ -297,10 +359,10 @@ def forward(cfg, sd, src_xyz, tgt_xyz, meta=None, mode=geom.INDEX):
     s_cond, t_cond = torch.stack(s_int), torch.stack(t_int)
 
     def corr_mlp(x):                                                           # :411-455
-        h = F.relu(x @ sd['correspondence_decoder.coor_mlp.0.weight'].t()
-                   + sd['correspondence_decoder.coor_mlp.0.bias'])
-        h = F.relu(h @ sd['correspondence_decoder.coor_mlp.2.weight'].t()
-                   + sd['correspondence_decoder.coor_mlp.2.bias'])
+        h = _relu(x @ sd['correspondence_decoder.coor_mlp.0.weight'].t()
+                  + sd['correspondence_decoder.coor_mlp.0.bias'], 'coor_mlp.0')
+        h = _relu(h @ sd['correspondence_decoder.coor_mlp.2.weight'].t()
+                  + sd['correspondence_decoder.coor_mlp.2.bias'], 'coor_mlp.2')
         return h @ sd['correspondence_decoder.coor_mlp.4.weight'].t() + sd['correspondence_decoder.coor_mlp.4.bias']
 
     def conf(x):
@@ -337,12 +399,13 @@ def forward(cfg, sd, src_xyz, tgt_xyz, meta=None, mode=geom.INDEX):
         'tgt_overlap': [t_ov[:, :nt[b], b] for b in range(B)],
     }
     poses = []
-    for b in range(B):                                                         # :198-218
-        a = torch.cat([src_xyz_c[b].expand(L, -1, -1), out['tgt_kp_warped'][b]], 1)
-        bb = torch.cat([out['src_kp_warped'][b], tgt_xyz_c[b].expand(L, -1, -1)], 1)
-        w = torch.cat([torch.sigmoid(out['src_overlap'][b][:, :, 0]),
-                       torch.sigmoid(out['tgt_overlap'][b][:, :, 0])], 1)
-        poses.append(weighted_procrustes(a, bb, w))
+    with torch.no_grad():
+        for b in range(B):                                                     # :198-218
+            a = torch.cat([src_xyz_c[b].expand(L, -1, -1), out['tgt_kp_warped'][b]], 1)
+            bb = torch.cat([out['src_kp_warped'][b], tgt_xyz_c[b].expand(L, -1, -1)], 1)
+            w = torch.cat([torch.sigmoid(out['src_overlap'][b][:, :, 0]),
+                           torch.sigmoid(out['tgt_overlap'][b][:, :, 0])], 1)
+            poses.append(weighted_procrustes(a, bb, w))
     out['pose'] = torch.stack(poses, 1)
     out['kpconv_meta'] = meta
     return out

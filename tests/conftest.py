@@ -107,3 +107,43 @@ def loss_fixture(device='cpu'):
     metrics = {k[7:]: g[k] for k in g.files if k.startswith('metric.')}
     pyr = {k[12:]: g[k] for k in g.files if k.startswith('overlap_pyr.')}
     return cfg, pred, batch, losses, metrics, pyr, T(g['W']), T(g['W_un'])
+
+
+def is_trainable(key):
+    """state_dict entries that are nn.Parameters with requires_grad in the reference (kernel
+    points are requires_grad=False, blocks:250-263; BatchNorm running statistics are buffers)."""
+    return not any(t in key for t in ('running_', 'num_batches', 'kernel_points'))
+
+
+def train_fixture():
+    """-> (cfg, sd, src, tgt, meta, loss batch (CPU), W, W_un, reference npz) for the training-
+    step fixture (tests/golden/train_modelnet_small.npz: the reference's train() forward +
+    compute_loss + backward on the model / inputs of forward_modelnet_small)."""
+    cfg, sd, src, tgt, meta, _ = forward_fixture('forward_modelnet_small')
+    _, _, batch, _, _, _, W, W_un = loss_fixture()
+    return cfg, sd, src, tgt, meta, batch, W, W_un, golden('train_modelnet_small')
+
+
+def oracle_train_grads(cfg, sd, src, tgt, meta, batch, W, W_un, dtype=torch.float64):
+    """The oracle's training step on CPU in ``dtype`` (fp64 by default: the checker of an fp32
+    implementation): forward_train + loss_oracle.compute_loss + backward -> (losses, {param
+    key: grad})."""
+    import loss_oracle as lo
+    import model_oracle as mo
+    cv = lambda t: t.detach().cpu().to(dtype) if t.is_floating_point() else t.cpu()
+    sd = {k: (cv(v).requires_grad_(True) if (v.is_floating_point() and is_trainable(k))
+              else cv(v)) for k, v in sd.items()}
+    meta = {k: [cv(t) for t in v] for k, v in meta.items()}
+    b = dict(batch)
+    b['pose'] = cv(batch['pose'])
+    b['src_overlap'] = [cv(t) for t in batch['src_overlap']]
+    b['tgt_overlap'] = [cv(t) for t in batch['tgt_overlap']]
+    b['kpconv_meta'] = {k: [cv(t) for t in v] for k, v in batch['kpconv_meta'].items()}
+    Wg, Wug = cv(W).requires_grad_(True), cv(W_un).requires_grad_(True)
+    pred = mo.forward_train(cfg, sd, [np.asarray(s) for s in src], tgt, meta=meta)
+    losses, _ = lo.compute_loss(cfg, Wg, Wug, pred, b)
+    losses['total'].backward()
+    grads = {k: v.grad for k, v in sd.items() if v.requires_grad and v.grad is not None}
+    grads['feature_criterion.W'] = Wg.grad
+    grads['feature_criterion_un.W'] = Wug.grad
+    return losses, grads

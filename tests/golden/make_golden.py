@@ -483,10 +483,84 @@ def make_loss(fr, fk):
     save('loss_modelnet_small', **arrays)
 
 
+# parameters whose full gradient is stored (one of every kind on the path); every other
+# parameter is pinned by its gradient's L2 norm and sum
+TRAIN_FULL_GRADS = (
+    'kpf_encoder.encoder_blocks.0.KPConv.weights',
+    'kpf_encoder.encoder_blocks.1.KPConv.weights',
+    'kpf_encoder.encoder_blocks.1.unary1.mlp.weight',
+    'kpf_encoder.encoder_blocks.1.res2net.layer1.0.convs.3.weight',
+    'kpf_encoder.encoder_blocks.1.res2net.layer1.0.bns.3.weight',
+    'kpf_encoder.encoder_blocks.1.res2net.layer1.0.bn3.bias',
+    'kpf_encoder.encoder_blocks.3.unary_shortcut.mlp.weight',
+    'kpf_encoder.encoder_blocks.3.KPConv.weights',
+    'feat_proj.weight',
+    'transformer_encoder.layers.0.self_attn.in_proj_weight',
+    'transformer_encoder.layers.2.multihead_attn.in_proj_bias',
+    'transformer_encoder.layers.5.norm2.weight',
+    'transformer_encoder.layers.5.linear1.weight',
+    'transformer_encoder.norm.bias',
+    'correspondence_decoder.coor_mlp.0.weight',
+    'correspondence_decoder.conf_logits_decoder.weight',
+)
+
+
+def make_train(fr, fk):
+    """Training-step fixture: the model of forward_modelnet_small switched
+    to train() (Res2Net BatchNorm on batch statistics), the reference's own forward and
+    compute_loss with the loss inputs of loss_modelnet_small, then losses['total'].backward()
+    (trainer.py:110-125 without the optimizer step). Stores the losses, the gradient norm and
+    sum of every parameter, the full gradient of TRAIN_FULL_GRADS and the updated running
+    statistics of two BatchNorm layers."""
+    cfg = load_cfg('modelnet.yaml', **SMALL_MODELNET)
+    pairs = [modelnet_like_pair(i, n_raw=512) for i in range(2)]
+    src = [p[0] for p in pairs]
+    tgt = [p[1] for p in pairs]
+    model, meta, out = run_forward(fr, fk, cfg, src, tgt)
+    lf = np.load(os.path.join(HERE, 'loss_modelnet_small.npz'))
+    model.feature_criterion.W.data.copy_(torch.from_numpy(lf['W']))
+    model.feature_criterion_un.W.data.copy_(torch.from_numpy(lf['W_un']))
+    model.train()
+    batch = {'src_xyz': [torch.from_numpy(c) for c in src],
+             'tgt_xyz': [torch.from_numpy(c) for c in tgt],
+             'pose': torch.from_numpy(lf['pose']),
+             'src_overlap': [torch.from_numpy(lf[f'src_overlap.{b}']) for b in range(2)],
+             'tgt_overlap': [torch.from_numpy(lf[f'tgt_overlap.{b}']) for b in range(2)]}
+    model.zero_grad()
+    with cuda_to_cpu():
+        pred = model(batch)
+        losses = model.compute_loss(pred, batch)
+        losses['total'].backward()
+    ref = np.load(os.path.join(HERE, 'forward_modelnet_small.npz'))
+    for l in range(len(meta['neighbors'])):     # same neighbour tables as the forward fixture
+        assert np.array_equal(batch['kpconv_meta']['neighbors'][l].numpy().astype(np.int32),
+                              ref[f'meta.neighbors.{l}'])
+    arrays = {}
+    for k, v in losses.items():
+        arrays[f'loss.{k}'] = np.float32(v.item())
+    for k, p in model.named_parameters():
+        if p.grad is None:
+            continue
+        g = p.grad.double()
+        arrays[f'gnorm.{k}'] = np.float64(g.norm().item())
+        arrays[f'gsum.{k}'] = np.float64(g.sum().item())
+        if k in TRAIN_FULL_GRADS:
+            arrays[f'grad.{k}'] = p.grad.numpy()
+    for bn in ('kpf_encoder.encoder_blocks.1.res2net.layer1.0.bn1',
+               'kpf_encoder.encoder_blocks.4.res2net.layer1.0.bns.6'):
+        m = dict(model.named_modules())[bn]
+        arrays[f'bn.{bn}.running_mean'] = m.running_mean.numpy()
+        arrays[f'bn.{bn}.running_var'] = m.running_var.numpy()
+    save('train_modelnet_small', **arrays)
+
+
 if __name__ == '__main__':
     fr, fk = import_reference()
     if sys.argv[1:] == ['loss']:
         make_loss(fr, fk)
+        sys.exit(0)
+    if sys.argv[1:] == ['train']:
+        make_train(fr, fk)
         sys.exit(0)
     if sys.argv[1:] == ['decoder']:
         make_forward_decoder(fr, fk)
@@ -496,3 +570,4 @@ if __name__ == '__main__':
     make_forward(fr, fk)
     make_forward_decoder(fr, fk)
     make_loss(fr, fk)
+    make_train(fr, fk)

@@ -6,13 +6,15 @@ GenericRegModel.test_step's call sequence (generic_reg_model.py:128-132):
 
 on the reference's own forward fixture (its kpconv_meta, state_dict and loss inputs) and is
 checked against the reference's compute_loss / _compute_metrics outputs
-(tests/golden/loss_modelnet_small.npz). Also: model.train() + forward with grad raises a
-clear NotImplementedError (the training guard).
+(tests/golden/loss_modelnet_small.npz). Also: train.py's training step (train() forward,
+compute_loss, backward, clip_grad_norm_) against the reference's own training step
+(tests/golden/train_modelnet_small.npz).
 
 The reference tree does not exist on the GPU box, so the three reference modules the drop-in
 imports (generic_reg_model, losses.corr_loss, losses.feature_loss) are given stand-ins here:
-the base class only carries cfg and the call sequence above, and the loss modules only their
-parameters (InfoNCELossFull.W, feature_loss.py:246-266), which is all the drop-in touches.
+the base class only carries cfg and the call sequence above, and the loss modules their
+parameters (InfoNCELossFull.W, feature_loss.py:246-266) and, for the training step, the
+oracle's restatement of their forward (oracle/loss_oracle.py, pinned to the reference).
 """
 import importlib.util
 import os
@@ -43,10 +45,26 @@ class _GenericRegModel(nn.Module):
 
 
 class _InfoNCELossFull(nn.Module):
+    """Stand-in with the reference's parameter (feature_loss.py:246-266) and, for the
+    training-step replay, its forward as restated by the oracle (loss_oracle.infonce_pair)."""
+
     def __init__(self, d_embed, r_p, r_n):
         super().__init__()
         self.W = nn.Parameter(torch.zeros(d_embed, d_embed))
         self.r_p, self.r_n = r_p, r_n
+
+    def forward(self, src_feat, tgt_feat, src_xyz, tgt_xyz):
+        import loss_oracle as lo
+        return torch.stack([lo.infonce_pair(self.W, a, p, ax, px, self.r_p, self.r_n)
+                            for a, p, ax, px in zip(src_feat, tgt_feat, src_xyz, tgt_xyz)]).mean()
+
+
+class _CorrCriterion(nn.Module):
+    """Stand-in for CorrCriterion('mae') (corr_loss.py:8-38) via loss_oracle.corr_mae."""
+
+    def forward(self, kp_before, kp_warped_pred, pose_gt, overlap_weights=None):
+        import loss_oracle as lo
+        return lo.corr_mae(kp_before, kp_warped_pred, pose_gt, overlap_weights)
 
 
 def _load_dropin():
@@ -55,7 +73,7 @@ def _load_dropin():
              'losses.corr_loss': types.ModuleType('losses.corr_loss'),
              'losses.feature_loss': types.ModuleType('losses.feature_loss')}
     stubs['generic_reg_model'].GenericRegModel = _GenericRegModel
-    stubs['losses.corr_loss'].CorrCriterion = lambda metric='mae': nn.Identity()
+    stubs['losses.corr_loss'].CorrCriterion = lambda metric='mae': _CorrCriterion()
     stubs['losses.feature_loss'].InfoNCELossFull = _InfoNCELossFull
     stubs['losses.feature_loss'].CircleLossFull = None
     saved = {k: sys.modules.get(k) for k in stubs}
@@ -99,11 +117,40 @@ def test_dropin_test_step_replay(gpu):
     np.testing.assert_allclose(pred['pose'].cpu().numpy(), d['out.pose'], atol=1e-4)
 
 
-def test_dropin_training_mode_raises(gpu):
+def test_dropin_training_step(gpu):
+    """train.py's step through the drop-in (trainer.py:110-125): model.train(),
+    training_step's forward + compute_loss (the reference's loss modules on the differentiable
+    outputs), backward, clip_grad_norm_: losses equal the reference's own training step
+    (tests/golden/train_modelnet_small.npz) and every trainable parameter gets a finite
+    gradient whose norm matches the reference's within 1e-2 (tests/test_gpu_train.py)."""
+    import fgreg
+    from conftest import golden, is_trainable
     mod = _load_dropin()
     cfg, sd, src, tgt, meta, d = forward_fixture('forward_modelnet_small')
-    model = mod.RegTR(cfg).to(gpu).train()
-    batch = {'src_xyz': [torch.from_numpy(s).to(gpu) for s in src],
-             'tgt_xyz': [torch.from_numpy(t).to(gpu) for t in tgt]}
-    with pytest.raises(NotImplementedError, match='inference forward'):
-        model(batch)
+    _, _, batch, _, _, _, W, W_un = loss_fixture(gpu)
+    ref = golden('train_modelnet_small')
+    model = mod.RegTR(cfg)
+    sd = dict(sd)
+    sd['feature_criterion.W'] = W.cpu()
+    sd['feature_criterion_un.W'] = W_un.cpu()
+    model.load_state_dict(sd, strict=True)
+    model = model.to(gpu).train()
+    model.preprocessor = fgreg.FixedMetaPreprocessor(batch['kpconv_meta'])
+    batch['kpconv_meta'] = {k: list(v) for k, v in batch['kpconv_meta'].items()}
+    pred = model(batch)
+    losses = model.compute_loss(pred, batch)
+    losses['total'].backward()
+    torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=0.1)
+    for k in ref.files:
+        if k.startswith('loss.'):
+            v = float(ref[k])
+            assert abs(float(losses[k[5:]]) - v) <= 1e-4 * max(1.0, abs(v)), (k, float(losses[k[5:]]), v)
+    names = {k[6:] for k in ref.files if k.startswith('gnorm.')}
+    got = {k: p.grad for k, p in model.named_parameters() if p.grad is not None}
+    assert names == {k for k in got if is_trainable(k)}
+    total = float(np.sqrt(sum(float(ref['gnorm.' + k]) ** 2 for k in names)))
+    scale = min(1.0, 0.1 / (total + 1e-6))             # clip_grad_norm_ on the reference's norms
+    for k in names:
+        assert torch.isfinite(got[k]).all(), k
+        n_ref = float(ref['gnorm.' + k]) * scale
+        assert abs(float(got[k].double().norm()) - n_ref) <= 1e-2 * n_ref + 1e-9, k

@@ -1,0 +1,387 @@
+"""Training backward on the GPU: every differentiable op of
+fgreg/autograd.py against torch autograd in fp64 on the same inputs, then whole training steps
+(train() forward + loss + backward) against the reference's own gradients and the fp64 oracle.
+
+Gradient tolerances. Each op's backward is checked at fp32-accuracy level (normwise 1e-5 / 1e-4
+for the reductions over tens of thousands of rows). End to end the gradient of this network is
+discontinuous wherever a ReLU / LeakyReLU input sits at its kink or two max-pool candidates
+tie; on random models thousands of activations lie within 1e-7..1e-6 (relative) of a kink
+(model_oracle.ACT_TRACE), so ANY two fp32 implementations take a few different branches: the
+oracle computed with torch's fused BatchNorm / InstanceNorm and the same oracle with the
+decomposed formulas differ by 0.7-1.9e-3 in the encoder gradients (Frobenius), although each
+agrees with its own fp64 run elsewhere. The whole-step checks therefore bound the encoder /
+transformer gradients at GRAD_TOL = 1e-2 relative Frobenius (a wiring or formula error is
+O(1)), the losses at 1e-5, and print the measured errors.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+import model_oracle as mo
+from conftest import (forward_fixture, is_trainable, loss_fixture, oracle_train_grads,
+                      rel_err, train_fixture)
+
+pytestmark = pytest.mark.gpu
+
+GRAD_TOL = 1e-2
+
+
+def fro(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return float((a - b).norm() / max(float(b.norm()), 1e-30))
+
+
+def _leaf(t, gpu):
+    return t.detach().to(gpu).float().requires_grad_(True), t.detach().double().requires_grad_(True)
+
+
+# ------------------------------------------------------------------------------------------
+# per-op backward vs torch fp64 autograd
+# ------------------------------------------------------------------------------------------
+@pytest.mark.parametrize('m,n,k', [(1000, 80, 96), (9544, 256, 128), (37, 3, 32), (2000, 1, 256)])
+@pytest.mark.parametrize('act', ['none', 'relu', 'residual'])
+def test_linear_backward(gpu, m, n, k, act):
+    from fgreg import ops
+    from fgreg.autograd import linear_t
+    g = torch.Generator().manual_seed(m + n + k)
+    x, x64 = _leaf(torch.randn(m, k, generator=g), gpu)
+    w, w64 = _leaf(torch.randn(n, k, generator=g) / math.sqrt(k), gpu)
+    b, b64 = _leaf(torch.randn(n, generator=g), gpu)
+    r, r64 = _leaf(torch.randn(m, n, generator=g), gpu)
+    R = torch.randn(m, n, generator=g)
+    if act == 'relu':
+        y = linear_t(x, w, b, act=ops.ACT_RELU)
+        y64 = torch.relu(x64 @ w64.t() + b64)
+    elif act == 'residual':
+        y = linear_t(x, w, b, residual=r)
+        y64 = x64 @ w64.t() + b64 + r64
+    else:
+        y = linear_t(x, w, b)
+        y64 = x64 @ w64.t() + b64
+    (y * R.to(gpu)).sum().backward()
+    (y64 * R.double()).sum().backward()
+    assert rel_err(y, y64) < 1e-5
+    for t, t64, name in ((x, x64, 'dx'), (w, w64, 'dw'), (b, b64, 'db')):
+        assert rel_err(t.grad, t64.grad) < 1e-5, (name, rel_err(t.grad, t64.grad))
+    if act == 'residual':
+        assert rel_err(r.grad, r64.grad) < 1e-6
+
+
+def _kpconv_case(cin):
+    gk = np.load(__import__('conftest').GOLDEN + '/kpconv_block.npz')
+    q = torch.from_numpy(gk['q'])
+    idx = torch.from_numpy(gk['idx'].astype(np.int64))
+    kp = torch.from_numpy(gk['kp'])
+    extent = float(gk['extent'])
+    g = torch.Generator().manual_seed(cin)
+    x = torch.randn(q.shape[0], cin, generator=g)
+    x[::5] = -x[::5].abs()                       # rows that do not count in the normaliser
+    W = torch.randn(15, cin, 24, generator=g) / math.sqrt(15 * cin)
+    return q, idx, kp, extent, x, W, gk
+
+
+@pytest.mark.parametrize('cin', [1, 16, 32, 64, 128, 256])
+@pytest.mark.parametrize('strided', [False, True])
+def test_kpconv_backward(gpu, cin, strided):
+    """kpconv_t (gather + weight GEMM, normalised by the returned nnorm) vs the oracle's KPConv
+    (finegrained_kpconv_blocks.py:265-401 restated) in fp64: dx (fgr_kpconv_scatter) and dW."""
+    from fgreg.autograd import kpconv_t
+    q, idx, kp, extent, x0, W0, gk = _kpconv_case(cin)
+    s = q
+    if strided:
+        q = torch.from_numpy(gk['sub'])
+        idx = torch.from_numpy(gk['pools'].astype(np.int64))
+
+    class Conv:
+        pass
+    conv = Conv()
+    x, x64 = _leaf(x0, gpu)
+    W, W64 = _leaf(W0, gpu)
+    conv.weights, conv.kernel_points, conv.KP_extent = W, kp.to(gpu), extent
+    out, nnorm = kpconv_t(conv, q.to(gpu), s.to(gpu), idx.to(gpu), x)
+    y = out / nnorm.unsqueeze(1)
+    y64 = mo.kpconv(q.double(), s.double(), idx, x64, W64, kp.double(), extent)
+    R = torch.randn(y64.shape, generator=torch.Generator().manual_seed(3))
+    (y * R.to(gpu)).sum().backward()
+    (y64 * R.double()).sum().backward()
+    assert rel_err(y, y64) < 1e-5
+    assert rel_err(x.grad, x64.grad) < 1e-5, rel_err(x.grad, x64.grad)
+    assert rel_err(W.grad, W64.grad) < 1e-5, rel_err(W.grad, W64.grad)
+
+
+def test_max_pool_backward(gpu):
+    from fgreg.autograd import max_pool_t
+    gk = np.load(__import__('conftest').GOLDEN + '/kpconv_block.npz')
+    idx = torch.from_numpy(gk['pools'].astype(np.int64))
+    x0 = torch.randn(gk['q'].shape[0], 48, generator=torch.Generator().manual_seed(1))
+    x0[:, :8] = -x0[:, :8].abs()                 # channels where the shadow zero wins
+    x, x64 = _leaf(x0, gpu)
+    y = max_pool_t(x, idx.to(gpu))
+    y64 = mo.max_pool(x64, idx)
+    R = torch.randn(y64.shape, generator=torch.Generator().manual_seed(2))
+    (y * R.to(gpu)).sum().backward()
+    (y64 * R.double()).sum().backward()
+    assert torch.equal(y.cpu().double(), y64.detach())
+    assert rel_err(x.grad, x64.grad) < 1e-6
+
+
+def _segnorm_ref(x, lens, row_div, gamma, beta, act, residual, post, eps=1e-5):
+    v = x / row_div[:, None] if row_div is not None else x
+    outs, o = [], 0
+    for n in lens:
+        seg = v[o:o + n]
+        mu = seg.mean(0)
+        var = ((seg - mu) ** 2).mean(0)
+        outs.append((seg - mu) / torch.sqrt(var + eps))
+        o += n
+    z = torch.cat(outs, 0)
+    if gamma is not None:
+        z = z * gamma + beta
+    fa = {'none': lambda t: t, 'relu': F.relu, 'leaky': lambda t: F.leaky_relu(t, 0.1)}
+    y = fa[act](z)
+    if residual is not None:
+        y = fa[post](y + residual)
+    return y
+
+
+@pytest.mark.parametrize('case', ['instnorm', 'instnorm_rowdiv_leaky', 'instnorm_residual',
+                                  'batchnorm_relu', 'batchnorm_residual_relu', 'long_segments'])
+def test_segnorm_backward(gpu, case):
+    """segnorm_t: InstanceNorm per cloud (with the KPConv row divisor, LeakyReLU, the
+    bottleneck's residual + LeakyReLU) and training BatchNorm (one segment, affine, ReLU,
+    residual + ReLU) vs the same formulas in fp64."""
+    from fgreg import ops
+    from fgreg.autograd import segnorm_t
+    g = torch.Generator().manual_seed(len(case))
+    lens = [700, 300, 1, 513] if case != 'long_segments' else [20000, 9000]
+    if case.startswith('batchnorm'):
+        lens = [sum(lens)]
+    n, c = sum(lens), 72
+    x, x64 = _leaf(torch.randn(n, c, generator=g) * 3 + 5, gpu)
+    rd = (1 + torch.randint(0, 9, (n,), generator=g)).float() if 'rowdiv' in case else None
+    affine = case.startswith('batchnorm')
+    gm, gm64 = _leaf(1 + 0.2 * torch.randn(c, generator=g), gpu) if affine else (None, None)
+    bt, bt64 = _leaf(0.1 * torch.randn(c, generator=g), gpu) if affine else (None, None)
+    res = 'residual' in case
+    r, r64 = _leaf(torch.randn(n, c, generator=g), gpu) if res else (None, None)
+    act = {'instnorm': 'none', 'instnorm_rowdiv_leaky': 'leaky', 'instnorm_residual': 'none',
+           'batchnorm_relu': 'relu', 'batchnorm_residual_relu': 'none', 'long_segments': 'leaky'}[case]
+    post = 'relu' if case == 'batchnorm_residual_relu' else 'leaky'
+    A = {'none': ops.ACT_NONE, 'relu': ops.ACT_RELU, 'leaky': ops.ACT_LEAKY}
+    off = ops.offsets(lens, gpu)
+    y = segnorm_t(x, off, lens, row_div=rd.to(gpu) if rd is not None else None, act=A[act],
+                  residual=r, post_act=A[post], gamma=gm, beta=bt)
+    y64 = _segnorm_ref(x64, lens, rd.double() if rd is not None else None, gm64, bt64, act, r64,
+                       post)
+    R = torch.randn(n, c, generator=g)
+    (y * R.to(gpu)).sum().backward()
+    (y64 * R.double()).sum().backward()
+    assert rel_err(y, y64) < 1e-5
+    assert rel_err(x.grad, x64.grad) < 1e-4, rel_err(x.grad, x64.grad)
+    if affine:
+        assert rel_err(gm.grad, gm64.grad) < 1e-5 and rel_err(bt.grad, bt64.grad) < 1e-5
+    if res:
+        assert rel_err(r.grad, r64.grad) < 1e-5
+
+
+def test_batchnorm_running_stats(gpu):
+    """batchnorm_t updates running_mean / running_var / num_batches_tracked like
+    nn.BatchNorm1d.train() (momentum, unbiased variance)."""
+    from fgreg.autograd import batchnorm_t
+    bn = torch.nn.BatchNorm1d(40).to(gpu)
+    ref = torch.nn.BatchNorm1d(40)
+    with torch.no_grad():
+        for m in (bn, ref):
+            m.running_mean.fill_(0.3)
+            m.running_var.fill_(2.0)
+    x = torch.randn(3001, 40) * 2 + 1
+    for _ in range(2):
+        y = batchnorm_t(bn, x.to(gpu))
+        y_ref = ref.train()(x)
+    assert rel_err(y, y_ref) < 1e-5
+    assert rel_err(bn.running_mean, ref.running_mean) < 1e-6
+    assert rel_err(bn.running_var, ref.running_var) < 1e-6
+    assert int(bn.num_batches_tracked) == int(ref.num_batches_tracked) == 2
+
+
+@pytest.mark.parametrize('d', [32, 256, 512, 96])
+def test_layernorm_backward(gpu, d):
+    from fgreg.autograd import layernorm_t
+    n = 3000
+    g = torch.Generator().manual_seed(d)
+    norm = torch.nn.LayerNorm(d).to(gpu)
+    with torch.no_grad():
+        norm.weight.copy_(1 + 0.2 * torch.randn(d, generator=g))
+        norm.bias.copy_(0.1 * torch.randn(d, generator=g))
+    x, x64 = _leaf(torch.randn(n, d, generator=g) * 2 + 3, gpu)
+    pos = torch.randn(n, d, generator=g)
+    y = layernorm_t(x, norm, add=pos.to(gpu))
+    w64 = norm.weight.detach().cpu().double().requires_grad_(True)
+    b64 = norm.bias.detach().cpu().double().requires_grad_(True)
+    y64 = F.layer_norm(x64, (d,), w64, b64, 1e-5) + pos.double()
+    R = torch.randn(n, d, generator=g)
+    (y * R.to(gpu)).sum().backward()
+    (y64 * R.double()).sum().backward()
+    assert rel_err(y, y64) < 1e-5
+    assert rel_err(x.grad, x64.grad) < 1e-5
+    assert rel_err(norm.weight.grad, w64.grad) < 1e-5
+    assert rel_err(norm.bias.grad, b64.grad) < 1e-5
+
+
+def _attn_ref(qkv, lens, kv_seg, nhead):
+    d = qkv.shape[1] // 3
+    dh = d // nhead
+    off = np.cumsum([0] + lens)
+    outs = []
+    for i in range(len(lens)):
+        j = kv_seg[i]
+        q = qkv[off[i]:off[i + 1], :d].reshape(-1, nhead, dh).transpose(0, 1) / math.sqrt(dh)
+        k = qkv[off[j]:off[j + 1], d:2 * d].reshape(-1, nhead, dh).transpose(0, 1)
+        v = qkv[off[j]:off[j + 1], 2 * d:].reshape(-1, nhead, dh).transpose(0, 1)
+        outs.append((torch.softmax(q @ k.transpose(1, 2), -1) @ v).transpose(0, 1).reshape(-1, d))
+    return torch.cat(outs, 0)
+
+
+@pytest.mark.parametrize('d,nhead', [(32, 8), (256, 8), (512, 8)])
+@pytest.mark.parametrize('kind', ['self', 'cross'])
+def test_attention_backward(gpu, d, nhead, kind):
+    """attention_t (fused QKV; self = every cloud to itself, cross = cloud c to (c + B) mod 2B)
+    vs fp64 softmax attention: dq, dk, dv through fgr_attention_bwd, unequal lengths incl. a
+    1-row cloud and clouds past one 64-row tile."""
+    from fgreg import ops
+    from fgreg.autograd import attention_t
+    lens = [130, 1, 65, 300]
+    B = len(lens) // 2
+    kv_seg = list(range(4)) if kind == 'self' else [(c + B) % 4 for c in range(4)]
+    g = torch.Generator().manual_seed(d)
+    qkv, qkv64 = _leaf(torch.randn(sum(lens), 3 * d, generator=g), gpu)
+    off = ops.offsets(lens, gpu)
+    o = attention_t(qkv, off, torch.tensor(kv_seg, dtype=torch.int32, device=gpu), max(lens), nhead)
+    o64 = _attn_ref(qkv64, lens, kv_seg, nhead)
+    R = torch.randn(o64.shape, generator=g)
+    (o * R.to(gpu)).sum().backward()
+    (o64 * R.double()).sum().backward()
+    assert rel_err(o, o64) < 1e-5
+    for sl, name in ((slice(0, d), 'dq'), (slice(d, 2 * d), 'dk'), (slice(2 * d, 3 * d), 'dv')):
+        e = rel_err(qkv.grad[:, sl], qkv64.grad[:, sl])
+        assert e < 1e-5, (name, e)
+
+
+def test_colsum(gpu):
+    from fgreg.autograd import colsum
+    x = torch.randn(40001, 300, dtype=torch.float64)
+    got = colsum(x.float().to(gpu)[:, 7:250])
+    assert rel_err(got, x.float().double()[:, 7:250].sum(0)) < 1e-6
+
+
+# ------------------------------------------------------------------------------------------
+# whole training steps
+# ------------------------------------------------------------------------------------------
+def _gpu_train_step(cfg, sd, src, tgt, meta, batch, W, W_un, gpu):
+    """fgreg.RegTR in train() on the given neighbour tables; the checker's loss
+    (loss_oracle.compute_loss) evaluated in fp64 on the host from the GPU outputs (so its
+    geometric masks are computed exactly as on the oracle side), backward through the GPU
+    graph -> (losses, grads, model)."""
+    import fgreg
+    import loss_oracle as lo
+    model = fgreg.RegTR(cfg)
+    model.load_state_dict({k: v for k, v in sd.items()}, strict=False)
+    model = model.to(gpu).train()
+    model.preprocessor = fgreg.FixedMetaPreprocessor({k: [t.to(gpu) for t in v]
+                                                      for k, v in meta.items()})
+    xb = {'src_xyz': [torch.from_numpy(np.asarray(s)).to(gpu) for s in src],
+          'tgt_xyz': [torch.from_numpy(np.asarray(t)).to(gpu) for t in tgt]}
+    pred = model(xb)
+    host = {k: ([t.cpu().double() for t in v] if isinstance(v, list) else v.cpu().double())
+            for k, v in pred.items()}
+    Wg = W.detach().cpu().double().requires_grad_(True)
+    Wug = W_un.detach().cpu().double().requires_grad_(True)
+    cv = lambda t: t.cpu().double() if t.is_floating_point() else t.cpu()
+    b = {'pose': cv(batch['pose']),
+         'kpconv_meta': {k: [cv(t) for t in v] for k, v in batch['kpconv_meta'].items()},
+         'src_overlap': [cv(t) for t in batch['src_overlap']],
+         'tgt_overlap': [cv(t) for t in batch['tgt_overlap']]}
+    losses, _ = lo.compute_loss(cfg, Wg, Wug, host, b)
+    losses['total'].backward()
+    grads = {k: p.grad for k, p in model.named_parameters() if p.grad is not None}
+    grads['feature_criterion.W'] = Wg.grad
+    grads['feature_criterion_un.W'] = Wug.grad
+    return losses, grads, model
+
+
+def test_train_step_vs_reference(gpu):
+    """The reference's own train() step (tests/golden/train_modelnet_small.npz: forward +
+    compute_loss + backward on the model / inputs / neighbour tables of forward_modelnet_small)
+    vs fgreg's: losses within 1e-5, every parameter's gradient norm and the full gradients of
+    one parameter of every kind within GRAD_TOL (see the module docstring), the Res2Net
+    BatchNorm running statistics after the step within 1e-5."""
+    cfg, sd, src, tgt, meta, batch, W, W_un, ref = train_fixture()
+    losses, grads, model = _gpu_train_step(cfg, sd, src, tgt, meta, batch, W, W_un, gpu)
+    for k in ref.files:
+        if k.startswith('loss.'):
+            v = float(ref[k])
+            assert abs(float(losses[k[5:]]) - v) <= 1e-5 * max(1.0, abs(v)), (k, float(losses[k[5:]]), v)
+    norms = {k[6:] for k in ref.files if k.startswith('gnorm.')}
+    assert norms == {k for k in grads if is_trainable(k)}, norms ^ set(grads)
+    worst = (0.0, None)
+    for k in norms:
+        n_ref = float(ref['gnorm.' + k])
+        e = abs(float(grads[k].double().norm()) - n_ref) / max(n_ref, 1e-12)
+        worst = max(worst, (e, k))
+        assert e < GRAD_TOL, (k, e)
+    errs = {k[5:]: fro(grads[k[5:]], torch.from_numpy(ref[k])) for k in ref.files if k.startswith('grad.')}
+    print('\nworst gradient-norm error', worst, '\nfull-gradient Frobenius errors',
+          {k.split('.', 1)[1][-40:]: f'{v:.1e}' for k, v in errs.items()})
+    for k, e in errs.items():
+        assert e < GRAD_TOL, (k, e)
+    mods = dict(model.named_modules())
+    for k in ref.files:
+        if k.startswith('bn.'):
+            name, stat = k[3:].rsplit('.', 1)
+            assert rel_err(getattr(mods[name], stat), ref[k]) < 1e-5, k
+
+
+def test_train_step_vs_oracle_modelnet(gpu):
+    """Full-width ModelNet config (d 256, head dim 32: the f16x3 attention and every GEMM path),
+    B = 2 pairs of the bench workload: fgreg's train() step vs the fp64 oracle's on the same
+    neighbour tables. Losses within 1e-5, every gradient within GRAD_TOL; the cosine of the
+    whole gradient vector above 1 - 1e-6."""
+    import fgreg
+    import fgreg.config as fc
+    from fgreg.synthetic import make_batch
+    cfg = fc.get('modelnet')
+    torch.manual_seed(5)
+    np.random.seed(5)
+    model = fgreg.RegTR(cfg)
+    sd = {k: v.clone() for k, v in model.state_dict().items()}
+    src, tgt, pose = make_batch('modelnet', 2)
+    meta = mo.preprocess(cfg, [np.asarray(c) for c in list(src) + list(tgt)])
+    _, _, lb, _, _, _, W, W_un = loss_fixture()
+    from scipy.spatial import cKDTree
+    sov, tov = [], []
+    for b in range(2):
+        sw = src[b] @ pose[b][:, :3].T + pose[b][:, 3]
+        sov.append(torch.from_numpy((cKDTree(tgt[b]).query(sw)[0] < 0.05).astype(np.float32)))
+        tov.append(torch.from_numpy((cKDTree(sw).query(tgt[b])[0] < 0.05).astype(np.float32)))
+    W = torch.randn(cfg.d_embed, cfg.d_embed, generator=torch.Generator().manual_seed(1)) * 0.1
+    W_un = torch.randn(cfg.d_embed, cfg.d_embed, generator=torch.Generator().manual_seed(2)) * 0.1
+    batch = {'pose': torch.from_numpy(pose), 'kpconv_meta': meta, 'src_overlap': sov,
+             'tgt_overlap': tov}
+    losses, grads, _ = _gpu_train_step(cfg, sd, src, tgt, meta, batch, W, W_un, gpu)
+    l64, g64 = oracle_train_grads(cfg, sd, src, tgt, meta, batch, W, W_un)
+    for k, v in l64.items():
+        assert abs(float(losses[k]) - float(v)) <= 1e-5 * max(1.0, abs(float(v))), (k, float(losses[k]), float(v))
+    errs = {k: fro(grads[k], g64[k]) for k in g64 if float(g64[k].norm()) > 0}
+    worst = sorted(errs.items(), key=lambda kv: -kv[1])[:5]
+    a = torch.cat([grads[k].detach().double().cpu().flatten() for k in errs])
+    b = torch.cat([g64[k].detach().flatten() for k in errs])
+    cos = float(a @ b / (a.norm() * b.norm()))
+    print(f'\nworst Frobenius errors {worst}, median {np.median(list(errs.values())):.2e}, '
+          f'cosine {cos:.10f}')
+    assert cos > 1 - 1e-6
+    for k, e in errs.items():
+        assert e < GRAD_TOL, (k, e)

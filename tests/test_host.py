@@ -183,16 +183,16 @@ def test_f16x3_split_numerics():
     assert (np.abs(got - ref) / den).max() < 2e-6
 
 
-def test_training_mode_with_grad_raises_clearly():
-    """model.train() + a forward with autograd on (what train.py does) fails fast with a clear
-    message before any kernel launch; eval() or no_grad() is the supported inference path."""
+def test_training_mode_refuses_host_tensors():
+    """model.train() runs the training forward (fgreg/training.py); like the inference forward
+    it has no CPU path: host tensors are refused with FgrError, with or without autograd."""
     import fgreg
     import fgreg.config as fc
     model = fgreg.RegTR(fc.get('modelnet')).train()
     batch = {'src_xyz': [torch.zeros(8, 3)], 'tgt_xyz': [torch.zeros(8, 3)]}
-    with pytest.raises(NotImplementedError, match='inference forward'):
+    with pytest.raises(fgreg.FgrError):
         model(batch)
-    with torch.no_grad(), pytest.raises(fgreg.FgrError):   # guard passes; CPU tensors refused
+    with torch.no_grad(), pytest.raises(fgreg.FgrError):
         model(batch)
 
 

@@ -177,3 +177,26 @@ def test_loss_oracle_matches_reference():
     rot, trans = lo.pose_errors(pred['pose'], batch['pose'])
     np.testing.assert_allclose(rot.numpy(), ref_metrics['rot_err_deg'], atol=1e-3)
     np.testing.assert_allclose(trans.numpy(), ref_metrics['trans_err'], rtol=1e-5, atol=1e-6)
+
+
+def test_train_oracle_matches_reference():
+    """The oracle's training step (model_oracle.forward_train: Res2Net BatchNorm on batch
+    statistics; loss_oracle.compute_loss; torch autograd) vs the reference's own train()
+    forward + compute_loss + backward (tests/golden/train_modelnet_small.npz): losses, the
+    gradient norm and sum of every parameter, full gradients of one parameter of every kind."""
+    from conftest import oracle_train_grads, train_fixture
+    cfg, sd, src, tgt, meta, batch, W, W_un, ref = train_fixture()
+    losses, grads = oracle_train_grads(cfg, sd, src, tgt, meta, batch, W, W_un)
+    for k in ref.files:
+        if k.startswith('loss.'):
+            v = float(ref[k])
+            assert abs(float(losses[k[5:]]) - v) <= 1e-5 * max(1.0, abs(v)), (k, float(losses[k[5:]]), v)
+    norms = [k[6:] for k in ref.files if k.startswith('gnorm.')]
+    assert set(norms) == set(grads), set(norms) ^ set(grads)
+    for k in norms:
+        g = grads[k].double()
+        n_ref = float(ref['gnorm.' + k])
+        assert abs(float(g.norm()) - n_ref) <= 1e-4 * n_ref + 1e-12, (k, float(g.norm()), n_ref)
+    for k in ref.files:
+        if k.startswith('grad.'):
+            assert rel_err(grads[k[5:]], ref[k]) < 1e-4, (k, rel_err(grads[k[5:]], ref[k]))
