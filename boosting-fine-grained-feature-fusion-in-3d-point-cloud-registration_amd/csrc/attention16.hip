@@ -42,7 +42,6 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 // 16-B units per (tile, head) image and the first V unit, by head dim
 template <int DH> constexpr int units() { return DH * 16 + (DH / 32) * 512; }
 template <int DH> constexpr int unit_v() { return (DH / 32) * 512; }
-constexpr float kPScale = 16384.f;       // 2^14
 
 __device__ __forceinline__ float xg_max16(float v) {   // max over lanes c, c^16, c^32, c^48
     auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
@@ -134,30 +133,74 @@ attn_kv_image16_kernel(const float* __restrict__ k, int64_t ld_k, const float* _
     }
 }
 
-// GLDS: the K/V tile images go global -> LDS by LDS-DMA into two buffers (tile t + 1 in
-// flight while tile t is computed; one barrier per tile, no staging registers, no ds_write
-// pass). The per-tile scale exponents come by scalar loads (block-uniform address: s_load,
-// counted by lgkmcnt, so the loop never waits on the DMA's vmcnt for them); no limit on the
-// key count, 32 KB of LDS at head dim 32 (5 blocks per CU).
-
 template <int N>
 __device__ __forceinline__ void wait_vm_lgkm0_a() {
     __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4));
 }
 
-template <int DH, bool GLDS>
-__global__ void __launch_bounds__(256, (GLDS && DH == 64) ? 2 : (GLDS ? 5 : 4))
-attn_f16x3_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __restrict__ img,
-                  const int2* __restrict__ sc, float* __restrict__ o, int64_t ld_o,
-                  const int64_t* __restrict__ q_off, const int64_t* __restrict__ kv_off,
-                  const int32_t* __restrict__ kv_seg, int n_head, int n_seg, int n_qblk,
-                  float scale_log2) {
-    constexpr int KD = DH / 32;                                  // k-steps of Q K^T
-    constexpr int TD = DH / 16;                                  // 16-row output tiles (dh)
-    constexpr int UN = units<DH>(), NS = UN / 256;
-    __shared__ u32x4 lds[(GLDS ? 2 : 1) * UN];
-    // XCD-aware block order: linear id L runs on XCD L % 8; all q-blocks of one
-    // (segment, head) get ids of one residue mod 8, so one XCD's L2 serves its K/V image.
+// ---- key-tile loop: the K/V tile images go global -> LDS by LDS-DMA into two buffers (tile
+// t + 1 in flight while tile t is computed; one barrier per tile, no staging registers, no
+// ds_write pass); the per-tile scale exponents come by scalar loads (block-uniform address).
+// Vector work per key tile is kept minimal (round 3; PMC in profiles/r03_pmc_attn_*.json):
+// the round-2 loop issued ~8.6 VALU
+// per MFMA at head dim 32 (154 VALU + 17 v_exp + 24 MFMA per wave and 64-key tile, 17 of the
+// VALU packed fp32 ops); this loop issues ~100 VALU + 17 v_exp per tile (6.7 VALU per MFMA
+// over the whole kernel), 50.6 -> 46.3 us on the ModelNet self-attention shape:
+//   * the P scale 2^14 folded into the exponent (p14 = exp2(s f - (m - 14))): no multiply;
+//   * P split with packed conversions: hi = v_cvt_pk_f16_f32 (2 per instruction), lo = one
+//     v_fma_mix per element reading hi's half by op_sel (24 instructions per 16 values);
+//   * row maxima by v_max3_f32 without NaN canonicalisation (scores are finite or -inf);
+//   * the tile loop unrolled by two, so both LDS buffers' addresses are per-lane constants +
+//     instruction offsets (no per-tile address arithmetic), K/V DMA pieces contiguous per
+//     wave (one 64-bit add per tile, the pieces by instruction offsets);
+//   * built with -fno-slp-vectorize (packed fp32 VALU costs ~22 extra cycles beside MFMAs).
+// maxima of MFMA results: plain fmaxf (the file is built -fno-honor-nans, so no NaN
+// canonicalisation of the inputs; inline asm cannot be used here: the compiler's hazard
+// recognizer does not see an asm block's reads of MFMA results)
+__device__ __forceinline__ float vmax3(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
+__device__ __forceinline__ float vmax2(float a, float b) { return fmaxf(a, b); }
+__device__ __forceinline__ float xg_max16_nc(float v) {   // max over lanes c, c^16, c^32, c^48
+    auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = vmax2(__uint_as_float(a[0]), __uint_as_float(a[1]));
+    auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return vmax2(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+// x[0..7] (in fp16 range) -> h = f16(x) packed by v_cvt_pk_f16_f32 (RNE, the bits of split2's
+// hi), l = f16(x - h) by v_fma_mix (x - h exact in fp32, one rounding). Ends with `s_nop 1`:
+// the terms feed MFMAs (cdna_hip_programming.md 5.7 item 2).
+__device__ __forceinline__ void split8_pk(const float (&x)[8], float one, u32x4& h, u32x4& l) {
+    unsigned h0, h1, h2, h3, l0, l1, l2, l3;
+    asm("v_cvt_pk_f16_f32 %0, %8, %9\n\t"
+        "v_cvt_pk_f16_f32 %1, %10, %11\n\t"
+        "v_cvt_pk_f16_f32 %2, %12, %13\n\t"
+        "v_cvt_pk_f16_f32 %3, %14, %15\n\t"
+        "v_fma_mixlo_f16 %4, %8, %16, -%0 op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixlo_f16 %5, %10, %16, -%1 op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixlo_f16 %6, %12, %16, -%2 op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixlo_f16 %7, %14, %16, -%3 op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixhi_f16 %4, %9, %16, -%0 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixhi_f16 %5, %11, %16, -%1 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixhi_f16 %6, %13, %16, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixhi_f16 %7, %15, %16, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+        "s_nop 1"
+        : "=&v"(h0), "=&v"(h1), "=&v"(h2), "=&v"(h3), "=&v"(l0), "=&v"(l1), "=&v"(l2), "=&v"(l3)
+        : "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(x[4]), "v"(x[5]), "v"(x[6]), "v"(x[7]),
+          "v"(one));
+    h = u32x4{h0, h1, h2, h3};
+    l = u32x4{l0, l1, l2, l3};
+}
+
+template <int DH>
+__global__ void __launch_bounds__(256, DH == 64 ? 2 : 5)
+attn_f16x3_v2_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __restrict__ img,
+                     const int2* __restrict__ sc, float* __restrict__ o, int64_t ld_o,
+                     const int64_t* __restrict__ q_off, const int64_t* __restrict__ kv_off,
+                     const int32_t* __restrict__ kv_seg, int n_head, int n_seg, int n_qblk,
+                     float scale_log2) {
+    constexpr int KD = DH / 32, TD = DH / 16;
+    constexpr int UN = units<DH>();
+    constexpr int PW = UN / 64 / 4;                              // DMA pieces per wave per tile
+    __shared__ u32x4 lds[2 * UN];
     const int L = blockIdx.x, xcd = L & 7, j0 = L >> 3;
     const int pair = (j0 / n_qblk) * 8 + xcd, qblk = j0 % n_qblk;
     if (pair >= n_seg * n_head) return;
@@ -170,13 +213,12 @@ attn_f16x3_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __rest
     const int nk = (int)(kv_off[ks + 1] - kb);
     const int ntile = (nk + 63) / 64;
     const int64_t tile0 = (kb / 64 + ks) * n_head + head;
-    const u32x4* tiles = reinterpret_cast<const u32x4*>(img) + tile0 * UN;
     const int64_t tile_stride = (int64_t)n_head * UN;
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
     const int g = lane >> 4, c = lane & 15;
+    // this lane's DMA source within a tile: pieces wv * PW .. + PW - 1 (1 KiB each, contiguous)
+    const u32x4* src_lane = reinterpret_cast<const u32x4*>(img) + tile0 * UN + wv * PW * 64 + lane;
 
-    // Q^T operand (B): lane (g, c) holds q[query c][32 kd + 8g .. +7] * scale * log2(e),
-    // scaled per query into fp16 range and split
     const int64_t qrow = q0 + wv * 16 + c;
     float x[KD][8];
 #pragma unroll
@@ -213,71 +255,43 @@ attn_f16x3_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __rest
 #pragma unroll
     for (int t = 0; t < TD; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
     float m_run = -INFINITY, l_run = 0.f;
+    const float one = 1.0f;
 
-    u32x4 stage[GLDS ? 1 : NS];
-    // transposed-read addresses of V: lane c = 4qq + p reads row 4g + qq (+16, +32j),
-    // columns 16t + 4p .. +3 (chunk 2t + (p >> 1), swizzled by row bit 2)
+    // per-lane LDS byte addresses (buffer 0); everything else is an instruction offset
+    const uint32_t lds0 = (uint32_t)(uintptr_t)lds;
+    const uint32_t kaddr = lds0 + (uint32_t)(g * 64 + c) * 16;     // K fragment reads
+    // V transposed reads: lane c = 4qq + p reads rows 4g + qq (+16 k, +32 j), columns
+    // 16t + 4p .. +3: chunk 2t + (p >> 1) XOR 2 (g & 1) (the image's swizzle, row bit 2 = g & 1)
     const int qq = c >> 2, pp = c & 3;
+    uint32_t vaddr[TD];
+#pragma unroll
+    for (int t = 0; t < TD; ++t)
+        vaddr[t] = lds0 + unit_v<DH>() * 16 + (4 * g + qq) * (2 * DH) +
+                   (((2 * t + (pp >> 1)) ^ ((g & 1) << 1)) * 16) + (pp & 1) * 8;
 
-    constexpr int PW = UN / 64 / 4;                              // DMA pieces per wave per tile
-    auto dma = [&](int t) {                                      // tile t -> buffer t & 1
-        const u32x4* src = tiles + t * tile_stride;
+    auto dma = [&](int t, auto buf_tag) {                        // tile t -> buffer BUF
+        constexpr int BUF = decltype(buf_tag)::value;
+        const u32x4* src = src_lane + (int64_t)t * tile_stride;
         __attribute__((address_space(3))) char* dst =
-            (__attribute__((address_space(3))) char*)(lds + (t & 1) * UN);
+            (__attribute__((address_space(3))) char*)(lds + BUF * UN) + wv * PW * 1024;
 #pragma unroll
-        for (int j = 0; j < PW; ++j) {
-            const int piece = wv + 4 * j;
-            __builtin_amdgcn_global_load_lds((const void*)(src + piece * 64 + lane),
-                                             (__attribute__((address_space(3))) void*)(dst + piece * 1024),
+        for (int j = 0; j < PW; ++j)
+            __builtin_amdgcn_global_load_lds((const void*)(src + j * 64),
+                                             (__attribute__((address_space(3))) void*)(dst + j * 1024),
                                              16, 0, 0);
-        }
     };
-    if constexpr (GLDS) {
-        if (ntile > 0) dma(0);
-    } else if (ntile > 0) {
-#pragma unroll
-        for (int i = 0; i < NS; ++i) stage[i] = tiles[tid + 256 * i];
-    }
-    // transposed V read offsets (byte, within the V part of a tile image): tile-invariant
-    int voff[2][TD][2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int t = 0; t < TD; ++t) {
-            const int r0 = 32 * j + 4 * g + qq, r1 = r0 + 16;
-            const int ch = 2 * t + (pp >> 1);
-            voff[j][t][0] = unit_v<DH>() * 16 + r0 * (2 * DH) +
-                            ((ch ^ (((r0 >> 2) & 1) << 1)) * 16) + (pp & 1) * 8;
-            voff[j][t][1] = unit_v<DH>() * 16 + r1 * (2 * DH) +
-                            ((ch ^ (((r1 >> 2) & 1) << 1)) * 16) + (pp & 1) * 8;
-        }
-    // one key tile; MASK only for the last, partial tile (no per-key selects elsewhere)
-    auto tile = [&](int tt, auto mask_tag) {
+    if (ntile > 0) dma(0, std::integral_constant<int, 0>{});
+
+    auto tile = [&](int tt, auto buf_tag, auto mask_tag) {
+        constexpr int BUF = decltype(buf_tag)::value;
         constexpr bool MASK = decltype(mask_tag)::value;
-        int2 e2;
-        const u32x4* tbuf;
-        if constexpr (GLDS) {
-            wait_vm_lgkm0_a<0>();           // this wave's pieces of tile tt landed
-            __builtin_amdgcn_s_barrier();   // everyone's landed; buffer (tt+1)&1 no longer read
-            if (tt + 1 < ntile) dma(tt + 1);
-            tbuf = lds + (tt & 1) * UN;
-            // block-uniform address: a scalar load (lgkmcnt), no wait on the DMA's vmcnt
-            e2 = sc[tile0 + (int64_t)__builtin_amdgcn_readfirstlane(tt) * n_head];
-        } else {
-            e2 = sc[tile0 + tt * n_head];
-            __syncthreads();
-#pragma unroll
-            for (int i = 0; i < NS; ++i) lds[tid + 256 * i] = stage[i];
-            __syncthreads();
-            if (tt + 1 < ntile) {
-                const u32x4* src = tiles + (tt + 1) * tile_stride;
-#pragma unroll
-                for (int i = 0; i < NS; ++i) stage[i] = src[tid + 256 * i];
-            }
-            tbuf = lds;
-        }
-        const uint32_t lb32 = (uint32_t)(uintptr_t)tbuf;
-        const int valid = nk - tt * 64;
+        wait_vm_lgkm0_a<0>();           // this wave's pieces of tile tt landed
+        __builtin_amdgcn_s_barrier();   // everyone's landed; buffer 1 - BUF no longer read
+        if (tt + 1 < ntile) dma(tt + 1, std::integral_constant<int, 1 - BUF>{});
+        const int2 e2 = sc[tile0 + (int64_t)__builtin_amdgcn_readfirstlane(tt) * n_head];
+        constexpr uint32_t BOFF = BUF * UN * 16;
+        typedef __attribute__((address_space(3))) u32x4 lds_u4;
+        typedef __attribute__((address_space(3))) s16x4 lds_s4;
 
         f32x4 s[4];
 #pragma unroll
@@ -285,38 +299,44 @@ attn_f16x3_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __rest
             f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int kd = 0; kd < KD; ++kd) {
-                const f16x8 kh = __builtin_bit_cast(f16x8, tbuf[((kd * 2 + 0) * 4 + g) * 64 + 16 * n + c]);
-                const f16x8 kl = __builtin_bit_cast(f16x8, tbuf[((kd * 2 + 1) * 4 + g) * 64 + 16 * n + c]);
+                const f16x8 kh = __builtin_bit_cast(
+                    f16x8, *(lds_u4*)(uintptr_t)(kaddr + BOFF + (((kd * 2 + 0) * 4) * 64 + 16 * n) * 16));
+                const f16x8 kl = __builtin_bit_cast(
+                    f16x8, *(lds_u4*)(uintptr_t)(kaddr + BOFF + (((kd * 2 + 1) * 4) * 64 + 16 * n) * 16));
                 a = __builtin_amdgcn_mfma_f32_16x16x32_f16(kl, qt[kd][0], a, 0, 0, 0);
                 a = __builtin_amdgcn_mfma_f32_16x16x32_f16(kh, qt[kd][1], a, 0, 0, 0);
                 a = __builtin_amdgcn_mfma_f32_16x16x32_f16(kh, qt[kd][0], a, 0, 0, 0);
             }
             s[n] = a;
         }
-        // s (scaled units) * f = log2-domain score; f > 0 so max commutes with it
         const float f = __builtin_ldexpf(1.f, -(e2.x + eq));
         if constexpr (MASK) {
+            const int valid = nk - tt * 64;
 #pragma unroll
             for (int n = 0; n < 4; ++n)
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
                     if (16 * n + 4 * g + r >= valid) s[n][r] = -INFINITY;
         }
-        float mx = s[0][0];
-#pragma unroll
-        for (int n = 0; n < 4; ++n)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[n][r]);
-        mx = xg_max16(mx) * f;
-        const float m_new = fmaxf(m_run, mx);          // finite: every tile has a valid key
+        float mx = vmax3(s[0][0], s[0][1], s[0][2]);
+        mx = vmax3(mx, s[0][3], s[1][0]);
+        mx = vmax3(mx, s[1][1], s[1][2]);
+        mx = vmax3(mx, s[1][3], s[2][0]);
+        mx = vmax3(mx, s[2][1], s[2][2]);
+        mx = vmax3(mx, s[2][3], s[3][0]);
+        mx = vmax3(mx, s[3][1], s[3][2]);
+        mx = vmax2(mx, s[3][3]);
+        mx = xg_max16_nc(mx) * f;
+        const float m_new = vmax2(m_run, mx);           // finite: every tile has a valid key
         const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
         m_run = m_new;
+        const float m14 = m_new - 14.f;                 // p14 = 2^14 p, in fp16's range
         float rs = 0.f;
 #pragma unroll
         for (int n = 0; n < 4; ++n)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[n][r], f, -m_new));
+                const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[n][r], f, -m14));
                 s[n][r] = p;
                 rs += p;
             }
@@ -328,46 +348,53 @@ attn_f16x3_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __rest
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             // P^T operand of step j (keys 32j + 4g + {0..3}, 32j + 16 + 4g + {0..3})
-            f16x8 pt[2];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                _Float16 h, m;
-                split2(s[2 * j + (e >> 2)][e & 3] * kPScale, h, m);
-                pt[0][e] = h; pt[1][e] = m;
-            }
+            const float pv[8] = {s[2 * j][0], s[2 * j][1], s[2 * j][2], s[2 * j][3],
+                                 s[2 * j + 1][0], s[2 * j + 1][1], s[2 * j + 1][2], s[2 * j + 1][3]};
+            u32x4 ph, pl;
+            split8_pk(pv, one, ph, pl);
+            const f16x8 pt0 = __builtin_bit_cast(f16x8, ph), pt1 = __builtin_bit_cast(f16x8, pl);
 #pragma unroll
             for (int t = 0; t < TD; ++t) {
                 f16x8 vf[2];
 #pragma unroll
                 for (int tm = 0; tm < 2; ++tm) {
-                    typedef __attribute__((address_space(3))) s16x4 lds_s4;
-                    // 32-bit LDS byte addresses (no 64-bit pointer arithmetic per read)
-                    const uint32_t vb = lb32 + tm * (128 * DH);
-                    const s16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                        (lds_s4*)(uintptr_t)(vb + voff[j][t][0]));
+                    const uint32_t vb = vaddr[t] + BOFF + tm * (128 * DH) + j * 32 * (2 * DH);
+                    const s16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(uintptr_t)vb);
                     const s16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                        (lds_s4*)(uintptr_t)(vb + voff[j][t][1]));
-                    const s16x8 w8 = __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7);
-                    vf[tm] = __builtin_bit_cast(f16x8, w8);
+                        (lds_s4*)(uintptr_t)(vb + 16 * (2 * DH)));
+                    vf[tm] = __builtin_bit_cast(f16x8, __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7));
                 }
                 f32x4 a = tmp[t];
-                a = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf[1], pt[0], a, 0, 0, 0);
-                a = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf[0], pt[1], a, 0, 0, 0);
-                a = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf[0], pt[0], a, 0, 0, 0);
+                a = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf[1], pt0, a, 0, 0, 0);
+                a = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf[0], pt1, a, 0, 0, 0);
+                a = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf[0], pt0, a, 0, 0, 0);
                 tmp[t] = a;
             }
         }
-        const float fv = __builtin_ldexpf(1.f, -(e2.y + 14));
+        const float fv = __builtin_ldexpf(1.f, -e2.y);   // p14's 2^14 cancels against l's
 #pragma unroll
         for (int t = 0; t < TD; ++t)
 #pragma unroll
             for (int r = 0; r < 4; ++r) acc[t][r] = __builtin_fmaf(tmp[t][r], fv, acc[t][r] * alpha);
     };
+    using B0 = std::integral_constant<int, 0>;
+    using B1 = std::integral_constant<int, 1>;
     const int nfull = nk / 64;                       // tiles with 64 valid keys
-    for (int tt = 0; tt < nfull; ++tt) tile(tt, std::false_type{});
-    if (nfull < ntile) tile(nfull, std::true_type{});
+    int tt = 0;
+    for (; tt + 2 <= nfull; tt += 2) {
+        tile(tt, B0{}, std::false_type{});
+        tile(tt + 1, B1{}, std::false_type{});
+    }
+    if (tt < nfull) {                                // tt even: buffer 0
+        tile(tt, B0{}, std::false_type{});
+        ++tt;
+    }
+    if (tt < ntile) {
+        if (tt & 1) tile(tt, B1{}, std::true_type{});
+        else tile(tt, B0{}, std::true_type{});
+    }
 
-    // O^T (dh 16t + 4g + r, query c) / l
+    // O^T (dh 16t + 4g + r, query c) / l (both in 2^14 units)
     const float inv = 1.0f / xg_sum16(l_run);
     if (qrow < qe) {
 #pragma unroll
@@ -438,29 +465,15 @@ extern "C" int fgr_attention_f16x3(const float* q, int64_t ld_q, const float* k,
     FGR_CHECK_LAUNCH("attn_kv_image16_kernel");
     const int n_qblk = (int)ceil_div(max_q_len, 64);
     const int64_t n_blocks = ceil_div((int64_t)n_seg * n_head, 8) * 8 * n_qblk;
-    // LDS-DMA K/V staging (measured: head dim 64 57 -> 42 us per launch on the 3DMatch
-    // forward although its 2 x 32-KB buffers halve the blocks per CU; head dim 32 on par)
-    // FGR_ATTN_GLDS=0 selects the
-    // register-staged loop (A/B)
-    const char* gl = getenv("FGR_ATTN_GLDS");
-    const bool glds = !(gl && gl[0] == '0');
     const float sl2 = scale * 1.4426950408889634f;
-    if (dh == 32 && glds)
-        hipLaunchKernelGGL((attn_f16x3_kernel<32, true>), dim3((unsigned)n_blocks), dim3(256), 0, st,
-                           q, ld_q, (const uint4*)img, (const int2*)sc, o, ld_o, q_off, kv_off,
-                           kv_seg, n_head, n_seg, n_qblk, sl2);
-    else if (dh == 32)
-        hipLaunchKernelGGL((attn_f16x3_kernel<32, false>), dim3((unsigned)n_blocks), dim3(256), 0,
-                           st, q, ld_q, (const uint4*)img, (const int2*)sc, o, ld_o, q_off, kv_off,
-                           kv_seg, n_head, n_seg, n_qblk, sl2);
-    else if (glds)
-        hipLaunchKernelGGL((attn_f16x3_kernel<64, true>), dim3((unsigned)n_blocks), dim3(256), 0, st,
-                           q, ld_q, (const uint4*)img, (const int2*)sc, o, ld_o, q_off, kv_off,
-                           kv_seg, n_head, n_seg, n_qblk, sl2);
+    if (dh == 32)
+        hipLaunchKernelGGL((attn_f16x3_v2_kernel<32>), dim3((unsigned)n_blocks), dim3(256), 0, st, q,
+                           ld_q, (const uint4*)img, (const int2*)sc, o, ld_o, q_off, kv_off, kv_seg,
+                           n_head, n_seg, n_qblk, sl2);
     else
-        hipLaunchKernelGGL((attn_f16x3_kernel<64, false>), dim3((unsigned)n_blocks), dim3(256), 0,
-                           st, q, ld_q, (const uint4*)img, (const int2*)sc, o, ld_o, q_off, kv_off,
-                           kv_seg, n_head, n_seg, n_qblk, sl2);
-    FGR_CHECK_LAUNCH("attn_f16x3_kernel");
+        hipLaunchKernelGGL((attn_f16x3_v2_kernel<64>), dim3((unsigned)n_blocks), dim3(256), 0, st, q,
+                           ld_q, (const uint4*)img, (const int2*)sc, o, ld_o, q_off, kv_off, kv_seg,
+                           n_head, n_seg, n_qblk, sl2);
+    FGR_CHECK_LAUNCH("attn_f16x3_v2_kernel");
     return FGR_OK;
 }

@@ -17,6 +17,8 @@
 // * fgr_attention_bf16: the flash attention of attention16.hip with single-term bf16 K / V
 //   images ([k-step][g 4][key 64] / [key 64][DH] with the ds_read_b64_tr_b16 swizzle), Q and
 //   P rounded to bf16 in registers, head_dim 32 or 64.
+#include <type_traits>
+
 #include "common.h"
 
 namespace fgr {
@@ -261,14 +263,23 @@ attn_kv_image_bf16_kernel(const float* __restrict__ k, int64_t ld_k, const float
     }
 }
 
+// v2 key-tile loop (as attention16.hip's attn_f16x3_v2_kernel): maxima by v_max3 without NaN
+// canonicalisation, the tile loop unrolled by two so both LDS buffers' addresses are per-lane
+// constants + instruction offsets, DMA pieces contiguous per wave; built -fno-slp-vectorize.
+// The round-2 loop issued ~14 VALU per MFMA at head dim 32 (profiles/r03_pmc_attn_v1_before.json).
+// (plain fmaxf: the file is built -fno-honor-nans; see attention16.hip)
+__device__ __forceinline__ float vmax3b(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
+__device__ __forceinline__ float vmax2b(float a, float b) { return fmaxf(a, b); }
+
 template <int DH>
 __global__ void __launch_bounds__(256, 4)
-attn_bf16_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __restrict__ img,
-                 float* __restrict__ o, int64_t ld_o, const int64_t* __restrict__ q_off,
-                 const int64_t* __restrict__ kv_off, const int32_t* __restrict__ kv_seg,
-                 int n_head, int n_seg, int n_qblk, float scale_log2) {
+attn_bf16_v2_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __restrict__ img,
+                    float* __restrict__ o, int64_t ld_o, const int64_t* __restrict__ q_off,
+                    const int64_t* __restrict__ kv_off, const int32_t* __restrict__ kv_seg,
+                    int n_head, int n_seg, int n_qblk, float scale_log2) {
     constexpr int KD = DH / 32, TD = DH / 16;
     constexpr int UN = bf_units<DH>();
+    constexpr int PW = UN / 64 / 4;
     __shared__ u32x4 lds[2 * UN];
     const int L = blockIdx.x, xcd = L & 7, j0 = L >> 3;
     const int pair = (j0 / n_qblk) * 8 + xcd, qblk = j0 % n_qblk;
@@ -282,10 +293,10 @@ attn_bf16_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __restr
     const int nk = (int)(kv_off[ks + 1] - kb);
     const int ntile = (nk + 63) / 64;
     const int64_t tile0 = (kb / 64 + ks) * n_head + head;
-    const u32x4* tiles = reinterpret_cast<const u32x4*>(img) + tile0 * UN;
     const int64_t tile_stride = (int64_t)n_head * UN;
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
     const int g = lane >> 4, c = lane & 15;
+    const u32x4* src_lane = reinterpret_cast<const u32x4*>(img) + tile0 * UN + wv * PW * 64 + lane;
 
     const int64_t qrow = q0 + wv * 16 + c;
     bf16x8 qt[KD];
@@ -305,30 +316,35 @@ attn_bf16_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __restr
 #pragma unroll
     for (int t = 0; t < TD; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
     float m_run = -INFINITY, l_run = 0.f;
-    // K/V tiles by LDS-DMA into two buffers: tile t + 1 in flight while tile t is computed,
-    // one barrier per tile (as attention16.hip's f16x3 loop)
+    const uint32_t lds0 = (uint32_t)(uintptr_t)lds;
+    const uint32_t kaddr = lds0 + (uint32_t)(g * 64 + c) * 16;
     const int qq = c >> 2, pp = c & 3;
-    constexpr int PW = UN / 64 / 4;                              // DMA pieces per wave per tile
-    auto dma = [&](int t) {
-        const u32x4* src = tiles + t * tile_stride;
-        __attribute__((address_space(3))) char* dst =
-            (__attribute__((address_space(3))) char*)(lds + (t & 1) * UN);
+    uint32_t vaddr[TD];
 #pragma unroll
-        for (int j = 0; j < PW; ++j) {
-            const int piece = wv + 4 * j;
-            __builtin_amdgcn_global_load_lds((const void*)(src + piece * 64 + lane),
-                                             (__attribute__((address_space(3))) void*)(dst + piece * 1024),
+    for (int t = 0; t < TD; ++t)
+        vaddr[t] = lds0 + bf_unit_v<DH>() * 16 + (4 * g + qq) * (2 * DH) +
+                   (((2 * t + (pp >> 1)) ^ ((g & 1) << 1)) * 16) + (pp & 1) * 8;
+    auto dma = [&](int t, auto buf_tag) {
+        constexpr int BUF = decltype(buf_tag)::value;
+        const u32x4* src = src_lane + (int64_t)t * tile_stride;
+        __attribute__((address_space(3))) char* dst =
+            (__attribute__((address_space(3))) char*)(lds + BUF * UN) + wv * PW * 1024;
+#pragma unroll
+        for (int j = 0; j < PW; ++j)
+            __builtin_amdgcn_global_load_lds((const void*)(src + j * 64),
+                                             (__attribute__((address_space(3))) void*)(dst + j * 1024),
                                              16, 0, 0);
-        }
     };
-    if (ntile > 0) dma(0);
-    for (int tt = 0; tt < ntile; ++tt) {
+    if (ntile > 0) dma(0, std::integral_constant<int, 0>{});
+    auto tile = [&](int tt, auto buf_tag, auto mask_tag) {
+        constexpr int BUF = decltype(buf_tag)::value;
+        constexpr bool MASK = decltype(mask_tag)::value;
         __builtin_amdgcn_s_waitcnt((7 << 4));                    // vmcnt(0) lgkmcnt(0)
         __builtin_amdgcn_s_barrier();
-        if (tt + 1 < ntile) dma(tt + 1);
-        const u32x4* tbuf = lds + (tt & 1) * UN;
-        const char* lbase = reinterpret_cast<const char*>(tbuf);
-        const int valid = nk - tt * 64;
+        if (tt + 1 < ntile) dma(tt + 1, std::integral_constant<int, 1 - BUF>{});
+        constexpr uint32_t BOFF = BUF * UN * 16;
+        typedef __attribute__((address_space(3))) u32x4 lds_u4;
+        typedef __attribute__((address_space(3))) s16x4 lds_s4;
         f32x4 s[4];
 #pragma unroll
         for (int n = 0; n < 4; ++n) {
@@ -336,23 +352,33 @@ attn_bf16_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __restr
 #pragma unroll
             for (int kd = 0; kd < KD; ++kd)
                 a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                    __builtin_bit_cast(bf16x8, tbuf[(kd * 4 + g) * 64 + 16 * n + c]), qt[kd], a, 0, 0, 0);
+                    __builtin_bit_cast(bf16x8, *(lds_u4*)(uintptr_t)(kaddr + BOFF + ((kd * 4) * 64 + 16 * n) * 16)),
+                    qt[kd], a, 0, 0, 0);
             s[n] = a;
         }
-        if (valid < 64) {
+        if constexpr (MASK) {
+            const int valid = nk - tt * 64;
 #pragma unroll
             for (int n = 0; n < 4; ++n)
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
                     if (16 * n + 4 * g + r >= valid) s[n][r] = -INFINITY;
         }
-        float mx = s[0][0];
-#pragma unroll
-        for (int n = 0; n < 4; ++n)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[n][r]);
-        mx = xg_max16b(mx);
-        const float m_new = fmaxf(m_run, mx);
+        float mx = vmax3b(s[0][0], s[0][1], s[0][2]);
+        mx = vmax3b(mx, s[0][3], s[1][0]);
+        mx = vmax3b(mx, s[1][1], s[1][2]);
+        mx = vmax3b(mx, s[1][3], s[2][0]);
+        mx = vmax3b(mx, s[2][1], s[2][2]);
+        mx = vmax3b(mx, s[2][3], s[3][0]);
+        mx = vmax3b(mx, s[3][1], s[3][2]);
+        mx = vmax2b(mx, s[3][3]);
+        {
+            auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+            mx = vmax2b(__uint_as_float(a[0]), __uint_as_float(a[1]));
+            auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+            mx = vmax2b(__uint_as_float(b[0]), __uint_as_float(b[1]));
+        }
+        const float m_new = vmax2b(m_run, mx);
         const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
         m_run = m_new;
         float rs = 0.f;
@@ -376,21 +402,31 @@ attn_bf16_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __restr
             for (int e = 0; e < 8; ++e) pt[e] = (__bf16)s[2 * j + (e >> 2)][e & 3];
 #pragma unroll
             for (int t = 0; t < TD; ++t) {
-                const int r0 = 32 * j + 4 * g + qq, r1 = r0 + 16;
-                const int ch = 2 * t + (pp >> 1);
-                const int off0 = r0 * (2 * DH) + ((ch ^ (((r0 >> 2) & 1) << 1)) * 16) + (pp & 1) * 8;
-                const int off1 = r1 * (2 * DH) + ((ch ^ (((r1 >> 2) & 1) << 1)) * 16) + (pp & 1) * 8;
-                typedef __attribute__((address_space(3))) s16x4 lds_s4;
-                const char* vb = lbase + bf_unit_v<DH>() * 16;
-                const s16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                    (lds_s4*)(uintptr_t)(uint32_t)(uintptr_t)(vb + off0));
+                const uint32_t vb = vaddr[t] + BOFF + j * 32 * (2 * DH);
+                const s16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(uintptr_t)vb);
                 const s16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                    (lds_s4*)(uintptr_t)(uint32_t)(uintptr_t)(vb + off1));
+                    (lds_s4*)(uintptr_t)(vb + 16 * (2 * DH)));
                 const s16x8 w8 = __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7);
                 acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, w8), pt,
                                                                  acc[t], 0, 0, 0);
             }
         }
+    };
+    using B0 = std::integral_constant<int, 0>;
+    using B1 = std::integral_constant<int, 1>;
+    const int nfull = nk / 64;
+    int tt = 0;
+    for (; tt + 2 <= nfull; tt += 2) {
+        tile(tt, B0{}, std::false_type{});
+        tile(tt + 1, B1{}, std::false_type{});
+    }
+    if (tt < nfull) {
+        tile(tt, B0{}, std::false_type{});
+        ++tt;
+    }
+    if (tt < ntile) {
+        if (tt & 1) tile(tt, B1{}, std::true_type{});
+        else tile(tt, B0{}, std::true_type{});
     }
     const float inv = 1.0f / xg_sum16b(l_run);
     if (qrow < qe) {
@@ -564,15 +600,15 @@ extern "C" int fgr_attention_bf16(const float* q, int64_t ld_q, const float* k, 
         hipLaunchKernelGGL(attn_kv_image_bf16_kernel<32>, kgrid, dim3(256), 0, st, k, ld_k, v, ld_v,
                            kv_off, n_head, img);
         FGR_CHECK_LAUNCH("attn_kv_image_bf16_kernel");
-        hipLaunchKernelGGL(attn_bf16_kernel<32>, dim3(nb), dim3(256), 0, st, q, ld_q,
-                           (const uint4*)img, o, ld_o, q_off, kv_off, kv_seg, n_head, n_seg, n_qblk, sl2);
+        hipLaunchKernelGGL(attn_bf16_v2_kernel<32>, dim3(nb), dim3(256), 0, st, q, ld_q,
+                               (const uint4*)img, o, ld_o, q_off, kv_off, kv_seg, n_head, n_seg, n_qblk, sl2);
     } else {
         hipLaunchKernelGGL(attn_kv_image_bf16_kernel<64>, kgrid, dim3(256), 0, st, k, ld_k, v, ld_v,
                            kv_off, n_head, img);
         FGR_CHECK_LAUNCH("attn_kv_image_bf16_kernel");
-        hipLaunchKernelGGL(attn_bf16_kernel<64>, dim3(nb), dim3(256), 0, st, q, ld_q,
-                           (const uint4*)img, o, ld_o, q_off, kv_off, kv_seg, n_head, n_seg, n_qblk, sl2);
+        hipLaunchKernelGGL(attn_bf16_v2_kernel<64>, dim3(nb), dim3(256), 0, st, q, ld_q,
+                               (const uint4*)img, o, ld_o, q_off, kv_off, kv_seg, n_head, n_seg, n_qblk, sl2);
     }
-    FGR_CHECK_LAUNCH("attn_bf16_kernel");
+    FGR_CHECK_LAUNCH("attn_bf16_v2_kernel");
     return FGR_OK;
 }

@@ -172,18 +172,16 @@ def test_attention_vs_torch(gpu, nhead, d):
         assert rel_err(out, ref) < TOL
 
 
-@pytest.mark.parametrize('glds', ['0', '1'])
 @pytest.mark.parametrize('split,d', [('bf16x6', 256), ('f16x3', 256), ('f16x3', 512)])
 @pytest.mark.parametrize('scale', [1.0, 6.0, 1e-6, 3e3])
-def test_attention_split_is_fp32_accurate(gpu, scale, split, d, glds, monkeypatch):
+def test_attention_split_is_fp32_accurate(gpu, scale, split, d):
     """The split attentions (fgr_attention_bf16x6 dh = 32; _f16x3 dh = 32 and 64) against a float64
     reference: error at fp32 level (<= 1e-5 normwise) and no worse than a few times the
     fp32-MFMA kernel's own error; separate key segmentation (kv lengths != q lengths,
     max_kv_len > max_q_len), partial and 1-key tiles, sharp softmax at scale 6, inputs far
     outside fp16's range (1e-6: subnormal in fp16 unscaled; 3e3: products past 65504).
-    f16x3 with both K/V staging loops (FGR_ATTN_GLDS: register-staged / LDS-DMA)."""
+    """
     import fgreg.ops as ops
-    monkeypatch.setenv('FGR_ATTN_GLDS', glds)
     rng = np.random.default_rng(7)
     nhead = 8
     qlens = [300, 1, 64, 129]
