@@ -52,19 +52,14 @@ HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md, chip tabl
 FP32_MFMA_PEAK_TFLOPS = 157.3
 F16_MFMA_PEAK_TFLOPS = 2500.0    # fp16 / bf16 dense (MI355X_MICROARCH.md)
 # matrix-core products issued per fp32-equivalent product, by precision mode
-PIPE = {'f16x3': 3, 'bf16x6': 6, 'bf16x3': 3, 'bf16': 1, 'fp32': 1}
+PIPE = {'f16x3': 3, 'bf16': 1}
 PRECISION = {'f16x3': 'fp32-accurate scaled split fp16 (3 fp16 MFMA products per fp32 '
                       'product, <= ~3 * 2^-22 relative each)',
-             'bf16x6': 'fp32-accurate split bf16 (6 bf16 MFMA products per fp32 product)',
-             'bf16x3': 'split bf16, 3 products (~2^-17 relative)',
              'bf16': 'bf16 (one bf16 MFMA product per product, fp32 accumulation, ~2^-9 '
-                     'relative per product)',
-             'fp32': 'fp32 MFMA / hipBLASLt fp32'}
+                     'relative per product)'}
 DTYPE = {'f16x3': 'f32 (emulated on the fp16 MFMA pipe: f16x3 split products)',
-         'bf16x6': 'f32 (emulated on the bf16 MFMA pipe: bf16x6 split products)',
          'bf16': 'bf16 (bf16 MFMA GEMMs + attention; fp32 accumulation, storage, norms, '
-                 'geometry and pose)',
-         'fp32': 'f32'}
+                 'geometry and pose)'}
 
 DATA = {
     'modelnet': 'synthetic ModelNet40-shaped pairs: 2048-pt box-surface raw clouds through the '
@@ -258,7 +253,7 @@ def main():
             torch.cuda.synchronize()
         else:
             # algorithmic work per launch (untimed pass with counting on)
-            fams = ['kpconv_gather', 'kpconv_fused', 'attention', 'gemm'] + list(OTHER)
+            fams = ['kpconv_gather', 'attention', 'gemm'] + list(OTHER)
             timer = ops.KernelTimer(fams)
             timer.count = True
             ops.TIMER = timer
@@ -304,7 +299,7 @@ def main():
         'metric': METRIC[wl], 'value': n_total * args.steps / elapsed, 'unit': 'pairs/s',
         'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': step_ms,
         'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
-        'dtype': DTYPE.get(lin.MODE, lin.MODE), 'data': DATA[wl],
+        'dtype': DTYPE[lin.MODE], 'data': DATA[wl],
         'config': {'workload': WORKLOAD[wl].format(P=P), 'pairs_per_gpu': P,
                    'global_batch': n_total,
                    'points_per_cloud': int(np.mean([len(c) for c in src])),
@@ -348,36 +343,20 @@ def main():
             'timing': 'HIP events recorded by libfgreg around each launch (fgr_time_next_call), '
                       'eager replay of the timed steps'}
 
-    # the KPConv stage: the fused gather + GEMM kernel where it runs (D4 bytes with the wf
-    # write replaced by the 4 Cout output row), else the gather-weight kernel
-    fused = bool(work['kpconv_fused'])
-    if fused:
-        line['roofline'] = kpconv_roofline('kpconv_fused', 'fgr_kpconv_fused')
-        fl = float(sum(2.0 * m * n * k for (m, n, k) in rtimer.labels['kpconv_fused']))
-        ms_f = rtimer.total_ms('kpconv_fused')
-        pipe = PIPE.get(lin.MODE, 1)
-        mpk = F16_MFMA_PEAK_TFLOPS / pipe
-        ach_tf = fl / (ms_f / 1e3) / 1e12 if ms_f > 0 else 0.0
-        line['roofline']['mfma'] = {
-            'flops_per_step': fl / args.steps, 'achieved': ach_tf, 'peak': mpk,
-            'unit': 'TFLOP/s (fp32-equivalent)', 'frac': ach_tf / mpk,
-            'note': 'the weight contraction 2 Nq K Cin Cout of the same launches'}
-    if work['kpconv_gather']:
-        line['roofline' if not fused else 'roofline_kpconv_gather'] = kpconv_roofline(
-            'kpconv_gather', 'fgr_kpconv_gather')
+    # the KPConv stage's gather-weight kernel (the dominant HBM-bound kernel)
+    line['roofline'] = kpconv_roofline('kpconv_gather', 'fgr_kpconv_gather')
 
     def mfma_family(name, mode, kernel):
         ms = rtimer.total_ms(name)
         flops = float(sum(work[name]))
         ach = flops * args.steps / (ms / 1e3) / 1e12 if ms > 0 else 0.0
-        pipe = PIPE.get(mode, 1)
-        peak = (F16_MFMA_PEAK_TFLOPS / pipe) if mode != 'fp32' else FP32_MFMA_PEAK_TFLOPS
+        pipe = PIPE[mode]
+        peak = F16_MFMA_PEAK_TFLOPS / pipe
         return {'kernel': kernel, 'bound': 'mfma', 'achieved': ach, 'peak': peak,
                 'unit': 'TFLOP/s (fp32-equivalent)', 'frac': ach / peak,
                 'peak_note': (f'fp16 dense MFMA {F16_MFMA_PEAK_TFLOPS:.0f} TF / {pipe} products '
                               f'per fp32-equivalent product; vs the {FP32_MFMA_PEAK_TFLOPS} TF '
-                              f'fp32-MFMA peak this would read {ach / FP32_MFMA_PEAK_TFLOPS:.2f}'
-                              if mode != 'fp32' else 'fp32 MFMA peak'),
+                              f'fp32-MFMA peak this would read {ach / FP32_MFMA_PEAK_TFLOPS:.2f}'),
                 'flops_per_step': flops, 'launches_per_step': len(work[name]),
                 'avg_launch_us': ms * 1e3 / max(len(rtimer.events[name]), 1),
                 'share_of_step': ms / args.steps / step_ms,
@@ -419,9 +398,9 @@ def write_gemm_table(path, rtimer, steps, step_ms, mode):
     roof per shape). bytes = the minimum operand traffic 4 M K (A) + 4 N K (f16x3 image:
     2 terms x 2 B; 2 N K for the single-term bf16 image) + 4 M N (C), assuming every operand
     is read once."""
-    pipe = PIPE.get(mode, 1)
+    pipe = PIPE[mode]
     wb = 2.0 if mode == 'bf16' else 4.0
-    mfma_peak = (F16_MFMA_PEAK_TFLOPS / pipe) if mode != 'fp32' else FP32_MFMA_PEAK_TFLOPS
+    mfma_peak = F16_MFMA_PEAK_TFLOPS / pipe
     rows = []
     for (m, n, k), (ms, cnt) in sorted(rtimer.per_label('gemm').items(),
                                        key=lambda kv: -kv[1][0]):

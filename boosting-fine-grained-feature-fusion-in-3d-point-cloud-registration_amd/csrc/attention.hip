@@ -362,291 +362,6 @@ void launch(dim3 grid, hipStream_t st, const float* q, int64_t ld_q, const float
                        ld_o, q_off, kv_off, kv_seg, scale);
 }
 
-
-// ------------------------------------------------------------------------------------
-// bf16x6 (head_dim 32): fp32-accurate attention on the bf16 matrix cores.
-//
-// Every fp32 operand x is split exactly into three bf16 terms x = h + m + l
-// (h = bf16(x), m = bf16(x - h), l = bf16(x - h - m); residual <= 2^-27 |x|) and each
-// product is accumulated in fp32 from the six terms that matter,
-//   hh + hm + mh + hl + lh + mm     (dropped: ml, lm, ll ~ 2^-27 relative),
-// i.e. fp32-level accuracy (the fp32 MFMA's own products round at 2^-24) at
-// 6 x 16 = 96 cycles per 16x16x32 step instead of 8 x 32 = 256 on v_mfma_f32_16x16x4_f32.
-//
-// Swapped products keep every softmax row lane-local (no LDS round trip for P):
-//   S^T[key][query] = K Q^T     A = K (LDS image), B = Q (registers, split once)
-//   O^T[dh][query] += V^T P^T   A = V (LDS, ds_read_b64_tr_b16), B = P (registers)
-// 16x16x32 bf16 lane maps (lane l, g = l >> 4, c = l & 15):
-//   A[i = c][k = 8g + e], B[k = 8g + e][j = c], C[i = 4g + r][j = c].
-// Lane (g, c) thus owns query c; its S^T values are keys 16n + 4g + r of each 16-key
-// subtile n, and the 8 k-slots of PV step j are keys 32j + 4g + {0..3} and
-// 32j + 16 + 4g + {0..3} -- exactly its own P values, so P is the B operand as is.
-// Row max needs the 4 lanes c, c+16, c+32, c+48 (permlane16/32 swaps); the row sum is
-// kept per lane and reduced once at the end.
-//
-// K/V are split once per call by attn_kv_image_kernel into per-(tile, head) images of
-// 64 keys (24 KB, laid out exactly as the LDS tile, so staging is a flat copy):
-//   K: [term 3][g 4][key 64] x 16 B (8 dims) -- ds_read_b128, conflict-free
-//   V: [term 3][key 64][32 dh] bf16, 16-B chunk index XOR ((key >> 2) & 1) << 1 so the
-//      transposed reads of 8 consecutive keys are conflict-free.
-// Tile t of kv segment s lives at tile index kv_off[s] / 64 + s + t (O(1), no table).
-// ------------------------------------------------------------------------------------
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-typedef short s16x8 __attribute__((ext_vector_type(8)));
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-constexpr int kImgUnits = 1536;          // 16-B units per (tile, head) image
-constexpr int kImgV = 768;               // first V unit
-
-__device__ __forceinline__ void split3(float x, __bf16& h, __bf16& m, __bf16& l) {
-    h = (__bf16)x;
-    const float r = x - (float)h;        // exact
-    m = (__bf16)r;
-    l = (__bf16)(r - (float)m);          // exact difference, rounded once
-}
-
-__device__ __forceinline__ float xg_max(float v) {   // max over lanes c, c^16, c^32, c^48
-    auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
-    auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
-}
-__device__ __forceinline__ float xg_sum(float v) {
-    auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
-    auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    return __uint_as_float(b[0]) + __uint_as_float(b[1]);
-}
-
-__global__ void __launch_bounds__(256)
-attn_kv_image_kernel(const float* __restrict__ k, int64_t ld_k, const float* __restrict__ v,
-                     int64_t ld_v, const int64_t* __restrict__ kv_off, int n_head,
-                     uint4* __restrict__ img) {
-    const int s = blockIdx.z, h = blockIdx.y, tt = blockIdx.x;
-    const int64_t kb = kv_off[s];
-    const int nk = (int)(kv_off[s + 1] - kb);
-    if (tt * 64 >= nk) return;
-    char* base = reinterpret_cast<char*>(img + ((kb / 64 + s + tt) * n_head + h) * kImgUnits);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int e = threadIdx.x + 256 * i;           // float4 of the 64 x 32 tile
-        const int key = e >> 3, d0 = (e & 7) * 4;
-        const bool ok = tt * 64 + key < nk;
-        const int64_t row = kb + tt * 64 + key;
-        const float4 kx = ok ? *reinterpret_cast<const float4*>(k + row * ld_k + h * 32 + d0)
-                             : make_float4(0.f, 0.f, 0.f, 0.f);
-        const float4 vx = ok ? *reinterpret_cast<const float4*>(v + row * ld_v + h * 32 + d0)
-                             : make_float4(0.f, 0.f, 0.f, 0.f);
-        const float kf[4] = {kx.x, kx.y, kx.z, kx.w}, vf[4] = {vx.x, vx.y, vx.z, vx.w};
-        __bf16 kt[3][4], vt[3][4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            split3(kf[j], kt[0][j], kt[1][j], kt[2][j]);
-            split3(vf[j], vt[0][j], vt[1][j], vt[2][j]);
-        }
-        const int g = d0 >> 3, half = (d0 >> 2) & 1;
-        const int vch = (d0 >> 3) ^ (((key >> 2) & 1) << 1);
-#pragma unroll
-        for (int t = 0; t < 3; ++t) {
-            *reinterpret_cast<uint2*>(base + ((t * 4 + g) * 64 + key) * 16 + half * 8) =
-                *reinterpret_cast<const uint2*>(kt[t]);
-            *reinterpret_cast<uint2*>(base + kImgV * 16 + t * 4096 + key * 64 + vch * 16 + half * 8) =
-                *reinterpret_cast<const uint2*>(vt[t]);
-        }
-    }
-}
-
-template <int RG>
-__global__ void __launch_bounds__(256, RG == 2 ? 3 : 4)
-attn_bf16x6_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __restrict__ img,
-                   float* __restrict__ o, int64_t ld_o, const int64_t* __restrict__ q_off,
-                   const int64_t* __restrict__ kv_off, const int32_t* __restrict__ kv_seg,
-                   int n_head, int n_seg, int n_qblk, float scale_log2) {
-    constexpr int BQ = 64 * RG;
-    __shared__ u32x4 lds[kImgUnits];
-    // XCD-aware block order: workgroups are dispatched round-robin over the 8 XCDs, so
-    // linear id L runs on XCD L % 8. All q-blocks of one (segment, head) get ids of one
-    // residue mod 8 and run on one XCD, whose L2 then serves the shared K/V image.
-    const int L = blockIdx.x, xcd = L & 7, j = L >> 3;
-    const int pair = (j / n_qblk) * 8 + xcd, qblk = j % n_qblk;
-    if (pair >= n_seg * n_head) return;
-    const int seg = pair / n_head, head = pair % n_head;
-    const int64_t qb = q_off[seg], qe = q_off[seg + 1];
-    const int64_t q0 = qb + (int64_t)qblk * BQ;
-    if (q0 >= qe) return;                              // block-uniform
-    const int ks = kv_seg[seg];
-    const int64_t kb = kv_off[ks];
-    const int nk = (int)(kv_off[ks + 1] - kb);
-    const int ntile = (nk + 63) / 64;
-    const u32x4* tiles = reinterpret_cast<const u32x4*>(img) + (kb / 64 + ks) * n_head * kImgUnits + (int64_t)head * kImgUnits;
-    const int64_t tile_stride = (int64_t)n_head * kImgUnits;
-    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
-    const int g = lane >> 4, c = lane & 15;
-
-    // Q^T operand (B): lane (g, c) holds q[query c][8g .. 8g+7] * scale * log2(e), split
-    bf16x8 qt[RG][3];
-#pragma unroll
-    for (int rg = 0; rg < RG; ++rg) {
-        const int64_t row = q0 + wv * 16 * RG + rg * 16 + c;
-        float x[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        if (row < qe) {
-            const float4* p = reinterpret_cast<const float4*>(q + row * ld_q + head * 32 + 8 * g);
-            const float4 a = p[0], b = p[1];
-            x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
-            x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
-        }
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            __bf16 h, m, l;
-            split3(x[e] * scale_log2, h, m, l);
-            qt[rg][0][e] = h; qt[rg][1][e] = m; qt[rg][2][e] = l;
-        }
-    }
-    f32x4 acc[RG][2];
-    float m_run[RG], l_run[RG];
-#pragma unroll
-    for (int rg = 0; rg < RG; ++rg) {
-        acc[rg][0] = f32x4{0.f, 0.f, 0.f, 0.f};
-        acc[rg][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-        m_run[rg] = -INFINITY;
-        l_run[rg] = 0.f;
-    }
-
-    u32x4 stage[6];
-    const char* lbase = reinterpret_cast<const char*>(lds);
-    // transposed-read addresses of V: lane c = 4qq + p reads row 4g + qq (+16, +32j),
-    // columns 16t + 4p .. +3 (chunk 2t + (p >> 1), swizzled by row bit 2)
-    const int qq = c >> 2, pp = c & 3;
-
-    if (ntile > 0) {
-#pragma unroll
-        for (int i = 0; i < 6; ++i) stage[i] = tiles[tid + 256 * i];
-    }
-    for (int tt = 0; tt < ntile; ++tt) {
-        __syncthreads();
-#pragma unroll
-        for (int i = 0; i < 6; ++i) lds[tid + 256 * i] = stage[i];
-        __syncthreads();
-        if (tt + 1 < ntile) {
-            const u32x4* src = tiles + (tt + 1) * tile_stride;
-#pragma unroll
-            for (int i = 0; i < 6; ++i) stage[i] = src[tid + 256 * i];
-        }
-        const int valid = nk - tt * 64;
-
-        f32x4 s[RG][4];
-#pragma unroll
-        for (int n = 0; n < 4; ++n) {
-            const bf16x8 kh = *reinterpret_cast<const bf16x8*>(lds + (0 * 4 + g) * 64 + 16 * n + c);
-            const bf16x8 km = *reinterpret_cast<const bf16x8*>(lds + (1 * 4 + g) * 64 + 16 * n + c);
-            const bf16x8 kl = *reinterpret_cast<const bf16x8*>(lds + (2 * 4 + g) * 64 + 16 * n + c);
-#pragma unroll
-            for (int rg = 0; rg < RG; ++rg) {
-                f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f};
-                a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(km, qt[rg][1], a, 0, 0, 0);
-                a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kl, qt[rg][0], a, 0, 0, 0);
-                a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kh, qt[rg][2], a, 0, 0, 0);
-                a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(km, qt[rg][0], a, 0, 0, 0);
-                a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kh, qt[rg][1], a, 0, 0, 0);
-                a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kh, qt[rg][0], a, 0, 0, 0);
-                s[rg][n] = a;
-            }
-        }
-
-#pragma unroll
-        for (int rg = 0; rg < RG; ++rg) {
-            if (valid < 64) {
-#pragma unroll
-                for (int n = 0; n < 4; ++n)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        if (16 * n + 4 * g + r >= valid) s[rg][n][r] = -INFINITY;
-            }
-            float mx = s[rg][0][0];
-#pragma unroll
-            for (int n = 0; n < 4; ++n)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[rg][n][r]);
-            mx = xg_max(mx);
-            const float m_new = fmaxf(m_run[rg], mx);  // finite: every tile has a valid key
-            const float alpha = __builtin_amdgcn_exp2f(m_run[rg] - m_new);
-            m_run[rg] = m_new;
-            float rs = 0.f;
-#pragma unroll
-            for (int n = 0; n < 4; ++n)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const float p = __builtin_amdgcn_exp2f(s[rg][n][r] - m_new);
-                    s[rg][n][r] = p;
-                    rs += p;
-                }
-            l_run[rg] = l_run[rg] * alpha + rs;
-#pragma unroll
-            for (int t = 0; t < 2; ++t)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) acc[rg][t][r] *= alpha;
-        }
-
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            // P^T operand of step j, split just before use (keeps 24 VGPRs, not 48)
-            bf16x8 pt[RG][3];
-#pragma unroll
-            for (int rg = 0; rg < RG; ++rg)
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    __bf16 h, m, l;
-                    split3(s[rg][2 * j + (e >> 2)][e & 3], h, m, l);
-                    pt[rg][0][e] = h; pt[rg][1][e] = m; pt[rg][2][e] = l;
-                }
-#pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                bf16x8 vf[3];
-                const int r0 = 32 * j + 4 * g + qq, r1 = r0 + 16;
-                const int ch = 2 * t + (pp >> 1);
-                const int off0 = r0 * 64 + ((ch ^ (((r0 >> 2) & 1) << 1)) * 16) + (pp & 1) * 8;
-                const int off1 = r1 * 64 + ((ch ^ (((r1 >> 2) & 1) << 1)) * 16) + (pp & 1) * 8;
-#pragma unroll
-                for (int tm = 0; tm < 3; ++tm) {
-                    typedef __attribute__((address_space(3))) s16x4 lds_s4;
-                    const char* vb = lbase + kImgV * 16 + tm * 4096;
-                    const s16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                        (lds_s4*)(uintptr_t)(uint32_t)(uintptr_t)(vb + off0));
-                    const s16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                        (lds_s4*)(uintptr_t)(uint32_t)(uintptr_t)(vb + off1));
-                    const s16x8 w8 = __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7);
-                    vf[tm] = __builtin_bit_cast(bf16x8, w8);
-                }
-#pragma unroll
-                for (int rg = 0; rg < RG; ++rg) {
-                    f32x4 a = acc[rg][t];
-                    a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[1], pt[rg][1], a, 0, 0, 0);
-                    a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[2], pt[rg][0], a, 0, 0, 0);
-                    a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[0], pt[rg][2], a, 0, 0, 0);
-                    a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[1], pt[rg][0], a, 0, 0, 0);
-                    a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[0], pt[rg][1], a, 0, 0, 0);
-                    a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[0], pt[rg][0], a, 0, 0, 0);
-                    acc[rg][t] = a;
-                }
-            }
-        }
-    }
-    // O^T (dh 16t + 4g + r, query c) / l
-#pragma unroll
-    for (int rg = 0; rg < RG; ++rg) {
-        const float inv = 1.0f / xg_sum(l_run[rg]);
-        const int64_t row = q0 + wv * 16 * RG + rg * 16 + c;
-        if (row >= qe) continue;
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-            float4 y;
-            y.x = acc[rg][t][0] * inv; y.y = acc[rg][t][1] * inv;
-            y.z = acc[rg][t][2] * inv; y.w = acc[rg][t][3] * inv;
-            *reinterpret_cast<float4*>(o + row * ld_o + head * 32 + 16 * t + 4 * g) = y;
-        }
-    }
-}
-
 }  // namespace
 }  // namespace fgr
 
@@ -683,56 +398,6 @@ extern "C" int fgr_attention(const float* q, int64_t ld_q, const float* k, int64
     return FGR_OK;
 }
 
-static int64_t kv_image_bytes(int64_t n_kv_rows, int32_t n_kv_seg, int32_t n_head) {
-    return (n_kv_rows / 64 + n_kv_seg + 1) * (int64_t)n_head * kImgUnits * 16;
-}
-
-extern "C" int fgr_attention_bf16x6_workspace(int64_t n_kv_rows, int32_t n_kv_seg,
-                                              int32_t n_head, size_t* bytes) {
-    FGR_REQUIRE(bytes && n_kv_rows >= 0 && n_kv_seg >= 0 && n_head > 0,
-                "fgr_attention_bf16x6_workspace: bad arguments");
-    *bytes = (size_t)kv_image_bytes(n_kv_rows, n_kv_seg, n_head);
-    return FGR_OK;
-}
-
-extern "C" int fgr_attention_bf16x6(const float* q, int64_t ld_q, const float* k, int64_t ld_k,
-                                    const float* v, int64_t ld_v, float* o, int64_t ld_o,
-                                    const int64_t* q_off, const int64_t* kv_off,
-                                    const int32_t* kv_seg, int32_t n_seg, int32_t n_kv_seg,
-                                    int64_t n_kv_rows, int32_t max_q_len, int32_t max_kv_len,
-                                    int32_t n_head, int32_t head_dim, float scale,
-                                    void* workspace, int64_t ws_bytes, void* stream) {
-    FGR_REQUIRE(q && k && v && o && q_off && kv_off && kv_seg && workspace && n_seg > 0 &&
-                    n_kv_seg > 0 && n_head > 0 && max_q_len >= 0 && max_kv_len >= 0,
-                "fgr_attention_bf16x6: bad arguments");
-    FGR_REQUIRE(head_dim == 32, "fgr_attention_bf16x6: head_dim %d (only 32)", head_dim);
-    FGR_REQUIRE(ld_q >= n_head * 32 && ld_k >= n_head * 32 && ld_v >= n_head * 32 &&
-                    ld_o >= n_head * 32 && ld_q % 4 == 0 && ld_k % 4 == 0 && ld_v % 4 == 0 &&
-                    ld_o % 4 == 0,
-                "fgr_attention_bf16x6: row strides must be >= n_head*32 and multiples of 4");
-    FGR_REQUIRE(((reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(k) |
-                  reinterpret_cast<uintptr_t>(v) | reinterpret_cast<uintptr_t>(o)) & 15) == 0,
-                "fgr_attention_bf16x6: q/k/v/o must be 16-B aligned");
-    const int64_t need = kv_image_bytes(n_kv_rows, n_kv_seg, n_head);
-    FGR_REQUIRE(ws_bytes >= need, "fgr_attention_bf16x6: workspace %lld < %lld bytes",
-                (long long)ws_bytes, (long long)need);
-    if (max_q_len == 0 || max_kv_len == 0) return FGR_OK;
-    hipStream_t st = as_stream(stream);
-    TimedCall timed_(st);
-    hipLaunchKernelGGL(attn_kv_image_kernel,
-                       dim3((unsigned)ceil_div(max_kv_len, 64), (unsigned)n_head, (unsigned)n_kv_seg),
-                       dim3(256), 0, st, k, ld_k, v, ld_v, kv_off, n_head, (uint4*)workspace);
-    FGR_CHECK_LAUNCH("attn_kv_image_kernel");
-    // RG = 1: 64 queries per block (measured equal to RG = 2 at 3 waves/SIMD, finer blocks)
-    constexpr int RG = 1;
-    const int n_qblk = (int)ceil_div(max_q_len, 64 * RG);
-    const int64_t n_blocks = ceil_div((int64_t)n_seg * n_head, 8) * 8 * n_qblk;
-    hipLaunchKernelGGL((attn_bf16x6_kernel<RG>), dim3((unsigned)n_blocks), dim3(256), 0, st, q,
-                       ld_q, (const uint4*)workspace, o, ld_o, q_off, kv_off, kv_seg, n_head,
-                       n_seg, n_qblk, scale * 1.4426950408889634f);
-    FGR_CHECK_LAUNCH("attn_bf16x6_kernel");
-    return FGR_OK;
-}
 
 // ------------------------------------------------------------------------------------------
 // CorrespondenceDecoder.simple_attention (finegrained_regtr.py:328-363), the soft

@@ -907,174 +907,6 @@ __global__ void __launch_bounds__(256) gemm_f16x3_v4(GemmH3Args p) {
     }
 }
 
-// ------------------------------------------------------------------------------------
-// Row-resident f16x3 GEMM for short contractions (K <= 256), optionally fused with the
-// LayerNorm (+ positional-embedding add) that produces its input:
-//   A = LN(X) * gamma + beta (+ P)      (or A = X),    C = act(A W^T + bias (+ R))
-// Each block keeps an N-panel of BNP output columns of the W image resident in LDS (loaded
-// once) and its NW waves loop, independently and barrier-free, over 16-row tiles of X: a
-// wave loads whole rows into registers (lane (g, c): row c, k = 32 ks + 8 g .. +7, i.e.
-// exactly its B-operand fragments), computes the LayerNorm statistics (two-pass, lanes
-// c, c+16, c+32, c+48 hold the row), takes the EXACT row max for the fp16 scale (no online
-// rescaling), splits, and runs KT x BNP/16 x 3 MFMAs from the LDS panel. Replaces the
-// LayerNorm launch + the tiled GEMM (and its A write/read) of the transformer layers.
-// ------------------------------------------------------------------------------------
-struct RowsArgs {
-    const float* X; int64_t ldx;
-    const float* gamma; const float* beta; float eps;   // LayerNorm (gamma == nullptr: none)
-    const float* P; int64_t ldp;                        // added after the LayerNorm (or null)
-    const u32x4* W; int ksteps;                         // f16x3 image (ksteps_h3(K))
-    const float* wsc;
-    float* C; int64_t ldc;
-    const float* bias;
-    const float* R; int64_t ldr;
-    int M, N, K, act, vec_out;
-    int nbx;                                            // column-panel blocks (grid = nbx * py)
-};
-
-template <int KT, int BNP, int NW, bool LN>
-__global__ void __launch_bounds__(64 * NW) gemm_rows_f16x3(RowsArgs p) {
-    constexpr int NP = BNP / 16;                         // 16-column panels per block
-    __shared__ u32x4 wl[NP * KT * 128];
-    __shared__ __attribute__((aligned(16))) float lnp[2][KT * 32];
-    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
-    const int g = lane >> 4, c = lane & 15;
-    const int npanel = (p.N + 15) / 16;
-    // XCD-aware order: the nbx blocks that read the same rows (one per column panel) get
-    // consecutive ids after the remap, i.e. one XCD, so the rows come from its L2 once
-    int t = blockIdx.x;
-    {
-        const int nwg = gridDim.x, q = nwg / 8, r = nwg % 8, x = t % 8, lo = t / 8;
-        t = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + lo;
-    }
-    const int bx = t % p.nbx, by = t / p.nbx, py = gridDim.x / p.nbx;
-    const int pn0 = bx * NP;                             // first 16-col panel of this block
-    // W panel -> LDS (panels past N are clamped; their columns are never stored); k-steps
-    // past the image (KT > ksteps) are zero so the zero A columns meet zeros, not garbage
-    for (int u = tid; u < NP * KT * 128; u += 64 * NW) {
-        const int pl = u / (KT * 128), rem = u % (KT * 128);
-        wl[u] = rem < p.ksteps * 128
-                    ? p.W[(int64_t)min(pn0 + pl, npanel - 1) * p.ksteps * 128 + rem]
-                    : u32x4{0u, 0u, 0u, 0u};
-    }
-    if (LN) {
-        for (int k = tid; k < KT * 32; k += 64 * NW) {
-            lnp[0][k] = k < p.K ? p.gamma[k] : 0.f;
-            lnp[1][k] = k < p.K ? p.beta[k] : 0.f;
-        }
-    }
-    __syncthreads();
-
-    const int ntiles = (p.M + 15) / 16;
-    for (int tile = by * NW + wv; tile < ntiles; tile += py * NW) {
-        const int row = tile * 16 + c;
-        const int64_t rr = min(row, p.M - 1);
-        float v[KT][8];
-#pragma unroll
-        for (int ks = 0; ks < KT; ++ks) {
-            const int k = 32 * ks + 8 * g;
-            float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
-            if (k < p.K) {
-                const float4* src = reinterpret_cast<const float4*>(p.X + rr * p.ldx + k);
-                a = src[0];
-                b = src[1];
-            }
-            v[ks][0] = a.x; v[ks][1] = a.y; v[ks][2] = a.z; v[ks][3] = a.w;
-            v[ks][4] = b.x; v[ks][5] = b.y; v[ks][6] = b.z; v[ks][7] = b.w;
-        }
-        if (LN) {
-            float s = 0.f;
-#pragma unroll
-            for (int ks = 0; ks < KT; ++ks)
-#pragma unroll
-                for (int e = 0; e < 8; ++e) s += v[ks][e];
-            const float mean = xg_sum16(s) / (float)p.K;
-            float sq = 0.f;
-#pragma unroll
-            for (int ks = 0; ks < KT; ++ks)
-#pragma unroll
-                for (int e = 0; e < 8; ++e)
-                    if (32 * ks + 8 * g + e < p.K) {
-                        const float d = v[ks][e] - mean;
-                        sq += d * d;
-                    }
-            const float rstd = 1.0f / sqrtf(xg_sum16(sq) / (float)p.K + p.eps);
-#pragma unroll
-            for (int ks = 0; ks < KT; ++ks) {
-                const int k = 32 * ks + 8 * g;
-                const float4 g0 = *reinterpret_cast<const float4*>(&lnp[0][k]);
-                const float4 g1 = *reinterpret_cast<const float4*>(&lnp[0][k + 4]);
-                const float4 b0 = *reinterpret_cast<const float4*>(&lnp[1][k]);
-                const float4 b1 = *reinterpret_cast<const float4*>(&lnp[1][k + 4]);
-                const float gv[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
-                const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-#pragma unroll
-                for (int e = 0; e < 8; ++e) v[ks][e] = (v[ks][e] - mean) * rstd * gv[e] + bv[e];
-            }
-        }
-        if (p.P) {
-#pragma unroll
-            for (int ks = 0; ks < KT; ++ks) {
-                const int k = 32 * ks + 8 * g;
-                if (k < p.K) {
-                    const float4* src = reinterpret_cast<const float4*>(p.P + rr * p.ldp + k);
-                    const float4 a = src[0], b = src[1];
-                    v[ks][0] += a.x; v[ks][1] += a.y; v[ks][2] += a.z; v[ks][3] += a.w;
-                    v[ks][4] += b.x; v[ks][5] += b.y; v[ks][6] += b.z; v[ks][7] += b.w;
-                }
-            }
-        }
-        float mx = 0.f;
-#pragma unroll
-        for (int ks = 0; ks < KT; ++ks)
-#pragma unroll
-            for (int e = 0; e < 8; ++e) mx = fmaxf(mx, fabsf(v[ks][e]));
-        mx = xg_max16(mx);
-        const int sh = mx > 0.f ? min(15 - __builtin_amdgcn_frexp_expf(mx), 127) : 0;
-        const float sc = __builtin_ldexpf(1.f, sh);
-
-        f32x4 acc[NP];
-#pragma unroll
-        for (int j = 0; j < NP; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ks = 0; ks < KT; ++ks) {
-            f16x8 ah, am;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const float xs = v[ks][e] * sc;
-                const _Float16 hh = (_Float16)xs;
-                ah[e] = hh;
-                am[e] = (_Float16)(xs - (float)hh);
-            }
-#pragma unroll
-            for (int j = 0; j < NP; ++j) {
-                const u32x4* wb = wl + (j * KT + ks) * 128 + g * 16 + c;
-                const f16x8 wh = __builtin_bit_cast(f16x8, wb[0]);
-                const f16x8 wlo = __builtin_bit_cast(f16x8, wb[64]);
-                acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wlo, ah, acc[j], 0, 0, 0);
-                acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, am, acc[j], 0, 0, 0);
-                acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, ah, acc[j], 0, 0, 0);
-            }
-            // keep each k-step's LDS fragment loads next to their MFMAs (hoisting all of
-            // them across the unrolled loop is what spilled)
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        if (row >= p.M) continue;
-        const float rs = __builtin_ldexpf(1.f, -sh);
-        float* crow = p.C + (int64_t)row * p.ldc;
-        const float* rrow = p.R ? p.R + (int64_t)row * p.ldr : nullptr;
-#pragma unroll
-        for (int j = 0; j < NP; ++j) {
-            const int n = (pn0 + j) * 16 + 4 * g;
-            if (n >= p.N) continue;
-            const float4 ws = *reinterpret_cast<const float4*>(p.wsc + n);
-            const float y[4] = {acc[j][0] * rs * ws.x, acc[j][1] * rs * ws.y,
-                                acc[j][2] * rs * ws.z, acc[j][3] * rs * ws.w};
-            store_out4(y, p.bias, rrow, crow, n, p.N, p.act, p.vec_out);
-        }
-    }
-}
-
 // Row max |w| of W (n x k, element (i, j) at w[i * sn + j * sk]) -> wsc[i] = 2^-e_i with
 // e_i the row scale exponent (max * 2^e_i in [2^14, 2^15)); one wave per row, rows padded
 // to a multiple of 16 get 0.
@@ -1349,74 +1181,4 @@ extern "C" int fgr_gemm_f16x3_ws(const float* a, int64_t lda, const void* w_img,
                                  int32_t m, int32_t n, int32_t k, int32_t act, void* ws,
                                  size_t ws_bytes, void* stream) {
     return gemm_f16x3_impl(a, lda, w_img, c, ldc, bias, r, ldr, m, n, k, act, ws, ws_bytes, stream);
-}
-
-namespace fgr {
-namespace {
-// Grid: nbx column-panel blocks x py row groups, py sized so that the grid fills every CU
-// to its resident-block limit once (each wave then loops over its row tiles).
-template <int KT, int BNP, bool LN>
-void launch_rows(RowsArgs a, hipStream_t st, int n_cu) {
-    constexpr int NW = 8;
-    static int per_cu = 0;                               // device-properties cache
-    if (per_cu <= 0) {
-        int nb = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                &nb, reinterpret_cast<const void*>(&gemm_rows_f16x3<KT, BNP, NW, LN>), 64 * NW,
-                0) != hipSuccess || nb <= 0)
-            nb = 1;
-        per_cu = nb;
-    }
-    a.nbx = (a.N + BNP - 1) / BNP;
-    const int ntiles = (a.M + 15) / 16;
-    int py = (per_cu * n_cu + a.nbx - 1) / a.nbx;
-    py = max(1, min(py, (ntiles + NW - 1) / NW));
-    hipLaunchKernelGGL((gemm_rows_f16x3<KT, BNP, NW, LN>), dim3((unsigned)(a.nbx * py)),
-                       dim3(64 * NW), 0, st, a);
-}
-template <int KT, bool LN>
-void launch_rows_n(const RowsArgs& a, hipStream_t st, int n_cu) {
-    if (a.N <= 16)
-        launch_rows<KT, 16, LN>(a, st, n_cu);
-    else
-        launch_rows<KT, 64, LN>(a, st, n_cu);
-}
-}  // namespace
-}  // namespace fgr
-
-extern "C" int fgr_gemm_rows_f16x3(const float* x, int64_t ldx, const float* ln_gamma,
-                                   const float* ln_beta, float ln_eps, const float* add,
-                                   int64_t ld_add, const void* w_img, float* c, int64_t ldc,
-                                   const float* bias, const float* r, int64_t ldr, int32_t m,
-                                   int32_t n, int32_t k, int32_t act, void* stream) {
-    FGR_REQUIRE(x && w_img && c && m >= 0 && n > 0 && k > 0 && k <= 256 && k % 8 == 0 &&
-                    ldx >= k && ldx % 4 == 0 && ldc >= n && (!r || ldr >= n) &&
-                    (!add || (ld_add >= k && ld_add % 4 == 0)) && (!ln_gamma || ln_beta),
-                "fgr_gemm_rows_f16x3: bad arguments (m %d n %d k %d)", m, n, k);
-    FGR_REQUIRE(((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w_img) |
-                  reinterpret_cast<uintptr_t>(add)) & 15) == 0,
-                "fgr_gemm_rows_f16x3: x / add / image must be 16-B aligned");
-    if (m == 0) return FGR_OK;
-    const bool vo = (ldc % 4 == 0) && ((reinterpret_cast<uintptr_t>(c) & 15) == 0) &&
-                    (!bias || (reinterpret_cast<uintptr_t>(bias) & 15) == 0) &&
-                    (!r || ((ldr % 4 == 0) && (reinterpret_cast<uintptr_t>(r) & 15) == 0));
-    const float* wsc = reinterpret_cast<const float*>(static_cast<const char*>(w_img) +
-                                                      image_bytes_h3(n, k));
-    RowsArgs g{x, ldx, ln_gamma, ln_beta, ln_eps, add, ld_add, (const u32x4*)w_img,
-               ksteps_h3(k), wsc, c, ldc, bias, r, ldr, m, n, k, act, vo ? 1 : 0};
-    hipStream_t st = as_stream(stream);
-    TimedCall timed_(st);
-    int dev = 0, n_cu = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        n_cu <= 0)
-        n_cu = 256;
-    const bool ln = ln_gamma != nullptr;
-    if (k <= 128) {
-        if (ln) launch_rows_n<4, true>(g, st, n_cu); else launch_rows_n<4, false>(g, st, n_cu);
-    } else {
-        if (ln) launch_rows_n<8, true>(g, st, n_cu); else launch_rows_n<8, false>(g, st, n_cu);
-    }
-    FGR_CHECK_LAUNCH("gemm_rows_f16x3");
-    return FGR_OK;
 }

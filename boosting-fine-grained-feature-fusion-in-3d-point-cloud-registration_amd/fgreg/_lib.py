@@ -33,11 +33,6 @@ SIGNATURES = {
     'fgr_kpconv_gather': [_vp, _vp, _i64, _i64, _vp, _i32, _vp, _i32, _vp, _i32, _f32, _vp, _vp,
                           _vp, _sz, _vp],
     'fgr_max_pool': [_vp, _i64, _i32, _vp, _i64, _i32, _vp, _vp],
-    'fgr_kpconv_fused_weights_bytes': [_i32, _i32, _i32, _i32, ctypes.POINTER(_sz)],
-    'fgr_kpconv_fused_weights': [_vp, _i32, _i32, _i32, _i32, _vp, _vp],
-    'fgr_kpconv_fused_workspace': [_i64, ctypes.POINTER(_sz)],
-    'fgr_kpconv_fused': [_vp, _vp, _i64, _i64, _vp, _i32, _vp, _i32, _vp, _i32, _f32, _vp, _i32,
-                         _i32, _vp, _i64, _vp, _vp, _sz, _vp],
     'fgr_instnorm_workspace': [_i64, _i32, _i32, ctypes.POINTER(_sz)],
     'fgr_instnorm': [_vp, _i64, _i32, _vp, _i32, _i64, _vp, _f32, _i32, _vp, _i32, _vp, _vp, _sz,
                      _vp],
@@ -45,24 +40,14 @@ SIGNATURES = {
     'fgr_sine_pos_embed': [_vp, _i64, _i32, _f32, _f32, _vp, _vp],
     'fgr_attention': [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i32, _i32, _i32,
                       _i32, _f32, _vp],
-    'fgr_attention_bf16x6_workspace': [_i64, _i32, _i32, ctypes.POINTER(_sz)],
-    'fgr_attention_bf16x6': [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i32, _i32,
-                             _i64, _i32, _i32, _i32, _i32, _f32, _vp, _i64, _vp],
     'fgr_attention_f16x3_workspace': [_i64, _i32, _i32, ctypes.POINTER(_sz)],
     'fgr_attention_f16x3': [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i32, _i32,
                             _i64, _i32, _i32, _i32, _i32, _f32, _vp, _i64, _vp],
     'fgr_attention_bf16_workspace': [_i64, _i32, _i32, ctypes.POINTER(_sz)],
     'fgr_attention_bf16': [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i32, _i32,
                            _i64, _i32, _i32, _i32, _i32, _f32, _vp, _i64, _vp],
-    'fgr_res2net_chain': [_vp, _i64, _i32, _i32, _vp, _vp, _vp, _i32, _vp, _i64, _vp],
     'fgr_res2net_chain6': [_vp, _i64, _i32, _i32, _vp, _vp, _vp, _i32, _vp, _i64, _vp],
     'fgr_res2net_chain_h3': [_vp, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _i32, _vp, _i64, _vp],
-    'fgr_split_weights': [_vp, _i32, _i32, _i64, _vp, _vp, _vp],
-    'fgr_gemm_bf16x3': [_vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _vp, _i64, _i32, _i32, _i32,
-                        _i32, _vp],
-    'fgr_split_weights3_bytes': [_i32, _i32, ctypes.POINTER(_sz)],
-    'fgr_split_weights3': [_vp, _i32, _i32, _i64, _i64, _vp, _vp],
-    'fgr_gemm_bf16x6': [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _vp],
     'fgr_split_weights_h3_bytes': [_i32, _i32, ctypes.POINTER(_sz)],
     'fgr_split_weights_h3': [_vp, _i32, _i32, _i64, _i64, _vp, _vp],
     'fgr_gemm_f16x3': [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _vp],
@@ -74,8 +59,6 @@ SIGNATURES = {
                           _sz, _vp],
     'fgr_gemm_bf16_ws': [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _vp,
                          _sz, _vp],
-    'fgr_gemm_rows_f16x3': [_vp, _i64, _vp, _vp, _f32, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _i64,
-                            _i32, _i32, _i32, _i32, _vp],
     'fgr_split_rows_h3_bytes': [_i32, _i32, ctypes.POINTER(_sz)],
     'fgr_split_rows_h3': [_vp, _i64, _i32, _i32, _vp, _vp],
     'fgr_gemm_h3_presplit': [_vp, _vp, _vp, _i64, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _vp],
@@ -117,7 +100,6 @@ SIGNATURES = {
 
 NB_INDEX, NB_DIST = 0, 1
 ACT_NONE, ACT_LEAKY, ACT_RELU, ACT_RELU_RES_LEAKY = 0, 1, 2, 3
-KPF_F16X3, KPF_BF16 = 0, 1
 
 _lib = None
 

@@ -18,7 +18,6 @@ statistics, every op differentiable on libfgreg's backward kernels) composes the
 in fgreg/training.py.
 """
 import math
-import os
 from typing import List
 
 import numpy as np
@@ -26,9 +25,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from . import _lib
 from . import ops
-from . import linear as lin
 from .linear import linear
 
 
@@ -189,22 +186,6 @@ def init_kernel_points(radius, n_kp, rng=np.random):
 # ------------------------------------------------------------------------------------------
 # Blocks
 # ------------------------------------------------------------------------------------------
-# Res2Net hierarchy kernel where both fp32-accurate chains exist (w = 112, 224): the bf16x6
-# chain at w = 224 (measured faster), the f16x3 chain otherwise; FGREG_R2N = h3 | bf16x6
-# forces one (A/B switch)
-R2N = os.environ.get('FGREG_R2N', 'auto')
-
-
-# Fused KPConv dispatch (FGREG_KPF): '1' every eligible layer, '0' never (gather + GEMM)
-KPF = os.environ.get('FGREG_KPF', '0')
-
-
-def _kpf_mode(cin, n_kp):
-    if KPF != '1' or cin % 16 != 0 or n_kp > 15:
-        return None
-    return {'f16x3': _lib.KPF_F16X3, 'bf16': _lib.KPF_BF16}.get(lin.MODE)
-
-
 class KPConv(nn.Module):
     """Rigid KPConv (finegrained_kpconv_blocks.py:171-401): linear influence, sum mode."""
 
@@ -224,13 +205,7 @@ class KPConv(nn.Module):
 
     def forward_unnormalized(self, q_pts, s_pts, neighb_inds, x):
         """-> (sum_k WF_k @ W_k (Nq, Cout), nnorm (Nq,)). The reference divides the first
-        by the second (:395-399); callers fuse that division into the next kernel.
-        Fused (fgr_kpconv_fused: gather + weight GEMM in one launch, wf never written) where
-        the channel width allows it (Cin % 16 == 0) in the f16x3 / bf16 modes; ``KPF``."""
-        mode = _kpf_mode(x.shape[1], self.K)
-        if mode is not None:
-            return ops.kpconv_fused(q_pts, s_pts, neighb_inds, x, self.kernel_points,
-                                    self.KP_extent, self.weights, mode)
+        by the second (:395-399); callers fuse that division into the next kernel."""
         wf, nnorm = ops.kpconv_gather(q_pts, s_pts, neighb_inds, x, self.kernel_points,
                                       self.KP_extent)
         out = linear(wf.view(wf.shape[0], -1), self.weights, transpose=True)
@@ -312,15 +287,14 @@ class my_Bottle2neck(nn.Module):  # noqa: N801 -- reference name (res2net.py:84)
                 else:
                     w3d, b3d = w3, b3
                 chain = None
-                if w1.is_cuda and self.nums > 0 and (ops.res2net_chain_supported(self.width) or
-                                                     ops.res2net_chain_supported(self.width, True)):
+                if w1.is_cuda and self.nums > 0 and self.downsample is not None:
                     wst = torch.stack([wi for wi, _ in ws])
-                    full = ops.res2net_chain_supported(self.width)
-                    chain = (ops.res2net_fragments(wst) if full else None,
-                             torch.stack([bi for _, bi in ws]).contiguous(),
-                             ops.res2net_fragments3(wst) if full else None,
-                             ops.res2net_fragments_h3(wst)
-                             if ops.res2net_chain_supported(self.width, True) else None)
+                    bst = torch.stack([bi for _, bi in ws]).contiguous()
+                    # w = 224: the bf16x6 chain (measured faster -- fewer barriers); else h3
+                    if self.width == 224:
+                        chain = (bst, ops.res2net_fragments3(wst), None)
+                    elif ops.res2net_chain_supported(self.width, True):
+                        chain = (bst,) + ops.res2net_fragments_h3(wst)
             self._folded = (key, w1, b1, ws, w3d, b3d, chain)
         return self._folded[1:]
 
@@ -335,45 +309,29 @@ class my_Bottle2neck(nn.Module):  # noqa: N801 -- reference name (res2net.py:84)
         w1, b1, ws, w3d, b3d, chain = self._folded_params()
         out = linear(x, w1, b1, act=ops.ACT_RELU)
         w = self.width
-        use = None
-        if chain is not None and self.downsample is not None:
-            prefer6 = R2N == 'bf16x6' or (R2N == 'auto' and w == 224)
-            if (lin.MODE in ('f16x3', 'bf16') and chain[3] is not None
-                    and (not prefer6 or chain[2] is None)):
-                use = 'h3'      # (w = 224: the bf16x6 chain measured faster -- fewer barriers)
-            elif lin.MODE in ('bf16x6', 'f16x3', 'bf16') and chain[2] is not None:
-                use = 'bf16x6'
-            elif chain[0] is not None and lin.MODE == 'fp32':
-                use = 'fp32'
-        if use is not None:
+        down = self.downsample is not None
+        cat_in = torch.empty((x.shape[0], w * self.scale + (x.shape[1] if down else 0)),
+                             dtype=x.dtype, device=x.device)
+        if chain is not None:
             # one launch for the whole hierarchy + the [.. | x] concat (fgr_res2net_chain*)
-            cat_in = torch.empty((x.shape[0], w * self.scale + x.shape[1]), dtype=x.dtype,
-                                 device=x.device)
-            if use == 'h3':
-                ops.res2net_chain(out, w, self.scale, chain[3][0], chain[1], x, cat_in,
-                                  w_scale=chain[3][1])
-            elif use == 'bf16x6':
-                ops.res2net_chain(out, w, self.scale, chain[2], chain[1], x, cat_in, split6=True)
-            else:
-                ops.res2net_chain(out, w, self.scale, chain[0], chain[1], x, cat_in)
+            ops.res2net_chain(out, w, self.scale, chain[1], chain[0], x, cat_in, w_scale=chain[2])
+        else:
+            # widths / layouts without a chain kernel: one GEMM (+ bias + ReLU) per step
+            sp = None
+            for i in range(self.nums):
+                chunk = out[:, i * w:(i + 1) * w]
+                sp = chunk if i == 0 else sp + chunk
+                sp = linear(sp, ws[i][0], ws[i][1], act=ops.ACT_RELU,
+                            out=cat_in[:, i * w:(i + 1) * w])
+            if self.scale != 1:
+                cat_in[:, self.nums * w:self.scale * w] = out[:, self.nums * w:self.scale * w]
+            if down:
+                cat_in[:, self.scale * w:] = x
+        if down:        # [conv3 | downsample] in one GEMM, the shortcut in its epilogue
             if shortcut is not None:
                 return linear(cat_in, w3d, b3d, act=ops.ACT_RELU_RES_LEAKY, residual=shortcut)
             return linear(cat_in, w3d, b3d, act=ops.ACT_RELU)
-        cat_in = torch.empty((x.shape[0], w * self.scale + (x.shape[1] if self.downsample is not None else 0)),
-                             dtype=x.dtype, device=x.device)
-        sp = None
-        for i in range(self.nums):
-            chunk = out[:, i * w:(i + 1) * w]
-            sp = chunk if i == 0 else sp + chunk
-            sp = torch._addmm_activation(ws[i][1], sp, ws[i][0].t())
-            cat_in[:, i * w:(i + 1) * w] = sp
-        if self.scale != 1:
-            cat_in[:, self.nums * w:self.scale * w] = out[:, self.nums * w:self.scale * w]
-        if self.downsample is not None:
-            cat_in[:, self.scale * w:] = x
-            y = torch._addmm_activation(b3d, cat_in, w3d.t())
-        else:
-            y = (torch.addmm(b3d, cat_in, w3d.t()) + x).relu_()
+        y = linear(cat_in, w3d, b3d, act=ops.ACT_RELU, residual=x)    # identity downsample
         return y if shortcut is None else F.leaky_relu(y + shortcut, 0.1)
 
 

@@ -1,45 +1,30 @@
 """Dense layers of the forward (every Linear / KPConv-weight product goes through
-``linear()``) on the GPU, in one of five precision modes (``FGREG_GEMM`` or ``set_mode``):
+``linear()``) on the GPU, in one of two precision modes (``set_mode``, or
+``fgreg.set_precision``):
 
 * ``f16x3`` (default): fgr_gemm_f16x3, the fp32-accurate scaled split-fp16 MFMA GEMM (operands
   scaled by per-row powers of two and split into two fp16 terms, three term products per
-  step: <= ~3 * 2^-22 relative per product) -- half the matrix-core work of bf16x6.
-* ``bf16x6``: fgr_gemm_bf16x6, the fp32-accurate split-bf16 MFMA GEMM (operands
-  split exactly into three bf16 terms, six term products per step: ~2^-27 relative
-  residual, below fp32's own rounding). Meets the 1e-4 parity bar on every fixture.
+  step: <= ~3 * 2^-22 relative per product) -- meets the 1e-4 parity bar on every fixture.
 * ``bf16``: fgr_gemm_bf16, one bf16 MFMA product per fp32 product (operands rounded to bf16,
   fp32 accumulation: ~2^-9 relative per product) -- the BASELINE configs[4] (3DLoMatch)
   compute mode, 3x fewer matrix-core cycles than f16x3; tolerance in DESIGN.md.
-* ``fp32``: PyTorch's fp32 GEMM (hipBLASLt, fp32 MFMA) -- the A/B baseline.
-* ``bf16x3``: fgr_gemm_bf16x3, two-term split (~2^-17 relative per product); faster, but
-  the 3DMatch fixture's pose misses the 1e-4 bar (1.3e-4), so it is opt-in only.
-Split weights are built once and cached against the fp32 tensor's identity, data pointer
-and version (a checkpoint load, .to() or in-place update invalidates the cache).
-
-In f16x3 mode, short contractions (K <= 256) can run on fgr_gemm_rows_f16x3 instead, which
-keeps a W panel in LDS and whole A rows in registers and fuses the LayerNorm (+ positional
-add) producing A into its row loads (``linear(..., ln=norm, add=pos)``). ``FGREG_ROWS``:
-'1' for the LayerNorm-fused calls, '2' for every eligible call, '0' (default) never (then
-``ln`` / ``add`` run as a separate fgr_layernorm launch). Measured on MI355X it is still
-slower than the LayerNorm launch + tiled GEMM at the transformer's shapes (QKV 9493 x 768 x
-256: 72 vs 37 us), so it is opt-in until it is reworked.
+Weight images are built once and cached against the fp32 tensor's identity, data pointer
+and version (a checkpoint load, .to() or in-place update invalidates the cache). There is no
+library / PyTorch GEMM fallback: a shape the kernels reject raises.
 """
-import os
-
 import torch
-import torch.nn.functional as F
 
 from . import _lib
 from . import ops
-from .ops import ACT_NONE, ACT_RELU, ACT_RELU_RES_LEAKY, _begin, _dev, _end, _ptr, _stream
+from .ops import ACT_NONE, _begin, _dev, _end, _ptr, _stream
 
-MODE = os.environ.get('FGREG_GEMM', 'f16x3')
-ROWS = os.environ.get('FGREG_ROWS', '0')
+MODES = ('f16x3', 'bf16')
+MODE = 'f16x3'
 
 
 def set_mode(mode):
     global MODE
-    assert mode in ('fp32', 'bf16x3', 'bf16x6', 'f16x3', 'bf16')
+    assert mode in MODES, mode
     MODE = mode
 
 
@@ -48,6 +33,7 @@ class mode_scope:  # noqa: N801 -- used as a context manager
     the pose-sensitive correspondence head of the bf16 forward in f16x3, regtr.py)."""
 
     def __init__(self, mode):
+        assert mode is None or mode in MODES, mode
         self.mode, self.prev = mode, None
 
     def __enter__(self):
@@ -61,69 +47,24 @@ class mode_scope:  # noqa: N801 -- used as a context manager
         return False
 
 
-class SplitWeight:
-    __slots__ = ('hi', 'lo', 'ldw', 'n', 'k', 'src', 'version', 'ptr')
-
-    def __init__(self, w: torch.Tensor, src: torch.Tensor):
-        """w: (n, k) fp32 (already in 'out x in' order)."""
-        n, k = w.shape
-        ldw = (k + 31) // 32 * 32
-        self.hi = torch.empty((n, ldw), dtype=torch.bfloat16, device=w.device)
-        self.lo = torch.empty((n, ldw), dtype=torch.bfloat16, device=w.device)
-        wc = w.contiguous()
-        _lib.check(_lib.load().fgr_split_weights(_ptr(wc), n, k, ldw, _ptr(self.hi), _ptr(self.lo),
-                                                 _stream()), 'fgr_split_weights')
-        self.ldw, self.n, self.k = ldw, n, k
-        self.src, self.version, self.ptr = src, src._version, src.data_ptr()
-
-
-class SplitWeight3:
-    """bf16x6 image of W (n, k) (fgr_split_weights3); element (i, j) at w[i * sn + j * sk]."""
+class _Image:
+    """Split image of W (n, k), element (i, j) at w2[i * sn + j * sk]: fgr_split_weights_h3
+    (f16x3: two fp16 terms, per-row power-of-two scales) or fgr_split_weights_bf16."""
     __slots__ = ('img', 'n', 'k', 'src', 'version', 'ptr')
+    FN = {'f16x3': 'fgr_split_weights_h3', 'bf16': 'fgr_split_weights_bf16'}
 
-    def __init__(self, w2: torch.Tensor, n, k, sn, sk, src: torch.Tensor):
+    def __init__(self, mode, w2: torch.Tensor, n, k, sn, sk, src: torch.Tensor):
         L = _lib.load()
+        fn = self.FN[mode]
         nb = _lib._sz(0)
-        _lib.check(L.fgr_split_weights3_bytes(n, k, nb), 'fgr_split_weights3_bytes')
+        _lib.check(getattr(L, fn + '_bytes')(n, k, nb), fn + '_bytes')
         self.img = torch.empty(nb.value, dtype=torch.uint8, device=w2.device)
-        _lib.check(L.fgr_split_weights3(_ptr(w2), n, k, sn, sk, _ptr(self.img), _stream()),
-                   'fgr_split_weights3')
-        self.n, self.k = n, k
-        self.src, self.version, self.ptr = src, src._version, src.data_ptr()
-
-
-class SplitWeightH3:
-    """f16x3 image of W (n, k) + per-row scales (fgr_split_weights_h3)."""
-    __slots__ = ('img', 'n', 'k', 'src', 'version', 'ptr')
-
-    def __init__(self, w2: torch.Tensor, n, k, sn, sk, src: torch.Tensor):
-        L = _lib.load()
-        nb = _lib._sz(0)
-        _lib.check(L.fgr_split_weights_h3_bytes(n, k, nb), 'fgr_split_weights_h3_bytes')
-        self.img = torch.empty(nb.value, dtype=torch.uint8, device=w2.device)
-        _lib.check(L.fgr_split_weights_h3(_ptr(w2), n, k, sn, sk, _ptr(self.img), _stream()),
-                   'fgr_split_weights_h3')
-        self.n, self.k = n, k
-        self.src, self.version, self.ptr = src, src._version, src.data_ptr()
-
-
-class SplitWeightBF:
-    """Single-term bf16 image of W (n, k) (fgr_split_weights_bf16)."""
-    __slots__ = ('img', 'n', 'k', 'src', 'version', 'ptr')
-
-    def __init__(self, w2: torch.Tensor, n, k, sn, sk, src: torch.Tensor):
-        L = _lib.load()
-        nb = _lib._sz(0)
-        _lib.check(L.fgr_split_weights_bf16_bytes(n, k, nb), 'fgr_split_weights_bf16_bytes')
-        self.img = torch.empty(nb.value, dtype=torch.uint8, device=w2.device)
-        _lib.check(L.fgr_split_weights_bf16(_ptr(w2), n, k, sn, sk, _ptr(self.img), _stream()),
-                   'fgr_split_weights_bf16')
+        _lib.check(getattr(L, fn)(_ptr(w2), n, k, sn, sk, _ptr(self.img), _stream()), fn)
         self.n, self.k = n, k
         self.src, self.version, self.ptr = src, src._version, src.data_ptr()
 
 
 _CACHE = {}
-_IMAGE = {3: SplitWeight3, 'h3': SplitWeightH3, 'bf16': SplitWeightBF}
 
 
 def _valid(ent, w):
@@ -131,147 +72,78 @@ def _valid(ent, w):
             and ent.ptr == w.data_ptr())            # .to() / load_state_dict swap .data
 
 
-def split_weight3(w: torch.Tensor, transpose=False, tag=None, kind=3, cache=True):
-    """Split image of w (kind 3: bf16x6, kind 'h3': f16x3, 'bf16': single bf16), cached unless ``cache`` is False
-    (operands that change every call, e.g. the loss's feature matrices)."""
-    ck = (id(w), transpose, tag, kind)
+def weight_image(w: torch.Tensor, transpose=False, tag=None, mode=None, cache=True, rows=None):
+    """Split image of w in ``mode`` (default: the current MODE), cached unless ``cache`` is
+    False (operands that change every call, e.g. the backward's activations). ``rows`` =
+    (r0, r1) takes the row slice w[r0:r1] (e.g. the q|k and v blocks of an in_proj weight),
+    cached against the parent tensor."""
+    mode = mode or MODE
+    ck = (id(w), transpose, tag, mode, rows)
     ent = _CACHE.get(ck) if cache else None
     if not _valid(ent, w):
-        cls = _IMAGE[kind]
+        src = w
+        if rows is not None:
+            w = w[rows[0]:rows[1]]
         if transpose == 'flat':          # (..., k) as W[n = leading index][k = last index]
             w2 = w.reshape(-1, w.shape[-1]).contiguous()
-            ent = cls(w2, w2.shape[0], w2.shape[1], w2.shape[1], 1, w)
+            ent = _Image(mode, w2, w2.shape[0], w2.shape[1], w2.shape[1], 1, src)
         elif transpose:                  # (K, Cin, Cout) as W[n = cout][k = K*Cin + cin]
             w2 = w.reshape(-1, w.shape[-1]).contiguous()
-            ent = cls(w2, w2.shape[1], w2.shape[0], 1, w2.shape[1], w)
+            ent = _Image(mode, w2, w2.shape[1], w2.shape[0], 1, w2.shape[1], src)
         else:
             w2 = w.contiguous()
-            ent = cls(w2, w2.shape[0], w2.shape[1], w2.shape[1], 1, w)
+            ent = _Image(mode, w2, w2.shape[0], w2.shape[1], w2.shape[1], 1, src)
         if cache:
             _CACHE[ck] = ent
     return ent
 
 
-def split_weight(w: torch.Tensor, transpose=False, tag=None) -> SplitWeight:
-    """Cached bf16 split of w (or of w.t() when transpose=True, e.g. KPConv (K*Cin, Cout))."""
-    ck = (id(w), transpose, tag)
-    ent = _CACHE.get(ck)
-    if not _valid(ent, w):
-        ent = SplitWeight(w.reshape(-1, w.shape[-1]).t() if transpose else w, w)
-        _CACHE[ck] = ent
-    return ent
-
-
-def _rows_ok(x, k, add, act):
-    return (k <= 256 and k % 8 == 0 and act in (ACT_NONE, ACT_RELU, ACT_RELU_RES_LEAKY)
-            and x.stride(1) == 1 and x.stride(0) % 4 == 0 and x.data_ptr() % 16 == 0
-            and (add is None or (add.stride(1) == 1 and add.stride(0) % 4 == 0
-                                 and add.data_ptr() % 16 == 0)))
-
-
-def _linear_rows(x, w, bias, act, residual, tag, out, ln, add, cache):
-    n, k = w.shape
-    sw = split_weight3(w, False, tag, 'h3', cache=cache)
-    m = x.shape[0]
-    if out is None:
-        out = torch.empty((m, n), dtype=torch.float32, device=x.device)
-    g, b, eps = (ln.weight, ln.bias, float(ln.eps)) if ln is not None else (None, None, 0.0)
-    t0 = _begin('gemm')
-    _lib.check(_lib.load().fgr_gemm_rows_f16x3(
-        _ptr(x), x.stride(0), _ptr(g), _ptr(b), eps, _ptr(add),
-        add.stride(0) if add is not None else 0, _ptr(sw.img), _ptr(out), out.stride(0),
-        _ptr(bias), _ptr(residual), residual.stride(0) if residual is not None else 0, m, n, k,
-        act, _stream()), 'fgr_gemm_rows_f16x3')
-    _end('gemm', t0, 2 * m * n * k)
-    return out
-
-
 def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act=ACT_NONE, residual=None,
-           transpose=False, tag=None, out=None, ln=None, add=None, cache=True) -> torch.Tensor:
-    """act(A @ W^T + bias (+ residual)), W = w (n, k), or W = w.reshape(k, n).t() if
-    transpose (e.g. KPConv weights (K, Cin, Cout) used as (K*Cin, Cout)), or W =
-    w.reshape(-1, w.shape[-1]) if transpose == 'flat' (the backward's d_wf = dout W2^T); A = x, or
-    A = ln(x) (+ add) for an nn.LayerNorm ``ln`` and / or an added tensor ``add`` (fused into
-    the GEMM's row loads where fgr_gemm_rows_f16x3 applies). ACT_RELU_RES_LEAKY applies the
-    residual after the ReLU: LeakyReLU_0.1(ReLU(A @ W^T + bias) + residual)."""
+           transpose=False, tag=None, out=None, cache=True, rows=None) -> torch.Tensor:
+    """act(A @ W^T + bias (+ residual)) with A = x and W = w (n, k), or w[r0:r1] for ``rows``
+    = (r0, r1), or W = w.reshape(k, n).t() if transpose (e.g. KPConv weights (K, Cin, Cout)
+    used as (K*Cin, Cout)), or W = w.reshape(-1, w.shape[-1]) if transpose == 'flat' (the
+    backward's d_wf = dout W2^T). ACT_RELU_RES_LEAKY applies the residual after the ReLU:
+    LeakyReLU_0.1(ReLU(A @ W^T + bias) + residual)."""
     if transpose == 'flat':
         k = w.shape[-1]
         n = w.numel() // k
     else:
         n = w.shape[-1] if transpose else w.shape[0]
         k = w.numel() // n if transpose else w.shape[1]
+    if rows is not None:
+        assert not transpose and 0 <= rows[0] < rows[1] <= n
+        n = rows[1] - rows[0]
     assert x.dim() == 2 and x.shape[1] == k and x.dtype == torch.float32
-    if not x.is_cuda:
-        _dev(x)
+    if not (x.is_cuda and w.is_cuda):
+        _dev(x, w)
     if residual is not None:
         assert residual.shape == (x.shape[0], n) and residual.stride(1) == 1
-    if add is not None:
-        assert add.shape == x.shape and add.dtype == torch.float32
-    fused = ln is not None or add is not None
-    if (MODE == 'f16x3' and not transpose and (ROWS == '2' or (fused and ROWS == '1'))
-            and _rows_ok(x, k, add, act)):
-        return _linear_rows(x, w, bias, act, residual, tag, out, ln, add, cache)
-    if fused:
-        x = (ops.layernorm(x.contiguous(), ln.weight, ln.bias, ln.eps, add=add)
-             if ln is not None else x + add)
-    if act == ACT_RELU_RES_LEAKY and MODE not in ('f16x3', 'bf16'):
-        y = linear(x, w, bias, ACT_RELU, None, transpose, tag, cache=cache)
-        y = F.leaky_relu(y + residual, 0.1)
-        return out.copy_(y) if out is not None else y
-    if MODE in ('bf16x6', 'f16x3', 'bf16'):
-        if x.shape[0] == 1 and x.stride(1) == 1 and x.stride(0) != k:
-            x = x.as_strided(x.shape, (k, 1))      # a 1-row view's row stride is arbitrary
-        if not (x.stride(1) == 1 and (k % 8 != 0 or (x.stride(0) % 4 == 0
-                                                     and x.data_ptr() % 16 == 0))):
-            x = x.contiguous()                 # the split kernels need 16-B aligned rows
-            if k % 8 == 0 and x.data_ptr() % 16 != 0:
-                x = x.clone()
-        kind = {'f16x3': 'h3', 'bf16x6': 3, 'bf16': 'bf16'}[MODE]
-        sw = split_weight3(w, transpose, tag, kind, cache=cache)
-        m = x.shape[0]
-        if out is None:
-            out = torch.empty((m, n), dtype=torch.float32, device=x.device)
-        L = _lib.load()
-        t0 = _begin('gemm', (m, n, k))
-        if MODE in ('f16x3', 'bf16'):
-            # split-K workspace where the dispatcher wants one (few rows, long K)
-            nb = _lib._sz(0)
-            _lib.check(L.fgr_gemm_workspace(m, n, k, 0 if MODE == 'f16x3' else 1, nb),
-                       'fgr_gemm_workspace')
-            ws = ops._workspace(x.device, nb.value) if nb.value else None
-            _lib.check(getattr(L, 'fgr_gemm_' + MODE + '_ws')(
-                _ptr(x), x.stride(0), _ptr(sw.img), _ptr(out), out.stride(0), _ptr(bias),
-                _ptr(residual), residual.stride(0) if residual is not None else 0, m, n, k, act,
-                _ptr(ws), nb.value, _stream()), 'fgr_gemm_' + MODE)
-        else:
-            _lib.check(getattr(L, 'fgr_gemm_' + MODE)(
-                _ptr(x), x.stride(0), _ptr(sw.img), _ptr(out), out.stride(0), _ptr(bias),
-                _ptr(residual), residual.stride(0) if residual is not None else 0, m, n, k, act,
-                _stream()), 'fgr_gemm_' + MODE)
-        _end('gemm', t0, 2 * m * n * k)
-        return out
-    ok = (MODE == 'bf16x3' and transpose != 'flat' and k % 4 == 0 and x.stride(1) == 1
-          and x.stride(0) % 4 == 0 and x.data_ptr() % 16 == 0)
-    if not ok:
-        W = w.reshape(n, k).t() if transpose == 'flat' else (w.reshape(k, n) if transpose else w.t())
-        if residual is not None:
-            y = torch.addmm(residual, x, W)
-            if bias is not None:
-                y.add_(bias)
-        elif bias is not None:
-            y = torch._addmm_activation(bias, x, W) if act == ACT_RELU else torch.addmm(bias, x, W)
-            return y
-        else:
-            y = torch.mm(x, W)
-        return y.relu_() if act == ACT_RELU else y
-    sw = split_weight(w, transpose, tag)
+    if bias is not None:
+        assert bias.numel() == n and bias.is_contiguous()
+    if x.shape[0] == 1 and x.stride(1) == 1 and x.stride(0) != k:
+        x = x.as_strided(x.shape, (k, 1))      # a 1-row view's row stride is arbitrary
+    if not (x.stride(1) == 1 and (k % 8 != 0 or (x.stride(0) % 4 == 0
+                                                 and x.data_ptr() % 16 == 0))):
+        x = x.contiguous()                 # the split kernels need 16-B aligned rows
+        if k % 8 == 0 and x.data_ptr() % 16 != 0:
+            x = x.clone()
+    sw = weight_image(w, transpose, tag, MODE, cache=cache, rows=rows)
     m = x.shape[0]
     if out is None:
         out = torch.empty((m, n), dtype=torch.float32, device=x.device)
-    _lib.check(_lib.load().fgr_gemm_bf16x3(_ptr(x), x.stride(0), _ptr(sw.hi), _ptr(sw.lo), sw.ldw,
-                                           _ptr(out), out.stride(0), _ptr(bias), _ptr(residual),
-                                           residual.stride(0) if residual is not None else 0,
-                                           m, n, k, act, _stream()), 'fgr_gemm_bf16x3')
+    L = _lib.load()
+    t0 = _begin('gemm', (m, n, k))
+    # split-K workspace where the dispatcher wants one (few rows, long K)
+    nb = _lib._sz(0)
+    _lib.check(L.fgr_gemm_workspace(m, n, k, 0 if MODE == 'f16x3' else 1, nb),
+               'fgr_gemm_workspace')
+    ws = ops._workspace(x.device, nb.value) if nb.value else None
+    _lib.check(getattr(L, 'fgr_gemm_' + MODE + '_ws')(
+        _ptr(x), x.stride(0), _ptr(sw.img), _ptr(out), out.stride(0), _ptr(bias),
+        _ptr(residual), residual.stride(0) if residual is not None else 0, m, n, k, act,
+        _ptr(ws), nb.value, _stream()), 'fgr_gemm_' + MODE)
+    _end('gemm', t0, 2 * m * n * k)
     return out
 
 
@@ -302,7 +174,7 @@ def linear_presplit(a: SplitRows, w: torch.Tensor, bias=None, act=ACT_NONE, resi
     """act(A @ W^T + bias (+ residual)) with A given as a SplitRows image (fgr_gemm_h3_presplit)."""
     n, k = w.shape
     assert k == a.k
-    sw = split_weight3(w, False, tag, 'h3')
+    sw = weight_image(w, False, tag, 'f16x3')
     if out is None:
         out = torch.empty((a.m, n), dtype=torch.float32, device=w.device)
     t0 = _begin('gemm', (a.m, n, k))

@@ -339,73 +339,6 @@ def gather_bytes(idx, ns, cin, n_kp):
     return nq * (8 * H + 12 + 4 * n_kp * cin + 4) + v * (12 + 4 * cin)
 
 
-class KPFusedWeight:
-    """fgr_kpconv_fused_weights image of a KPConv weight (K, Cin, Cout) for one mode, cached
-    against the tensor's identity / version / data pointer (as linear.split_weight3)."""
-    __slots__ = ('img', 'mode', 'src', 'version', 'ptr')
-
-    def __init__(self, w, mode):
-        L = _lib.load()
-        K, cin, cout = w.shape
-        nb = _lib._sz(0)
-        _lib.check(L.fgr_kpconv_fused_weights_bytes(K, cin, cout, mode, nb),
-                   'fgr_kpconv_fused_weights_bytes')
-        self.img = torch.empty(nb.value, dtype=torch.uint8, device=w.device)
-        wc = w.detach().contiguous()
-        _lib.check(L.fgr_kpconv_fused_weights(_ptr(wc), K, cin, cout, mode, _ptr(self.img),
-                                              _stream()), 'fgr_kpconv_fused_weights')
-        self.mode, self.src, self.version, self.ptr = mode, w, w._version, w.data_ptr()
-
-
-_KPF_CACHE = {}
-
-
-def kpconv_fused_weight(w, mode) -> KPFusedWeight:
-    ent = _KPF_CACHE.get((id(w), mode))
-    if not (ent is not None and ent.src is w and ent.version == w._version
-            and ent.ptr == w.data_ptr()):
-        ent = KPFusedWeight(w, mode)
-        _KPF_CACHE[(id(w), mode)] = ent
-    return ent
-
-
-def kpconv_fused(q, s, idx, x, kernel_points, extent, w, mode=_lib.KPF_F16X3):
-    """-> (out (Nq, Cout) = sum_k wf_k @ W_k, nnorm (Nq,)) by fgr_kpconv_fused: the gather and
-    the weight GEMM in one launch (finegrained_kpconv_blocks.py:296-399 up to the division)."""
-    _dev(q, s, idx, x, kernel_points, w)
-    q, s, x = _c(q, torch.float32), _c(s, torch.float32), _c(x, torch.float32)
-    idx = _c(idx, torch.int64)
-    kp = _c(kernel_points, torch.float32)
-    nq, ns = q.shape[0], s.shape[0]
-    K, cin, cout = w.shape
-    assert idx.dim() == 2 and idx.shape[0] == nq and x.dim() == 2 and x.shape == (ns, cin)
-    assert kp.shape == (K, 3)
-    if x.data_ptr() % 16:
-        x = x.clone()
-    img = kpconv_fused_weight(w, mode)
-    out = torch.empty((nq, cout), dtype=torch.float32, device=q.device)
-    nnorm = torch.empty((nq,), dtype=torch.float32, device=q.device)
-    L = _lib.load()
-    nb = _lib._sz(0)
-    _lib.check(L.fgr_kpconv_fused_workspace(ns, nb), 'fgr_kpconv_fused_workspace')
-    ws = _workspace(q.device, nb.value)
-    t0 = _begin('kpconv_fused', (nq, cout, K * cin))
-    _lib.check(L.fgr_kpconv_fused(_ptr(q), _ptr(s), nq, ns, _ptr(idx), idx.shape[1], _ptr(x), cin,
-                                  _ptr(kp), K, float(extent), _ptr(img.img), cout, mode, _ptr(out),
-                                  out.stride(0), _ptr(nnorm), _ptr(ws), nb.value, _stream()),
-               'fgr_kpconv_fused')
-    _end('kpconv_fused', t0, lambda: fused_bytes(idx, ns, cin, cout))
-    return out, nnorm
-
-
-def fused_bytes(idx, ns, cin, cout):
-    """Algorithmic HBM bytes of one fgr_kpconv_fused launch (SURVEY.md §8(d) D4 with the wf
-    term replaced by the output row): sum_q [8*H + 12 + v_q*(12 + 4*cin) + 4*cout + 4]."""
-    nq, H = idx.shape
-    v = int((idx < ns).sum().item())
-    return nq * (8 * H + 12 + 4 * cout + 4) + v * (12 + 4 * cin)
-
-
 def max_pool(x, idx) -> torch.Tensor:
     _dev(x, idx)
     x, idx = _c(x, torch.float32), _c(idx, torch.int64)
@@ -487,14 +420,6 @@ def sine_pos_embed(xyz, d_model, temperature=10000.0, scale=1.0) -> torch.Tensor
 # ------------------------------------------------------------------------------------------
 # Res2Net hierarchy
 # ------------------------------------------------------------------------------------------
-def res2net_fragments(weights: torch.Tensor) -> torch.Tensor:
-    """(nums, w, w) Linear weights (out, in) -> MFMA fragment order [i][jt][k4][lane][4]
-    with value W_i[jt*16 + (lane & 15)][(4*k4 + q)*4 + (lane >> 4)]."""
-    nums, w, _ = weights.shape
-    t = weights.reshape(nums, w // 16, 16, w // 16, 4, 4)      # [i, jt, c, k4, q, g]
-    return t.permute(0, 1, 3, 5, 2, 4).contiguous()             # [i, jt, k4, g, c, q]
-
-
 def res2net_fragments3(weights: torch.Tensor) -> torch.Tensor:
     """(nums, w, w) Linear weights (out, in) -> the bf16x6 image of fgr_res2net_chain6:
     K zero-padded to a multiple of 32, each value split exactly into three bf16 terms
@@ -536,51 +461,47 @@ def res2net_fragments_h3(weights: torch.Tensor):
 
 
 def res2net_chain_supported(w, h3=False):
-    """fp32 / bf16x6 chains: w = 112, 224; the f16x3 chain: any w % 4 == 0 up to 224 whose
-    16-column tile count has a kernel instance (28, 56, 112, 224: every reference width)."""
+    """bf16x6 chain (fgr_res2net_chain6): w = 112, 224; the f16x3 chain: any w % 4 == 0 up to
+    224 whose 16-column tile count has a kernel instance (28, 56, 112, 224: every reference
+    width)."""
     if h3:
         return w % 4 == 0 and (w + 15) // 16 in (2, 4, 7, 14)
     return w in (112, 224)
 
 
-def res2net_chain(h, w, scale, w_frag, bias, x, cat, split6=False, w_scale=None):
-    """cat[:, :] = [sp_0..sp_{scale-2} | h_{scale-1} | x] (fgr_res2net_chain, fp32 MFMA;
-    fgr_res2net_chain6, fp32-accurate split bf16, with w_frag = res2net_fragments3; or
-    fgr_res2net_chain_h3, scaled split fp16, with (w_frag, w_scale) = res2net_fragments_h3)."""
-    if w_scale is not None:
-        _dev(h, w_frag, w_scale, bias, x, cat)
-        h = _c(h, torch.float32)
-        n = h.shape[0]
-        assert h.shape[1] == scale * w and cat.shape[0] == n and cat.stride(1) == 1
-        cin = 0 if x is None else x.shape[1]
-        if x is not None:
-            x = _c(x, torch.float32)
-        _lib.check(_lib.load().fgr_res2net_chain_h3(
-            _ptr(h), n, w, scale, _ptr(w_frag), _ptr(w_scale), _ptr(bias), _ptr(x), cin,
-            _ptr(cat), cat.stride(0), _stream()), 'fgr_res2net_chain_h3')
-        return cat
-    _dev(h, w_frag, bias, x, cat)
+def res2net_chain(h, w, scale, w_frag, bias, x, cat, w_scale=None):
+    """cat[:, :] = [sp_0..sp_{scale-2} | h_{scale-1} | x] by fgr_res2net_chain_h3 (scaled split
+    fp16, (w_frag, w_scale) = res2net_fragments_h3) or, when w_scale is None,
+    fgr_res2net_chain6 (exact three-term split bf16, w_frag = res2net_fragments3)."""
+    _dev(h, w_frag, w_scale, bias, x, cat)
     h = _c(h, torch.float32)
     n = h.shape[0]
     assert h.shape[1] == scale * w and cat.shape[0] == n and cat.stride(1) == 1
     cin = 0 if x is None else x.shape[1]
     if x is not None:
         x = _c(x, torch.float32)
-    fn = _lib.load().fgr_res2net_chain6 if split6 else _lib.load().fgr_res2net_chain
-    _lib.check(fn(_ptr(h), n, w, scale, _ptr(w_frag), _ptr(bias), _ptr(x), cin, _ptr(cat),
-                  cat.stride(0), _stream()), 'fgr_res2net_chain6' if split6 else 'fgr_res2net_chain')
+    L = _lib.load()
+    if w_scale is not None:
+        _lib.check(L.fgr_res2net_chain_h3(
+            _ptr(h), n, w, scale, _ptr(w_frag), _ptr(w_scale), _ptr(bias), _ptr(x), cin,
+            _ptr(cat), cat.stride(0), _stream()), 'fgr_res2net_chain_h3')
+    else:
+        _lib.check(L.fgr_res2net_chain6(_ptr(h), n, w, scale, _ptr(w_frag), _ptr(bias), _ptr(x),
+                                        cin, _ptr(cat), cat.stride(0), _stream()),
+                   'fgr_res2net_chain6')
     return cat
 
 
 # ------------------------------------------------------------------------------------------
 # attention
 # ------------------------------------------------------------------------------------------
-# head_dim 32 / 64: fgr_attention_f16x3 (fp32-accurate scaled split-fp16 MFMA, default);
-# head_dim 32: fgr_attention_bf16x6 (split-bf16, 6 products); fgr_attention (fp32 MFMA)
-# otherwise; 'bf16' (head_dim 32 / 64): fgr_attention_bf16, one bf16 product per fp32 product
-# (the BASELINE configs[4] compute mode, set together with linear.MODE by set_precision).
-# FGREG_ATTN = f16x3 | bf16x6 | bf16 | fp32 selects (a precision A/B switch, all on the GPU).
+# head_dim 32 / 64 (every reference config): fgr_attention_f16x3 (fp32-accurate scaled
+# split-fp16 MFMA, default) or, in the 'bf16' mode (the BASELINE configs[4] compute mode, set
+# together with linear.MODE by set_precision), fgr_attention_bf16 -- one bf16 product per fp32
+# product. Any other head_dim (4, 8, 16, 128, 256) or unaligned operand: fgr_attention (fp32
+# MFMA). FGREG_ATTN = f16x3 | bf16 overrides the attention mode alone (profiling A/B switch).
 ATTN_MODE = os.environ.get('FGREG_ATTN', 'f16x3')
+assert ATTN_MODE in ('f16x3', 'bf16'), ATTN_MODE
 
 
 def attention(q, k, v, q_off, kv_off, kv_seg, max_q_len, n_head, out=None,
@@ -604,8 +525,7 @@ def attention(q, k, v, q_off, kv_off, kv_seg, max_q_len, n_head, out=None,
     assert kv_seg.dtype == torch.int32 and kv_seg.numel() == n_seg
     max_kv_len = max_q_len if max_kv_len is None else max_kv_len
     L = _lib.load()
-    split = (((ATTN_MODE in ('f16x3', 'bf16') and dh in (32, 64))
-              or (ATTN_MODE == 'bf16x6' and dh == 32))
+    split = (dh in (32, 64)
              and all(t.stride(0) % 4 == 0 and t.data_ptr() % 16 == 0 for t in (q, k, v, out)))
     t0 = _begin('attention')
     if split:

@@ -22,9 +22,7 @@ import copy
 
 import torch
 import torch.nn as nn
-import torch.nn.functional as F
 
-from . import linear as lin
 from . import ops
 from .linear import linear
 
@@ -93,9 +91,9 @@ class TransformerCrossEncoderLayer(nn.Module):
             qkv = linear(h_pos, W, b)                                 # (N, 3d): [q | k | v]
             q, k, v = qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:]
         else:
-            qk = torch.addmm(b[:2 * d], h_pos, W[:2 * d].t())
+            qk = linear(h_pos, W, b[:2 * d], rows=(0, 2 * d))         # [q | k]
             q, k = qk[:, :d], qk[:, d:]
-            v = torch.addmm(b[2 * d:], h_nopos, W[2 * d:].t())
+            v = linear(h_nopos, W, b[2 * d:], rows=(2 * d, 3 * d))
         o = ops.attention(q, k, v, seg.off, seg.off, kv_seg, seg.max_len, self.nhead)
         return o
 
@@ -106,9 +104,6 @@ class TransformerCrossEncoderLayer(nn.Module):
         LayerNorm only reads x (no in-place bias pass writing x back); ``pending_bias`` (a
         bias still to be added to x by the first LayerNorm) is accepted for callers that
         defer one, and the returned pending bias is None."""
-        if (pending_bias is None and lin.MODE == 'f16x3' and lin.ROWS != '0'
-                and self.sa_val_has_pos_emb and self.ca_val_has_pos_emb and x.shape[1] <= 256):
-            return self._forward_rows(x, pos, seg)
         # self-attention, shared weights for src and tgt (:193-210)
         h = ops.layernorm(x, self.norm1.weight, self.norm1.bias, self.norm1.eps, add=pos,
                           pre_bias=pending_bias)
@@ -127,20 +122,6 @@ class TransformerCrossEncoderLayer(nn.Module):
         h = ops.layernorm(x, self.norm3.weight, self.norm3.bias, self.norm3.eps)
         h = linear(h, self.linear1.weight, self.linear1.bias, act=ops.ACT_RELU)
         return linear(h, self.linear2.weight, self.linear2.bias, residual=x), None
-
-    def _forward_rows(self, x, pos, seg: Segments):
-        """forward_pre with each LayerNorm (+ pos) fused into the GEMM that consumes it
-        (fgr_gemm_rows_f16x3: norm1/norm2 + pos -> in_proj, norm3 -> linear1) and every
-        bias / residual in a GEMM epilogue; x is updated in place. -> (x, None)."""
-        d = x.shape[1]
-        for norm, mha, kv_seg in ((self.norm1, self.self_attn, seg.self_seg),
-                                  (self.norm2, self.multihead_attn, seg.cross_seg)):
-            qkv = linear(x, mha.in_proj_weight, mha.in_proj_bias, ln=norm, add=pos)
-            o = ops.attention(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], seg.off, seg.off,
-                              kv_seg, seg.max_len, self.nhead)
-            x = linear(o, mha.out_proj.weight, mha.out_proj.bias, residual=x, out=x)
-        h = linear(x, self.linear1.weight, self.linear1.bias, act=ops.ACT_RELU, ln=self.norm3)
-        return linear(h, self.linear2.weight, self.linear2.bias, residual=x, out=x), None
 
 
 class TransformerCrossEncoder(nn.Module):

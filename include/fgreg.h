@@ -57,8 +57,8 @@ const char* fgr_last_error(void);
 
 /* Opt-in instrumentation (bench.py's per-kernel rooflines; not part of the reference's
  * interface): arms two caller-created hipEvent_t for the NEXT timed entry point called on
- * this thread (fgr_kpconv_gather, fgr_attention*, fgr_gemm_bf16x6, fgr_gemm_f16x3,
- * fgr_gemm_bf16, fgr_gemm_rows_f16x3, fgr_grid_subsample_count / _fill, fgr_radius_search,
+ * this thread (fgr_kpconv_gather, fgr_attention*, fgr_gemm_f16x3, fgr_gemm_bf16,
+ * fgr_grid_subsample_count / _fill, fgr_radius_search,
  * fgr_radius_grid_build, fgr_radius_search_grid, fgr_instnorm, fgr_layernorm,
  * fgr_pair_pose). That call records `start_event` on its stream right before its
  * first kernel launch and `end_event` after its last one, then disarms; (NULL, NULL)
@@ -132,27 +132,6 @@ int fgr_kpconv_gather(const float* q, const float* s, int64_t nq, int64_t ns, co
                       float extent, float* wf, float* nnorm, void* workspace, size_t ws_bytes,
                       void* stream);
 
-/* Fused KPConv: the gather-weight stage above and the weight GEMM in ONE
- * launch, wf never written (finegrained_kpconv_blocks.py:296-399 up to the division):
- *   out[q, n] = sum_{k, c} wf[q, k, c] W[k, c, n]   (out: nq x cout, row stride ldo),
- *   nnorm[q]  = as fgr_kpconv_gather;  the caller divides (or fuses out / nnorm downstream).
- * mode FGR_KPF_F16X3: fp32-accurate (f16x3 split MFMA, the contract of fgr_gemm_f16x3);
- * FGR_KPF_BF16: wf rounded to bf16 where it enters the MFMA (the bf16 compute mode).
- * W (n_kp, cin, cout) fp32 contiguous -> image by fgr_kpconv_fused_weights (built once per
- * weight, fgr_kpconv_fused_weights_bytes() bytes, 16-B aligned; the contraction order of the
- * fused kernel). cin % 16 == 0, n_kp <= 15; x, w_img, out 16-B aligned.
- * workspace: fgr_kpconv_fused_workspace() bytes (per-source-row flags of the normaliser). */
-enum { FGR_KPF_F16X3 = 0, FGR_KPF_BF16 = 1 };
-int fgr_kpconv_fused_weights_bytes(int32_t n_kp, int32_t cin, int32_t cout, int32_t mode,
-                                   size_t* bytes);
-int fgr_kpconv_fused_weights(const float* w, int32_t n_kp, int32_t cin, int32_t cout,
-                             int32_t mode, void* img, void* stream);
-int fgr_kpconv_fused_workspace(int64_t ns, size_t* bytes);
-int fgr_kpconv_fused(const float* q, const float* s, int64_t nq, int64_t ns, const int64_t* idx,
-                     int32_t width, const float* x, int32_t cin, const float* kp, int32_t n_kp,
-                     float extent, const void* w_img, int32_t cout, int32_t mode, float* out,
-                     int64_t ldo, float* nnorm, void* workspace, size_t ws_bytes, void* stream);
-
 /* max_pool (finegrained_kpconv_blocks.py:125-141): out[q, c] = max over the row of
  * x[idx[q, h], c], shadow entries contributing 0 (the appended zero row). */
 int fgr_max_pool(const float* x, int64_t ns, int32_t c, const int64_t* idx, int64_t nq,
@@ -188,14 +167,10 @@ int fgr_sine_pos_embed(const float* xyz, int64_t n, int32_t d_model, float tempe
  * folded into the Linears: for i < scale - 1,
  *   sp_i = ReLU(W_i (sp_{i-1} + h_i) + b_i)          (sp_{-1} = 0)
  * writing cat = [sp_0 .. sp_{scale-2} | h_{scale-1} | x] (the conv3 / downsample operand).
- * h (n, scale*w), x (n, cin) or NULL, cat (n, ld_cat); w_frag = the (scale-1) folded
- * (w, w) weights permuted to MFMA fragment order [i][jt][k4][lane][4] (see fgreg/backbone.py);
- * bias (scale-1, w). Needs w % 112 == 0 (w = 112, 224: the ModelNet / 3DMatch deep widths). */
-int fgr_res2net_chain(const float* h, int64_t n, int32_t w, int32_t scale, const float* w_frag,
-                      const float* bias, const float* x, int32_t cin, float* cat, int64_t ld_cat,
-                      void* stream);
-/* fp32-accurate bf16x6 variant (used for w = 224, where it measured faster): w_img = the (nums, w, w) folded weights
- * K-padded to a multiple of 32, split into three bf16 terms and laid out in 16x16x32
+ * h (n, scale*w), x (n, cin) or NULL, cat (n, ld_cat); bias (scale-1, w).
+ * fgr_res2net_chain6 (fp32-accurate split bf16: three exact bf16 terms, six products; w = 112
+ * or 224, dispatched at w = 224 where it measured faster): w_img = the (scale-1, w, w) folded
+ * weights K-padded to a multiple of 32, split into three bf16 terms and laid out in 16x16x32
  * fragment order [i][jt][ks][term][g][c][8] (fgreg.ops.res2net_fragments3); h 16-B aligned. */
 int fgr_res2net_chain6(const float* h, int64_t n, int32_t w, int32_t scale, const void* w_img,
                        const float* bias, const float* x, int32_t cin, float* cat,
@@ -210,40 +185,18 @@ int fgr_res2net_chain_h3(const float* h, int64_t n, int32_t w, int32_t scale, co
                          float* cat, int64_t ld_cat, void* stream);
 
 /* ---- dense layers ----------------------------------------------------------------------
- * Split-precision GEMM for every Linear / KPConv-weight product of the forward:
+ * Every Linear / KPConv-weight product of the forward:
  *   C[m, n] = act(A[m, :] . W[n, :] + bias[n] (+ R[m, n]))
- * A fp32 (row stride lda, 16-B aligned, k % 4 == 0); W given as bf16 (hi, lo) pairs of shape
- * (n, ldw), ldw % 32 == 0, zero-padded beyond k (fgr_split_weights). Products accumulate in
- * fp32 as A_lo W_hi + A_hi W_lo + A_hi W_hi on v_mfma_f32_16x16x32_bf16: ~2^-16 relative
- * per product, at the bf16 matrix rate (gfx950 has no xf32). act: FGR_ACT_NONE / _RELU. */
-int fgr_split_weights(const float* w, int32_t n, int32_t k, int64_t ldw, void* w_hi, void* w_lo,
-                      void* stream);
-int fgr_gemm_bf16x3(const float* a, int64_t lda, const void* w_hi, const void* w_lo, int64_t ldw,
-                    float* c, int64_t ldc, const float* bias, const float* r, int64_t ldr,
-                    int32_t m, int32_t n, int32_t k, int32_t act, void* stream);
-
-/* fp32-accurate split-bf16 GEMM ("bf16x6", opt-in FGREG_GEMM=bf16x6; the default is
- * fgr_gemm_f16x3 below):
- *   C[m, n] = act(A[m, :] . W[n, :] + bias[n] (+ R[m, n]))
- * Operands are split exactly into three bf16 terms (x = h + m + l, residual <= 2^-27 |x|)
- * and the six significant term products accumulate in fp32 on v_mfma_f32_16x16x32_bf16.
- * W is given as an image built once by fgr_split_weights3 (W element (i, j) read from
- * w[i * stride_n + j * stride_k], so a (K, Cin, Cout) KPConv weight needs no transpose
- * copy); A fp32 row-major, 16-B aligned with lda % 4 == 0 when k % 8 == 0. */
-int fgr_split_weights3_bytes(int32_t n, int32_t k, size_t* bytes);
-int fgr_split_weights3(const float* w, int32_t n, int32_t k, int64_t stride_n, int64_t stride_k,
-                       void* img, void* stream);
-int fgr_gemm_bf16x6(const float* a, int64_t lda, const void* w_img, float* c, int64_t ldc,
-                    const float* bias, const float* r, int64_t ldr, int32_t m, int32_t n,
-                    int32_t k, int32_t act, void* stream);
-
-/* fp32-accurate scaled split-fp16 GEMM ("f16x3"), same contract as fgr_gemm_bf16x6:
- *   C[m, n] = act(A[m, :] . W[n, :] + bias[n] (+ R[m, n]))
+ * W is given as an image built once per weight (element (i, j) read from
+ * w[i * stride_n + j * stride_k], so a (K, Cin, Cout) KPConv weight needs no transpose copy);
+ * A fp32 row-major, 16-B aligned with lda % 4 == 0 when k % 8 == 0.
+ *
+ * fp32-accurate scaled split-fp16 GEMM ("f16x3", the default mode):
  * W rows are scaled by powers of two (row max in [2^14, 2^15)) and A rows on the fly (per
  * row, lowered only when a later k chunk would overflow fp16, with an exact rescale of the
  * partial sums); each operand is then split into two fp16 terms (2^-22 relative) and the
  * three significant term products accumulate in fp32 on v_mfma_f32_16x16x32_f16: <= ~3 *
- * 2^-22 relative per product, half the matrix-core work of bf16x6. The image (built once by
+ * 2^-22 relative per product (fp32's own rounding is 2^-24). The image (built once by
  * fgr_split_weights_h3, fgr_split_weights_h3_bytes() bytes, 16-B aligned) holds the split W
  * in tile order followed by the per-row inverse scales. */
 int fgr_split_weights_h3_bytes(int32_t n, int32_t k, size_t* bytes);
@@ -294,52 +247,27 @@ int fgr_gemm_h3_presplit(const void* a_img, const void* w_img, float* c, int64_t
                          const float* bias, const float* r, int64_t ldr, int32_t m, int32_t n,
                          int32_t k, int32_t act, void* stream);
 
-/* Row-resident f16x3 GEMM for short contractions (k <= 256, k % 8 == 0) with the LayerNorm
- * (+ positional add) that produces its input fused into the row loads -- the transformer's
- * norm -> Linear pairs (transformers.py:193-238: norm1/2 + pos -> in_proj, norm3 -> linear1):
- *   A = ln_gamma ? LN(x) * ln_gamma + ln_beta (+ add) : x (+ add)   (LN eps ln_eps, biased var)
- *   C = act(A . W^T + bias (+ R))                                    (act as fgr_gemm_f16x3)
- * Each A row is scaled by its exact max (no online rescale). w_img from fgr_split_weights_h3;
- * x, add, w_img 16-B aligned with ldx, ld_add % 4 == 0. */
-int fgr_gemm_rows_f16x3(const float* x, int64_t ldx, const float* ln_gamma, const float* ln_beta,
-                        float ln_eps, const float* add, int64_t ld_add, const void* w_img, float* c,
-                        int64_t ldc, const float* bias, const float* r, int64_t ldr, int32_t m,
-                        int32_t n, int32_t k, int32_t act, void* stream);
-
 /* ---- attention ---------------------------------------------------------------------
  * Multi-head scaled-dot-product attention core of nn.MultiheadAttention
  * (transformers.py:95-96, 197-226) on packed, unpadded segments: query segment
  * i (rows q_off[i]..q_off[i+1]) attends to key segment kv_seg[i] (rows
  * kv_off[j]..kv_off[j+1]); the reference's key padding mask is the segment end.
  * Head h reads columns [h*dh, (h+1)*dh) of q/k/v rows (row strides ld_*).
- * o = softmax((q * scale) k^T) v, fp32 in/out, fp32 MFMA (v_mfma_f32_16x16x4_f32). */
+ * o = softmax((q * scale) k^T) v, fp32 in/out, fp32 MFMA (v_mfma_f32_16x16x4_f32); any
+ * head_dim in {4, 8, 16, 32, 64, 128, 256} (the forward dispatches head_dim 32 / 64 -- every
+ * reference config -- to fgr_attention_f16x3 / _bf16 below). */
 int fgr_attention(const float* q, int64_t ld_q, const float* k, int64_t ld_k, const float* v,
                   int64_t ld_v, float* o, int64_t ld_o, const int64_t* q_off,
                   const int64_t* kv_off, const int32_t* kv_seg, int32_t n_seg,
                   int32_t max_q_len, int32_t n_head, int32_t head_dim, float scale, void* stream);
 
-/* fp32-accurate attention on the bf16 matrix cores (head_dim 32, the reference configs'
- * d_embed 256 / nhead 8): same semantics and arguments as fgr_attention, plus the key
- * segment count / row count / longest key segment, and a caller workspace of
- * fgr_attention_bf16x6_workspace() bytes holding the split K/V images. Every operand is
- * split exactly into three bf16 terms and each product accumulates the six significant
- * term products in fp32 (residual ~2^-27 relative, below fp32's own 2^-24 rounding).
- * q/k/v/o 16-B aligned, row strides multiples of 4. */
-int fgr_attention_bf16x6_workspace(int64_t n_kv_rows, int32_t n_kv_seg, int32_t n_head,
-                                   size_t* bytes);
-int fgr_attention_bf16x6(const float* q, int64_t ld_q, const float* k, int64_t ld_k,
-                         const float* v, int64_t ld_v, float* o, int64_t ld_o,
-                         const int64_t* q_off, const int64_t* kv_off, const int32_t* kv_seg,
-                         int32_t n_seg, int32_t n_kv_seg, int64_t n_kv_rows, int32_t max_q_len,
-                         int32_t max_kv_len, int32_t n_head, int32_t head_dim, float scale,
-                         void* workspace, int64_t ws_bytes, void* stream);
-
 /* fp32-accurate attention on the fp16 matrix cores (head_dim 32 -- ModelNet's d 256 / 8 heads --
- * or 64 -- 3DMatch's d 512 / 8 heads), same semantics and
- * arguments as fgr_attention_bf16x6: K/V are scaled per (64-key tile, head), Q per query and
- * P by 2^14 into fp16's normal range (exact powers of two), split into two fp16 terms and
- * the three significant term products accumulate in fp32 (<= ~3 * 2^-22 per product) at half
- * the matrix-core work of bf16x6. Workspace: fgr_attention_f16x3_workspace() bytes (split
+ * or 64 -- 3DMatch's d 512 / 8 heads), same semantics and arguments as fgr_attention plus
+ * the key segment count / row count / longest key segment and a caller workspace: K/V are
+ * scaled per (64-key tile, head), Q per query and P by 2^14 into fp16's normal range (exact
+ * powers of two), split into two fp16 terms and the three significant term products
+ * accumulate in fp32 (<= ~3 * 2^-22 per product); q/k/v/o 16-B aligned, row strides
+ * multiples of 4. Workspace: fgr_attention_f16x3_workspace() bytes (split
  * K/V images + per-tile scale exponents), 16-B aligned. */
 int fgr_attention_f16x3_workspace(int64_t n_kv_rows, int32_t n_kv_seg, int32_t n_head,
                                   size_t* bytes);
