@@ -81,31 +81,11 @@ __device__ __forceinline__ float kp_weight(float nx, float ny, float nz, const f
     return fmaxf(1.0f - sqrtf(d2) * inv_extent, 0.0f);
 }
 
-// Row flags for the normaliser: pos[r] = (sum_c x[r, c] > 0), one wave per row. The
-// positivity of a source row does not depend on the query, so it is computed once per
-// call instead of once per (query, neighbour) -- the gather then counts positive
-// neighbours with one ballot per 64 neighbours instead of a 64-lane reduction each.
-template <int VEC>
-__global__ void __launch_bounds__(256)
-row_positive_kernel(const float* __restrict__ x, int64_t ns, unsigned char* __restrict__ pos) {
-    constexpr int CIN = 64 * VEC;
-    const int64_t r = (int64_t)blockIdx.x * 4 + threadIdx.x / 64;
-    const int lane = threadIdx.x % 64;
-    if (r >= ns) return;
-    float xv[VEC];
-    load_vec<VEC>(x + r * CIN + lane * VEC, xv);
-    float t = 0.f;
-#pragma unroll
-    for (int j = 0; j < VEC; ++j) t += xv[j];
-    t = wave_sum(t);
-    if (lane == 0) pos[r] = t > 0.f ? 1 : 0;
-}
-
 // One wave per query, cin = 64 * VEC, K kernel points (runtime, <= kMaxKp, unrolled by KU).
 // Valid neighbours of each 64-wide chunk are compacted by ballot; their feature rows are
 // then streamed 4 at a time (4 x 16-B loads in flight per lane) into K accumulators.
 // POSI: the normaliser's "row sum > 0" is taken from the rows as they stream by (a DPP /
-// permlane wave sum per row, no LDS); otherwise from the row_positive_kernel flags.
+// permlane wave sum per row, no LDS); otherwise from per-source-row flags `pos`.
 template <int VEC, int KU, bool POSI>
 __global__ void __launch_bounds__(64 * kGatherWaves)
 kpconv_gather_wide(const float* __restrict__ q, const float* __restrict__ s, int64_t nq, int64_t ns,
@@ -411,36 +391,18 @@ void launch_narrow(const float* q, const float* s, int64_t nq, int64_t ns, const
                        st, q, s, nq, ns, idx, width, x, cin, kp, n_kp, inv_ext, wf, nnorm);
 }
 
-template <int VEC, bool POSI>
+template <int VEC>
 void launch_wide_k(const float* q, const float* s, int64_t nq, int64_t ns, const int64_t* idx,
-                   int width, const float* x, unsigned char* pos, const float* kp, int n_kp,
-                   float inv_ext, float* wf, float* nnorm, hipStream_t st) {
+                   int width, const float* x, const float* kp, int n_kp, float inv_ext, float* wf,
+                   float* nnorm, hipStream_t st) {
     dim3 grid((unsigned)ceil_div(nq, kGatherWaves));
     if (n_kp <= 16)
-        hipLaunchKernelGGL((kpconv_gather_wide<VEC, 16, POSI>), grid, dim3(64 * kGatherWaves), 0,
-                           st, q, s, nq, ns, idx, width, x, pos, kp, n_kp, inv_ext, wf, nnorm);
+        hipLaunchKernelGGL((kpconv_gather_wide<VEC, 16, true>), grid, dim3(64 * kGatherWaves), 0,
+                           st, q, s, nq, ns, idx, width, x, nullptr, kp, n_kp, inv_ext, wf, nnorm);
     else
-        hipLaunchKernelGGL((kpconv_gather_wide<VEC, kMaxKp, POSI>), grid, dim3(64 * kGatherWaves),
-                           0, st, q, s, nq, ns, idx, width, x, pos, kp, n_kp, inv_ext, wf, nnorm);
-}
-
-// Positivity inline (default) or from the per-source-row pre-pass (FGR_GATHER_PREPASS=1,
-// kept for A/B measurements).
-template <int VEC>
-void launch_wide(const float* q, const float* s, int64_t nq, int64_t ns, const int64_t* idx,
-                 int width, const float* x, unsigned char* pos, const float* kp, int n_kp,
-                 float inv_ext, float* wf, float* nnorm, hipStream_t st) {
-    const char* pre = getenv("FGR_GATHER_PREPASS");
-    if (pre && pre[0] == '1') {
-        if (ns > 0)
-            hipLaunchKernelGGL(row_positive_kernel<VEC>, dim3((unsigned)ceil_div(ns, 4)),
-                               dim3(256), 0, st, x, ns, pos);
-        launch_wide_k<VEC, false>(q, s, nq, ns, idx, width, x, pos, kp, n_kp, inv_ext, wf, nnorm,
-                                  st);
-    } else {
-        launch_wide_k<VEC, true>(q, s, nq, ns, idx, width, x, pos, kp, n_kp, inv_ext, wf, nnorm,
-                                 st);
-    }
+        hipLaunchKernelGGL((kpconv_gather_wide<VEC, kMaxKp, true>), grid, dim3(64 * kGatherWaves),
+                           0, st, q, s, nq, ns, idx, width, x, nullptr, kp, n_kp, inv_ext, wf,
+                           nnorm);
 }
 
 // max_pool, one wave per query (c % 64 == 0, VEC floats per lane): valid neighbours are
@@ -509,7 +471,7 @@ using namespace fgr;
 
 extern "C" int fgr_kpconv_gather_workspace(int64_t ns, int32_t cin, size_t* bytes) {
     FGR_REQUIRE(bytes && ns >= 0 && cin > 0, "fgr_kpconv_gather_workspace: bad arguments");
-    *bytes = (cin % 64 == 0) ? (size_t)ns : 0;
+    *bytes = 0;       // kept in the ABI; the normaliser's positivity is taken inline now
     return FGR_OK;
 }
 
@@ -517,6 +479,7 @@ extern "C" int fgr_kpconv_gather(const float* q, const float* s, int64_t nq, int
                                  const int64_t* idx, int32_t width, const float* x, int32_t cin,
                                  const float* kp, int32_t n_kp, float extent, float* wf,
                                  float* nnorm, void* workspace, size_t ws_bytes, void* stream) {
+    (void)workspace; (void)ws_bytes;
     FGR_REQUIRE(nq >= 0 && ns >= 0 && width >= 0 && cin > 0 && n_kp > 0 && n_kp <= kMaxKp &&
                     extent > 0.f,
                 "fgr_kpconv_gather: bad arguments (cin %d, n_kp %d, width %d)", cin, n_kp, width);
@@ -527,13 +490,10 @@ extern "C" int fgr_kpconv_gather(const float* q, const float* s, int64_t nq, int
     TimedCall timed_(st);
     const float inv_ext = 1.0f / extent;
     if (cin % 64 == 0 && cin <= 256) {
-        FGR_REQUIRE(workspace && ws_bytes >= (size_t)ns,
-                    "fgr_kpconv_gather: workspace of %lld bytes needed", (long long)ns);
-        unsigned char* pos = (unsigned char*)workspace;
         switch (cin / 64) {
-            case 1: launch_wide<1>(q, s, nq, ns, idx, width, x, pos, kp, n_kp, inv_ext, wf, nnorm, st); break;
-            case 2: launch_wide<2>(q, s, nq, ns, idx, width, x, pos, kp, n_kp, inv_ext, wf, nnorm, st); break;
-            default: launch_wide<4>(q, s, nq, ns, idx, width, x, pos, kp, n_kp, inv_ext, wf, nnorm, st); break;
+            case 1: launch_wide_k<1>(q, s, nq, ns, idx, width, x, kp, n_kp, inv_ext, wf, nnorm, st); break;
+            case 2: launch_wide_k<2>(q, s, nq, ns, idx, width, x, kp, n_kp, inv_ext, wf, nnorm, st); break;
+            default: launch_wide_k<4>(q, s, nq, ns, idx, width, x, kp, n_kp, inv_ext, wf, nnorm, st); break;
         }
     } else if (cin <= 64) {
         if (cin == 1) {

@@ -59,9 +59,6 @@ SIGNATURES = {
                           _sz, _vp],
     'fgr_gemm_bf16_ws': [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _vp,
                          _sz, _vp],
-    'fgr_split_rows_h3_bytes': [_i32, _i32, ctypes.POINTER(_sz)],
-    'fgr_split_rows_h3': [_vp, _i64, _i32, _i32, _vp, _vp],
-    'fgr_gemm_h3_presplit': [_vp, _vp, _vp, _i64, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _vp],
     'fgr_copy_batch': [_i32, _vp, _vp, _vp, _vp],
     'fgr_lengths_to_offsets': [_vp, _i32, _vp, _vp],
     'fgr_overlap_pool': [_vp, _i64, _vp, _i64, _i32, _vp, _vp],

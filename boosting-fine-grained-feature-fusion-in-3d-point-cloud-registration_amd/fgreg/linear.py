@@ -145,42 +145,3 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act=ACT_NONE, residual=N
         _ptr(ws), nb.value, _stream()), 'fgr_gemm_' + MODE)
     _end('gemm', t0, 2 * m * n * k)
     return out
-
-
-class SplitRows:
-    """f16x3 image of activation rows (fgr_split_rows_h3): the A operand of
-    fgr_gemm_h3_presplit, split once instead of inside every consuming GEMM block."""
-    __slots__ = ('img', 'm', 'k')
-
-    def __init__(self, img, m, k):
-        self.img, self.m, self.k = img, m, k
-
-
-def split_rows(x: torch.Tensor, out: SplitRows = None) -> SplitRows:
-    m, k = x.shape
-    L = _lib.load()
-    nb = _lib._sz(0)
-    _lib.check(L.fgr_split_rows_h3_bytes(m, k, nb), 'fgr_split_rows_h3_bytes')
-    if out is None or out.img.numel() < nb.value:
-        out = SplitRows(torch.empty(nb.value, dtype=torch.uint8, device=x.device), m, k)
-    out.m, out.k = m, k
-    _lib.check(L.fgr_split_rows_h3(_ptr(x), x.stride(0), m, k, _ptr(out.img), _stream()),
-               'fgr_split_rows_h3')
-    return out
-
-
-def linear_presplit(a: SplitRows, w: torch.Tensor, bias=None, act=ACT_NONE, residual=None,
-                    out=None, tag=None) -> torch.Tensor:
-    """act(A @ W^T + bias (+ residual)) with A given as a SplitRows image (fgr_gemm_h3_presplit)."""
-    n, k = w.shape
-    assert k == a.k
-    sw = weight_image(w, False, tag, 'f16x3')
-    if out is None:
-        out = torch.empty((a.m, n), dtype=torch.float32, device=w.device)
-    t0 = _begin('gemm', (a.m, n, k))
-    _lib.check(_lib.load().fgr_gemm_h3_presplit(
-        _ptr(a.img), _ptr(sw.img), _ptr(out), out.stride(0), _ptr(bias), _ptr(residual),
-        residual.stride(0) if residual is not None else 0, a.m, n, k, act, _stream()),
-        'fgr_gemm_h3_presplit')
-    _end('gemm', t0, 2 * a.m * n * k)
-    return out

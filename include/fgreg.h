@@ -236,17 +236,6 @@ int fgr_gemm_bf16(const float* a, int64_t lda, const void* w_img, float* c, int6
                   const float* bias, const float* r, int64_t ldr, int32_t m, int32_t n, int32_t k,
                   int32_t act, void* stream);
 
-/* Pre-split f16x3 GEMM (experimental; not on the forward's default path, DESIGN.md §(f)):
- * the activation operand as an "A image" in the weight images' fragment order with one
- * inverse scale per (row, k32 step) -- built by fgr_split_rows_h3 (fgr_split_rows_h3_bytes()
- * bytes, 16-B aligned) or by a producer kernel -- so no split runs inside the GEMM:
- *   C = act(sum_s sA[s][m] (A_s . W^T) wsc + bias (+ R)); w_img from fgr_split_weights_h3. */
-int fgr_split_rows_h3_bytes(int32_t m, int32_t k, size_t* bytes);
-int fgr_split_rows_h3(const float* x, int64_t ldx, int32_t m, int32_t k, void* img, void* stream);
-int fgr_gemm_h3_presplit(const void* a_img, const void* w_img, float* c, int64_t ldc,
-                         const float* bias, const float* r, int64_t ldr, int32_t m, int32_t n,
-                         int32_t k, int32_t act, void* stream);
-
 /* ---- attention ---------------------------------------------------------------------
  * Multi-head scaled-dot-product attention core of nn.MultiheadAttention
  * (transformers.py:95-96, 197-226) on packed, unpadded segments: query segment

@@ -37,26 +37,29 @@ def test_kpconv_block_vs_reference(gpu):
     assert torch.equal(mp.cpu(), torch.from_numpy(g['maxpool']))
 
 
-@pytest.mark.parametrize('cin,H,prepass', [(1, 50, '0'), (1, 7, '0'), (3, 50, '0'), (16, 50, '0'),
-                                           (32, 50, '0'), (64, 50, '0'), (128, 50, '0'),
-                                           (256, 50, '0'), (128, 50, '1'), (256, 70, '1'),
-                                           (64, 130, '0'), (32, 130, '0'), (32, 5, '0'),
-                                           (16, 70, '0')])
-def test_kpconv_gather_vs_torch(gpu, cin, H, prepass, monkeypatch):
-    """Gather-weight stage vs the fp32 torch restatement (all channel widths in the configs;
-    the cin = 1 stem kernel; the quad-lane kernel of cin 16 / 32 incl. widths past one
-    64-neighbour chunk; wide kernels with the inline and the pre-pass normaliser)."""
-    import fgreg.ops as ops
-    monkeypatch.setenv('FGR_GATHER_PREPASS', prepass)
-    rng = np.random.default_rng(cin + H)
-    ns, nq = 900, 700
+def _gather_case(cin, H, nq=700, ns=900, n_kp=15, seed=None):
+    rng = np.random.default_rng(cin + H if seed is None else seed)
     s = rng.uniform(-1, 1, (ns, 3)).astype(np.float32)
     q = s[rng.choice(ns, nq, replace=False)] + rng.normal(0, 0.01, (nq, 3)).astype(np.float32)
     idx = rng.integers(0, ns, (nq, H))
     idx[rng.uniform(size=(nq, H)) < 0.6] = ns            # shadows
+    if nq > 3:
+        idx[3] = ns                                      # a query with no valid neighbour
     x = rng.normal(size=(ns, cin)).astype(np.float32)
-    kp = (rng.normal(size=(15, 3)) * 0.3).astype(np.float32)
-    ext = 0.5
+    kp = (rng.normal(size=(n_kp, 3)) * 0.3).astype(np.float32)
+    return q, s, idx, x, kp
+
+
+@pytest.mark.parametrize('cin,H', [(1, 50), (1, 7), (3, 50), (16, 50), (32, 50), (64, 50),
+                                   (128, 50), (256, 50), (256, 70), (64, 130), (32, 130),
+                                   (32, 5), (16, 70)])
+def test_kpconv_gather_vs_torch(gpu, cin, H):
+    """Gather-weight stage vs the fp32 torch restatement (all channel widths in the configs;
+    the cin = 1 stem kernel; the quad-lane kernel of cin 16 / 32 incl. widths past one
+    64-neighbour chunk; the wide kernels)."""
+    import fgreg.ops as ops
+    q, s, idx, x, kp = _gather_case(cin, H)
+    ns, ext = s.shape[0], 0.5
     T = lambda a: torch.from_numpy(a).to(gpu)
     wf, nn_ = ops.kpconv_gather(T(q), T(s), T(idx), T(x), T(kp), ext)
     # torch fp32 reference of the same op (blocks:296-381, 395-398)
@@ -404,30 +407,3 @@ def test_gemm_f16x3_tiles(gpu, tile, monkeypatch):
             assert rel_err(out, ref) < 2e-6, (tile, m, n, k)
     finally:
         fl.set_mode(old)
-
-
-@pytest.mark.parametrize('tile', list('abcdefgh'))
-def test_gemm_h3_presplit(gpu, tile, monkeypatch):
-    """fgr_split_rows_h3 + fgr_gemm_h3_presplit (both operands pre-split images, per-(row,
-    k32 step) activation scales) vs fp64: ragged M / N / K (K % 32 != 0, M not a multiple of
-    any tile), rows spanning 1e-12 .. 1e12, zero rows, bias / residual epilogues."""
-    from fgreg import linear as fl
-    monkeypatch.setenv('FGR_GEMM_G6_TILE', tile)
-    g = torch.Generator().manual_seed(3)
-    for m, n, k in ((1000, 200, 1000), (333, 3, 96), (130, 520, 40), (4099, 272, 264)):
-        x = torch.randn(m, k, generator=g, dtype=torch.float64)
-        x *= torch.tensor([10.0 ** e for e in np.linspace(-12, 12, m)], dtype=torch.float64)[:, None]
-        x[7] = 0
-        w = torch.randn(n, k, generator=g) / math.sqrt(k)
-        b = torch.randn(n, generator=g)
-        r = torch.randn(m, n, generator=g)
-        X = x.float()
-        ref = X.double() @ w.double().t()
-        a = fl.split_rows(X.to(gpu))
-        out = fl.linear_presplit(a, w.to(gpu)).double().cpu()
-        den = (X.double().abs() @ w.double().abs().t()).clamp_min(1e-300)
-        assert float(((out - ref).abs() / den).max()) < 2e-6, (tile, m, n, k)
-        assert (out[7] == 0).all()
-        out = fl.linear_presplit(a, w.to(gpu), b.to(gpu), residual=r.to(gpu)).double().cpu()
-        full = ref + b.double() + r.double()
-        assert rel_err(out, full) < 2e-6, (tile, m, n, k)
