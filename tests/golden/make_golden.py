@@ -60,6 +60,12 @@ def _i32(a):
     return np.ascontiguousarray(np.asarray(a, dtype=np.int32))
 
 
+def _idx(a):
+    """Index table for storage: int16 where every value fits (the loaders widen to int64)."""
+    a = np.asarray(a)
+    return a.astype(np.int16) if a.size and a.min() >= 0 and a.max() < 32767 else a.astype(np.int32)
+
+
 def ref_batch_query(queries, supports, q_batches, s_batches, radius):
     q, s, qb, sb = _f32(queries), _f32(supports), _i32(q_batches), _i32(s_batches)
     w = _lib.ref_neighbors_run(q.ctypes.data_as(_fp), q.shape[0], s.ctypes.data_as(_fp), s.shape[0],
@@ -212,7 +218,7 @@ def make_geometry():
         conv1 = ref_batch_query(sub_pts, sub_pts, sub_lens, sub_lens, 2 * r0)
         save(f'geom_{name}', points=pts, lengths=lens, dl=np.float64(dl1), r0=np.float64(r0),
              limit=np.int64(limit), sub_points=sub_pts, sub_lengths=sub_lens,
-             conv=conv, pool=pool, up=up, conv1=conv1)
+             conv=_idx(conv), pool=_idx(pool), up=_idx(up), conv1=_idx(conv1))
 
     # Exact-boundary radius case: supports at |d| == r exactly in float32 must be excluded
     # (strict d2 < r2, nanoflann.hpp:249-250).
@@ -253,18 +259,20 @@ def make_modules(fr, fk):
     kp.eval()
     x = torch.randn(len(pts), 16)
     x[::7] = -x[::7].abs()  # rows whose feature sum is <= 0 do not count (blocks:395-399)
+    # queries: the first NQ rows of each table (every support row stays, shadows = len(pts))
+    NQ = 700
     with torch.no_grad():
-        out = kp(torch.from_numpy(pts), torch.from_numpy(pts), torch.from_numpy(neighb), x)
-        sub = torch.from_numpy(g['sub_points'])
-        out_strided = kp(sub, torch.from_numpy(pts), torch.from_numpy(pools), x)
-        mp = fb.max_pool(x, torch.from_numpy(pools))
-    save('kpconv_block', q=pts, s=pts, idx=neighb.astype(np.int32), x=x.numpy(), W=kp.weights.detach().numpy(),
+        out = kp(torch.from_numpy(pts[:NQ]), torch.from_numpy(pts), torch.from_numpy(neighb[:NQ]), x)
+        sub = torch.from_numpy(g['sub_points'][:NQ])
+        out_strided = kp(sub, torch.from_numpy(pts), torch.from_numpy(pools[:NQ]), x)
+        mp = fb.max_pool(x, torch.from_numpy(pools[:NQ]))
+    save('kpconv_block', q=pts[:NQ], s=pts, idx=_idx(neighb[:NQ]), x=x.numpy(), W=kp.weights.detach().numpy(),
          kp=kp.kernel_points.detach().numpy(), extent=np.float64(kp.KP_extent), out=out.numpy(),
-         sub=g['sub_points'], pools=pools.astype(np.int32), out_strided=out_strided.numpy(), maxpool=mp.numpy())
+         sub=g['sub_points'][:NQ], pools=_idx(pools[:NQ]), out_strided=out_strided.numpy(), maxpool=mp.numpy())
 
     # ---- InstanceNorm per cloud (BatchNormBlock, blocks:462-518)
-    bn = fb.BatchNormBlock(24, True, 0.02)
-    y = torch.randn(len(pts), 24) * 3 + 1
+    bn = fb.BatchNormBlock(12, True, 0.02)
+    y = torch.randn(len(pts), 12) * 3 + 1
     with torch.no_grad():
         yn = bn(y, torch.from_numpy(lens.astype(np.int64)))
     save('instnorm', x=y.numpy(), lengths=lens, out=yn.numpy())
@@ -300,7 +308,7 @@ def make_modules(fr, fk):
 
     # ---- Sine position embedding (position_embedding.py:8-49)
     pe = PositionEmbeddingCoordsSine(3, 256, scale=1.0)
-    xyz = torch.from_numpy(pts[:100])
+    xyz = torch.from_numpy(pts[:32])
     pe512 = PositionEmbeddingCoordsSine(3, 512, scale=1.0)
     pe64 = PositionEmbeddingCoordsSine(3, 64, scale=1.0)
     save('pos_embed', xyz=xyz.numpy(), pe256=pe(xyz).numpy(), pe512=pe512(xyz).numpy(),
@@ -350,7 +358,12 @@ def make_modules(fr, fk):
 # --------------------------------------------------------------------------------------
 # End-to-end forward fixtures
 # --------------------------------------------------------------------------------------
-SMALL_MODELNET = dict(first_feats_dim=32, d_embed=32, d_feedforward=64)
+# 3 encoder layers instead of 6 (the losses on the last one, as the configs' [5]): a third of
+# the stored per-layer features, the same layer structure
+SMALL_LAYERS = dict(num_encoder_layers=3, overlap_loss_on=[2], feature_loss_on=[2], corr_loss_on=[2])
+SMALL_MODELNET = dict(first_feats_dim=32, d_embed=32, d_feedforward=64, **SMALL_LAYERS)
+sys.path.insert(0, HERE)
+from named_weights import named_state_dict  # noqa: E402
 
 
 def run_forward(fr, fk, cfg, clouds_src, clouds_tgt, bias=4.0, seed=0):
@@ -363,18 +376,18 @@ def run_forward(fr, fk, cfg, clouds_src, clouds_tgt, bias=4.0, seed=0):
     finally:
         os.chdir(cwd)
     model.preprocessor = fk.Preprocessor(cfg)  # the reference's own CPU preprocessor
-    with torch.no_grad():
-        model.correspondence_decoder.conf_logits_decoder.bias.fill_(bias)
-        # Non-trivial normalisation statistics, so that BatchNorm folding and LayerNorm
-        # affine terms are exercised (a fresh init has mean 0 / var 1 / weight 1 / bias 0).
-        g = torch.Generator().manual_seed(seed + 123)
-        for m in model.modules():
-            if isinstance(m, torch.nn.BatchNorm1d):
-                m.running_mean.copy_(0.1 * torch.randn(m.running_mean.shape, generator=g))
-                m.running_var.copy_(0.75 + 0.5 * torch.rand(m.running_var.shape, generator=g))
-            if isinstance(m, (torch.nn.BatchNorm1d, torch.nn.LayerNorm)):
-                m.weight.copy_(1 + 0.1 * torch.randn(m.weight.shape, generator=g))
-                m.bias.copy_(0.1 * torch.randn(m.bias.shape, generator=g))
+    # weights from (key, shape, seed) only (named_weights.py), so the fixture need not store
+    # them: non-trivial normalisation statistics and affine terms (BatchNorm folding and the
+    # LayerNorm affine are exercised), the logits bias `bias`; the kernel points keep the
+    # reference's own random rotation and are stored
+    sd = model.state_dict()
+    keys_shapes = [(k, tuple(v.shape)) for k, v in sd.items() if not k.startswith('feature_criterion')]
+    stored = {k: v.numpy() for k, v in sd.items() if 'kernel_points' in k}
+    vals = named_state_dict(keys_shapes, seed, bias, stored)
+    missing, unexpected = model.load_state_dict({k: torch.from_numpy(v) for k, v in vals.items()},
+                                                strict=False)
+    assert not unexpected and all(k.startswith('feature_criterion') for k in missing), missing
+    model.sd_keys_shapes, model.sd_seed = keys_shapes, seed
     model.eval()
     batch = {'src_xyz': [torch.from_numpy(c) for c in clouds_src],
              'tgt_xyz': [torch.from_numpy(c) for c in clouds_tgt]}
@@ -393,16 +406,21 @@ def pack_forward(model, meta, out, cfg_over, clouds_src, clouds_tgt, bias):
     for key in ('points', 'neighbors', 'pools', 'upsamples', 'stack_lengths'):
         for l, t in enumerate(meta[key]):
             a = t.numpy()
-            arrays[f'meta.{key}.{l}'] = a.astype(np.int32) if a.dtype == np.int64 else a
+            if a.dtype == np.int64:      # index tables: int16 where they fit (loaders widen)
+                a = a.astype(np.int16 if a.size and a.max() < 32767 and a.min() >= 0 else np.int32)
+            arrays[f'meta.{key}.{l}'] = a
     for k in ('src_feat_un', 'tgt_feat_un', 'src_feat', 'tgt_feat', 'src_kp', 'src_kp_warped',
               'tgt_kp', 'tgt_kp_warped', 'src_overlap', 'tgt_overlap'):
         for b, t in enumerate(out[k]):
             arrays[f'out.{k}.{b}'] = t.numpy()
     arrays['out.pose'] = out['pose'].numpy()
+    # the state_dict is rebuilt by the tests from (key, shape, seed): named_weights.py; only
+    # the reference's own random kernel points are stored
+    arrays['sd_keys'] = np.bytes_(repr([(k, list(sh)) for k, sh in model.sd_keys_shapes]))
+    arrays['sd_seed'] = np.int64(model.sd_seed)
     for k, v in model.state_dict().items():
-        if k.startswith('feature_criterion'):
-            continue  # loss-only parameters
-        arrays[f'sd.{k}'] = v.numpy()
+        if 'kernel_points' in k:
+            arrays[f'sd.{k}'] = v.numpy()
     arrays['cfg_overrides'] = np.array(repr(cfg_over))
     arrays['bias'] = np.float64(bias)
     return arrays
@@ -418,7 +436,7 @@ def make_forward(fr, fk):
     save('forward_modelnet_small', **pack_forward(model, meta, out, SMALL_MODELNET, src, tgt, 4.0))
 
     # (2) reduced-width 3DMatch config (4 levels, limits 40, d_embed 64)
-    over = dict(first_feats_dim=16, d_embed=32, d_feedforward=64)
+    over = dict(first_feats_dim=16, d_embed=32, d_feedforward=64, **SMALL_LAYERS)
     cfg = load_cfg('3dmatch.yaml', **over)
     s, t, _ = indoor_like_pair(1, n_points=1500)
     model, meta, out = run_forward(fr, fk, cfg, [s], [t])
@@ -497,8 +515,8 @@ TRAIN_FULL_GRADS = (
     'feat_proj.weight',
     'transformer_encoder.layers.0.self_attn.in_proj_weight',
     'transformer_encoder.layers.2.multihead_attn.in_proj_bias',
-    'transformer_encoder.layers.5.norm2.weight',
-    'transformer_encoder.layers.5.linear1.weight',
+    'transformer_encoder.layers.2.norm2.weight',
+    'transformer_encoder.layers.2.linear1.weight',
     'transformer_encoder.norm.bias',
     'correspondence_decoder.coor_mlp.0.weight',
     'correspondence_decoder.conf_logits_decoder.weight',
@@ -533,8 +551,8 @@ def make_train(fr, fk):
         losses['total'].backward()
     ref = np.load(os.path.join(HERE, 'forward_modelnet_small.npz'))
     for l in range(len(meta['neighbors'])):     # same neighbour tables as the forward fixture
-        assert np.array_equal(batch['kpconv_meta']['neighbors'][l].numpy().astype(np.int32),
-                              ref[f'meta.neighbors.{l}'])
+        assert np.array_equal(batch['kpconv_meta']['neighbors'][l].numpy(),
+                              ref[f'meta.neighbors.{l}'].astype(np.int64))
     arrays = {}
     for k, v in losses.items():
         arrays[f'loss.{k}'] = np.float32(v.item())

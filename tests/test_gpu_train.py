@@ -73,15 +73,15 @@ def test_linear_backward(gpu, m, n, k, act):
 
 def _kpconv_case(cin):
     gk = np.load(__import__('conftest').GOLDEN + '/kpconv_block.npz')
-    q = torch.from_numpy(gk['q'])
+    q, s = torch.from_numpy(gk['q']), torch.from_numpy(gk['s'])
     idx = torch.from_numpy(gk['idx'].astype(np.int64))
     kp = torch.from_numpy(gk['kp'])
     extent = float(gk['extent'])
     g = torch.Generator().manual_seed(cin)
-    x = torch.randn(q.shape[0], cin, generator=g)
+    x = torch.randn(s.shape[0], cin, generator=g)    # features of the support rows
     x[::5] = -x[::5].abs()                       # rows that do not count in the normaliser
     W = torch.randn(15, cin, 24, generator=g) / math.sqrt(15 * cin)
-    return q, idx, kp, extent, x, W, gk
+    return q, s, idx, kp, extent, x, W, gk
 
 
 @pytest.mark.parametrize('cin', [1, 16, 32, 64, 128, 256])
@@ -90,8 +90,7 @@ def test_kpconv_backward(gpu, cin, strided):
     """kpconv_t (gather + weight GEMM, normalised by the returned nnorm) vs the oracle's KPConv
     (finegrained_kpconv_blocks.py:265-401 restated) in fp64: dx (fgr_kpconv_scatter) and dW."""
     from fgreg.autograd import kpconv_t
-    q, idx, kp, extent, x0, W0, gk = _kpconv_case(cin)
-    s = q
+    q, s, idx, kp, extent, x0, W0, gk = _kpconv_case(cin)
     if strided:
         q = torch.from_numpy(gk['sub'])
         idx = torch.from_numpy(gk['pools'].astype(np.int64))
@@ -117,7 +116,7 @@ def test_max_pool_backward(gpu):
     from fgreg.autograd import max_pool_t
     gk = np.load(__import__('conftest').GOLDEN + '/kpconv_block.npz')
     idx = torch.from_numpy(gk['pools'].astype(np.int64))
-    x0 = torch.randn(gk['q'].shape[0], 48, generator=torch.Generator().manual_seed(1))
+    x0 = torch.randn(gk['s'].shape[0], 48, generator=torch.Generator().manual_seed(1))
     x0[:, :8] = -x0[:, :8].abs()                 # channels where the shadow zero wins
     x, x64 = _leaf(x0, gpu)
     y = max_pool_t(x, idx.to(gpu))
