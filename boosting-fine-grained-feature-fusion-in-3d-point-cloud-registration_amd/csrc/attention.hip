@@ -479,6 +479,118 @@ corr_attention_kernel(const float* __restrict__ q, int64_t ld_q, const float* __
     }
 }
 
+// ---- num_neighbors > 0 (finegrained_regtr.py:353-357) ------------------------------------
+// The reference builds neighbor_mask (L, B, Q, S) = -inf and then runs
+//   neighbor_mask[:, :, topk(attn, k).indices] = 0,
+// which indexes the QUERY dimension with the top-k KEY indices of every (layer, pair, query)
+// row: query row j of every layer and pair keeps its plain softmax iff j is among the union of
+// all top-k key indices of that direction, every other query row is all -inf and its softmax
+// (hence its correspondence) is NaN. Restated here as: scores (the same q.k * scale as
+// corr_attention_kernel) -> per-row top-k by successive maxima -> a byte flag per index of
+// the direction's union -> NaN rows. Ties rank the lower key index first.
+
+// scores[row * ld_s + (j - kb)] for every key j of the row's key segment.
+template <int D>
+__global__ void __launch_bounds__(256)
+corr_scores_kernel(const float* __restrict__ q, int64_t ld_q, const float* __restrict__ k,
+                   int64_t ld_k, const int64_t* __restrict__ q_off,
+                   const int64_t* __restrict__ kv_off, const int32_t* __restrict__ kv_seg,
+                   float scale, float* __restrict__ scores, int64_t ld_s) {
+    constexpr int DL = D / 8;
+    __shared__ float kt[kCaK][D + 4];
+    const int seg = blockIdx.y;
+    const int64_t qb = q_off[seg], qe = q_off[seg + 1];
+    const int64_t q0 = qb + (int64_t)blockIdx.x * kCaQ;
+    if (q0 >= qe) return;
+    const int ks = kv_seg[seg];
+    const int64_t kb = kv_off[ks], ke = kv_off[ks + 1];
+    const int tid = threadIdx.x, qi = tid >> 3, sl = tid & 7;
+    const int64_t row = q0 + qi;
+    const bool active = row < qe;
+    float qv[DL];
+#pragma unroll
+    for (int e = 0; e < DL; ++e) qv[e] = active ? q[row * ld_q + sl * DL + e] * scale : 0.f;
+    for (int64_t j0 = kb; j0 < ke; j0 += kCaK) {
+        const int nk = (int)min((int64_t)kCaK, ke - j0);
+        __syncthreads();
+        for (int e = tid; e < kCaK * D; e += 256) {
+            const int r = e / D, cc = e - r * D;
+            kt[r][cc] = r < nk ? k[(j0 + r) * ld_k + cc] : 0.f;
+        }
+        __syncthreads();
+        for (int r = 0; r < nk; ++r) {
+            float s = 0.f;
+#pragma unroll
+            for (int e = 0; e < DL; ++e) s = fmaf(qv[e], kt[r][sl * DL + e], s);
+            s += dpp<0xB1>(s);
+            s += dpp<0x4E>(s);
+            s += dpp<0x141>(s);
+            if (active && sl == 0) scores[row * ld_s + (j0 - kb) + r] = s;
+        }
+    }
+}
+
+// (value, index) ordered by value descending, then index ascending: a ranks before b.
+__device__ __forceinline__ bool rank_before(float va, int ia, float vb, int ib) {
+    return va > vb || (va == vb && ia < ib);
+}
+
+// One wave per query row: n_top rounds, each taking the best-ranked key strictly after the
+// previous round's winner (no writes to the scores), flagging its index in the direction's
+// union (flags[dir * ld_f + j] = 1; concurrent writers store the same byte).
+__global__ void __launch_bounds__(256)
+corr_topk_flags_kernel(const float* __restrict__ scores, int64_t ld_s,
+                       const int64_t* __restrict__ q_off, const int64_t* __restrict__ kv_off,
+                       const int32_t* __restrict__ kv_seg, int32_t n_clouds, int32_t n_top,
+                       uint8_t* __restrict__ flags, int64_t ld_f) {
+    const int seg = blockIdx.y;
+    const int64_t row = q_off[seg] + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= q_off[seg + 1]) return;                     // wave-uniform
+    const int lane = threadIdx.x & 63;
+    const int ks = kv_seg[seg];
+    const int nk = (int)(kv_off[ks + 1] - kv_off[ks]);
+    const int dir = (seg % n_clouds) >= n_clouds / 2;
+    const float* sr = scores + row * ld_s;
+    float pv = INFINITY;
+    int pi = -1;                                           // previous winner: ranks before all
+    for (int t = 0; t < n_top; ++t) {
+        float bv = -INFINITY;
+        int bi = 0x7fffffff;
+        for (int j = lane; j < nk; j += 64) {
+            const float v = sr[j];
+            if (rank_before(pv, pi, v, j) && rank_before(v, j, bv, bi)) { bv = v; bi = j; }
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            const float ov = __shfl_xor(bv, o);
+            const int oi = __shfl_xor(bi, o);
+            if (rank_before(ov, oi, bv, bi)) { bv = ov; bi = oi; }
+        }
+        if (bi == 0x7fffffff) break;                       // fewer than n_top keys (rejected on the host)
+        if (lane == 0) flags[dir * ld_f + bi] = 1;
+        pv = bv;
+        pi = bi;
+    }
+}
+
+// corr rows whose in-cloud index is not in their direction's union become NaN (the softmax of
+// an all -inf row).
+__global__ void __launch_bounds__(256)
+corr_nan_rows_kernel(float* __restrict__ out, const int64_t* __restrict__ q_off,
+                     int32_t n_clouds, const uint8_t* __restrict__ flags, int64_t ld_f) {
+    const int seg = blockIdx.y;
+    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t row = q_off[seg] + j;
+    if (row >= q_off[seg + 1]) return;
+    const int dir = (seg % n_clouds) >= n_clouds / 2;
+    if (j >= ld_f || !flags[dir * ld_f + j]) {             // an index >= S is never in the union
+        const float nan = __builtin_nanf("");
+        out[row * 3 + 0] = nan;
+        out[row * 3 + 1] = nan;
+        out[row * 3 + 2] = nan;
+    }
+}
+
 }  // namespace
 }  // namespace fgr
 
@@ -510,5 +622,56 @@ extern "C" int fgr_corr_attention(const float* q, int64_t ld_q, const float* k, 
     }
 #undef FGR_CA
     FGR_CHECK_LAUNCH("corr_attention_kernel");
+    return FGR_OK;
+}
+
+extern "C" int fgr_corr_topk_workspace(int64_t n_rows, int32_t max_kv_len, size_t* bytes) {
+    FGR_REQUIRE(bytes && n_rows >= 0 && max_kv_len >= 0, "fgr_corr_topk_workspace: bad arguments");
+    *bytes = (size_t)n_rows * (size_t)max_kv_len * sizeof(float);
+    return FGR_OK;
+}
+
+extern "C" int fgr_corr_topk_mask(const float* q, int64_t ld_q, const float* k, int64_t ld_k,
+                                  float* out, const int64_t* q_off, const int64_t* kv_off,
+                                  const int32_t* kv_seg, int32_t n_seg, int32_t n_clouds,
+                                  int64_t n_rows, int32_t max_q_len, int32_t max_kv_len, int32_t d,
+                                  float scale, int32_t n_top, uint8_t* flags, void* ws,
+                                  size_t ws_bytes, void* stream) {
+    FGR_REQUIRE(q && k && out && q_off && kv_off && kv_seg && flags && n_seg > 0 && n_rows >= 0 &&
+                    n_clouds > 0 && n_clouds % 2 == 0 && max_q_len >= 0 && max_kv_len >= 0 &&
+                    n_top > 0 && ld_q >= d && ld_k >= d,
+                "fgr_corr_topk_mask: bad arguments");
+    FGR_REQUIRE(d == 32 || d == 64 || d == 128 || d == 256 || d == 512,
+                "fgr_corr_topk_mask: d %d unsupported (32, 64, 128, 256, 512)", d);
+    size_t need = 0;
+    fgr_corr_topk_workspace(n_rows, max_kv_len, &need);
+    FGR_REQUIRE(ws && ws_bytes >= need, "fgr_corr_topk_mask: workspace %zu < %zu bytes", ws_bytes, need);
+    hipStream_t st = as_stream(stream);
+    FGR_REQUIRE(hipMemsetAsync(flags, 0, 2 * (size_t)max_kv_len, st) == hipSuccess,
+                "fgr_corr_topk_mask: memset failed");
+    if (max_q_len == 0 || max_kv_len == 0) return FGR_OK;
+    float* scores = (float*)ws;
+    const dim3 grid((unsigned)ceil_div(max_q_len, kCaQ), (unsigned)n_seg);
+#define FGR_CS(DD)                                                                                \
+    case DD:                                                                                      \
+        hipLaunchKernelGGL(corr_scores_kernel<DD>, grid, dim3(256), 0, st, q, ld_q, k, ld_k,      \
+                           q_off, kv_off, kv_seg, scale, scores, (int64_t)max_kv_len);            \
+        break;
+    switch (d) {
+        FGR_CS(32)
+        FGR_CS(64)
+        FGR_CS(128)
+        FGR_CS(256)
+        FGR_CS(512)
+    }
+#undef FGR_CS
+    FGR_CHECK_LAUNCH("corr_scores_kernel");
+    hipLaunchKernelGGL(corr_topk_flags_kernel, dim3((unsigned)ceil_div(max_q_len, 4), (unsigned)n_seg),
+                       dim3(256), 0, st, scores, (int64_t)max_kv_len, q_off, kv_off, kv_seg, n_clouds,
+                       n_top, flags, (int64_t)max_kv_len);
+    FGR_CHECK_LAUNCH("corr_topk_flags_kernel");
+    hipLaunchKernelGGL(corr_nan_rows_kernel, dim3((unsigned)ceil_div(max_q_len, 256), (unsigned)n_seg),
+                       dim3(256), 0, st, out, q_off, n_clouds, flags, (int64_t)max_kv_len);
+    FGR_CHECK_LAUNCH("corr_nan_rows_kernel");
     return FGR_OK;
 }

@@ -532,10 +532,55 @@ sine_pe_kernel(const float* __restrict__ xyz, int64_t n, int d, int npf, float t
     }
 }
 
+// out = a + b elementwise (the post-norm layer's `with_pos_embed`, transformers.py:121-124):
+// 16-B accesses, four per thread in flight.
+__global__ void __launch_bounds__(256)
+add4_kernel(const float4* __restrict__ a, const float4* __restrict__ b, int64_t n4,
+            float4* __restrict__ out) {
+    const int64_t i0 = ((int64_t)blockIdx.x * 256 * 4) + threadIdx.x;
+    float4 va[4], vb[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int64_t i = i0 + 256 * u;
+        if (i < n4) { va[u] = a[i]; vb[u] = b[i]; }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int64_t i = i0 + 256 * u;
+        if (i < n4)
+            out[i] = make_float4(va[u].x + vb[u].x, va[u].y + vb[u].y, va[u].z + vb[u].z,
+                                 va[u].w + vb[u].w);
+    }
+}
+
+__global__ void __launch_bounds__(256)
+add1_kernel(const float* __restrict__ a, const float* __restrict__ b, int64_t n,
+            float* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) out[i] = a[i] + b[i];
+}
+
 }  // namespace
 }  // namespace fgr
 
 using namespace fgr;
+
+extern "C" int fgr_add(const float* a, const float* b, int64_t n, float* out, void* stream) {
+    FGR_REQUIRE(n >= 0, "fgr_add: bad arguments");
+    FGR_REQUIRE(n == 0 || (a && b && out), "fgr_add: null pointer");
+    if (n == 0) return FGR_OK;
+    hipStream_t st = as_stream(stream);
+    const bool vec = n % 4 == 0 && ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b) |
+                                     reinterpret_cast<uintptr_t>(out)) & 15) == 0;
+    if (vec)
+        hipLaunchKernelGGL(add4_kernel, dim3((unsigned)ceil_div(n / 4, 1024)), dim3(256), 0, st,
+                           reinterpret_cast<const float4*>(a), reinterpret_cast<const float4*>(b),
+                           n / 4, reinterpret_cast<float4*>(out));
+    else
+        hipLaunchKernelGGL(add1_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, st, a, b, n, out);
+    FGR_CHECK_LAUNCH("add_kernel");
+    return FGR_OK;
+}
 
 extern "C" int fgr_instnorm_workspace(int64_t max_seg_len, int32_t c, int32_t n_seg,
                                       size_t* bytes) {

@@ -38,6 +38,7 @@ SIGNATURES = {
                      _vp],
     'fgr_layernorm': [_vp, _i64, _i32, _vp, _vp, _f32, _vp, _vp, _vp, _vp],
     'fgr_sine_pos_embed': [_vp, _i64, _i32, _f32, _f32, _vp, _vp],
+    'fgr_add': [_vp, _vp, _i64, _vp, _vp],
     'fgr_attention': [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i32, _i32, _i32,
                       _i32, _f32, _vp],
     'fgr_attention_f16x3_workspace': [_i64, _i32, _i32, ctypes.POINTER(_sz)],
@@ -70,6 +71,9 @@ SIGNATURES = {
     'fgr_se3_compare': [_vp, _vp, _i32, _i32, _vp, _vp, _vp],
     'fgr_corr_attention': [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32,
                            _f32, _vp],
+    'fgr_corr_topk_workspace': [_i64, _i32, ctypes.POINTER(_sz)],
+    'fgr_corr_topk_mask': [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _i32, _i32, _i64, _i32, _i32,
+                           _i32, _f32, _i32, _vp, _vp, _sz, _vp],
     'fgr_procrustes': [_vp, _vp, _vp, _i64, _i64, _f32, _vp, _vp],
     'fgr_time_next_call': [_vp, _vp],
     'fgr_pair_pose': [_vp, _vp, _vp, _i64, _vp, _i32, _i32, _f32, _vp, _vp],

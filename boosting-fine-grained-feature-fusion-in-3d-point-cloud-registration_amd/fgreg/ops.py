@@ -406,6 +406,18 @@ def layernorm(x, weight, bias, eps=1e-5, add=None, pre_bias=None, out=None) -> t
     return out
 
 
+def add(a, b, out=None) -> torch.Tensor:
+    """a + b (same shape, fp32) on fgr_add: the post-norm layer's with_pos_embed."""
+    _dev(a, b)
+    a, b = _c(a, torch.float32), _c(b, torch.float32)
+    assert a.shape == b.shape
+    if out is None:
+        out = torch.empty_like(a)
+    assert out.is_contiguous() and out.shape == a.shape
+    _lib.check(_lib.load().fgr_add(_ptr(a), _ptr(b), a.numel(), _ptr(out), _stream()), 'fgr_add')
+    return out
+
+
 def sine_pos_embed(xyz, d_model, temperature=10000.0, scale=1.0) -> torch.Tensor:
     _dev(xyz)
     xyz = _c(xyz, torch.float32)
@@ -643,6 +655,29 @@ def corr_attention(q, k, xyz, q_off, kv_off, kv_seg, v_off, max_q_len, scale) ->
         float(scale), _stream()), 'fgr_corr_attention')
     _end('attention', t0, lambda: attention_flops(q_off, kv_off, kv_seg, d) // 2)
     return out
+
+
+def corr_topk_mask(corr, q, k, q_off, kv_off, kv_seg, n_clouds, max_q_len, max_kv_len, scale,
+                   n_top) -> torch.Tensor:
+    """num_neighbors > 0 of CorrespondenceDecoder.simple_attention (finegrained_regtr.py:
+    353-357) on fgr_corr_topk_mask: rows of ``corr`` (the fgr_corr_attention output, same
+    segments) outside their direction's top-k index union become NaN, in place. Returns the
+    (2, max_kv_len) uint8 union flags (src direction first)."""
+    _dev(corr, q, k, q_off, kv_off, kv_seg)
+    for t in (q, k):
+        assert t.dtype == torch.float32 and t.dim() == 2 and t.stride(1) == 1
+    assert corr.dtype == torch.float32 and corr.is_contiguous() and corr.shape == (q.shape[0], 3)
+    d = q.shape[1]
+    flags = torch.empty((2, max_kv_len), dtype=torch.uint8, device=q.device)
+    L = _lib.load()
+    nb = _lib._sz(0)
+    _lib.check(L.fgr_corr_topk_workspace(q.shape[0], max_kv_len, nb), 'fgr_corr_topk_workspace')
+    ws = torch.empty(max(nb.value, 1), dtype=torch.uint8, device=q.device)
+    _lib.check(L.fgr_corr_topk_mask(
+        _ptr(q), q.stride(0), _ptr(k), k.stride(0), _ptr(corr), _ptr(q_off), _ptr(kv_off),
+        _ptr(kv_seg), q_off.numel() - 1, n_clouds, q.shape[0], int(max_q_len), int(max_kv_len), d,
+        float(scale), int(n_top), _ptr(flags), _ptr(ws), nb.value, _stream()), 'fgr_corr_topk_mask')
+    return flags
 
 
 # ------------------------------------------------------------------------------------------

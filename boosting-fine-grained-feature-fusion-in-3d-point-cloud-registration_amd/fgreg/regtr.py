@@ -63,12 +63,18 @@ class CorrespondenceDecoder(nn.Module):
     whose values are the other cloud's coordinates. Parameter layout of the reference. The
     q / k projections run once over all L layers' rows (f16x3 GEMMs) and the attention of
     every (layer, cloud) segment is ONE fgr_corr_attention launch (values = the partner's 3
-    coordinates, no padding to width d)."""
+    coordinates, no padding to width d).
+
+    num_neighbors > 0 reproduces the reference's masking as it executes (:353-357, see
+    fgr_corr_topk_mask in include/fgreg.h): a query row keeps its plain softmax iff its index
+    is in the union of all top-k key indices of its direction, else it is NaN; an index >= the
+    padded query length raises IndexError like the reference's indexing. Exact for batches
+    without padding (every src cloud of one length, every tgt cloud of one length, e.g. B = 1);
+    padded batches raise NotImplementedError (the reference's padded query rows -- transformer
+    outputs at padded positions -- feed its union and do not exist in the packed layout)."""
 
     def __init__(self, d_embed, use_pos_emb, pos_embed=None, num_neighbors=0):
         super().__init__()
-        if num_neighbors > 0:
-            raise NotImplementedError('top-k neighbour masking is not in the reference configs')
         self.use_pos_emb = use_pos_emb
         self.pos_embed = pos_embed
         self.q_norm = nn.LayerNorm(d_embed)   # present in the reference, unused by its forward
@@ -85,9 +91,30 @@ class CorrespondenceDecoder(nn.Module):
         q_off, kv_seg, v_off = seg.layer_tables
         corr = ops.corr_attention(q, k, xyz, q_off, q_off, kv_seg, v_off, seg.max_len,
                                   1.0 / math.sqrt(d))        # q_proj(query) / sqrt(D) (:344)
+        if self.num_neighbors > 0:
+            self._topk_mask(corr, q, k, seg, d)
         logits = linear(feats.reshape(L * N, d), self.conf_logits_decoder.weight,
                         self.conf_logits_decoder.bias)
         return corr.view(L, N, 3), logits.view(L, N, 1)
+
+
+    def _topk_mask(self, corr, q, k, seg: Segments, d):
+        B = seg.B
+        src_l, tgt_l = seg.lengths[:B], seg.lengths[B:]
+        if len(set(src_l)) > 1 or len(set(tgt_l)) > 1:
+            raise NotImplementedError('num_neighbors > 0 with padded batches (clouds of unequal '
+                                      'length in one direction)')
+        n_src, n_tgt = src_l[0], tgt_l[0]
+        if self.num_neighbors > min(n_src, n_tgt):
+            raise RuntimeError('selected index k out of range')              # torch.topk
+        q_off, kv_seg, _ = seg.layer_tables
+        flags = ops.corr_topk_mask(corr, q, k, q_off, q_off, kv_seg, 2 * B, seg.max_len,
+                                   max(n_src, n_tgt), 1.0 / math.sqrt(d), self.num_neighbors)
+        # src queries pick tgt key indices that index the src query dim, and vice versa
+        for dir_, n_q, n_k in ((0, n_src, n_tgt), (1, n_tgt, n_src)):
+            if n_k > n_q and bool(flags[dir_, n_q:n_k].any()):
+                hi = int(flags[dir_, :n_k].nonzero().max())
+                raise IndexError(f'index {hi} is out of bounds for dimension 2 with size {n_q}')
 
 
 class _LossParams(nn.Module):
@@ -315,6 +342,9 @@ def _graph_for(model, meta, slens_c, B):
     while len(seen) > SEEN_CACHE:
         seen.popitem(last=False)
     if n <= 0:
+        return None
+    dec = model.correspondence_decoder
+    if getattr(dec, 'num_neighbors', 0) > 0:           # the top-k mask reads flags back: eager
         return None
     try:
         g = _CoreGraph(model, meta, slens_c, B)

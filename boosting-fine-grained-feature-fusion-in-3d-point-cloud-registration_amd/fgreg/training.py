@@ -69,7 +69,10 @@ def block_train(block, x, meta):
 
 
 def layer_train(layer, x, pos, seg):
-    """TransformerCrossEncoderLayer.forward_pre (transformers.py:183-244), both clouds packed."""
+    """TransformerCrossEncoderLayer.forward_pre (transformers.py:183-244), both clouds packed;
+    forward_post (:109-181) for pre_norm: False."""
+    if not layer.normalize_before:
+        return _layer_post_train(layer, x, pos, seg)
     for norm, mha, kv_seg in ((layer.norm1, layer.self_attn, seg.self_seg),
                               (layer.norm2, layer.multihead_attn, seg.cross_seg)):
         h = layernorm_t(x, norm, add=pos)
@@ -78,6 +81,16 @@ def layer_train(layer, x, pos, seg):
         x = linear_t(o, mha.out_proj.weight, mha.out_proj.bias, residual=x)
     h = linear_t(layernorm_t(x, layer.norm3), layer.linear1.weight, layer.linear1.bias, act=ACT_RELU)
     return linear_t(h, layer.linear2.weight, layer.linear2.bias, residual=x)
+
+
+def _layer_post_train(layer, x, pos, seg):
+    for norm, mha, kv_seg in ((layer.norm1, layer.self_attn, seg.self_seg),
+                              (layer.norm2, layer.multihead_attn, seg.cross_seg)):
+        qkv = linear_t(x if pos is None else x + pos, mha.in_proj_weight, mha.in_proj_bias)
+        o = attention_t(qkv, seg.off, kv_seg, seg.max_len, layer.nhead)
+        x = layernorm_t(linear_t(o, mha.out_proj.weight, mha.out_proj.bias, residual=x), norm)
+    h = linear_t(x, layer.linear1.weight, layer.linear1.bias, act=ACT_RELU)
+    return layernorm_t(linear_t(h, layer.linear2.weight, layer.linear2.bias, residual=x), layer.norm3)
 
 
 def core_train(model, meta, seg, B):

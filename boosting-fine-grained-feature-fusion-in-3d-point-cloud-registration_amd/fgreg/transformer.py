@@ -60,7 +60,8 @@ class Segments:
 
 
 class TransformerCrossEncoderLayer(nn.Module):
-    """transformers.py:84-258 (pre-norm forward_pre; dropout must be 0 at inference)."""
+    """transformers.py:84-258: forward_pre (pre_norm: True, the shipped configs) and
+    forward_post (pre_norm: False); dropout must be 0 at inference."""
 
     def __init__(self, d_model, nhead, dim_feedforward=2048, dropout=0.1, activation='relu',
                  normalize_before=False, sa_val_has_pos_emb=False, ca_val_has_pos_emb=False,
@@ -70,8 +71,6 @@ class TransformerCrossEncoderLayer(nn.Module):
             raise NotImplementedError(attention_type)
         if activation != 'relu':
             raise NotImplementedError('transformer_act other than relu is not in the configs')
-        if not normalize_before:
-            raise NotImplementedError('post-norm (pre_norm: False) is not in the reference configs')
         self.self_attn = nn.MultiheadAttention(d_model, nhead, dropout=dropout)
         self.multihead_attn = nn.MultiheadAttention(d_model, nhead, dropout=dropout)
         self.linear1 = nn.Linear(d_model, dim_feedforward)
@@ -104,6 +103,8 @@ class TransformerCrossEncoderLayer(nn.Module):
         LayerNorm only reads x (no in-place bias pass writing x back); ``pending_bias`` (a
         bias still to be added to x by the first LayerNorm) is accepted for callers that
         defer one, and the returned pending bias is None."""
+        if not self.normalize_before:
+            return self._forward_post(x, pos, seg, pending_bias), None
         # self-attention, shared weights for src and tgt (:193-210)
         h = ops.layernorm(x, self.norm1.weight, self.norm1.bias, self.norm1.eps, add=pos,
                           pre_bias=pending_bias)
@@ -122,6 +123,26 @@ class TransformerCrossEncoderLayer(nn.Module):
         h = ops.layernorm(x, self.norm3.weight, self.norm3.bias, self.norm3.eps)
         h = linear(h, self.linear1.weight, self.linear1.bias, act=ops.ACT_RELU)
         return linear(h, self.linear2.weight, self.linear2.bias, residual=x), None
+
+    def _forward_post(self, x, pos, seg: Segments, pending_bias=None):
+        """forward_post (transformers.py:109-181): each sub-block's residual sum is formed in
+        its output GEMM's epilogue, then LayerNorm'd; the norm1 output is also written with the
+        positional embedding added (the cross-attention's q / k input, :139-147). Both
+        directions of each attention run in one launch, reading the same pre-update rows
+        like the reference's simultaneous src / tgt update."""
+        assert pending_bias is None          # only the pre-norm path defers a bias
+        h = ops.add(x, pos)                                       # with_pos_embed (:121-124)
+        o = self._attend(self.self_attn, h, x, self.sa_val_has_pos_emb, seg, seg.self_seg)
+        t = linear(o, self.self_attn.out_proj.weight, self.self_attn.out_proj.bias, residual=x)
+        x = ops.layernorm(t, self.norm1.weight, self.norm1.bias, self.norm1.eps)       # :127
+        h = ops.layernorm(t, self.norm1.weight, self.norm1.bias, self.norm1.eps, add=pos)
+        o = self._attend(self.multihead_attn, h, x, self.ca_val_has_pos_emb, seg, seg.cross_seg)
+        t = linear(o, self.multihead_attn.out_proj.weight, self.multihead_attn.out_proj.bias,
+                   residual=x)
+        x = ops.layernorm(t, self.norm2.weight, self.norm2.bias, self.norm2.eps)       # :163
+        h = linear(x, self.linear1.weight, self.linear1.bias, act=ops.ACT_RELU)        # :167-169
+        t = linear(h, self.linear2.weight, self.linear2.bias, residual=x)
+        return ops.layernorm(t, self.norm3.weight, self.norm3.bias, self.norm3.eps)
 
 
 class TransformerCrossEncoder(nn.Module):

@@ -158,6 +158,10 @@ int fgr_instnorm(const float* x, int64_t n, int32_t c, const int64_t* seg_off, i
 int fgr_layernorm(float* x, int64_t n, int32_t d, const float* gamma, const float* beta,
                   float eps, const float* add, const float* pre_bias, float* out, void* stream);
 
+/* out = a + b over n floats: the post-norm layer's with_pos_embed (transformers.py:121-124,
+ * pre_norm: False; the pre-norm path fuses this add into fgr_layernorm). */
+int fgr_add(const float* a, const float* b, int64_t n, float* out, void* stream);
+
 /* PositionEmbeddingCoordsSine (position_embedding.py:29-49) for 3-D input. */
 int fgr_sine_pos_embed(const float* xyz, int64_t n, int32_t d_model, float temperature,
                        float scale, float* out, void* stream);
@@ -291,6 +295,22 @@ int fgr_corr_attention(const float* q, int64_t ld_q, const float* k, int64_t ld_
                        const float* xyz, float* out, const int64_t* q_off, const int64_t* kv_off,
                        const int32_t* kv_seg, const int64_t* v_off, int32_t n_seg,
                        int32_t max_q_len, int32_t d, float scale, void* stream);
+
+/* CorrespondenceDecoder with num_neighbors > 0 (finegrained_regtr.py:353-357), applied to the
+ * output of fgr_corr_attention (same q, k, segments and scale). The reference's
+ * `neighbor_mask[:, :, topk(attn, k).indices] = 0` indexes the QUERY dimension with top-k KEY
+ * indices, so a query row j keeps its unmasked softmax iff j is in the union U_dir of the
+ * top-k key indices of every (layer, pair, query) row of its direction (src->tgt, tgt->src);
+ * every other row is NaN (softmax of an all -inf row). Segments i with (i % n_clouds) <
+ * n_clouds / 2 are the src direction. flags (2 * max_kv_len bytes, device) receive U as
+ * bytes, direction-major, for the caller's index-range check (an index >= Q raises in the
+ * reference). Ties rank the lower key index first. Workspace: fgr_corr_topk_workspace. */
+int fgr_corr_topk_workspace(int64_t n_rows, int32_t max_kv_len, size_t* bytes);
+int fgr_corr_topk_mask(const float* q, int64_t ld_q, const float* k, int64_t ld_k, float* out,
+                       const int64_t* q_off, const int64_t* kv_off, const int32_t* kv_seg,
+                       int32_t n_seg, int32_t n_clouds, int64_t n_rows, int32_t max_q_len,
+                       int32_t max_kv_len, int32_t d, float scale, int32_t n_top, uint8_t* flags,
+                       void* ws, size_t ws_bytes, void* stream);
 
 /* Batched device-to-device copies: n (src[i] -> dst[i], bytes[i]) triples (host arrays of device
  * pointers) in one launch per 32 copies; 16-B accesses where both ends are 16-B aligned. Not a

@@ -266,8 +266,23 @@ def _ln(sd, p, x):
     return F.layer_norm(x, x.shape[-1:], sd[p + '.weight'], sd[p + '.bias'], 1e-5)
 
 
-def cross_encoder_layer(sd, p, src, tgt, smask, tmask, spos, tpos, nhead):
-    """TransformerCrossEncoderLayer.forward_pre (transformers.py:183-244), values with pos."""
+def cross_encoder_layer(sd, p, src, tgt, smask, tmask, spos, tpos, nhead, pre_norm=True):
+    """TransformerCrossEncoderLayer.forward_pre (transformers.py:183-244), values with pos;
+    forward_post (:109-181) for pre_norm=False."""
+    if not pre_norm:
+        src = _ln(sd, p + '.norm1', src + mha(sd, p + '.self_attn', src + spos, src + spos,
+                                              src + spos, smask, nhead))
+        tgt = _ln(sd, p + '.norm1', tgt + mha(sd, p + '.self_attn', tgt + tpos, tgt + tpos,
+                                              tgt + tpos, tmask, nhead))
+        s2, t2 = src + spos, tgt + tpos
+        s3 = mha(sd, p + '.multihead_attn', s2, t2, t2, tmask, nhead)
+        t3 = mha(sd, p + '.multihead_attn', t2, s2, s2, smask, nhead)
+        src, tgt = _ln(sd, p + '.norm2', src + s3), _ln(sd, p + '.norm2', tgt + t3)
+
+        def ffn_post(x):
+            h = _relu(x @ sd[p + '.linear1.weight'].t() + sd[p + '.linear1.bias'], p + '.ffn')
+            return _ln(sd, p + '.norm3', x + h @ sd[p + '.linear2.weight'].t() + sd[p + '.linear2.bias'])
+        return ffn_post(src), ffn_post(tgt)
     s2 = _ln(sd, p + '.norm1', src) + spos
     src = src + mha(sd, p + '.self_attn', s2, s2, s2, smask, nhead)
     t2 = _ln(sd, p + '.norm1', tgt) + tpos
@@ -293,6 +308,28 @@ def _pad(seqs):
         out[:len(s), b] = s
         mask[b, :len(s)] = False
     return out, mask
+
+
+def corr_simple_attention(sd, p, query, key, value, kmask, num_neighbors=0):
+    """CorrespondenceDecoder.simple_attention (finegrained_regtr.py:328-363) on padded
+    ([L,] N, B, D) inputs. num_neighbors > 0 restates the reference's masking as it executes:
+    `neighbor_mask[:, :, topk_indices] = 0` indexes the QUERY dim (2) of the (L, B, Q, S) mask
+    with the top-k KEY indices of every row, so query row j keeps its softmax iff j is among
+    all top-k indices of every (layer, pair, row); other rows are all -inf (NaN softmax); an
+    index >= Q raises IndexError."""
+    q = (query @ sd[p + 'q_proj.weight'].t() + sd[p + 'q_proj.bias']) / math.sqrt(query.shape[-1])
+    k = key @ sd[p + 'k_proj.weight'].t() + sd[p + 'k_proj.bias']
+    attn = torch.einsum('...qbd,...sbd->...bqs', q, k)
+    attn = attn.masked_fill(kmask[:, None, :], float('-inf'))
+    if num_neighbors > 0:
+        Q = attn.shape[-2]
+        idx = torch.topk(attn, k=num_neighbors, dim=-1).indices.reshape(-1)
+        if idx.numel() and int(idx.max()) >= Q:
+            raise IndexError(f'index {int(idx.max())} is out of bounds for dimension 2 with size {Q}')
+        keep = torch.zeros(Q, dtype=torch.bool)
+        keep[idx] = True
+        attn = attn.masked_fill(~keep[:, None], float('-inf'))
+    return torch.einsum('...bqs,...sbd->...qbd', torch.softmax(attn, -1), value)
 
 
 # ----------------------------------------------------------------------------------------
@@ -352,10 +389,12 @@ def _forward(cfg, sd, src_xyz, tgt_xyz, meta, mode, train):
     nhead, L = cfg['nhead'], cfg['num_encoder_layers']
     s_int, t_int = [], []
     for l in range(L):                                                         # transformers.py:37-57
+        pre = cfg.get('pre_norm', True)
         src, tgt = cross_encoder_layer(sd, f'transformer_encoder.layers.{l}', src, tgt, smask, tmask,
-                                       spos, tpos, nhead)
-        s_int.append(_ln(sd, 'transformer_encoder.norm', src))
-        t_int.append(_ln(sd, 'transformer_encoder.norm', tgt))
+                                       spos, tpos, nhead, pre_norm=pre)
+        # the final norm exists for pre_norm only (finegrained_regtr.py:56-58)
+        s_int.append(_ln(sd, 'transformer_encoder.norm', src) if pre else src)
+        t_int.append(_ln(sd, 'transformer_encoder.norm', tgt) if pre else tgt)
     s_cond, t_cond = torch.stack(s_int), torch.stack(t_int)
 
     def corr_mlp(x):                                                           # :411-455
@@ -370,12 +409,7 @@ def _forward(cfg, sd, src_xyz, tgt_xyz, meta, mode, train):
                 + sd['correspondence_decoder.conf_logits_decoder.bias'])
 
     def simple_attention(query, key, value, kmask):                          # :328-363
-        q = (query @ sd['correspondence_decoder.q_proj.weight'].t()
-             + sd['correspondence_decoder.q_proj.bias']) / math.sqrt(query.shape[-1])
-        k = key @ sd['correspondence_decoder.k_proj.weight'].t() + sd['correspondence_decoder.k_proj.bias']
-        attn = torch.einsum('...qbd,...sbd->...bqs', q, k)
-        attn = attn.masked_fill(kmask[:, None, :], float('-inf'))
-        return torch.einsum('...bqs,...sbd->...qbd', torch.softmax(attn, -1), value)
+        return corr_simple_attention(sd, 'correspondence_decoder.', query, key, value, kmask)
 
     if cfg.get('direct_regress_coor', False):
         s_corr, t_corr = corr_mlp(s_cond), corr_mlp(t_cond)

@@ -457,6 +457,69 @@ def make_forward_decoder(fr, fk):
     save('forward_modelnet_decoder', **pack_forward(model, meta, out, over, src, tgt, 4.0))
 
 
+def make_forward_postnorm(fr, fk):
+    """(4) the post-norm transformer (pre_norm: False -> forward_post, transformers.py:109-181,
+    and no final encoder norm, finegrained_regtr.py:56-58): the reduced ModelNet config,
+    inactive in the shipped configs, pinned for API completeness."""
+    over = dict(SMALL_MODELNET, pre_norm=False)
+    cfg = load_cfg('modelnet.yaml', **over)
+    pairs = [modelnet_like_pair(i + 9, n_raw=512) for i in range(2)]
+    src = [p[0] for p in pairs]
+    tgt = [p[1] for p in pairs]
+    model, meta, out = run_forward(fr, fk, cfg, src, tgt, seed=11)
+    save('forward_modelnet_postnorm', **pack_forward(model, meta, out, over, src, tgt, 4.0))
+
+
+def make_decoder_topk(fr):
+    """(5) CorrespondenceDecoder with num_neighbors > 0 (finegrained_regtr.py:312-408; the
+    option is a constructor argument only, RegTR never passes it). The module is run as the
+    reference runs it, its (L, N, B, D) inputs built here; cases:
+      eq_k4    B = 1, three layers, 64 + 64 rows, k = 4: the union leaves a few NaN rows;
+      eq_k24   B = 1, 64 + 64 rows, k = 24: a larger union;
+      eq_k1    B = 1, one layer, 64 + 64 rows, k = 1: about a third of the rows NaN;
+      b2_k6    B = 2, every cloud 48 rows (no padding), k = 6;
+      ne_k8    B = 1, 40 src + 64 tgt rows, k = 8: records whether the reference raised
+               (an index >= 40 into the src query dim).
+    Weights: nn.Linear default init under torch.manual_seed(20 + case), stored."""
+    from transformer.position_embedding import PositionEmbeddingCoordsSine
+    arrays = {'cases': np.array(['eq_k4', 'eq_k24', 'eq_k1', 'b2_k6', 'ne_k8'])}
+    D = 32
+    for ci, (name, L, ns, nt, k) in enumerate([('eq_k4', 3, [64], [64], 4),
+                                               ('eq_k24', 3, [64], [64], 24),
+                                               ('eq_k1', 1, [64], [64], 1),
+                                               ('b2_k6', 3, [48, 48], [48, 48], 6),
+                                               ('ne_k8', 3, [40], [64], 8)]):
+        torch.manual_seed(20 + ci)
+        pe = PositionEmbeddingCoordsSine(3, D, scale=1.0)
+        dec = fr.CorrespondenceDecoder(D, True, pe, num_neighbors=k).eval()
+        B = len(ns)
+        sx = [torch.rand(n, 3) for n in ns]
+        tx = [torch.rand(n, 3) for n in nt]
+        sf = torch.randn(L, max(ns), B, D)
+        tf = torch.randn(L, max(nt), B, D)
+        p = f'{name}.'
+        try:
+            with torch.no_grad():
+                sc, tc, so, to = dec(sf, tf, sx, tx)
+            for b in range(B):
+                arrays[p + f'out.src_corr.{b}'] = sc[b].numpy()
+                arrays[p + f'out.tgt_corr.{b}'] = tc[b].numpy()
+                arrays[p + f'out.src_overlap.{b}'] = so[b].numpy()
+                arrays[p + f'out.tgt_overlap.{b}'] = to[b].numpy()
+            arrays[p + 'raised'] = np.bytes_(b'')
+        except (IndexError, RuntimeError) as e:
+            arrays[p + 'raised'] = np.bytes_(type(e).__name__.encode())
+        arrays[p + 'k'] = np.int64(k)
+        arrays[p + 'src_feats'] = sf.numpy()
+        arrays[p + 'tgt_feats'] = tf.numpy()
+        for b in range(B):
+            arrays[p + f'src_xyz.{b}'] = sx[b].numpy()
+            arrays[p + f'tgt_xyz.{b}'] = tx[b].numpy()
+        for kk, v in dec.state_dict().items():
+            arrays[p + 'w.' + kk] = v.numpy()
+    save('decoder_topk', **arrays)
+
+
 def make_loss(fr, fk):
     """Test-step tail fixture: the reference's own RegTR.compute_loss
     (finegrained_regtr.py:252-309) and GenericRegModel._compute_metrics
@@ -583,9 +646,17 @@ if __name__ == '__main__':
     if sys.argv[1:] == ['decoder']:
         make_forward_decoder(fr, fk)
         sys.exit(0)
+    if sys.argv[1:] == ['postnorm']:
+        make_forward_postnorm(fr, fk)
+        sys.exit(0)
+    if sys.argv[1:] == ['topk']:
+        make_decoder_topk(fr)
+        sys.exit(0)
     make_geometry()
     make_modules(fr, fk)
     make_forward(fr, fk)
     make_forward_decoder(fr, fk)
+    make_forward_postnorm(fr, fk)
+    make_decoder_topk(fr)
     make_loss(fr, fk)
     make_train(fr, fk)

@@ -18,7 +18,8 @@ from conftest import elem_err, forward_fixture, rel_err
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-4
-FIXTURES = ['forward_modelnet_small', 'forward_3dmatch_small', 'forward_modelnet_decoder']
+FIXTURES = ['forward_modelnet_small', 'forward_3dmatch_small', 'forward_modelnet_decoder',
+            'forward_modelnet_postnorm']
 KEYS = ['src_feat_un', 'tgt_feat_un', 'src_feat', 'tgt_feat', 'src_kp', 'tgt_kp',
         'src_kp_warped', 'tgt_kp_warped', 'src_overlap', 'tgt_overlap']
 

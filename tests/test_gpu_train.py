@@ -344,15 +344,17 @@ def test_train_step_vs_reference(gpu):
             assert rel_err(getattr(mods[name], stat), ref[k]) < 1e-5, k
 
 
-def test_train_step_vs_oracle_modelnet(gpu):
+@pytest.mark.parametrize('pre_norm', [True, False])
+def test_train_step_vs_oracle_modelnet(gpu, pre_norm):
     """Full-width ModelNet config (d 256, head dim 32: the f16x3 attention and every GEMM path),
     B = 2 pairs of the bench workload: fgreg's train() step vs the fp64 oracle's on the same
     neighbour tables. Losses within 1e-5, every gradient within GRAD_TOL; the cosine of the
-    whole gradient vector above 1 - 1e-6."""
+    whole gradient vector above 1 - 1e-6. pre_norm=False: the post-norm transformer
+    (forward_post, transformers.py:109-181)."""
     import fgreg
     import fgreg.config as fc
     from fgreg.synthetic import make_batch
-    cfg = fc.get('modelnet')
+    cfg = fc.get('modelnet', pre_norm=pre_norm)
     torch.manual_seed(5)
     np.random.seed(5)
     model = fgreg.RegTR(cfg)

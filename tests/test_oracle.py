@@ -64,7 +64,7 @@ def test_oracle_radius_boundary():
 
 
 @pytest.mark.parametrize('name', ['forward_modelnet_small', 'forward_3dmatch_small',
-                                  'forward_modelnet_decoder'])
+                                  'forward_modelnet_decoder', 'forward_modelnet_postnorm'])
 def test_oracle_forward_matches_reference(name):
     cfg, sd, src, tgt, meta, d = forward_fixture(name)
     out = mo.forward(cfg, sd, src, tgt, meta=meta)
