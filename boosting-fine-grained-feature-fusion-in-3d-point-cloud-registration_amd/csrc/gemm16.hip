@@ -40,6 +40,9 @@ bool g5_tile(char cfg, int* bm, int* bn);
 int g5_ksplit(int M, int N, int K, int BM, int BN);
 char bf16_tile(int m, int n, int k);
 int bf16_ksplit(char cfg, int m, int n, int k);
+bool gemm_rs_f16x3(const float* A, int64_t lda, const void* W, int ksteps, const float* wsc,
+                   float* C, int64_t ldc, const float* bias, const float* R, int64_t ldr, int M,
+                   int N, int K, int act, hipStream_t st);
 // few 64 x 64 tiles, narrow output, long contraction: split-K pays (measured)
 inline bool splitk_shape(int m, int n, int k) {
     return k >= 1920 && n <= 256 && (int64_t)((m + 63) / 64) * ((n + 63) / 64) <= 160;
@@ -1044,9 +1047,22 @@ namespace fgr {
 // Few tiles (<= 400 of 64 x 64, e.g. the 3DMatch transformer's 2 x 1060 tokens) with
 // K >= 512: the two-k-group g5 ('W', 'T'; 8 waves per block) -- 1.1-1.45x there
 // (profiles/r02_gemm_tiles_splitk*.txt).
+char h3_tile_kloop(int m, int n, int k);
 char h3_tile(int m, int n, int k) {
     const char* force = getenv("FGR_GEMM16_TILE");
     if (force && force[0]) return force[0];
+    // short contractions over many rows: the row-stationary kernel (gemm_rs.hip) where it
+    // measured faster than the k-looped choice (profiles/r03_gemm_rs_sweep.txt: K <= 128 with
+    // N >= 224 1.08-1.31x, 57264 x 256 x 256 1.14x; elsewhere equal or slower -- the loop of
+    // both structures sits at ~35 % of the MFMA pipe). FGR_GEMM_RS=0 disables.
+    static const bool rs_on = [] { const char* e = getenv("FGR_GEMM_RS"); return !(e && e[0] == '0'); }();
+    if (rs_on && k % 8 == 0 && ((k <= 128 && n >= 224 && m >= 8000) || (k <= 256 && n >= 128 && m >= 50000)))
+        return 'z';
+    return h3_tile_kloop(m, n, k);
+}
+
+// the k-looped kernels' choice
+char h3_tile_kloop(int m, int n, int k) {
     const bool g5ok = k % 8 == 0;
     const int64_t tiles64 = (int64_t)ceil_div(m, 64) * ceil_div(n, 64);
     // very few tiles with a long K (3DMatch's 2120 x 256 x 3840, 2120 x 128 x 1920 KPConv
@@ -1113,7 +1129,16 @@ static int gemm_f16x3_impl(const float* a, int64_t lda, const void* w_img, float
     // tile BM x BN (activation rows x output channels): h3_tile; FGR_GEMM16_TILE overrides it
     // for tuning (a = 128x128, b = 64x128, c = 64x64, d = 128x64, e..x: v2-v4 variants, A..Z,
     // 0..9: g5)
-    const char cfg = h3_tile(m, n, k);
+    char cfg = h3_tile(m, n, k);
+    // rs (gemm_rs.hip): K <= 256, 16-B aligned operands
+    if (cfg == 'z') {
+        if (vec && vo && gemm_rs_f16x3(a, lda, w_img, ksteps_h3(k), wsc, c, ldc, bias, r, ldr, m,
+                                       n, k, act, st)) {
+            FGR_CHECK_LAUNCH("gemm_rs");
+            return FGR_OK;
+        }
+        cfg = h3_tile_kloop(m, n, k);                 // unaligned operands
+    }
     // g5 (gemm5.hip: LDS-DMA pipeline, A split after the read): A..W, K % 8 == 0 only
     if (((cfg >= 'A' && cfg <= 'Z') || (cfg >= '0' && cfg <= '9')) && k % 8 == 0) {
         int ks = h3_ksplit(cfg, m, n, k);

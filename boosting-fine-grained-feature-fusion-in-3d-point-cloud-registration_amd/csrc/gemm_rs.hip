@@ -1,0 +1,307 @@
+// "rs" (row-stationary) f16x3 GEMM for short contractions (K <= 256, K % 8 == 0):
+//
+//   C[M, N] = act(A[M, K] . W[N, K]^T + bias[N] (+ R[M, N]))
+//
+// Why. At K <= 256 a tile of the k-looped kernels (gemm16.hip, gemm5.hip) runs 4-8 k32-steps:
+// every step waits an operand round trip, and every block that shares an A row panel loads
+// and splits it again. Here a wave loads its activation rows ONCE, whole (16 * RT rows x K),
+// splits them in registers into the two fp16 terms with ONE power-of-two scale per row (the
+// row max over all of K into [2^14, 2^15): no in-flight rescaling, the scale goes to the
+// epilogue), and keeps them resident; the block then streams its range of W panels (16
+// output columns x K each, the fgr_split_weights_h3 image as it lies) global -> LDS by
+// LDS-DMA into a two-panel ring shared by the 4 waves, and per panel runs a pure MFMA loop
+// (3 * RT * K/32 MFMAs per wave, no split VALU) followed by a 16-B-per-lane epilogue.
+//
+// Precision: per product the three significant fp16 products hh, hm, mh in fp32
+// accumulation as in gemm16.hip; one scale per row means elements far below the row max
+// lose low bits of their lo term to fp16 subnormals, an ABSOLUTE error <= 2^-39 max|a_row|
+// per element (2^-24 / 2 of the subnormal spacing over the 2^14 scale floor) -- relative to
+// the dot product's own fp32 rounding (K 2^-24 sum|a w|) negligible.
+//
+// Swapped orientation (gemm16.hip): W fragments are the MFMA A operand, activation fragments
+// the B operand, so a lane's 4 accumulators are 4 consecutive output columns of ONE row.
+// 16x16x32 f16 lane maps (lane l, g = l >> 4, c = l & 15): A[i = c][k = 8g + e],
+// B[k = 8g + e][j = c], C[i = 4g + r][j = c].
+#include <algorithm>
+#include <cstdlib>
+
+#include "common.h"
+
+namespace fgr {
+namespace {
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+struct RsArgs {
+    const float* A; int64_t lda;
+    const u32x4* W;                   // image [panel][kstep KS][term 2][g 4][16] x 16 B
+    const float* wsc;                 // per n: 2^-e_n (padded to 16)
+    float* C; int64_t ldc;
+    const float* bias;
+    const float* R; int64_t ldr;
+    int M, N, K, act;
+    int nc;                           // W panels (16 columns) per block
+};
+
+// s_waitcnt vmcnt(n) lgkmcnt(0) -- gfx9 encoding
+template <int N>
+__device__ __forceinline__ void wait_vm_lgkm0_rs() {
+    static_assert(N >= 0 && N < 64, "vmcnt");
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4));
+}
+
+__device__ __forceinline__ float xg_max_rs(float v) {     // max over lanes c, c^16, c^32, c^48
+    auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+    auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+
+__device__ __forceinline__ float finish_rs(float y, float b, float r, int act) {
+    if (act == FGR_ACT_RELU_RES_LEAKY) {
+        const float t = fmaxf(y + b, 0.f) + r;
+        return t > 0.f ? t : 0.1f * t;
+    }
+    const float t = y + b + r;
+    return act == FGR_ACT_RELU ? fmaxf(t, 0.f) : t;
+}
+
+// vmcnt(n) lgkmcnt(0) for a wave-uniform runtime n <= 15 (s_waitcnt takes an immediate)
+__device__ __forceinline__ void wait_vm_lgkm0_dyn(int n) {
+    switch (n) {
+        case 0: wait_vm_lgkm0_rs<0>(); break;   case 1: wait_vm_lgkm0_rs<1>(); break;
+        case 2: wait_vm_lgkm0_rs<2>(); break;   case 3: wait_vm_lgkm0_rs<3>(); break;
+        case 4: wait_vm_lgkm0_rs<4>(); break;   case 5: wait_vm_lgkm0_rs<5>(); break;
+        case 6: wait_vm_lgkm0_rs<6>(); break;   case 7: wait_vm_lgkm0_rs<7>(); break;
+        case 8: wait_vm_lgkm0_rs<8>(); break;   case 9: wait_vm_lgkm0_rs<9>(); break;
+        case 10: wait_vm_lgkm0_rs<10>(); break; case 11: wait_vm_lgkm0_rs<11>(); break;
+        case 12: wait_vm_lgkm0_rs<12>(); break; case 13: wait_vm_lgkm0_rs<13>(); break;
+        case 14: wait_vm_lgkm0_rs<14>(); break; default: wait_vm_lgkm0_rs<15>(); break;
+    }
+}
+
+constexpr int kRsNb = 3;           // W panels in the LDS ring (two in flight while one computes)
+constexpr int kRsMaxNc = 64;       // panels per block (the per-block column scales / bias in LDS)
+
+// RT row tiles of 16 per wave (block = 4 waves = 64 RT rows), KS k32-steps (the image's
+// ksteps: K <= 32 KS), residual present or not. C / R / bias 16-B aligned (the dispatcher
+// checks), N padded to 16 in the image and wsc.
+// Per panel q (program order): wait for its DMA, barrier, residual loads for panel q + 1,
+// DMA of panel q + 2 into the buffer panel q - 1 used, MFMAs, epilogue stores. vm operations
+// complete in issue order, so "panel q's DMA landed" = at most (the ops issued after it)
+// outstanding, counted from below (stores >= one per row tile with a valid row, residual
+// loads >= 0): a stronger wait whenever more were issued.
+template <int RT, int KS, bool RES>
+__global__ void __launch_bounds__(256) gemm_rs_kernel(RsArgs p) {
+    constexpr int PANEL_U = KS * 128;                  // 16-B units per W panel
+    constexpr int PW = PANEL_U / 256;                  // DMA pieces (1 KiB) per wave per panel
+    static_assert(PANEL_U % 256 == 0, "KS even");
+    __shared__ u32x4 ring[kRsNb * PANEL_U];
+    __shared__ float4 colw[kRsMaxNc * 4], colb[kRsMaxNc * 4];   // per (panel, g): wsc, bias
+
+    const int nbm = (p.M + 64 * RT - 1) / (64 * RT);
+    const int npanel = (p.N + 15) / 16;
+    const int ngrp = (npanel + p.nc - 1) / p.nc;
+    const int nwg = nbm * ngrp;
+    int t = blockIdx.x;
+    {   // XCD-aware order: each XCD a contiguous range, the column groups of a row block adjacent
+        const int q = nwg / 8, r = nwg % 8, x = t % 8, lo = t / 8;
+        t = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + lo;
+    }
+    const int bm = t / ngrp, grp = t % ngrp;
+    const int p0 = grp * p.nc;
+    const int np = min(p.nc, npanel - p0);             // block-uniform
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+    const int g = lane >> 4, c = lane & 15;
+    const int mw = bm * 64 * RT + wv * 16 * RT;        // this wave's first row
+
+    // W panel DMA: wave wv moves pieces wv, wv + 4, ... (1 KiB each, contiguous in the image)
+    const u32x4* wsrc = p.W + (int64_t)p0 * PANEL_U + wv * 64 + lane;
+    auto dma = [&](int q) {
+        __attribute__((address_space(3))) char* dst =
+            (__attribute__((address_space(3))) char*)(ring + (q % kRsNb) * PANEL_U) + wv * 1024;
+#pragma unroll
+        for (int j = 0; j < PW; ++j)
+            __builtin_amdgcn_global_load_lds((const void*)(wsrc + (int64_t)q * PANEL_U + j * 256),
+                                             (__attribute__((address_space(3))) void*)(dst + j * 4096),
+                                             16, 0, 0);
+    };
+    dma(0);
+    if (np > 1) dma(1);
+
+    // activation rows -> registers, one scale per row, split once
+    f16x8 af[RT][KS][2];
+    float rs[RT];
+#pragma unroll
+    for (int i = 0; i < RT; ++i) {
+        const int64_t row = min(mw + 16 * i + c, p.M - 1);
+        const float* ar = p.A + row * p.lda;
+        float x[KS][8];
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            const int k = 32 * s + 8 * g;
+            float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0;
+            if (k < p.K) {
+                a0 = *reinterpret_cast<const float4*>(ar + k);
+                a1 = *reinterpret_cast<const float4*>(ar + k + 4);
+            }
+            x[s][0] = a0.x; x[s][1] = a0.y; x[s][2] = a0.z; x[s][3] = a0.w;
+            x[s][4] = a1.x; x[s][5] = a1.y; x[s][6] = a1.z; x[s][7] = a1.w;
+        }
+        float mx = 0.f;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            mx = fmaxf(mx, max3_abs(x[s][0], x[s][1], x[s][2]));
+            mx = fmaxf(mx, max3_abs(x[s][3], x[s][4], x[s][5]));
+            mx = fmaxf(mx, max3_abs(x[s][6], x[s][7], 0.f));
+        }
+        mx = xg_max_rs(mx);
+        // max * 2^e in [2^14, 2^15) (e = 0 for an all-zero row)
+        const int e = mx > 0.f ? min(15 - __builtin_amdgcn_frexp_expf(mx), 127) : 0;
+        rs[i] = __builtin_ldexpf(1.f, -e);
+        const float sc = __builtin_ldexpf(1.f, e);
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            u32x4 h, l;
+            split8_f16(x[s], sc, h, l);
+            af[i][s][0] = __builtin_bit_cast(f16x8, h);
+            af[i][s][1] = __builtin_bit_cast(f16x8, l);
+        }
+    }
+    // the block's column scales and bias, by (panel, g) float4 (read by the epilogues)
+    for (int u = tid; u < np * 4; u += 256) {
+        const int n = p0 * 16 + 4 * u;
+        colw[u] = *reinterpret_cast<const float4*>(p.wsc + n);
+        float e[4] = {0.f, 0.f, 0.f, 0.f};
+        if (p.bias)
+            for (int j = 0; j < 4 && n + j < p.N; ++j) e[j] = p.bias[n + j];
+        colb[u] = make_float4(e[0], e[1], e[2], e[3]);
+    }
+
+    // row tiles of this wave with at least one row < M (a tile past M is skipped by the wave)
+    int nst = 0;
+#pragma unroll
+    for (int i = 0; i < RT; ++i) nst += (mw + 16 * i < p.M) ? 1 : 0;
+    auto load_res = [&](int q, float4 (&rv)[RT]) {
+        const int n = (p0 + q) * 16 + 4 * g;
+#pragma unroll
+        for (int i = 0; i < RT; ++i) {
+            const int64_t row = min(mw + 16 * i + c, p.M - 1);
+            const float* src = p.R + row * p.ldr + n;
+            if (n + 3 < p.N) {
+                rv[i] = *reinterpret_cast<const float4*>(src);
+            } else {
+                float e[4] = {0.f, 0.f, 0.f, 0.f};
+                for (int j = 0; j < 4 && n + j < p.N; ++j) e[j] = src[j];
+                rv[i] = make_float4(e[0], e[1], e[2], e[3]);
+            }
+        }
+    };
+    float4 rcur[RT], rnext[RT];
+    if constexpr (RES) load_res(0, rcur);
+
+    for (int q = 0; q < np; ++q) {
+        // ops issued after panel q's DMA, counted from below: q = 0: DMA of panel 1 (the
+        // prologue's loads are consumed; panel 0's residual is not counted); q >= 1: stores of
+        // panel q - 2 (q >= 2), [residual loads of panel q], DMA of panel q + 1 if any, stores
+        // of panel q - 1
+        if (q == 0) wait_vm_lgkm0_dyn(np > 1 ? PW : 0);
+        else wait_vm_lgkm0_dyn((q >= 2 ? nst : 0) + nst + (q + 1 < np ? PW : 0));
+        __builtin_amdgcn_s_barrier();                    // every wave's pieces; buffer of q - 1 free
+        if constexpr (RES)
+            if (q + 1 < np) load_res(q + 1, rnext);
+        if (q + 2 < np) dma(q + 2);
+
+        typedef __attribute__((address_space(3))) u32x4 lds_u4;
+        const uint32_t base = (uint32_t)(uintptr_t)(ring + (q % kRsNb) * PANEL_U) +
+                              (uint32_t)(g * 16 + c) * 16;
+        f32x4 acc[RT];
+#pragma unroll
+        for (int i = 0; i < RT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            const f16x8 wh = __builtin_bit_cast(f16x8, *(lds_u4*)(uintptr_t)(base + (s * 2 + 0) * 64 * 16));
+            const f16x8 wl = __builtin_bit_cast(f16x8, *(lds_u4*)(uintptr_t)(base + (s * 2 + 1) * 64 * 16));
+#pragma unroll
+            for (int i = 0; i < RT; ++i) {
+                acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, af[i][s][0], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, af[i][s][1], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, af[i][s][0], acc[i], 0, 0, 0);
+            }
+        }
+        // epilogue: lane holds C[row = mw + 16i + c][n .. n + 3]
+        const int n = (p0 + q) * 16 + 4 * g;
+        const float4 ws = colw[q * 4 + g], bv = colb[q * 4 + g];
+        if (n < p.N) {
+#pragma unroll
+            for (int i = 0; i < RT; ++i) {
+                const int64_t row = mw + 16 * i + c;
+                if (row >= p.M) continue;
+                float4 r4 = make_float4(0.f, 0.f, 0.f, 0.f);
+                if constexpr (RES) r4 = rcur[i];
+                const float y0 = acc[i][0] * rs[i] * ws.x, y1 = acc[i][1] * rs[i] * ws.y;
+                const float y2 = acc[i][2] * rs[i] * ws.z, y3 = acc[i][3] * rs[i] * ws.w;
+                float* crow = p.C + row * p.ldc;
+                if (n + 3 < p.N) {
+                    *reinterpret_cast<float4*>(crow + n) =
+                        make_float4(finish_rs(y0, bv.x, r4.x, p.act), finish_rs(y1, bv.y, r4.y, p.act),
+                                    finish_rs(y2, bv.z, r4.z, p.act), finish_rs(y3, bv.w, r4.w, p.act));
+                } else {                                   // ragged last panel (N % 4 != 0)
+                    const float yy[4] = {y0, y1, y2, y3};
+                    const float bb[4] = {bv.x, bv.y, bv.z, bv.w}, rr[4] = {r4.x, r4.y, r4.z, r4.w};
+                    for (int e = 0; e < 4 && n + e < p.N; ++e)
+                        crow[n + e] = finish_rs(yy[e], bb[e], rr[e], p.act);
+                }
+            }
+        }
+        if constexpr (RES)
+#pragma unroll
+            for (int i = 0; i < RT; ++i) rcur[i] = rnext[i];
+    }
+}
+
+template <int RT, int KS>
+bool launch_rs_k(const RsArgs& a, unsigned blocks, hipStream_t st) {
+    if (a.R)
+        hipLaunchKernelGGL((gemm_rs_kernel<RT, KS, true>), dim3(blocks), dim3(256), 0, st, a);
+    else
+        hipLaunchKernelGGL((gemm_rs_kernel<RT, KS, false>), dim3(blocks), dim3(256), 0, st, a);
+    return true;
+}
+
+}  // namespace
+
+// The rs kernel applies to K <= 256, K % 8 == 0 with 16-B aligned A / C / R / bias rows
+// (checked by the caller). ksteps = the image's k32-steps (even, <= 8).
+bool gemm_rs_f16x3(const float* A, int64_t lda, const void* W, int ksteps, const float* wsc,
+                   float* C, int64_t ldc, const float* bias, const float* R, int64_t ldr, int M,
+                   int N, int K, int act, hipStream_t st) {
+    if (K % 8 != 0 || ksteps > 8 || ksteps % 2 != 0) return false;
+    // row tiles per wave: 2 (W fragments reused twice) unless that leaves too few blocks
+    const char* rte = getenv("FGR_RS_RT");
+    int RT = (rte && rte[0]) ? atoi(rte) : 2;
+    if (RT != 1 && RT != 2) RT = 2;
+    const int npanel = (N + 15) / 16;
+    const int nbm = (M + 64 * RT - 1) / (64 * RT);
+    // panels per block: 8 (the measured best or within 5 % of it on every dispatched shape,
+    // profiles/r03_gemm_rs_sweep.txt); FGR_RS_NC overrides, 0 = ~3 blocks per CU
+    const char* nce = getenv("FGR_RS_NC");
+    int nc = (nce && nce[0]) ? atoi(nce) : 8;
+    if (nc <= 0) {
+        const int64_t target = 768;
+        nc = (int)std::max<int64_t>(1, std::min<int64_t>(npanel, ((int64_t)nbm * npanel + target - 1) / target));
+    }
+    nc = std::min(std::min(nc, npanel), kRsMaxNc);
+    const int ngrp = (npanel + nc - 1) / nc;
+    const unsigned blocks = (unsigned)((int64_t)nbm * ngrp);
+    RsArgs a{A, lda, (const u32x4*)W, wsc, C, ldc, bias, R, ldr, M, N, K, act, nc};
+#define RS_CASE(rt, ks) \
+    if (RT == rt && ksteps == ks) return launch_rs_k<rt, ks>(a, blocks, st);
+    RS_CASE(2, 2) RS_CASE(2, 4) RS_CASE(2, 6) RS_CASE(2, 8)
+    RS_CASE(1, 2) RS_CASE(1, 4) RS_CASE(1, 6) RS_CASE(1, 8)
+#undef RS_CASE
+    return false;
+}
+
+}  // namespace fgr

@@ -346,7 +346,7 @@ def test_gemm_split_vs_fp64(gpu, m, n, k):
             assert rel_err(fl.linear(X, W, Bb[:h], rows=(0, h)), ref[:, :h]) < tol
 
 
-@pytest.mark.parametrize('tile', ['', 'b', 'I', 'K', 'O', 'S'])
+@pytest.mark.parametrize('tile', ['', 'b', 'I', 'K', 'O', 'S', 'z'])
 def test_gemm_f16x3_dynamic_range(gpu, tile, monkeypatch):
     """f16x3 row scaling (tile: '' the default dispatch, else FGR_GEMM16_TILE) under
     adversarial magnitudes: rows at 1e-15 .. 1e15 (far outside fp16's range), all-zero rows, rows whose first k chunks are zero, rows that grow by
@@ -355,12 +355,12 @@ def test_gemm_f16x3_dynamic_range(gpu, tile, monkeypatch):
     monkeypatch.setenv('FGR_GEMM16_TILE', tile)
     from fgreg import linear as fl
     g = torch.Generator().manual_seed(7)
-    m, n, k = 700, 96, 320
+    m, n, k = 700, 96, 256 if tile == 'z' else 320     # z: the K <= 256 row-stationary kernel
     x = torch.randn(m, k, generator=g, dtype=torch.float64)
     row_scale = torch.tensor([10.0 ** e for e in np.linspace(-15, 15, m)], dtype=torch.float64)
     x *= row_scale[:, None]
     x[5] = 0
-    x[17, :200] = 0                                  # first nonzero chunk late
+    x[17, :200 if k > 256 else 160] = 0              # first nonzero chunk late
     ramp = torch.pow(2.0, torch.linspace(0, 40, k, dtype=torch.float64))
     x[30:60] *= ramp                                 # growing rows: rescales mid-k
     x[60:90] *= ramp.flip(0)                         # shrinking rows
@@ -385,7 +385,7 @@ def test_gemm_f16x3_dynamic_range(gpu, tile, monkeypatch):
     del ref
 
 
-@pytest.mark.parametrize('tile', list('abcdefghijklmnopqrstuvwxy') + list('ABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789'))
+@pytest.mark.parametrize('tile', list('abcdefghijklmnopqrstuvwxyz') + list('ABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789'))
 def test_gemm_f16x3_tiles(gpu, tile, monkeypatch):
     """Every f16x3 tile / pipeline variant (FGR_GEMM16_TILE; A..R: the LDS-DMA g5 kernels of
     gemm5.hip) at fp32 accuracy on ragged shapes (M, N, K not multiples of the tiles; K % 64
@@ -397,7 +397,8 @@ def test_gemm_f16x3_tiles(gpu, tile, monkeypatch):
     try:
         fl.set_mode('f16x3')
         for m, n, k in ((1000, 200, 1000), (333, 3, 96), (130, 520, 40), (77, 50, 36),
-                        (4099, 272, 264)):
+                        (4099, 272, 264), (1000, 200, 256), (257, 1, 128), (4100, 33, 200),
+                        (64, 16, 8)):
             x = torch.randn(m, k, generator=g)
             w = torch.randn(n, k, generator=g) / math.sqrt(k)
             b = torch.randn(n, generator=g)
