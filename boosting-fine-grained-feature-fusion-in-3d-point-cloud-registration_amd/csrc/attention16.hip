@@ -24,11 +24,9 @@
 // Per-(tile, head) image, 256 * DH B (16 KB at DH 32, 32 KB at DH 64), staged into LDS by a
 // flat copy:
 //   K: [k-step DH/32][term 2][g 4][key 64] x 16 B (8 dims)   ds_read_b128, conflict-free
-//   V: [term 2][key 64][DH] f16, 16-B chunk index XOR ((key >> 2) & 1) << 1
+//   V: [term 2][key 64][DH] f16, 16-B chunk index XOR v_swz<DH>(key)
 // Tile t of kv segment s sits at tile index kv_off[s] / 64 + s + t; the (e_k, e_v) scale
 // exponents of all tiles follow the images.
-#include <algorithm>
-#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -66,6 +64,18 @@ __device__ __forceinline__ int range_exp(float mx) {
 __device__ __forceinline__ void split2(float x, _Float16& h, _Float16& m) {
     h = (_Float16)x;
     m = (_Float16)(x - (float)h);
+}
+
+// V image row swizzle: XOR applied to the 16-B chunk index of key row `key`, so that the
+// ds_read_b64_tr_b16 of a 32-lane group (8 key rows x 32 B) hits 64 distinct banks. DH 32
+// (64-B rows, 4 per 256-B bank period): rows r, r + 4 separated by 32 B (row bit 2); DH 64
+// (128-B rows, 2 per period): rows r, r + 2, r + 4, r + 6 share banks and take four distinct
+// 32-B chunk pairs (row bits 1-2) -- without it they read 2-way conflicted (round-3 PMC:
+// 1.2 M conflict cycles per 0.9 M LDS instructions at DH 64, none at DH 32).
+template <int DH>
+__device__ __forceinline__ int v_swz(int key) {
+    if constexpr (DH == 64) return ((key >> 1) & 3) << 1;
+    else return ((key >> 2) & 1) << 1;
 }
 
 template <int DH>
@@ -123,7 +133,7 @@ attn_kv_image16_kernel(const float* __restrict__ k, int64_t ld_k, const float* _
             split2(vf[i][j] * sv, vt[0][j], vt[1][j]);
         }
         const int ks = d0 >> 5, g = (d0 & 31) >> 3, half = (d0 >> 2) & 1;
-        const int vch = (d0 >> 3) ^ (((key >> 2) & 1) << 1);
+        const int vch = (d0 >> 3) ^ v_swz<DH>(key);
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
             *reinterpret_cast<uint2*>(base + (((ks * 2 + t) * 4 + g) * 64 + key) * 16 + half * 8) =
@@ -198,7 +208,7 @@ attn_f16x3_v2_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __r
                      const int2* __restrict__ sc, float* __restrict__ o, int64_t ld_o,
                      const int64_t* __restrict__ q_off, const int64_t* __restrict__ kv_off,
                      const int32_t* __restrict__ kv_seg, int n_head, int n_seg, int n_qblk,
-                     float scale_log2, int n_split, float* __restrict__ part, int max_q_len) {
+                     float scale_log2) {
     constexpr int KD = DH / 32, TD = DH / 16;
     constexpr int UN = units<DH>();
     constexpr int PW = UN / 64 / 4;                              // DMA pieces per wave per tile
@@ -207,10 +217,8 @@ attn_f16x3_v2_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __r
     // reads of the other (one array + integer addresses made it wait for the in-flight DMA of
     // the next tile -- vmcnt(0) -- before the first V read of every tile)
     __shared__ u32x4 lds_b0[UN], lds_b1[UN];
-    // key split (attn_kv_splits): blocks [split * nbase, (split + 1) * nbase) take the split's
-    // share of every segment's key tiles
-    const int nbase = gridDim.x / n_split, split = blockIdx.x / nbase;
-    const int L = blockIdx.x % nbase, xcd = L & 7, j0 = L >> 3;
+    typedef __attribute__((address_space(3))) char lds_c;
+    const int L = blockIdx.x, xcd = L & 7, j0 = L >> 3;
     const int pair = (j0 / n_qblk) * 8 + xcd, qblk = j0 % n_qblk;
     if (pair >= n_seg * n_head) return;
     const int seg = pair / n_head, head = pair % n_head;
@@ -221,7 +229,6 @@ attn_f16x3_v2_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __r
     const int64_t kb = kv_off[ks];
     const int nk = (int)(kv_off[ks + 1] - kb);
     const int ntile = (nk + 63) / 64;
-    const int t_beg = split * ntile / n_split, t_end = (split + 1) * ntile / n_split;
     const int64_t tile0 = (kb / 64 + ks) * n_head + head;
     const int64_t tile_stride = (int64_t)n_head * UN;
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
@@ -268,16 +275,15 @@ attn_f16x3_v2_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __r
     const float one = 1.0f;
 
     // per-lane LDS byte addresses (buffer 0); everything else is an instruction offset
-    typedef __attribute__((address_space(3))) char lds_c;
     const uint32_t kaddr = (uint32_t)(g * 64 + c) * 16;            // K fragment reads (bytes)
     // V transposed reads: lane c = 4qq + p reads rows 4g + qq (+16 k, +32 j), columns
-    // 16t + 4p .. +3: chunk 2t + (p >> 1) XOR 2 (g & 1) (the image's swizzle, row bit 2 = g & 1)
+    // 16t + 4p .. +3: chunk 2t + (p >> 1) XOR the image's row swizzle (v_swz)
     const int qq = c >> 2, pp = c & 3;
     uint32_t vaddr[TD];
 #pragma unroll
     for (int t = 0; t < TD; ++t)
         vaddr[t] = unit_v<DH>() * 16 + (4 * g + qq) * (2 * DH) +
-                   (((2 * t + (pp >> 1)) ^ ((g & 1) << 1)) * 16) + (pp & 1) * 8;
+                   (((2 * t + (pp >> 1)) ^ v_swz<DH>(4 * g + qq)) * 16) + (pp & 1) * 8;
 
     auto dma = [&](int t, auto buf_tag) {                        // tile t -> buffer BUF
         constexpr int BUF = decltype(buf_tag)::value;
@@ -290,14 +296,14 @@ attn_f16x3_v2_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __r
                                              (__attribute__((address_space(3))) void*)(dst + j * 1024),
                                              16, 0, 0);
     };
-    if (t_end > t_beg) dma(t_beg, std::integral_constant<int, 0>{});
+    if (ntile > 0) dma(0, std::integral_constant<int, 0>{});
 
     auto tile = [&](int tt, auto buf_tag, auto mask_tag) {
         constexpr int BUF = decltype(buf_tag)::value;
         constexpr bool MASK = decltype(mask_tag)::value;
         wait_vm_lgkm0_a<0>();           // this wave's pieces of tile tt landed
         __builtin_amdgcn_s_barrier();   // everyone's landed; buffer 1 - BUF no longer read
-        if (tt + 1 < t_end) dma(tt + 1, std::integral_constant<int, 1 - BUF>{});
+        if (tt + 1 < ntile) dma(tt + 1, std::integral_constant<int, 1 - BUF>{});
         const int2 e2 = sc[tile0 + (int64_t)__builtin_amdgcn_readfirstlane(tt) * n_head];
         lds_c* const bp = (lds_c*)(BUF == 0 ? lds_b0 : lds_b1);
         typedef __attribute__((address_space(3))) u32x4 lds_u4;
@@ -388,37 +394,21 @@ attn_f16x3_v2_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __r
     };
     using B0 = std::integral_constant<int, 0>;
     using B1 = std::integral_constant<int, 1>;
-    const int nfull = min(nk / 64, t_end);           // this split's tiles with 64 valid keys
-    int tt = t_beg;                                  // buffers alternate from t_beg (B0)
+    const int nfull = nk / 64;                       // tiles with 64 valid keys
+    int tt = 0;
     for (; tt + 2 <= nfull; tt += 2) {
         tile(tt, B0{}, std::false_type{});
         tile(tt + 1, B1{}, std::false_type{});
     }
-    if (tt < nfull) {
+    if (tt < nfull) {                                // tt even: buffer 0
         tile(tt, B0{}, std::false_type{});
         ++tt;
     }
-    if (tt < t_end) {
-        if ((tt - t_beg) & 1) tile(tt, B1{}, std::true_type{});
+    if (tt < ntile) {
+        if (tt & 1) tile(tt, B1{}, std::true_type{});
         else tile(tt, B0{}, std::true_type{});
     }
 
-    if (n_split > 1) {           // unnormalised partial (2^14 units) + (row max, sum): combined later
-        const float lsum = xg_sum16(l_run);
-        if (qrow < qe) {
-            const int64_t slot = (int64_t)(split * n_seg + seg) * max_q_len + (qrow - qb);
-            float* pa = part + slot * (n_head * DH) + head * DH;
-#pragma unroll
-            for (int t = 0; t < TD; ++t)
-                *reinterpret_cast<float4*>(pa + 16 * t + 4 * g) =
-                    make_float4(acc[t][0], acc[t][1], acc[t][2], acc[t][3]);
-            if (g == 0) {
-                float2* ml = reinterpret_cast<float2*>(part + (int64_t)n_split * n_seg * max_q_len * n_head * DH);
-                ml[slot * n_head + head] = make_float2(m_run, lsum);
-            }
-        }
-        return;
-    }
     // O^T (dh 16t + 4g + r, query c) / l (both in 2^14 units)
     const float inv = 1.0f / xg_sum16(l_run);
     if (qrow < qe) {
@@ -434,88 +424,18 @@ attn_f16x3_v2_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __r
 
 int64_t n_tiles16(int64_t n_kv_rows, int32_t n_kv_seg) { return n_kv_rows / 64 + n_kv_seg + 1; }
 
-// Key-split combine: per (segment, query row) one wave over the row's n_head * dh outputs,
-// o = sum_s 2^(m_s - M) acc_s / sum_s 2^(m_s - M) l_s with M = max_s m_s (empty splits carry
-// m = -inf, l = 0).
-__global__ void __launch_bounds__(256)
-attn_split_combine_kernel(float* __restrict__ o, int64_t ld_o, const int64_t* __restrict__ q_off,
-                          int n_seg, int max_q_len, int n_head, int dh, int n_split,
-                          const float* __restrict__ part) {
-    const int seg = blockIdx.y;
-    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int64_t qb = q_off[seg];
-    if (qb + r >= q_off[seg + 1]) return;
-    const int lane = threadIdx.x & 63, W = n_head * dh;
-    const float2* ml = reinterpret_cast<const float2*>(part + (int64_t)n_split * n_seg * max_q_len * W);
-    for (int j = lane; j < W / 4; j += 64) {
-        const int col = 4 * j, head = col / dh;
-        float M = -INFINITY;
-        for (int s = 0; s < n_split; ++s)
-            M = fmaxf(M, ml[((int64_t)(s * n_seg + seg) * max_q_len + r) * n_head + head].x);
-        float lt = 0.f;
-        float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-        for (int s = 0; s < n_split; ++s) {
-            const int64_t slot = (int64_t)(s * n_seg + seg) * max_q_len + r;
-            const float2 v = ml[slot * n_head + head];
-            const float w = __builtin_amdgcn_exp2f(v.x - M);
-            lt = __builtin_fmaf(w, v.y, lt);
-            const float4 x = *reinterpret_cast<const float4*>(part + slot * W + col);
-            a.x = __builtin_fmaf(w, x.x, a.x); a.y = __builtin_fmaf(w, x.y, a.y);
-            a.z = __builtin_fmaf(w, x.z, a.z); a.w = __builtin_fmaf(w, x.w, a.w);
-        }
-        const float inv = 1.0f / lt;
-        *reinterpret_cast<float4*>(o + (qb + r) * ld_o + col) =
-            make_float4(a.x * inv, a.y * inv, a.z * inv, a.w * inv);
-    }
-}
-
 }  // namespace
-
-// Key splits of one attention launch: when the (segment, head, 64-query block) grid leaves
-// the chip's resident-block slots mostly idle (3DMatch's 2 x 1060-token clouds: 272 blocks
-// for 512 slots at head dim 64; one wave per SIMD), every block takes 1 / n_split of its
-// segment's key tiles and a combine pass merges the partials. At least two key tiles per
-// split; FGR_ATTN_SPLIT overrides (1 = never).
-int attn_kv_splits(int n_seg, int n_head, int max_q_len, int max_kv_len, int slots) {
-    const char* e = getenv("FGR_ATTN_SPLIT");
-    const int64_t useful = (int64_t)n_seg * n_head * ceil_div(max_q_len, 64);
-    const int max_by_tiles = (int)std::max<int64_t>(1, ceil_div(max_kv_len, 64) / 2);
-    int s;
-    if (e && e[0]) s = atoi(e);
-    else s = useful >= slots ? 1 : (int)ceil_div(slots, useful);
-    return std::max(1, std::min(std::min(s, max_by_tiles), 8));
-}
-
-size_t attn_split_bytes(int n_split, int n_seg, int max_q_len, int n_head, int dh) {
-    if (n_split <= 1) return 0;
-    return (size_t)n_split * n_seg * max_q_len * n_head * (dh + 2) * sizeof(float);
-}
-
-int attn_split_combine(float* o, int64_t ld_o, const int64_t* q_off, int n_seg, int max_q_len,
-                       int n_head, int dh, int n_split, const float* part, hipStream_t st) {
-    hipLaunchKernelGGL(attn_split_combine_kernel, dim3((unsigned)ceil_div(max_q_len, 4), (unsigned)n_seg),
-                       dim3(256), 0, st, o, ld_o, q_off, n_seg, max_q_len, n_head, dh, n_split, part);
-    FGR_CHECK_LAUNCH("attn_split_combine_kernel");
-    return FGR_OK;
-}
 }  // namespace fgr
 
 using namespace fgr;
 
-// resident blocks per CU of attn_f16x3_v2_kernel (its __launch_bounds__ occupancy)
-static int f16x3_slots(int dh) { return (dh == 64 ? 2 : 5) * 256; }
-
 extern "C" int fgr_attention_f16x3_workspace(int64_t n_kv_rows, int32_t n_kv_seg,
-                                             int32_t n_head, int32_t n_seg, int32_t max_q_len,
-                                             int32_t max_kv_len, int32_t head_dim, size_t* bytes) {
-    FGR_REQUIRE(bytes && n_kv_rows >= 0 && n_kv_seg >= 0 && n_head > 0 && n_seg >= 0 &&
-                    max_q_len >= 0 && max_kv_len >= 0 && (head_dim == 32 || head_dim == 64),
+                                             int32_t n_head, size_t* bytes) {
+    FGR_REQUIRE(bytes && n_kv_rows >= 0 && n_kv_seg >= 0 && n_head > 0,
                 "fgr_attention_f16x3_workspace: bad arguments");
-    // images sized for the largest supported head dim (64), then the key-split partials
+    // sized for the largest supported head dim (64)
     const int64_t nt = n_tiles16(n_kv_rows, n_kv_seg) * n_head;
-    const size_t img = (size_t)(nt * units<64>() * 16 + nt * 8);
-    const int ns = attn_kv_splits(n_seg, n_head, max_q_len, max_kv_len, f16x3_slots(head_dim));
-    *bytes = (img + 15) / 16 * 16 + attn_split_bytes(ns, n_seg, max_q_len, n_head, head_dim);
+    *bytes = (size_t)(nt * units<64>() * 16 + nt * 8);
     return FGR_OK;
 }
 
@@ -561,20 +481,14 @@ extern "C" int fgr_attention_f16x3(const float* q, int64_t ld_q, const float* k,
     const int n_qblk = (int)ceil_div(max_q_len, 64);
     const int64_t n_blocks = ceil_div((int64_t)n_seg * n_head, 8) * 8 * n_qblk;
     const float sl2 = scale * 1.4426950408889634f;
-    // key splits where the grid is small (attn_kv_splits) and the workspace holds the partials
-    int ns = attn_kv_splits(n_seg, n_head, max_q_len, max_kv_len, f16x3_slots(dh));
-    const size_t img_bytes = (size_t)(nt * un * 16 + nt * 8 + 15) / 16 * 16;
-    if ((size_t)ws_bytes < img_bytes + attn_split_bytes(ns, n_seg, max_q_len, n_head, dh)) ns = 1;
-    float* part = reinterpret_cast<float*>(static_cast<char*>(workspace) + img_bytes);
     if (dh == 32)
-        hipLaunchKernelGGL((attn_f16x3_v2_kernel<32>), dim3((unsigned)(n_blocks * ns)), dim3(256), 0, st,
-                           q, ld_q, (const uint4*)img, (const int2*)sc, o, ld_o, q_off, kv_off, kv_seg,
-                           n_head, n_seg, n_qblk, sl2, ns, part, max_q_len);
+        hipLaunchKernelGGL((attn_f16x3_v2_kernel<32>), dim3((unsigned)n_blocks), dim3(256), 0, st, q,
+                           ld_q, (const uint4*)img, (const int2*)sc, o, ld_o, q_off, kv_off, kv_seg,
+                           n_head, n_seg, n_qblk, sl2);
     else
-        hipLaunchKernelGGL((attn_f16x3_v2_kernel<64>), dim3((unsigned)(n_blocks * ns)), dim3(256), 0, st,
-                           q, ld_q, (const uint4*)img, (const int2*)sc, o, ld_o, q_off, kv_off, kv_seg,
-                           n_head, n_seg, n_qblk, sl2, ns, part, max_q_len);
+        hipLaunchKernelGGL((attn_f16x3_v2_kernel<64>), dim3((unsigned)n_blocks), dim3(256), 0, st, q,
+                           ld_q, (const uint4*)img, (const int2*)sc, o, ld_o, q_off, kv_off, kv_seg,
+                           n_head, n_seg, n_qblk, sl2);
     FGR_CHECK_LAUNCH("attn_f16x3_v2_kernel");
-    if (ns > 1) return attn_split_combine(o, ld_o, q_off, n_seg, max_q_len, n_head, dh, ns, part, st);
     return FGR_OK;
 }

@@ -230,6 +230,13 @@ __device__ __forceinline__ float xg_sum16b(float v) {
 template <int DH> constexpr int bf_units() { return DH * 8 + (DH / 32) * 256; }
 template <int DH> constexpr int bf_unit_v() { return (DH / 32) * 256; }
 
+// V image row swizzle (as attention16.hip v_swz): conflict-free transposed reads at DH 32 and 64
+template <int DH>
+__device__ __forceinline__ int bf_v_swz(int key) {
+    if constexpr (DH == 64) return ((key >> 1) & 3) << 1;
+    else return ((key >> 2) & 1) << 1;
+}
+
 template <int DH>
 __global__ void __launch_bounds__(256)
 attn_kv_image_bf16_kernel(const float* __restrict__ k, int64_t ld_k, const float* __restrict__ v,
@@ -255,7 +262,7 @@ attn_kv_image_bf16_kernel(const float* __restrict__ k, int64_t ld_k, const float
         const __bf16 kt[4] = {(__bf16)kx.x, (__bf16)kx.y, (__bf16)kx.z, (__bf16)kx.w};
         const __bf16 vt[4] = {(__bf16)vx.x, (__bf16)vx.y, (__bf16)vx.z, (__bf16)vx.w};
         const int ks = d0 >> 5, g = (d0 & 31) >> 3, half = (d0 >> 2) & 1;
-        const int vch = (d0 >> 3) ^ (((key >> 2) & 1) << 1);
+        const int vch = (d0 >> 3) ^ bf_v_swz<DH>(key);
         *reinterpret_cast<uint2*>(base + ((ks * 4 + g) * 64 + key) * 16 + half * 8) =
             *reinterpret_cast<const uint2*>(kt);
         *reinterpret_cast<uint2*>(base + bf_unit_v<DH>() * 16 + key * (2 * DH) + vch * 16 +
@@ -276,8 +283,7 @@ __global__ void __launch_bounds__(256, 4)
 attn_bf16_v2_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __restrict__ img,
                     float* __restrict__ o, int64_t ld_o, const int64_t* __restrict__ q_off,
                     const int64_t* __restrict__ kv_off, const int32_t* __restrict__ kv_seg,
-                    int n_head, int n_seg, int n_qblk, float scale_log2, int n_split,
-                    float* __restrict__ part, int max_q_len) {
+                    int n_head, int n_seg, int n_qblk, float scale_log2) {
     constexpr int KD = DH / 32, TD = DH / 16;
     constexpr int UN = bf_units<DH>();
     constexpr int PW = UN / 64 / 4;
@@ -285,9 +291,7 @@ attn_bf16_v2_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __re
     // does not hold the V reads of the current one)
     __shared__ u32x4 lds_b0[UN], lds_b1[UN];
     typedef __attribute__((address_space(3))) char lds_c;
-    // key split as attn_f16x3_v2_kernel (attention16.hip attn_kv_splits)
-    const int nbase = gridDim.x / n_split, split = blockIdx.x / nbase;
-    const int L = blockIdx.x % nbase, xcd = L & 7, j0 = L >> 3;
+    const int L = blockIdx.x, xcd = L & 7, j0 = L >> 3;
     const int pair = (j0 / n_qblk) * 8 + xcd, qblk = j0 % n_qblk;
     if (pair >= n_seg * n_head) return;
     const int seg = pair / n_head, head = pair % n_head;
@@ -298,7 +302,6 @@ attn_bf16_v2_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __re
     const int64_t kb = kv_off[ks];
     const int nk = (int)(kv_off[ks + 1] - kb);
     const int ntile = (nk + 63) / 64;
-    const int t_beg = split * ntile / n_split, t_end = (split + 1) * ntile / n_split;
     const int64_t tile0 = (kb / 64 + ks) * n_head + head;
     const int64_t tile_stride = (int64_t)n_head * UN;
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
@@ -329,7 +332,7 @@ attn_bf16_v2_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __re
 #pragma unroll
     for (int t = 0; t < TD; ++t)
         vaddr[t] = bf_unit_v<DH>() * 16 + (4 * g + qq) * (2 * DH) +
-                   (((2 * t + (pp >> 1)) ^ ((g & 1) << 1)) * 16) + (pp & 1) * 8;
+                   (((2 * t + (pp >> 1)) ^ bf_v_swz<DH>(4 * g + qq)) * 16) + (pp & 1) * 8;
     auto dma = [&](int t, auto buf_tag) {
         constexpr int BUF = decltype(buf_tag)::value;
         const u32x4* src = src_lane + (int64_t)t * tile_stride;
@@ -341,13 +344,13 @@ attn_bf16_v2_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __re
                                              (__attribute__((address_space(3))) void*)(dst + j * 1024),
                                              16, 0, 0);
     };
-    if (t_end > t_beg) dma(t_beg, std::integral_constant<int, 0>{});
+    if (ntile > 0) dma(0, std::integral_constant<int, 0>{});
     auto tile = [&](int tt, auto buf_tag, auto mask_tag) {
         constexpr int BUF = decltype(buf_tag)::value;
         constexpr bool MASK = decltype(mask_tag)::value;
         __builtin_amdgcn_s_waitcnt((7 << 4));                    // vmcnt(0) lgkmcnt(0)
         __builtin_amdgcn_s_barrier();
-        if (tt + 1 < t_end) dma(tt + 1, std::integral_constant<int, 1 - BUF>{});
+        if (tt + 1 < ntile) dma(tt + 1, std::integral_constant<int, 1 - BUF>{});
         lds_c* const bp = (lds_c*)(BUF == 0 ? lds_b0 : lds_b1);
         typedef __attribute__((address_space(3))) u32x4 lds_u4;
         typedef __attribute__((address_space(3))) s16x4 lds_s4;
@@ -419,8 +422,8 @@ attn_bf16_v2_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __re
     };
     using B0 = std::integral_constant<int, 0>;
     using B1 = std::integral_constant<int, 1>;
-    const int nfull = min(nk / 64, t_end);
-    int tt = t_beg;
+    const int nfull = nk / 64;
+    int tt = 0;
     for (; tt + 2 <= nfull; tt += 2) {
         tile(tt, B0{}, std::false_type{});
         tile(tt + 1, B1{}, std::false_type{});
@@ -429,25 +432,9 @@ attn_bf16_v2_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __re
         tile(tt, B0{}, std::false_type{});
         ++tt;
     }
-    if (tt < t_end) {
-        if ((tt - t_beg) & 1) tile(tt, B1{}, std::true_type{});
+    if (tt < ntile) {
+        if (tt & 1) tile(tt, B1{}, std::true_type{});
         else tile(tt, B0{}, std::true_type{});
-    }
-    if (n_split > 1) {                   // unnormalised partial + (row max, sum): combined later
-        const float lsum = xg_sum16b(l_run);
-        if (qrow < qe) {
-            const int64_t slot = (int64_t)(split * n_seg + seg) * max_q_len + (qrow - qb);
-            float* pa = part + slot * (n_head * DH) + head * DH;
-#pragma unroll
-            for (int t = 0; t < TD; ++t)
-                *reinterpret_cast<float4*>(pa + 16 * t + 4 * g) =
-                    make_float4(acc[t][0], acc[t][1], acc[t][2], acc[t][3]);
-            if (g == 0) {
-                float2* ml = reinterpret_cast<float2*>(part + (int64_t)n_split * n_seg * max_q_len * n_head * DH);
-                ml[slot * n_head + head] = make_float2(m_run, lsum);
-            }
-        }
-        return;
     }
     const float inv = 1.0f / xg_sum16b(l_run);
     if (qrow < qe) {
@@ -471,10 +458,6 @@ bool gemm_g5_bf16(char cfg, const float* A, int64_t lda, const void* W, int kste
                   int act, int vec_out, hipStream_t st, int ksplit, float* part);
 bool g5_tile(char cfg, int* bm, int* bn);
 int g5_ksplit(int M, int N, int K, int BM, int BN);
-int attn_kv_splits(int n_seg, int n_head, int max_q_len, int max_kv_len, int slots);
-size_t attn_split_bytes(int n_split, int n_seg, int max_q_len, int n_head, int dh);
-int attn_split_combine(float* o, int64_t ld_o, const int64_t* q_off, int n_seg, int max_q_len,
-                       int n_head, int dh, int n_split, const float* part, hipStream_t st);
 inline bool splitk_shape(int m, int n, int k) {        // as gemm16.hip
     return k >= 1920 && n <= 256 && (int64_t)((m + 63) / 64) * ((n + 63) / 64) <= 160;
 }
@@ -580,18 +563,11 @@ extern "C" int fgr_gemm_bf16_ws(const float* a, int64_t lda, const void* w_img, 
     return gemm_bf16_impl(a, lda, w_img, c, ldc, bias, r, ldr, m, n, k, act, ws, ws_bytes, stream);
 }
 
-// resident blocks of attn_bf16_v2_kernel (__launch_bounds__(256, 4))
-constexpr int kBfAttnSlots = 4 * 256;
-
 extern "C" int fgr_attention_bf16_workspace(int64_t n_kv_rows, int32_t n_kv_seg, int32_t n_head,
-                                            int32_t n_seg, int32_t max_q_len, int32_t max_kv_len,
-                                            int32_t head_dim, size_t* bytes) {
-    FGR_REQUIRE(bytes && n_kv_rows >= 0 && n_kv_seg >= 0 && n_head > 0 && n_seg >= 0 &&
-                    max_q_len >= 0 && max_kv_len >= 0 && (head_dim == 32 || head_dim == 64),
+                                            size_t* bytes) {
+    FGR_REQUIRE(bytes && n_kv_rows >= 0 && n_kv_seg >= 0 && n_head > 0,
                 "fgr_attention_bf16_workspace: bad arguments");
-    const size_t img = (size_t)(n_tiles_bf(n_kv_rows, n_kv_seg) * n_head * bf_units<64>() * 16);
-    const int ns = attn_kv_splits(n_seg, n_head, max_q_len, max_kv_len, kBfAttnSlots);
-    *bytes = img + attn_split_bytes(ns, n_seg, max_q_len, n_head, head_dim);
+    *bytes = (size_t)(n_tiles_bf(n_kv_rows, n_kv_seg) * n_head * bf_units<64>() * 16);
     return FGR_OK;
 }
 
@@ -628,27 +604,19 @@ extern "C" int fgr_attention_bf16(const float* q, int64_t ld_q, const float* k, 
     const int n_qblk = (int)ceil_div(max_q_len, 64);
     const unsigned nb = (unsigned)(ceil_div((int64_t)n_seg * n_head, 8) * 8 * n_qblk);
     const float sl2 = scale * 1.4426950408889634f;
-    // key splits where the grid is small (attn_kv_splits) and the workspace holds the partials
-    int ns = attn_kv_splits(n_seg, n_head, max_q_len, max_kv_len, kBfAttnSlots);
-    if ((size_t)ws_bytes < (size_t)need + attn_split_bytes(ns, n_seg, max_q_len, n_head, dh)) ns = 1;
-    float* part = reinterpret_cast<float*>(static_cast<char*>(workspace) + need);
-    const unsigned nbs = nb * (unsigned)ns;
     if (dh == 32) {
         hipLaunchKernelGGL(attn_kv_image_bf16_kernel<32>, kgrid, dim3(256), 0, st, k, ld_k, v, ld_v,
                            kv_off, n_head, img);
         FGR_CHECK_LAUNCH("attn_kv_image_bf16_kernel");
-        hipLaunchKernelGGL(attn_bf16_v2_kernel<32>, dim3(nbs), dim3(256), 0, st, q, ld_q,
-                           (const uint4*)img, o, ld_o, q_off, kv_off, kv_seg, n_head, n_seg, n_qblk,
-                           sl2, ns, part, max_q_len);
+        hipLaunchKernelGGL(attn_bf16_v2_kernel<32>, dim3(nb), dim3(256), 0, st, q, ld_q,
+                               (const uint4*)img, o, ld_o, q_off, kv_off, kv_seg, n_head, n_seg, n_qblk, sl2);
     } else {
         hipLaunchKernelGGL(attn_kv_image_bf16_kernel<64>, kgrid, dim3(256), 0, st, k, ld_k, v, ld_v,
                            kv_off, n_head, img);
         FGR_CHECK_LAUNCH("attn_kv_image_bf16_kernel");
-        hipLaunchKernelGGL(attn_bf16_v2_kernel<64>, dim3(nbs), dim3(256), 0, st, q, ld_q,
-                           (const uint4*)img, o, ld_o, q_off, kv_off, kv_seg, n_head, n_seg, n_qblk,
-                           sl2, ns, part, max_q_len);
+        hipLaunchKernelGGL(attn_bf16_v2_kernel<64>, dim3(nb), dim3(256), 0, st, q, ld_q,
+                               (const uint4*)img, o, ld_o, q_off, kv_off, kv_seg, n_head, n_seg, n_qblk, sl2);
     }
     FGR_CHECK_LAUNCH("attn_bf16_v2_kernel");
-    if (ns > 1) return attn_split_combine(o, ld_o, q_off, n_seg, max_q_len, n_head, dh, ns, part, st);
     return FGR_OK;
 }

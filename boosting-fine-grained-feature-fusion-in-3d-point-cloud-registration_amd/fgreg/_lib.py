@@ -41,10 +41,10 @@ SIGNATURES = {
     'fgr_add': [_vp, _vp, _i64, _vp, _vp],
     'fgr_attention': [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i32, _i32, _i32,
                       _i32, _f32, _vp],
-    'fgr_attention_f16x3_workspace': [_i64, _i32, _i32, _i32, _i32, _i32, _i32, ctypes.POINTER(_sz)],
+    'fgr_attention_f16x3_workspace': [_i64, _i32, _i32, ctypes.POINTER(_sz)],
     'fgr_attention_f16x3': [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i32, _i32,
                             _i64, _i32, _i32, _i32, _i32, _f32, _vp, _i64, _vp],
-    'fgr_attention_bf16_workspace': [_i64, _i32, _i32, _i32, _i32, _i32, _i32, ctypes.POINTER(_sz)],
+    'fgr_attention_bf16_workspace': [_i64, _i32, _i32, ctypes.POINTER(_sz)],
     'fgr_attention_bf16': [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i32, _i32,
                            _i64, _i32, _i32, _i32, _i32, _f32, _vp, _i64, _vp],
     'fgr_res2net_chain6': [_vp, _i64, _i32, _i32, _vp, _vp, _vp, _i32, _vp, _i64, _vp],

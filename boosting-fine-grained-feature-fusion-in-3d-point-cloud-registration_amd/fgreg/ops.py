@@ -543,8 +543,7 @@ def attention(q, k, v, q_off, kv_off, kv_seg, max_q_len, n_head, out=None,
     if split:
         name = 'fgr_attention_' + ATTN_MODE
         nb = _lib._sz(0)
-        _lib.check(getattr(L, name + '_workspace')(k.shape[0], n_kv_seg, n_head, n_seg,
-                                                   int(max_q_len), int(max_kv_len), dh, nb),
+        _lib.check(getattr(L, name + '_workspace')(k.shape[0], n_kv_seg, n_head, nb),
                    name + '_workspace')
         ws = _workspace(q.device, nb.value)
         _lib.check(getattr(L, name)(

@@ -261,13 +261,9 @@ int fgr_attention(const float* q, int64_t ld_q, const float* k, int64_t ld_k, co
  * powers of two), split into two fp16 terms and the three significant term products
  * accumulate in fp32 (<= ~3 * 2^-22 per product); q/k/v/o 16-B aligned, row strides
  * multiples of 4. Workspace: fgr_attention_f16x3_workspace() bytes (split
- * K/V images + per-tile scale exponents, and -- when the (segment, head, 64-query block) grid
- * would leave most resident-block slots idle, e.g. 3DMatch's two 1060-token clouds -- the
- * partials of a key split: each block takes 1 / n of its segment's key tiles and a combine
- * pass merges them; a smaller workspace runs unsplit), 16-B aligned. */
+ * K/V images + per-tile scale exponents), 16-B aligned. */
 int fgr_attention_f16x3_workspace(int64_t n_kv_rows, int32_t n_kv_seg, int32_t n_head,
-                                  int32_t n_seg, int32_t max_q_len, int32_t max_kv_len,
-                                  int32_t head_dim, size_t* bytes);
+                                  size_t* bytes);
 int fgr_attention_f16x3(const float* q, int64_t ld_q, const float* k, int64_t ld_k,
                         const float* v, int64_t ld_v, float* o, int64_t ld_o,
                         const int64_t* q_off, const int64_t* kv_off, const int32_t* kv_seg,
@@ -279,10 +275,9 @@ int fgr_attention_f16x3(const float* q, int64_t ld_q, const float* k, int64_t ld
  * fgr_attention_f16x3: q * scale * log2(e), K, V and the softmax numerators P rounded to bf16
  * (RNE) where they enter v_mfma_f32_16x16x32_bf16; scores, the online softmax, accumulation
  * and the output stay fp32. Workspace: fgr_attention_bf16_workspace() bytes (bf16 K/V
- * images, and the key-split partials as fgr_attention_f16x3), 16-B aligned. */
+ * images), 16-B aligned. */
 int fgr_attention_bf16_workspace(int64_t n_kv_rows, int32_t n_kv_seg, int32_t n_head,
-                                 int32_t n_seg, int32_t max_q_len, int32_t max_kv_len,
-                                 int32_t head_dim, size_t* bytes);
+                                 size_t* bytes);
 int fgr_attention_bf16(const float* q, int64_t ld_q, const float* k, int64_t ld_k,
                        const float* v, int64_t ld_v, float* o, int64_t ld_o,
                        const int64_t* q_off, const int64_t* kv_off, const int32_t* kv_seg,

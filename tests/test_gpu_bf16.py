@@ -93,10 +93,9 @@ def _attn_ref(q, k, v, qlens, klens, kv_seg, nhead):
     return out
 
 
-@pytest.mark.parametrize('kv_split', ['', '3'])
 @pytest.mark.parametrize('d', [256, 512])
 @pytest.mark.parametrize('scale', [1.0, 4.0, 1e-6, 3e3])
-def test_attention_bf16(gpu, bf16_mode, d, scale, kv_split, monkeypatch):
+def test_attention_bf16(gpu, bf16_mode, d, scale):
     """fgr_attention_bf16 (head_dim 32 / 64): separate key segmentation, partial and 1-key
     tiles, sharp softmax (scale 4: scores ~16), magnitudes far from 1 (bf16 shares fp32's
     exponent range, so no scaling is needed).
@@ -104,10 +103,8 @@ def test_attention_bf16(gpu, bf16_mode, d, scale, kv_split, monkeypatch):
       remaining rounding is P's, ~2^-9 per weight) -- pins where the kernel rounds;
     * vs exact fp64: within 1e-2 where scores are O(1); a sharp softmax amplifies the bf16
       rounding of q and k (absolute score error ~ |s| 2^-8), so scale 4 is only reported;
-    * clearly above the fp32-accurate path's error (the mode really is bf16).
-    kv_split '3': the key-split path (FGR_ATTN_SPLIT) with its combine pass."""
+    * clearly above the fp32-accurate path's error (the mode really is bf16)."""
     import fgreg.ops as ops
-    monkeypatch.setenv('FGR_ATTN_SPLIT', kv_split)
     rng = np.random.default_rng(11)
     nhead = 8
     dh = d // nhead

@@ -188,20 +188,16 @@ def _attention_fp32(q, k, v, q_off, kv_off, kv_seg, max_q_len, n_head):
     return o
 
 
-@pytest.mark.parametrize('kv_split', ['', '3'])
 @pytest.mark.parametrize('d', [256, 512])
 @pytest.mark.parametrize('scale', [1.0, 6.0, 1e-6, 3e3])
-def test_attention_split_is_fp32_accurate(gpu, scale, d, kv_split, monkeypatch):
+def test_attention_split_is_fp32_accurate(gpu, scale, d):
     """The split attention (fgr_attention_f16x3, dh = 32 and 64) against a float64
     reference: error at fp32 level (<= 1e-5 normwise) and no worse than a few times the
     fp32-MFMA kernel's own error; separate key segmentation (kv lengths != q lengths,
     max_kv_len > max_q_len), partial and 1-key tiles, sharp softmax at scale 6, inputs far
     outside fp16's range (1e-6: subnormal in fp16 unscaled; 3e3: products past 65504).
-    kv_split '3': every block takes a third of its segment's key tiles and the combine pass
-    merges the partials (FGR_ATTN_SPLIT; the 1-key segment leaves two splits empty).
     """
     import fgreg.ops as ops
-    monkeypatch.setenv('FGR_ATTN_SPLIT', kv_split)
     rng = np.random.default_rng(7)
     nhead = 8
     qlens = [300, 1, 64, 129]

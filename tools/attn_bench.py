@@ -1,8 +1,6 @@
 """Attention microbenchmark (development tool, GPU): ops.attention on the forward's packed
 segment shapes, device time from HIP-graph replays, error vs an fp64 reference.
-usage: python tools/attn_bench.py [splits] [bf16]
-  splits: sweep FGR_ATTN_SPLIT (the key split) over 1, 2, 3, 4 and the launcher's own choice
-  bf16:   the bf16 attention (ops.ATTN_MODE = 'bf16') instead of f16x3"""
+usage: python tools/attn_bench.py [bf16]      (bf16: ops.ATTN_MODE = 'bf16' instead of f16x3)"""
 import os
 import sys
 
@@ -17,8 +15,7 @@ CASES = [('modelnet self', [596] * 16, 256, 8), ('3dmatch self', [1060, 1060], 5
          ('3dmatch dh32', [1060, 1060], 256, 8), ('3dlomatch', [935, 936], 512, 8)]
 
 
-def run_case(ops, dev, g, name, lens, d, nh, sp):
-    os.environ['FGR_ATTN_SPLIT'] = sp
+def run_case(ops, dev, g, name, lens, d, nh):
     n = sum(lens)
     qkv = torch.randn(n, 3 * d, device=dev, generator=g)
     q, k, v = qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:]
@@ -34,7 +31,7 @@ def run_case(ops, dev, g, name, lens, d, nh, sp):
     ref = ref.transpose(0, 1).reshape(L0, d)
     err = float((out[:L0].double() - ref).abs().max() / ref.abs().max())
     flop = 4 * sum(l * l for l in lens) * d
-    print(f'{name:14s} {ops.ATTN_MODE} split={sp or "auto":4s} n={n:6d} d={d} heads={nh}: '
+    print(f'{name:14s} {ops.ATTN_MODE} n={n:6d} d={d} heads={nh}: '
           f'{us:7.1f} us  {flop / us / 1e6:6.1f} TF(fp32-eq)  err {err:.1e}', flush=True)
 
 
@@ -42,13 +39,10 @@ def main():
     from fgreg import ops
     if 'bf16' in sys.argv[1:]:
         ops.ATTN_MODE = 'bf16'
-    splits = ['1', '2', '3', '4', ''] if 'splits' in sys.argv[1:] else ['']
     dev = torch.device('cuda:0')
     g = torch.Generator(device=dev).manual_seed(0)
     for name, lens, d, nh in CASES:
-        for sp in splits:
-            run_case(ops, dev, g, name, lens, d, nh, sp)
-    os.environ['FGR_ATTN_SPLIT'] = ''
+        run_case(ops, dev, g, name, lens, d, nh)
 
 
 if __name__ == '__main__':
