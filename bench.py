@@ -479,6 +479,11 @@ def cpu_baseline(cfg, model, src, tgt, budget_s, tail_inputs=None, workload='mod
         it += 1
     res = {'value': n_pairs / t_tot, 'unit': 'pairs/s', 'cores': threads, 'kind': 'port',
            'cpu_model': _cpu_model(),
+           # the GPU box leases a CPU share per GPU: torch's thread count follows the lease's
+           # OMP_NUM_THREADS (16 per GPU), while the affinity mask / os.cpu_count() show more
+           'cores_note': {'torch_threads': threads, 'omp_num_threads': os.environ.get('OMP_NUM_THREADS'),
+                          'affinity_cpus': len(os.sched_getaffinity(0)), 'machine_cpus': os.cpu_count(),
+                          'basis': 'the per-GPU CPU share of the lease (OMP_NUM_THREADS)'},
            'sample': f'{n_pairs} pairs (B=1 forwards) of the same workload, '
                      f'{t_tot:.1f} s, torch CPU fp32 with {threads} threads'}
     if len(src) > 1:
