@@ -40,9 +40,10 @@ bool g5_tile(char cfg, int* bm, int* bn);
 int g5_ksplit(int M, int N, int K, int BM, int BN);
 char bf16_tile(int m, int n, int k);
 int bf16_ksplit(char cfg, int m, int n, int k);
+struct RsLn { const float* g; const float* b; const float* add; int64_t ld_add; float eps; };
 bool gemm_rs_f16x3(const float* A, int64_t lda, const void* W, int ksteps, const float* wsc,
                    float* C, int64_t ldc, const float* bias, const float* R, int64_t ldr, int M,
-                   int N, int K, int act, hipStream_t st);
+                   int N, int K, int act, hipStream_t st, const RsLn* ln = nullptr);
 // few 64 x 64 tiles, narrow output, long contraction: split-K pays (measured)
 inline bool splitk_shape(int m, int n, int k) {
     return k >= 1920 && n <= 256 && (int64_t)((m + 63) / 64) * ((n + 63) / 64) <= 160;
@@ -1052,11 +1053,13 @@ char h3_tile(int m, int n, int k) {
     const char* force = getenv("FGR_GEMM16_TILE");
     if (force && force[0]) return force[0];
     // short contractions over many rows: the row-stationary kernel (gemm_rs.hip) where it
-    // measured faster than the k-looped choice (profiles/r03_gemm_rs_sweep.txt: K <= 128 with
-    // N >= 224 1.08-1.31x, 57264 x 256 x 256 1.14x; elsewhere equal or slower -- the loop of
-    // both structures sits at ~35 % of the MFMA pipe). FGR_GEMM_RS=0 disables.
+    // measured faster than the k-looped choice (profiles/r03_gemm_rs_sweep3.txt: 9544 x 1792 x
+    // 256 1.37x, x 1024 x 256 1.17x, x 768 x 256 1.10x, 57264 x 256 x 256 1.46x, K <= 128 with
+    // N >= 224 1.0-1.41x; narrow outputs, short row counts and N = 256-512 at ~10k rows stay on
+    // the k-looped kernels). FGR_GEMM_RS=0 disables.
     static const bool rs_on = [] { const char* e = getenv("FGR_GEMM_RS"); return !(e && e[0] == '0'); }();
-    if (rs_on && k % 8 == 0 && ((k <= 128 && n >= 224 && m >= 8000) || (k <= 256 && n >= 128 && m >= 50000)))
+    if (rs_on && k % 8 == 0 && k <= 256 && n % 16 == 0 && m >= 8000 &&
+        (n >= 640 || (k <= 128 && n >= 224) || (m >= 25000 && n >= 224)))
         return 'z';
     return h3_tile_kloop(m, n, k);
 }
@@ -1206,4 +1209,40 @@ extern "C" int fgr_gemm_f16x3_ws(const float* a, int64_t lda, const void* w_img,
                                  int32_t m, int32_t n, int32_t k, int32_t act, void* ws,
                                  size_t ws_bytes, void* stream) {
     return gemm_f16x3_impl(a, lda, w_img, c, ldc, bias, r, ldr, m, n, k, act, ws, ws_bytes, stream);
+}
+
+// LayerNorm -> (+ add) -> Linear in one launch (the row-stationary kernel's LN prologue,
+// gemm_rs.hip): supported where the dispatcher picks that kernel for (m, n, k).
+extern "C" int fgr_gemm_f16x3_ln_supported(int32_t m, int32_t n, int32_t k) {
+    return (m > 0 && n > 0 && k > 0 && h3_tile(m, n, k) == 'z') ? 1 : 0;
+}
+
+extern "C" int fgr_gemm_f16x3_ln(const float* x, int64_t ldx, const float* gamma, const float* beta,
+                                 float eps, const float* add, int64_t ld_add, const void* w_img,
+                                 float* c, int64_t ldc, const float* bias, int32_t m, int32_t n,
+                                 int32_t k, int32_t act, void* stream) {
+    FGR_REQUIRE(x && gamma && beta && w_img && c && m >= 0 && n > 0 && k > 0 && ldx >= k &&
+                    ldc >= n && (!add || ld_add >= k) && eps >= 0.f &&
+                    (act == FGR_ACT_NONE || act == FGR_ACT_RELU),
+                "fgr_gemm_f16x3_ln: bad arguments (m %d n %d k %d act %d)", m, n, k, act);
+    FGR_REQUIRE(m == 0 || fgr_gemm_f16x3_ln_supported(m, n, k),
+                "fgr_gemm_f16x3_ln: shape %d x %d x %d not supported (fgr_gemm_f16x3_ln_supported)",
+                m, n, k);
+    const uintptr_t al = reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(gamma) |
+                         reinterpret_cast<uintptr_t>(beta) | reinterpret_cast<uintptr_t>(add) |
+                         reinterpret_cast<uintptr_t>(w_img) | reinterpret_cast<uintptr_t>(c) |
+                         reinterpret_cast<uintptr_t>(bias);
+    FGR_REQUIRE((al & 15) == 0 && ldx % 4 == 0 && ldc % 4 == 0 && (!add || ld_add % 4 == 0),
+                "fgr_gemm_f16x3_ln: operands must be 16-B aligned with row strides %% 4 == 0");
+    if (m == 0) return FGR_OK;
+    const float* wsc = reinterpret_cast<const float*>(static_cast<const char*>(w_img) +
+                                                      image_bytes_h3(n, k));
+    hipStream_t st = as_stream(stream);
+    TimedCall timed_(st);
+    const RsLn ln{gamma, beta, add, ld_add, eps};
+    FGR_REQUIRE(gemm_rs_f16x3(x, ldx, w_img, ksteps_h3(k), wsc, c, ldc, bias, nullptr, 0, m, n, k,
+                              act, st, &ln),
+                "fgr_gemm_f16x3_ln: row-stationary kernel rejected %d x %d x %d", m, n, k);
+    FGR_CHECK_LAUNCH("gemm_rs_ln");
+    return FGR_OK;
 }

@@ -18,6 +18,14 @@
 // per element (2^-24 / 2 of the subnormal spacing over the 2^14 scale floor) -- relative to
 // the dot product's own fp32 rounding (K 2^-24 sum|a w|) negligible.
 //
+// LayerNorm prologue (LN = true; fgr_gemm_f16x3_ln): A = LayerNorm(X) * gamma + beta (+ add),
+// i.e. the pre-norm transformer's norm -> with_pos_embed -> Linear (transformers.py:193-196,
+// :213-221, :231-232) in one launch. A wave holds whole rows (K = d) in registers anyway, so
+// the row mean and the centred variance come from its own values (two passes over registers,
+// the lane sums over the four k-groups by permlane swaps), gamma / beta are staged once per
+// block in LDS, and the normalised row is split as above: the LayerNorm output never goes to
+// memory and its launch disappears.
+//
 // Swapped orientation (gemm16.hip): W fragments are the MFMA A operand, activation fragments
 // the B operand, so a lane's 4 accumulators are 4 consecutive output columns of ONE row.
 // 16x16x32 f16 lane maps (lane l, g = l >> 4, c = l & 15): A[i = c][k = 8g + e],
@@ -42,6 +50,9 @@ struct RsArgs {
     const float* R; int64_t ldr;
     int M, N, K, act;
     int nc;                           // W panels (16 columns) per block
+    const float* ln_g; const float* ln_b;   // LN prologue: gamma, beta (K)
+    const float* ln_add; int64_t ld_add;    //   optional row add (pos) after the affine
+    float eps;
 };
 
 // s_waitcnt vmcnt(n) lgkmcnt(0) -- gfx9 encoding
@@ -57,14 +68,11 @@ __device__ __forceinline__ float xg_max_rs(float v) {     // max over lanes c, c
     auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
     return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
 }
-
-__device__ __forceinline__ float finish_rs(float y, float b, float r, int act) {
-    if (act == FGR_ACT_RELU_RES_LEAKY) {
-        const float t = fmaxf(y + b, 0.f) + r;
-        return t > 0.f ? t : 0.1f * t;
-    }
-    const float t = y + b + r;
-    return act == FGR_ACT_RELU ? fmaxf(t, 0.f) : t;
+__device__ __forceinline__ float xg_sum_rs(float v) {     // sum over lanes c, c^16, c^32, c^48
+    auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+    auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 
 // vmcnt(n) lgkmcnt(0) for a wave-uniform runtime n <= 15 (s_waitcnt takes an immediate)
@@ -84,21 +92,31 @@ __device__ __forceinline__ void wait_vm_lgkm0_dyn(int n) {
 constexpr int kRsNb = 3;           // W panels in the LDS ring (two in flight while one computes)
 constexpr int kRsMaxNc = 64;       // panels per block (the per-block column scales / bias in LDS)
 
-// RT row tiles of 16 per wave (block = 4 waves = 64 RT rows), KS k32-steps (the image's
-// ksteps: K <= 32 KS), residual present or not. C / R / bias 16-B aligned (the dispatcher
-// checks), N padded to 16 in the image and wsc.
-// Per panel q (program order): wait for its DMA, barrier, residual loads for panel q + 1,
-// DMA of panel q + 2 into the buffer panel q - 1 used, MFMAs, epilogue stores. vm operations
-// complete in issue order, so "panel q's DMA landed" = at most (the ops issued after it)
-// outstanding, counted from below (stores >= one per row tile with a valid row, residual
-// loads >= 0): a stronger wait whenever more were issued.
-template <int RT, int KS, bool RES>
+// the epilogue of one output, the activation fixed at compile time
+template <int ACT, bool RES>
+__device__ __forceinline__ float finish_ct(float y, float b, float r) {
+    if constexpr (ACT == FGR_ACT_RELU_RES_LEAKY) {
+        float t = fmaxf(y + b, 0.f);
+        if constexpr (RES) t += r;
+        return t > 0.f ? t : 0.1f * t;
+    } else {
+        float t = y + b;
+        if constexpr (RES) t += r;
+        if constexpr (ACT == FGR_ACT_RELU) t = fmaxf(t, 0.f);
+        return t;
+    }
+}
+
+// LNM: 0 plain, 1 LayerNorm prologue, 2 LayerNorm prologue + row add
+template <int RT, int KS, bool RES, int ACT, int LNM>
 __global__ void __launch_bounds__(256) gemm_rs_kernel(RsArgs p) {
+    constexpr bool LN = LNM > 0;
     constexpr int PANEL_U = KS * 128;                  // 16-B units per W panel
     constexpr int PW = PANEL_U / 256;                  // DMA pieces (1 KiB) per wave per panel
     static_assert(PANEL_U % 256 == 0, "KS even");
     __shared__ u32x4 ring[kRsNb * PANEL_U];
     __shared__ float4 colw[kRsMaxNc * 4], colb[kRsMaxNc * 4];   // per (panel, g): wsc, bias
+    __shared__ float4 lng[LN ? KS * 8 : 1], lnb[LN ? KS * 8 : 1];  // LN gamma / beta (K / 4)
 
     const int nbm = (p.M + 64 * RT - 1) / (64 * RT);
     const int npanel = (p.N + 15) / 16;
@@ -142,12 +160,80 @@ __global__ void __launch_bounds__(256) gemm_rs_kernel(RsArgs p) {
         for (int s = 0; s < KS; ++s) {
             const int k = 32 * s + 8 * g;
             float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0;
-            if (k < p.K) {
+            if constexpr (LN) {
+                // LN: unconditional loads (a chunk past K re-reads the last one and is zeroed
+                // below), so all 2 * KS are in flight before the row statistics. (Measured
+                // slower for the plain kernel, which keeps the guarded loads:
+                // profiles/r03_gemm_rs_sweep_ln.txt.)
+                const int kl = min(k, p.K - 8);
+                a0 = *reinterpret_cast<const float4*>(ar + kl);
+                a1 = *reinterpret_cast<const float4*>(ar + kl + 4);
+            } else if (k < p.K) {
                 a0 = *reinterpret_cast<const float4*>(ar + k);
                 a1 = *reinterpret_cast<const float4*>(ar + k + 4);
             }
             x[s][0] = a0.x; x[s][1] = a0.y; x[s][2] = a0.z; x[s][3] = a0.w;
             x[s][4] = a1.x; x[s][5] = a1.y; x[s][6] = a1.z; x[s][7] = a1.w;
+        }
+        if constexpr (LN) {
+#pragma unroll
+            for (int s = 0; s < KS; ++s)
+                if (32 * s + 8 * g >= p.K)
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) x[s][e] = 0.f;
+        }
+        if constexpr (LN) {
+            if (i == 0) {          // gamma / beta -> LDS (K <= 32 * KS), the first rows in flight
+                float4 gv = make_float4(0.f, 0.f, 0.f, 0.f), bv = gv;
+                if (tid < p.K / 4) {
+                    gv = reinterpret_cast<const float4*>(p.ln_g)[tid];
+                    bv = reinterpret_cast<const float4*>(p.ln_b)[tid];
+                }
+                if (tid < KS * 8) { lng[tid] = gv; lnb[tid] = bv; }
+                __syncthreads();
+            }
+            // row mean, then the centred variance (as the LayerNorm kernels: norm.hip), from
+            // the row's K values held by lanes c, c + 16, c + 32, c + 48
+            float sm = 0.f;
+#pragma unroll
+            for (int s = 0; s < KS; ++s)
+                sm += ((x[s][0] + x[s][1]) + (x[s][2] + x[s][3])) +
+                      ((x[s][4] + x[s][5]) + (x[s][6] + x[s][7]));
+            const float mean = xg_sum_rs(sm) / (float)p.K;
+            float sq = 0.f;
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+                const bool in = 32 * s + 8 * g < p.K;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const float d = in ? x[s][e] - mean : 0.f;
+                    sq += d * d;
+                }
+            }
+            const float rstd = 1.0f / sqrtf(xg_sum_rs(sq) / (float)p.K + p.eps);
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+                // no branches around the loads (all in flight); chunks past K zeroed below
+                const int kl = min(32 * s + 8 * g, p.K - 8);
+                const float4 g0 = lng[kl / 4], g1 = lng[kl / 4 + 1];
+                const float4 b0 = lnb[kl / 4], b1 = lnb[kl / 4 + 1];
+                float4 d0 = make_float4(0.f, 0.f, 0.f, 0.f), d1 = d0;
+                if constexpr (LNM == 2) {
+                    const float* dr = p.ln_add + row * p.ld_add + kl;
+                    d0 = *reinterpret_cast<const float4*>(dr);
+                    d1 = *reinterpret_cast<const float4*>(dr + 4);
+                }
+                const float gg[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+                const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+                const float dd[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+#pragma unroll
+                for (int e = 0; e < 8; ++e) x[s][e] = (x[s][e] - mean) * rstd * gg[e] + bb[e] + dd[e];
+            }
+#pragma unroll
+            for (int s = 0; s < KS; ++s)
+                if (32 * s + 8 * g >= p.K)
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) x[s][e] = 0.f;
         }
         float mx = 0.f;
 #pragma unroll
@@ -188,14 +274,7 @@ __global__ void __launch_bounds__(256) gemm_rs_kernel(RsArgs p) {
 #pragma unroll
         for (int i = 0; i < RT; ++i) {
             const int64_t row = min(mw + 16 * i + c, p.M - 1);
-            const float* src = p.R + row * p.ldr + n;
-            if (n + 3 < p.N) {
-                rv[i] = *reinterpret_cast<const float4*>(src);
-            } else {
-                float e[4] = {0.f, 0.f, 0.f, 0.f};
-                for (int j = 0; j < 4 && n + j < p.N; ++j) e[j] = src[j];
-                rv[i] = make_float4(e[0], e[1], e[2], e[3]);
-            }
+            rv[i] = *reinterpret_cast<const float4*>(p.R + row * p.ldr + n);
         }
     };
     float4 rcur[RT], rnext[RT];
@@ -233,26 +312,18 @@ __global__ void __launch_bounds__(256) gemm_rs_kernel(RsArgs p) {
         // epilogue: lane holds C[row = mw + 16i + c][n .. n + 3]
         const int n = (p0 + q) * 16 + 4 * g;
         const float4 ws = colw[q * 4 + g], bv = colb[q * 4 + g];
-        if (n < p.N) {
+        {                                                  // N % 16 == 0: every panel in range
 #pragma unroll
             for (int i = 0; i < RT; ++i) {
                 const int64_t row = mw + 16 * i + c;
-                if (row >= p.M) continue;
+                const float s0 = rs[i] * ws.x, s1 = rs[i] * ws.y, s2 = rs[i] * ws.z, s3 = rs[i] * ws.w;
                 float4 r4 = make_float4(0.f, 0.f, 0.f, 0.f);
                 if constexpr (RES) r4 = rcur[i];
-                const float y0 = acc[i][0] * rs[i] * ws.x, y1 = acc[i][1] * rs[i] * ws.y;
-                const float y2 = acc[i][2] * rs[i] * ws.z, y3 = acc[i][3] * rs[i] * ws.w;
-                float* crow = p.C + row * p.ldc;
-                if (n + 3 < p.N) {
-                    *reinterpret_cast<float4*>(crow + n) =
-                        make_float4(finish_rs(y0, bv.x, r4.x, p.act), finish_rs(y1, bv.y, r4.y, p.act),
-                                    finish_rs(y2, bv.z, r4.z, p.act), finish_rs(y3, bv.w, r4.w, p.act));
-                } else {                                   // ragged last panel (N % 4 != 0)
-                    const float yy[4] = {y0, y1, y2, y3};
-                    const float bb[4] = {bv.x, bv.y, bv.z, bv.w}, rr[4] = {r4.x, r4.y, r4.z, r4.w};
-                    for (int e = 0; e < 4 && n + e < p.N; ++e)
-                        crow[n + e] = finish_rs(yy[e], bb[e], rr[e], p.act);
-                }
+                const float4 y = make_float4(finish_ct<ACT, RES>(acc[i][0] * s0, bv.x, r4.x),
+                                             finish_ct<ACT, RES>(acc[i][1] * s1, bv.y, r4.y),
+                                             finish_ct<ACT, RES>(acc[i][2] * s2, bv.z, r4.z),
+                                             finish_ct<ACT, RES>(acc[i][3] * s3, bv.w, r4.w));
+                if (row < p.M) *reinterpret_cast<float4*>(p.C + row * p.ldc + n) = y;
             }
         }
         if constexpr (RES)
@@ -261,41 +332,78 @@ __global__ void __launch_bounds__(256) gemm_rs_kernel(RsArgs p) {
     }
 }
 
+template <int RT, int KS, int ACT>
+void launch_rs_act(const RsArgs& a, unsigned blocks, hipStream_t st) {
+    // LN prologue: one row tile per wave (at two, the row + add registers of the prologue
+    // exceed the 256 VGPRs of two waves per SIMD and spill), no residual (checked by the caller)
+    if constexpr (RT == 1 && ACT != FGR_ACT_RELU_RES_LEAKY) {
+        if (a.ln_g && a.ln_add) {
+            hipLaunchKernelGGL((gemm_rs_kernel<RT, KS, false, ACT, 2>), dim3(blocks), dim3(256), 0, st, a);
+            return;
+        }
+        if (a.ln_g) {
+            hipLaunchKernelGGL((gemm_rs_kernel<RT, KS, false, ACT, 1>), dim3(blocks), dim3(256), 0, st, a);
+            return;
+        }
+    }
+    if (a.R)
+        hipLaunchKernelGGL((gemm_rs_kernel<RT, KS, true, ACT, 0>), dim3(blocks), dim3(256), 0, st, a);
+    else
+        hipLaunchKernelGGL((gemm_rs_kernel<RT, KS, false, ACT, 0>), dim3(blocks), dim3(256), 0, st, a);
+}
+
 template <int RT, int KS>
 bool launch_rs_k(const RsArgs& a, unsigned blocks, hipStream_t st) {
-    if (a.R)
-        hipLaunchKernelGGL((gemm_rs_kernel<RT, KS, true>), dim3(blocks), dim3(256), 0, st, a);
-    else
-        hipLaunchKernelGGL((gemm_rs_kernel<RT, KS, false>), dim3(blocks), dim3(256), 0, st, a);
-    return true;
+    switch (a.act) {
+        case FGR_ACT_RELU: launch_rs_act<RT, KS, FGR_ACT_RELU>(a, blocks, st); return true;
+        case FGR_ACT_RELU_RES_LEAKY: launch_rs_act<RT, KS, FGR_ACT_RELU_RES_LEAKY>(a, blocks, st); return true;
+        default: launch_rs_act<RT, KS, FGR_ACT_NONE>(a, blocks, st); return true;
+    }
 }
 
 }  // namespace
 
-// The rs kernel applies to K <= 256, K % 8 == 0 with 16-B aligned A / C / R / bias rows
-// (checked by the caller). ksteps = the image's k32-steps (even, <= 8).
+// The rs kernel applies to K <= 256, K % 8 == 0, N % 16 == 0 with 16-B aligned A / C / R / bias rows
+// (checked by the caller). ksteps = the image's k32-steps (even, <= 8). `ln` (optional, no R):
+// the LayerNorm prologue's gamma, beta, add (16-B aligned rows), ld_add and eps.
+struct RsLn { const float* g; const float* b; const float* add; int64_t ld_add; float eps; };
 bool gemm_rs_f16x3(const float* A, int64_t lda, const void* W, int ksteps, const float* wsc,
                    float* C, int64_t ldc, const float* bias, const float* R, int64_t ldr, int M,
-                   int N, int K, int act, hipStream_t st) {
-    if (K % 8 != 0 || ksteps > 8 || ksteps % 2 != 0) return false;
+                   int N, int K, int act, hipStream_t st, const RsLn* ln) {
+    if (K % 8 != 0 || N % 16 != 0 || ksteps > 8 || ksteps % 2 != 0) return false;
+    if (ln && R) return false;
     // row tiles per wave: 2 (W fragments reused twice) unless that leaves too few blocks
     const char* rte = getenv("FGR_RS_RT");
     int RT = (rte && rte[0]) ? atoi(rte) : 2;
     if (RT != 1 && RT != 2) RT = 2;
+    if (ln) RT = 1;
     const int npanel = (N + 15) / 16;
     const int nbm = (M + 64 * RT - 1) / (64 * RT);
-    // panels per block: 8 (the measured best or within 5 % of it on every dispatched shape,
-    // profiles/r03_gemm_rs_sweep.txt); FGR_RS_NC overrides, 0 = ~3 blocks per CU
+    // panels per block: as few column groups as fill the resident-block slots once (a second,
+    // partial round of blocks costs a whole block time; every group re-reads and re-splits its
+    // rows): slots = 256 CUs x blocks per CU (2 at K > 128, 188 VGPRs; 4 below).
+    // FGR_RS_NC overrides (0: ~3 blocks per CU regardless of occupancy)
     const char* nce = getenv("FGR_RS_NC");
-    int nc = (nce && nce[0]) ? atoi(nce) : 8;
-    if (nc <= 0) {
-        const int64_t target = 768;
-        nc = (int)std::max<int64_t>(1, std::min<int64_t>(npanel, ((int64_t)nbm * npanel + target - 1) / target));
+    int nc;
+    if (nce && nce[0]) {
+        nc = atoi(nce);
+        if (nc <= 0) {
+            const int64_t target = 768;
+            nc = (int)std::max<int64_t>(1, std::min<int64_t>(npanel, ((int64_t)nbm * npanel + target - 1) / target));
+        }
+    } else {
+        // (the LN prologue at RT 1: 256 / 190 VGPRs at ksteps 8 / 6 -> 2 blocks per CU, 4 below)
+        const int slots = ln ? 256 * (ksteps > 4 ? 2 : 4)
+                             : 256 * (ksteps > 4 ? 2 : 4) * (RT == 1 ? 2 : 1);
+        const int ngrp = std::max(1, slots / std::max(nbm, 1));
+        nc = (npanel + ngrp - 1) / ngrp;
     }
     nc = std::min(std::min(nc, npanel), kRsMaxNc);
     const int ngrp = (npanel + nc - 1) / nc;
     const unsigned blocks = (unsigned)((int64_t)nbm * ngrp);
-    RsArgs a{A, lda, (const u32x4*)W, wsc, C, ldc, bias, R, ldr, M, N, K, act, nc};
+    RsArgs a{A, lda, (const u32x4*)W, wsc, C, ldc, bias, R, ldr, M, N, K, act, nc,
+             ln ? ln->g : nullptr, ln ? ln->b : nullptr, ln ? ln->add : nullptr,
+             ln ? ln->ld_add : 0, ln ? ln->eps : 0.f};
 #define RS_CASE(rt, ks) \
     if (RT == rt && ksteps == ks) return launch_rs_k<rt, ks>(a, blocks, st);
     RS_CASE(2, 2) RS_CASE(2, 4) RS_CASE(2, 6) RS_CASE(2, 8)

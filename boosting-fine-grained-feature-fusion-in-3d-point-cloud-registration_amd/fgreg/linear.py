@@ -12,6 +12,8 @@ Weight images are built once and cached against the fp32 tensor's identity, data
 and version (a checkpoint load, .to() or in-place update invalidates the cache). There is no
 library / PyTorch GEMM fallback: a shape the kernels reject raises.
 """
+import os
+
 import torch
 
 from . import _lib
@@ -143,5 +145,48 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act=ACT_NONE, residual=N
         _ptr(x), x.stride(0), _ptr(sw.img), _ptr(out), out.stride(0), _ptr(bias),
         _ptr(residual), residual.stride(0) if residual is not None else 0, m, n, k, act,
         _ptr(ws), nb.value, _stream()), 'fgr_gemm_' + MODE)
+    _end('gemm', t0, 2 * m * n * k)
+    return out
+
+
+# fgr_gemm_f16x3_ln where supported (False, or FGR_LN_FUSE=0: layernorm, then linear)
+LN_FUSE = os.environ.get('FGR_LN_FUSE', '1') != '0'
+
+
+def ln_fusable(m, n, k) -> bool:
+    """True if LayerNorm -> Linear of an (m, k) input to n outputs runs as one launch
+    (fgr_gemm_f16x3_ln: f16x3 mode, the row-stationary kernel's shapes)."""
+    return (LN_FUSE and MODE == 'f16x3'
+            and bool(_lib.load().fgr_gemm_f16x3_ln_supported(m, n, k)))
+
+
+def linear_ln(x: torch.Tensor, norm, w: torch.Tensor, bias=None, act=ACT_NONE, add=None,
+              out=None) -> torch.Tensor:
+    """act((LayerNorm(x) (+ add)) @ W^T + bias) with ``norm`` an nn.LayerNorm over x's
+    features: the pre-norm sub-layer inputs of transformers.py:193-196, :213-221 (add = the
+    positional embedding) and :231-232. One launch (fgr_gemm_f16x3_ln) where ln_fusable,
+    else ops.layernorm then linear() -- the same arithmetic in two launches."""
+    m, k = x.shape
+    n = w.shape[0]
+    assert w.shape[1] == k and norm.weight.numel() == k
+    if not ln_fusable(m, n, k):
+        return linear(ops.layernorm(x, norm.weight, norm.bias, norm.eps, add=add), w, bias,
+                      act=act, out=out)
+    _dev(x, w)
+    x = x.contiguous()
+    if add is not None:
+        assert add.shape == x.shape
+        add = add.contiguous()
+    gamma, beta = norm.weight.contiguous(), norm.bias.contiguous()
+    if bias is not None:
+        assert bias.numel() == n and bias.is_contiguous()
+    sw = weight_image(w, mode='f16x3')
+    if out is None:
+        out = torch.empty((m, n), dtype=torch.float32, device=x.device)
+    t0 = _begin('gemm', (m, n, k))
+    _lib.check(_lib.load().fgr_gemm_f16x3_ln(
+        _ptr(x), x.stride(0), _ptr(gamma), _ptr(beta), float(norm.eps), _ptr(add),
+        add.stride(0) if add is not None else 0, _ptr(sw.img), _ptr(out), out.stride(0),
+        _ptr(bias), m, n, k, act, _stream()), 'fgr_gemm_f16x3_ln')
     _end('gemm', t0, 2 * m * n * k)
     return out

@@ -24,7 +24,7 @@ import torch
 import torch.nn as nn
 
 from . import ops
-from .linear import linear
+from .linear import linear, linear_ln, ln_fusable
 
 
 class Segments:
@@ -83,9 +83,17 @@ class TransformerCrossEncoderLayer(nn.Module):
         self.sa_val_has_pos_emb = sa_val_has_pos_emb
         self.ca_val_has_pos_emb = ca_val_has_pos_emb
 
-    def _attend(self, mha, h_pos, h_nopos, val_has_pos, seg, kv_seg):
-        d = h_pos.shape[1]
+    def _attend(self, mha, h_pos, h_nopos, val_has_pos, seg, kv_seg, ln=None):
+        """``ln`` = (x, norm, pos): h_pos = norm(x) + pos is formed inside the in_proj GEMM
+        (linear_ln; val_has_pos only)."""
         W, b = mha.in_proj_weight, mha.in_proj_bias
+        if ln is not None:
+            x, norm, pos = ln
+            d = x.shape[1]
+            qkv = linear_ln(x, norm, W, b, add=pos)                   # (N, 3d): [q | k | v]
+            q, k, v = qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:]
+            return ops.attention(q, k, v, seg.off, seg.off, kv_seg, seg.max_len, self.nhead)
+        d = h_pos.shape[1]
         if val_has_pos:
             qkv = linear(h_pos, W, b)                                 # (N, 3d): [q | k | v]
             q, k, v = qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:]
@@ -105,23 +113,35 @@ class TransformerCrossEncoderLayer(nn.Module):
         defer one, and the returned pending bias is None."""
         if not self.normalize_before:
             return self._forward_post(x, pos, seg, pending_bias), None
+        n, d = x.shape
+        # LayerNorm (+ pos) folded into the next GEMM where that GEMM supports it
+        # (linear_ln): the norm output is never written
+        fuse_in = ln_fusable(n, 3 * d, d)
         # self-attention, shared weights for src and tgt (:193-210)
-        h = ops.layernorm(x, self.norm1.weight, self.norm1.bias, self.norm1.eps, add=pos,
-                          pre_bias=pending_bias)
-        h0 = None if self.sa_val_has_pos_emb else ops.layernorm(x, self.norm1.weight,
-                                                                 self.norm1.bias, self.norm1.eps)
-        o = self._attend(self.self_attn, h, h0, self.sa_val_has_pos_emb, seg, seg.self_seg)
+        if fuse_in and self.sa_val_has_pos_emb and pending_bias is None:
+            o = self._attend(self.self_attn, None, None, True, seg, seg.self_seg,
+                             ln=(x, self.norm1, pos))
+        else:
+            h = ops.layernorm(x, self.norm1.weight, self.norm1.bias, self.norm1.eps, add=pos,
+                              pre_bias=pending_bias)
+            h0 = None if self.sa_val_has_pos_emb else ops.layernorm(
+                x, self.norm1.weight, self.norm1.bias, self.norm1.eps)
+            o = self._attend(self.self_attn, h, h0, self.sa_val_has_pos_emb, seg, seg.self_seg)
         x = linear(o, self.self_attn.out_proj.weight, self.self_attn.out_proj.bias, residual=x)
         # cross-attention, both directions at once (:212-229)
-        h = ops.layernorm(x, self.norm2.weight, self.norm2.bias, self.norm2.eps, add=pos)
-        h0 = None if self.ca_val_has_pos_emb else ops.layernorm(x, self.norm2.weight,
-                                                                 self.norm2.bias, self.norm2.eps)
-        o = self._attend(self.multihead_attn, h, h0, self.ca_val_has_pos_emb, seg, seg.cross_seg)
+        if fuse_in and self.ca_val_has_pos_emb:
+            o = self._attend(self.multihead_attn, None, None, True, seg, seg.cross_seg,
+                             ln=(x, self.norm2, pos))
+        else:
+            h = ops.layernorm(x, self.norm2.weight, self.norm2.bias, self.norm2.eps, add=pos)
+            h0 = None if self.ca_val_has_pos_emb else ops.layernorm(
+                x, self.norm2.weight, self.norm2.bias, self.norm2.eps)
+            o = self._attend(self.multihead_attn, h, h0, self.ca_val_has_pos_emb, seg,
+                             seg.cross_seg)
         x = linear(o, self.multihead_attn.out_proj.weight, self.multihead_attn.out_proj.bias,
                    residual=x)
-        # position-wise feed-forward (:231-238)
-        h = ops.layernorm(x, self.norm3.weight, self.norm3.bias, self.norm3.eps)
-        h = linear(h, self.linear1.weight, self.linear1.bias, act=ops.ACT_RELU)
+        # position-wise feed-forward (:231-238); linear_ln falls back to layernorm + linear
+        h = linear_ln(x, self.norm3, self.linear1.weight, self.linear1.bias, act=ops.ACT_RELU)
         return linear(h, self.linear2.weight, self.linear2.bias, residual=x), None
 
     def _forward_post(self, x, pos, seg: Segments, pending_bias=None):

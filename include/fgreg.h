@@ -233,6 +233,22 @@ int fgr_gemm_bf16_ws(const float* a, int64_t lda, const void* w_img, float* c, i
                      const float* bias, const float* r, int64_t ldr, int32_t m, int32_t n,
                      int32_t k, int32_t act, void* ws, size_t ws_bytes, void* stream);
 
+/* Pre-norm transformer sub-layer input, fused (transformers.py:193-196 norm1 ->
+ * with_pos_embed -> self_attn in_proj; :213-221 norm2 -> multihead_attn in_proj; :231-232
+ * norm3 -> linear1):
+ *   C[m, n] = act(A[m, :] . W[n, :] + bias[n]),  A = LayerNorm_eps(X) * gamma + beta (+ add)
+ * with the LayerNorm over the k features of each row (biased variance, as nn.LayerNorm) and
+ * the f16x3 product of fgr_gemm_f16x3 (w_img from fgr_split_weights_h3). act: FGR_ACT_NONE or
+ * FGR_ACT_RELU; add (optional, e.g. the positional embedding) has row stride ld_add. All
+ * pointers 16-B aligned, row strides multiples of 4. Only for shapes where
+ * fgr_gemm_f16x3_ln_supported(m, n, k) returns 1 (the row-stationary kernel: k <= 256,
+ * k % 8 == 0, n % 16 == 0, many rows); FGR_E_ARG otherwise. */
+int fgr_gemm_f16x3_ln_supported(int32_t m, int32_t n, int32_t k);
+int fgr_gemm_f16x3_ln(const float* x, int64_t ldx, const float* gamma, const float* beta,
+                      float eps, const float* add, int64_t ld_add, const void* w_img, float* c,
+                      int64_t ldc, const float* bias, int32_t m, int32_t n, int32_t k,
+                      int32_t act, void* stream);
+
 int fgr_split_weights_bf16_bytes(int32_t n, int32_t k, size_t* bytes);
 int fgr_split_weights_bf16(const float* w, int32_t n, int32_t k, int64_t stride_n,
                            int64_t stride_k, void* img, void* stream);

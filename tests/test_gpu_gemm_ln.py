@@ -1,0 +1,137 @@
+"""LayerNorm -> (+ pos) -> Linear in one launch (fgr_gemm_f16x3_ln; the pre-norm transformer
+sub-layer inputs, transformers.py:193-196, :213-221, :231-232).
+
+Checked: the fused op against a float64 LayerNorm + product (error at fp32 level and no worse
+than a few times torch's own fp32 LayerNorm + GEMM), against the unfused path (ops.layernorm
+then linear), the fallback below the supported shapes, the C-ABI's refusal of unsupported
+shapes, and a full pre-norm encoder layer at the ModelNet bench size (9544 rows, where every
+in_proj and linear1 takes the fused launch) against the oracle's restatement of forward_pre.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+import model_oracle as mo
+from conftest import rel_err
+
+pytestmark = pytest.mark.gpu
+
+
+def _inputs(m, k, n, seed, mean=3.0):
+    g = torch.Generator().manual_seed(seed)
+    x = mean + 2.0 * torch.randn(m, k, generator=g)
+    x[7] = 0.0                                   # constant rows: var 0, output = beta (+ pos)
+    x[8] = 5.0
+    norm = torch.nn.LayerNorm(k)
+    with torch.no_grad():
+        norm.weight.copy_(1 + 0.2 * torch.randn(k, generator=g))
+        norm.bias.copy_(0.2 * torch.randn(k, generator=g))
+    pos = torch.randn(m, k, generator=g)
+    w = torch.randn(n, k, generator=g) / math.sqrt(k)
+    b = torch.randn(n, generator=g)
+    return x, norm, pos, w, b
+
+
+def _ref64(x, norm, pos, w, b, relu):
+    xd = x.double()
+    mu = xd.mean(1, keepdim=True)
+    var = ((xd - mu) ** 2).mean(1, keepdim=True)
+    h = (xd - mu) / torch.sqrt(var + norm.eps) * norm.weight.double() + norm.bias.double()
+    if pos is not None:
+        h = h + pos.double()
+    y = h @ w.double().t() + b.double()
+    return y.clamp_min(0) if relu else y
+
+
+@pytest.mark.parametrize('m,n,k', [(9544, 768, 256), (9544, 1024, 256), (9000, 256, 128),
+                                   (8001, 640, 64), (25003, 256, 256)])
+@pytest.mark.parametrize('with_pos,relu', [(True, False), (False, True)])
+def test_gemm_ln_vs_fp64(gpu, m, n, k, with_pos, relu):
+    from fgreg import linear as fl
+    from fgreg import ops
+    assert fl.MODE == 'f16x3' and fl.ln_fusable(m, n, k)
+    x, norm, pos, w, b = _inputs(m, k, n, m + n + k)
+    if not with_pos:
+        pos = None
+    ref = _ref64(x, norm, pos, w, b, relu)
+    act = ops.ACT_RELU if relu else ops.ACT_NONE
+    X, W, B = x.to(gpu), w.to(gpu), b.to(gpu)
+    P = pos.to(gpu) if pos is not None else None
+    N = norm.to(gpu)
+    out = fl.linear_ln(X, N, W, B, act=act, add=P)
+    # torch fp32 LayerNorm + GEMM (the comparison baseline only)
+    h32 = torch.nn.functional.layer_norm(X, (k,), N.weight, N.bias, N.eps)
+    if P is not None:
+        h32 = h32 + P
+    y32 = torch.addmm(B, h32, W.t())
+    e32 = rel_err(y32.clamp_min(0) if relu else y32, ref)
+    e = rel_err(out, ref)
+    assert e < 1e-5 and e < 4 * e32 + 1e-6, (e, e32)
+    # the unfused path (ops.layernorm, then the GEMM): same arithmetic, two launches
+    old = fl.LN_FUSE
+    try:
+        fl.LN_FUSE = False
+        un = fl.linear_ln(X, N, W, B, act=act, add=P)
+    finally:
+        fl.LN_FUSE = old
+    assert rel_err(out, un) < 4e-6
+    # constant rows normalise to beta (+ pos) exactly as the LayerNorm kernel does
+    assert rel_err(out[7:9], un[7:9]) < 4e-6
+
+
+def test_gemm_ln_fallback_and_refusal(gpu):
+    """Below the supported shapes linear_ln runs layernorm + linear; the C ABI refuses them."""
+    from fgreg import _lib
+    from fgreg import linear as fl
+    m, n, k = 500, 768, 256
+    assert not fl.ln_fusable(m, n, k)
+    x, norm, pos, w, b = _inputs(m, k, n, 3)
+    ref = _ref64(x, norm, pos, w, b, False)
+    norm = norm.to(gpu)                          # (in place)
+    out = fl.linear_ln(x.to(gpu), norm, w.to(gpu), b.to(gpu), add=pos.to(gpu))
+    assert rel_err(out, ref) < 1e-5
+    L = _lib.load()
+    X, W = x.to(gpu), w.to(gpu)
+    sw = fl.weight_image(W, mode='f16x3')
+    o = torch.empty(m, n, device=gpu)
+    rc = L.fgr_gemm_f16x3_ln(X.data_ptr(), k, norm.weight.data_ptr(), norm.bias.data_ptr(), 1e-5, None, 0, sw.img.data_ptr(),
+                             o.data_ptr(), n, None, m, n, k, 0,
+                             torch.cuda.current_stream().cuda_stream)
+    assert rc == -1 and b'not supported' in L.fgr_last_error()
+
+
+def test_prenorm_layer_bench_size_vs_oracle(gpu):
+    """One pre-norm TransformerCrossEncoderLayer (d 256, 8 heads, ffn 1024, values with pos:
+    the ModelNet config) on 8 pairs of 596-point clouds = 9536 rows: the in_proj and linear1
+    GEMMs take the fused LayerNorm launch; against the oracle's forward_pre (fp32 CPU)."""
+    from fgreg import linear as fl
+    from fgreg.transformer import Segments, TransformerCrossEncoderLayer
+    d, nhead, ff, B, L = 256, 8, 1024, 8, 596
+    assert fl.ln_fusable(2 * B * L, 3 * d, d) and fl.ln_fusable(2 * B * L, ff, d)
+    torch.manual_seed(5)
+    layer = TransformerCrossEncoderLayer(d, nhead, ff, 0.0, normalize_before=True,
+                                         sa_val_has_pos_emb=True, ca_val_has_pos_emb=True)
+    with torch.no_grad():
+        for nm in ('norm1', 'norm2', 'norm3'):
+            getattr(layer, nm).weight.normal_(1.0, 0.2)
+            getattr(layer, nm).bias.normal_(0.0, 0.2)
+    sd = {f'l.{k}': v.clone() for k, v in layer.state_dict().items()}
+    g = torch.Generator().manual_seed(6)
+    src = torch.randn(L, B, d, generator=g) + 1.0
+    tgt = torch.randn(L, B, d, generator=g) - 0.5
+    spos = torch.randn(L, B, d, generator=g)
+    tpos = torch.randn(L, B, d, generator=g)
+    mask = torch.zeros(B, L, dtype=torch.bool)
+    rs, rt = mo.cross_encoder_layer(sd, 'l', src, tgt, mask, mask, spos, tpos, nhead)
+    pack = lambda a, c: torch.cat([a[:, b] for b in range(B)] + [c[:, b] for b in range(B)])  # noqa: E731
+    x, pos = pack(src, tgt).to(gpu), pack(spos, tpos).to(gpu)
+    ref = pack(rs, rt)
+    layer = layer.to(gpu).eval()
+    seg = Segments([L] * (2 * B), gpu)
+    with torch.no_grad():
+        y, pending = layer.forward_packed(x.clone(), pos, seg)
+        if pending is not None:
+            y = y + pending
+    assert rel_err(y, ref) < 1e-4

@@ -26,7 +26,7 @@ OLD = {(9544, 768, 256): 'y', (9544, 256, 256): 'X', (9544, 1024, 256): 'y',
        (57264, 3, 256): 'X', (57264, 1, 256): 'X', (40000, 128, 256): 'X',
        (2120, 896, 128): 'X', (2120, 1792, 256): 'Y', (26778, 256, 128): 'X',
        (40000, 224, 32): 'X', (26778, 448, 64): 'X', (26778, 64, 256): 'X'}
-VARIANTS = [('1', '0'), ('2', '0'), ('1', '2'), ('1', '4'), ('2', '2'), ('2', '4'), ('2', '8')]
+VARIANTS = [('2', ''), ('1', ''), ('2', '0'), ('2', '4'), ('2', '8'), ('2', '16')]
 
 
 def main():
@@ -49,9 +49,9 @@ def main():
             y = lin.linear(x, w, b, out=out)
             err = float((y.double() - ref).abs().max() / ref.abs().max())
             us = timeit(lambda: lin.linear(x, w, b, out=out))
-            line += f' | rt{rt}/nc{nc} {us:6.1f}us{"" if err < 2e-6 else " ERR%.1e" % err}'
+            line += f' | rt{rt}/nc{nc or "auto"} {us:6.1f}us{"" if err < 2e-6 else " ERR%.1e" % err}'
             if best is None or us < best[1]:
-                best = (f'rt{rt}/nc{nc}', us)
+                best = (f'rt{rt}/nc{nc or "auto"}', us)
         os.environ['FGR_RS_RT'], os.environ['FGR_RS_NC'] = '', ''
         os.environ['FGR_GEMM16_TILE'] = ''
         print(line + f' || best {best[0]} {us_old / best[1]:.2f}x', flush=True)
