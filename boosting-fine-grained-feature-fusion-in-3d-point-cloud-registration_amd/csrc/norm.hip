@@ -145,13 +145,16 @@ __device__ __forceinline__ float xg16_32_sum(float v) {   // sum over lanes l, l
     return v;
 }
 
+template <int VEC>
 __global__ void __launch_bounds__(64 * kInW) instnorm_seg16_kernel(InArgs a) {
-    __shared__ float red[kInW][16];
+    // VEC consecutive channels per lane (VEC = 2: 8-B accesses, 128-B row segments per 16
+    // lanes, for C >= 512 where C / 32 x n_seg blocks still fill the chip)
+    __shared__ float red[kInW][16 * VEC];
     const int seg = blockIdx.y;
     const int wv = threadIdx.x / 64, lane = threadIdx.x % 64;
     const int rl = lane >> 4, cc = lane & 15;
-    const int ch = blockIdx.x * 16 + cc;
-    const bool cok = ch < a.c;
+    const int ch = (blockIdx.x * 16 + cc) * VEC;
+    const bool cok = ch < a.c;                           // C % VEC == 0 (checked by the caller)
     const int64_t b = a.seg_off[seg], e = a.seg_off[seg + 1];
     const int nrow = (int)(e - b);
     if (nrow <= 0) return;
@@ -159,57 +162,100 @@ __global__ void __launch_bounds__(64 * kInW) instnorm_seg16_kernel(InArgs a) {
     // every load issued before any use (clamped rows / channels, masked afterwards), so a
     // lane's 16 loads are in flight together instead of one round trip each
     const int chc = cok ? ch : 0;
-    float v[kSegRpl], dv[kSegRpl];
+    // segment-uniform bases + 32-bit lane offsets (one scalar base, no 64-bit address per row)
+    const float* xs = a.x + b * a.c;
+    float v[kSegRpl][VEC], dv[kSegRpl];
 #pragma unroll
     for (int j = 0; j < kSegRpl; ++j) {
         const int rr = min(r0 + 64 * j, nrow - 1);
-        v[j] = a.x[(b + rr) * a.c + chc];
+        const float* src = xs + (uint32_t)(rr * a.c + chc);
+        if constexpr (VEC == 2) {
+            const float2 t = *reinterpret_cast<const float2*>(src);
+            v[j][0] = t.x; v[j][1] = t.y;
+        } else {
+            v[j][0] = *src;
+        }
         dv[j] = a.row_div ? a.row_div[b + rr] : 1.f;
     }
-    float s = 0.f;
+    float s[VEC];
+#pragma unroll
+    for (int u = 0; u < VEC; ++u) s[u] = 0.f;
 #pragma unroll
     for (int j = 0; j < kSegRpl; ++j) {
         const bool ok = r0 + 64 * j < nrow && cok;
-        v[j] = ok ? (a.row_div ? v[j] / dv[j] : v[j]) : 0.f;
-        s += v[j];
-    }
-    s = xg16_32_sum(s);
-    if (rl == 0) red[wv][cc] = s;
-    __syncthreads();
-    float tot = 0.f;
 #pragma unroll
-    for (int w = 0; w < kInW; ++w) tot += red[w][cc];
+        for (int u = 0; u < VEC; ++u) {
+            v[j][u] = ok ? (a.row_div ? v[j][u] / dv[j] : v[j][u]) : 0.f;
+            s[u] += v[j][u];
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < VEC; ++u) {
+        s[u] = xg16_32_sum(s[u]);
+        if (rl == 0) red[wv][cc * VEC + u] = s[u];
+    }
+    __syncthreads();
     const float cnt = (float)nrow;
-    const float mean = tot / cnt;
-    __syncthreads();
-    float sq = 0.f;
+    float mean[VEC];
 #pragma unroll
-    for (int j = 0; j < kSegRpl; ++j) {
-        const float d = (r0 + 64 * j < nrow) ? v[j] - mean : 0.f;
-        sq += d * d;
+    for (int u = 0; u < VEC; ++u) {
+        float tot = 0.f;
+#pragma unroll
+        for (int w = 0; w < kInW; ++w) tot += red[w][cc * VEC + u];
+        mean[u] = tot / cnt;
     }
-    sq = xg16_32_sum(sq);
-    if (rl == 0) red[wv][cc] = sq;
     __syncthreads();
-    float m2 = 0.f;
+    float sq[VEC];
 #pragma unroll
-    for (int w = 0; w < kInW; ++w) m2 += red[w][cc];
-    const float rstd = 1.0f / sqrtf(m2 / cnt + a.eps);
+    for (int u = 0; u < VEC; ++u) sq[u] = 0.f;
+#pragma unroll
+    for (int j = 0; j < kSegRpl; ++j)
+#pragma unroll
+        for (int u = 0; u < VEC; ++u) {
+            const float d = (r0 + 64 * j < nrow) ? v[j][u] - mean[u] : 0.f;
+            sq[u] += d * d;
+        }
+#pragma unroll
+    for (int u = 0; u < VEC; ++u) {
+        sq[u] = xg16_32_sum(sq[u]);
+        if (rl == 0) red[wv][cc * VEC + u] = sq[u];
+    }
+    __syncthreads();
+    float rstd[VEC];
+#pragma unroll
+    for (int u = 0; u < VEC; ++u) {
+        float m2 = 0.f;
+#pragma unroll
+        for (int w = 0; w < kInW; ++w) m2 += red[w][cc * VEC + u];
+        rstd[u] = 1.0f / sqrtf(m2 / cnt + a.eps);
+    }
     if (!cok) return;
-    float rv[kSegRpl];
+    float rv[kSegRpl][VEC];
     if (a.residual) {
 #pragma unroll
-        for (int j = 0; j < kSegRpl; ++j)
-            rv[j] = a.residual[(b + min(r0 + 64 * j, nrow - 1)) * a.c + ch];
+        for (int j = 0; j < kSegRpl; ++j) {
+            const float* src = a.residual + b * a.c + (uint32_t)(min(r0 + 64 * j, nrow - 1) * a.c + ch);
+            if constexpr (VEC == 2) {
+                const float2 t = *reinterpret_cast<const float2*>(src);
+                rv[j][0] = t.x; rv[j][1] = t.y;
+            } else {
+                rv[j][0] = *src;
+            }
+        }
     }
 #pragma unroll
     for (int j = 0; j < kSegRpl; ++j) {
         const int rr = r0 + 64 * j;
         if (rr < nrow) {
-            const int64_t o = (b + rr) * a.c + ch;
-            float y = act_fn((v[j] - mean) * rstd, a.act);
-            if (a.residual) y = act_fn(y + rv[j], a.post_act);
-            a.out[o] = y;
+            float* const dst = a.out + b * a.c + (uint32_t)(rr * a.c + ch);
+            float y[VEC];
+#pragma unroll
+            for (int u = 0; u < VEC; ++u) {
+                y[u] = act_fn((v[j][u] - mean[u]) * rstd[u], a.act);
+                if (a.residual) y[u] = act_fn(y[u] + rv[j][u], a.post_act);
+            }
+            if constexpr (VEC == 2) *reinterpret_cast<float2*>(dst) = make_float2(y[0], y[1]);
+            else *dst = y[0];
         }
     }
 }
@@ -609,8 +655,16 @@ extern "C" int fgr_instnorm(const float* x, int64_t n, int32_t c, const int64_t*
     TimedCall timed_(st);
     const unsigned cx = (unsigned)ceil_div(c, 64);
     if (max_seg_len <= kSegRows) {
-        hipLaunchKernelGGL(instnorm_seg16_kernel, dim3((unsigned)ceil_div(c, 16), n_seg, 1),
-                           dim3(64 * kInW), 0, st, a);
+        // 2 channels per lane for wide features (C / 32 x n_seg blocks) when 8-B aligned
+        const bool v2 = c >= 512 && c % 2 == 0 &&
+                        ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(out) |
+                          reinterpret_cast<uintptr_t>(residual)) & 7) == 0;
+        if (v2)
+            hipLaunchKernelGGL(instnorm_seg16_kernel<2>, dim3((unsigned)ceil_div(c, 32), n_seg, 1),
+                               dim3(64 * kInW), 0, st, a);
+        else
+            hipLaunchKernelGGL(instnorm_seg16_kernel<1>, dim3((unsigned)ceil_div(c, 16), n_seg, 1),
+                               dim3(64 * kInW), 0, st, a);
     } else if (ls_ok(c)) {
         const int rows = ls_rows(c);
         const int64_t lc = ceil_div(max_seg_len, rows);
