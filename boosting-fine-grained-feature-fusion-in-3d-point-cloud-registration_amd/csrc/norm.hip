@@ -443,11 +443,15 @@ __device__ __forceinline__ float lpr_sum(float v) {
     return v;
 }
 
-template <int LPR, int NV>
+// DUAL: a second affine output from the same statistics, out2 = xhat * g2 + b2 (+ add2) (the
+// encoder's output norm of layer l and norm1 (+ pos) of layer l + 1 read the same rows)
+template <int LPR, int NV, bool DUAL = false>
 __global__ void __launch_bounds__(256)
 layernorm_lpr_kernel(float* __restrict__ x, int64_t n, int d, const float* __restrict__ g,
                      const float* __restrict__ bta, float eps, const float* __restrict__ add,
-                     const float* __restrict__ pre_bias, float* __restrict__ out) {
+                     const float* __restrict__ pre_bias, float* __restrict__ out,
+                     const float* __restrict__ g2 = nullptr, const float* __restrict__ b2 = nullptr,
+                     const float* __restrict__ add2 = nullptr, float* __restrict__ out2 = nullptr) {
     constexpr int RPB = 256 / LPR;
     const int64_t r = (int64_t)blockIdx.x * RPB + threadIdx.x / LPR;
     const int l = threadIdx.x % LPR;
@@ -496,6 +500,18 @@ layernorm_lpr_kernel(float* __restrict__ x, int64_t n, int d, const float* __res
             y.z = (v[j].z - mean) * rstd * gg[j].z + bb[j].z + ad[j].z;
             y.w = (v[j].w - mean) * rstd * gg[j].w + bb[j].w + ad[j].w;
             *reinterpret_cast<float4*>(out + r * d + col) = y;
+            if constexpr (DUAL) {
+                const float4 g4 = *reinterpret_cast<const float4*>(g2 + col);
+                const float4 b4 = *reinterpret_cast<const float4*>(b2 + col);
+                const float4 a4 = add2 ? *reinterpret_cast<const float4*>(add2 + r * d + col)
+                                       : make_float4(0.f, 0.f, 0.f, 0.f);
+                float4 z;
+                z.x = (v[j].x - mean) * rstd * g4.x + b4.x + a4.x;
+                z.y = (v[j].y - mean) * rstd * g4.y + b4.y + a4.y;
+                z.z = (v[j].z - mean) * rstd * g4.z + b4.z + a4.z;
+                z.w = (v[j].w - mean) * rstd * g4.w + b4.w + a4.w;
+                *reinterpret_cast<float4*>(out2 + r * d + col) = z;
+            }
         }
     }
 }
@@ -759,5 +775,40 @@ extern "C" int fgr_sine_pos_embed(const float* xyz, int64_t n, int32_t d_model, 
     hipLaunchKernelGGL(sine_pe_kernel, dim3((unsigned)ceil_div(n, kPeRows)), dim3(256), 0,
                        as_stream(stream), xyz, n, d_model, npf, temperature, scale, out);
     FGR_CHECK_LAUNCH("sine_pe_kernel");
+    return FGR_OK;
+}
+
+extern "C" int fgr_layernorm_dual(const float* x, int64_t n, int32_t d, const float* gamma,
+                                  const float* beta, const float* add, float* out,
+                                  const float* gamma2, const float* beta2, const float* add2,
+                                  float* out2, float eps, void* stream) {
+    FGR_REQUIRE(n >= 0 && d > 0 && d <= 1024 && gamma && beta && gamma2 && beta2,
+                "fgr_layernorm_dual: bad arguments");
+    FGR_REQUIRE(n == 0 || (x && out && out2), "fgr_layernorm_dual: null pointer");
+    if (n == 0) return FGR_OK;
+    const bool vec = d % 64 == 0 && d <= 512 &&
+                     ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(out) |
+                       reinterpret_cast<uintptr_t>(gamma) | reinterpret_cast<uintptr_t>(beta) |
+                       reinterpret_cast<uintptr_t>(add) | reinterpret_cast<uintptr_t>(out2) |
+                       reinterpret_cast<uintptr_t>(gamma2) | reinterpret_cast<uintptr_t>(beta2) |
+                       reinterpret_cast<uintptr_t>(add2)) & 15) == 0;
+    if (!vec) {                       // two passes of fgr_layernorm
+        const int r1 = fgr_layernorm(const_cast<float*>(x), n, d, gamma, beta, eps, add, nullptr, out, stream);
+        if (r1 != FGR_OK) return r1;
+        return fgr_layernorm(const_cast<float*>(x), n, d, gamma2, beta2, eps, add2, nullptr, out2, stream);
+    }
+    hipStream_t st = as_stream(stream);
+    TimedCall timed_(st);
+    float* xm = const_cast<float*>(x);                 // read only (no pre_bias)
+    if (d <= 128)
+        hipLaunchKernelGGL((layernorm_lpr_kernel<32, 1, true>), dim3((unsigned)ceil_div(n, 8)), dim3(256), 0,
+                           st, xm, n, d, gamma, beta, eps, add, nullptr, out, gamma2, beta2, add2, out2);
+    else if (d <= 256)
+        hipLaunchKernelGGL((layernorm_lpr_kernel<32, 2, true>), dim3((unsigned)ceil_div(n, 8)), dim3(256), 0,
+                           st, xm, n, d, gamma, beta, eps, add, nullptr, out, gamma2, beta2, add2, out2);
+    else
+        hipLaunchKernelGGL((layernorm_lpr_kernel<32, 4, true>), dim3((unsigned)ceil_div(n, 8)), dim3(256), 0,
+                           st, xm, n, d, gamma, beta, eps, add, nullptr, out, gamma2, beta2, add2, out2);
+    FGR_CHECK_LAUNCH("layernorm_dual_kernel");
     return FGR_OK;
 }

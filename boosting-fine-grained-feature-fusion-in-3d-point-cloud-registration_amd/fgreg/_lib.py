@@ -39,6 +39,7 @@ SIGNATURES = {
     'fgr_layernorm': [_vp, _i64, _i32, _vp, _vp, _f32, _vp, _vp, _vp, _vp],
     'fgr_sine_pos_embed': [_vp, _i64, _i32, _f32, _f32, _vp, _vp],
     'fgr_add': [_vp, _vp, _i64, _vp, _vp],
+    'fgr_layernorm_dual': [_vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f32, _vp],
     'fgr_attention': [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i32, _i32, _i32,
                       _i32, _f32, _vp],
     'fgr_attention_f16x3_workspace': [_i64, _i32, _i32, ctypes.POINTER(_sz)],

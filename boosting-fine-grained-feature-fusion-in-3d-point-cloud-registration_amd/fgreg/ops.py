@@ -406,6 +406,27 @@ def layernorm(x, weight, bias, eps=1e-5, add=None, pre_bias=None, out=None) -> t
     return out
 
 
+def layernorm_dual(x, norm_a, norm_b, add_b=None, out_a=None, out_b=None):
+    """(LN_a(x), LN_b(x) (+ add_b)) in one pass (fgr_layernorm_dual): two nn.LayerNorm modules
+    of the same width and eps over the same rows."""
+    _dev(x, norm_a.weight, norm_b.weight, add_b)
+    assert x.dtype == torch.float32 and x.is_contiguous() and norm_a.eps == norm_b.eps
+    n, d = x.shape
+    if add_b is not None:
+        add_b = _c(add_b, torch.float32)
+        assert add_b.shape == x.shape
+    out_a = torch.empty_like(x) if out_a is None else out_a
+    out_b = torch.empty_like(x) if out_b is None else out_b
+    assert out_a.is_contiguous() and out_b.is_contiguous()
+    t0 = _begin('layernorm')
+    _lib.check(_lib.load().fgr_layernorm_dual(
+        _ptr(x), n, d, _ptr(norm_a.weight.contiguous()), _ptr(norm_a.bias.contiguous()), None,
+        _ptr(out_a), _ptr(norm_b.weight.contiguous()), _ptr(norm_b.bias.contiguous()),
+        _ptr(add_b), _ptr(out_b), float(norm_a.eps), _stream()), 'fgr_layernorm_dual')
+    _end('layernorm', t0, n * d * (12 + (4 if add_b is not None else 0)))
+    return out_a, out_b
+
+
 def add(a, b, out=None) -> torch.Tensor:
     """a + b (same shape, fp32) on fgr_add: the post-norm layer's with_pos_embed."""
     _dev(a, b)

@@ -104,7 +104,14 @@ class TransformerCrossEncoderLayer(nn.Module):
         o = ops.attention(q, k, v, seg.off, seg.off, kv_seg, seg.max_len, self.nhead)
         return o
 
-    def forward_packed(self, x, pos, seg: Segments, pending_bias=None):
+    def wants_h1(self, x):
+        """True if forward_packed takes a precomputed norm1(x) + pos (``h1``): pre-norm, values
+        with pos, and norm1 not folded into the in_proj GEMM."""
+        n, d = x.shape
+        return (self.normalize_before and self.sa_val_has_pos_emb
+                and not ln_fusable(n, 3 * d, d))
+
+    def forward_packed(self, x, pos, seg: Segments, pending_bias=None, h1=None):
         """x (N_tot, d) packed clouds -> (x, pending bias) (forward_pre, transformers.py:183-244).
 
         Every residual GEMM adds its Linear's bias and the residual in its epilogue, so each
@@ -121,6 +128,9 @@ class TransformerCrossEncoderLayer(nn.Module):
         if fuse_in and self.sa_val_has_pos_emb and pending_bias is None:
             o = self._attend(self.self_attn, None, None, True, seg, seg.self_seg,
                              ln=(x, self.norm1, pos))
+        elif h1 is not None:              # norm1(x) + pos from the previous layer's output norm
+            assert pending_bias is None and self.sa_val_has_pos_emb
+            o = self._attend(self.self_attn, h1, None, True, seg, seg.self_seg)
         else:
             h = ops.layernorm(x, self.norm1.weight, self.norm1.bias, self.norm1.eps, add=pos,
                               pre_bias=pending_bias)
@@ -183,10 +193,19 @@ class TransformerCrossEncoder(nn.Module):
                             device=x.device)
         x = x.clone()                      # the residual stream is updated in place
         pending = None
+        h1 = None
         for l, layer in enumerate(self.layers):
-            x, pending = layer.forward_packed(x, pos, seg, pending)
+            x, pending = layer.forward_packed(x, pos, seg, pending, h1=h1)
+            h1 = None
             if self.return_intermediate or l == L - 1:
-                self._norm(x, pending, inter[l if self.return_intermediate else 0])
+                nxt = self.layers[l + 1] if l + 1 < L else None
+                if (nxt is not None and self.norm is not None and pending is None
+                        and nxt.wants_h1(x) and self.norm.eps == nxt.norm1.eps):
+                    # this layer's output norm and the next layer's norm1 (+ pos): one pass
+                    _, h1 = ops.layernorm_dual(x, self.norm, nxt.norm1, add_b=pos,
+                                               out_a=inter[l if self.return_intermediate else 0])
+                else:
+                    self._norm(x, pending, inter[l if self.return_intermediate else 0])
                 pending = None
         return inter
 

@@ -157,6 +157,14 @@ int fgr_instnorm(const float* x, int64_t n, int32_t c, const int64_t* seg_off, i
  * deferred bias of the Linear that produced the residual stream). */
 int fgr_layernorm(float* x, int64_t n, int32_t d, const float* gamma, const float* beta,
                   float eps, const float* add, const float* pre_bias, float* out, void* stream);
+/* Two LayerNorms of the same rows in one pass (same eps, shared statistics):
+ * out = LN(x)*gamma + beta (+ add), out2 = LN(x)*gamma2 + beta2 (+ add2). The cross encoder's
+ * per-layer output norm (transformers.py:43-44, return_intermediate) of layer l and norm1 +
+ * with_pos_embed of layer l + 1 (:193-195) read the same residual stream. x is not written. */
+int fgr_layernorm_dual(const float* x, int64_t n, int32_t d, const float* gamma,
+                       const float* beta, const float* add, float* out, const float* gamma2,
+                       const float* beta2, const float* add2, float* out2, float eps,
+                       void* stream);
 
 /* out = a + b over n floats: the post-norm layer's with_pos_embed (transformers.py:121-124,
  * pre_norm: False; the pre-norm path fuses this add into fgr_layernorm). */

@@ -135,3 +135,28 @@ def test_prenorm_layer_bench_size_vs_oracle(gpu):
         if pending is not None:
             y = y + pending
     assert rel_err(y, ref) < 1e-4
+
+
+@pytest.mark.parametrize('d', [64, 256, 512, 96, 1024])
+def test_layernorm_dual_matches_two_passes(gpu, d):
+    """fgr_layernorm_dual (the encoder's output norm of layer l and norm1 + pos of layer l + 1
+    in one pass) == two fgr_layernorm launches, bit for bit (d 96 / 1024: the two-launch
+    fallback inside the library)."""
+    from fgreg import ops
+    g = torch.Generator().manual_seed(d)
+    x = (2.0 + 3.0 * torch.randn(777, d, generator=g)).to(gpu)
+    pos = torch.randn(777, d, generator=g).to(gpu)
+    na, nb = torch.nn.LayerNorm(d), torch.nn.LayerNorm(d)
+    with torch.no_grad():
+        for nm in (na, nb):
+            nm.weight.copy_(1 + 0.3 * torch.randn(d, generator=g))
+            nm.bias.copy_(0.3 * torch.randn(d, generator=g))
+    na, nb = na.to(gpu), nb.to(gpu)
+    x0 = x.clone()
+    a, b = ops.layernorm_dual(x, na, nb, add_b=pos)
+    ra = ops.layernorm(x, na.weight, na.bias, na.eps)
+    rb = ops.layernorm(x, nb.weight, nb.bias, nb.eps, add=pos)
+    assert torch.equal(x, x0)
+    assert torch.equal(a, ra) and torch.equal(b, rb)
+    ref = torch.nn.functional.layer_norm(x.double(), (d,), nb.weight.double(), nb.bias.double(), nb.eps) + pos.double()
+    assert rel_err(b, ref) < 1e-5
