@@ -40,7 +40,10 @@ bool g5_tile(char cfg, int* bm, int* bn);
 int g5_ksplit(int M, int N, int K, int BM, int BN);
 char bf16_tile(int m, int n, int k);
 int bf16_ksplit(char cfg, int m, int n, int k);
-struct RsLn { const float* g; const float* b; const float* add; int64_t ld_add; float eps; };
+struct RsLn {
+    const float* g; const float* b; const float* add; int64_t ld_add; float eps;
+    const float* g2; const float* b2; float* out2; int64_t ld_out2;
+};
 bool gemm_rs_f16x3(const float* A, int64_t lda, const void* W, int ksteps, const float* wsc,
                    float* C, int64_t ldc, const float* bias, const float* R, int64_t ldr, int M,
                    int N, int K, int act, hipStream_t st, const RsLn* ln = nullptr);
@@ -1217,21 +1220,25 @@ extern "C" int fgr_gemm_f16x3_ln_supported(int32_t m, int32_t n, int32_t k) {
     return (m > 0 && n > 0 && k > 0 && h3_tile(m, n, k) == 'z') ? 1 : 0;
 }
 
-extern "C" int fgr_gemm_f16x3_ln(const float* x, int64_t ldx, const float* gamma, const float* beta,
-                                 float eps, const float* add, int64_t ld_add, const void* w_img,
-                                 float* c, int64_t ldc, const float* bias, int32_t m, int32_t n,
-                                 int32_t k, int32_t act, void* stream) {
+static int gemm_f16x3_ln_impl(const float* x, int64_t ldx, const float* gamma, const float* beta,
+                              float eps, const float* add, int64_t ld_add, const void* w_img,
+                              float* c, int64_t ldc, const float* bias, int32_t m, int32_t n,
+                              int32_t k, int32_t act, const float* gamma2, const float* beta2,
+                              float* out2, int64_t ld_out2, void* stream) {
     FGR_REQUIRE(x && gamma && beta && w_img && c && m >= 0 && n > 0 && k > 0 && ldx >= k &&
                     ldc >= n && (!add || ld_add >= k) && eps >= 0.f &&
                     (act == FGR_ACT_NONE || act == FGR_ACT_RELU),
                 "fgr_gemm_f16x3_ln: bad arguments (m %d n %d k %d act %d)", m, n, k, act);
+    FGR_REQUIRE(!out2 || (gamma2 && beta2 && add && ld_out2 >= k && ld_out2 % 4 == 0),
+                "fgr_gemm_f16x3_ln_out2: the side output needs gamma2 / beta2, the add and ld_out2 >= k");
     FGR_REQUIRE(m == 0 || fgr_gemm_f16x3_ln_supported(m, n, k),
                 "fgr_gemm_f16x3_ln: shape %d x %d x %d not supported (fgr_gemm_f16x3_ln_supported)",
                 m, n, k);
     const uintptr_t al = reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(gamma) |
                          reinterpret_cast<uintptr_t>(beta) | reinterpret_cast<uintptr_t>(add) |
                          reinterpret_cast<uintptr_t>(w_img) | reinterpret_cast<uintptr_t>(c) |
-                         reinterpret_cast<uintptr_t>(bias);
+                         reinterpret_cast<uintptr_t>(bias) | reinterpret_cast<uintptr_t>(gamma2) |
+                         reinterpret_cast<uintptr_t>(beta2) | reinterpret_cast<uintptr_t>(out2);
     FGR_REQUIRE((al & 15) == 0 && ldx % 4 == 0 && ldc % 4 == 0 && (!add || ld_add % 4 == 0),
                 "fgr_gemm_f16x3_ln: operands must be 16-B aligned with row strides %% 4 == 0");
     if (m == 0) return FGR_OK;
@@ -1239,10 +1246,29 @@ extern "C" int fgr_gemm_f16x3_ln(const float* x, int64_t ldx, const float* gamma
                                                       image_bytes_h3(n, k));
     hipStream_t st = as_stream(stream);
     TimedCall timed_(st);
-    const RsLn ln{gamma, beta, add, ld_add, eps};
+    const RsLn ln{gamma, beta, add, ld_add, eps, gamma2, beta2, out2, ld_out2};
     FGR_REQUIRE(gemm_rs_f16x3(x, ldx, w_img, ksteps_h3(k), wsc, c, ldc, bias, nullptr, 0, m, n, k,
                               act, st, &ln),
                 "fgr_gemm_f16x3_ln: row-stationary kernel rejected %d x %d x %d", m, n, k);
     FGR_CHECK_LAUNCH("gemm_rs_ln");
     return FGR_OK;
+}
+
+extern "C" int fgr_gemm_f16x3_ln(const float* x, int64_t ldx, const float* gamma, const float* beta,
+                                 float eps, const float* add, int64_t ld_add, const void* w_img,
+                                 float* c, int64_t ldc, const float* bias, int32_t m, int32_t n,
+                                 int32_t k, int32_t act, void* stream) {
+    return gemm_f16x3_ln_impl(x, ldx, gamma, beta, eps, add, ld_add, w_img, c, ldc, bias, m, n, k,
+                              act, nullptr, nullptr, nullptr, 0, stream);
+}
+
+extern "C" int fgr_gemm_f16x3_ln_out2(const float* x, int64_t ldx, const float* gamma,
+                                      const float* beta, float eps, const float* add, int64_t ld_add,
+                                      const void* w_img, float* c, int64_t ldc, const float* bias,
+                                      int32_t m, int32_t n, int32_t k, int32_t act,
+                                      const float* gamma2, const float* beta2, float* out2,
+                                      int64_t ld_out2, void* stream) {
+    FGR_REQUIRE(out2, "fgr_gemm_f16x3_ln_out2: out2 is required");
+    return gemm_f16x3_ln_impl(x, ldx, gamma, beta, eps, add, ld_add, w_img, c, ldc, bias, m, n, k,
+                              act, gamma2, beta2, out2, ld_out2, stream);
 }

@@ -53,6 +53,8 @@ struct RsArgs {
     const float* ln_g; const float* ln_b;   // LN prologue: gamma, beta (K)
     const float* ln_add; int64_t ld_add;    //   optional row add (pos) after the affine
     float eps;
+    const float* ln_g2; const float* ln_b2; //   side output (LNM 3): LN(x) * g2 + b2 -> out2
+    float* ln_out2; int64_t ld_out2;
 };
 
 // s_waitcnt vmcnt(n) lgkmcnt(0) -- gfx9 encoding
@@ -107,7 +109,9 @@ __device__ __forceinline__ float finish_ct(float y, float b, float r) {
     }
 }
 
-// LNM: 0 plain, 1 LayerNorm prologue, 2 LayerNorm prologue + row add
+// LNM: 0 plain, 1 LayerNorm prologue, 2 LayerNorm prologue + row add, 3 as 2 plus a second
+// LayerNorm output of the same rows (the encoder's per-layer output norm), written by the
+// blocks of the first column group
 template <int RT, int KS, bool RES, int ACT, int LNM>
 __global__ void __launch_bounds__(256) gemm_rs_kernel(RsArgs p) {
     constexpr bool LN = LNM > 0;
@@ -117,6 +121,7 @@ __global__ void __launch_bounds__(256) gemm_rs_kernel(RsArgs p) {
     __shared__ u32x4 ring[kRsNb * PANEL_U];
     __shared__ float4 colw[kRsMaxNc * 4], colb[kRsMaxNc * 4];   // per (panel, g): wsc, bias
     __shared__ float4 lng[LN ? KS * 8 : 1], lnb[LN ? KS * 8 : 1];  // LN gamma / beta (K / 4)
+    __shared__ float4 lng2[LNM == 3 ? KS * 8 : 1], lnb2[LNM == 3 ? KS * 8 : 1];
 
     const int nbm = (p.M + 64 * RT - 1) / (64 * RT);
     const int npanel = (p.N + 15) / 16;
@@ -190,6 +195,14 @@ __global__ void __launch_bounds__(256) gemm_rs_kernel(RsArgs p) {
                     bv = reinterpret_cast<const float4*>(p.ln_b)[tid];
                 }
                 if (tid < KS * 8) { lng[tid] = gv; lnb[tid] = bv; }
+                if constexpr (LNM == 3) {
+                    float4 g2v = make_float4(0.f, 0.f, 0.f, 0.f), b2v = g2v;
+                    if (tid < p.K / 4) {
+                        g2v = reinterpret_cast<const float4*>(p.ln_g2)[tid];
+                        b2v = reinterpret_cast<const float4*>(p.ln_b2)[tid];
+                    }
+                    if (tid < KS * 8) { lng2[tid] = g2v; lnb2[tid] = b2v; }
+                }
                 __syncthreads();
             }
             // row mean, then the centred variance (as the LayerNorm kernels: norm.hip), from
@@ -211,6 +224,28 @@ __global__ void __launch_bounds__(256) gemm_rs_kernel(RsArgs p) {
                 }
             }
             const float rstd = 1.0f / sqrtf(xg_sum_rs(sq) / (float)p.K + p.eps);
+            if constexpr (LNM == 3) {
+                // the side output first, fenced off from the add loads below (scheduled
+                // together they exceed the 256 registers of two waves per SIMD)
+                if (grp == 0 && mw + 16 * i + c < p.M) {
+#pragma unroll
+                    for (int s = 0; s < KS; ++s) {
+                        const int k = 32 * s + 8 * g;
+                        if (k < p.K) {
+                            const float4 h0 = lng2[k / 4], h1 = lng2[k / 4 + 1];
+                            const float4 c0 = lnb2[k / 4], c1 = lnb2[k / 4 + 1];
+                            float* o2 = p.ln_out2 + row * p.ld_out2 + k;
+                            *reinterpret_cast<float4*>(o2) = make_float4(
+                                (x[s][0] - mean) * rstd * h0.x + c0.x, (x[s][1] - mean) * rstd * h0.y + c0.y,
+                                (x[s][2] - mean) * rstd * h0.z + c0.z, (x[s][3] - mean) * rstd * h0.w + c0.w);
+                            *reinterpret_cast<float4*>(o2 + 4) = make_float4(
+                                (x[s][4] - mean) * rstd * h1.x + c1.x, (x[s][5] - mean) * rstd * h1.y + c1.y,
+                                (x[s][6] - mean) * rstd * h1.z + c1.z, (x[s][7] - mean) * rstd * h1.w + c1.w);
+                        }
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
 #pragma unroll
             for (int s = 0; s < KS; ++s) {
                 // no branches around the loads (all in flight); chunks past K zeroed below
@@ -218,7 +253,7 @@ __global__ void __launch_bounds__(256) gemm_rs_kernel(RsArgs p) {
                 const float4 g0 = lng[kl / 4], g1 = lng[kl / 4 + 1];
                 const float4 b0 = lnb[kl / 4], b1 = lnb[kl / 4 + 1];
                 float4 d0 = make_float4(0.f, 0.f, 0.f, 0.f), d1 = d0;
-                if constexpr (LNM == 2) {
+                if constexpr (LNM >= 2) {
                     const float* dr = p.ln_add + row * p.ld_add + kl;
                     d0 = *reinterpret_cast<const float4*>(dr);
                     d1 = *reinterpret_cast<const float4*>(dr + 4);
@@ -337,6 +372,10 @@ void launch_rs_act(const RsArgs& a, unsigned blocks, hipStream_t st) {
     // LN prologue: one row tile per wave (at two, the row + add registers of the prologue
     // exceed the 256 VGPRs of two waves per SIMD and spill), no residual (checked by the caller)
     if constexpr (RT == 1 && ACT != FGR_ACT_RELU_RES_LEAKY) {
+        if (a.ln_g && a.ln_add && a.ln_out2) {
+            hipLaunchKernelGGL((gemm_rs_kernel<RT, KS, false, ACT, 3>), dim3(blocks), dim3(256), 0, st, a);
+            return;
+        }
         if (a.ln_g && a.ln_add) {
             hipLaunchKernelGGL((gemm_rs_kernel<RT, KS, false, ACT, 2>), dim3(blocks), dim3(256), 0, st, a);
             return;
@@ -366,12 +405,15 @@ bool launch_rs_k(const RsArgs& a, unsigned blocks, hipStream_t st) {
 // The rs kernel applies to K <= 256, K % 8 == 0, N % 16 == 0 with 16-B aligned A / C / R / bias rows
 // (checked by the caller). ksteps = the image's k32-steps (even, <= 8). `ln` (optional, no R):
 // the LayerNorm prologue's gamma, beta, add (16-B aligned rows), ld_add and eps.
-struct RsLn { const float* g; const float* b; const float* add; int64_t ld_add; float eps; };
+struct RsLn {
+    const float* g; const float* b; const float* add; int64_t ld_add; float eps;
+    const float* g2; const float* b2; float* out2; int64_t ld_out2;    // optional side output
+};
 bool gemm_rs_f16x3(const float* A, int64_t lda, const void* W, int ksteps, const float* wsc,
                    float* C, int64_t ldc, const float* bias, const float* R, int64_t ldr, int M,
                    int N, int K, int act, hipStream_t st, const RsLn* ln) {
     if (K % 8 != 0 || N % 16 != 0 || ksteps > 8 || ksteps % 2 != 0) return false;
-    if (ln && R) return false;
+    if (ln && (R || (ln->out2 && !ln->add))) return false;
     // row tiles per wave: 2 (W fragments reused twice) unless that leaves too few blocks
     const char* rte = getenv("FGR_RS_RT");
     int RT = (rte && rte[0]) ? atoi(rte) : 2;
@@ -403,7 +445,8 @@ bool gemm_rs_f16x3(const float* A, int64_t lda, const void* W, int ksteps, const
     const unsigned blocks = (unsigned)((int64_t)nbm * ngrp);
     RsArgs a{A, lda, (const u32x4*)W, wsc, C, ldc, bias, R, ldr, M, N, K, act, nc,
              ln ? ln->g : nullptr, ln ? ln->b : nullptr, ln ? ln->add : nullptr,
-             ln ? ln->ld_add : 0, ln ? ln->eps : 0.f};
+             ln ? ln->ld_add : 0, ln ? ln->eps : 0.f, ln ? ln->g2 : nullptr,
+             ln ? ln->b2 : nullptr, ln ? ln->out2 : nullptr, ln ? ln->ld_out2 : 0};
 #define RS_CASE(rt, ks) \
     if (RT == rt && ksteps == ks) return launch_rs_k<rt, ks>(a, blocks, st);
     RS_CASE(2, 2) RS_CASE(2, 4) RS_CASE(2, 6) RS_CASE(2, 8)

@@ -56,6 +56,8 @@ SIGNATURES = {
     'fgr_gemm_f16x3_ln_supported': [_i32, _i32, _i32],
     'fgr_gemm_f16x3_ln': [_vp, _i64, _vp, _vp, _f32, _vp, _i64, _vp, _vp, _i64, _vp, _i32, _i32,
                           _i32, _i32, _vp],
+    'fgr_gemm_f16x3_ln_out2': [_vp, _i64, _vp, _vp, _f32, _vp, _i64, _vp, _vp, _i64, _vp, _i32,
+                               _i32, _i32, _i32, _vp, _vp, _vp, _i64, _vp],
     'fgr_split_weights_bf16_bytes': [_i32, _i32, ctypes.POINTER(_sz)],
     'fgr_split_weights_bf16': [_vp, _i32, _i32, _i64, _i64, _vp, _vp],
     'fgr_gemm_bf16': [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _vp],

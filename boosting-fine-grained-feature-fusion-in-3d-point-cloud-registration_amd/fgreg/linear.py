@@ -161,15 +161,19 @@ def ln_fusable(m, n, k) -> bool:
 
 
 def linear_ln(x: torch.Tensor, norm, w: torch.Tensor, bias=None, act=ACT_NONE, add=None,
-              out=None) -> torch.Tensor:
+              out=None, side=None) -> torch.Tensor:
     """act((LayerNorm(x) (+ add)) @ W^T + bias) with ``norm`` an nn.LayerNorm over x's
     features: the pre-norm sub-layer inputs of transformers.py:193-196, :213-221 (add = the
     positional embedding) and :231-232. One launch (fgr_gemm_f16x3_ln) where ln_fusable,
-    else ops.layernorm then linear() -- the same arithmetic in two launches."""
+    else ops.layernorm then linear() -- the same arithmetic in two launches. ``side`` =
+    (norm2, out2): also out2 = norm2(x) (the encoder's output norm of the previous layer; the
+    fused launch writes it from the same statistics, fgr_gemm_f16x3_ln_out2; needs ``add``)."""
     m, k = x.shape
     n = w.shape[0]
     assert w.shape[1] == k and norm.weight.numel() == k
-    if not ln_fusable(m, n, k):
+    if not ln_fusable(m, n, k) or (side is not None and (add is None or side[0].eps != norm.eps)):
+        if side is not None:
+            ops.layernorm(x, side[0].weight, side[0].bias, side[0].eps, out=side[1])
         return linear(ops.layernorm(x, norm.weight, norm.bias, norm.eps, add=add), w, bias,
                       act=act, out=out)
     _dev(x, w)
@@ -184,9 +188,18 @@ def linear_ln(x: torch.Tensor, norm, w: torch.Tensor, bias=None, act=ACT_NONE, a
     if out is None:
         out = torch.empty((m, n), dtype=torch.float32, device=x.device)
     t0 = _begin('gemm', (m, n, k))
-    _lib.check(_lib.load().fgr_gemm_f16x3_ln(
-        _ptr(x), x.stride(0), _ptr(gamma), _ptr(beta), float(norm.eps), _ptr(add),
-        add.stride(0) if add is not None else 0, _ptr(sw.img), _ptr(out), out.stride(0),
-        _ptr(bias), m, n, k, act, _stream()), 'fgr_gemm_f16x3_ln')
+    if side is None:
+        _lib.check(_lib.load().fgr_gemm_f16x3_ln(
+            _ptr(x), x.stride(0), _ptr(gamma), _ptr(beta), float(norm.eps), _ptr(add),
+            add.stride(0) if add is not None else 0, _ptr(sw.img), _ptr(out), out.stride(0),
+            _ptr(bias), m, n, k, act, _stream()), 'fgr_gemm_f16x3_ln')
+    else:
+        norm2, out2 = side
+        assert out2.shape == x.shape and out2.stride(1) == 1
+        _lib.check(_lib.load().fgr_gemm_f16x3_ln_out2(
+            _ptr(x), x.stride(0), _ptr(gamma), _ptr(beta), float(norm.eps), _ptr(add),
+            add.stride(0), _ptr(sw.img), _ptr(out), out.stride(0), _ptr(bias), m, n, k, act,
+            _ptr(norm2.weight.contiguous()), _ptr(norm2.bias.contiguous()), _ptr(out2),
+            out2.stride(0), _stream()), 'fgr_gemm_f16x3_ln_out2')
     _end('gemm', t0, 2 * m * n * k)
     return out

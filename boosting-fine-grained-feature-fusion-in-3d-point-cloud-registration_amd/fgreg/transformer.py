@@ -83,14 +83,14 @@ class TransformerCrossEncoderLayer(nn.Module):
         self.sa_val_has_pos_emb = sa_val_has_pos_emb
         self.ca_val_has_pos_emb = ca_val_has_pos_emb
 
-    def _attend(self, mha, h_pos, h_nopos, val_has_pos, seg, kv_seg, ln=None):
+    def _attend(self, mha, h_pos, h_nopos, val_has_pos, seg, kv_seg, ln=None, side=None):
         """``ln`` = (x, norm, pos): h_pos = norm(x) + pos is formed inside the in_proj GEMM
-        (linear_ln; val_has_pos only)."""
+        (linear_ln; val_has_pos only); ``side`` = (norm2, out2): out2 = norm2(x) as well."""
         W, b = mha.in_proj_weight, mha.in_proj_bias
         if ln is not None:
             x, norm, pos = ln
             d = x.shape[1]
-            qkv = linear_ln(x, norm, W, b, add=pos)                   # (N, 3d): [q | k | v]
+            qkv = linear_ln(x, norm, W, b, add=pos, side=side)        # (N, 3d): [q | k | v]
             q, k, v = qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:]
             return ops.attention(q, k, v, seg.off, seg.off, kv_seg, seg.max_len, self.nhead)
         d = h_pos.shape[1]
@@ -104,6 +104,13 @@ class TransformerCrossEncoderLayer(nn.Module):
         o = ops.attention(q, k, v, seg.off, seg.off, kv_seg, seg.max_len, self.nhead)
         return o
 
+    def takes_side(self, x, pos):
+        """True if forward_packed can also write another LayerNorm of its input x (``side``)
+        from its fused norm1 -> in_proj launch."""
+        n, d = x.shape
+        return (self.normalize_before and self.sa_val_has_pos_emb and pos is not None
+                and ln_fusable(n, 3 * d, d))
+
     def wants_h1(self, x):
         """True if forward_packed takes a precomputed norm1(x) + pos (``h1``): pre-norm, values
         with pos, and norm1 not folded into the in_proj GEMM."""
@@ -111,7 +118,7 @@ class TransformerCrossEncoderLayer(nn.Module):
         return (self.normalize_before and self.sa_val_has_pos_emb
                 and not ln_fusable(n, 3 * d, d))
 
-    def forward_packed(self, x, pos, seg: Segments, pending_bias=None, h1=None):
+    def forward_packed(self, x, pos, seg: Segments, pending_bias=None, h1=None, side=None):
         """x (N_tot, d) packed clouds -> (x, pending bias) (forward_pre, transformers.py:183-244).
 
         Every residual GEMM adds its Linear's bias and the residual in its epilogue, so each
@@ -127,11 +134,15 @@ class TransformerCrossEncoderLayer(nn.Module):
         # self-attention, shared weights for src and tgt (:193-210)
         if fuse_in and self.sa_val_has_pos_emb and pending_bias is None:
             o = self._attend(self.self_attn, None, None, True, seg, seg.self_seg,
-                             ln=(x, self.norm1, pos))
+                             ln=(x, self.norm1, pos), side=side)
+            side = None
         elif h1 is not None:              # norm1(x) + pos from the previous layer's output norm
             assert pending_bias is None and self.sa_val_has_pos_emb
             o = self._attend(self.self_attn, h1, None, True, seg, seg.self_seg)
         else:
+            if side is not None:
+                ops.layernorm(x, side[0].weight, side[0].bias, side[0].eps, out=side[1])
+                side = None
             h = ops.layernorm(x, self.norm1.weight, self.norm1.bias, self.norm1.eps, add=pos,
                               pre_bias=pending_bias)
             h0 = None if self.sa_val_has_pos_emb else ops.layernorm(
@@ -193,13 +204,18 @@ class TransformerCrossEncoder(nn.Module):
                             device=x.device)
         x = x.clone()                      # the residual stream is updated in place
         pending = None
-        h1 = None
+        h1 = side = None
         for l, layer in enumerate(self.layers):
-            x, pending = layer.forward_packed(x, pos, seg, pending, h1=h1)
-            h1 = None
+            x, pending = layer.forward_packed(x, pos, seg, pending, h1=h1, side=side)
+            h1 = side = None
             if self.return_intermediate or l == L - 1:
                 nxt = self.layers[l + 1] if l + 1 < L else None
                 if (nxt is not None and self.norm is not None and pending is None
+                        and nxt.takes_side(x, pos) and self.norm.eps == nxt.norm1.eps):
+                    # this layer's output norm is written by the next layer's fused
+                    # norm1 -> in_proj launch (same rows, same statistics)
+                    side = (self.norm, inter[l if self.return_intermediate else 0])
+                elif (nxt is not None and self.norm is not None and pending is None
                         and nxt.wants_h1(x) and self.norm.eps == nxt.norm1.eps):
                     # this layer's output norm and the next layer's norm1 (+ pos): one pass
                     _, h1 = ops.layernorm_dual(x, self.norm, nxt.norm1, add_b=pos,

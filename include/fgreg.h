@@ -256,6 +256,15 @@ int fgr_gemm_f16x3_ln(const float* x, int64_t ldx, const float* gamma, const flo
                       float eps, const float* add, int64_t ld_add, const void* w_img, float* c,
                       int64_t ldc, const float* bias, int32_t m, int32_t n, int32_t k,
                       int32_t act, void* stream);
+/* fgr_gemm_f16x3_ln plus a second LayerNorm output of the same rows, written once:
+ *   out2 = LayerNorm_eps(X) * gamma2 + beta2   (row stride ld_out2, 16-B aligned)
+ * -- the cross encoder's per-layer output norm of layer l (transformers.py:43-44) computed in
+ * the prologue of layer l + 1's in_proj, which normalises the same rows. Requires `add`. */
+int fgr_gemm_f16x3_ln_out2(const float* x, int64_t ldx, const float* gamma, const float* beta,
+                           float eps, const float* add, int64_t ld_add, const void* w_img,
+                           float* c, int64_t ldc, const float* bias, int32_t m, int32_t n,
+                           int32_t k, int32_t act, const float* gamma2, const float* beta2,
+                           float* out2, int64_t ld_out2, void* stream);
 
 int fgr_split_weights_bf16_bytes(int32_t n, int32_t k, size_t* bytes);
 int fgr_split_weights_bf16(const float* w, int32_t n, int32_t k, int64_t stride_n,

@@ -160,3 +160,64 @@ def test_layernorm_dual_matches_two_passes(gpu, d):
     assert torch.equal(a, ra) and torch.equal(b, rb)
     ref = torch.nn.functional.layer_norm(x.double(), (d,), nb.weight.double(), nb.bias.double(), nb.eps) + pos.double()
     assert rel_err(b, ref) < 1e-5
+
+
+def test_gemm_ln_side_output(gpu):
+    """fgr_gemm_f16x3_ln_out2: the GEMM as fgr_gemm_f16x3_ln, plus out2 = LayerNorm(x) with a
+    second affine (written once per row) == ops.layernorm to fp32 rounding."""
+    from fgreg import linear as fl
+    from fgreg import ops
+    m, n, k = 9544, 768, 256
+    x, norm, pos, w, b = _inputs(m, k, n, 11)
+    norm2 = torch.nn.LayerNorm(k)
+    with torch.no_grad():
+        norm2.weight.normal_(1.0, 0.3)
+        norm2.bias.normal_(0.0, 0.3)
+    X, P, W, B = x.to(gpu), pos.to(gpu), w.to(gpu), b.to(gpu)
+    N, N2 = norm.to(gpu), norm2.to(gpu)
+    out2 = torch.full((m, k), float('nan'), device=gpu)
+    y = fl.linear_ln(X, N, W, B, add=P, side=(N2, out2))
+    assert rel_err(y, fl.linear_ln(X, N, W, B, add=P)) == 0.0
+    ref2 = ops.layernorm(X, N2.weight, N2.bias, N2.eps)
+    assert torch.isfinite(out2).all() and rel_err(out2, ref2) < 1e-6
+
+
+def test_encoder_bench_size_vs_oracle(gpu):
+    """TransformerCrossEncoder (3 pre-norm layers, return_intermediate, final norm) at the
+    ModelNet bench size: every in_proj / linear1 takes the fused LayerNorm launch and each
+    layer's output norm is written by the next layer's fused launch; the stacked outputs
+    against the oracle's forward_pre + norm per layer (transformers.py:31-59)."""
+    from fgreg import linear as fl
+    from fgreg.transformer import (Segments, TransformerCrossEncoder,
+                                   TransformerCrossEncoderLayer)
+    d, nhead, ff, B, L, NL = 256, 8, 1024, 8, 596, 3
+    assert fl.ln_fusable(2 * B * L, 3 * d, d)
+    torch.manual_seed(9)
+    layer = TransformerCrossEncoderLayer(d, nhead, ff, 0.0, normalize_before=True,
+                                         sa_val_has_pos_emb=True, ca_val_has_pos_emb=True)
+    enc = TransformerCrossEncoder(layer, NL, torch.nn.LayerNorm(d), return_intermediate=True)
+    with torch.no_grad():
+        for mod in enc.modules():
+            if isinstance(mod, torch.nn.LayerNorm):
+                mod.weight.normal_(1.0, 0.2)
+                mod.bias.normal_(0.0, 0.2)
+    sd = {f'e.{kk}': v.clone() for kk, v in enc.state_dict().items()}
+    g = torch.Generator().manual_seed(10)
+    src = torch.randn(L, B, d, generator=g)
+    tgt = torch.randn(L, B, d, generator=g)
+    spos = torch.randn(L, B, d, generator=g)
+    tpos = torch.randn(L, B, d, generator=g)
+    mask = torch.zeros(B, L, dtype=torch.bool)
+    refs = []
+    s_, t_ = src, tgt
+    for i in range(NL):
+        s_, t_ = mo.cross_encoder_layer(sd, f'e.layers.{i}', s_, t_, mask, mask, spos, tpos, nhead)
+        refs.append((mo._ln(sd, 'e.norm', s_), mo._ln(sd, 'e.norm', t_)))
+    pack = lambda a, c: torch.cat([a[:, b] for b in range(B)] + [c[:, b] for b in range(B)])  # noqa: E731
+    enc = enc.to(gpu).eval()
+    with torch.no_grad():
+        out = enc.forward_packed(pack(src, tgt).to(gpu), pack(spos, tpos).to(gpu),
+                                 Segments([L] * (2 * B), gpu))
+    assert out.shape == (NL, 2 * B * L, d)
+    for i in range(NL):
+        assert rel_err(out[i], pack(*refs[i])) < 1e-4, i
