@@ -8,6 +8,13 @@ stream. Without it every forward's preprocessing waits, at its first voxel-count
 for the previous forward's whole core to drain, and the GPU then idles while the host
 enqueues the rest of the preprocessing.
 
+``depth`` cores are kept enqueued ahead of the output being yielded (default 2): the
+preprocessing of batch i + 2 runs (with its host readbacks) while the cores of batches i and
+i + 1 are both queued on the current stream, so the GPU does not idle when a preprocessing
+takes longer than one core (the 20k-point workloads). depth = 1 is the one-ahead pipeline.
+Graph replays clone their outputs (fgreg.regtr._CoreGraph.run), so an output stays valid
+while the next core runs.
+
 Ordering contract (no extra synchronisation needed by the caller):
   * batch i + 1 is drawn from the iterator BEFORE batch i's core is enqueued, and the side
     stream waits for an event recorded on the current stream at that moment -- so any work
@@ -19,9 +26,14 @@ Ordering contract (no extra synchronisation needed by the caller):
     hand its memory to the side stream while the current stream may still read it;
   * outputs are produced on the current stream, as with ``model(batch)``.
 """
+import os
+from collections import deque
+
 import torch
 
 from .regtr import RegTR
+
+DEPTH = int(os.environ.get('FGREG_PIPE_DEPTH', '2'))
 
 
 def _meta_tensors(meta):
@@ -47,31 +59,45 @@ def _prepare(model, batch, side, ready):
     return meta, done
 
 
-def pipeline(model: RegTR, batches):
+def pipeline(model: RegTR, batches, depth=None):
     """Yields model(batch) for each batch of ``batches`` (an iterable of forward() batch
-    dicts on one device), preprocessing batch i + 1 while batch i's core runs."""
+    dicts on one device), preprocessing later batches while earlier cores run (``depth``
+    cores in flight ahead of the yielded output; default DEPTH = FGREG_PIPE_DEPTH or 2)."""
     if model.training and torch.is_grad_enabled():
         raise NotImplementedError('fgreg.pipeline is inference only (eval() / no_grad)')
+    depth = max(1, int(DEPTH if depth is None else depth))
     it = iter(batches)
-    cur = next(it, None)
-    if cur is None:
+    first = next(it, None)
+    if first is None:
         return
-    dev = cur['src_xyz'][0].device
+    dev = first['src_xyz'][0].device
     if dev.type != 'cuda':
         raise RuntimeError('fgreg.pipeline needs GPU batches')
     with torch.no_grad(), torch.cuda.device(dev):
         side = torch.cuda.Stream(dev)
+        main = torch.cuda.current_stream()
+
+        def draw():
+            """the next batch and an event recorded now, before any later core is enqueued"""
+            b = next(it, None)
+            if b is None:
+                return None
+            ready = torch.cuda.Event()
+            ready.record()
+            return b, ready
+
         ready = torch.cuda.Event()
         ready.record()
-        meta, done = _prepare(model, cur, side, ready)
-        while cur is not None:
-            nxt = next(it, None)
-            if nxt is not None:
-                ready = torch.cuda.Event()
-                ready.record()                      # before cur's core is enqueued
-            torch.cuda.current_stream().wait_event(done)
-            out = model._forward(cur, meta)
-            if nxt is not None:
-                meta, done = _prepare(model, nxt, side, ready)
-            yield out
-            cur = nxt
+        prepared = deque([(first,) + _prepare(model, first, side, ready)])
+        outs = deque()
+        while prepared:
+            while prepared and len(outs) < depth:
+                b, meta, done = prepared.popleft()
+                item = draw()                       # before b's core is enqueued
+                main.wait_event(done)
+                outs.append(model._forward(b, meta))
+                if item is not None:
+                    prepared.append((item[0],) + _prepare(model, item[0], side, item[1]))
+            yield outs.popleft()
+        while outs:
+            yield outs.popleft()

@@ -1,5 +1,6 @@
-"""fgreg.pipeline (preprocessing of batch i + 1 on a side stream while batch i's core runs)
-yields exactly model(batch) for every batch: same kernels, same order of operations."""
+"""fgreg.pipeline (preprocessing of later batches on a side stream while earlier cores run,
+1-3 cores in flight) yields exactly model(batch) for every batch: same kernels, same order
+of operations."""
 import numpy as np
 import pytest
 import torch
@@ -26,8 +27,9 @@ def _same(a, b):
             assert torch.equal(x, y), k
 
 
+@pytest.mark.parametrize('depth', [1, 2, 3])
 @pytest.mark.parametrize('kind', ['modelnet', '3dmatch'])
-def test_pipeline_equals_sequential(gpu, kind):
+def test_pipeline_equals_sequential(gpu, kind, depth):
     import fgreg
     torch.manual_seed(0)
     np.random.seed(0)
@@ -35,18 +37,18 @@ def test_pipeline_equals_sequential(gpu, kind):
     P = 2 if kind == 'modelnet' else 1
     # two shape signatures, each seen three times (the graph path captures on the second)
     sizes = [(0, P), (5, P), (0, P), (5, P), (0, P), (5, P)]
-    kw = {} if kind == 'modelnet' else {}
     batches = _batches(kind, gpu, sizes)
     with torch.no_grad():
         ref = [model(dict(b)) for b in batches]
-    got = list(fgreg.pipeline(model, [dict(b) for b in batches]))
+    got = list(fgreg.pipeline(model, [dict(b) for b in batches], depth=depth))
     torch.cuda.synchronize()
     assert len(got) == len(ref)
     for a, b in zip(got, ref):
         _same(a, b)
 
 
-def test_pipeline_inputs_produced_on_the_current_stream(gpu):
+@pytest.mark.parametrize('depth', [1, 2])
+def test_pipeline_inputs_produced_on_the_current_stream(gpu, depth):
     """Inputs written by the caller on the current stream right before each draw are read
     by the side-stream preprocessing only after that write (the ready event)."""
     import fgreg
@@ -64,5 +66,8 @@ def test_pipeline_inputs_produced_on_the_current_stream(gpu):
                 for d, s in zip(b[k], base[k]):
                     d.copy_(s)
             yield b
-    for out in fgreg.pipeline(model, gen()):
+    n = 0
+    for out in fgreg.pipeline(model, gen(), depth=depth):
         _same(out, ref)
+        n += 1
+    assert n == 4
