@@ -18,6 +18,6 @@ for wl in modelnet 3dmatch 3dlomatch; do
   { python3 tools/kernel_stats.py gpurun_out/prof_${wl}_$tag/*/*_kernel_trace.csv 20 $ms
     echo "no-pipeline bench line of the same build (separate process, 50 steps): $msb ms/step"; } > profiles/${tag}_${wl}_kernel_stats_per_step.txt
 done
-for wl in modelnet 3dmatch; do
+for wl in modelnet 3dmatch 3dlomatch; do
   [ -f gpurun_out/pmc_kpconv_${wl}_$tag.json ] && cp gpurun_out/pmc_kpconv_${wl}_$tag.json profiles/pmc_kpconv_$wl.json
 done

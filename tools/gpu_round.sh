@@ -15,7 +15,7 @@ if [ "$2" != "skip-tests" ]; then
 fi
 # PMC passes first (their summaries feed the bench lines' roofline.traffic): FETCH_SIZE and
 # WRITE_SIZE in separate runs, gather kernels only, per workload
-for wl in modelnet 3dmatch; do
+for wl in modelnet 3dmatch 3dlomatch; do
   timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex 'kpconv_gather' --output-format csv -d gpurun_out/pmcf_${wl}_$tag -- python3 bench.py --profile --workload $wl --steps 3 --warmup 1 > gpurun_out/pmcf_${wl}_$tag.log 2>&1 || exit 1
   timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex 'kpconv_gather' --output-format csv -d gpurun_out/pmcw_${wl}_$tag -- python3 bench.py --profile --workload $wl --steps 3 --warmup 1 > gpurun_out/pmcw_${wl}_$tag.log 2>&1 || exit 1
   op=fgr_kpconv_gather; rx=kpconv_gather
