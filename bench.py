@@ -126,6 +126,9 @@ def parse():
                         'preprocesses step i + 1 on a side stream while step i\'s core runs)')
     p.add_argument('--profile', action='store_true',
                    help='warmup + timed steps only (for rocprofv3 kernel-trace runs)')
+    p.add_argument('--train', action='store_true',
+                   help='time training steps instead (SURVEY §8(f) row 4): train() forward + '
+                        'backward + clip_grad_norm_ + AdamW step; a side line, not the headline')
     p.add_argument('--gemm-table', default=None,
                    help='write the per-shape GEMM table (M, N, K, launches, us, TFLOP/s, '
                         'bytes, fractions) of the instrumented replay to this JSON file')
@@ -156,8 +159,103 @@ def _cpu_model():
     return platform.processor() or 'unknown'
 
 
+def train_main(args):
+    """ms per training step of the workload's batch on one GPU (trainer.py:110-125: forward,
+    loss.backward(), clip_grad_norm_, optimizer.step()). The reference's loss modules are not
+    part of the path (they stay the reference's own in the drop-in); the objective here is a
+    fixed random linear functional of every differentiable output (warped keypoints, overlap
+    logits, per-layer and un-projected features), so every parameter receives a gradient."""
+    import fgreg
+    from fgreg import linear as lin
+    from fgreg.synthetic import make_batch
+    dev = torch.device('cuda', 0)
+    torch.cuda.set_device(dev)
+    wl = args.workload
+    fgreg.set_precision(args.precision or PRECISION_DEFAULT.get(wl, 'fp32'))
+    cfg = fgreg.config.get(CFG_NAME[wl])
+    torch.manual_seed(0)
+    np.random.seed(0)
+    model = fgreg.RegTR(cfg).to(dev).train()
+    P = args.pairs_per_gpu or PAIRS[wl]
+    kind = {'raw2048': 'modelnet_raw'}.get(wl, wl)
+    src, tgt, _ = make_batch(kind, P)
+    batch = {'src_xyz': [torch.from_numpy(a).to(dev) for a in src],
+             'tgt_xyz': [torch.from_numpy(b).to(dev) for b in tgt]}
+    params = [p for p in model.parameters() if p.requires_grad]
+    opt = torch.optim.AdamW(params, lr=1e-4, weight_decay=1e-4, foreach=True)
+    gen = torch.Generator(device=dev).manual_seed(1)
+    coef = {}
+
+    def objective(out):
+        tot = torch.zeros((), device=dev)
+        for key in ('src_kp_warped', 'tgt_kp_warped', 'src_overlap', 'tgt_overlap', 'src_feat',
+                    'tgt_feat', 'src_feat_un', 'tgt_feat_un'):
+            for i, t in enumerate(out[key]):
+                c = coef.get((key, i))
+                if c is None:
+                    c = coef[(key, i)] = torch.randn(t.shape, device=dev, generator=gen) / t.numel() ** 0.5
+                tot = tot + (t * c).sum()
+        return tot
+
+    def step(split=None):
+        opt.zero_grad(set_to_none=True)
+        out = model(batch)
+        loss = objective(out)
+        if split is not None:
+            split[0].record()
+        loss.backward()
+        if split is not None:
+            split[1].record()
+        torch.nn.utils.clip_grad_norm_(params, 0.1)
+        opt.step()
+
+    for _ in range(max(args.warmup, 1)):
+        step()
+    torch.cuda.synchronize()
+    if args.profile:
+        torch.cuda._sleep(1000)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if args.profile:
+        torch.cuda._sleep(1000)
+        torch.cuda.synchronize()
+    line = {'metric': f'training step ms ({METRIC[wl].split(" on ")[1]})',
+            'value': elapsed / args.steps * 1e3, 'unit': 'ms/step', 'n_gpus': 1,
+            'steps': args.steps, 'warmup': args.warmup, 'higher_is_better': False,
+            'pairs_per_s': P * args.steps / elapsed, 'dtype': DTYPE[lin.MODE],
+            'data': DATA[wl], 'config': {'workload': WORKLOAD[wl].format(P=P), 'pairs_per_gpu': P,
+                                         'precision': fgreg.precision(), 'mode': 'train()'},
+            'what': 'train() forward (Res2Net BatchNorm on batch statistics) + backward of a fixed '
+                    'random linear functional of every output + clip_grad_norm_(0.1) + AdamW '
+                    'step (torch foreach); eager launches (no HIP graph in training); gradients '
+                    'deterministic (no floating-point atomics)'}
+    if not args.profile:
+        # forward / backward split of extra steps (events around backward)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        fw, bw = [], []
+        for _ in range(min(args.steps, 10)):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            step(ev)
+            torch.cuda.synchronize()
+            tot = (time.perf_counter() - t0) * 1e3
+            b = ev[0].elapsed_time(ev[1])
+            bw.append(b)
+            fw.append(tot - b)
+        line['split_ms'] = {'forward_loss_optimizer': float(np.median(fw)),
+                            'backward': float(np.median(bw))}
+    print(json.dumps(line), flush=True)
+
+
 def main():
     args = parse()
+    if args.train:
+        if args.gpus != 1:
+            raise SystemExit('--train runs on one GPU')
+        return train_main(args)
     import fgreg
     from fgreg import linear as lin
     from fgreg import ops

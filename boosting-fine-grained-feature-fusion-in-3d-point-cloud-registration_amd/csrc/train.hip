@@ -3,10 +3,15 @@
 // runs on the f16x3 / bf16 GEMMs with transposed weight images (fgreg/autograd.py); this file
 // holds the rest:
 //
+//   fgr_nbr_inverse         the inverse (CSR) of a neighbour table: for every support row the
+//                           (query, slot) entries naming it, in ascending entry order -- built
+//                           once per table, shared by every scatter over that table
 //   fgr_kpconv_scatter      KPConv gather-weight backward: dx[idx[q,h], c] += sum_k w(q,h,k)
 //                           dwf[q,k,c] -- the scatter-add that the reference's
 //                           `gather(method=2)` exists for (finegrained_kpconv_blocks.py:66-97)
 //   fgr_max_pool_bwd        max_pool (:125-141): the gradient goes to the row's first max entry
+//   fgr_corr_attention_bwd  CorrespondenceDecoder.simple_attention (finegrained_regtr.py:328-363)
+//                           backward: dq, dk of softmax(q.k scale) xyz
 //   fgr_segnorm_stats/_apply/_bwd
 //                           per-(segment, channel) normalisation with batch statistics: the
 //                           InstanceNorm of BatchNormBlock (:462-518, segment = cloud) and the
@@ -15,9 +20,10 @@
 //   fgr_colsum              deterministic column sums (bias gradients)
 //   fgr_attention_bwd       MHA core backward (transformers.py:197-226) over packed segments
 //
-// Reductions are deterministic (fixed-order partials in fp64, merged in order) except the two
-// scatters (KPConv, max-pool), which add with fp32 global atomics: their sums are exact up to
-// fp32 rounding in an order that can vary between runs (|err| ~ 1e-7 relative).
+// Every reduction is deterministic: fixed-order partials (fp64 where they are long), merged in
+// order, and no floating-point atomics anywhere. The two scatters (KPConv, max-pool) run as
+// gathers over the table's inverse: each support row sums its own contributions in ascending
+// (query, slot) order, so two backward passes give bit-identical gradients.
 #include "common.h"
 
 #include <algorithm>
@@ -34,17 +40,103 @@ __device__ __forceinline__ float kp_w(float nx, float ny, float nz, const float*
     return fmaxf(1.0f - sqrtf(d2) * inv_extent, 0.0f);
 }
 
+// ---- inverse neighbour table ----------------------------------------------------------------
+// Entry e = q * width + h of an (nq, width) table names support row idx[e] when 0 <= idx[e] < ns
+// (the shadow index ns and negatives name none). The inverse lists, per support row s, the
+// entries naming s in ascending e: start[s] .. start[s + 1] - 1 index ent[], and pos[e] is the
+// CSR slot of entry e (-1 for a non-entry). count (int atomics: an exact count) -> one-block
+// exclusive scan -> fill through per-row cursors (arbitrary order) -> per-row rank sort.
+__global__ void __launch_bounds__(256)
+nbr_count_kernel(const int64_t* __restrict__ idx, int64_t n_ent, int64_t ns, int* __restrict__ cnt) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= n_ent) return;
+    const int64_t id = idx[e];
+    if (id >= 0 && id < ns) atomicAdd(cnt + id, 1);
+}
+
+// One 1024-thread block: thread t scans a contiguous run of rows; cnt becomes the fill cursors.
+__global__ void __launch_bounds__(1024)
+nbr_scan_kernel(int* __restrict__ cnt, int64_t ns, int* __restrict__ start) {
+    __shared__ int wtot[16];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int64_t per = (ns + 1023) / 1024;
+    const int64_t b = min(ns, (int64_t)t * per), e = min(ns, b + per);
+    int sum = 0;
+    for (int64_t i = b; i < e; ++i) sum += cnt[i];
+    int inc = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += v;
+    }
+    if (lane == 63) wtot[w] = inc;
+    __syncthreads();
+    int base = inc - sum;
+    for (int i = 0; i < w; ++i) base += wtot[i];
+    for (int64_t i = b; i < e; ++i) {
+        const int c = cnt[i];
+        start[i] = base;
+        cnt[i] = base;
+        base += c;
+    }
+    if (t == 1023) start[ns] = base;
+}
+
+__global__ void __launch_bounds__(256)
+nbr_fill_kernel(const int64_t* __restrict__ idx, int64_t n_ent, int64_t ns, int* __restrict__ cursor,
+                int* __restrict__ tmp) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= n_ent) return;
+    const int64_t id = idx[e];
+    if (id >= 0 && id < ns) tmp[atomicAdd(cursor + id, 1)] = (int)e;
+}
+
+// One wave per support row: entry keys are unique, so each one's rank in the row is the count
+// of smaller keys.
+__global__ void __launch_bounds__(256)
+nbr_sort_kernel(const int* __restrict__ start, int64_t ns, const int* __restrict__ tmp,
+                int* __restrict__ ent, int* __restrict__ pos) {
+    const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (s >= ns) return;
+    const int lane = threadIdx.x & 63;
+    const int b = start[s], n = start[s + 1] - b;
+    for (int j = lane; j < n; j += 64) {
+        const int key = tmp[b + j];
+        int rank = 0;
+        for (int i = 0; i < n; ++i) rank += tmp[b + i] < key ? 1 : 0;
+        ent[b + rank] = key;
+        pos[key] = b + rank;
+    }
+}
+
+// Segmented row sums over the inverse: dx[s, c] = sum_{j = start[s]}^{start[s+1]-1} g[j, c], in
+// slot (= ascending entry) order; rows nobody names get 0.
+__global__ void __launch_bounds__(256)
+csr_rowsum_kernel(const int* __restrict__ start, int64_t ns, const float* __restrict__ g, int cin,
+                  float* __restrict__ dx) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= ns * cin) return;
+    const int64_t s = t / cin;
+    const int c = (int)(t - s * cin);
+    const int b = start[s], e = start[s + 1];
+    float acc = 0.f;
+    for (int j = b; j < e; ++j) acc += g[(int64_t)j * cin + c];
+    dx[t] = acc;
+}
+
 // One wave per query: the valid neighbours of each 64-wide chunk are compacted by ballot and
 // their K influences computed once into LDS (the forward gather's recipe, kpconv.hip); then for
 // every 64-channel slice the query's dwf rows (K x 64) are held in registers and each valid
-// neighbour receives sum_k w_hk dwf[q, k, c] by one atomic add per channel.
+// neighbour's contribution sum_k w_hk dwf[q, k, c] is written to its CSR slot of the inverse
+// (g[pos[q * width + h], c]); csr_rowsum_kernel then adds each support row's slots in order.
 __global__ void __launch_bounds__(256)
-kpconv_scatter_kernel(const float* __restrict__ q, const float* __restrict__ s, int64_t nq, int64_t ns,
-                      const int64_t* __restrict__ idx, int width, const float* __restrict__ dwf,
-                      int cin, const float* __restrict__ kp_g, int n_kp, float inv_extent,
-                      float* __restrict__ dx) {
+kpconv_scatter_rows_kernel(const float* __restrict__ q, const float* __restrict__ s, int64_t nq,
+                           int64_t ns, const int64_t* __restrict__ idx, int width,
+                           const float* __restrict__ dwf, int cin, const float* __restrict__ kp_g,
+                           int n_kp, float inv_extent, const int* __restrict__ pos,
+                           float* __restrict__ g) {
     __shared__ float w_lds[4][64][kMaxKpT + 1];
-    __shared__ int nb_lds[4][64];
+    __shared__ int slot_lds[4][64];
     __shared__ float kp[3 * kMaxKpT];
     const int wv = threadIdx.x / 64, lane = threadIdx.x % 64;
     for (int i = threadIdx.x; i < 3 * n_kp; i += blockDim.x) kp[i] = kp_g[i];
@@ -63,7 +155,7 @@ kpconv_scatter_kernel(const float* __restrict__ q, const float* __restrict__ s, 
         if (v == 0) continue;
         if (valid) {
             const int p = __popcll(m & ((1ull << lane) - 1ull));
-            nb_lds[wv][p] = (int)id;
+            slot_lds[wv][p] = pos[qi * width + h];
             const float nx = s[3 * id] - qx, ny = s[3 * id + 1] - qy, nz = s[3 * id + 2] - qz;
             for (int k = 0; k < n_kp; ++k) w_lds[wv][p][k] = kp_w(nx, ny, nz, kp, k, inv_extent);
         }
@@ -76,29 +168,29 @@ kpconv_scatter_kernel(const float* __restrict__ q, const float* __restrict__ s, 
             for (int k = 0; k < kMaxKpT; ++k)
                 dw[k] = (act && k < n_kp) ? dq[(int64_t)k * cin + c] : 0.f;
             for (int hh = 0; hh < v; ++hh) {
-                float g = 0.f;
+                float acc = 0.f;
 #pragma unroll
                 for (int k = 0; k < kMaxKpT; ++k)
-                    if (k < n_kp) g = fmaf(w_lds[wv][hh][k], dw[k], g);
-                if (act) unsafeAtomicAdd(dx + (int64_t)nb_lds[wv][hh] * cin + c, g);
+                    if (k < n_kp) acc = fmaf(w_lds[wv][hh][k], dw[k], acc);
+                if (act) g[(int64_t)slot_lds[wv][hh] * cin + c] = acc;
             }
         }
         __builtin_amdgcn_wave_barrier();
     }
 }
 
-// Thread per (query, channel): the row's first maximum over x[idx[q, h], c] with shadow entries
-// reading 0 (the appended zero row, finegrained_kpconv_blocks.py:134-140); a real winner
-// receives dy[q, c].
+// Thread per (query, channel): the slot of the row's first maximum over x[idx[q, h], c] with
+// shadow entries reading 0 (the appended zero row, finegrained_kpconv_blocks.py:134-140); -1
+// when a shadow entry wins (its gradient goes nowhere).
 __global__ void __launch_bounds__(256)
-max_pool_bwd_kernel(const float* __restrict__ x, int64_t ns, int c, const int64_t* __restrict__ idx,
-                    int64_t nq, int width, const float* __restrict__ dy, float* __restrict__ dx) {
+max_pool_argmax_kernel(const float* __restrict__ x, int64_t ns, int c, const int64_t* __restrict__ idx,
+                       int64_t nq, int width, int* __restrict__ am) {
     const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (t >= nq * c) return;
     const int64_t qi = t / c;
     const int ch = (int)(t - qi * c);
     const int64_t* row = idx + qi * width;
-    int64_t arg = ns;
+    int arg = -1;
     float best = 0.f;
     for (int h = 0; h < width; ++h) {
         const int64_t id = row[h];
@@ -106,10 +198,31 @@ max_pool_bwd_kernel(const float* __restrict__ x, int64_t ns, int c, const int64_
         const float v = real ? x[id * c + ch] : 0.f;
         if (h == 0 || v > best) {
             best = v;
-            arg = real ? id : ns;
+            arg = real ? h : -1;
         }
     }
-    if (arg < ns) unsafeAtomicAdd(dx + arg * c + ch, dy[t]);
+    am[t] = arg;
+}
+
+// Thread per (support row, channel): the gradients of every (query, slot) entry naming the row
+// whose channel arg-max is that slot, in ascending entry order.
+__global__ void __launch_bounds__(256)
+max_pool_bwd_csr_kernel(const int* __restrict__ start, const int* __restrict__ ent, int64_t ns, int c,
+                        int width, const int* __restrict__ am, const float* __restrict__ dy,
+                        float* __restrict__ dx) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= ns * c) return;
+    const int64_t s = t / c;
+    const int ch = (int)(t - s * c);
+    float acc = 0.f;
+    for (int j = start[s]; j < start[s + 1]; ++j) {
+        const int e = ent[j];
+        const int64_t qi = e / width;
+        const int h = e - (int)(qi * width);
+        const int64_t qc = qi * c + ch;
+        if (am[qc] == h) acc += dy[qc];
+    }
+    dx[t] = acc;
 }
 
 // ---- per-(segment, channel) normalisation --------------------------------------------------
@@ -587,34 +700,322 @@ attn_bwd_dkdv_kernel(AttnBwd a) {
     }
 }
 
+// ---- CorrespondenceDecoder.simple_attention backward ----------------------------------------
+// corr[i] = sum_j P_ij v_j, P = softmax_j(s_ij), s_ij = scale q_i.k_j, v_j = the partner cloud's
+// xyz (3 columns, no gradient). With D_i = dO_i . corr_i and dS_ij = P_ij (dO_i . v_j - D_i):
+//   dq_i = scale sum_j dS_ij k_j,   dk_j = scale sum_i dS_ij q_i.
+// The forward kernel's layout (attention.hip corr_attention_kernel): 32 rows x 8 lanes per
+// block, each lane a D/8 slice of the dot products reduced over its 8 lanes with DPP, the other
+// side's rows staged 32 at a time through LDS; fp32, no atomics (kernel 2 owns its key rows).
+constexpr int kCbQ = 32;
+
+__device__ __forceinline__ float sum8(float s) {
+    s += dpp<0xB1>(s);
+    s += dpp<0x4E>(s);
+    s += dpp<0x141>(s);
+    return s;
+}
+
+struct CorrBwd {
+    const float* q; int64_t ld_q;
+    const float* k; int64_t ld_k;
+    const float* xyz;
+    const float* dout;
+    float* dq; int64_t ld_dq;
+    float* dk; int64_t ld_dk;
+    const int64_t* q_off;
+    const int64_t* kv_off;
+    const int32_t* kv_seg;
+    const int64_t* v_off;
+    int n_seg;
+    float scale;
+    float* lse;
+    float* dsum;
+};
+
+template <int D>
+__global__ void __launch_bounds__(256)
+corr_attn_bwd_dq_kernel(CorrBwd a) {
+    constexpr int DL = D / 8;
+    __shared__ float kt[kCbQ][D + 4];
+    __shared__ float vt[kCbQ][3];
+    const int seg = blockIdx.y;
+    const int64_t qb = a.q_off[seg], qe = a.q_off[seg + 1];
+    const int64_t q0 = qb + (int64_t)blockIdx.x * kCbQ;
+    if (q0 >= qe) return;                                  // block-uniform
+    const int ks = a.kv_seg[seg];
+    const int64_t kb = a.kv_off[ks], ke = a.kv_off[ks + 1];
+    const int64_t vb = a.v_off[ks];
+    const int tid = threadIdx.x, qi = tid >> 3, sl = tid & 7;
+    const int64_t row = q0 + qi;
+    const bool active = row < qe;
+    float qv[DL], dqv[DL];
+#pragma unroll
+    for (int e = 0; e < DL; ++e) {
+        qv[e] = active ? a.q[row * a.ld_q + sl * DL + e] * a.scale : 0.f;
+        dqv[e] = 0.f;
+    }
+    const float d0 = active ? a.dout[row * 3] : 0.f, d1 = active ? a.dout[row * 3 + 1] : 0.f,
+                d2 = active ? a.dout[row * 3 + 2] : 0.f;
+    float m = -INFINITY, l = 0.f, a0 = 0.f, a1 = 0.f, a2 = 0.f;
+    for (int pass = 0; pass < 2; ++pass) {
+        float inv_l = 0.f, dsum = 0.f;
+        if (pass == 1) {
+            inv_l = 1.0f / l;
+            dsum = d0 * (a0 * inv_l) + d1 * (a1 * inv_l) + d2 * (a2 * inv_l);   // dO . corr
+        }
+        for (int64_t j0 = kb; j0 < ke; j0 += kCbQ) {
+            const int nk = (int)min((int64_t)kCbQ, ke - j0);
+            __syncthreads();
+            for (int e = tid; e < kCbQ * D; e += 256) {
+                const int r = e / D, cc = e - r * D;
+                kt[r][cc] = r < nk ? a.k[(j0 + r) * a.ld_k + cc] : 0.f;
+            }
+            if (tid < kCbQ * 3) {
+                const int r = tid / 3, cc = tid - r * 3;
+                vt[r][cc] = r < nk ? a.xyz[(vb + (j0 - kb) + r) * 3 + cc] : 0.f;
+            }
+            __syncthreads();
+            for (int r = 0; r < nk; ++r) {
+                float s = 0.f;
+#pragma unroll
+                for (int e = 0; e < DL; ++e) s = fmaf(qv[e], kt[r][sl * DL + e], s);
+                s = sum8(s);
+                if (pass == 0) {                           // the forward's online softmax
+                    if (s > m) {
+                        const float f = __expf(m - s);
+                        l *= f; a0 *= f; a1 *= f; a2 *= f;
+                        m = s;
+                    }
+                    const float p = __expf(s - m);
+                    l += p;
+                    a0 = fmaf(p, vt[r][0], a0);
+                    a1 = fmaf(p, vt[r][1], a1);
+                    a2 = fmaf(p, vt[r][2], a2);
+                } else {
+                    const float p = __expf(s - m) * inv_l;
+                    const float dp = d0 * vt[r][0] + d1 * vt[r][1] + d2 * vt[r][2];
+                    const float ds = p * (dp - dsum);
+#pragma unroll
+                    for (int e = 0; e < DL; ++e) dqv[e] = fmaf(ds, kt[r][sl * DL + e], dqv[e]);
+                }
+            }
+        }
+        if (pass == 1 && active) {
+#pragma unroll
+            for (int e = 0; e < DL; ++e) a.dq[row * a.ld_dq + sl * DL + e] = dqv[e] * a.scale;
+            if (sl == 0) {
+                a.lse[row] = m + logf(l);
+                a.dsum[row] = dsum;
+            }
+        }
+    }
+}
+
+template <int D>
+__global__ void __launch_bounds__(256)
+corr_attn_bwd_dk_kernel(CorrBwd a) {
+    constexpr int DL = D / 8;
+    __shared__ float qt[kCbQ][D + 4];
+    __shared__ float dt[kCbQ][5];                          // dO (3), lse, D of each staged query
+    const int ks = blockIdx.y;
+    const int64_t kb = a.kv_off[ks], ke = a.kv_off[ks + 1];
+    const int64_t k0 = kb + (int64_t)blockIdx.x * kCbQ;
+    if (k0 >= ke) return;                                  // block-uniform
+    const int tid = threadIdx.x, ki = tid >> 3, sl = tid & 7;
+    const int64_t row = k0 + ki;
+    const bool active = row < ke;
+    float kv[DL], dkv[DL];
+#pragma unroll
+    for (int e = 0; e < DL; ++e) {
+        kv[e] = active ? a.k[row * a.ld_k + sl * DL + e] : 0.f;
+        dkv[e] = 0.f;
+    }
+    for (int seg = 0; seg < a.n_seg; ++seg) {
+        if (a.kv_seg[seg] != ks) continue;
+        const int64_t vb = a.v_off[ks] + (row - kb);
+        const float v0 = active ? a.xyz[vb * 3] : 0.f, v1 = active ? a.xyz[vb * 3 + 1] : 0.f,
+                    v2 = active ? a.xyz[vb * 3 + 2] : 0.f;
+        const int64_t qb = a.q_off[seg], qe = a.q_off[seg + 1];
+        for (int64_t i0 = qb; i0 < qe; i0 += kCbQ) {
+            const int nq = (int)min((int64_t)kCbQ, qe - i0);
+            __syncthreads();
+            for (int e = tid; e < kCbQ * D; e += 256) {
+                const int r = e / D, cc = e - r * D;
+                qt[r][cc] = r < nq ? a.q[(i0 + r) * a.ld_q + cc] * a.scale : 0.f;
+            }
+            if (tid < kCbQ) {
+                const bool ok = tid < nq;
+                const int64_t r = i0 + tid;
+                dt[tid][0] = ok ? a.dout[r * 3] : 0.f;
+                dt[tid][1] = ok ? a.dout[r * 3 + 1] : 0.f;
+                dt[tid][2] = ok ? a.dout[r * 3 + 2] : 0.f;
+                dt[tid][3] = ok ? a.lse[r] : 0.f;
+                dt[tid][4] = ok ? a.dsum[r] : 0.f;
+            }
+            __syncthreads();
+            for (int r = 0; r < nq; ++r) {
+                float s = 0.f;
+#pragma unroll
+                for (int e = 0; e < DL; ++e) s = fmaf(qt[r][sl * DL + e], kv[e], s);
+                s = sum8(s);
+                const float p = __expf(s - dt[r][3]);
+                const float dp = dt[r][0] * v0 + dt[r][1] * v1 + dt[r][2] * v2;
+                const float ds = p * (dp - dt[r][4]);
+#pragma unroll
+                for (int e = 0; e < DL; ++e) dkv[e] = fmaf(ds, qt[r][sl * DL + e], dkv[e]);   // qt = scale q
+            }
+        }
+    }
+    if (!active) return;
+#pragma unroll
+    for (int e = 0; e < DL; ++e) a.dk[row * a.ld_dk + sl * DL + e] = dkv[e];
+}
+
 }  // namespace
 }  // namespace fgr
 
 using namespace fgr;
 
+extern "C" int fgr_nbr_inverse_workspace(int64_t nq, int32_t width, int64_t ns, size_t* bytes) {
+    FGR_REQUIRE(bytes && nq >= 0 && width >= 0 && ns >= 0 && nq * (int64_t)width < (1ll << 31),
+                "fgr_nbr_inverse_workspace: bad arguments");
+    *bytes = (size_t)(ns + 1) * sizeof(int) + (size_t)nq * width * sizeof(int);
+    return FGR_OK;
+}
+
+extern "C" int fgr_nbr_inverse(const int64_t* idx, int64_t nq, int32_t width, int64_t ns, int32_t* start,
+                               int32_t* pos, int32_t* ent, void* ws, size_t ws_bytes, void* stream) {
+    FGR_REQUIRE(nq >= 0 && width >= 0 && ns >= 0 && nq * (int64_t)width < (1ll << 31),
+                "fgr_nbr_inverse: bad arguments");
+    FGR_REQUIRE(start && pos && ent && ws && (nq * width == 0 || idx), "fgr_nbr_inverse: null pointer");
+    size_t need = 0;
+    fgr_nbr_inverse_workspace(nq, width, ns, &need);
+    FGR_REQUIRE(ws_bytes >= need, "fgr_nbr_inverse: workspace %zu < %zu bytes", ws_bytes, need);
+    hipStream_t st = as_stream(stream);
+    const int64_t n_ent = nq * (int64_t)width;
+    int* cnt = (int*)ws;
+    int* tmp = cnt + (ns + 1);
+    FGR_CHECK_HIP(hipMemsetAsync(cnt, 0, (size_t)(ns + 1) * sizeof(int), st));
+    if (n_ent > 0)
+        FGR_CHECK_HIP(hipMemsetAsync(pos, 0xFF, (size_t)n_ent * sizeof(int), st));
+    const unsigned eb = (unsigned)std::max<int64_t>(1, ceil_div(n_ent, 256));
+    if (n_ent > 0) {
+        hipLaunchKernelGGL(nbr_count_kernel, dim3(eb), dim3(256), 0, st, idx, n_ent, ns, cnt);
+        FGR_CHECK_LAUNCH("nbr_count_kernel");
+    }
+    hipLaunchKernelGGL(nbr_scan_kernel, dim3(1), dim3(1024), 0, st, cnt, ns, start);
+    FGR_CHECK_LAUNCH("nbr_scan_kernel");
+    if (n_ent == 0 || ns == 0) return FGR_OK;
+    hipLaunchKernelGGL(nbr_fill_kernel, dim3(eb), dim3(256), 0, st, idx, n_ent, ns, cnt, tmp);
+    FGR_CHECK_LAUNCH("nbr_fill_kernel");
+    hipLaunchKernelGGL(nbr_sort_kernel, dim3((unsigned)ceil_div(ns, 4)), dim3(256), 0, st, start, ns,
+                       (const int*)tmp, ent, pos);
+    FGR_CHECK_LAUNCH("nbr_sort_kernel");
+    return FGR_OK;
+}
+
+extern "C" int fgr_kpconv_scatter_workspace(int64_t nq, int32_t width, int32_t cin, size_t* bytes) {
+    FGR_REQUIRE(bytes && nq >= 0 && width >= 0 && cin > 0, "fgr_kpconv_scatter_workspace: bad arguments");
+    *bytes = std::max<size_t>(1, (size_t)nq * width * cin * sizeof(float));
+    return FGR_OK;
+}
+
 extern "C" int fgr_kpconv_scatter(const float* q, const float* s, int64_t nq, int64_t ns,
                                   const int64_t* idx, int32_t width, const float* dwf, int32_t cin,
-                                  const float* kernel_points, int32_t n_kp, float extent, float* dx,
-                                  void* stream) {
+                                  const float* kernel_points, int32_t n_kp, float extent,
+                                  const int32_t* start, const int32_t* pos, float* dx, void* ws,
+                                  size_t ws_bytes, void* stream) {
     FGR_REQUIRE(nq >= 0 && ns >= 0 && width >= 0 && cin > 0 && n_kp > 0 && n_kp <= kMaxKpT &&
                     extent > 0.f, "fgr_kpconv_scatter: bad arguments");
-    if (nq == 0 || width == 0) return FGR_OK;
-    FGR_REQUIRE(q && s && idx && dwf && kernel_points && dx, "fgr_kpconv_scatter: null pointer");
-    hipLaunchKernelGGL(kpconv_scatter_kernel, dim3((unsigned)ceil_div(nq, 4)), dim3(256), 0,
-                       as_stream(stream), q, s, nq, ns, idx, width, dwf, cin, kernel_points, n_kp,
-                       1.0f / extent, dx);
-    FGR_CHECK_LAUNCH("kpconv_scatter_kernel");
+    if (ns == 0) return FGR_OK;
+    FGR_REQUIRE(start && dx && ws, "fgr_kpconv_scatter: null pointer");
+    size_t need = 0;
+    fgr_kpconv_scatter_workspace(nq, width, cin, &need);
+    FGR_REQUIRE(ws_bytes >= need, "fgr_kpconv_scatter: workspace %zu < %zu bytes", ws_bytes, need);
+    hipStream_t st = as_stream(stream);
+    float* g = (float*)ws;
+    if (nq > 0 && width > 0) {
+        FGR_REQUIRE(q && s && idx && dwf && kernel_points && pos, "fgr_kpconv_scatter: null pointer");
+        hipLaunchKernelGGL(kpconv_scatter_rows_kernel, dim3((unsigned)ceil_div(nq, 4)), dim3(256), 0, st,
+                           q, s, nq, ns, idx, width, dwf, cin, kernel_points, n_kp, 1.0f / extent,
+                           (const int*)pos, g);
+        FGR_CHECK_LAUNCH("kpconv_scatter_rows_kernel");
+    }
+    hipLaunchKernelGGL(csr_rowsum_kernel, dim3((unsigned)ceil_div(ns * cin, 256)), dim3(256), 0, st,
+                       (const int*)start, ns, (const float*)g, cin, dx);
+    FGR_CHECK_LAUNCH("csr_rowsum_kernel");
+    return FGR_OK;
+}
+
+extern "C" int fgr_max_pool_bwd_workspace(int64_t nq, int32_t c, size_t* bytes) {
+    FGR_REQUIRE(bytes && nq >= 0 && c > 0, "fgr_max_pool_bwd_workspace: bad arguments");
+    *bytes = std::max<size_t>(1, (size_t)nq * c * sizeof(int));
     return FGR_OK;
 }
 
 extern "C" int fgr_max_pool_bwd(const float* x, int64_t ns, int32_t c, const int64_t* idx, int64_t nq,
-                                int32_t width, const float* dy, float* dx, void* stream) {
+                                int32_t width, const float* dy, const int32_t* start,
+                                const int32_t* ent, float* dx, void* ws, size_t ws_bytes,
+                                void* stream) {
     FGR_REQUIRE(ns >= 0 && nq >= 0 && c > 0 && width > 0, "fgr_max_pool_bwd: bad arguments");
-    if (nq == 0) return FGR_OK;
-    FGR_REQUIRE(x && idx && dy && dx, "fgr_max_pool_bwd: null pointer");
-    hipLaunchKernelGGL(max_pool_bwd_kernel, dim3((unsigned)ceil_div(nq * c, 256)), dim3(256), 0,
-                       as_stream(stream), x, ns, c, idx, nq, width, dy, dx);
-    FGR_CHECK_LAUNCH("max_pool_bwd_kernel");
+    if (ns == 0) return FGR_OK;
+    FGR_REQUIRE(start && ent && dx && ws && (nq == 0 || (x && idx && dy)), "fgr_max_pool_bwd: null pointer");
+    size_t need = 0;
+    fgr_max_pool_bwd_workspace(nq, c, &need);
+    FGR_REQUIRE(ws_bytes >= need, "fgr_max_pool_bwd: workspace %zu < %zu bytes", ws_bytes, need);
+    hipStream_t st = as_stream(stream);
+    int* am = (int*)ws;
+    if (nq > 0) {
+        hipLaunchKernelGGL(max_pool_argmax_kernel, dim3((unsigned)ceil_div(nq * c, 256)), dim3(256), 0, st,
+                           x, ns, c, idx, nq, width, am);
+        FGR_CHECK_LAUNCH("max_pool_argmax_kernel");
+    }
+    hipLaunchKernelGGL(max_pool_bwd_csr_kernel, dim3((unsigned)ceil_div(ns * c, 256)), dim3(256), 0, st,
+                       (const int*)start, (const int*)ent, ns, c, width, (const int*)am, dy, dx);
+    FGR_CHECK_LAUNCH("max_pool_bwd_csr_kernel");
+    return FGR_OK;
+}
+
+extern "C" int fgr_corr_attention_bwd_workspace(int64_t n_rows, size_t* bytes) {
+    FGR_REQUIRE(bytes && n_rows >= 0, "fgr_corr_attention_bwd_workspace: bad arguments");
+    *bytes = (size_t)std::max<int64_t>(n_rows, 1) * 2 * sizeof(float);
+    return FGR_OK;
+}
+
+extern "C" int fgr_corr_attention_bwd(const float* q, int64_t ld_q, const float* k, int64_t ld_k,
+                                      const float* xyz, const float* dout, float* dq, int64_t ld_dq,
+                                      float* dk, int64_t ld_dk, const int64_t* q_off,
+                                      const int64_t* kv_off, const int32_t* kv_seg,
+                                      const int64_t* v_off, int32_t n_seg, int32_t n_kv_seg,
+                                      int64_t n_rows, int32_t max_q_len, int32_t max_kv_len, int32_t d,
+                                      float scale, void* ws, size_t ws_bytes, void* stream) {
+    FGR_REQUIRE(n_seg > 0 && n_kv_seg > 0 && n_rows >= 0 && max_q_len >= 0 && max_kv_len >= 0 &&
+                    ld_q >= d && ld_k >= d && ld_dq >= d && ld_dk >= d,
+                "fgr_corr_attention_bwd: bad arguments");
+    FGR_REQUIRE(d == 32 || d == 64 || d == 128 || d == 256 || d == 512,
+                "fgr_corr_attention_bwd: d %d unsupported (32, 64, 128, 256, 512)", d);
+    FGR_REQUIRE(q && k && xyz && dout && dq && dk && q_off && kv_off && kv_seg && v_off && ws,
+                "fgr_corr_attention_bwd: null pointer");
+    size_t need = 0;
+    fgr_corr_attention_bwd_workspace(n_rows, &need);
+    FGR_REQUIRE(ws_bytes >= need, "fgr_corr_attention_bwd: workspace %zu < %zu bytes", ws_bytes, need);
+    const int64_t nr = std::max<int64_t>(n_rows, 1);
+    CorrBwd a{q, ld_q, k, ld_k, xyz, dout, dq, ld_dq, dk, ld_dk, q_off, kv_off, kv_seg, v_off, n_seg,
+              scale, (float*)ws, (float*)ws + nr};
+    hipStream_t st = as_stream(stream);
+    const dim3 g1((unsigned)std::max<int64_t>(1, ceil_div(max_q_len, kCbQ)), (unsigned)n_seg);
+    const dim3 g2((unsigned)std::max<int64_t>(1, ceil_div(max_kv_len, kCbQ)), (unsigned)n_kv_seg);
+    switch (d) {
+#define CAB(DD) case DD: \
+        hipLaunchKernelGGL(corr_attn_bwd_dq_kernel<DD>, g1, dim3(256), 0, st, a); \
+        FGR_CHECK_LAUNCH("corr_attn_bwd_dq_kernel"); \
+        hipLaunchKernelGGL(corr_attn_bwd_dk_kernel<DD>, g2, dim3(256), 0, st, a); \
+        break;
+        CAB(32) CAB(64) CAB(128) CAB(256) CAB(512)
+#undef CAB
+    }
+    FGR_CHECK_LAUNCH("corr_attn_bwd_dk_kernel");
     return FGR_OK;
 }
 

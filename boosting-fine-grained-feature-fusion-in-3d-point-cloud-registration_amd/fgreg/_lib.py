@@ -18,6 +18,8 @@ _i64 = ctypes.c_int64
 _f32 = ctypes.c_float
 _sz = ctypes.c_size_t
 
+ABI_VERSION = 2     # FGR_ABI_VERSION of include/fgreg.h (INTEGRATION.md "ABI history")
+
 # name -> argtypes (all return int status)
 SIGNATURES = {
     'fgr_grid_subsample_workspace': [_i64, _i32, _i64, ctypes.POINTER(_sz)],
@@ -83,8 +85,16 @@ SIGNATURES = {
     'fgr_procrustes': [_vp, _vp, _vp, _i64, _i64, _f32, _vp, _vp],
     'fgr_time_next_call': [_vp, _vp],
     'fgr_pair_pose': [_vp, _vp, _vp, _i64, _vp, _i32, _i32, _f32, _vp, _vp],
-    'fgr_kpconv_scatter': [_vp, _vp, _i64, _i64, _vp, _i32, _vp, _i32, _vp, _i32, _f32, _vp, _vp],
-    'fgr_max_pool_bwd': [_vp, _i64, _i32, _vp, _i64, _i32, _vp, _vp, _vp],
+    'fgr_nbr_inverse_workspace': [_i64, _i32, _i64, ctypes.POINTER(_sz)],
+    'fgr_nbr_inverse': [_vp, _i64, _i32, _i64, _vp, _vp, _vp, _vp, _sz, _vp],
+    'fgr_kpconv_scatter_workspace': [_i64, _i32, _i32, ctypes.POINTER(_sz)],
+    'fgr_kpconv_scatter': [_vp, _vp, _i64, _i64, _vp, _i32, _vp, _i32, _vp, _i32, _f32, _vp, _vp,
+                           _vp, _vp, _sz, _vp],
+    'fgr_max_pool_bwd_workspace': [_i64, _i32, ctypes.POINTER(_sz)],
+    'fgr_max_pool_bwd': [_vp, _i64, _i32, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _sz, _vp],
+    'fgr_corr_attention_bwd_workspace': [_i64, ctypes.POINTER(_sz)],
+    'fgr_corr_attention_bwd': [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp,
+                               _vp, _i32, _i32, _i64, _i32, _i32, _i32, _f32, _vp, _sz, _vp],
     'fgr_segnorm_workspace': [_i64, _i32, _i32, ctypes.POINTER(_sz)],
     'fgr_segnorm_stats': [_vp, _i64, _i32, _vp, _i32, _i64, _vp, _f32, _vp, _vp, _vp, _vp, _sz, _vp],
     'fgr_segnorm_apply': [_vp, _i64, _i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _i32, _vp,
@@ -130,12 +140,14 @@ def load():
     L = ctypes.CDLL(LIB_PATH)
     L.fgr_abi_version.restype = ctypes.c_int
     L.fgr_last_error.restype = ctypes.c_char_p
+    # version first: a stale library fails here, not on a missing symbol below
+    if L.fgr_abi_version() != ABI_VERSION:
+        raise FgrError(f'libfgreg ABI version mismatch: {LIB_PATH} has {L.fgr_abi_version()}, '
+                       f'fgreg expects {ABI_VERSION} (rebuild: make -C {CSRC})')
     for name, argtypes in SIGNATURES.items():
         fn = getattr(L, name)
         fn.restype = ctypes.c_int
         fn.argtypes = argtypes
-    if L.fgr_abi_version() != 1:
-        raise FgrError('libfgreg ABI version mismatch')
     _lib = L
     return L
 

@@ -11,7 +11,7 @@ Each op is a ``torch.autograd.Function`` whose forward AND backward run in libfg
                     265-399 up to the division, which the following norm applies): backward
                     d_wf = dout W2^T (GEMM), dW = wf^T dout (GEMM; wf regathered, not kept),
                     dx = fgr_kpconv_scatter(d_wf) (the scatter-add of the reference's
-                    ``gather(method=2)``, :66-97);
+                    ``gather(method=2)``, :66-97, as a gather over the table's inverse);
 * ``segnorm_t``     per-(segment, channel) normalisation with batch statistics
                     (fgr_segnorm_*): InstanceNorm per cloud (BatchNormBlock, :462-518) and the
                     Res2Net BatchNorm1d in train() (res2net.py:126-159, one segment + affine,
@@ -19,7 +19,12 @@ Each op is a ``torch.autograd.Function`` whose forward AND backward run in libfg
 * ``layernorm_t``   nn.LayerNorm (+ the positional add) -> fgr_layernorm / fgr_layernorm_bwd;
 * ``attention_t``   the packed-segment MHA core on the fused QKV tensor -> fgr_attention_f16x3
                     forward, fgr_attention_bwd backward;
-* ``max_pool_t``    max_pool (:125-141) -> fgr_max_pool / fgr_max_pool_bwd.
+* ``max_pool_t``    max_pool (:125-141) -> fgr_max_pool / fgr_max_pool_bwd;
+* ``corr_attention_t`` the CorrespondenceDecoder head's simple_attention (finegrained_regtr.py:
+                    328-363) -> fgr_corr_attention / fgr_corr_attention_bwd.
+Both scatters (KPConv dx, max-pool dx) read the neighbour table's CSR inverse (fgr_nbr_inverse,
+built once per table): no floating-point atomics anywhere, so a backward pass is bit-for-bit
+reproducible.
 Elementwise glue between them (ReLU masks, the bottleneck's LeakyReLU(x + shortcut),
 concatenation) is torch on the same device. No CPU path: every op raises on host tensors.
 """
@@ -29,6 +34,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _lib, ops
+from . import linear as lin
 from .linear import linear
 from .ops import ACT_LEAKY, ACT_NONE, ACT_RELU, _c, _dev, _ptr, _stream
 
@@ -60,6 +66,7 @@ class _LinearFn(torch.autograd.Function):
     def forward(ctx, x, w, b, residual, act):
         assert act in (ACT_NONE, ACT_RELU)
         y = linear(x, w, b, act=act, residual=residual)
+        ctx.mode = lin.MODE          # the backward's products run in the forward's mode
         ctx.act, ctx.has_b, ctx.has_r = act, b is not None, residual is not None
         ctx.save_for_backward(x, w, y if act == ACT_RELU else None)
         return y
@@ -71,10 +78,11 @@ class _LinearFn(torch.autograd.Function):
         if ctx.act == ACT_RELU:
             dy = _relu_mask(dy, y)
         dx = dw = db = None
-        if ctx.needs_input_grad[0]:
-            dx = linear(dy, w, transpose=True, tag='bwd_dx')          # dY W
-        if ctx.needs_input_grad[1]:
-            dw = linear(dy.t().contiguous(), x, transpose=True, cache=False)   # dY^T X
+        with lin.mode_scope(ctx.mode):
+            if ctx.needs_input_grad[0]:
+                dx = linear(dy, w, transpose=True, tag='bwd_dx')          # dY W
+            if ctx.needs_input_grad[1]:
+                dw = linear(dy.t().contiguous(), x, transpose=True, cache=False)   # dY^T X
         if ctx.has_b and ctx.needs_input_grad[2]:
             db = colsum(dy)
         dres = dy if ctx.has_r and ctx.needs_input_grad[3] else None
@@ -91,11 +99,59 @@ def linear_t(x, w, b=None, act=ACT_NONE, residual=None):
 # ------------------------------------------------------------------------------------------
 # KPConv
 # ------------------------------------------------------------------------------------------
+def nbr_inverse(idx: torch.Tensor, ns: int):
+    """-> (start (ns + 1,), pos (nq * width,), ent (nq * width,)) int32: the CSR inverse of the
+    neighbour table idx over ns support rows (fgr_nbr_inverse: per support row, the entries
+    q * width + h naming it in ascending order). Cached on the table tensor (a kpconv_meta
+    table is shared by every conv / pool of its level and never written in place)."""
+    _dev(idx)
+    idx = _c(idx, torch.int64)
+    cache = getattr(idx, '_fgr_inverse', None)
+    if cache is not None and cache[0] == (ns, idx._version):
+        return cache[1]
+    nq, width = idx.shape
+    dev = idx.device
+    start = torch.empty(ns + 1, dtype=torch.int32, device=dev)
+    pos = torch.empty(max(nq * width, 1), dtype=torch.int32, device=dev)
+    ent = torch.empty_like(pos)
+    L = _lib.load()
+    nb = _lib._sz(0)
+    _lib.check(L.fgr_nbr_inverse_workspace(nq, width, ns, nb), 'fgr_nbr_inverse_workspace')
+    ws = torch.empty(max(nb.value, 1), dtype=torch.uint8, device=dev)
+    _lib.check(L.fgr_nbr_inverse(_ptr(idx), nq, width, ns, _ptr(start), _ptr(pos), _ptr(ent),
+                                 _ptr(ws), nb.value, _stream()), 'fgr_nbr_inverse')
+    res = (start, pos, ent)
+    idx._fgr_inverse = ((ns, idx._version), res)
+    return res
+
+
+def kpconv_scatter(q, s, idx, dwf, kp, extent):
+    """dx (ns, cin) of the KPConv gather from d_wf (nq, K * cin): fgr_kpconv_scatter over the
+    table's inverse (deterministic: each support row adds its entries in CSR order)."""
+    _dev(q, s, idx, dwf, kp)
+    nq, width = idx.shape
+    ns = s.shape[0]
+    K = kp.shape[0]
+    cin = dwf.shape[1] // K
+    start, pos, _ = nbr_inverse(idx, ns)
+    dx = torch.empty((ns, cin), dtype=torch.float32, device=dwf.device)
+    L = _lib.load()
+    nb = _lib._sz(0)
+    _lib.check(L.fgr_kpconv_scatter_workspace(nq, width, cin, nb), 'fgr_kpconv_scatter_workspace')
+    ws = torch.empty(nb.value, dtype=torch.uint8, device=dwf.device)
+    _lib.check(L.fgr_kpconv_scatter(
+        _ptr(_c(q, torch.float32)), _ptr(_c(s, torch.float32)), nq, ns, _ptr(_c(idx, torch.int64)),
+        width, _ptr(dwf), cin, _ptr(_c(kp, torch.float32)), K, float(extent), _ptr(start),
+        _ptr(pos), _ptr(dx), _ptr(ws), nb.value, _stream()), 'fgr_kpconv_scatter')
+    return dx
+
+
 class _KPConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, W, q, s, idx, kp, extent):
         wf, nnorm = ops.kpconv_gather(q, s, idx, x, kp, extent)
         out = linear(wf.view(wf.shape[0], -1), W, transpose=True)
+        ctx.mode = lin.MODE
         ctx.extent = float(extent)
         ctx.save_for_backward(x, W, q, s, idx, kp)
         ctx.mark_non_differentiable(nnorm)
@@ -108,18 +164,15 @@ class _KPConvFn(torch.autograd.Function):
         nq = q.shape[0]
         K, cin, cout = W.shape
         dx = dW = None
-        if ctx.needs_input_grad[0]:
-            dwf = linear(dout, W, transpose='flat', tag='bwd_dwf')           # (nq, K * cin)
-            dx = torch.zeros_like(x)
-            _dev(q, s, idx, dwf, kp, dx)
-            _lib.check(_lib.load().fgr_kpconv_scatter(
-                _ptr(_c(q, torch.float32)), _ptr(_c(s, torch.float32)), nq, s.shape[0],
-                _ptr(_c(idx, torch.int64)), idx.shape[1], _ptr(dwf), cin, _ptr(_c(kp, torch.float32)),
-                K, ctx.extent, _ptr(dx), _stream()), 'fgr_kpconv_scatter')
-        if ctx.needs_input_grad[1]:
-            wf, _ = ops.kpconv_gather(q, s, idx, x, kp, ctx.extent)          # regathered
-            dWt = linear(dout.t().contiguous(), wf.view(nq, K * cin), transpose=True, cache=False)
-            dW = dWt.t().reshape(K, cin, cout)                               # (dout^T wf)^T
+        with lin.mode_scope(ctx.mode):
+            if ctx.needs_input_grad[0]:
+                dwf = linear(dout, W, transpose='flat', tag='bwd_dwf')       # (nq, K * cin)
+                dx = kpconv_scatter(q, s, idx, dwf, kp, ctx.extent)
+            if ctx.needs_input_grad[1]:
+                wf, _ = ops.kpconv_gather(q, s, idx, x, kp, ctx.extent)      # regathered
+                dWt = linear(dout.t().contiguous(), wf.view(nq, K * cin), transpose=True,
+                             cache=False)
+                dW = dWt.t().reshape(K, cin, cout)                           # (dout^T wf)^T
         return dx, dW, None, None, None, None, None
 
 
@@ -138,11 +191,18 @@ class _MaxPoolFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, idx = ctx.saved_tensors
-        dy = dy.contiguous()
-        dx = torch.zeros_like(x)
-        _lib.check(_lib.load().fgr_max_pool_bwd(_ptr(x.contiguous()), x.shape[0], x.shape[1],
-                                                _ptr(idx.contiguous()), idx.shape[0], idx.shape[1],
-                                                _ptr(dy), _ptr(dx), _stream()), 'fgr_max_pool_bwd')
+        x, dy = x.contiguous(), dy.contiguous()
+        ns, c = x.shape
+        nq, width = idx.shape
+        start, _, ent = nbr_inverse(idx, ns)
+        dx = torch.empty_like(x)
+        L = _lib.load()
+        nb = _lib._sz(0)
+        _lib.check(L.fgr_max_pool_bwd_workspace(nq, c, nb), 'fgr_max_pool_bwd_workspace')
+        ws = torch.empty(nb.value, dtype=torch.uint8, device=x.device)
+        _lib.check(L.fgr_max_pool_bwd(_ptr(x), ns, c, _ptr(idx.contiguous()), nq, width, _ptr(dy),
+                                      _ptr(start), _ptr(ent), _ptr(dx), _ptr(ws), nb.value,
+                                      _stream()), 'fgr_max_pool_bwd')
         return dx, None
 
 
@@ -304,6 +364,44 @@ def attention_t(qkv, off, kv_seg, max_len, nhead):
     """Packed-segment MHA core on a fused (N, 3d) [q | k | v] tensor: query segment i attends
     to key segment kv_seg[i] (self- or cross-attention over one segmentation)."""
     return _AttentionFn.apply(qkv, off, kv_seg, max_len, nhead)
+
+
+class _CorrAttentionFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, xyz, q_off, kv_seg, v_off, max_len, scale):
+        q, k = _c(q, torch.float32), _c(k, torch.float32)
+        corr = ops.corr_attention(q, k, xyz, q_off, q_off, kv_seg, v_off, max_len, scale)
+        ctx.meta = (int(max_len), float(scale))
+        ctx.save_for_backward(q, k, xyz, q_off, kv_seg, v_off)
+        return corr
+
+    @staticmethod
+    def backward(ctx, dcorr):
+        q, k, xyz, q_off, kv_seg, v_off = ctx.saved_tensors
+        max_len, scale = ctx.meta
+        dcorr = _c(dcorr, torch.float32)
+        n, d = q.shape
+        dq = torch.zeros_like(q)
+        dk = torch.zeros_like(k)
+        L = _lib.load()
+        nb = _lib._sz(0)
+        _lib.check(L.fgr_corr_attention_bwd_workspace(n, nb), 'fgr_corr_attention_bwd_workspace')
+        ws = torch.empty(nb.value, dtype=torch.uint8, device=q.device)
+        n_seg = q_off.numel() - 1
+        _lib.check(L.fgr_corr_attention_bwd(
+            _ptr(q), q.stride(0), _ptr(k), k.stride(0), _ptr(_c(xyz, torch.float32)), _ptr(dcorr),
+            _ptr(dq), dq.stride(0), _ptr(dk), dk.stride(0), _ptr(q_off), _ptr(q_off), _ptr(kv_seg),
+            _ptr(v_off), n_seg, n_seg, n, max_len, max_len, d, scale, _ptr(ws), nb.value,
+            _stream()), 'fgr_corr_attention_bwd')
+        return dq, dk, None, None, None, None, None, None
+
+
+def corr_attention_t(q, k, xyz, seg, scale):
+    """CorrespondenceDecoder.simple_attention (finegrained_regtr.py:328-363) over the (layer,
+    cloud) segments of ``seg.layer_tables``: softmax(q.k scale) weighted partner coordinates,
+    differentiable in q and k (fgr_corr_attention / fgr_corr_attention_bwd)."""
+    q_off, kv_seg, v_off = seg.layer_tables
+    return _CorrAttentionFn.apply(q, k, xyz, q_off, kv_seg, v_off, seg.max_len, scale)
 
 
 def leaky(x):

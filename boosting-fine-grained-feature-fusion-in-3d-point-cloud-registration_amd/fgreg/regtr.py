@@ -171,6 +171,8 @@ class RegTR(nn.Module):
         and backward kernels (train.py's loss.backward())."""
         dev = batch['src_xyz'][0].device
         if self.training:
+            from .training import check_trainable
+            check_trainable(self)
             if dev.type != 'cuda':      # the ops raise FgrError on host tensors (no CPU path)
                 return self._forward(batch, train=True)
             with torch.cuda.device(dev):

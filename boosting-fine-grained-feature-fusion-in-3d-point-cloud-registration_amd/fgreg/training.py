@@ -11,11 +11,14 @@ outputs as the inference forward (models/finegrained_regtr.py:108-250), with
 The pose is computed without gradients (the reference's losses never read it,
 finegrained_regtr.py:252-309).
 """
+import math
+
 import torch
 
 from . import ops
-from .autograd import (attention_t, batchnorm_t, kpconv_t, layernorm_t, leaky, linear_t,
-                       max_pool_t, segnorm_t)
+from . import linear as lin
+from .autograd import (attention_t, batchnorm_t, corr_attention_t, kpconv_t, layernorm_t, leaky,
+                       linear_t, max_pool_t, segnorm_t)
 from .backbone import ResnetBottleneckBlock, SimpleBlock, UnaryBlock, _level_inputs, host_layout
 from .ops import ACT_LEAKY, ACT_NONE, ACT_RELU
 
@@ -93,16 +96,29 @@ def _layer_post_train(layer, x, pos, seg):
     return layernorm_t(linear_t(h, layer.linear2.weight, layer.linear2.bias, residual=x), layer.norm3)
 
 
-def core_train(model, meta, seg, B):
-    """RegTR._core in training mode -> (feats_un, feats (L, N, d), corr, logits, pose)."""
-    from .regtr import CorrespondenceRegressor
+def check_trainable(model):
+    """Raises NotImplementedError for configurations this training forward does not restate
+    (checked before any work, so CPU and GPU callers see the same error)."""
     cfg = model.cfg
     if not (cfg.sa_val_has_pos_emb and cfg.ca_val_has_pos_emb):
         raise NotImplementedError('training with value-without-positional-embedding attention is '
                                   'not in the reference configs')
-    if not isinstance(model.correspondence_decoder, CorrespondenceRegressor):
-        raise NotImplementedError('training the CorrespondenceDecoder head (direct_regress_coor: '
-                                  'False) is not in the reference configs')
+    if float(cfg.get('dropout', 0.0) or 0.0) > 0.0:
+        # transformers.py:102-110, 201-238 apply dropout1/2/3 and the MHA's own dropout in
+        # train(); every shipped config sets 0.0 (conf/*.yaml), and this forward has none
+        raise NotImplementedError(f'training with dropout {cfg.dropout} > 0 (the reference '
+                                  'configs train with 0.0)')
+    if getattr(model.correspondence_decoder, 'num_neighbors', 0) > 0:
+        raise NotImplementedError('training the CorrespondenceDecoder with num_neighbors > 0 (a '
+                                  'constructor argument the reference RegTR never passes)')
+
+
+def core_train(model, meta, seg, B):
+    """RegTR._core in training mode -> (feats_un, feats (L, N, d), corr, logits, pose)."""
+    from .regtr import HEAD_MODE, CorrespondenceRegressor
+    cfg = model.cfg
+    check_trainable(model)
+    head = model.correspondence_decoder
     pts0 = meta['points'][0]
     x = torch.ones((pts0.shape[0], 1), dtype=torch.float32, device=pts0.device)
     for block in model.kpf_encoder.encoder_blocks:
@@ -121,13 +137,22 @@ def core_train(model, meta, seg, B):
             inter.append(layernorm_t(h, enc.norm) if enc.norm is not None else h)
     feats = torch.stack(inter, 0)                                          # (L, N, d)
     L, N, d = feats.shape
-    head = model.correspondence_decoder
     f = feats.reshape(L * N, d)
-    m = head.coor_mlp
-    t = linear_t(f, m[0].weight, m[0].bias, act=ACT_RELU)
-    t = linear_t(t, m[2].weight, m[2].bias, act=ACT_RELU)
-    corr = linear_t(t, m[4].weight, m[4].bias).view(L, N, 3)
-    logits = linear_t(f, head.conf_logits_decoder.weight, head.conf_logits_decoder.bias).view(L, N, 1)
+    if isinstance(head, CorrespondenceRegressor):                          # :411-455
+        # the inference head's compute mode (regtr.py CorrespondenceRegressor.forward_packed)
+        with lin.mode_scope(HEAD_MODE if lin.MODE == 'bf16' else None):
+            m = head.coor_mlp
+            t = linear_t(f, m[0].weight, m[0].bias, act=ACT_RELU)
+            t = linear_t(t, m[2].weight, m[2].bias, act=ACT_RELU)
+            corr = linear_t(t, m[4].weight, m[4].bias)
+            logits = linear_t(f, head.conf_logits_decoder.weight, head.conf_logits_decoder.bias)
+    else:                                                                  # :312-408
+        fq = (feats + pe.unsqueeze(0) if head.use_pos_emb else feats).reshape(L * N, d)
+        q = linear_t(fq, head.q_proj.weight, head.q_proj.bias)
+        k = linear_t(fq, head.k_proj.weight, head.k_proj.bias)
+        corr = corr_attention_t(q, k, xyz_c, seg, 1.0 / math.sqrt(d))     # q_proj(.) / sqrt(D)
+        logits = linear_t(f, head.conf_logits_decoder.weight, head.conf_logits_decoder.bias)
+    corr, logits = corr.view(L, N, 3), logits.view(L, N, 1)
     with torch.no_grad():
         pose = ops.pair_pose(xyz_c, corr.detach(), logits.detach()[..., 0], seg.off, B,
                              model.pose_threshold)

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define FGR_ABI_VERSION 1
+#define FGR_ABI_VERSION 2
 
 enum {
     FGR_OK = 0,
@@ -444,14 +444,27 @@ int fgr_crop_pairs_assemble(const float* raw, int32_t ld, const int64_t* offsets
 
 /* ---- Training backward (train.py -> trainer.py:110-125 backward) -------
  * The dense products' gradients run on the GEMM entry points above with transposed weight
- * images (fgreg/autograd.py); these cover the rest. The two scatters add with fp32 global
- * atomics (exact up to fp32 rounding, order may vary between runs); every reduction is
- * deterministic (fixed-order fp64 partials).
- *  fgr_kpconv_scatter   KPConv gather-weight backward: dx[idx[q,h], c] += sum_k w(q,h,k)
- *                       dwf[q,k,c] with the forward's influences (finegrained_kpconv_blocks.py:
- *                       296-381; the reference's gather(method=2), :66-97). dx is accumulated.
- *  fgr_max_pool_bwd     max_pool (:125-141): dx[arg, c] += dy[q, c], arg = the row's first
- *                       maximum (shadow entries read 0 and receive nothing). dx is accumulated.
+ * images (fgreg/autograd.py); these cover the rest. Every entry point is deterministic: no
+ * floating-point atomics, every reduction in a fixed order (ABI 2; ABI 1's two scatters added
+ * with fp32 atomics).
+ *  fgr_nbr_inverse      the inverse (CSR) of an (nq, width) neighbour table over ns support rows:
+ *                       start[ns + 1], and for support row s the entries e = q * width + h with
+ *                       idx[e] == s in ascending e at ent[start[s] .. start[s + 1]); pos[e] = the
+ *                       CSR slot of entry e, -1 where idx[e] names no support row (shadow index
+ *                       / negative). ent and pos hold nq * width ints; workspace
+ *                       fgr_nbr_inverse_workspace bytes. Built once per table, read by both
+ *                       scatters below (the reference's gather(method=2) transpose,
+ *                       finegrained_kpconv_blocks.py:66-97, as a gather over the inverse).
+ *  fgr_kpconv_scatter   KPConv gather-weight backward: dx[s, c] = sum over the entries (q, h)
+ *                       naming s, in CSR order, of sum_k w(q,h,k) dwf[q,k,c] with the forward's
+ *                       influences (finegrained_kpconv_blocks.py:296-381). dx (ns, cin) is
+ *                       WRITTEN (rows nobody names get 0); start / pos from fgr_nbr_inverse of
+ *                       idx; workspace fgr_kpconv_scatter_workspace bytes (one cin-row per
+ *                       table entry).
+ *  fgr_max_pool_bwd     max_pool (:125-141): dx[s, c] = sum of dy[q, c] over the entries (q, h)
+ *                       naming s whose slot h is the row's first maximum of channel c (shadow
+ *                       entries read 0 and pass nothing on). dx (ns, c) is WRITTEN; start / ent
+ *                       from fgr_nbr_inverse of idx; workspace fgr_max_pool_bwd_workspace.
  *  fgr_segnorm_stats    per-(segment, channel) mean / rstd / biased var of v = x / row_div:
  *                       InstanceNorm1d per cloud (:498-507) or BatchNorm1d batch statistics
  *                       (one segment, res2net.py:126-159 in train()); workspace
@@ -465,12 +478,33 @@ int fgr_crop_pairs_assemble(const float* raw, int32_t ld, const int64_t* offsets
  *  fgr_attention_bwd    softmax attention backward over packed segments (the layout of
  *                       fgr_attention*): dq, dk, dv (each may alias column slices of one
  *                       tensor), head dim 4 / 8 / 16 / 32 / 64, fp32; key segments may be attended by any
- *                       number of query segments. */
+ *                       number of query segments.
+ *  fgr_corr_attention_bwd  backward of fgr_corr_attention (CorrespondenceDecoder.simple_attention,
+ *                       finegrained_regtr.py:328-363): from dout (n_rows, 3) = d corr, writes
+ *                       dq = scale dS K and dk = scale dS^T Q (dS = P (dout . xyz_j - dout .
+ *                       corr_i)) over the same segment tables; xyz gets no gradient (the
+ *                       reference's values are coordinates). Key rows no query segment attends
+ *                       get dk = 0; d 32 / 64 / 128 / 256 / 512, fp32; workspace
+ *                       fgr_corr_attention_bwd_workspace(n_rows) bytes. */
+int fgr_nbr_inverse_workspace(int64_t nq, int32_t width, int64_t ns, size_t* bytes);
+int fgr_nbr_inverse(const int64_t* idx, int64_t nq, int32_t width, int64_t ns, int32_t* start,
+                    int32_t* pos, int32_t* ent, void* ws, size_t ws_bytes, void* stream);
+int fgr_kpconv_scatter_workspace(int64_t nq, int32_t width, int32_t cin, size_t* bytes);
 int fgr_kpconv_scatter(const float* q, const float* s, int64_t nq, int64_t ns, const int64_t* idx,
                        int32_t width, const float* dwf, int32_t cin, const float* kernel_points,
-                       int32_t n_kp, float extent, float* dx, void* stream);
+                       int32_t n_kp, float extent, const int32_t* start, const int32_t* pos,
+                       float* dx, void* ws, size_t ws_bytes, void* stream);
+int fgr_max_pool_bwd_workspace(int64_t nq, int32_t c, size_t* bytes);
 int fgr_max_pool_bwd(const float* x, int64_t ns, int32_t c, const int64_t* idx, int64_t nq,
-                     int32_t width, const float* dy, float* dx, void* stream);
+                     int32_t width, const float* dy, const int32_t* start, const int32_t* ent,
+                     float* dx, void* ws, size_t ws_bytes, void* stream);
+int fgr_corr_attention_bwd_workspace(int64_t n_rows, size_t* bytes);
+int fgr_corr_attention_bwd(const float* q, int64_t ld_q, const float* k, int64_t ld_k,
+                           const float* xyz, const float* dout, float* dq, int64_t ld_dq, float* dk,
+                           int64_t ld_dk, const int64_t* q_off, const int64_t* kv_off,
+                           const int32_t* kv_seg, const int64_t* v_off, int32_t n_seg,
+                           int32_t n_kv_seg, int64_t n_rows, int32_t max_q_len, int32_t max_kv_len,
+                           int32_t d, float scale, void* ws, size_t ws_bytes, void* stream);
 int fgr_segnorm_workspace(int64_t max_seg_len, int32_t c, int32_t n_seg, size_t* bytes);
 int fgr_segnorm_stats(const float* x, int64_t n, int32_t c, const int64_t* seg_off, int32_t n_seg,
                       int64_t max_seg_len, const float* row_div, float eps, float* mean, float* rstd,

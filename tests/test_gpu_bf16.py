@@ -153,11 +153,18 @@ def _rot_deg(a, b):
     return math.degrees(math.acos(max(-1.0, min(1.0, (np.trace(r) - 1) / 2))))
 
 
-@pytest.mark.parametrize('seed,n_points', [(s, 6000) for s in range(8)] + [(20, 20000), (21, 20000)])
+# the sweep's cases (the bound was set from them) and HELD-OUT cases that did not enter the
+# sweep (round 4: seeds 100-103 at 6k points, 110-111 at 20k), run against the same fixed bound
+SWEEP_CASES = [(s, 6000) for s in range(8)] + [(20, 20000), (21, 20000)]
+HELD_OUT_CASES = [(s, 6000) for s in range(100, 104)] + [(110, 20000), (111, 20000)]
+
+
+@pytest.mark.parametrize('seed,n_points', SWEEP_CASES + HELD_OUT_CASES)
 def test_bf16_forward_3dlomatch_vs_oracle(gpu, bf16_mode, seed, n_points):
     """The configs[4] forward in bf16 on low-overlap pairs against the fp32 CPU oracle, over
-    10 random models and input pairs (seeded per case; no hand-picked seed): geometry
-    bit-exact, outputs within the stated bf16 tolerance."""
+    16 random models and input pairs (seeded per case; no hand-picked seed; 6 of them held out
+    of the sweep that set the bound): geometry bit-exact, outputs within the stated bf16
+    tolerance."""
     import fgreg.config as fc
     from fgreg.synthetic import make_batch
     cfg = fc.get('3dlomatch')

@@ -270,6 +270,86 @@ def test_attention_backward(gpu, d, nhead, kind):
         assert e < 1e-5, (name, e)
 
 
+@pytest.mark.parametrize('d', [64, 256])
+def test_corr_attention_backward(gpu, d):
+    """corr_attention_t (CorrespondenceDecoder.simple_attention over the (layer, cloud)
+    segments, finegrained_regtr.py:328-363) vs fp64 autograd of the reference formula: dq, dk
+    through fgr_corr_attention_bwd; unequal clouds incl. a 1-row cloud, 2 layers."""
+    from fgreg.autograd import corr_attention_t
+    from fgreg.transformer import Segments
+    lens = [130, 1, 65, 300]
+    B, L = 2, 2
+    N = sum(lens)
+    g = torch.Generator().manual_seed(d)
+    q, q64 = _leaf(torch.randn(L * N, d, generator=g), gpu)
+    k, k64 = _leaf(torch.randn(L * N, d, generator=g), gpu)
+    xyz = torch.randn(N, 3, generator=g)
+    seg = Segments(lens, gpu, n_layers=L)
+    corr = corr_attention_t(q, k, xyz.to(gpu), seg, 1.0 / math.sqrt(d))
+    off = np.cumsum([0] + lens)
+    outs = []
+    for l in range(L):
+        for c in range(2 * B):
+            p = (c + B) % (2 * B)
+            qi = q64[l * N + off[c]:l * N + off[c + 1]] / math.sqrt(d)
+            kj = k64[l * N + off[p]:l * N + off[p + 1]]
+            outs.append(torch.softmax(qi @ kj.t(), -1) @ xyz[off[p]:off[p + 1]].double())
+    corr64 = torch.cat(outs, 0)
+    R = torch.randn(corr64.shape, generator=g)
+    (corr * R.to(gpu)).sum().backward()
+    (corr64 * R.double()).sum().backward()
+    assert rel_err(corr, corr64) < 1e-5
+    assert rel_err(q.grad, q64.grad) < 1e-5, rel_err(q.grad, q64.grad)
+    assert rel_err(k.grad, k64.grad) < 1e-5, rel_err(k.grad, k64.grad)
+
+
+@pytest.mark.parametrize('strided', [False, True])
+def test_nbr_inverse(gpu, strided):
+    """fgr_nbr_inverse: the CSR inverse of a neighbour table (the golden KPConv block's conv /
+    pool tables with their shadow entries) equals the host's stable inverse."""
+    from fgreg.autograd import nbr_inverse
+    gk = np.load(__import__('conftest').GOLDEN + '/kpconv_block.npz')
+    idx = gk['pools' if strided else 'idx'].astype(np.int64)
+    ns = gk['s'].shape[0]
+    start, pos, ent = (t.cpu().numpy() for t in nbr_inverse(torch.from_numpy(idx).to(gpu), ns))
+    flat = idx.reshape(-1)
+    valid = (flat >= 0) & (flat < ns)
+    e = np.nonzero(valid)[0]
+    order = e[np.argsort(flat[e], kind='stable')]
+    cnt = np.bincount(flat[e], minlength=ns)
+    assert np.array_equal(start, np.concatenate([[0], np.cumsum(cnt)]))
+    assert np.array_equal(ent[:len(order)], order)
+    want_pos = np.full(flat.shape, -1)
+    want_pos[order] = np.arange(len(order))
+    assert np.array_equal(pos[:flat.size], want_pos)
+
+
+def test_backward_is_deterministic(gpu):
+    """Two backward passes of one training step give bit-identical gradients (no floating-
+    point atomics: the KPConv / max-pool scatters are gathers over the table's inverse)."""
+    import fgreg
+    import fgreg.config as fc
+    from fgreg.synthetic import make_batch
+    cfg = fc.get('modelnet')
+    torch.manual_seed(7)
+    model = fgreg.RegTR(cfg).to(gpu).train()
+    src, tgt, _ = make_batch('modelnet', 2)
+    batch = {'src_xyz': [torch.from_numpy(s).to(gpu) for s in src],
+             'tgt_xyz': [torch.from_numpy(t).to(gpu) for t in tgt]}
+    runs = []
+    for _ in range(2):
+        model.zero_grad(set_to_none=True)
+        out = model(batch)
+        loss = sum((t.square().sum() for t in out['src_kp_warped'] + out['tgt_kp_warped']),
+                   torch.zeros((), device=gpu))
+        loss = loss + sum(f.sum() for f in out['src_feat'] + out['tgt_feat_un'])
+        loss.backward()
+        runs.append({k: p.grad.clone() for k, p in model.named_parameters() if p.grad is not None})
+    assert runs[0].keys() == runs[1].keys() and len(runs[0]) > 100
+    diff = [k for k in runs[0] if not torch.equal(runs[0][k], runs[1][k])]
+    assert not diff, diff[:5]
+
+
 def test_colsum(gpu):
     from fgreg.autograd import colsum
     x = torch.randn(40001, 300, dtype=torch.float64)
@@ -344,8 +424,9 @@ def test_train_step_vs_reference(gpu):
             assert rel_err(getattr(mods[name], stat), ref[k]) < 1e-5, k
 
 
-@pytest.mark.parametrize('pre_norm', [True, False])
-def test_train_step_vs_oracle_modelnet(gpu, pre_norm):
+@pytest.mark.parametrize('pre_norm,head', [(True, 'regressor'), (False, 'regressor'),
+                                           (True, 'decoder')])
+def test_train_step_vs_oracle_modelnet(gpu, pre_norm, head):
     """Full-width ModelNet config (d 256, head dim 32: the f16x3 attention and every GEMM path),
     B = 2 pairs of the bench workload: fgreg's train() step vs the fp64 oracle's on the same
     neighbour tables. Losses within 1e-5, every gradient within GRAD_TOL; the cosine of the
@@ -354,11 +435,13 @@ def test_train_step_vs_oracle_modelnet(gpu, pre_norm):
     oracle's OWN fp32 step differs from its fp64 step by up to 2.6e-3 (median 7.4e-4, 1 - cos
     8.6e-7) there vs 1.8e-3 (1.3e-4, 3.8e-8) pre-norm (tools/grad_chaos.py), and the f16x3
     products perturb ~10x more than fp32 rounding, so post-norm is bounded at 3e-2 / 1 - 1e-4
-    (a wiring or formula error stays O(1))."""
+    (a wiring or formula error stays O(1)). head='decoder': the CorrespondenceDecoder head
+    (direct_regress_coor: False, finegrained_regtr.py:312-408: q / k projections and the
+    softmax-weighted partner coordinates) trained through fgr_corr_attention_bwd."""
     import fgreg
     import fgreg.config as fc
     from fgreg.synthetic import make_batch
-    cfg = fc.get('modelnet', pre_norm=pre_norm)
+    cfg = fc.get('modelnet', pre_norm=pre_norm, direct_regress_coor=head == 'regressor')
     torch.manual_seed(5)
     np.random.seed(5)
     model = fgreg.RegTR(cfg)

@@ -24,7 +24,8 @@ def test_library_exports_every_header_symbol():
     assert len(syms) >= 14
     for s in syms:
         assert hasattr(L, s), s
-    assert L.fgr_abi_version() == 1
+    from fgreg import _lib
+    assert L.fgr_abi_version() == _lib.ABI_VERSION == 2
 
 
 def test_python_signatures_cover_header():
@@ -193,6 +194,26 @@ def test_training_mode_refuses_host_tensors():
     with pytest.raises(fgreg.FgrError):
         model(batch)
     with torch.no_grad(), pytest.raises(fgreg.FgrError):
+        model(batch)
+
+
+@pytest.mark.parametrize('what', ['dropout', 'num_neighbors'])
+def test_training_refuses_untrainable_configs(what):
+    """Configurations the training forward does not restate raise NotImplementedError before
+    any work (the reference applies dropout1/2/3 + the MHA dropout in train(),
+    transformers.py:102-110, 201-238; every shipped config sets 0.0)."""
+    import fgreg
+    import fgreg.config as fc
+    if what == 'dropout':
+        model = fgreg.RegTR(fc.get('modelnet', dropout=0.1)).train()
+    else:
+        model = fgreg.RegTR(fc.get('modelnet', direct_regress_coor=False)).train()
+        model.correspondence_decoder.num_neighbors = 4
+    batch = {'src_xyz': [torch.zeros(8, 3)], 'tgt_xyz': [torch.zeros(8, 3)]}
+    with pytest.raises(NotImplementedError, match=what.replace('_', '.')):
+        model(batch)
+    model.eval()                     # inference has no dropout and restates num_neighbors
+    with pytest.raises(fgreg.FgrError):
         model(batch)
 
 
