@@ -44,9 +44,14 @@ struct RsLn {
     const float* g; const float* b; const float* add; int64_t ld_add; float eps;
     const float* g2; const float* b2; float* out2; int64_t ld_out2;
 };
+struct RsHead {
+    int n_act; float* c2;
+    const float* w4; const float* b4; float* out3;
+};
 bool gemm_rs_f16x3(const float* A, int64_t lda, const void* W, int ksteps, const float* wsc,
                    float* C, int64_t ldc, const float* bias, const float* R, int64_t ldr, int M,
-                   int N, int K, int act, hipStream_t st, const RsLn* ln = nullptr);
+                   int N, int K, int act, hipStream_t st, const RsLn* ln = nullptr,
+                   const RsHead* head = nullptr);
 // few 64 x 64 tiles, narrow output, long contraction: split-K pays (measured)
 inline bool splitk_shape(int m, int n, int k) {
     return k >= 1920 && n <= 256 && (int64_t)((m + 63) / 64) * ((n + 63) / 64) <= 160;
@@ -1271,4 +1276,47 @@ extern "C" int fgr_gemm_f16x3_ln_out2(const float* x, int64_t ldx, const float* 
     FGR_REQUIRE(out2, "fgr_gemm_f16x3_ln_out2: out2 is required");
     return gemm_f16x3_ln_impl(x, ldx, gamma, beta, eps, add, ld_add, w_img, c, ldc, bias, m, n, k,
                               act, gamma2, beta2, out2, ld_out2, stream);
+}
+
+// The CorrespondenceRegressor head (finegrained_regtr.py:411-455) in two row-stationary launches
+// (gemm_rs.hip): [coor_mlp[0] | conf_logits_decoder] as one product over the stacked image of
+// [W0; Wc; 0] (ReLU on the first d columns -> hidden, column d -> logits), then coor_mlp[2] ->
+// ReLU -> coor_mlp[4] with the 3-wide output formed in the epilogue (hidden2 never written).
+extern "C" int fgr_corr_head_supported(int32_t m, int32_t d) {
+    return (m > 0 && d > 0 && d % 16 == 0 && d <= 256 && d / 16 + 1 <= 64) ? 1 : 0;
+}
+
+extern "C" int fgr_corr_head_f16x3(const float* f, int64_t ldf, int32_t m, int32_t d,
+                                   const void* w0c_img, const float* b0c, const void* w2_img,
+                                   const float* b2, const float* w4, const float* b4, float* hidden,
+                                   float* corr, float* logits, void* stream) {
+    FGR_REQUIRE(f && w0c_img && b0c && w2_img && b2 && w4 && b4 && hidden && corr && logits &&
+                    m >= 0 && ldf >= d && ldf % 4 == 0,
+                "fgr_corr_head_f16x3: bad arguments");
+    FGR_REQUIRE(m == 0 || fgr_corr_head_supported(m, d),
+                "fgr_corr_head_f16x3: d %d not supported (fgr_corr_head_supported)", d);
+    const uintptr_t al = reinterpret_cast<uintptr_t>(f) | reinterpret_cast<uintptr_t>(w0c_img) |
+                         reinterpret_cast<uintptr_t>(b0c) | reinterpret_cast<uintptr_t>(w2_img) |
+                         reinterpret_cast<uintptr_t>(b2) | reinterpret_cast<uintptr_t>(w4) |
+                         reinterpret_cast<uintptr_t>(hidden);
+    FGR_REQUIRE((al & 15) == 0, "fgr_corr_head_f16x3: operands must be 16-B aligned");
+    if (m == 0) return FGR_OK;
+    hipStream_t st = as_stream(stream);
+    TimedCall timed_(st);
+    const int ks = ksteps_h3(d);
+    const float* wsc0 = reinterpret_cast<const float*>(static_cast<const char*>(w0c_img) +
+                                                       image_bytes_h3(d + 16, d));
+    const float* wsc2 = reinterpret_cast<const float*>(static_cast<const char*>(w2_img) +
+                                                       image_bytes_h3(d, d));
+    const RsHead h0{d, logits, nullptr, nullptr, nullptr};
+    FGR_REQUIRE(gemm_rs_f16x3(f, ldf, w0c_img, ks, wsc0, hidden, d, b0c, nullptr, 0, m, d + 16, d,
+                              FGR_ACT_RELU, st, nullptr, &h0),
+                "fgr_corr_head_f16x3: row-stationary kernel rejected the first product");
+    FGR_CHECK_LAUNCH("gemm_rs (corr head, coor_mlp[0] | conf_logits)");
+    const RsHead h2{d, nullptr, w4, b4, corr};
+    FGR_REQUIRE(gemm_rs_f16x3(hidden, d, w2_img, ks, wsc2, hidden, d, b2, nullptr, 0, m, d, d,
+                              FGR_ACT_RELU, st, nullptr, &h2),
+                "fgr_corr_head_f16x3: row-stationary kernel rejected the second product");
+    FGR_CHECK_LAUNCH("gemm_rs (corr head, coor_mlp[2] -> coor_mlp[4])");
+    return FGR_OK;
 }

@@ -26,6 +26,15 @@
 // block in LDS, and the normalised row is split as above: the LayerNorm output never goes to
 // memory and its launch disappears.
 //
+// Correspondence-head epilogues (fgr_corr_head_f16x3; CorrespondenceRegressor,
+// finegrained_regtr.py:411-455): (a) `n_act` / `c2`: columns >= n_act take no activation and
+// column n_act goes to c2[row] instead of C -- coor_mlp[0] (ReLU) and conf_logits_decoder
+// (none) as ONE product over [W0; Wc; 0] (the 15 zero rows pad N to a panel); (b) HEAD: the
+// block covers every panel of its rows and instead of storing the ReLU'd outputs it
+// accumulates their dot products with the 3 rows of coor_mlp[4] (fp32 FMAs on the fp32
+// outputs, no split), reduced over the 4 lane groups at the end: coor_mlp[2] -> ReLU ->
+// coor_mlp[4] in one launch, the hidden (rows, d) tensor never written.
+//
 // Swapped orientation (gemm16.hip): W fragments are the MFMA A operand, activation fragments
 // the B operand, so a lane's 4 accumulators are 4 consecutive output columns of ONE row.
 // 16x16x32 f16 lane maps (lane l, g = l >> 4, c = l & 15): A[i = c][k = 8g + e],
@@ -55,6 +64,10 @@ struct RsArgs {
     float eps;
     const float* ln_g2; const float* ln_b2; //   side output (LNM 3): LN(x) * g2 + b2 -> out2
     float* ln_out2; int64_t ld_out2;
+    int n_act;                        // columns >= n_act: no activation (n_act % 16 == 0)
+    float* c2;                        //   and column n_act -> c2[row] (not stored in C)
+    const float* w4; const float* b4; // HEAD: (3, N) fp32 rows and bias of the 3-wide output
+    float* out3;                      //   -> out3 (M, 3)
 };
 
 // s_waitcnt vmcnt(n) lgkmcnt(0) -- gfx9 encoding
@@ -112,7 +125,7 @@ __device__ __forceinline__ float finish_ct(float y, float b, float r) {
 // LNM: 0 plain, 1 LayerNorm prologue, 2 LayerNorm prologue + row add, 3 as 2 plus a second
 // LayerNorm output of the same rows (the encoder's per-layer output norm), written by the
 // blocks of the first column group
-template <int RT, int KS, bool RES, int ACT, int LNM>
+template <int RT, int KS, bool RES, int ACT, int LNM, bool HEAD = false, bool DEFER = false>
 __global__ void __launch_bounds__(256) gemm_rs_kernel(RsArgs p) {
     constexpr bool LN = LNM > 0;
     constexpr int PANEL_U = KS * 128;                  // 16-B units per W panel
@@ -122,6 +135,7 @@ __global__ void __launch_bounds__(256) gemm_rs_kernel(RsArgs p) {
     __shared__ float4 colw[kRsMaxNc * 4], colb[kRsMaxNc * 4];   // per (panel, g): wsc, bias
     __shared__ float4 lng[LN ? KS * 8 : 1], lnb[LN ? KS * 8 : 1];  // LN gamma / beta (K / 4)
     __shared__ float4 lng2[LNM == 3 ? KS * 8 : 1], lnb2[LNM == 3 ? KS * 8 : 1];
+    __shared__ float4 colh[HEAD ? 3 * kRsMaxNc * 4 : 1];            // HEAD: w4 by (j, panel, g)
 
     const int nbm = (p.M + 64 * RT - 1) / (64 * RT);
     const int npanel = (p.N + 15) / 16;
@@ -298,6 +312,16 @@ __global__ void __launch_bounds__(256) gemm_rs_kernel(RsArgs p) {
         if (p.bias)
             for (int j = 0; j < 4 && n + j < p.N; ++j) e[j] = p.bias[n + j];
         colb[u] = make_float4(e[0], e[1], e[2], e[3]);
+        if constexpr (HEAD) {
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+                colh[j * kRsMaxNc * 4 + u] = *reinterpret_cast<const float4*>(p.w4 + (int64_t)j * p.N + n);
+        }
+    }
+    float h3[RT][3];
+    if constexpr (HEAD) {
+#pragma unroll
+        for (int i = 0; i < RT; ++i) h3[i][0] = h3[i][1] = h3[i][2] = 0.f;
     }
 
     // row tiles of this wave with at least one row < M (a tile past M is skipped by the wave)
@@ -312,25 +336,19 @@ __global__ void __launch_bounds__(256) gemm_rs_kernel(RsArgs p) {
             rv[i] = *reinterpret_cast<const float4*>(p.R + row * p.ldr + n);
         }
     };
-    float4 rcur[RT], rnext[RT];
-    if constexpr (RES) load_res(0, rcur);
-
-    for (int q = 0; q < np; ++q) {
-        // ops issued after panel q's DMA, counted from below: q = 0: DMA of panel 1 (the
-        // prologue's loads are consumed; panel 0's residual is not counted); q >= 1: stores of
-        // panel q - 2 (q >= 2), [residual loads of panel q], DMA of panel q + 1 if any, stores
-        // of panel q - 1
-        if (q == 0) wait_vm_lgkm0_dyn(np > 1 ? PW : 0);
-        else wait_vm_lgkm0_dyn((q >= 2 ? nst : 0) + nst + (q + 1 < np ? PW : 0));
-        __builtin_amdgcn_s_barrier();                    // every wave's pieces; buffer of q - 1 free
-        if constexpr (RES)
-            if (q + 1 < np) load_res(q + 1, rnext);
-        if (q + 2 < np) dma(q + 2);
-
-        typedef __attribute__((address_space(3))) u32x4 lds_u4;
+    // vector stores a wave issues in panel qq's epilogue (counted by the waits below; an
+    // over-count would let a panel's DMA still be in flight when it is read)
+    auto nstore = [&](int qq) -> int {
+        if constexpr (HEAD) return 0;
+        const int col = (p0 + qq) * 16;
+        if (p.c2 && col >= p.n_act) return col == p.n_act ? nst : 0;
+        return nst;
+    };
+    typedef __attribute__((address_space(3))) u32x4 lds_u4;
+    // panel q's pure MFMA loop (W fragments from the LDS ring, A resident)
+    auto panel_mfma = [&](int q, f32x4 (&acc)[RT]) {
         const uint32_t base = (uint32_t)(uintptr_t)(ring + (q % kRsNb) * PANEL_U) +
                               (uint32_t)(g * 16 + c) * 16;
-        f32x4 acc[RT];
 #pragma unroll
         for (int i = 0; i < RT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -344,16 +362,54 @@ __global__ void __launch_bounds__(256) gemm_rs_kernel(RsArgs p) {
                 acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, af[i][s][0], acc[i], 0, 0, 0);
             }
         }
-        // epilogue: lane holds C[row = mw + 16i + c][n .. n + 3]
+    };
+    // panel q's epilogue: lane holds C[row = mw + 16i + c][n .. n + 3]
+    auto epilogue = [&](int q, const f32x4 (&acc)[RT], const float4 (&rv)[RT]) {
         const int n = (p0 + q) * 16 + 4 * g;
         const float4 ws = colw[q * 4 + g], bv = colb[q * 4 + g];
-        {                                                  // N % 16 == 0: every panel in range
+        if constexpr (HEAD) {
+            // the ReLU'd outputs against coor_mlp[4]'s rows, fp32, not stored
+            const float4 w0 = colh[q * 4 + g], w1 = colh[kRsMaxNc * 4 + q * 4 + g],
+                         w2 = colh[2 * kRsMaxNc * 4 + q * 4 + g];
+#pragma unroll
+            for (int i = 0; i < RT; ++i) {
+                const float s0 = rs[i] * ws.x, s1 = rs[i] * ws.y, s2 = rs[i] * ws.z, s3 = rs[i] * ws.w;
+                const float y0 = finish_ct<ACT, false>(acc[i][0] * s0, bv.x, 0.f);
+                const float y1 = finish_ct<ACT, false>(acc[i][1] * s1, bv.y, 0.f);
+                const float y2 = finish_ct<ACT, false>(acc[i][2] * s2, bv.z, 0.f);
+                const float y3 = finish_ct<ACT, false>(acc[i][3] * s3, bv.w, 0.f);
+                h3[i][0] = fmaf(y3, w0.w, fmaf(y2, w0.z, fmaf(y1, w0.y, fmaf(y0, w0.x, h3[i][0]))));
+                h3[i][1] = fmaf(y3, w1.w, fmaf(y2, w1.z, fmaf(y1, w1.y, fmaf(y0, w1.x, h3[i][1]))));
+                h3[i][2] = fmaf(y3, w2.w, fmaf(y2, w2.z, fmaf(y1, w2.y, fmaf(y0, w2.x, h3[i][2]))));
+            }
+        } else if ((p0 + q) * 16 >= p.n_act) {            // panel-uniform: no activation
+            if (p.c2 && (p0 + q) * 16 == p.n_act && g == 0) {
+#pragma unroll
+                for (int i = 0; i < RT; ++i) {
+                    const int64_t row = mw + 16 * i + c;
+                    if (row < p.M) p.c2[row] = acc[i][0] * (rs[i] * ws.x) + bv.x;
+                }
+            } else if (!p.c2) {
+#pragma unroll
+                for (int i = 0; i < RT; ++i) {
+                    const int64_t row = mw + 16 * i + c;
+                    const float s0 = rs[i] * ws.x, s1 = rs[i] * ws.y, s2 = rs[i] * ws.z, s3 = rs[i] * ws.w;
+                    float4 r4 = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if constexpr (RES) r4 = rv[i];
+                    const float4 y = make_float4(finish_ct<FGR_ACT_NONE, RES>(acc[i][0] * s0, bv.x, r4.x),
+                                                 finish_ct<FGR_ACT_NONE, RES>(acc[i][1] * s1, bv.y, r4.y),
+                                                 finish_ct<FGR_ACT_NONE, RES>(acc[i][2] * s2, bv.z, r4.z),
+                                                 finish_ct<FGR_ACT_NONE, RES>(acc[i][3] * s3, bv.w, r4.w));
+                    if (row < p.M) *reinterpret_cast<float4*>(p.C + row * p.ldc + n) = y;
+                }
+            }
+        } else {                                           // N % 16 == 0: every panel in range
 #pragma unroll
             for (int i = 0; i < RT; ++i) {
                 const int64_t row = mw + 16 * i + c;
                 const float s0 = rs[i] * ws.x, s1 = rs[i] * ws.y, s2 = rs[i] * ws.z, s3 = rs[i] * ws.w;
                 float4 r4 = make_float4(0.f, 0.f, 0.f, 0.f);
-                if constexpr (RES) r4 = rcur[i];
+                if constexpr (RES) r4 = rv[i];
                 const float4 y = make_float4(finish_ct<ACT, RES>(acc[i][0] * s0, bv.x, r4.x),
                                              finish_ct<ACT, RES>(acc[i][1] * s1, bv.y, r4.y),
                                              finish_ct<ACT, RES>(acc[i][2] * s2, bv.z, r4.z),
@@ -361,43 +417,114 @@ __global__ void __launch_bounds__(256) gemm_rs_kernel(RsArgs p) {
                 if (row < p.M) *reinterpret_cast<float4*>(p.C + row * p.ldc + n) = y;
             }
         }
-        if constexpr (RES)
+    };
+
+    float4 rcur[RT], rnext[RT];
+    if constexpr (RES && !DEFER) load_res(0, rcur);
+    f32x4 prev[RT];
+    for (int q = 0; q < np; ++q) {
+        // vector-memory ops issued after panel q's DMA (issued in iteration q - 2), counted so
+        // that vmcnt guarantees that DMA has landed: the epilogue stores of iteration q - 2
+        // (panel q - 2, or q - 3 when DEFERred), then iteration q - 1's [residual loads, not
+        // counted: waiting for them too is merely stricter], DMA of panel q + 1 if any, and its
+        // epilogue stores (panel q - 1, or q - 2 when DEFERred)
+        if (q == 0) {
+            wait_vm_lgkm0_dyn(np > 1 ? PW : 0);
+        } else if constexpr (!DEFER) {
+            wait_vm_lgkm0_dyn((q >= 2 ? nstore(q - 2) : 0) + nstore(q - 1) + (q + 1 < np ? PW : 0));
+        } else {
+            wait_vm_lgkm0_dyn((q >= 3 ? nstore(q - 3) : 0) + (q >= 2 ? nstore(q - 2) : 0) +
+                              (q + 1 < np ? PW : 0));
+        }
+        __builtin_amdgcn_s_barrier();                    // every wave's pieces; buffer of q - 1 free
+        if constexpr (RES) {
+            if constexpr (!DEFER) {
+                if (q + 1 < np) load_res(q + 1, rnext);
+            } else {
+                if (q >= 1) load_res(q - 1, rcur);
+            }
+        }
+        if (q + 2 < np) dma(q + 2);
+        f32x4 acc[RT];
+        panel_mfma(q, acc);
+        if constexpr (!DEFER) {
+            epilogue(q, acc, rcur);
+            if constexpr (RES)
 #pragma unroll
-            for (int i = 0; i < RT; ++i) rcur[i] = rnext[i];
+                for (int i = 0; i < RT; ++i) rcur[i] = rnext[i];
+        } else {
+            // the previous panel's epilogue after this panel's MFMAs: its VALU and stores can
+            // issue in the MFMA shadows instead of between two panels' matrix work
+            if (q >= 1) epilogue(q - 1, prev, rcur);
+#pragma unroll
+            for (int i = 0; i < RT; ++i) prev[i] = acc[i];
+        }
+    }
+    if constexpr (DEFER) {
+        if constexpr (RES) load_res(np - 1, rcur);
+        epilogue(np - 1, prev, rcur);
+    }
+    if constexpr (HEAD) {
+        // sum the lane groups' column quads: lanes c, c + 16, c + 32, c + 48 hold one row
+#pragma unroll
+        for (int i = 0; i < RT; ++i) {
+            const int64_t row = mw + 16 * i + c;
+            const float t0 = xg_sum_rs(h3[i][0]), t1 = xg_sum_rs(h3[i][1]), t2 = xg_sum_rs(h3[i][2]);
+            if (g == 0 && row < p.M) {
+                p.out3[row * 3 + 0] = t0 + p.b4[0];
+                p.out3[row * 3 + 1] = t1 + p.b4[1];
+                p.out3[row * 3 + 2] = t2 + p.b4[2];
+            }
+        }
     }
 }
 
-template <int RT, int KS, int ACT>
+template <int RT, int KS, int ACT, bool D>
 void launch_rs_act(const RsArgs& a, unsigned blocks, hipStream_t st) {
     // LN prologue: one row tile per wave (at two, the row + add registers of the prologue
     // exceed the 256 VGPRs of two waves per SIMD and spill), no residual (checked by the caller)
     if constexpr (RT == 1 && ACT != FGR_ACT_RELU_RES_LEAKY) {
         if (a.ln_g && a.ln_add && a.ln_out2) {
-            hipLaunchKernelGGL((gemm_rs_kernel<RT, KS, false, ACT, 3>), dim3(blocks), dim3(256), 0, st, a);
+            hipLaunchKernelGGL((gemm_rs_kernel<RT, KS, false, ACT, 3, false, D>), dim3(blocks), dim3(256), 0, st, a);
             return;
         }
         if (a.ln_g && a.ln_add) {
-            hipLaunchKernelGGL((gemm_rs_kernel<RT, KS, false, ACT, 2>), dim3(blocks), dim3(256), 0, st, a);
+            hipLaunchKernelGGL((gemm_rs_kernel<RT, KS, false, ACT, 2, false, D>), dim3(blocks), dim3(256), 0, st, a);
             return;
         }
         if (a.ln_g) {
-            hipLaunchKernelGGL((gemm_rs_kernel<RT, KS, false, ACT, 1>), dim3(blocks), dim3(256), 0, st, a);
+            hipLaunchKernelGGL((gemm_rs_kernel<RT, KS, false, ACT, 1, false, D>), dim3(blocks), dim3(256), 0, st, a);
+            return;
+        }
+    }
+    if constexpr (ACT == FGR_ACT_RELU) {
+        if (a.out3) {
+            hipLaunchKernelGGL((gemm_rs_kernel<RT, KS, false, ACT, 0, true, D>), dim3(blocks), dim3(256), 0, st, a);
             return;
         }
     }
     if (a.R)
-        hipLaunchKernelGGL((gemm_rs_kernel<RT, KS, true, ACT, 0>), dim3(blocks), dim3(256), 0, st, a);
+        hipLaunchKernelGGL((gemm_rs_kernel<RT, KS, true, ACT, 0, false, D>), dim3(blocks), dim3(256), 0, st, a);
     else
-        hipLaunchKernelGGL((gemm_rs_kernel<RT, KS, false, ACT, 0>), dim3(blocks), dim3(256), 0, st, a);
+        hipLaunchKernelGGL((gemm_rs_kernel<RT, KS, false, ACT, 0, false, D>), dim3(blocks), dim3(256), 0, st, a);
+}
+
+// FGR_RS_DEFER=1: the deferred-epilogue panel loop (A/B tuning switch)
+inline bool rs_defer() {
+    const char* e = getenv("FGR_RS_DEFER");
+    return e && e[0] == '1';
 }
 
 template <int RT, int KS>
 bool launch_rs_k(const RsArgs& a, unsigned blocks, hipStream_t st) {
+    const bool d = rs_defer();
+#define RS_ACT(A) (d ? launch_rs_act<RT, KS, A, true>(a, blocks, st) : launch_rs_act<RT, KS, A, false>(a, blocks, st))
     switch (a.act) {
-        case FGR_ACT_RELU: launch_rs_act<RT, KS, FGR_ACT_RELU>(a, blocks, st); return true;
-        case FGR_ACT_RELU_RES_LEAKY: launch_rs_act<RT, KS, FGR_ACT_RELU_RES_LEAKY>(a, blocks, st); return true;
-        default: launch_rs_act<RT, KS, FGR_ACT_NONE>(a, blocks, st); return true;
+        case FGR_ACT_RELU: RS_ACT(FGR_ACT_RELU); return true;
+        case FGR_ACT_RELU_RES_LEAKY: RS_ACT(FGR_ACT_RELU_RES_LEAKY); return true;
+        default: RS_ACT(FGR_ACT_NONE); return true;
     }
+#undef RS_ACT
 }
 
 }  // namespace
@@ -409,11 +536,19 @@ struct RsLn {
     const float* g; const float* b; const float* add; int64_t ld_add; float eps;
     const float* g2; const float* b2; float* out2; int64_t ld_out2;    // optional side output
 };
+// the correspondence-head epilogues (see the top of this file): n_act / c2, or out3 with w4 / b4
+struct RsHead {
+    int n_act; float* c2;
+    const float* w4; const float* b4; float* out3;
+};
 bool gemm_rs_f16x3(const float* A, int64_t lda, const void* W, int ksteps, const float* wsc,
                    float* C, int64_t ldc, const float* bias, const float* R, int64_t ldr, int M,
-                   int N, int K, int act, hipStream_t st, const RsLn* ln) {
+                   int N, int K, int act, hipStream_t st, const RsLn* ln, const RsHead* head) {
     if (K % 8 != 0 || N % 16 != 0 || ksteps > 8 || ksteps % 2 != 0) return false;
     if (ln && (R || (ln->out2 && !ln->add))) return false;
+    if (head && (ln || R || (head->out3 && (act != FGR_ACT_RELU || N / 16 > kRsMaxNc)) ||
+                 head->n_act % 16 != 0))
+        return false;
     // row tiles per wave: 2 (W fragments reused twice) unless that leaves too few blocks
     const char* rte = getenv("FGR_RS_RT");
     int RT = (rte && rte[0]) ? atoi(rte) : 2;
@@ -441,12 +576,15 @@ bool gemm_rs_f16x3(const float* A, int64_t lda, const void* W, int ksteps, const
         nc = (npanel + ngrp - 1) / ngrp;
     }
     nc = std::min(std::min(nc, npanel), kRsMaxNc);
+    if (head && head->out3) nc = npanel;              // the 3-wide head needs whole rows
     const int ngrp = (npanel + nc - 1) / nc;
     const unsigned blocks = (unsigned)((int64_t)nbm * ngrp);
     RsArgs a{A, lda, (const u32x4*)W, wsc, C, ldc, bias, R, ldr, M, N, K, act, nc,
              ln ? ln->g : nullptr, ln ? ln->b : nullptr, ln ? ln->add : nullptr,
              ln ? ln->ld_add : 0, ln ? ln->eps : 0.f, ln ? ln->g2 : nullptr,
-             ln ? ln->b2 : nullptr, ln ? ln->out2 : nullptr, ln ? ln->ld_out2 : 0};
+             ln ? ln->b2 : nullptr, ln ? ln->out2 : nullptr, ln ? ln->ld_out2 : 0,
+             head ? head->n_act : N, head ? head->c2 : nullptr, head ? head->w4 : nullptr,
+             head ? head->b4 : nullptr, head ? head->out3 : nullptr};
 #define RS_CASE(rt, ks) \
     if (RT == rt && ksteps == ks) return launch_rs_k<rt, ks>(a, blocks, st);
     RS_CASE(2, 2) RS_CASE(2, 4) RS_CASE(2, 6) RS_CASE(2, 8)

@@ -68,6 +68,8 @@ SIGNATURES = {
                           _sz, _vp],
     'fgr_gemm_bf16_ws': [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _vp,
                          _sz, _vp],
+    'fgr_corr_head_supported': [_i32, _i32],
+    'fgr_corr_head_f16x3': [_vp, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     'fgr_copy_batch': [_i32, _vp, _vp, _vp, _vp],
     'fgr_lengths_to_offsets': [_vp, _i32, _vp, _vp],
     'fgr_overlap_pool': [_vp, _i64, _vp, _i64, _i32, _vp, _vp],

@@ -658,6 +658,31 @@ def attention_flops(q_off, kv_off, kv_seg, d):
     return sum(4 * (qo[i + 1] - qo[i]) * (ko[ks[i] + 1] - ko[ks[i]]) * d for i in range(len(ks)))
 
 
+def corr_head_supported(m, d) -> bool:
+    return bool(_lib.load().fgr_corr_head_supported(int(m), int(d)))
+
+
+def corr_head(f, img0c, b0c, img2, b2, w4, b4):
+    """CorrespondenceRegressor (finegrained_regtr.py:411-455) on f (m, d) in two launches
+    (fgr_corr_head_f16x3): -> corr (m, 3), logits (m, 1). img0c: the f16x3 image of the stacked
+    [W0; Wc; 0] (d + 16, d) with bias b0c; img2: coor_mlp[2]'s image; w4 / b4: coor_mlp[4]."""
+    _dev(f, b0c, b2, w4, b4)
+    m, d = f.shape
+    assert f.stride(1) == 1 and f.stride(0) % 4 == 0 and f.data_ptr() % 16 == 0
+    w4, b4 = _c(w4, torch.float32), _c(b4, torch.float32)
+    assert w4.shape == (3, d) and b0c.numel() == d + 16 and b2.numel() == d
+    hidden = _workspace(f.device, 4 * m * d)
+    corr = torch.empty((m, 3), dtype=torch.float32, device=f.device)
+    logits = torch.empty((m, 1), dtype=torch.float32, device=f.device)
+    t0 = _begin('gemm', (m, 2 * d + 16, d))
+    _lib.check(_lib.load().fgr_corr_head_f16x3(
+        _ptr(f), f.stride(0), m, d, _ptr(img0c.img), _ptr(_c(b0c, torch.float32)), _ptr(img2.img),
+        _ptr(_c(b2, torch.float32)), _ptr(w4), _ptr(b4), _ptr(hidden), _ptr(corr), _ptr(logits),
+        _stream()), 'fgr_corr_head_f16x3')
+    _end('gemm', t0, 2 * m * (d + 16) * d + 2 * m * d * d + 6 * m * d)
+    return corr, logits
+
+
 def corr_attention(q, k, xyz, q_off, kv_off, kv_seg, v_off, max_q_len, scale) -> torch.Tensor:
     """CorrespondenceDecoder.simple_attention over packed (layer, cloud) segments
     (fgr_corr_attention): -> (rows, 3) softmax-weighted partner coordinates."""

@@ -32,6 +32,9 @@ _logger = logging.getLogger(__name__)
 # compute mode of the correspondence head's GEMMs when the forward runs in bf16 (None: bf16
 # like the rest); FGREG_BF16_HEAD=f16x3 keeps the pose-sensitive head fp32-accurate
 HEAD_MODE = os.environ.get('FGREG_BF16_HEAD') or None
+# the CorrespondenceRegressor head in two fused launches where supported (FGREG_FUSED_HEAD=0: one
+# GEMM per Linear, for A/B)
+FUSED_HEAD = os.environ.get('FGREG_FUSED_HEAD', '1') != '0'
 
 
 class CorrespondenceRegressor(nn.Module):
@@ -44,12 +47,42 @@ class CorrespondenceRegressor(nn.Module):
                                       nn.Linear(d_embed, 3))
         self.conf_logits_decoder = nn.Linear(d_embed, 1)
 
+    def _stacked(self):
+        """[W0; Wc; 0] (d + 16, d) and [b0; bc; 0]: coor_mlp[0] and conf_logits_decoder as one
+        product (fgr_corr_head_f16x3), rebuilt when a source tensor changes."""
+        m = self.coor_mlp
+        srcs = (m[0].weight, self.conf_logits_decoder.weight, m[0].bias,
+                self.conf_logits_decoder.bias)
+        key = tuple((t.data_ptr(), t._version) for t in srcs)
+        st = getattr(self, '_stack_cache', None)
+        if st is None or st[0] != key:
+            d = m[0].weight.shape[1]
+            with torch.no_grad():
+                w = torch.zeros((d + 16, d), dtype=torch.float32, device=m[0].weight.device)
+                w[:d] = m[0].weight
+                w[d] = self.conf_logits_decoder.weight[0]
+                b = torch.zeros((d + 16,), dtype=torch.float32, device=w.device)
+                b[:d] = m[0].bias
+                b[d] = self.conf_logits_decoder.bias[0]
+            st = (key, w, b)
+            object.__setattr__(self, '_stack_cache', st)     # not a parameter / buffer
+        return st[1], st[2]
+
     def forward_packed(self, feats):
         """feats (L, N, d) -> corr (L, N, 3), logits (L, N, 1). In the bf16 mode the head
-        runs in ``HEAD_MODE`` (the pose reads its outputs directly; DESIGN.md "bf16 mode")."""
+        runs in ``HEAD_MODE`` (the pose reads its outputs directly; DESIGN.md "bf16 mode").
+        f16x3 with d % 16 == 0, d <= 256 (ModelNet): two launches (fgr_corr_head_f16x3), else
+        one GEMM per Linear."""
         L, N, d = feats.shape
         f = feats.reshape(L * N, d)
         m = self.coor_mlp
+        mode = (HEAD_MODE or lin.MODE) if lin.MODE == 'bf16' else lin.MODE
+        if FUSED_HEAD and mode == 'f16x3' and ops.corr_head_supported(L * N, d):
+            w0c, b0c = self._stacked()
+            corr, logits = ops.corr_head(f, lin.weight_image(w0c, mode='f16x3'), b0c,
+                                         lin.weight_image(m[2].weight, mode='f16x3'), m[2].bias,
+                                         m[4].weight, m[4].bias)
+            return corr.view(L, N, 3), logits.view(L, N, 1)
         with lin.mode_scope(HEAD_MODE if lin.MODE == 'bf16' else None):
             h = linear(f, m[0].weight, m[0].bias, act=ops.ACT_RELU)
             h = linear(h, m[2].weight, m[2].bias, act=ops.ACT_RELU)

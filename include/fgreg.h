@@ -442,6 +442,20 @@ int fgr_crop_pairs_assemble(const float* raw, int32_t ld, const int64_t* offsets
                             const double* noise, const float* rt, int32_t m, float* xyz,
                             uint8_t* overlap, int64_t* corr, int32_t* n_corr, void* stream);
 
+/* The CorrespondenceRegressor head (finegrained_regtr.py:411-455, direct_regress_coor: True) on
+ * the (m, d) stacked layer outputs f in two row-stationary f16x3 launches:
+ *   hidden = ReLU(f W0^T + b0), logits = f Wc^T + bc   -- ONE product over the image of the
+ *            stacked (d + 16, d) weight [W0; Wc; 0] (fgr_split_weights_h3) with bias
+ *            b0c = [b0; bc; 0] (d + 16 floats); hidden (m, d) is caller scratch;
+ *   corr   = ReLU(hidden W2^T + b2) W4^T + b4           -- the 3-wide coor_mlp[4] formed in the
+ *            second product's epilogue from its fp32 outputs (w4 (3, d) and b4 (3) fp32).
+ * corr (m, 3), logits (m) contiguous. fgr_corr_head_supported(m, d): d % 16 == 0, d <= 256;
+ * other widths use fgr_gemm_f16x3 per layer. */
+int fgr_corr_head_supported(int32_t m, int32_t d);
+int fgr_corr_head_f16x3(const float* f, int64_t ldf, int32_t m, int32_t d, const void* w0c_img,
+                        const float* b0c, const void* w2_img, const float* b2, const float* w4,
+                        const float* b4, float* hidden, float* corr, float* logits, void* stream);
+
 /* ---- Training backward (train.py -> trainer.py:110-125 backward) -------
  * The dense products' gradients run on the GEMM entry points above with transposed weight
  * images (fgreg/autograd.py); these cover the rest. Every entry point is deterministic: no

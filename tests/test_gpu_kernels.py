@@ -408,3 +408,37 @@ def test_gemm_f16x3_tiles(gpu, tile, monkeypatch):
             assert rel_err(out, ref) < 2e-6, (tile, m, n, k)
     finally:
         fl.set_mode(old)
+
+
+@pytest.mark.parametrize('m,d', [(57264, 256), (1000, 256), (333, 128), (97, 64), (4097, 32)])
+def test_corr_head_fused_vs_fp64(gpu, m, d):
+    """fgr_corr_head_f16x3 (CorrespondenceRegressor, finegrained_regtr.py:411-455, in two
+    row-stationary launches: [coor_mlp[0] | conf_logits] over the stacked weight, then
+    coor_mlp[2] -> ReLU -> coor_mlp[4] formed in the epilogue) vs the four Linear layers in fp64
+    (per row within 1e-5 of the row's |.|-weighted magnitude) and vs the unfused per-Linear path
+    of the same module (fgreg.regtr.FUSED_HEAD off) within 1e-5."""
+    from fgreg import regtr
+    from fgreg.regtr import CorrespondenceRegressor
+    torch.manual_seed(m + d)
+    head = CorrespondenceRegressor(d).to(gpu)
+    f = torch.randn(2, m, d, device=gpu) * 0.7
+    f[0, :7] = 0.0                                   # all-zero rows
+    f[1, 3] *= 1e4                                   # a row far above the rest
+    corr, logits = head.forward_packed(f)
+    regtr.FUSED_HEAD = False
+    try:
+        corr_u, logits_u = head.forward_packed(f)
+    finally:
+        regtr.FUSED_HEAD = True
+    x = f.reshape(-1, d).double().cpu()
+    p = {k: v.detach().double().cpu() for k, v in head.state_dict().items()}
+    h = torch.relu(x @ p['coor_mlp.0.weight'].t() + p['coor_mlp.0.bias'])
+    h2 = torch.relu(h @ p['coor_mlp.2.weight'].t() + p['coor_mlp.2.bias'])
+    c64 = h2 @ p['coor_mlp.4.weight'].t() + p['coor_mlp.4.bias']
+    l64 = x @ p['conf_logits_decoder.weight'].t() + p['conf_logits_decoder.bias']
+    den_c = (h2.abs() @ p['coor_mlp.4.weight'].abs().t()).max(1, keepdim=True).values + 1e-30
+    den_l = (x.abs() @ p['conf_logits_decoder.weight'].abs().t()) + 1e-30
+    ec = float(((corr.reshape(-1, 3).double().cpu() - c64).abs() / den_c).max())
+    el = float(((logits.reshape(-1, 1).double().cpu() - l64).abs() / den_l).max())
+    assert ec < 1e-5 and el < 1e-5, (ec, el)
+    assert rel_err(corr, corr_u) < 1e-5 and rel_err(logits, logits_u) < 1e-6

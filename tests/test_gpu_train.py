@@ -463,7 +463,13 @@ def test_train_step_vs_oracle_modelnet(gpu, pre_norm, head):
     l64, g64 = oracle_train_grads(cfg, sd, src, tgt, meta, batch, W, W_un)
     for k, v in l64.items():
         assert abs(float(losses[k]) - float(v)) <= 1e-5 * max(1.0, abs(float(v))), (k, float(losses[k]), float(v))
-    errs = {k: fro(grads[k], g64[k]) for k in g64 if float(g64[k].norm()) > 0}
+    # gradients that vanish mathematically (the decoder head's k_proj.bias shifts every score
+    # of a query row equally, which the softmax cancels) are compared in absolute terms
+    scale = max(float(g64[k].norm()) for k in g64)
+    tiny = [k for k in g64 if float(g64[k].norm()) <= 1e-7 * scale]
+    for k in tiny:
+        assert float(grads[k].double().norm()) <= 1e-5 * scale, (k, float(grads[k].norm()), scale)
+    errs = {k: fro(grads[k], g64[k]) for k in g64 if k not in tiny}
     worst = sorted(errs.items(), key=lambda kv: -kv[1])[:5]
     a = torch.cat([grads[k].detach().double().cpu().flatten() for k in errs])
     b = torch.cat([g64[k].detach().flatten() for k in errs])
