@@ -208,7 +208,7 @@ attn_f16x3_v2_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __r
                      const int2* __restrict__ sc, float* __restrict__ o, int64_t ld_o,
                      const int64_t* __restrict__ q_off, const int64_t* __restrict__ kv_off,
                      const int32_t* __restrict__ kv_seg, int n_head, int n_seg, int n_qblk,
-                     float scale_log2) {
+                     float scale_log2, int global_tiles) {
     constexpr int KD = DH / 32, TD = DH / 16;
     constexpr int UN = units<DH>();
     constexpr int PW = UN / 64 / 4;                              // DMA pieces per wave per tile
@@ -228,8 +228,12 @@ attn_f16x3_v2_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __r
     const int ks = kv_seg[seg];
     const int64_t kb = kv_off[ks];
     const int nk = (int)(kv_off[ks + 1] - kb);
-    const int ntile = (nk + 63) / 64;
-    const int64_t tile0 = (kb / 64 + ks) * n_head + head;
+    // per-segment images (attn_kv_image16_kernel: tile t of segment ks at kb / 64 + ks + t) or
+    // images of GLOBAL 64-row tiles (written by the in_proj GEMM, fgr_gemm_f16x3_ln_qkv): the
+    // segment's keys then start `lead` rows into its first tile
+    const int lead = global_tiles ? (int)(kb & 63) : 0;
+    const int ntile = (lead + nk + 63) / 64;
+    const int64_t tile0 = (global_tiles ? kb / 64 : kb / 64 + ks) * n_head + head;
     const int64_t tile_stride = (int64_t)n_head * UN;
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
     const int g = lane >> 4, c = lane & 15;
@@ -296,7 +300,13 @@ attn_f16x3_v2_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __r
                                              (__attribute__((address_space(3))) void*)(dst + j * 1024),
                                              16, 0, 0);
     };
-    if (ntile > 0) dma(0, std::integral_constant<int, 0>{});
+    // tile tt lives in LDS buffer (tt + shift) & 1: a masked first tile (lead > 0) takes buffer 1
+    // so that the unrolled pairs of full tiles always start on buffer 0
+    const int shift = lead > 0 ? 1 : 0;
+    if (ntile > 0) {
+        if (shift) dma(0, std::integral_constant<int, 1>{});
+        else dma(0, std::integral_constant<int, 0>{});
+    }
 
     auto tile = [&](int tt, auto buf_tag, auto mask_tag) {
         constexpr int BUF = decltype(buf_tag)::value;
@@ -327,12 +337,14 @@ attn_f16x3_v2_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __r
         }
         const float f = __builtin_ldexpf(1.f, -(e2.x + eq));
         if constexpr (MASK) {
-            const int valid = nk - tt * 64;
+            const int lo = tt == 0 ? lead : 0, hi = lead + nk - tt * 64;   // valid keys [lo, hi)
 #pragma unroll
             for (int n = 0; n < 4; ++n)
 #pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    if (16 * n + 4 * g + r >= valid) s[n][r] = -INFINITY;
+                for (int r = 0; r < 4; ++r) {
+                    const int kl = 16 * n + 4 * g + r;
+                    if (kl < lo || kl >= hi) s[n][r] = -INFINITY;
+                }
         }
         float mx = vmax3(s[0][0], s[0][1], s[0][2]);
         mx = vmax3(mx, s[0][3], s[1][0]);
@@ -394,18 +406,22 @@ attn_f16x3_v2_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __r
     };
     using B0 = std::integral_constant<int, 0>;
     using B1 = std::integral_constant<int, 1>;
-    const int nfull = nk / 64;                       // tiles with 64 valid keys
+    const int nfull = (lead + nk) / 64;              // tiles [shift, nfull) have 64 valid keys
     int tt = 0;
-    for (; tt + 2 <= nfull; tt += 2) {
+    if (shift) {                                     // the first tile, keys before the segment masked
+        tile(0, B1{}, std::true_type{});
+        tt = 1;
+    }
+    for (; tt + 2 <= nfull; tt += 2) {               // (tt + shift) even: buffer 0
         tile(tt, B0{}, std::false_type{});
         tile(tt + 1, B1{}, std::false_type{});
     }
-    if (tt < nfull) {                                // tt even: buffer 0
+    if (tt < nfull) {
         tile(tt, B0{}, std::false_type{});
         ++tt;
     }
     if (tt < ntile) {
-        if (tt & 1) tile(tt, B1{}, std::true_type{});
+        if ((tt + shift) & 1) tile(tt, B1{}, std::true_type{});
         else tile(tt, B0{}, std::true_type{});
     }
 
@@ -484,11 +500,41 @@ extern "C" int fgr_attention_f16x3(const float* q, int64_t ld_q, const float* k,
     if (dh == 32)
         hipLaunchKernelGGL((attn_f16x3_v2_kernel<32>), dim3((unsigned)n_blocks), dim3(256), 0, st, q,
                            ld_q, (const uint4*)img, (const int2*)sc, o, ld_o, q_off, kv_off, kv_seg,
-                           n_head, n_seg, n_qblk, sl2);
+                           n_head, n_seg, n_qblk, sl2, 0);
     else
         hipLaunchKernelGGL((attn_f16x3_v2_kernel<64>), dim3((unsigned)n_blocks), dim3(256), 0, st, q,
                            ld_q, (const uint4*)img, (const int2*)sc, o, ld_o, q_off, kv_off, kv_seg,
-                           n_head, n_seg, n_qblk, sl2);
+                           n_head, n_seg, n_qblk, sl2, 0);
     FGR_CHECK_LAUNCH("attn_f16x3_v2_kernel");
+    return FGR_OK;
+}
+
+// The attention on K / V images of GLOBAL 64-row tiles written by fgr_gemm_f16x3_ln_qkv (head
+// dim 32): no image launch here.
+extern "C" int fgr_attention_f16x3_img(const float* q, int64_t ld_q, const void* kv_img,
+                                       int64_t n_kv_rows, float* o, int64_t ld_o,
+                                       const int64_t* q_off, const int64_t* kv_off,
+                                       const int32_t* kv_seg, int32_t n_seg, int32_t max_q_len,
+                                       int32_t n_head, int32_t head_dim, float scale, void* stream) {
+    FGR_REQUIRE(q && kv_img && o && q_off && kv_off && kv_seg && n_seg > 0 && n_head > 0 &&
+                    max_q_len >= 0 && n_kv_rows >= 0,
+                "fgr_attention_f16x3_img: bad arguments");
+    FGR_REQUIRE(head_dim == 32, "fgr_attention_f16x3_img: head_dim %d (32)", head_dim);
+    FGR_REQUIRE(ld_q >= n_head * 32 && ld_o >= n_head * 32 && ld_q % 4 == 0 && ld_o % 4 == 0 &&
+                    ((reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(o) |
+                      reinterpret_cast<uintptr_t>(kv_img)) & 15) == 0,
+                "fgr_attention_f16x3_img: strides / alignment");
+    if (max_q_len == 0 || n_kv_rows == 0) return FGR_OK;
+    hipStream_t st = as_stream(stream);
+    TimedCall timed_(st);
+    const int64_t nt = ceil_div(n_kv_rows, 64) * n_head;
+    const uint4* img = static_cast<const uint4*>(kv_img);
+    const int2* sc = reinterpret_cast<const int2*>(static_cast<const char*>(kv_img) + nt * units<32>() * 16);
+    const int n_qblk = (int)ceil_div(max_q_len, 64);
+    const int64_t n_blocks = ceil_div((int64_t)n_seg * n_head, 8) * 8 * n_qblk;
+    const float sl2 = scale * 1.4426950408889634f;
+    hipLaunchKernelGGL((attn_f16x3_v2_kernel<32>), dim3((unsigned)n_blocks), dim3(256), 0, st, q, ld_q,
+                       img, sc, o, ld_o, q_off, kv_off, kv_seg, n_head, n_seg, n_qblk, sl2, 1);
+    FGR_CHECK_LAUNCH("attn_f16x3_v2_kernel (global tiles)");
     return FGR_OK;
 }

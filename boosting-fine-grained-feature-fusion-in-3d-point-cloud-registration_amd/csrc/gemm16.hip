@@ -42,7 +42,8 @@ char bf16_tile(int m, int n, int k);
 int bf16_ksplit(char cfg, int m, int n, int k);
 struct RsLn {
     const float* g; const float* b; const float* add; int64_t ld_add; float eps;
-    const float* g2; const float* b2; float* out2; int64_t ld_out2;
+    const float* g2; const float* b2; float* out2; int64_t ld_out2;    // optional side output
+    char* kv_img; int2* kv_sc; int n_head; int kv_col0;                // optional K / V images
 };
 struct RsHead {
     int n_act; float* c2;
@@ -1251,7 +1252,7 @@ static int gemm_f16x3_ln_impl(const float* x, int64_t ldx, const float* gamma, c
                                                       image_bytes_h3(n, k));
     hipStream_t st = as_stream(stream);
     TimedCall timed_(st);
-    const RsLn ln{gamma, beta, add, ld_add, eps, gamma2, beta2, out2, ld_out2};
+    const RsLn ln{gamma, beta, add, ld_add, eps, gamma2, beta2, out2, ld_out2, nullptr, nullptr, 0, 0};
     FGR_REQUIRE(gemm_rs_f16x3(x, ldx, w_img, ksteps_h3(k), wsc, c, ldc, bias, nullptr, 0, m, n, k,
                               act, st, &ln),
                 "fgr_gemm_f16x3_ln: row-stationary kernel rejected %d x %d x %d", m, n, k);
@@ -1318,5 +1319,57 @@ extern "C" int fgr_corr_head_f16x3(const float* f, int64_t ldf, int32_t m, int32
                               FGR_ACT_RELU, st, nullptr, &h2),
                 "fgr_corr_head_f16x3: row-stationary kernel rejected the second product");
     FGR_CHECK_LAUNCH("gemm_rs (corr head, coor_mlp[2] -> coor_mlp[4])");
+    return FGR_OK;
+}
+
+// ---- the pre-norm in_proj with the attention's K / V images in its epilogue ----------------
+// Image geometry (attention16.hip, head dim 32): one 16 KB image per (global 64-row tile,
+// head), then the int2 scale exponents of all of them.
+extern "C" int fgr_kv_image_bytes(int64_t n_rows, int32_t n_head, int32_t head_dim, size_t* bytes) {
+    FGR_REQUIRE(bytes && n_rows >= 0 && n_head > 0 && head_dim == 32,
+                "fgr_kv_image_bytes: bad arguments (head_dim 32)");
+    const int64_t nt = std::max<int64_t>(1, ceil_div(n_rows, 64)) * n_head;
+    *bytes = (size_t)(nt * 1024 * 16 + nt * 8);
+    return FGR_OK;
+}
+
+extern "C" int fgr_gemm_f16x3_ln_qkv_supported(int32_t m, int32_t d, int32_t n_head) {
+    return (m > 0 && d == 32 * n_head && d == 256 && fgr_gemm_f16x3_ln_supported(m, 3 * d, d)) ? 1 : 0;
+}
+
+extern "C" int fgr_gemm_f16x3_ln_qkv(const float* x, int64_t ldx, const float* gamma,
+                                     const float* beta, float eps, const float* add, int64_t ld_add,
+                                     const void* w_img, float* q, int64_t ld_q, const float* bias,
+                                     int32_t m, int32_t d, int32_t n_head, void* kv_img,
+                                     const float* gamma2, const float* beta2, float* out2,
+                                     int64_t ld_out2, void* stream) {
+    FGR_REQUIRE(x && gamma && beta && add && w_img && q && bias && kv_img && m >= 0 && ldx >= d &&
+                    ld_add >= d && ld_q >= d && eps >= 0.f && (!out2 || (gamma2 && beta2 && ld_out2 >= d)),
+                "fgr_gemm_f16x3_ln_qkv: bad arguments");
+    FGR_REQUIRE(m == 0 || fgr_gemm_f16x3_ln_qkv_supported(m, d, n_head),
+                "fgr_gemm_f16x3_ln_qkv: m %d d %d heads %d not supported", m, d, n_head);
+    const uintptr_t al = reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(gamma) |
+                         reinterpret_cast<uintptr_t>(beta) | reinterpret_cast<uintptr_t>(add) |
+                         reinterpret_cast<uintptr_t>(w_img) | reinterpret_cast<uintptr_t>(q) |
+                         reinterpret_cast<uintptr_t>(bias) | reinterpret_cast<uintptr_t>(kv_img) |
+                         reinterpret_cast<uintptr_t>(gamma2) | reinterpret_cast<uintptr_t>(beta2) |
+                         reinterpret_cast<uintptr_t>(out2);
+    FGR_REQUIRE((al & 15) == 0 && ldx % 4 == 0 && ld_q % 4 == 0 && ld_add % 4 == 0 &&
+                    (!out2 || ld_out2 % 4 == 0),
+                "fgr_gemm_f16x3_ln_qkv: operands must be 16-B aligned with row strides %% 4 == 0");
+    if (m == 0) return FGR_OK;
+    const int n = 3 * d;
+    const float* wsc = reinterpret_cast<const float*>(static_cast<const char*>(w_img) +
+                                                      image_bytes_h3(n, d));
+    const int64_t nt = ceil_div(m, 64) * n_head;
+    hipStream_t st = as_stream(stream);
+    TimedCall timed_(st);
+    const RsLn ln{gamma, beta, add, ld_add, eps, gamma2, beta2, out2, ld_out2,
+                  static_cast<char*>(kv_img),
+                  reinterpret_cast<int2*>(static_cast<char*>(kv_img) + nt * 1024 * 16), n_head, d};
+    FGR_REQUIRE(gemm_rs_f16x3(x, ldx, w_img, ksteps_h3(d), wsc, q, ld_q, bias, nullptr, 0, m, n, d,
+                              FGR_ACT_NONE, st, &ln),
+                "fgr_gemm_f16x3_ln_qkv: row-stationary kernel rejected %d x %d x %d", m, n, d);
+    FGR_CHECK_LAUNCH("gemm_rs_ln_qkv");
     return FGR_OK;
 }

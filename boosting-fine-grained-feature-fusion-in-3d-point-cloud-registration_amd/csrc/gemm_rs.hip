@@ -35,6 +35,15 @@
 // outputs, no split), reduced over the 4 lane groups at the end: coor_mlp[2] -> ReLU ->
 // coor_mlp[4] in one launch, the hidden (rows, d) tensor never written.
 //
+// K / V attention images (KV; fgr_gemm_f16x3_ln_qkv, head dim 32): the in_proj launch of the
+// pre-norm layer writes the q columns as fp32 and the k / v columns straight into the f16x3
+// attention images that attention16.hip reads (one per GLOBAL 64-row tile and head: the
+// block's 64 rows, RT = 1), instead of fp32 k / v for a separate image launch. A head is two
+// panels: its 8 values per lane stay in registers until both are done, each wave's max |.|
+// goes to LDS, and after the next panel barrier every wave reads the four maxima, takes the
+// tile's power-of-two exponent (max in [2^14, 2^15), as attn_kv_image16_kernel) and stores
+// its split terms.
+//
 // Swapped orientation (gemm16.hip): W fragments are the MFMA A operand, activation fragments
 // the B operand, so a lane's 4 accumulators are 4 consecutive output columns of ONE row.
 // 16x16x32 f16 lane maps (lane l, g = l >> 4, c = l & 15): A[i = c][k = 8g + e],
@@ -68,6 +77,9 @@ struct RsArgs {
     float* c2;                        //   and column n_act -> c2[row] (not stored in C)
     const float* w4; const float* b4; // HEAD: (3, N) fp32 rows and bias of the 3-wide output
     float* out3;                      //   -> out3 (M, 3)
+    char* kv_img;                     // KV: attention K / V images per (global 64-row tile, head)
+    int2* kv_sc;                      //   and their scale exponents (x: K, y: V)
+    int n_head, kv_col0;              //   heads (head dim 32); first K column (V: + 32 n_head)
 };
 
 // s_waitcnt vmcnt(n) lgkmcnt(0) -- gfx9 encoding
@@ -125,8 +137,14 @@ __device__ __forceinline__ float finish_ct(float y, float b, float r) {
 // LNM: 0 plain, 1 LayerNorm prologue, 2 LayerNorm prologue + row add, 3 as 2 plus a second
 // LayerNorm output of the same rows (the encoder's per-layer output norm), written by the
 // blocks of the first column group
-template <int RT, int KS, bool RES, int ACT, int LNM, bool HEAD = false, bool DEFER = false>
-__global__ void __launch_bounds__(256) gemm_rs_kernel(RsArgs p) {
+// f16x3 attention image geometry for head dim 32 (attention16.hip units<32>, unit_v<32>,
+// v_swz<32>): 1024 16-B units per (tile, head), V from unit 512
+constexpr int kKvUnits = 1024;
+constexpr int kKvUnitV = 512;
+
+template <int RT, int KS, bool RES, int ACT, int LNM, bool HEAD = false, bool DEFER = false,
+          bool KV = false>
+__global__ void __launch_bounds__(256, KV ? 2 : 1) gemm_rs_kernel(RsArgs p) {
     constexpr bool LN = LNM > 0;
     constexpr int PANEL_U = KS * 128;                  // 16-B units per W panel
     constexpr int PW = PANEL_U / 256;                  // DMA pieces (1 KiB) per wave per panel
@@ -136,6 +154,9 @@ __global__ void __launch_bounds__(256) gemm_rs_kernel(RsArgs p) {
     __shared__ float4 lng[LN ? KS * 8 : 1], lnb[LN ? KS * 8 : 1];  // LN gamma / beta (K / 4)
     __shared__ float4 lng2[LNM == 3 ? KS * 8 : 1], lnb2[LNM == 3 ? KS * 8 : 1];
     __shared__ float4 colh[HEAD ? 3 * kRsMaxNc * 4 : 1];            // HEAD: w4 by (j, panel, g)
+    __shared__ float kvred[KV ? 2 : 1][4];                          // KV: per-wave head maxima
+    __shared__ float kvbuf[KV ? 4 : 1][KV ? 8 : 1][64];             // KV: the head's 8 values per lane
+    static_assert(!KV || RT == 1, "KV images: one 64-row tile per block");
 
     const int nbm = (p.M + 64 * RT - 1) / (64 * RT);
     const int npanel = (p.N + 15) / 16;
@@ -318,6 +339,45 @@ __global__ void __launch_bounds__(256) gemm_rs_kernel(RsArgs p) {
                 colh[j * kRsMaxNc * 4 + u] = *reinterpret_cast<const float4*>(p.w4 + (int64_t)j * p.N + n);
         }
     }
+    // KV: the running max of the current head's 8 values per lane (two panels; the values in
+    // kvbuf), and the head (+1) whose image is due after the next barrier (0: none)
+    float kvm = 0.f;
+    int kv_pend = 0;
+    auto kv_finish = [&]() {
+        const int hd = kv_pend - 1;
+        kv_pend = 0;
+        const float tm = fmaxf(fmaxf(kvred[hd & 1][0], kvred[hd & 1][1]),
+                               fmaxf(kvred[hd & 1][2], kvred[hd & 1][3]));
+        const int isv = hd >= p.n_head ? 1 : 0, head = hd - isv * p.n_head;
+        const int e = tm > 0.f ? min(15 - __builtin_amdgcn_frexp_expf(tm), 127) : 0;
+        const float sc = __builtin_ldexpf(1.f, e);
+        const int64_t tile = (int64_t)bm * p.n_head + head;
+        if (tid == 0) reinterpret_cast<int*>(p.kv_sc + tile)[isv] = e;
+        char* base = p.kv_img + tile * (kKvUnits * 16);
+        const int key = wv * 16 + c;
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            _Float16 tv[2][4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float x = kvbuf[wv][4 * half + j][lane] * sc;
+                tv[0][j] = (_Float16)x;
+                tv[1][j] = (_Float16)(x - (float)tv[0][j]);
+            }
+            const int d0 = 16 * half + 4 * g;               // first of the lane's 4 dims
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                char* dst;
+                if (isv) {                                  // [term][key][32] f16, chunks ^ v_swz
+                    const int ch = (d0 >> 3) ^ (((key >> 2) & 1) << 1);
+                    dst = base + kKvUnitV * 16 + t * (128 * 32) + key * 64 + ch * 16 + (d0 & 4) * 2;
+                } else {                                    // [term][g'][key] x 8 dims
+                    dst = base + ((t * 4 + (d0 >> 3)) * 64 + key) * 16 + (d0 & 4) * 2;
+                }
+                *reinterpret_cast<uint2*>(dst) = *reinterpret_cast<const uint2*>(tv[t]);
+            }
+        }
+    };
     float h3[RT][3];
     if constexpr (HEAD) {
 #pragma unroll
@@ -341,6 +401,10 @@ __global__ void __launch_bounds__(256) gemm_rs_kernel(RsArgs p) {
     auto nstore = [&](int qq) -> int {
         if constexpr (HEAD) return 0;
         const int col = (p0 + qq) * 16;
+        // KV panels store nothing in their epilogue (their image stores come after the next
+        // barrier and are not counted: an under-count only makes a wait stricter)
+        if constexpr (KV)
+            if (col >= p.kv_col0) return 0;
         if (p.c2 && col >= p.n_act) return col == p.n_act ? nst : 0;
         return nst;
     };
@@ -367,6 +431,32 @@ __global__ void __launch_bounds__(256) gemm_rs_kernel(RsArgs p) {
     auto epilogue = [&](int q, const f32x4 (&acc)[RT], const float4 (&rv)[RT]) {
         const int n = (p0 + q) * 16 + 4 * g;
         const float4 ws = colw[q * 4 + g], bv = colb[q * 4 + g];
+        if constexpr (KV) {
+            const int col = (p0 + q) * 16;
+            if (col >= p.kv_col0) {                         // panel-uniform: a K or V panel
+                const int rel = col - p.kv_col0;
+                const int half = (rel >> 4) & 1;
+                const float s0 = rs[0] * ws.x, s1 = rs[0] * ws.y, s2 = rs[0] * ws.z, s3 = rs[0] * ws.w;
+                const bool ok = mw + c < p.M;               // rows past M: zeros, not in the max
+                const float y0 = ok ? acc[0][0] * s0 + bv.x : 0.f, y1 = ok ? acc[0][1] * s1 + bv.y : 0.f;
+                const float y2 = ok ? acc[0][2] * s2 + bv.z : 0.f, y3 = ok ? acc[0][3] * s3 + bv.w : 0.f;
+                const float mx = max3_abs(y0, y1, fmaxf(fabsf(y2), fabsf(y3)));
+                // parked in LDS (registers are at their limit in the LN prologue's kernel)
+                kvbuf[wv][4 * half + 0][lane] = y0;
+                kvbuf[wv][4 * half + 1][lane] = y1;
+                kvbuf[wv][4 * half + 2][lane] = y2;
+                kvbuf[wv][4 * half + 3][lane] = y3;
+                if (half == 0) {
+                    kvm = mx;
+                } else {
+                    const float wm = wave_max(fmaxf(kvm, mx));
+                    const int hd = rel >> 5;                    // head index over [K heads | V heads]
+                    if (lane == 0) kvred[hd & 1][wv] = wm;
+                    kv_pend = 1 + hd;                           // finalised after the next barrier
+                }
+                return;
+            }
+        }
         if constexpr (HEAD) {
             // the ReLU'd outputs against coor_mlp[4]'s rows, fp32, not stored
             const float4 w0 = colh[q * 4 + g], w1 = colh[kRsMaxNc * 4 + q * 4 + g],
@@ -437,6 +527,8 @@ __global__ void __launch_bounds__(256) gemm_rs_kernel(RsArgs p) {
                               (q + 1 < np ? PW : 0));
         }
         __builtin_amdgcn_s_barrier();                    // every wave's pieces; buffer of q - 1 free
+        if constexpr (KV)
+            if (kv_pend) kv_finish();                    // block-uniform
         if constexpr (RES) {
             if constexpr (!DEFER) {
                 if (q + 1 < np) load_res(q + 1, rnext);
@@ -464,6 +556,12 @@ __global__ void __launch_bounds__(256) gemm_rs_kernel(RsArgs p) {
         if constexpr (RES) load_res(np - 1, rcur);
         epilogue(np - 1, prev, rcur);
     }
+    if constexpr (KV) {
+        if (kv_pend) {                                   // the last head of the block
+            __syncthreads();
+            kv_finish();
+        }
+    }
     if constexpr (HEAD) {
         // sum the lane groups' column quads: lanes c, c + 16, c + 32, c + 48 hold one row
 #pragma unroll
@@ -483,6 +581,15 @@ template <int RT, int KS, int ACT, bool D>
 void launch_rs_act(const RsArgs& a, unsigned blocks, hipStream_t st) {
     // LN prologue: one row tile per wave (at two, the row + add registers of the prologue
     // exceed the 256 VGPRs of two waves per SIMD and spill), no residual (checked by the caller)
+    if constexpr (RT == 1 && ACT == FGR_ACT_NONE && KS == 8) {
+        if (a.ln_g && a.ln_add && a.kv_img) {
+            if (a.ln_out2)
+                hipLaunchKernelGGL((gemm_rs_kernel<RT, KS, false, ACT, 3, false, D, true>), dim3(blocks), dim3(256), 0, st, a);
+            else
+                hipLaunchKernelGGL((gemm_rs_kernel<RT, KS, false, ACT, 2, false, D, true>), dim3(blocks), dim3(256), 0, st, a);
+            return;
+        }
+    }
     if constexpr (RT == 1 && ACT != FGR_ACT_RELU_RES_LEAKY) {
         if (a.ln_g && a.ln_add && a.ln_out2) {
             hipLaunchKernelGGL((gemm_rs_kernel<RT, KS, false, ACT, 3, false, D>), dim3(blocks), dim3(256), 0, st, a);
@@ -535,6 +642,7 @@ bool launch_rs_k(const RsArgs& a, unsigned blocks, hipStream_t st) {
 struct RsLn {
     const float* g; const float* b; const float* add; int64_t ld_add; float eps;
     const float* g2; const float* b2; float* out2; int64_t ld_out2;    // optional side output
+    char* kv_img; int2* kv_sc; int n_head; int kv_col0;                // optional K / V images
 };
 // the correspondence-head epilogues (see the top of this file): n_act / c2, or out3 with w4 / b4
 struct RsHead {
@@ -577,6 +685,14 @@ bool gemm_rs_f16x3(const float* A, int64_t lda, const void* W, int ksteps, const
     }
     nc = std::min(std::min(nc, npanel), kRsMaxNc);
     if (head && head->out3) nc = npanel;              // the 3-wide head needs whole rows
+    if (ln && ln->kv_img) {
+        // K / V images: head dim 32 (two panels per head, never split between blocks), the
+        // k | v columns the last 64 n_head, one 64-row tile per block (RT = 1, K = 256)
+        if (ksteps != 8 || ln->n_head <= 0 || ln->kv_col0 % 32 != 0 ||
+            N != ln->kv_col0 + 64 * ln->n_head)
+            return false;
+        nc += nc & 1;
+    }
     const int ngrp = (npanel + nc - 1) / nc;
     const unsigned blocks = (unsigned)((int64_t)nbm * ngrp);
     RsArgs a{A, lda, (const u32x4*)W, wsc, C, ldc, bias, R, ldr, M, N, K, act, nc,
@@ -584,7 +700,9 @@ bool gemm_rs_f16x3(const float* A, int64_t lda, const void* W, int ksteps, const
              ln ? ln->ld_add : 0, ln ? ln->eps : 0.f, ln ? ln->g2 : nullptr,
              ln ? ln->b2 : nullptr, ln ? ln->out2 : nullptr, ln ? ln->ld_out2 : 0,
              head ? head->n_act : N, head ? head->c2 : nullptr, head ? head->w4 : nullptr,
-             head ? head->b4 : nullptr, head ? head->out3 : nullptr};
+             head ? head->b4 : nullptr, head ? head->out3 : nullptr,
+             ln ? ln->kv_img : nullptr, ln ? ln->kv_sc : nullptr, ln ? ln->n_head : 0,
+             ln ? ln->kv_col0 : N};
 #define RS_CASE(rt, ks) \
     if (RT == rt && ksteps == ks) return launch_rs_k<rt, ks>(a, blocks, st);
     RS_CASE(2, 2) RS_CASE(2, 4) RS_CASE(2, 6) RS_CASE(2, 8)

@@ -658,6 +658,45 @@ def attention_flops(q_off, kv_off, kv_seg, d):
     return sum(4 * (qo[i + 1] - qo[i]) * (ko[ks[i] + 1] - ko[ks[i]]) * d for i in range(len(ks)))
 
 
+def ln_qkv_supported(m, d, n_head) -> bool:
+    return bool(_lib.load().fgr_gemm_f16x3_ln_qkv_supported(int(m), int(d), int(n_head)))
+
+
+def ln_qkv_attention(x, norm, w_img, bias, pos, q_off, kv_seg, max_len, n_head, side=None):
+    """The pre-norm attention sub-layer's in_proj + attention core in two launches:
+    fgr_gemm_f16x3_ln_qkv (LayerNorm(x) + pos -> q fp32 and the K / V images of every global
+    64-row tile, transformers.py:193-196 / :213-221) then fgr_attention_f16x3_img (head dim 32).
+    ``side`` = (norm2, out2): out2 = norm2(x) from the same statistics. -> o (N, d)."""
+    _dev(x, bias, pos, q_off, kv_seg)
+    n, d = x.shape
+    x, pos = x.contiguous(), pos.contiguous()
+    gamma, beta = norm.weight.contiguous(), norm.bias.contiguous()
+    L = _lib.load()
+    nb = _lib._sz(0)
+    _lib.check(L.fgr_kv_image_bytes(n, n_head, d // n_head, nb), 'fgr_kv_image_bytes')
+    img = _workspace(x.device, nb.value)
+    q = torch.empty((n, d), dtype=torch.float32, device=x.device)
+    g2 = b2 = out2 = None
+    if side is not None:
+        g2, b2, out2 = side[0].weight.contiguous(), side[0].bias.contiguous(), side[1]
+        assert out2.shape == x.shape and out2.stride(1) == 1
+    t0 = _begin('gemm', (n, 3 * d, d))
+    _lib.check(L.fgr_gemm_f16x3_ln_qkv(
+        _ptr(x), x.stride(0), _ptr(gamma), _ptr(beta), float(norm.eps), _ptr(pos), pos.stride(0),
+        _ptr(w_img.img), _ptr(q), q.stride(0), _ptr(bias), n, d, n_head, _ptr(img), _ptr(g2),
+        _ptr(b2), _ptr(out2), out2.stride(0) if out2 is not None else 0, _stream()),
+        'fgr_gemm_f16x3_ln_qkv')
+    _end('gemm', t0, 2 * n * 3 * d * d)
+    o = torch.empty((n, d), dtype=torch.float32, device=x.device)
+    t0 = _begin('attention')
+    _lib.check(L.fgr_attention_f16x3_img(
+        _ptr(q), q.stride(0), _ptr(img), n, _ptr(o), o.stride(0), _ptr(q_off), _ptr(q_off),
+        _ptr(kv_seg), q_off.numel() - 1, int(max_len), n_head, d // n_head,
+        float(math.sqrt(1.0 / float(d // n_head))), _stream()), 'fgr_attention_f16x3_img')
+    _end('attention', t0, lambda: attention_flops(q_off, q_off, kv_seg, d))
+    return o
+
+
 def corr_head_supported(m, d) -> bool:
     return bool(_lib.load().fgr_corr_head_supported(int(m), int(d)))
 

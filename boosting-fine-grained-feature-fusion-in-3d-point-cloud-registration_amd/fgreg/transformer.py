@@ -23,8 +23,15 @@ import copy
 import torch
 import torch.nn as nn
 
+import os
+
+from . import linear as lin
 from . import ops
 from .linear import linear, linear_ln, ln_fusable
+
+# the pre-norm in_proj writes the attention's K / V images itself where supported
+# (fgr_gemm_f16x3_ln_qkv; FGREG_QKV_IMAGES=0: fp32 q | k | v and the attention's own image launch)
+QKV_IMAGES = os.environ.get('FGREG_QKV_IMAGES', '1') != '0'
 
 
 class Segments:
@@ -90,6 +97,12 @@ class TransformerCrossEncoderLayer(nn.Module):
         if ln is not None:
             x, norm, pos = ln
             d = x.shape[1]
+            if (QKV_IMAGES and lin.MODE == 'f16x3' and ops.ATTN_MODE == 'f16x3'
+                    and ops.ln_qkv_supported(x.shape[0], d, self.nhead)
+                    and (side is None or side[0].eps == norm.eps)):
+                # k / v straight into the attention's images (no fp32 k / v, no image launch)
+                return ops.ln_qkv_attention(x, norm, lin.weight_image(W, mode='f16x3'), b, pos,
+                                            seg.off, kv_seg, seg.max_len, self.nhead, side=side)
             qkv = linear_ln(x, norm, W, b, add=pos, side=side)        # (N, 3d): [q | k | v]
             q, k, v = qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:]
             return ops.attention(q, k, v, seg.off, seg.off, kv_seg, seg.max_len, self.nhead)

@@ -442,6 +442,28 @@ int fgr_crop_pairs_assemble(const float* raw, int32_t ld, const int64_t* offsets
                             const double* noise, const float* rt, int32_t m, float* xyz,
                             uint8_t* overlap, int64_t* corr, int32_t* n_corr, void* stream);
 
+/* The pre-norm layer's in_proj with the attention's K / V images written in its epilogue
+ * (transformers.py:193-196 / :213-221 + the image building of fgr_attention_f16x3, head dim 32):
+ * qkv = (LayerNorm(x) * gamma + beta + add) W^T + bias as fgr_gemm_f16x3_ln, but only the q
+ * columns [0, d) go to q (m, d; ld_q) as fp32 -- the k and v columns go straight into kv_img:
+ * the f16x3 K / V images of every GLOBAL 64-row tile and head, then their int2 scale exponents
+ * (fgr_kv_image_bytes(m, n_head, 32) bytes). Optional side output out2 = LayerNorm(x) * gamma2 +
+ * beta2 as fgr_gemm_f16x3_ln_out2. fgr_gemm_f16x3_ln_qkv_supported(m, d, n_head): d = 32 n_head =
+ * 256 and the row-stationary kernel for (m, 3d, d).
+ * fgr_attention_f16x3_img: fgr_attention_f16x3 (head dim 32) reading those images (kv rows = the
+ * same packed rows, n_kv_rows = m) instead of building its own. */
+int fgr_kv_image_bytes(int64_t n_rows, int32_t n_head, int32_t head_dim, size_t* bytes);
+int fgr_gemm_f16x3_ln_qkv_supported(int32_t m, int32_t d, int32_t n_head);
+int fgr_gemm_f16x3_ln_qkv(const float* x, int64_t ldx, const float* gamma, const float* beta,
+                          float eps, const float* add, int64_t ld_add, const void* w_img, float* q,
+                          int64_t ld_q, const float* bias, int32_t m, int32_t d, int32_t n_head,
+                          void* kv_img, const float* gamma2, const float* beta2, float* out2,
+                          int64_t ld_out2, void* stream);
+int fgr_attention_f16x3_img(const float* q, int64_t ld_q, const void* kv_img, int64_t n_kv_rows,
+                            float* o, int64_t ld_o, const int64_t* q_off, const int64_t* kv_off,
+                            const int32_t* kv_seg, int32_t n_seg, int32_t max_q_len,
+                            int32_t n_head, int32_t head_dim, float scale, void* stream);
+
 /* The CorrespondenceRegressor head (finegrained_regtr.py:411-455, direct_regress_coor: True) on
  * the (m, d) stacked layer outputs f in two row-stationary f16x3 launches:
  *   hidden = ReLU(f W0^T + b0), logits = f Wc^T + bc   -- ONE product over the image of the

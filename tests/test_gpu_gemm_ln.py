@@ -221,3 +221,52 @@ def test_encoder_bench_size_vs_oracle(gpu):
     assert out.shape == (NL, 2 * B * L, d)
     for i in range(NL):
         assert rel_err(out[i], pack(*refs[i])) < 1e-4, i
+
+
+@pytest.mark.parametrize('lens,side', [([717, 596, 1, 700, 64, 130, 5000, 2336], False),
+                                       ([596] * 16, True), ([65, 63, 64, 1, 128], False)])
+def test_ln_qkv_images_vs_two_launch_path(gpu, lens, side):
+    """fgr_gemm_f16x3_ln_qkv (the in_proj writing q fp32 and the K / V images of every global
+    64-row tile, head dim 32) + fgr_attention_f16x3_img vs the path it replaces (LN-fused in_proj
+    -> fp32 q | k | v -> fgr_attention_f16x3 with per-segment images): segments starting
+    anywhere inside a tile (incl. a 1-row cloud and tiles shared by three clouds), self- and
+    cross-attention, the side output. Both are fp32-accurate: <= 2e-6 normwise apart and
+    <= 1e-5 from a float64 LayerNorm -> in_proj -> softmax attention."""
+    from fgreg import linear as lin
+    from fgreg import ops
+    n, d, nh = sum(lens), 256, 8
+    x, norm, pos, w, b = _inputs(n, d, 3 * d, seed=len(lens))
+    x, pos, w, b, norm = x.to(gpu), pos.to(gpu), w.to(gpu), b.to(gpu), norm.to(gpu)
+    assert ops.ln_qkv_supported(n, d, nh) or n < 8000
+    if not ops.ln_qkv_supported(n, d, nh):
+        pytest.skip('shape not on the row-stationary path')
+    off = ops.offsets(lens, gpu)
+    B = len(lens) // 2
+    for kv in (list(range(len(lens))), [(c + B) % len(lens) for c in range(len(lens))]
+               if len(lens) % 2 == 0 else list(range(len(lens)))):
+        kv_seg = torch.tensor(kv, dtype=torch.int32, device=gpu)
+        norm2 = torch.nn.LayerNorm(d).to(gpu)
+        out2 = torch.empty_like(x) if side else None
+        o = ops.ln_qkv_attention(x, norm, lin.weight_image(w, mode='f16x3'), b, pos, off, kv_seg,
+                                 max(lens), nh, side=(norm2, out2) if side else None)
+        qkv = lin.linear_ln(x, norm, w, b, add=pos)
+        o2 = ops.attention(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], off, off, kv_seg,
+                           max(lens), nh)
+        assert rel_err(o, o2) < 2e-6, rel_err(o, o2)
+        h = torch.nn.functional.layer_norm(x.double(), (d,), norm.weight.double(),
+                                           norm.bias.double(), norm.eps) + pos.double()
+        qkv64 = h @ w.double().t() + b.double()
+        offs = np.cumsum([0] + lens)
+        outs = []
+        for i in range(len(lens)):
+            j = kv[i]
+            q = qkv64[offs[i]:offs[i + 1], :d].reshape(-1, nh, 32).transpose(0, 1) / math.sqrt(32)
+            k = qkv64[offs[j]:offs[j + 1], d:2 * d].reshape(-1, nh, 32).transpose(0, 1)
+            v = qkv64[offs[j]:offs[j + 1], 2 * d:].reshape(-1, nh, 32).transpose(0, 1)
+            outs.append((torch.softmax(q @ k.transpose(1, 2), -1) @ v).transpose(0, 1).reshape(-1, d))
+        o64 = torch.cat(outs, 0)
+        assert rel_err(o, o64) < 1e-5, rel_err(o, o64)
+        if side:
+            ref2 = torch.nn.functional.layer_norm(x.double(), (d,), norm2.weight.double(),
+                                                  norm2.bias.double(), norm2.eps)
+            assert rel_err(out2, ref2) < 1e-6

@@ -5,7 +5,7 @@ set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 tag=${1:-r04}
-timeout -k 10 300 python -u -m pytest "tests/test_gpu_kernels.py::test_corr_head_fused_vs_fp64" tests/test_gpu_forward.py -x -q --timeout 150 --timeout-method thread -p no:cacheprovider > gpurun_out/tests_${tag}_a.log 2>&1 || { echo "TESTS A FAILED"; tail -30 gpurun_out/tests_${tag}_a.log; exit 1; }
+timeout -k 10 400 python -u -m pytest "tests/test_gpu_kernels.py::test_corr_head_fused_vs_fp64" tests/test_gpu_gemm_ln.py tests/test_gpu_forward.py -x -q --timeout 150 --timeout-method thread -p no:cacheprovider > gpurun_out/tests_${tag}_a.log 2>&1 || { echo "TESTS A FAILED"; tail -30 gpurun_out/tests_${tag}_a.log; exit 1; }
 tail -2 gpurun_out/tests_${tag}_a.log
 timeout -k 10 240 python -u tools/rs_defer_ab.py > gpurun_out/rs_defer_ab_${tag}.txt 2>&1 || { echo "AB FAILED"; tail -20 gpurun_out/rs_defer_ab_${tag}.txt; exit 1; }
 cat gpurun_out/rs_defer_ab_${tag}.txt | grep -v amdgpu.ids
