@@ -9,8 +9,10 @@
 // row max over all of K into [2^14, 2^15): no in-flight rescaling, the scale goes to the
 // epilogue), and keeps them resident; the block then streams its range of W panels (16
 // output columns x K each, the fgr_split_weights_h3 image as it lies) global -> LDS by
-// LDS-DMA into a two-panel ring shared by the 4 waves, and per panel runs a pure MFMA loop
-// (3 * RT * K/32 MFMAs per wave, no split VALU) followed by a 16-B-per-lane epilogue.
+// LDS-DMA into a three-panel ring shared by the 4 waves (two in flight), and per panel runs a
+// pure MFMA loop (3 * RT * K/32 MFMAs per wave, no split VALU); the 16-B-per-lane epilogue of
+// panel q - 1 is issued after panel q's MFMAs, so its VALU and stores fill the MFMA shadows
+// (round 4: 1.09-1.17x on the LN-fused and 57264-row shapes).
 //
 // Precision: per product the three significant fp16 products hh, hm, mh in fp32
 // accumulation as in gemm16.hip; one scale per row means elements far below the row max
@@ -142,14 +144,15 @@ __device__ __forceinline__ float finish_ct(float y, float b, float r) {
 constexpr int kKvUnits = 1024;
 constexpr int kKvUnitV = 512;
 
-template <int RT, int KS, bool RES, int ACT, int LNM, bool HEAD = false, bool DEFER = false,
-          bool KV = false>
+template <int RT, int KS, bool RES, int ACT, int LNM, bool HEAD = false, bool KV = false>
 __global__ void __launch_bounds__(256, KV ? 2 : 1) gemm_rs_kernel(RsArgs p) {
     constexpr bool LN = LNM > 0;
     constexpr int PANEL_U = KS * 128;                  // 16-B units per W panel
     constexpr int PW = PANEL_U / 256;                  // DMA pieces (1 KiB) per wave per panel
     static_assert(PANEL_U % 256 == 0, "KS even");
-    __shared__ u32x4 ring[kRsNb * PANEL_U];
+    constexpr int NB = kRsNb;                          // W panel ring
+    constexpr int LA = NB - 1;                         // DMA lookahead in panels
+    __shared__ u32x4 ring[NB * PANEL_U];
     __shared__ float4 colw[kRsMaxNc * 4], colb[kRsMaxNc * 4];   // per (panel, g): wsc, bias
     __shared__ float4 lng[LN ? KS * 8 : 1], lnb[LN ? KS * 8 : 1];  // LN gamma / beta (K / 4)
     __shared__ float4 lng2[LNM == 3 ? KS * 8 : 1], lnb2[LNM == 3 ? KS * 8 : 1];
@@ -178,7 +181,7 @@ __global__ void __launch_bounds__(256, KV ? 2 : 1) gemm_rs_kernel(RsArgs p) {
     const u32x4* wsrc = p.W + (int64_t)p0 * PANEL_U + wv * 64 + lane;
     auto dma = [&](int q) {
         __attribute__((address_space(3))) char* dst =
-            (__attribute__((address_space(3))) char*)(ring + (q % kRsNb) * PANEL_U) + wv * 1024;
+            (__attribute__((address_space(3))) char*)(ring + (q % NB) * PANEL_U) + wv * 1024;
 #pragma unroll
         for (int j = 0; j < PW; ++j)
             __builtin_amdgcn_global_load_lds((const void*)(wsrc + (int64_t)q * PANEL_U + j * 256),
@@ -186,7 +189,7 @@ __global__ void __launch_bounds__(256, KV ? 2 : 1) gemm_rs_kernel(RsArgs p) {
                                              16, 0, 0);
     };
     dma(0);
-    if (np > 1) dma(1);
+    if (LA >= 2 && np > 1) dma(1);
 
     // activation rows -> registers, one scale per row, split once
     f16x8 af[RT][KS][2];
@@ -411,7 +414,7 @@ __global__ void __launch_bounds__(256, KV ? 2 : 1) gemm_rs_kernel(RsArgs p) {
     typedef __attribute__((address_space(3))) u32x4 lds_u4;
     // panel q's pure MFMA loop (W fragments from the LDS ring, A resident)
     auto panel_mfma = [&](int q, f32x4 (&acc)[RT]) {
-        const uint32_t base = (uint32_t)(uintptr_t)(ring + (q % kRsNb) * PANEL_U) +
+        const uint32_t base = (uint32_t)(uintptr_t)(ring + (q % NB) * PANEL_U) +
                               (uint32_t)(g * 16 + c) * 16;
 #pragma unroll
         for (int i = 0; i < RT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -509,53 +512,35 @@ __global__ void __launch_bounds__(256, KV ? 2 : 1) gemm_rs_kernel(RsArgs p) {
         }
     };
 
-    float4 rcur[RT], rnext[RT];
-    if constexpr (RES && !DEFER) load_res(0, rcur);
+    float4 rcur[RT];
     f32x4 prev[RT];
     for (int q = 0; q < np; ++q) {
         // vector-memory ops issued after panel q's DMA (issued in iteration q - 2), counted so
         // that vmcnt guarantees that DMA has landed: the epilogue stores of iteration q - 2
-        // (panel q - 2, or q - 3 when DEFERred), then iteration q - 1's [residual loads, not
-        // counted: waiting for them too is merely stricter], DMA of panel q + 1 if any, and its
-        // epilogue stores (panel q - 1, or q - 2 when DEFERred)
-        if (q == 0) {
-            wait_vm_lgkm0_dyn(np > 1 ? PW : 0);
-        } else if constexpr (!DEFER) {
-            wait_vm_lgkm0_dyn((q >= 2 ? nstore(q - 2) : 0) + nstore(q - 1) + (q + 1 < np ? PW : 0));
-        } else {
-            wait_vm_lgkm0_dyn((q >= 3 ? nstore(q - 3) : 0) + (q >= 2 ? nstore(q - 2) : 0) +
-                              (q + 1 < np ? PW : 0));
-        }
+        // (panel q - 3), then iteration q - 1's [residual loads, not counted: waiting for them
+        // too is merely stricter], DMA of panel q + 1 if any, and its epilogue stores (panel
+        // q - 2)
+        static_assert(LA == 2, "the wait counts below assume two panels in flight");
+        if (q == 0) wait_vm_lgkm0_dyn(np > 1 ? PW : 0);
+        else wait_vm_lgkm0_dyn((q >= 3 ? nstore(q - 3) : 0) + (q >= 2 ? nstore(q - 2) : 0) +
+                               (q + 1 < np ? PW : 0));
         __builtin_amdgcn_s_barrier();                    // every wave's pieces; buffer of q - 1 free
         if constexpr (KV)
             if (kv_pend) kv_finish();                    // block-uniform
-        if constexpr (RES) {
-            if constexpr (!DEFER) {
-                if (q + 1 < np) load_res(q + 1, rnext);
-            } else {
-                if (q >= 1) load_res(q - 1, rcur);
-            }
-        }
-        if (q + 2 < np) dma(q + 2);
+        if constexpr (RES)
+            if (q >= 1) load_res(q - 1, rcur);
+        if (q + LA < np) dma(q + LA);
         f32x4 acc[RT];
         panel_mfma(q, acc);
-        if constexpr (!DEFER) {
-            epilogue(q, acc, rcur);
-            if constexpr (RES)
+        // the previous panel's epilogue after this panel's MFMAs: its VALU and stores issue in
+        // the MFMA shadows instead of between two panels' matrix work (measured 1.09-1.17x on
+        // the LN-fused and 57264-row shapes, equal elsewhere: profiles/r04_rs_defer_ab.txt)
+        if (q >= 1) epilogue(q - 1, prev, rcur);
 #pragma unroll
-                for (int i = 0; i < RT; ++i) rcur[i] = rnext[i];
-        } else {
-            // the previous panel's epilogue after this panel's MFMAs: its VALU and stores can
-            // issue in the MFMA shadows instead of between two panels' matrix work
-            if (q >= 1) epilogue(q - 1, prev, rcur);
-#pragma unroll
-            for (int i = 0; i < RT; ++i) prev[i] = acc[i];
-        }
+        for (int i = 0; i < RT; ++i) prev[i] = acc[i];
     }
-    if constexpr (DEFER) {
-        if constexpr (RES) load_res(np - 1, rcur);
-        epilogue(np - 1, prev, rcur);
-    }
+    if constexpr (RES) load_res(np - 1, rcur);
+    epilogue(np - 1, prev, rcur);
     if constexpr (KV) {
         if (kv_pend) {                                   // the last head of the block
             __syncthreads();
@@ -577,61 +562,52 @@ __global__ void __launch_bounds__(256, KV ? 2 : 1) gemm_rs_kernel(RsArgs p) {
     }
 }
 
-template <int RT, int KS, int ACT, bool D>
+template <int RT, int KS, int ACT>
 void launch_rs_act(const RsArgs& a, unsigned blocks, hipStream_t st) {
-    // LN prologue: one row tile per wave (at two, the row + add registers of the prologue
-    // exceed the 256 VGPRs of two waves per SIMD and spill), no residual (checked by the caller)
     if constexpr (RT == 1 && ACT == FGR_ACT_NONE && KS == 8) {
         if (a.ln_g && a.ln_add && a.kv_img) {
             if (a.ln_out2)
-                hipLaunchKernelGGL((gemm_rs_kernel<RT, KS, false, ACT, 3, false, D, true>), dim3(blocks), dim3(256), 0, st, a);
+                hipLaunchKernelGGL((gemm_rs_kernel<RT, KS, false, ACT, 3, false, true>), dim3(blocks), dim3(256), 0, st, a);
             else
-                hipLaunchKernelGGL((gemm_rs_kernel<RT, KS, false, ACT, 2, false, D, true>), dim3(blocks), dim3(256), 0, st, a);
+                hipLaunchKernelGGL((gemm_rs_kernel<RT, KS, false, ACT, 2, false, true>), dim3(blocks), dim3(256), 0, st, a);
             return;
         }
     }
+    // LN prologue: one row tile per wave (at two, the row + add registers of the prologue
+    // exceed the 256 VGPRs of two waves per SIMD and spill), no residual (checked by the caller)
     if constexpr (RT == 1 && ACT != FGR_ACT_RELU_RES_LEAKY) {
         if (a.ln_g && a.ln_add && a.ln_out2) {
-            hipLaunchKernelGGL((gemm_rs_kernel<RT, KS, false, ACT, 3, false, D>), dim3(blocks), dim3(256), 0, st, a);
+            hipLaunchKernelGGL((gemm_rs_kernel<RT, KS, false, ACT, 3>), dim3(blocks), dim3(256), 0, st, a);
             return;
         }
         if (a.ln_g && a.ln_add) {
-            hipLaunchKernelGGL((gemm_rs_kernel<RT, KS, false, ACT, 2, false, D>), dim3(blocks), dim3(256), 0, st, a);
+            hipLaunchKernelGGL((gemm_rs_kernel<RT, KS, false, ACT, 2>), dim3(blocks), dim3(256), 0, st, a);
             return;
         }
         if (a.ln_g) {
-            hipLaunchKernelGGL((gemm_rs_kernel<RT, KS, false, ACT, 1, false, D>), dim3(blocks), dim3(256), 0, st, a);
+            hipLaunchKernelGGL((gemm_rs_kernel<RT, KS, false, ACT, 1>), dim3(blocks), dim3(256), 0, st, a);
             return;
         }
     }
     if constexpr (ACT == FGR_ACT_RELU) {
         if (a.out3) {
-            hipLaunchKernelGGL((gemm_rs_kernel<RT, KS, false, ACT, 0, true, D>), dim3(blocks), dim3(256), 0, st, a);
+            hipLaunchKernelGGL((gemm_rs_kernel<RT, KS, false, ACT, 0, true>), dim3(blocks), dim3(256), 0, st, a);
             return;
         }
     }
     if (a.R)
-        hipLaunchKernelGGL((gemm_rs_kernel<RT, KS, true, ACT, 0, false, D>), dim3(blocks), dim3(256), 0, st, a);
+        hipLaunchKernelGGL((gemm_rs_kernel<RT, KS, true, ACT, 0>), dim3(blocks), dim3(256), 0, st, a);
     else
-        hipLaunchKernelGGL((gemm_rs_kernel<RT, KS, false, ACT, 0, false, D>), dim3(blocks), dim3(256), 0, st, a);
-}
-
-// FGR_RS_DEFER=1: the deferred-epilogue panel loop (A/B tuning switch)
-inline bool rs_defer() {
-    const char* e = getenv("FGR_RS_DEFER");
-    return e && e[0] == '1';
+        hipLaunchKernelGGL((gemm_rs_kernel<RT, KS, false, ACT, 0>), dim3(blocks), dim3(256), 0, st, a);
 }
 
 template <int RT, int KS>
 bool launch_rs_k(const RsArgs& a, unsigned blocks, hipStream_t st) {
-    const bool d = rs_defer();
-#define RS_ACT(A) (d ? launch_rs_act<RT, KS, A, true>(a, blocks, st) : launch_rs_act<RT, KS, A, false>(a, blocks, st))
     switch (a.act) {
-        case FGR_ACT_RELU: RS_ACT(FGR_ACT_RELU); return true;
-        case FGR_ACT_RELU_RES_LEAKY: RS_ACT(FGR_ACT_RELU_RES_LEAKY); return true;
-        default: RS_ACT(FGR_ACT_NONE); return true;
+        case FGR_ACT_RELU: launch_rs_act<RT, KS, FGR_ACT_RELU>(a, blocks, st); return true;
+        case FGR_ACT_RELU_RES_LEAKY: launch_rs_act<RT, KS, FGR_ACT_RELU_RES_LEAKY>(a, blocks, st); return true;
+        default: launch_rs_act<RT, KS, FGR_ACT_NONE>(a, blocks, st); return true;
     }
-#undef RS_ACT
 }
 
 }  // namespace
