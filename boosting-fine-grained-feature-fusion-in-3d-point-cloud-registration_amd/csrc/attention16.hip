@@ -510,7 +510,7 @@ extern "C" int fgr_attention_f16x3(const float* q, int64_t ld_q, const float* k,
 }
 
 // The attention on K / V images of GLOBAL 64-row tiles written by fgr_gemm_f16x3_ln_qkv (head
-// dim 32): no image launch here.
+// dim 32) or fgr_gemm_f16x3_qkv (head dim 64): no image launch here.
 extern "C" int fgr_attention_f16x3_img(const float* q, int64_t ld_q, const void* kv_img,
                                        int64_t n_kv_rows, float* o, int64_t ld_o,
                                        const int64_t* q_off, const int64_t* kv_off,
@@ -519,8 +519,9 @@ extern "C" int fgr_attention_f16x3_img(const float* q, int64_t ld_q, const void*
     FGR_REQUIRE(q && kv_img && o && q_off && kv_off && kv_seg && n_seg > 0 && n_head > 0 &&
                     max_q_len >= 0 && n_kv_rows >= 0,
                 "fgr_attention_f16x3_img: bad arguments");
-    FGR_REQUIRE(head_dim == 32, "fgr_attention_f16x3_img: head_dim %d (32)", head_dim);
-    FGR_REQUIRE(ld_q >= n_head * 32 && ld_o >= n_head * 32 && ld_q % 4 == 0 && ld_o % 4 == 0 &&
+    FGR_REQUIRE(head_dim == 32 || head_dim == 64, "fgr_attention_f16x3_img: head_dim %d (32 or 64)",
+                head_dim);
+    FGR_REQUIRE(ld_q >= n_head * head_dim && ld_o >= n_head * head_dim && ld_q % 4 == 0 && ld_o % 4 == 0 &&
                     ((reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(o) |
                       reinterpret_cast<uintptr_t>(kv_img)) & 15) == 0,
                 "fgr_attention_f16x3_img: strides / alignment");
@@ -528,13 +529,18 @@ extern "C" int fgr_attention_f16x3_img(const float* q, int64_t ld_q, const void*
     hipStream_t st = as_stream(stream);
     TimedCall timed_(st);
     const int64_t nt = ceil_div(n_kv_rows, 64) * n_head;
+    const int un = head_dim == 32 ? units<32>() : units<64>();
     const uint4* img = static_cast<const uint4*>(kv_img);
-    const int2* sc = reinterpret_cast<const int2*>(static_cast<const char*>(kv_img) + nt * units<32>() * 16);
+    const int2* sc = reinterpret_cast<const int2*>(static_cast<const char*>(kv_img) + nt * un * 16);
     const int n_qblk = (int)ceil_div(max_q_len, 64);
     const int64_t n_blocks = ceil_div((int64_t)n_seg * n_head, 8) * 8 * n_qblk;
     const float sl2 = scale * 1.4426950408889634f;
-    hipLaunchKernelGGL((attn_f16x3_v2_kernel<32>), dim3((unsigned)n_blocks), dim3(256), 0, st, q, ld_q,
-                       img, sc, o, ld_o, q_off, kv_off, kv_seg, n_head, n_seg, n_qblk, sl2, 1);
+    if (head_dim == 32)
+        hipLaunchKernelGGL((attn_f16x3_v2_kernel<32>), dim3((unsigned)n_blocks), dim3(256), 0, st, q, ld_q,
+                           img, sc, o, ld_o, q_off, kv_off, kv_seg, n_head, n_seg, n_qblk, sl2, 1);
+    else
+        hipLaunchKernelGGL((attn_f16x3_v2_kernel<64>), dim3((unsigned)n_blocks), dim3(256), 0, st, q, ld_q,
+                           img, sc, o, ld_o, q_off, kv_off, kv_seg, n_head, n_seg, n_qblk, sl2, 1);
     FGR_CHECK_LAUNCH("attn_f16x3_v2_kernel (global tiles)");
     return FGR_OK;
 }

@@ -37,6 +37,9 @@ bool gemm_g5_f16x3(char cfg, const float* A, int64_t lda, const void* W, int kst
                    int64_t ldr, int M, int N, int K, int act, int vec_out, hipStream_t st,
                    int ksplit, float* part);
 bool g5_tile(char cfg, int* bm, int* bn);
+bool gemm_g5_f16x3_qkv(const float* A, int64_t lda, const void* W, int ksteps, const float* wsc,
+                       float* q, int64_t ld_q, const float* bias, int M, int d, int n_head,
+                       char* kv_img, int2* kv_sc, hipStream_t st);
 int g5_ksplit(int M, int N, int K, int BM, int BN);
 char bf16_tile(int m, int n, int k);
 int bf16_ksplit(char cfg, int m, int n, int k);
@@ -1326,10 +1329,43 @@ extern "C" int fgr_corr_head_f16x3(const float* f, int64_t ldf, int32_t m, int32
 // Image geometry (attention16.hip, head dim 32): one 16 KB image per (global 64-row tile,
 // head), then the int2 scale exponents of all of them.
 extern "C" int fgr_kv_image_bytes(int64_t n_rows, int32_t n_head, int32_t head_dim, size_t* bytes) {
-    FGR_REQUIRE(bytes && n_rows >= 0 && n_head > 0 && head_dim == 32,
-                "fgr_kv_image_bytes: bad arguments (head_dim 32)");
+    FGR_REQUIRE(bytes && n_rows >= 0 && n_head > 0 && (head_dim == 32 || head_dim == 64),
+                "fgr_kv_image_bytes: bad arguments (head_dim 32 or 64)");
     const int64_t nt = std::max<int64_t>(1, ceil_div(n_rows, 64)) * n_head;
-    *bytes = (size_t)(nt * 1024 * 16 + nt * 8);
+    *bytes = (size_t)(nt * (head_dim == 32 ? 1024 : 2048) * 16 + nt * 8);
+    return FGR_OK;
+}
+
+// the in_proj (no LayerNorm prologue) with the K / V images of head dim 64 in the staged g5
+// epilogue (gemm5.hip gemm_g5_f16x3_qkv)
+extern "C" int fgr_gemm_f16x3_qkv_supported(int32_t m, int32_t d, int32_t n_head) {
+    return (m > 0 && n_head > 0 && d == 64 * n_head && d % 128 == 0) ? 1 : 0;
+}
+
+extern "C" int fgr_gemm_f16x3_qkv(const float* a, int64_t lda, const void* w_img, float* q,
+                                  int64_t ld_q, const float* bias, int32_t m, int32_t d,
+                                  int32_t n_head, void* kv_img, void* stream) {
+    FGR_REQUIRE(a && w_img && q && bias && kv_img && m >= 0 && lda >= d && ld_q >= d,
+                "fgr_gemm_f16x3_qkv: bad arguments");
+    FGR_REQUIRE(m == 0 || fgr_gemm_f16x3_qkv_supported(m, d, n_head),
+                "fgr_gemm_f16x3_qkv: d %d heads %d not supported (head dim 64, d %% 128 == 0)", d, n_head);
+    const uintptr_t al = reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(w_img) |
+                         reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(bias) |
+                         reinterpret_cast<uintptr_t>(kv_img);
+    FGR_REQUIRE((al & 15) == 0 && lda % 4 == 0 && ld_q % 4 == 0,
+                "fgr_gemm_f16x3_qkv: operands must be 16-B aligned with row strides %% 4 == 0");
+    if (m == 0) return FGR_OK;
+    const int n = 3 * d;
+    const float* wsc = reinterpret_cast<const float*>(static_cast<const char*>(w_img) +
+                                                      image_bytes_h3(n, d));
+    const int64_t nt = ceil_div(m, 64) * n_head;
+    hipStream_t st = as_stream(stream);
+    TimedCall timed_(st);
+    FGR_REQUIRE(gemm_g5_f16x3_qkv(a, lda, w_img, ksteps_h3(d), wsc, q, ld_q, bias, m, d, n_head,
+                                  static_cast<char*>(kv_img),
+                                  reinterpret_cast<int2*>(static_cast<char*>(kv_img) + nt * 2048 * 16), st),
+                "fgr_gemm_f16x3_qkv: g5 variant unavailable");
+    FGR_CHECK_LAUNCH("gemm_g5_qkv");
     return FGR_OK;
 }
 

@@ -55,7 +55,16 @@ struct G5Args {
     const float* R; int64_t ldr;
     int M, N, K, act, vec_out;
     int ksplit; float* part;          // split-K: partials [ksplit][M][N] (scaled, no epilogue)
+    // K / V attention images (head dim 64, staged-epilogue 64 x 128 tiles only): columns >=
+    // kv_col0 go to the f16x3 images of their GLOBAL 64-row tile and head (attention16.hip
+    // layout) instead of C; the k | v columns are the last 128 n_head
+    char* kv_img; int2* kv_sc; int n_head; int kv_col0;
 };
+
+// f16x3 attention image geometry for head dim 64 (attention16.hip units<64>, unit_v<64>,
+// v_swz<64>): 2048 16-B units per (tile, head), V from unit 1024
+constexpr int kKv64Units = 2048;
+constexpr int kKv64UnitV = 1024;
 
 // chunk swizzle of A row r (16-B chunk q of a 128-B row line lands at q ^ swz(r)): rows
 // {0-3, 12-15} and {4-11} of one ds_read_b128 lane group hit 16 distinct 16-B bank slots
@@ -457,6 +466,82 @@ __global__ void __launch_bounds__(256 * KW) gemm_g5(G5Args p) {
                 }
             }
             __syncthreads();
+            if constexpr (BM == 64 && BN == 128 && TERMS == 2) {
+                if (p.kv_img && n0 >= p.kv_col0) {              // block-uniform: 2 K or V heads
+                    // the staged 64 x 128 tile (wave w's rows at buf_w = lds + w * WR * RS_) is
+                    // two heads of the global 64-row tile bm: bias added, rows past M zero, per
+                    // head max |.| -> power-of-two exponent (max in [2^14, 2^15), as
+                    // attn_kv_image16_kernel), split terms into the image units
+                    __shared__ float kvred[2][4];
+                    const float* tile = reinterpret_cast<const float*>(lds);
+                    float v[4][8];
+                    float hm[2] = {0.f, 0.f};
+#pragma unroll
+                    for (int it = 0; it < 4; ++it) {                // items: (key, 8-dim group)
+                        const int item = tid + 256 * it;            // 0 .. 1023
+                        const int hh = item >> 9, key = (item >> 3) & 63, gg = item & 7;
+                        const int col = 64 * hh + 8 * gg;
+                        const float* src = tile + (key / WR) * (WR * RS_) + (key % WR) * RS_ + col;
+                        const float4 b0 = *reinterpret_cast<const float4*>(p.bias + n0 + col);
+                        const float4 b1 = *reinterpret_cast<const float4*>(p.bias + n0 + col + 4);
+                        const float4 x0 = *reinterpret_cast<const float4*>(src);
+                        const float4 x1 = *reinterpret_cast<const float4*>(src + 4);
+                        const bool ok = m0 + key < p.M;
+                        v[it][0] = ok ? x0.x + b0.x : 0.f; v[it][1] = ok ? x0.y + b0.y : 0.f;
+                        v[it][2] = ok ? x0.z + b0.z : 0.f; v[it][3] = ok ? x0.w + b0.w : 0.f;
+                        v[it][4] = ok ? x1.x + b1.x : 0.f; v[it][5] = ok ? x1.y + b1.y : 0.f;
+                        v[it][6] = ok ? x1.z + b1.z : 0.f; v[it][7] = ok ? x1.w + b1.w : 0.f;
+                        float mx = 0.f;
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) mx = fmaxf(mx, fabsf(v[it][e]));
+                        hm[hh] = fmaxf(hm[hh], mx);             // it 0-1: head 0, 2-3: head 1
+                    }
+#pragma unroll
+                    for (int hh = 0; hh < 2; ++hh) {
+                        float m = hm[hh];
+#pragma unroll
+                        for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+                        if (lane == 0) kvred[hh][wv] = m;
+                    }
+                    __syncthreads();
+                    const int rel = n0 - p.kv_col0;
+                    const int isv = rel >= 64 * p.n_head ? 1 : 0;
+                    const int head0 = (rel - isv * 64 * p.n_head) / 64;
+#pragma unroll
+                    for (int it = 0; it < 4; ++it) {
+                        const int item = tid + 256 * it;
+                        const int hh = item >> 9, key = (item >> 3) & 63, gg = item & 7;
+                        const float tm = fmaxf(fmaxf(kvred[hh][0], kvred[hh][1]),
+                                               fmaxf(kvred[hh][2], kvred[hh][3]));
+                        const int e = tm > 0.f ? min(15 - __builtin_amdgcn_frexp_expf(tm), 127) : 0;
+                        const float sc = __builtin_ldexpf(1.f, e);
+                        const int64_t ti = (int64_t)bm * p.n_head + head0 + hh;
+                        if (tid == 0 && it == 0) reinterpret_cast<int*>(p.kv_sc + ti)[isv] = e;
+                        if (tid == 0 && it == 2) reinterpret_cast<int*>(p.kv_sc + ti)[isv] = e;
+                        _Float16 th[8], tl[8];
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) {
+                            const float x = v[it][j] * sc;
+                            th[j] = (_Float16)x;
+                            tl[j] = (_Float16)(x - (float)th[j]);
+                        }
+                        char* base = p.kv_img + ti * (int64_t)(kKv64Units * 16);
+                        char *d0, *d1;
+                        if (isv) {                          // [term][key][64] f16, chunk ^ v_swz<64>
+                            const int ch = gg ^ (((key >> 1) & 3) << 1);
+                            d0 = base + kKv64UnitV * 16 + key * 128 + ch * 16;
+                            d1 = d0 + 128 * 64;
+                        } else {                            // [ks][term][g'][key] x 8 dims
+                            const int ks = gg >> 2, gq = gg & 3;
+                            d0 = base + (((ks * 2 + 0) * 4 + gq) * 64 + key) * 16;
+                            d1 = base + (((ks * 2 + 1) * 4 + gq) * 64 + key) * 16;
+                        }
+                        *reinterpret_cast<uint4*>(d0) = *reinterpret_cast<const uint4*>(th);
+                        *reinterpret_cast<uint4*>(d1) = *reinterpret_cast<const uint4*>(tl);
+                    }
+                    return;
+                }
+            }
             constexpr int LPRW = BN / 4, RPI = 64 / LPRW;       // lanes per row, rows per pass
             const int col = 4 * (lane % LPRW);
             const int n = n0 + col;
@@ -644,15 +729,25 @@ bool gemm_g5_f16x3(char cfg, const float* A, int64_t lda, const void* W, int kst
                    int64_t ldr, int M, int N, int K, int act, int vec_out, hipStream_t st,
                    int ksplit, float* part) {
     G5Args a{A, lda, g5_zero_ptr(), (const u32x4*)W, ksteps, wsc, C, ldc, bias, R, ldr, M, N, K,
-             act, vec_out, ksplit > 1 && part ? ksplit : 1, part};
+             act, vec_out, ksplit > 1 && part ? ksplit : 1, part, nullptr, nullptr, 0, 0};
     return dispatch_g5<2>(cfg, a, st);
+}
+
+// the in_proj with the K / V images of every global 64-row tile (head dim 64) in the staged
+// epilogue: g5 'Y' (64 x 128 tiles, 3 stages, staged epilogue), q columns to C
+bool gemm_g5_f16x3_qkv(const float* A, int64_t lda, const void* W, int ksteps, const float* wsc,
+                       float* q, int64_t ld_q, const float* bias, int M, int d, int n_head,
+                       char* kv_img, int2* kv_sc, hipStream_t st) {
+    G5Args a{A, lda, g5_zero_ptr(), (const u32x4*)W, ksteps, wsc, q, ld_q, bias, nullptr, 0, M,
+             3 * d, d, FGR_ACT_NONE, 1, 1, nullptr, kv_img, kv_sc, n_head, d};
+    return dispatch_g5<2>('Y', a, st);
 }
 
 bool gemm_g5_bf16(char cfg, const float* A, int64_t lda, const void* W, int ksteps, float* C,
                   int64_t ldc, const float* bias, const float* R, int64_t ldr, int M, int N, int K,
                   int act, int vec_out, hipStream_t st, int ksplit, float* part) {
     G5Args a{A, lda, g5_zero_ptr(), (const u32x4*)W, ksteps, nullptr, C, ldc, bias, R, ldr, M, N,
-             K, act, vec_out, ksplit > 1 && part ? ksplit : 1, part};
+             K, act, vec_out, ksplit > 1 && part ? ksplit : 1, part, nullptr, nullptr, 0, 0};
     return dispatch_g5<1>(cfg, a, st);
 }
 

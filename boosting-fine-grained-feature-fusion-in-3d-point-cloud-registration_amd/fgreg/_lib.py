@@ -72,6 +72,8 @@ SIGNATURES = {
     'fgr_gemm_f16x3_ln_qkv_supported': [_i32, _i32, _i32],
     'fgr_gemm_f16x3_ln_qkv': [_vp, _i64, _vp, _vp, _f32, _vp, _i64, _vp, _vp, _i64, _vp, _i32, _i32,
                               _i32, _vp, _vp, _vp, _vp, _i64, _vp],
+    'fgr_gemm_f16x3_qkv_supported': [_i32, _i32, _i32],
+    'fgr_gemm_f16x3_qkv': [_vp, _i64, _vp, _vp, _i64, _vp, _i32, _i32, _i32, _vp, _vp],
     'fgr_attention_f16x3_img': [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i32, _i32, _i32,
                                 _i32, _f32, _vp],
     'fgr_corr_head_supported': [_i32, _i32],

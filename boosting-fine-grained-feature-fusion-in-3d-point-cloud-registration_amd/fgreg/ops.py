@@ -697,6 +697,37 @@ def ln_qkv_attention(x, norm, w_img, bias, pos, q_off, kv_seg, max_len, n_head, 
     return o
 
 
+def qkv_supported(m, d, n_head) -> bool:
+    return bool(_lib.load().fgr_gemm_f16x3_qkv_supported(int(m), int(d), int(n_head)))
+
+
+def qkv_attention(h, w_img, bias, q_off, kv_seg, max_len, n_head):
+    """The attention sub-layer's in_proj + attention core in two launches, head dim 64:
+    fgr_gemm_f16x3_qkv (h W^T + b -> q fp32 and the K / V images of every global 64-row tile)
+    then fgr_attention_f16x3_img. -> o (N, d)."""
+    _dev(h, bias, q_off, kv_seg)
+    n, d = h.shape
+    h = h.contiguous()
+    L = _lib.load()
+    nb = _lib._sz(0)
+    _lib.check(L.fgr_kv_image_bytes(n, n_head, d // n_head, nb), 'fgr_kv_image_bytes')
+    img = _workspace(h.device, nb.value)
+    q = torch.empty((n, d), dtype=torch.float32, device=h.device)
+    t0 = _begin('gemm', (n, 3 * d, d))
+    _lib.check(L.fgr_gemm_f16x3_qkv(_ptr(h), h.stride(0), _ptr(w_img.img), _ptr(q), q.stride(0),
+                                    _ptr(bias), n, d, n_head, _ptr(img), _stream()),
+               'fgr_gemm_f16x3_qkv')
+    _end('gemm', t0, 2 * n * 3 * d * d)
+    o = torch.empty((n, d), dtype=torch.float32, device=h.device)
+    t0 = _begin('attention')
+    _lib.check(L.fgr_attention_f16x3_img(
+        _ptr(q), q.stride(0), _ptr(img), n, _ptr(o), o.stride(0), _ptr(q_off), _ptr(q_off),
+        _ptr(kv_seg), q_off.numel() - 1, int(max_len), n_head, d // n_head,
+        float(math.sqrt(1.0 / float(d // n_head))), _stream()), 'fgr_attention_f16x3_img')
+    _end('attention', t0, lambda: attention_flops(q_off, q_off, kv_seg, d))
+    return o
+
+
 def corr_head_supported(m, d) -> bool:
     return bool(_lib.load().fgr_corr_head_supported(int(m), int(d)))
 

@@ -107,6 +107,11 @@ class TransformerCrossEncoderLayer(nn.Module):
             q, k, v = qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:]
             return ops.attention(q, k, v, seg.off, seg.off, kv_seg, seg.max_len, self.nhead)
         d = h_pos.shape[1]
+        if (val_has_pos and QKV_IMAGES and lin.MODE == 'f16x3' and ops.ATTN_MODE == 'f16x3'
+                and ops.qkv_supported(h_pos.shape[0], d, self.nhead)):
+            # head dim 64: the in_proj writes the attention's K / V images itself
+            return ops.qkv_attention(h_pos, lin.weight_image(W, mode='f16x3'), b, seg.off, kv_seg,
+                                     seg.max_len, self.nhead)
         if val_has_pos:
             qkv = linear(h_pos, W, b)                                 # (N, 3d): [q | k | v]
             q, k, v = qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:]

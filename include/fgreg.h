@@ -459,6 +459,14 @@ int fgr_gemm_f16x3_ln_qkv(const float* x, int64_t ldx, const float* gamma, const
                           int64_t ld_q, const float* bias, int32_t m, int32_t d, int32_t n_head,
                           void* kv_img, const float* gamma2, const float* beta2, float* out2,
                           int64_t ld_out2, void* stream);
+/* fgr_gemm_f16x3_qkv: the same for an in_proj without the LayerNorm prologue, head dim 64
+ * (qkv = a W^T + bias, a (m, d); the staged 64 x 128-tile g5 epilogue writes the images):
+ * fgr_gemm_f16x3_qkv_supported(m, d, n_head): d = 64 n_head, d % 128 == 0. fgr_kv_image_bytes
+ * takes head_dim 32 or 64, fgr_attention_f16x3_img reads either. */
+int fgr_gemm_f16x3_qkv_supported(int32_t m, int32_t d, int32_t n_head);
+int fgr_gemm_f16x3_qkv(const float* a, int64_t lda, const void* w_img, float* q, int64_t ld_q,
+                       const float* bias, int32_t m, int32_t d, int32_t n_head, void* kv_img,
+                       void* stream);
 int fgr_attention_f16x3_img(const float* q, int64_t ld_q, const void* kv_img, int64_t n_kv_rows,
                             float* o, int64_t ld_o, const int64_t* q_off, const int64_t* kv_off,
                             const int32_t* kv_seg, int32_t n_seg, int32_t max_q_len,

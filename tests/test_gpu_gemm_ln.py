@@ -270,3 +270,39 @@ def test_ln_qkv_images_vs_two_launch_path(gpu, lens, side):
             ref2 = torch.nn.functional.layer_norm(x.double(), (d,), norm2.weight.double(),
                                                   norm2.bias.double(), norm2.eps)
             assert rel_err(out2, ref2) < 1e-6
+
+
+@pytest.mark.parametrize('lens', [[1060, 1060], [1100, 977, 64, 1, 3000, 130]])
+def test_qkv_images_dh64_vs_two_launch_path(gpu, lens):
+    """fgr_gemm_f16x3_qkv (in_proj without the LayerNorm prologue writing q fp32 and the head
+    dim 64 K / V images of every global 64-row tile in the staged g5 epilogue: the 3DMatch
+    transformer, d 512 / 8 heads) + fgr_attention_f16x3_img vs linear -> fgr_attention_f16x3
+    (<= 2e-6 apart) and vs float64 (<= 1e-5), self- and cross-attention, segments starting
+    inside tiles."""
+    from fgreg import linear as lin
+    from fgreg import ops
+    n, d, nh = sum(lens), 512, 8
+    g = torch.Generator().manual_seed(n)
+    h = (torch.randn(n, d, generator=g) * 1.5).to(gpu)
+    w = (torch.randn(3 * d, d, generator=g) / math.sqrt(d)).to(gpu)
+    b = torch.randn(3 * d, generator=g).to(gpu)
+    assert ops.qkv_supported(n, d, nh)
+    off = ops.offsets(lens, gpu)
+    B = len(lens) // 2
+    for kv in (list(range(len(lens))), [(c + B) % len(lens) for c in range(len(lens))]):
+        kv_seg = torch.tensor(kv, dtype=torch.int32, device=gpu)
+        o = ops.qkv_attention(h, lin.weight_image(w, mode='f16x3'), b, off, kv_seg, max(lens), nh)
+        qkv = lin.linear(h, w, b)
+        o2 = ops.attention(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], off, off, kv_seg,
+                           max(lens), nh)
+        assert rel_err(o, o2) < 2e-6, rel_err(o, o2)
+        qkv64 = h.double() @ w.double().t() + b.double()
+        offs = np.cumsum([0] + lens)
+        outs = []
+        for i in range(len(lens)):
+            j = kv[i]
+            q = qkv64[offs[i]:offs[i + 1], :d].reshape(-1, nh, 64).transpose(0, 1) / 8.0
+            k = qkv64[offs[j]:offs[j + 1], d:2 * d].reshape(-1, nh, 64).transpose(0, 1)
+            v = qkv64[offs[j]:offs[j + 1], 2 * d:].reshape(-1, nh, 64).transpose(0, 1)
+            outs.append((torch.softmax(q @ k.transpose(1, 2), -1) @ v).transpose(0, 1).reshape(-1, d))
+        assert rel_err(o, torch.cat(outs, 0)) < 1e-5
