@@ -66,7 +66,14 @@ struct GemmBfArgs {
     const float* bias;
     const float* R; int64_t ldr;
     int M, N, K, act, vec_out;
+    // K / V attention images (bf16, head dim 64; BM = 64, BN = 128): columns >= kv_col0 go to
+    // the images of their GLOBAL 64-row tile and head (layout of attn_kv_image_bf16_kernel)
+    char* kv_img; int n_head; int kv_col0;
 };
+
+// bf16 attention image of head dim 64 (bf_units<64>() below): 1024 16-B units per (tile, head),
+// V from unit 512
+constexpr int bf_units_kv() { return 64 * 8 + 2 * 256; }
 
 template <int BM, int BN, bool KVEC>
 __global__ void __launch_bounds__(256) gemm_bf16_kernel(GemmBfArgs p) {
@@ -183,6 +190,41 @@ __global__ void __launch_bounds__(256) gemm_bf16_kernel(GemmBfArgs p) {
         }
         compute(1, w1);
     }
+    if constexpr (BM == 64 && BN == 128) {
+        if (p.kv_img && n0 >= p.kv_col0) {                 // block-uniform: K or V columns
+            // bf16 has fp32's range: no scale, every lane converts its own 4 outputs; rows
+            // past M are written as zeros (the attention's P is 0 there, V must be finite)
+            const int rel0 = n0 + wn - p.kv_col0;
+            const int isv = rel0 >= 64 * p.n_head ? 1 : 0;
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const int m = m0 + 16 * i + c;
+                const int key = 16 * i + c;
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    const int n = n0 + wn + 16 * j + 4 * g;
+                    const int rel = n - p.kv_col0 - isv * 64 * p.n_head;
+                    const int head = rel >> 6, d0 = rel & 63;
+                    const float4 bb = *reinterpret_cast<const float4*>(p.bias + n);
+                    const bool ok = m < p.M;
+                    const __bf16 t[4] = {(__bf16)(ok ? acc[j][i][0] + bb.x : 0.f),
+                                         (__bf16)(ok ? acc[j][i][1] + bb.y : 0.f),
+                                         (__bf16)(ok ? acc[j][i][2] + bb.z : 0.f),
+                                         (__bf16)(ok ? acc[j][i][3] + bb.w : 0.f)};
+                    char* base = p.kv_img + ((int64_t)bm * p.n_head + head) * (int64_t)(bf_units_kv() * 16);
+                    char* dst;
+                    if (isv) {
+                        const int vch = (d0 >> 3) ^ (((key >> 1) & 3) << 1);
+                        dst = base + 512 * 16 + key * 128 + vch * 16 + ((d0 >> 2) & 1) * 8;
+                    } else {
+                        dst = base + (((d0 >> 5) * 4 + ((d0 & 31) >> 3)) * 64 + key) * 16 + ((d0 >> 2) & 1) * 8;
+                    }
+                    *reinterpret_cast<uint2*>(dst) = *reinterpret_cast<const uint2*>(t);
+                }
+            }
+            return;
+        }
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
         const int m = m0 + 16 * i + c;
@@ -283,7 +325,7 @@ __global__ void __launch_bounds__(256, 4)
 attn_bf16_v2_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __restrict__ img,
                     float* __restrict__ o, int64_t ld_o, const int64_t* __restrict__ q_off,
                     const int64_t* __restrict__ kv_off, const int32_t* __restrict__ kv_seg,
-                    int n_head, int n_seg, int n_qblk, float scale_log2) {
+                    int n_head, int n_seg, int n_qblk, float scale_log2, int global_tiles) {
     constexpr int KD = DH / 32, TD = DH / 16;
     constexpr int UN = bf_units<DH>();
     constexpr int PW = UN / 64 / 4;
@@ -301,8 +343,11 @@ attn_bf16_v2_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __re
     const int ks = kv_seg[seg];
     const int64_t kb = kv_off[ks];
     const int nk = (int)(kv_off[ks + 1] - kb);
-    const int ntile = (nk + 63) / 64;
-    const int64_t tile0 = (kb / 64 + ks) * n_head + head;
+    // per-segment images or images of GLOBAL 64-row tiles (written by the in_proj GEMM,
+    // fgr_gemm_bf16_qkv): the segment's keys then start `lead` rows into its first tile
+    const int lead = global_tiles ? (int)(kb & 63) : 0;
+    const int ntile = (lead + nk + 63) / 64;
+    const int64_t tile0 = (global_tiles ? kb / 64 : kb / 64 + ks) * n_head + head;
     const int64_t tile_stride = (int64_t)n_head * UN;
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
     const int g = lane >> 4, c = lane & 15;
@@ -344,7 +389,12 @@ attn_bf16_v2_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __re
                                              (__attribute__((address_space(3))) void*)(dst + j * 1024),
                                              16, 0, 0);
     };
-    if (ntile > 0) dma(0, std::integral_constant<int, 0>{});
+    // tile tt lives in LDS buffer (tt + shift) & 1 (a masked first tile takes buffer 1)
+    const int shift = lead > 0 ? 1 : 0;
+    if (ntile > 0) {
+        if (shift) dma(0, std::integral_constant<int, 1>{});
+        else dma(0, std::integral_constant<int, 0>{});
+    }
     auto tile = [&](int tt, auto buf_tag, auto mask_tag) {
         constexpr int BUF = decltype(buf_tag)::value;
         constexpr bool MASK = decltype(mask_tag)::value;
@@ -366,12 +416,14 @@ attn_bf16_v2_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __re
             s[n] = a;
         }
         if constexpr (MASK) {
-            const int valid = nk - tt * 64;
+            const int lo = tt == 0 ? lead : 0, hi = lead + nk - tt * 64;   // valid keys [lo, hi)
 #pragma unroll
             for (int n = 0; n < 4; ++n)
 #pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    if (16 * n + 4 * g + r >= valid) s[n][r] = -INFINITY;
+                for (int r = 0; r < 4; ++r) {
+                    const int kl = 16 * n + 4 * g + r;
+                    if (kl < lo || kl >= hi) s[n][r] = -INFINITY;
+                }
         }
         float mx = vmax3b(s[0][0], s[0][1], s[0][2]);
         mx = vmax3b(mx, s[0][3], s[1][0]);
@@ -422,9 +474,13 @@ attn_bf16_v2_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __re
     };
     using B0 = std::integral_constant<int, 0>;
     using B1 = std::integral_constant<int, 1>;
-    const int nfull = nk / 64;
+    const int nfull = (lead + nk) / 64;              // tiles [shift, nfull) have 64 valid keys
     int tt = 0;
-    for (; tt + 2 <= nfull; tt += 2) {
+    if (shift) {                                     // the first tile, keys before the segment masked
+        tile(0, B1{}, std::true_type{});
+        tt = 1;
+    }
+    for (; tt + 2 <= nfull; tt += 2) {               // (tt + shift) even: buffer 0
         tile(tt, B0{}, std::false_type{});
         tile(tt + 1, B1{}, std::false_type{});
     }
@@ -433,7 +489,7 @@ attn_bf16_v2_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __re
         ++tt;
     }
     if (tt < ntile) {
-        if (tt & 1) tile(tt, B1{}, std::true_type{});
+        if ((tt + shift) & 1) tile(tt, B1{}, std::true_type{});
         else tile(tt, B0{}, std::true_type{});
     }
     const float inv = 1.0f / xg_sum16b(l_run);
@@ -522,7 +578,7 @@ static int gemm_bf16_impl(const float* a, int64_t lda, const void* w_img, float*
                     (!bias || (reinterpret_cast<uintptr_t>(bias) & 15) == 0) &&
                     (!r || ((ldr % 4 == 0) && (reinterpret_cast<uintptr_t>(r) & 15) == 0));
     GemmBfArgs g{a, lda, (const u32x4*)w_img, ksteps_bf(k), c, ldc, bias, r, ldr, m, n, k, act,
-                 vo ? 1 : 0};
+                 vo ? 1 : 0, nullptr, 0, 0};
     hipStream_t st = as_stream(stream);
     TimedCall timed_(st);
     const char cfg = bf16_tile(m, n, k);
@@ -609,14 +665,78 @@ extern "C" int fgr_attention_bf16(const float* q, int64_t ld_q, const float* k, 
                            kv_off, n_head, img);
         FGR_CHECK_LAUNCH("attn_kv_image_bf16_kernel");
         hipLaunchKernelGGL(attn_bf16_v2_kernel<32>, dim3(nb), dim3(256), 0, st, q, ld_q,
-                               (const uint4*)img, o, ld_o, q_off, kv_off, kv_seg, n_head, n_seg, n_qblk, sl2);
+                               (const uint4*)img, o, ld_o, q_off, kv_off, kv_seg, n_head, n_seg, n_qblk, sl2, 0);
     } else {
         hipLaunchKernelGGL(attn_kv_image_bf16_kernel<64>, kgrid, dim3(256), 0, st, k, ld_k, v, ld_v,
                            kv_off, n_head, img);
         FGR_CHECK_LAUNCH("attn_kv_image_bf16_kernel");
         hipLaunchKernelGGL(attn_bf16_v2_kernel<64>, dim3(nb), dim3(256), 0, st, q, ld_q,
-                               (const uint4*)img, o, ld_o, q_off, kv_off, kv_seg, n_head, n_seg, n_qblk, sl2);
+                               (const uint4*)img, o, ld_o, q_off, kv_off, kv_seg, n_head, n_seg, n_qblk, sl2, 0);
     }
     FGR_CHECK_LAUNCH("attn_bf16_v2_kernel");
+    return FGR_OK;
+}
+
+// ---- the in_proj with the bf16 K / V attention images in its epilogue (head dim 64) ---------
+extern "C" int fgr_kv_image_bf16_bytes(int64_t n_rows, int32_t n_head, int32_t head_dim, size_t* bytes) {
+    FGR_REQUIRE(bytes && n_rows >= 0 && n_head > 0 && head_dim == 64,
+                "fgr_kv_image_bf16_bytes: bad arguments (head_dim 64)");
+    *bytes = (size_t)std::max<int64_t>(1, ceil_div(n_rows, 64)) * n_head * bf_units<64>() * 16;
+    return FGR_OK;
+}
+
+extern "C" int fgr_gemm_bf16_qkv_supported(int32_t m, int32_t d, int32_t n_head) {
+    return (m > 0 && n_head > 0 && d == 64 * n_head && d % 128 == 0) ? 1 : 0;
+}
+
+// q = (a W^T + bias)[:, :d] fp32; k / v columns as bf16 images of every GLOBAL 64-row tile and
+// head (the register-staged 64 x 128 bf16 kernel's epilogue)
+extern "C" int fgr_gemm_bf16_qkv(const float* a, int64_t lda, const void* w_img, float* q,
+                                 int64_t ld_q, const float* bias, int32_t m, int32_t d,
+                                 int32_t n_head, void* kv_img, void* stream) {
+    FGR_REQUIRE(a && w_img && q && bias && kv_img && m >= 0 && lda >= d && ld_q >= d,
+                "fgr_gemm_bf16_qkv: bad arguments");
+    FGR_REQUIRE(m == 0 || fgr_gemm_bf16_qkv_supported(m, d, n_head),
+                "fgr_gemm_bf16_qkv: d %d heads %d not supported (head dim 64, d %% 128 == 0)", d, n_head);
+    const uintptr_t al = reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(w_img) |
+                         reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(bias) |
+                         reinterpret_cast<uintptr_t>(kv_img);
+    FGR_REQUIRE((al & 15) == 0 && lda % 4 == 0 && ld_q % 4 == 0 && d % 8 == 0,
+                "fgr_gemm_bf16_qkv: operands must be 16-B aligned with row strides %% 4 == 0");
+    if (m == 0) return FGR_OK;
+    const int n = 3 * d;
+    GemmBfArgs g{a, lda, (const u32x4*)w_img, ksteps_bf(d), q, ld_q, bias, nullptr, 0, m, n, d,
+                 FGR_ACT_NONE, 1, static_cast<char*>(kv_img), n_head, d};
+    hipStream_t st = as_stream(stream);
+    TimedCall timed_(st);
+    const unsigned nblk = (unsigned)(ceil_div(m, 64) * ceil_div(n, 128));
+    hipLaunchKernelGGL((gemm_bf16_kernel<64, 128, true>), dim3(nblk), dim3(256), 0, st, g);
+    FGR_CHECK_LAUNCH("gemm_bf16_kernel (qkv images)");
+    return FGR_OK;
+}
+
+// the bf16 attention on those images (no image launch)
+extern "C" int fgr_attention_bf16_img(const float* q, int64_t ld_q, const void* kv_img,
+                                      int64_t n_kv_rows, float* o, int64_t ld_o,
+                                      const int64_t* q_off, const int64_t* kv_off,
+                                      const int32_t* kv_seg, int32_t n_seg, int32_t max_q_len,
+                                      int32_t n_head, int32_t head_dim, float scale, void* stream) {
+    FGR_REQUIRE(q && kv_img && o && q_off && kv_off && kv_seg && n_seg > 0 && n_head > 0 &&
+                    max_q_len >= 0 && n_kv_rows >= 0 && head_dim == 64,
+                "fgr_attention_bf16_img: bad arguments (head_dim 64)");
+    FGR_REQUIRE(ld_q >= n_head * 64 && ld_o >= n_head * 64 && ld_q % 4 == 0 && ld_o % 4 == 0 &&
+                    ((reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(o) |
+                      reinterpret_cast<uintptr_t>(kv_img)) & 15) == 0,
+                "fgr_attention_bf16_img: strides / alignment");
+    if (max_q_len == 0 || n_kv_rows == 0) return FGR_OK;
+    hipStream_t st = as_stream(stream);
+    TimedCall timed_(st);
+    const int n_qblk = (int)ceil_div(max_q_len, 64);
+    const unsigned nb = (unsigned)(ceil_div((int64_t)n_seg * n_head, 8) * 8 * n_qblk);
+    const float sl2 = scale * 1.4426950408889634f;
+    hipLaunchKernelGGL(attn_bf16_v2_kernel<64>, dim3(nb), dim3(256), 0, st, q, ld_q,
+                       static_cast<const uint4*>(kv_img), o, ld_o, q_off, kv_off, kv_seg, n_head,
+                       n_seg, n_qblk, sl2, 1);
+    FGR_CHECK_LAUNCH("attn_bf16_v2_kernel (global tiles)");
     return FGR_OK;
 }

@@ -74,6 +74,11 @@ SIGNATURES = {
                               _i32, _vp, _vp, _vp, _vp, _i64, _vp],
     'fgr_gemm_f16x3_qkv_supported': [_i32, _i32, _i32],
     'fgr_gemm_f16x3_qkv': [_vp, _i64, _vp, _vp, _i64, _vp, _i32, _i32, _i32, _vp, _vp],
+    'fgr_kv_image_bf16_bytes': [_i64, _i32, _i32, ctypes.POINTER(_sz)],
+    'fgr_gemm_bf16_qkv_supported': [_i32, _i32, _i32],
+    'fgr_gemm_bf16_qkv': [_vp, _i64, _vp, _vp, _i64, _vp, _i32, _i32, _i32, _vp, _vp],
+    'fgr_attention_bf16_img': [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i32, _i32, _i32,
+                               _i32, _f32, _vp],
     'fgr_attention_f16x3_img': [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i32, _i32, _i32,
                                 _i32, _f32, _vp],
     'fgr_corr_head_supported': [_i32, _i32],

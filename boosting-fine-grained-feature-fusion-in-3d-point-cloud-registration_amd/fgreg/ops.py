@@ -701,29 +701,36 @@ def qkv_supported(m, d, n_head) -> bool:
     return bool(_lib.load().fgr_gemm_f16x3_qkv_supported(int(m), int(d), int(n_head)))
 
 
-def qkv_attention(h, w_img, bias, q_off, kv_seg, max_len, n_head):
+def qkv_bf16_supported(m, d, n_head) -> bool:
+    return bool(_lib.load().fgr_gemm_bf16_qkv_supported(int(m), int(d), int(n_head)))
+
+
+def qkv_attention(h, w_img, bias, q_off, kv_seg, max_len, n_head, mode='f16x3'):
     """The attention sub-layer's in_proj + attention core in two launches, head dim 64:
     fgr_gemm_f16x3_qkv (h W^T + b -> q fp32 and the K / V images of every global 64-row tile)
-    then fgr_attention_f16x3_img. -> o (N, d)."""
+    then fgr_attention_f16x3_img; mode 'bf16': fgr_gemm_bf16_qkv (bf16 images) then
+    fgr_attention_bf16_img. -> o (N, d)."""
     _dev(h, bias, q_off, kv_seg)
     n, d = h.shape
     h = h.contiguous()
     L = _lib.load()
     nb = _lib._sz(0)
-    _lib.check(L.fgr_kv_image_bytes(n, n_head, d // n_head, nb), 'fgr_kv_image_bytes')
+    bytes_fn = 'fgr_kv_image_bytes' if mode == 'f16x3' else 'fgr_kv_image_bf16_bytes'
+    _lib.check(getattr(L, bytes_fn)(n, n_head, d // n_head, nb), bytes_fn)
     img = _workspace(h.device, nb.value)
     q = torch.empty((n, d), dtype=torch.float32, device=h.device)
     t0 = _begin('gemm', (n, 3 * d, d))
-    _lib.check(L.fgr_gemm_f16x3_qkv(_ptr(h), h.stride(0), _ptr(w_img.img), _ptr(q), q.stride(0),
-                                    _ptr(bias), n, d, n_head, _ptr(img), _stream()),
-               'fgr_gemm_f16x3_qkv')
+    gemm_fn = 'fgr_gemm_f16x3_qkv' if mode == 'f16x3' else 'fgr_gemm_bf16_qkv'
+    _lib.check(getattr(L, gemm_fn)(_ptr(h), h.stride(0), _ptr(w_img.img), _ptr(q), q.stride(0),
+                                   _ptr(bias), n, d, n_head, _ptr(img), _stream()), gemm_fn)
     _end('gemm', t0, 2 * n * 3 * d * d)
     o = torch.empty((n, d), dtype=torch.float32, device=h.device)
     t0 = _begin('attention')
-    _lib.check(L.fgr_attention_f16x3_img(
+    attn_fn = 'fgr_attention_f16x3_img' if mode == 'f16x3' else 'fgr_attention_bf16_img'
+    _lib.check(getattr(L, attn_fn)(
         _ptr(q), q.stride(0), _ptr(img), n, _ptr(o), o.stride(0), _ptr(q_off), _ptr(q_off),
         _ptr(kv_seg), q_off.numel() - 1, int(max_len), n_head, d // n_head,
-        float(math.sqrt(1.0 / float(d // n_head))), _stream()), 'fgr_attention_f16x3_img')
+        float(math.sqrt(1.0 / float(d // n_head))), _stream()), attn_fn)
     _end('attention', t0, lambda: attention_flops(q_off, q_off, kv_seg, d))
     return o
 

@@ -112,6 +112,10 @@ class TransformerCrossEncoderLayer(nn.Module):
             # head dim 64: the in_proj writes the attention's K / V images itself
             return ops.qkv_attention(h_pos, lin.weight_image(W, mode='f16x3'), b, seg.off, kv_seg,
                                      seg.max_len, self.nhead)
+        if (val_has_pos and QKV_IMAGES and lin.MODE == 'bf16' and ops.ATTN_MODE == 'bf16'
+                and ops.qkv_bf16_supported(h_pos.shape[0], d, self.nhead)):
+            return ops.qkv_attention(h_pos, lin.weight_image(W, mode='bf16'), b, seg.off, kv_seg,
+                                     seg.max_len, self.nhead, mode='bf16')
         if val_has_pos:
             qkv = linear(h_pos, W, b)                                 # (N, 3d): [q | k | v]
             q, k, v = qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:]

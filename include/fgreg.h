@@ -467,6 +467,18 @@ int fgr_gemm_f16x3_qkv_supported(int32_t m, int32_t d, int32_t n_head);
 int fgr_gemm_f16x3_qkv(const float* a, int64_t lda, const void* w_img, float* q, int64_t ld_q,
                        const float* bias, int32_t m, int32_t d, int32_t n_head, void* kv_img,
                        void* stream);
+/* bf16 mode: fgr_gemm_bf16_qkv writes q (fp32) and the bf16 K / V images (head dim 64, no
+ * scales; fgr_kv_image_bf16_bytes) of every global 64-row tile from the register-staged 64 x
+ * 128 bf16 kernel's epilogue, fgr_attention_bf16_img reads them. */
+int fgr_kv_image_bf16_bytes(int64_t n_rows, int32_t n_head, int32_t head_dim, size_t* bytes);
+int fgr_gemm_bf16_qkv_supported(int32_t m, int32_t d, int32_t n_head);
+int fgr_gemm_bf16_qkv(const float* a, int64_t lda, const void* w_img, float* q, int64_t ld_q,
+                      const float* bias, int32_t m, int32_t d, int32_t n_head, void* kv_img,
+                      void* stream);
+int fgr_attention_bf16_img(const float* q, int64_t ld_q, const void* kv_img, int64_t n_kv_rows,
+                           float* o, int64_t ld_o, const int64_t* q_off, const int64_t* kv_off,
+                           const int32_t* kv_seg, int32_t n_seg, int32_t max_q_len,
+                           int32_t n_head, int32_t head_dim, float scale, void* stream);
 int fgr_attention_f16x3_img(const float* q, int64_t ld_q, const void* kv_img, int64_t n_kv_rows,
                             float* o, int64_t ld_o, const int64_t* q_off, const int64_t* kv_off,
                             const int32_t* kv_seg, int32_t n_seg, int32_t max_q_len,

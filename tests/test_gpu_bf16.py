@@ -188,3 +188,29 @@ def test_bf16_forward_3dlomatch_vs_oracle(gpu, bf16_mode, seed, n_points):
         assert v < BF16_FEAT_TOL, (k, v)
     assert rot < BF16_ROT_DEG and trans < BF16_TRANS, (rot, trans)
     assert max(errs.values()) > 1e-4            # really the bf16 mode, not the fp32-accurate path
+
+
+@pytest.mark.parametrize('lens', [[935, 936], [1100, 977, 64, 1, 3000, 130]])
+def test_bf16_qkv_images_vs_two_launch_path(gpu, bf16_mode, lens):
+    """fgr_gemm_bf16_qkv (the bf16 in_proj writing q fp32 and the bf16 K / V images of every
+    global 64-row tile, head dim 64) + fgr_attention_bf16_img vs fgr_gemm_bf16 ->
+    fgr_attention_bf16 (per-segment images): the images hold the same bf16 values, only the key
+    tiling differs (<= 1e-5 apart); self- and cross-attention, segments starting inside tiles."""
+    from fgreg import linear as lin
+    from fgreg import ops
+    n, d, nh = sum(lens), 512, 8
+    g = torch.Generator().manual_seed(n + 1)
+    h = (torch.randn(n, d, generator=g) * 1.5).to(gpu)
+    w = (torch.randn(3 * d, d, generator=g) / math.sqrt(d)).to(gpu)
+    b = torch.randn(3 * d, generator=g).to(gpu)
+    assert ops.qkv_bf16_supported(n, d, nh)
+    off = ops.offsets(lens, gpu)
+    B = len(lens) // 2
+    for kv in (list(range(len(lens))), [(c + B) % len(lens) for c in range(len(lens))]):
+        kv_seg = torch.tensor(kv, dtype=torch.int32, device=gpu)
+        o = ops.qkv_attention(h, lin.weight_image(w, mode='bf16'), b, off, kv_seg, max(lens), nh,
+                              mode='bf16')
+        qkv = lin.linear(h, w, b)
+        o2 = ops.attention(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], off, off, kv_seg,
+                           max(lens), nh)
+        assert rel_err(o, o2) < 1e-5, rel_err(o, o2)
