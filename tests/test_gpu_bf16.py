@@ -194,8 +194,11 @@ def test_bf16_forward_3dlomatch_vs_oracle(gpu, bf16_mode, seed, n_points):
 def test_bf16_qkv_images_vs_two_launch_path(gpu, bf16_mode, lens):
     """fgr_gemm_bf16_qkv (the bf16 in_proj writing q fp32 and the bf16 K / V images of every
     global 64-row tile, head dim 64) + fgr_attention_bf16_img vs fgr_gemm_bf16 ->
-    fgr_attention_bf16 (per-segment images): the images hold the same bf16 values, only the key
-    tiling differs (<= 1e-5 apart); self- and cross-attention, segments starting inside tiles."""
+    fgr_attention_bf16 (per-segment images): the images hold the same bf16 values and only the
+    key tiling differs, which moves where the online softmax rounds P to bf16 -- so both are
+    compared with the fp64 attention of the same q / k / v: the new path's error within 1.25x
+    of the old one's (+ 1e-4) and below 1e-2; self- and cross-attention, segments starting
+    inside tiles."""
     from fgreg import linear as lin
     from fgreg import ops
     n, d, nh = sum(lens), 512, 8
@@ -213,4 +216,8 @@ def test_bf16_qkv_images_vs_two_launch_path(gpu, bf16_mode, lens):
         qkv = lin.linear(h, w, b)
         o2 = ops.attention(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], off, off, kv_seg,
                            max(lens), nh)
-        assert rel_err(o, o2) < 1e-5, rel_err(o, o2)
+        q64 = qkv.double().cpu()
+        ref = _attn_ref(q64[:, :d], q64[:, d:2 * d], q64[:, 2 * d:], lens, lens, kv, nh)
+        e_new, e_old = rel_err(o, ref), rel_err(o2, ref)
+        print(f'\nlens {lens} kv {kv}: new {e_new:.2e} old {e_old:.2e} apart {rel_err(o, o2):.2e}')
+        assert e_new < 1.25 * e_old + 1e-4 and e_new < 1e-2, (e_new, e_old)
