@@ -121,6 +121,9 @@ def parse():
     p.add_argument('--cpu-seconds', type=float, default=10.0,
                    help='budget of the CPU baseline B=1 sample (0 disables it)')
     p.add_argument('--no-cpu-baseline', action='store_true')
+    p.add_argument('--lead-cycles', type=int, default=250000,
+                   help='spin kernel ahead of every per-launch timed call of the rooflines\' '
+                        'eager replay (ops.KernelTimer.lead_cycles; 0 = off)')
     p.add_argument('--no-pipeline', action='store_true',
                    help='time back-to-back model(batch) calls instead of fgreg.pipeline (which '
                         'preprocesses step i + 1 on a side stream while step i\'s core runs)')
@@ -374,6 +377,7 @@ def main():
             # rocprofv3 trace of the timed region (profiles/) cross-checks the durations
             rtimer = ops.KernelTimer(fams)
             rtimer.prealloc(args.steps * sum(len(work[n]) + 2 for n in rtimer.names))
+            rtimer.lead_cycles = args.lead_cycles
             ops.TIMER = rtimer
             for _ in range(args.steps):
                 step()
@@ -439,7 +443,8 @@ def main():
             'launches_per_step': len(work[name]),
             'share_of_step': ms / args.steps / step_ms,
             'timing': 'HIP events recorded by libfgreg around each launch (fgr_time_next_call), '
-                      'eager replay of the timed steps'}
+                      'eager replay of the timed steps, a spin kernel queued ahead of each timed '
+                      f'call (--lead-cycles {args.lead_cycles})'}
 
     # the KPConv stage's gather-weight kernel (the dominant HBM-bound kernel)
     line['roofline'] = kpconv_roofline('kpconv_gather', 'fgr_kpconv_gather')

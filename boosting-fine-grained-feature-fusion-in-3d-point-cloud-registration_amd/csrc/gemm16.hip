@@ -940,6 +940,44 @@ __global__ void weight_scale_kernel(const float* __restrict__ w, int n, int k, i
     }
 }
 
+// The same row maxima for a W stored column-major (sn == 1: the transposed operand of the
+// backward's dW = dY^T X, W = X^T): a block takes 64 consecutive rows (one 256-B load per
+// wave and k index) over a chunk of k and folds its maxima into wsc with an unsigned-integer
+// atomic max on the bit patterns (order-preserving for non-negative floats; max is exact, so
+// the result is independent of the order). wsc must be zeroed first; weight_scale_finish
+// turns the maxima into the scales.
+__global__ void weight_scale_cols_kernel(const float* __restrict__ w, int n, int k, int64_t sk,
+                                         int kchunk, unsigned* __restrict__ wmax) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int row = blockIdx.x * 64 + lane;
+    const int j0 = blockIdx.y * kchunk, j1 = min(k, j0 + kchunk);
+    float mx = 0.f;
+    if (row < n) {
+        int j = j0 + wv;
+        for (; j + 12 < j1; j += 16) {
+            const float a = w[(int64_t)j * sk + row], b = w[(int64_t)(j + 4) * sk + row];
+            const float c = w[(int64_t)(j + 8) * sk + row], d = w[(int64_t)(j + 12) * sk + row];
+            mx = fmaxf(mx, fmaxf(fmaxf(fabsf(a), fabsf(b)), fmaxf(fabsf(c), fabsf(d))));
+        }
+        for (; j < j1; j += 4) mx = fmaxf(mx, fabsf(w[(int64_t)j * sk + row]));
+    }
+    __shared__ float red[4][64];
+    red[wv][lane] = mx;
+    __syncthreads();
+    if (wv == 0 && row < n) {
+        mx = fmaxf(fmaxf(red[0][lane], red[1][lane]), fmaxf(red[2][lane], red[3][lane]));
+        if (mx > 0.f) atomicMax(wmax + row, __float_as_uint(mx));
+    }
+}
+
+__global__ void weight_scale_finish(int n, int npad, float* __restrict__ wsc) {
+    const int row = blockIdx.x * 256 + threadIdx.x;
+    if (row >= npad) return;
+    const float mx = __uint_as_float(reinterpret_cast<const unsigned*>(wsc)[row]);
+    const int e = mx > 0.f ? min(15 - __builtin_amdgcn_frexp_expf(mx), 127) : 0;
+    wsc[row] = row < n ? __builtin_ldexpf(1.f, -e) : 0.f;
+}
+
 // W -> f16x3 image [panel][kstep][term 2][g 4][16 rows] x 16 B (8 k each), rows scaled by
 // 1 / wsc[row] (exact powers of two), zero-padded past n and k.
 __global__ void split_weights_h3_kernel(const float* __restrict__ w, int n, int k, int64_t sn,
@@ -1038,9 +1076,25 @@ extern "C" int fgr_split_weights_h3(const float* w, int32_t n, int32_t k, int64_
     const int npad = (n + 15) / 16 * 16;
     float* wsc = reinterpret_cast<float*>(static_cast<char*>(img) + image_bytes_h3(n, k));
     hipStream_t st = as_stream(stream);
-    hipLaunchKernelGGL(weight_scale_kernel, dim3((unsigned)ceil_div(npad, 4)), dim3(256), 0, st, w,
-                       n, k, stride_n, stride_k, npad, wsc);
-    FGR_CHECK_LAUNCH("weight_scale_kernel");
+    if (stride_n == 1 && k >= 1024) {
+        // column-major W (the backward's transposed activations): coalesced chunked maxima;
+        // >= 512 blocks of 64 rows x kchunk (a multiple of 64)
+        const int nrb = ceil_div(n, 64);
+        int nkc = ceil_div(512, nrb);
+        if (nkc > ceil_div(k, 256)) nkc = ceil_div(k, 256);
+        const int kchunk = ceil_div(ceil_div(k, nkc), 64) * 64;
+        FGR_CHECK_HIP(hipMemsetAsync(wsc, 0, (size_t)npad * sizeof(float), st));
+        hipLaunchKernelGGL(weight_scale_cols_kernel, dim3((unsigned)nrb, (unsigned)ceil_div(k, kchunk)),
+                           dim3(256), 0, st, w, n, k, stride_k, kchunk, (unsigned*)wsc);
+        FGR_CHECK_LAUNCH("weight_scale_cols_kernel");
+        hipLaunchKernelGGL(weight_scale_finish, dim3((unsigned)ceil_div(npad, 256)), dim3(256), 0,
+                           st, n, npad, wsc);
+        FGR_CHECK_LAUNCH("weight_scale_finish");
+    } else {
+        hipLaunchKernelGGL(weight_scale_kernel, dim3((unsigned)ceil_div(npad, 4)), dim3(256), 0, st,
+                           w, n, k, stride_n, stride_k, npad, wsc);
+        FGR_CHECK_LAUNCH("weight_scale_kernel");
+    }
     const int64_t total = (int64_t)(npad / 16) * ksteps * 128;
     hipLaunchKernelGGL(split_weights_h3_kernel, dim3((unsigned)ceil_div(total, 256)), dim3(256), 0,
                        st, w, n, k, stride_n, stride_k, ksteps, wsc, (u32x4*)img);

@@ -158,7 +158,8 @@ __global__ void __launch_bounds__(256, KV ? 2 : 1) gemm_rs_kernel(RsArgs p) {
     __shared__ float4 lng2[LNM == 3 ? KS * 8 : 1], lnb2[LNM == 3 ? KS * 8 : 1];
     __shared__ float4 colh[HEAD ? 3 * kRsMaxNc * 4 : 1];            // HEAD: w4 by (j, panel, g)
     __shared__ float kvred[KV ? 2 : 1][4];                          // KV: per-wave head maxima
-    __shared__ float kvbuf[KV ? 4 : 1][KV ? 8 : 1][64];             // KV: the head's 8 values per lane
+    // KV: the head's 16 x 32 outputs of each wave as float4 dim quads [key][quad 8]
+    __shared__ float4 kvbuf[KV ? 4 : 1][KV ? 16 : 1][8];
     static_assert(!KV || RT == 1, "KV images: one 64-row tile per block");
 
     const int nbm = (p.M + 64 * RT - 1) / (64 * RT);
@@ -357,28 +358,26 @@ __global__ void __launch_bounds__(256, KV ? 2 : 1) gemm_rs_kernel(RsArgs p) {
         const int64_t tile = (int64_t)bm * p.n_head + head;
         if (tid == 0) reinterpret_cast<int*>(p.kv_sc + tile)[isv] = e;
         char* base = p.kv_img + tile * (kKvUnits * 16);
-        const int key = wv * 16 + c;
+        // lane -> (key kl of the wave's 16, 8-dim group gq): one whole 16-B unit per term
+        const int kl = lane >> 2, gq = lane & 3;
+        const int key = wv * 16 + kl;
+        const float4 a0 = kvbuf[wv][kl][2 * gq], a1 = kvbuf[wv][kl][2 * gq + 1];
+        const float xv[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+        _Float16 tv[2][8];
 #pragma unroll
-        for (int half = 0; half < 2; ++half) {
-            _Float16 tv[2][4];
+        for (int j = 0; j < 8; ++j) {
+            const float x = xv[j] * sc;
+            tv[0][j] = (_Float16)x;
+            tv[1][j] = (_Float16)(x - (float)tv[0][j]);
+        }
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const float x = kvbuf[wv][4 * half + j][lane] * sc;
-                tv[0][j] = (_Float16)x;
-                tv[1][j] = (_Float16)(x - (float)tv[0][j]);
-            }
-            const int d0 = 16 * half + 4 * g;               // first of the lane's 4 dims
-#pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                char* dst;
-                if (isv) {                                  // [term][key][32] f16, chunks ^ v_swz
-                    const int ch = (d0 >> 3) ^ (((key >> 2) & 1) << 1);
-                    dst = base + kKvUnitV * 16 + t * (128 * 32) + key * 64 + ch * 16 + (d0 & 4) * 2;
-                } else {                                    // [term][g'][key] x 8 dims
-                    dst = base + ((t * 4 + (d0 >> 3)) * 64 + key) * 16 + (d0 & 4) * 2;
-                }
-                *reinterpret_cast<uint2*>(dst) = *reinterpret_cast<const uint2*>(tv[t]);
-            }
+        for (int t = 0; t < 2; ++t) {
+            char* dst;
+            if (isv)                                        // [term][key][32] f16, chunks ^ v_swz
+                dst = base + kKvUnitV * 16 + t * (128 * 32) + key * 64 + (gq ^ (((key >> 2) & 1) << 1)) * 16;
+            else                                            // [term][g'][key] x 8 dims
+                dst = base + ((t * 4 + gq) * 64 + key) * 16;
+            *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(tv[t]);
         }
     };
     float h3[RT][3];
@@ -444,15 +443,13 @@ __global__ void __launch_bounds__(256, KV ? 2 : 1) gemm_rs_kernel(RsArgs p) {
                 const float y0 = ok ? acc[0][0] * s0 + bv.x : 0.f, y1 = ok ? acc[0][1] * s1 + bv.y : 0.f;
                 const float y2 = ok ? acc[0][2] * s2 + bv.z : 0.f, y3 = ok ? acc[0][3] * s3 + bv.w : 0.f;
                 const float mx = max3_abs(y0, y1, fmaxf(fabsf(y2), fabsf(y3)));
-                // parked in LDS (registers are at their limit in the LN prologue's kernel)
-                kvbuf[wv][4 * half + 0][lane] = y0;
-                kvbuf[wv][4 * half + 1][lane] = y1;
-                kvbuf[wv][4 * half + 2][lane] = y2;
-                kvbuf[wv][4 * half + 3][lane] = y3;
+                // parked in LDS (registers are at their limit in the LN prologue's kernel): dims
+                // 16 half + 4g .. + 3 of key c are quad 4 half + g
+                kvbuf[wv][c][4 * half + g] = make_float4(y0, y1, y2, y3);
                 if (half == 0) {
                     kvm = mx;
                 } else {
-                    const float wm = wave_max(fmaxf(kvm, mx));
+                    const float wm = xg_max_rs(row16_max(fmaxf(kvm, mx)));   // DPP + permlanes
                     const int hd = rel >> 5;                    // head index over [K heads | V heads]
                     if (lane == 0) kvred[hd & 1][wv] = wm;
                     kv_pend = 1 + hd;                           // finalised after the next barrier

@@ -512,7 +512,7 @@ layernorm_bwd_kernel(const float* __restrict__ x, int64_t n, int d, const float*
 }
 
 // ---- column sums -----------------------------------------------------------------------
-constexpr int kColRows = 1024;
+constexpr int kColRows = 256;     // rows per partial: >= 4 blocks per CU on the tall inputs
 
 __global__ void __launch_bounds__(256)
 colsum_part_kernel(const float* __restrict__ x, int64_t n, int c, int64_t ldx, double* __restrict__ part) {
@@ -521,7 +521,16 @@ colsum_part_kernel(const float* __restrict__ x, int64_t n, int c, int64_t ldx, d
     double s = 0.0;
     if (ch < c) {
         const int64_t r1 = min(n, r0 + kColRows);
-        for (int64_t r = r0 + rg; r < r1; r += 4) s += (double)x[r * ldx + ch];
+        double s1 = 0.0, s2 = 0.0, s3 = 0.0;       // four chains: the loads stay in flight
+        int64_t r = r0 + rg;
+        for (; r + 12 < r1; r += 16) {
+            s += (double)x[r * ldx + ch];
+            s1 += (double)x[(r + 4) * ldx + ch];
+            s2 += (double)x[(r + 8) * ldx + ch];
+            s3 += (double)x[(r + 12) * ldx + ch];
+        }
+        for (; r < r1; r += 4) s += (double)x[r * ldx + ch];
+        s = (s + s1) + (s2 + s3);
     }
     __shared__ double l[4][64];
     l[rg][threadIdx.x % 64] = s;

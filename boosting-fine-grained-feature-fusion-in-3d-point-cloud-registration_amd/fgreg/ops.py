@@ -33,6 +33,13 @@ class KernelTimer:
         self.labels = {n: [] for n in names}     # optional per-launch label (e.g. GEMM shape)
         self.count = False
         self.pool = []
+        # lead_cycles > 0: a spin kernel of that many cycles (torch.cuda._sleep) goes on the
+        # launch stream ahead of every timed call, so the GPU is still busy with it while the
+        # host records the start event and submits the call's kernels: the start event then
+        # fires right before the first kernel instead of a host launch latency earlier (an
+        # eager replay is host-bound; without the lead each interval also holds the
+        # submission gap, several us per launch against the kernel trace's durations)
+        self.lead_cycles = 0
 
     def begin(self, name, label=None):
         """Creates the event pair of one launch and arms it in libfgreg
@@ -41,6 +48,8 @@ class KernelTimer:
         ctypes time before the launch, during which the GPU may sit idle."""
         if name not in self.names:
             return None
+        if self.lead_cycles > 0:
+            torch.cuda._sleep(self.lead_cycles)
         start, end = self.pool.pop() if self.pool else self._pair()
         _lib.check(_lib.load().fgr_time_next_call(start.cuda_event, end.cuda_event),
                    'fgr_time_next_call')
