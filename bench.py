@@ -121,7 +121,7 @@ def parse():
     p.add_argument('--cpu-seconds', type=float, default=10.0,
                    help='budget of the CPU baseline B=1 sample (0 disables it)')
     p.add_argument('--no-cpu-baseline', action='store_true')
-    p.add_argument('--lead-cycles', type=int, default=250000,
+    p.add_argument('--lead-cycles', type=int, default=0,
                    help='spin kernel ahead of every per-launch timed call of the rooflines\' '
                         'eager replay (ops.KernelTimer.lead_cycles; 0 = off)')
     p.add_argument('--no-pipeline', action='store_true',
@@ -132,6 +132,8 @@ def parse():
     p.add_argument('--train', action='store_true',
                    help='time training steps instead (SURVEY §8(f) row 4): train() forward + '
                         'backward + clip_grad_norm_ + AdamW step; a side line, not the headline')
+    p.add_argument('--gather-table', default=None,
+                   help='write the per-launch KPConv gather table (JSON) here')
     p.add_argument('--gemm-table', default=None,
                    help='write the per-shape GEMM table (M, N, K, launches, us, TFLOP/s, '
                         'bytes, fractions) of the instrumented replay to this JSON file')
@@ -467,6 +469,8 @@ def main():
 
     if args.gemm_table and rank == 0:
         write_gemm_table(args.gemm_table, rtimer, args.steps, step_ms, lin.MODE)
+    if args.gather_table and rank == 0:
+        write_gather_table(args.gather_table, rtimer, work['kpconv_gather'], args.steps, step_ms)
     line['roofline_attention'] = mfma_family('attention', ops.ATTN_MODE,
                                              f'fgr_attention_{ops.ATTN_MODE}')
     line['roofline_gemm'] = mfma_family('gemm', lin.MODE, f'fgr_gemm_{lin.MODE} (all dense layers)')
@@ -494,6 +498,33 @@ def main():
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def write_gather_table(path, rtimer, work, steps, step_ms):
+    """Per-launch table of the KPConv gather: per call of a step (nq
+    queries, H table width, Cin, K kernel points), the valid neighbours per query (recovered
+    from the algorithmic bytes), the event-timed us averaged over the
+    replayed steps, the algorithmic bytes and their fraction of the HBM peak."""
+    per = len(work)
+    ev, lab = rtimer.events['kpconv_gather'], rtimer.labels['kpconv_gather']
+    rows = []
+    for i in range(per):
+        ts = [ev[j][0].elapsed_time(ev[j][1]) for j in range(i, len(ev), per)]
+        us = float(np.mean(ts)) * 1e3
+        nq, H, cin, K = lab[i]
+        byt = float(work[i])
+        valid = (byt - nq * (8 * H + 12 + 4 * K * cin + 4)) / (12 + 4 * cin) / max(nq, 1)
+        rows.append({'call': i, 'nq': nq, 'H': H, 'cin': cin, 'K': K,
+                     'valid_per_query': valid, 'us': us, 'mbytes': byt / 1e6,
+                     'wf_write_mbytes': nq * K * cin * 4 / 1e6,
+                     'gbs': byt / (us * 1e-6) / 1e9, 'frac': byt / (us * 1e-6) / 1e9 / HBM_PEAK_GBS})
+    tot_b = sum(r['mbytes'] for r in rows) * 1e6
+    tot_us = sum(r['us'] for r in rows)
+    with open(path, 'w') as f:
+        json.dump({'hbm_peak_gbs': HBM_PEAK_GBS, 'ms_per_step': step_ms,
+                   'gather_us_per_step': tot_us,
+                   'frac_all': tot_b / (tot_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 'calls': rows},
+                  f, indent=1)
 
 
 def write_gemm_table(path, rtimer, steps, step_ms, mode):

@@ -55,6 +55,15 @@
 
 #include "common.h"
 
+#ifdef FGR_RS_STAMP
+// Diagnostic build only (tools/build_stamp.sh, tools/rs_stamp.py): per-block clock stamps of
+// the rs kernel, read back by fgr_debug_rs_stamps. [0] s_memrealtime at entry, [1]
+// s_memtime at entry, [2] after the prologue (rows loaded and split), [3] after panel 0's
+// barrier, [4] after the last panel's barrier, [5] at exit, [6] s_memrealtime at exit, [7]
+// panels of the block.
+__device__ unsigned long long g_rs_stamp[1 << 14][8];
+#endif
+
 namespace fgr {
 namespace {
 
@@ -162,6 +171,11 @@ __global__ void __launch_bounds__(256, KV ? 2 : 1) gemm_rs_kernel(RsArgs p) {
     __shared__ float4 kvbuf[KV ? 4 : 1][KV ? 16 : 1][8];
     static_assert(!KV || RT == 1, "KV images: one 64-row tile per block");
 
+#ifdef FGR_RS_STAMP
+    unsigned long long st_[8];
+    st_[0] = __builtin_amdgcn_s_memrealtime();
+    st_[1] = __builtin_amdgcn_s_memtime();
+#endif
     const int nbm = (p.M + 64 * RT - 1) / (64 * RT);
     const int npanel = (p.N + 15) / 16;
     const int ngrp = (npanel + p.nc - 1) / p.nc;
@@ -509,6 +523,9 @@ __global__ void __launch_bounds__(256, KV ? 2 : 1) gemm_rs_kernel(RsArgs p) {
         }
     };
 
+#ifdef FGR_RS_STAMP
+    st_[2] = __builtin_amdgcn_s_memtime();
+#endif
     float4 rcur[RT];
     f32x4 prev[RT];
     for (int q = 0; q < np; ++q) {
@@ -522,6 +539,10 @@ __global__ void __launch_bounds__(256, KV ? 2 : 1) gemm_rs_kernel(RsArgs p) {
         else wait_vm_lgkm0_dyn((q >= 3 ? nstore(q - 3) : 0) + (q >= 2 ? nstore(q - 2) : 0) +
                                (q + 1 < np ? PW : 0));
         __builtin_amdgcn_s_barrier();                    // every wave's pieces; buffer of q - 1 free
+#ifdef FGR_RS_STAMP
+        if (q == 0) st_[3] = __builtin_amdgcn_s_memtime();
+        if (q == np - 1) st_[4] = __builtin_amdgcn_s_memtime();
+#endif
         if constexpr (KV)
             if (kv_pend) kv_finish();                    // block-uniform
         if constexpr (RES)
@@ -544,6 +565,13 @@ __global__ void __launch_bounds__(256, KV ? 2 : 1) gemm_rs_kernel(RsArgs p) {
             kv_finish();
         }
     }
+#ifdef FGR_RS_STAMP
+    __syncthreads();
+    st_[5] = __builtin_amdgcn_s_memtime();
+    st_[6] = __builtin_amdgcn_s_memrealtime();
+    st_[7] = (unsigned long long)np;
+    if (tid < 8 && blockIdx.x < (1 << 14)) g_rs_stamp[blockIdx.x][tid] = st_[tid];
+#endif
     if constexpr (HEAD) {
         // sum the lane groups' column quads: lanes c, c + 16, c + 32, c + 48 hold one row
 #pragma unroll
@@ -685,3 +713,11 @@ bool gemm_rs_f16x3(const float* A, int64_t lda, const void* W, int ksteps, const
 }
 
 }  // namespace fgr
+
+#ifdef FGR_RS_STAMP
+extern "C" int fgr_debug_rs_stamps(void* dst, int32_t nblocks) {
+    if (nblocks > (1 << 14)) nblocks = 1 << 14;
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_rs_stamp), (size_t)nblocks * 64, 0,
+                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -331,7 +331,7 @@ def kpconv_gather(q, s, idx, x, kernel_points, extent) -> Tuple[torch.Tensor, to
     nb = _lib._sz(0)
     _lib.check(L.fgr_kpconv_gather_workspace(ns, cin, nb), 'fgr_kpconv_gather_workspace')
     ws = _workspace(q.device, nb.value) if nb.value else None
-    t0 = _begin('kpconv_gather')
+    t0 = _begin('kpconv_gather', (nq, idx.shape[1], cin, K))
     _lib.check(L.fgr_kpconv_gather(_ptr(q), _ptr(s), nq, ns, _ptr(idx), idx.shape[1], _ptr(x), cin,
                                    _ptr(kp), K, float(extent), _ptr(wf), _ptr(nnorm), _ptr(ws),
                                    nb.value, _stream()), 'fgr_kpconv_gather')
