@@ -97,7 +97,9 @@ class TransformerCrossEncoderLayer(nn.Module):
         if ln is not None:
             x, norm, pos = ln
             d = x.shape[1]
-            if (QKV_IMAGES and lin.MODE == 'f16x3' and ops.ATTN_MODE == 'f16x3'
+            # the image path forms norm(x) + pos in its prologue: it needs the pos rows
+            # (transformer_encoder_has_pos_emb False -> pos None -> linear_ln below)
+            if (QKV_IMAGES and lin.MODE == 'f16x3' and ops.ATTN_MODE == 'f16x3' and pos is not None
                     and ops.ln_qkv_supported(x.shape[0], d, self.nhead)
                     and (side is None or side[0].eps == norm.eps)):
                 # k / v straight into the attention's images (no fp32 k / v, no image launch)

@@ -81,7 +81,11 @@ def main():
         print(f'world {world} backend {dist.get_backend()} workload {args.workload}: {B} pairs, '
               f'{how} {counts}, gathered {tuple(poses.shape)} on {poses.device}, '
               f'max |pose diff| {err:.3e}', flush=True)
-        ok[0] = 1.0 if err < 1e-4 and poses.shape == full.shape else 0.0
+        # ModelNet pairs are equal-sized: a shard's rows run the same GEMM dispatch as the full
+        # batch's, 1e-5. Ragged 3DMatch shards change the row counts M of every GEMM, hence the
+        # dispatched tile family and its summation order: rounding-level pose differences, 1e-4.
+        tol = 1e-5 if args.workload == 'modelnet' else 1e-4
+        ok[0] = 1.0 if err < tol and poses.shape == full.shape else 0.0
     dist.broadcast(ok, 0)
     dist.destroy_process_group()
     sys.exit(0 if ok.item() == 1.0 else 1)

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Per-launch event timing of the bench's roofline replay vs the kernel trace (GPU box):
-# the same workload with --lead-cycles 0 and the default lead, then a rocprofv3 kernel trace
+# the same workload with --lead-cycles 0 (the default) and a 250k-cycle spin lead, then a rocprofv3 kernel trace
 # of a default run, whose per-kernel average durations the event averages should match.
 # usage: bash tools/timing_check.sh <tag> [workload]
 set -o pipefail
@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 timeout -k 10 300 python bench.py --workload $wl --steps 20 --warmup 5 --no-cpu-baseline --lead-cycles 0 \
     --gemm-table gpurun_out/tc_${tag}_lead0_gemm.json > gpurun_out/tc_${tag}_lead0.json 2> gpurun_out/tc_${tag}_lead0.err || exit 1
-timeout -k 10 300 python bench.py --workload $wl --steps 20 --warmup 5 --no-cpu-baseline \
+timeout -k 10 300 python bench.py --workload $wl --steps 20 --warmup 5 --no-cpu-baseline --lead-cycles 250000 \
     --gemm-table gpurun_out/tc_${tag}_lead_gemm.json > gpurun_out/tc_${tag}_lead.json 2> gpurun_out/tc_${tag}_lead.err || exit 1
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/tc_${tag}_prof -- \
     python3 bench.py --workload $wl --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/tc_${tag}_prof.json 2> gpurun_out/tc_${tag}_prof.err || exit 1
