@@ -102,6 +102,7 @@ OTHER = {
     'instnorm': ('hbm', '8 N C bytes (+ 4 N C residual, + 4 N row divisor)'),
     'layernorm': ('hbm', '8 N d bytes (+ 4 N d per add / pre-bias)'),
     'pose': ('hbm', '28 B per (layer, point) + 48 B per pose'),
+    'max_pool': ('hbm', '8 H + 4 C bytes per query + 4 C per valid neighbour row'),
 }
 
 
@@ -356,7 +357,7 @@ def main():
             torch.cuda.synchronize()
         else:
             # algorithmic work per launch (untimed pass with counting on)
-            fams = ['kpconv_gather', 'attention', 'gemm'] + list(OTHER)
+            fams = ['kpconv_gather', 'attention', 'gemm', 'res2net'] + list(OTHER)
             timer = ops.KernelTimer(fams)
             timer.count = True
             ops.TIMER = timer
@@ -474,6 +475,21 @@ def main():
     line['roofline_attention'] = mfma_family('attention', ops.ATTN_MODE,
                                              f'fgr_attention_{ops.ATTN_MODE}')
     line['roofline_gemm'] = mfma_family('gemm', lin.MODE, f'fgr_gemm_{lin.MODE} (all dense layers)')
+    if work['res2net']:
+        # the Res2Net hierarchy (fgr_res2net_chain_h3: 3 fp16 products per product;
+        # fgr_res2net_chain6: 6 bf16 products): work counted in matrix-core products
+        ms = rtimer.total_ms('res2net')
+        prod = float(sum(work['res2net']))
+        ach = prod * args.steps / (ms / 1e3) / 1e12 if ms > 0 else 0.0
+        kinds = sorted(set(rtimer.labels['res2net']))
+        line['roofline_res2net'] = {
+            'kernel': 'fgr_res2net_chain_' + '+'.join('h3' if k == 'h3' else '6' for k in kinds),
+            'bound': 'mfma', 'achieved': ach, 'peak': F16_MFMA_PEAK_TFLOPS,
+            'unit': 'TFLOP/s (fp16 / bf16 matrix-core products)', 'frac': ach / F16_MFMA_PEAK_TFLOPS,
+            'work': '2 N w^2 (scale - 1) per chain x 3 (h3) / 6 (bf16x6) products',
+            'products_per_step': prod, 'launches_per_step': len(work['res2net']),
+            'avg_launch_us': ms * 1e3 / max(len(rtimer.events['res2net']), 1),
+            'us_per_step': ms * 1e3 / args.steps, 'share_of_step': ms / args.steps / step_ms}
     other = {}
     for name, (bound, what) in OTHER.items():
         ms = rtimer.total_ms(name)
@@ -596,28 +612,67 @@ def _calibration():
         return json.load(f)
 
 
+def _physical_cores():
+    """Physical cores in this process's affinity mask (SMT siblings counted once), from
+    /proc/cpuinfo's (physical id, core id) pairs; the affinity count if that is unreadable."""
+    cpus = os.sched_getaffinity(0)
+    try:
+        cores, cur, phys = set(), None, 0
+        with open('/proc/cpuinfo') as f:
+            for line in f:
+                k, _, v = line.partition(':')
+                k = k.strip()
+                if k == 'processor':
+                    cur = int(v)
+                elif k == 'physical id':
+                    phys = int(v)
+                elif k == 'core id' and cur in cpus:
+                    cores.add((phys, int(v)))
+        return len(cores) or len(cpus)
+    except (OSError, ValueError):
+        return len(cpus)
+
+
+def _cpu_leg(mo, cfg, sd, src, tgt, budget_s, threads):
+    """B=1 forwards of the port with `threads` torch threads for ~budget_s -> (pairs, s)."""
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        n_pairs, t_tot, it = 0, 0.0, 0
+        while t_tot < budget_s and it < 64:
+            b = it % len(src)
+            t0 = time.perf_counter()
+            mo.forward(cfg, sd, [src[b]], [tgt[b]], mode=mo.geom.INDEX)
+            t_tot += time.perf_counter() - t0
+            n_pairs += 1
+            it += 1
+    finally:
+        torch.set_num_threads(prev)
+    return n_pairs, t_tot
+
+
 def cpu_baseline(cfg, model, src, tgt, budget_s, tail_inputs=None, workload='modelnet'):
     """CPU restatement (oracle/model_oracle.py, "port") on the same pairs: B=1 forwards for
-    ~budget_s, then one B=len(src) forward (BASELINE.md §3 asks for both legs)."""
+    ~budget_s on every physical core of the host, the same on the per-GPU CPU
+    share of the lease (OMP_NUM_THREADS) for ~budget_s / 2 beside it, then one B=len(batch)
+    leg."""
     sys.path.insert(0, os.path.join(REPO, 'oracle'))
     import model_oracle as mo
     sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
-    threads = torch.get_num_threads()
-    n_pairs, t_tot, it = 0, 0.0, 0
-    while t_tot < budget_s and it < 64:
-        b = it % len(src)
-        t0 = time.perf_counter()
-        mo.forward(cfg, sd, [src[b]], [tgt[b]], mode=mo.geom.INDEX)
-        t_tot += time.perf_counter() - t0
-        n_pairs += 1
-        it += 1
+    share = torch.get_num_threads()
+    threads = _physical_cores()
+    mo.forward(cfg, sd, [src[0]], [tgt[0]], mode=mo.geom.INDEX)       # warm (allocator, pools)
+    n_pairs, t_tot = _cpu_leg(mo, cfg, sd, src, tgt, budget_s, threads)
+    n_sh, t_sh = _cpu_leg(mo, cfg, sd, src, tgt, budget_s / 2, share)
     res = {'value': n_pairs / t_tot, 'unit': 'pairs/s', 'cores': threads, 'kind': 'port',
            'cpu_model': _cpu_model(),
-           # the GPU box leases a CPU share per GPU: torch's thread count follows the lease's
-           # OMP_NUM_THREADS (16 per GPU), while the affinity mask / os.cpu_count() show more
-           'cores_note': {'torch_threads': threads, 'omp_num_threads': os.environ.get('OMP_NUM_THREADS'),
-                          'affinity_cpus': len(os.sched_getaffinity(0)), 'machine_cpus': os.cpu_count(),
-                          'basis': 'the per-GPU CPU share of the lease (OMP_NUM_THREADS)'},
+           'cores_note': {'torch_threads': threads, 'basis': 'every physical core of the affinity '
+                          'mask (SMT siblings once)', 'omp_num_threads': os.environ.get('OMP_NUM_THREADS'),
+                          'affinity_cpus': len(os.sched_getaffinity(0)), 'machine_cpus': os.cpu_count()},
+           'per_gpu_share': {'value': n_sh / t_sh, 'unit': 'pairs/s', 'cores': share,
+                             'what': 'the same B=1 leg on the per-GPU CPU share of the lease '
+                                     '(torch threads = OMP_NUM_THREADS)',
+                             'sample': f'{n_sh} pairs, {t_sh:.1f} s'},
            'sample': f'{n_pairs} pairs (B=1 forwards) of the same workload, '
                      f'{t_tot:.1f} s, torch CPU fp32 with {threads} threads'}
     if len(src) > 1:

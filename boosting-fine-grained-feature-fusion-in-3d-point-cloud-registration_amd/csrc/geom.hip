@@ -1,174 +1,14 @@
-// KPConv pyramid geometry on gfx950: grid subsampling and radius neighbour search.
+// KPConv pyramid geometry on gfx950: brute-force radius neighbour search (grid subsampling
+// and the voxel-binned radius search live in grid.hip).
 //
 // Built with -ffp-contract=off: every float expression below rounds exactly as
 // written, which is what makes voxel keys, barycentres and the d2 < r2 test
 // bit-identical to the reference's C++ (grid_subsampling.cpp, neighbors.cpp +
 // nanoflann.hpp) and to oracle/geom_oracle.c.
-#include <hipcub/hipcub.hpp>
-
 #include "common.h"
 
 namespace fgr {
 namespace {
-
-// ------------------------------------------------------------------------------------
-// Grid subsampling
-// ------------------------------------------------------------------------------------
-struct CloudGrid {
-    float org[3];
-    float pad;
-    unsigned long long nx, ny;
-};
-
-// One block per cloud: bounding box -> origin and grid dims (grid_subsampling.cpp:25-31).
-__global__ void __launch_bounds__(256) grid_bbox_kernel(const float* __restrict__ pts,
-                                                        const int64_t* __restrict__ off,
-                                                        float dl, CloudGrid* __restrict__ grids) {
-    const int c = blockIdx.x;
-    const int64_t b = off[c], e = off[c + 1];
-    float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
-    for (int64_t i = b + threadIdx.x; i < e; i += blockDim.x) {
-#pragma unroll
-        for (int d = 0; d < 3; ++d) {
-            float v = pts[3 * i + d];
-            mn[d] = fminf(mn[d], v);
-            mx[d] = fmaxf(mx[d], v);
-        }
-    }
-    __shared__ float red[2][3][4];
-#pragma unroll
-    for (int d = 0; d < 3; ++d) {
-        for (int o = 32; o > 0; o >>= 1) {
-            mn[d] = fminf(mn[d], __shfl_xor(mn[d], o, kWave));
-            mx[d] = fmaxf(mx[d], __shfl_xor(mx[d], o, kWave));
-        }
-    }
-    const int w = threadIdx.x / kWave, l = threadIdx.x % kWave;
-    if (l == 0) {
-        for (int d = 0; d < 3; ++d) { red[0][d][w] = mn[d]; red[1][d][w] = mx[d]; }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        CloudGrid g;
-        float inv = 1.0f / dl;
-        float fmn[3], fmx[3];
-        for (int d = 0; d < 3; ++d) {
-            fmn[d] = fminf(fminf(red[0][d][0], red[0][d][1]), fminf(red[0][d][2], red[0][d][3]));
-            fmx[d] = fmaxf(fmaxf(red[1][d][0], red[1][d][1]), fmaxf(red[1][d][2], red[1][d][3]));
-            g.org[d] = floorf(fmn[d] * inv) * dl;
-        }
-        g.pad = 0.f;
-        g.nx = (unsigned long long)(long long)floorf((fmx[0] - g.org[0]) / dl) + 1ull;
-        g.ny = (unsigned long long)(long long)floorf((fmx[1] - g.org[1]) / dl) + 1ull;
-        grids[c] = g;
-    }
-}
-
-// Voxel key per point (grid_subsampling.cpp:53-56); value = point index.
-__global__ void grid_key_kernel(const float* __restrict__ pts, const int64_t* __restrict__ off,
-                                int n_clouds, int64_t n, float dl,
-                                const CloudGrid* __restrict__ grids,
-                                unsigned long long* __restrict__ keys, int* __restrict__ vals) {
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int c = find_segment(off, n_clouds, i);
-    const CloudGrid g = grids[c];
-    unsigned long long ix = (unsigned long long)(long long)floorf((pts[3 * i] - g.org[0]) / dl);
-    unsigned long long iy = (unsigned long long)(long long)floorf((pts[3 * i + 1] - g.org[1]) / dl);
-    unsigned long long iz = (unsigned long long)(long long)floorf((pts[3 * i + 2] - g.org[2]) / dl);
-    keys[i] = ix + g.nx * iy + g.nx * g.ny * iz;
-    vals[i] = (int)i;
-}
-
-// Voxel-head flags over the (cloud, key)-sorted keys.
-__global__ void grid_head_kernel(const unsigned long long* __restrict__ skeys,
-                                 const int64_t* __restrict__ off, int n_clouds, int64_t n,
-                                 int* __restrict__ flags) {
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int c = find_segment(off, n_clouds, i);
-    flags[i] = (i == off[c] || skeys[i] != skeys[i - 1]) ? 1 : 0;
-}
-
-// Per-cloud voxel counts + total (from the inclusive scan of head flags); voxel starts.
-__global__ void grid_count_kernel(const int* __restrict__ scan, const int* __restrict__ flags,
-                                  const int64_t* __restrict__ off, int n_clouds, int64_t n,
-                                  int64_t* __restrict__ counts, int* __restrict__ vstart) {
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n && flags[i]) vstart[scan[i] - 1] = (int)i;
-    if (i < n_clouds) {
-        int64_t b = off[i], e = off[i + 1];
-        int64_t before = b > 0 ? scan[b - 1] : 0;
-        int64_t upto = e > 0 ? scan[e - 1] : 0;
-        counts[i] = e > b ? upto - before : 0;
-    }
-    if (i == 0) {
-        int total = n > 0 ? scan[n - 1] : 0;
-        counts[n_clouds] = total;
-        vstart[total] = (int)n;
-    }
-}
-
-// Barycentre per voxel: members summed in input order (grid_subsampling.cpp:70, 87).
-__global__ void grid_fill_kernel(const float* __restrict__ pts, const int* __restrict__ svals,
-                                 const unsigned long long* __restrict__ skeys,
-                                 const int* __restrict__ vstart, int64_t n_out,
-                                 float* __restrict__ out, int64_t* __restrict__ out_keys) {
-    int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= n_out) return;
-    const int b = vstart[v], e = vstart[v + 1];
-    float sx = 0.f, sy = 0.f, sz = 0.f;
-    for (int j = b; j < e; ++j) {
-        const int p = svals[j];
-        sx += pts[3 * p];
-        sy += pts[3 * p + 1];
-        sz += pts[3 * p + 2];
-    }
-    const float s = (float)(1.0 / (double)(e - b));
-    out[3 * v] = sx * s;
-    out[3 * v + 1] = sy * s;
-    out[3 * v + 2] = sz * s;
-    if (out_keys) out_keys[v] = (int64_t)skeys[b];
-}
-
-struct GridWs {
-    CloudGrid* grids;
-    unsigned long long *keys, *skeys;
-    int *vals, *svals, *flags, *scan, *vstart;
-    void* temp;
-    size_t temp_bytes;
-    size_t total;
-};
-
-size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
-
-int carve(void* ws, int64_t n, int32_t n_clouds, size_t temp_bytes, GridWs* g) {
-    char* p = static_cast<char*>(ws);
-    size_t o = 0;
-    auto take = [&](size_t bytes) { void* r = p ? p + o : nullptr; o += align_up(bytes); return r; };
-    g->grids = (CloudGrid*)take(sizeof(CloudGrid) * n_clouds);
-    g->keys = (unsigned long long*)take(8 * n);
-    g->skeys = (unsigned long long*)take(8 * n);
-    g->vals = (int*)take(4 * n);
-    g->svals = (int*)take(4 * n);
-    g->flags = (int*)take(4 * n);
-    g->scan = (int*)take(4 * n);
-    g->vstart = (int*)take(4 * (n + 1));
-    g->temp = take(temp_bytes);
-    g->temp_bytes = temp_bytes;
-    g->total = o;
-    return 0;
-}
-
-size_t cub_temp_bytes(int64_t n, int32_t n_clouds) {
-    size_t a = 0, b = 0;
-    (void)hipcub::DeviceSegmentedRadixSort::SortPairs(
-        nullptr, a, (const unsigned long long*)nullptr, (unsigned long long*)nullptr,
-        (const int*)nullptr, (int*)nullptr, (int)n, n_clouds, (const int64_t*)nullptr,
-        (const int64_t*)nullptr + 1);
-    (void)hipcub::DeviceScan::InclusiveSum(nullptr, b, (const int*)nullptr, (int*)nullptr, (int)n);
-    return a > b ? a : b;
-}
 
 // ------------------------------------------------------------------------------------
 // Radius search
@@ -322,69 +162,6 @@ radius_dist_kernel(const float* __restrict__ q, const int64_t* __restrict__ q_of
 }  // namespace fgr
 
 using namespace fgr;
-
-namespace fgr {
-
-// The radix-sort path of grid subsampling (hipCUB segmented sort of the voxel keys), used by
-// the entry points in grid.hip when the caller selects it (max_cells < 0): it handles any key
-// space, the dense counting-sort path only those that fit its histogram.
-size_t grid_radix_ws_bytes(int64_t n_points, int32_t n_clouds) {
-    GridWs g;
-    carve(nullptr, n_points, n_clouds, cub_temp_bytes(n_points, n_clouds), &g);
-    return g.total;
-}
-
-int grid_radix_count(const float* points, const int64_t* off, int32_t n_clouds, int64_t n_points,
-                     float dl, void* ws, size_t ws_bytes, int64_t* counts, hipStream_t st) {
-    GridWs g;
-    size_t tb = cub_temp_bytes(n_points, n_clouds);
-    carve(ws, n_points, n_clouds, tb, &g);
-    if (g.total > ws_bytes) {
-        set_error("fgr_grid_subsample_count: workspace %zu < %zu bytes", ws_bytes, g.total);
-        return FGR_E_WORKSPACE;
-    }
-    hipLaunchKernelGGL(grid_bbox_kernel, dim3(n_clouds), dim3(256), 0, st, points, off, dl,
-                       g.grids);
-    FGR_CHECK_LAUNCH("grid_bbox_kernel");
-    if (n_points > 0) {
-        const int64_t nb = ceil_div(n_points, 256);
-        hipLaunchKernelGGL(grid_key_kernel, dim3(nb), dim3(256), 0, st, points, off, n_clouds,
-                           n_points, dl, g.grids, g.keys, g.vals);
-        FGR_CHECK_LAUNCH("grid_key_kernel");
-        size_t tmp = g.temp_bytes;
-        FGR_CHECK_HIP(hipcub::DeviceSegmentedRadixSort::SortPairs(
-            g.temp, tmp, g.keys, g.skeys, g.vals, g.svals, (int)n_points, n_clouds, off, off + 1,
-            0, 64, st));
-        hipLaunchKernelGGL(grid_head_kernel, dim3(nb), dim3(256), 0, st, g.skeys, off, n_clouds,
-                           n_points, g.flags);
-        FGR_CHECK_LAUNCH("grid_head_kernel");
-        tmp = g.temp_bytes;
-        FGR_CHECK_HIP(hipcub::DeviceScan::InclusiveSum(g.temp, tmp, g.flags, g.scan,
-                                                       (int)n_points, st));
-    }
-    const int64_t nthreads = n_points > n_clouds ? n_points : n_clouds;
-    hipLaunchKernelGGL(grid_count_kernel, dim3(ceil_div(nthreads, 256)), dim3(256), 0, st, g.scan,
-                       g.flags, off, n_clouds, n_points, counts, g.vstart);
-    FGR_CHECK_LAUNCH("grid_count_kernel");
-    return FGR_OK;
-}
-
-int grid_radix_fill(int64_t n_points, int32_t n_clouds, int64_t n_out, void* ws, size_t ws_bytes,
-                    const float* points, float* out_points, int64_t* out_keys, hipStream_t st) {
-    GridWs g;
-    carve(ws, n_points, n_clouds, cub_temp_bytes(n_points, n_clouds), &g);
-    if (g.total > ws_bytes) {
-        set_error("fgr_grid_subsample_fill: workspace %zu < %zu bytes", ws_bytes, g.total);
-        return FGR_E_WORKSPACE;
-    }
-    if (n_out == 0) return FGR_OK;
-    hipLaunchKernelGGL(grid_fill_kernel, dim3(ceil_div(n_out, 256)), dim3(256), 0, st, points,
-                       g.svals, g.skeys, g.vstart, n_out, out_points, out_keys);
-    FGR_CHECK_LAUNCH("grid_fill_kernel");
-    return FGR_OK;
-}
-
-}  // namespace fgr
 
 extern "C" int fgr_radius_count(const float* q, const int64_t* q_off, const float* s,
                                 const int64_t* s_off, int32_t n_clouds, int64_t nq,

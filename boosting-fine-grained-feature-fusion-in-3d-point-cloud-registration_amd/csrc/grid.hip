@@ -14,9 +14,9 @@
 //   nx * ny * nz; clouds are laid end to end in one histogram of `max_cells` counters sized
 //   by the caller. Voxels come out in ascending key order per cloud (= histogram order) and
 //   each barycentre sums its members in ascending point index, i.e. the reference's input
-//   order -- bit-identical to the radix-sort path and to oracle/geom_oracle.c. A key space
-//   larger than the histogram is reported back (counts[n_clouds] = -cells needed), never
-//   truncated.
+//   order -- bit-identical to oracle/geom_oracle.c. A key space larger than the histogram
+//   is reported back (counts[n_clouds] = -cells needed), never truncated; the host redoes the
+//   count with that capacity, up to 2^28 cells (fgreg.ops.grid_subsample raises past it).
 // * Radius search: supports binned into cubic cells of edge >= 1.0625 r (grown by 1.25x
 //   steps until the cloud's grid fits 4 n_c + 1024 cells, so the workspace size depends on
 //   the point count only); a query scans the 27 cells around its own. Every support within r
@@ -28,13 +28,6 @@
 #include "common.h"
 
 namespace fgr {
-
-// the radix-sort (hipCUB) path of geom.hip, kept for key spaces past any dense histogram
-size_t grid_radix_ws_bytes(int64_t n, int32_t nc);
-int grid_radix_count(const float* points, const int64_t* off, int32_t n_clouds, int64_t n_points,
-                     float dl, void* ws, size_t ws_bytes, int64_t* counts, hipStream_t st);
-int grid_radix_fill(int64_t n_points, int32_t n_clouds, int64_t n_out, void* ws, size_t ws_bytes,
-                    const float* points, float* out_points, int64_t* out_keys, hipStream_t st);
 
 namespace {
 
@@ -238,7 +231,7 @@ __global__ void __launch_bounds__(1024) dgrid_bbox_kernel(const float* __restric
         g.nx = g.ny = 1;
         g.cells = 0;
     } else {
-        // origin and dims exactly as grid_subsampling.cpp:25-31 (and geom.hip's radix path)
+        // origin and dims exactly as grid_subsampling.cpp:25-31
         const float inv = 1.0f / dl;
         long long dims[3];
         for (int d = 0; d < 3; ++d) {
@@ -648,10 +641,8 @@ extern "C" int fgr_grid_subsample_workspace(int64_t n_points, int32_t n_clouds, 
     FGR_REQUIRE(bytes && n_points >= 0 && n_clouds > 0 && n_points < (1ll << 31) &&
                     max_cells < (1ll << 31) - 1,
                 "fgr_grid_subsample_workspace: bad arguments");
-    if (max_cells < 0) {
-        *bytes = grid_radix_ws_bytes(n_points, n_clouds);
-        return FGR_OK;
-    }
+    FGR_REQUIRE(max_cells >= 0, "fgr_grid_subsample_workspace: max_cells < 0 (the radix-sort path "
+                "was removed: the dense counting sort takes key spaces up to 2^28 cells)");
     DGridWs g;
     carve_dense(nullptr, n_points, n_clouds, dense_cap(n_points, max_cells), &g);
     *bytes = g.total;
@@ -667,8 +658,7 @@ extern "C" int fgr_grid_subsample_count(const float* points, const int64_t* off,
                 "fgr_grid_subsample_count: bad arguments");
     hipStream_t st = as_stream(stream);
     TimedCall timed_(st);
-    if (max_cells < 0)
-        return grid_radix_count(points, off, n_clouds, n_points, dl, ws, ws_bytes, counts, st);
+    FGR_REQUIRE(max_cells >= 0, "fgr_grid_subsample_count: max_cells < 0 (no radix-sort path)");
     const int64_t cap = dense_cap(n_points, max_cells);
     DGridWs g;
     carve_dense(ws, n_points, n_clouds, cap, &g);
@@ -707,9 +697,7 @@ extern "C" int fgr_grid_subsample_fill(int64_t n_points, int32_t n_clouds, int64
                 "fgr_grid_subsample_fill: bad arguments");
     hipStream_t st = as_stream(stream);
     TimedCall timed_(st);
-    if (max_cells < 0)
-        return grid_radix_fill(n_points, n_clouds, n_out, ws, ws_bytes, points, out_points,
-                               out_keys, st);
+    FGR_REQUIRE(max_cells >= 0, "fgr_grid_subsample_fill: max_cells < 0 (no radix-sort path)");
     DGridWs g;
     carve_dense(ws, n_points, n_clouds, dense_cap(n_points, max_cells), &g);
     if (g.total > ws_bytes) {

@@ -143,7 +143,7 @@ def offsets(lengths: Sequence[int], device) -> torch.Tensor:
 # ------------------------------------------------------------------------------------------
 # geometry
 # ------------------------------------------------------------------------------------------
-GRID_RADIX = os.environ.get('FGREG_GRID_SORT', 'dense') == 'radix'   # A/B switch (tests)
+GRID_MAX_CELLS = 1 << 28     # dense voxel histogram ceiling (1 GiB of counters)
 
 
 def grid_subsample(points: torch.Tensor, off: torch.Tensor, lengths: Sequence[int], dl: float,
@@ -152,9 +152,10 @@ def grid_subsample(points: torch.Tensor, off: torch.Tensor, lengths: Sequence[in
 
     Returns (sub_points (M,3) f32, sub_lengths List[int][, keys (M,) int64]). One host
     sync (the voxel counts), as in the reference's own GPU path. ``max_cells``: the dense
-    voxel-key histogram's capacity (None = the library default, -1 = the radix-sort path);
-    a key space past it is reported by the count call and the count is redone with the
-    needed capacity (or the radix path beyond 2^28 counters). ``device_layout``: also return
+    voxel-key histogram's capacity (None = the library default); a key space past it is
+    reported by the count call and the count is redone with the needed capacity, up to
+    GRID_MAX_CELLS (2^28 cells: a 645-voxel cube per cloud, 16 m at 3DMatch's 2.5 cm); past
+    that it raises. ``device_layout``: also return
     the sub-clouds' lengths (nc,) and row offsets (nc + 1,) as device int64 tensors, built on
     the device from the counts (no host -> device copy): (sub, lengths, len_dev, off_dev).
     """
@@ -163,7 +164,7 @@ def grid_subsample(points: torch.Tensor, off: torch.Tensor, lengths: Sequence[in
     n, nc = pts.shape[0], len(lengths)
     assert pts.dim() == 2 and pts.shape[1] == 3 and off.numel() == nc + 1
     L = _lib.load()
-    cap = (-1 if GRID_RADIX else 0) if max_cells is None else int(max_cells)
+    cap = 0 if max_cells is None else int(max_cells)
     counts = torch.empty(nc + 1, dtype=torch.int64, device=pts.device)
     st = _stream()
     for _ in range(2):
@@ -180,7 +181,10 @@ def grid_subsample(points: torch.Tensor, off: torch.Tensor, lengths: Sequence[in
         if host[nc] >= 0:
             break
         need = -host[nc]           # dense key space past the histogram: retry once
-        cap = need if need <= (1 << 28) else -1
+        if need > GRID_MAX_CELLS:
+            raise _lib.FgrError(f'grid subsampling: the clouds\' voxel key space ({need} cells at '
+                                f'dl = {dl}) exceeds the dense histogram limit {GRID_MAX_CELLS}')
+        cap = need
     m = host[nc]
     assert m >= 0, 'grid subsampling: key space overflow after retry'
     out = torch.empty((m, 3), dtype=torch.float32, device=pts.device)
@@ -352,9 +356,19 @@ def max_pool(x, idx) -> torch.Tensor:
     _dev(x, idx)
     x, idx = _c(x, torch.float32), _c(idx, torch.int64)
     out = torch.empty((idx.shape[0], x.shape[1]), dtype=torch.float32, device=x.device)
+    t0 = _begin('max_pool')
     _lib.check(_lib.load().fgr_max_pool(_ptr(x), x.shape[0], x.shape[1], _ptr(idx), idx.shape[0],
                                         idx.shape[1], _ptr(out), _stream()), 'fgr_max_pool')
+    _end('max_pool', t0, lambda: max_pool_bytes(idx, x.shape[0], x.shape[1]))
     return out
+
+
+def max_pool_bytes(idx, ns, c):
+    """Algorithmic HBM bytes of one fgr_max_pool launch: sum_q [8 H (idx row) + 4 C (output
+    row)] + 4 C per valid neighbour row read (finegrained_kpconv_blocks.py:125-141)."""
+    nq, H = idx.shape
+    v = int((idx < ns).sum().item())
+    return nq * (8 * H + 4 * c) + v * 4 * c
 
 
 # ------------------------------------------------------------------------------------------
@@ -523,6 +537,10 @@ def res2net_chain(h, w, scale, w_frag, bias, x, cat, w_scale=None):
     if x is not None:
         x = _c(x, torch.float32)
     L = _lib.load()
+    # MFMA work: (scale - 1) chained w x w Linears over n rows, 3 (f16x3) or 6 (bf16x6) fp16 /
+    # bf16 matrix-core products per product (res2net.py:126-159)
+    t0 = _begin('res2net', 'h3' if w_scale is not None else 'x6')
+    work = 2 * n * w * w * (scale - 1) * (3 if w_scale is not None else 6)
     if w_scale is not None:
         _lib.check(L.fgr_res2net_chain_h3(
             _ptr(h), n, w, scale, _ptr(w_frag), _ptr(w_scale), _ptr(bias), _ptr(x), cin,
@@ -531,6 +549,7 @@ def res2net_chain(h, w, scale, w_frag, bias, x, cat, w_scale=None):
         _lib.check(L.fgr_res2net_chain6(_ptr(h), n, w, scale, _ptr(w_frag), _ptr(bias), _ptr(x),
                                         cin, _ptr(cat), cat.stride(0), _stream()),
                    'fgr_res2net_chain6')
+    _end('res2net', t0, work)
     return cat
 
 

@@ -101,10 +101,11 @@ class CorrespondenceDecoder(nn.Module):
     num_neighbors > 0 reproduces the reference's masking as it executes (:353-357, see
     fgr_corr_topk_mask in include/fgreg.h): a query row keeps its plain softmax iff its index
     is in the union of all top-k key indices of its direction, else it is NaN; an index >= the
-    padded query length raises IndexError like the reference's indexing. Exact for batches
-    without padding (every src cloud of one length, every tgt cloud of one length, e.g. B = 1);
-    padded batches raise NotImplementedError (the reference's padded query rows -- transformer
-    outputs at padded positions -- feed its union and do not exist in the packed layout)."""
+    padded query length raises IndexError like the reference's indexing. On padded batches the
+    reference's padded query rows (its transformer's outputs at padded positions, queries of
+    every attention and never keys) feed the union too: they are carried as query-only
+    "phantom" rows after the clouds' rows (Segments(phantoms=...), RegTR._segments: one row per
+    padded cloud, since all padded positions of a cloud compute the same row)."""
 
     def __init__(self, d_embed, use_pos_emb, pos_embed=None, num_neighbors=0):
         super().__init__()
@@ -117,7 +118,11 @@ class CorrespondenceDecoder(nn.Module):
         self.num_neighbors = num_neighbors
 
     def forward_packed(self, feats, xyz, pos, seg: Segments):
+        """feats (L, N + P, d): the clouds' rows, then seg's P phantom rows (whose positional
+        embedding is the reference's zero padding); xyz / pos: the clouds' N rows."""
         L, N, d = feats.shape
+        if self.use_pos_emb and pos.shape[0] < N:
+            pos = torch.cat([pos, pos.new_zeros((N - pos.shape[0], d))])
         f = (feats + pos.unsqueeze(0) if self.use_pos_emb else feats).reshape(L * N, d)
         q = linear(f, self.q_proj.weight, self.q_proj.bias)
         k = linear(f, self.k_proj.weight, self.k_proj.bias)
@@ -134,20 +139,73 @@ class CorrespondenceDecoder(nn.Module):
     def _topk_mask(self, corr, q, k, seg: Segments, d):
         B = seg.B
         src_l, tgt_l = seg.lengths[:B], seg.lengths[B:]
-        if len(set(src_l)) > 1 or len(set(tgt_l)) > 1:
-            raise NotImplementedError('num_neighbors > 0 with padded batches (clouds of unequal '
-                                      'length in one direction)')
-        n_src, n_tgt = src_l[0], tgt_l[0]
+        n_src, n_tgt = max(src_l), max(tgt_l)                # the padded Q / S of each direction
         if self.num_neighbors > min(n_src, n_tgt):
             raise RuntimeError('selected index k out of range')              # torch.topk
+        if self.num_neighbors > min(src_l + tgt_l):
+            # the top-k of a row would then rank -inf padded keys, whose order torch.topk
+            # leaves unspecified
+            raise NotImplementedError('num_neighbors > the shortest cloud of a padded batch')
+        if (any(p > 0 for p in seg.phantoms[:B]) and len(set(src_l)) == 1) or \
+                (any(p > 0 for p in seg.phantoms[B:]) and len(set(tgt_l)) == 1):
+            raise ValueError('phantom rows for a direction without padding')
+        for c in range(2 * B):
+            if (len(set(src_l)) > 1 if c < B else len(set(tgt_l)) > 1) and \
+                    seg.lengths[c] < (n_src if c < B else n_tgt) and seg.phantoms[c] == 0:
+                raise ValueError(f'cloud {c} is padded in the reference but has no phantom row')
         q_off, kv_seg, _ = seg.layer_tables
-        flags = ops.corr_topk_mask(corr, q, k, q_off, q_off, kv_seg, 2 * B, seg.max_len,
-                                   max(n_src, n_tgt), 1.0 / math.sqrt(d), self.num_neighbors)
+        if seg.n_phantom == 0:
+            flags = ops.corr_topk_mask(corr, q, k, q_off, q_off, kv_seg, 2 * B, seg.max_len,
+                                       max(n_src, n_tgt), 1.0 / math.sqrt(d), self.num_neighbors)
+        else:
+            flags = self._topk_mask_phantoms(corr, q, k, seg, d, max(n_src, n_tgt))
         # src queries pick tgt key indices that index the src query dim, and vice versa
         for dir_, n_q, n_k in ((0, n_src, n_tgt), (1, n_tgt, n_src)):
             if n_k > n_q and bool(flags[dir_, n_q:n_k].any()):
                 hi = int(flags[dir_, :n_k].nonzero().max())
                 raise IndexError(f'index {hi} is out of bounds for dimension 2 with size {n_q}')
+
+    def _topk_mask_phantoms(self, corr, q, k, seg: Segments, d, max_kv):
+        """The mask with phantom rows: fgr_corr_topk_mask takes a segment's direction from its
+        position in the layer ((s mod n) >= n / 2), so the rows are gathered per layer into
+        [src clouds, src phantom groups, tgt clouds, tgt phantom groups] (empty groups for the
+        clouds without padding), masked there, and scattered back."""
+        B, n = seg.B, 2 * seg.B
+        N = sum(seg.seg_lengths)
+        L = q.shape[0] // N
+        start = [0]
+        for ln in seg.seg_lengths:
+            start.append(start[-1] + ln)
+        ph_start, j = {}, n
+        for c in range(n):
+            if seg.phantoms[c] > 0:
+                ph_start[c] = start[j]
+                j += 1
+        rows, lens = [], []
+        for l in range(L):
+            for dir_ in (0, 1):
+                for b in range(B):                                   # the clouds
+                    c = dir_ * B + b
+                    rows.append(torch.arange(start[c], start[c + 1]) + l * N)
+                    lens.append(seg.lengths[c])
+                for b in range(B):                                   # their phantom groups
+                    c = dir_ * B + b
+                    p = seg.phantoms[c]
+                    rows.append(torch.arange(ph_start.get(c, 0), ph_start.get(c, 0) + p) + l * N)
+                    lens.append(p)
+        real = lambda c: c if c < B else 2 * B + (c - B)           # noqa: E731
+        cloud = [b for b in range(B)] * 2 + [B + b for b in range(B)] * 2
+        kv = [l * 4 * B + real((cloud[s] + B) % n) for l in range(L) for s in range(4 * B)]
+        dev = q.device
+        idx = torch.cat(rows).to(dev)
+        off = ops.offsets(lens, dev)
+        kv_seg = torch.tensor(kv, dtype=torch.int32, device=dev)
+        cp = corr[idx].contiguous()
+        flags = ops.corr_topk_mask(cp, q[idx].contiguous(), k[idx].contiguous(), off, off, kv_seg,
+                                   4 * B, max(lens), max_kv, 1.0 / math.sqrt(d),
+                                   self.num_neighbors)
+        corr[idx] = cp
+        return flags
 
 
 class _LossParams(nn.Module):
@@ -265,9 +323,15 @@ class RegTR(nn.Module):
         return outputs
 
     def _segments(self, slens_c, xyz_c):
-        n_layers = (0 if isinstance(self.correspondence_decoder, CorrespondenceRegressor)
-                    else len(self.transformer_encoder.layers))
-        return Segments(slens_c, xyz_c.device, n_layers)
+        dec = self.correspondence_decoder
+        n_layers = 0 if isinstance(dec, CorrespondenceRegressor) else len(self.transformer_encoder.layers)
+        phantoms = None
+        if getattr(dec, 'num_neighbors', 0) > 0:
+            # top-k masking on a padded batch: one query-only row per padded cloud
+            B = len(slens_c) // 2
+            mx = (max(slens_c[:B]), max(slens_c[B:]))
+            phantoms = [int(n < mx[c >= B]) for c, n in enumerate(slens_c)]
+        return Segments(slens_c, xyz_c.device, n_layers, phantoms=phantoms)
 
     def _core(self, meta, seg, B):
         """The post-preprocessing forward (finegrained_regtr.py:126-218): encoder, feat_proj,
@@ -283,12 +347,22 @@ class RegTR(nn.Module):
         pos = pe if self.cfg.transformer_encoder_has_pos_emb else None
         if pos is None:
             pos = torch.zeros_like(both)
-        feats = self.transformer_encoder.forward_packed(both, pos, seg)        # (L, N, d)
+        if seg.n_phantom:
+            # the reference's padded positions that feed the decoder's top-k union: input
+            # features and positional embedding are its zero padding (finegrained_regtr.py:
+            # 163-171)
+            z = both.new_zeros((seg.n_phantom, both.shape[1]))
+            feats = self.transformer_encoder.forward_packed(torch.cat([both, z]),
+                                                            torch.cat([pos, z]), seg)
+        else:
+            feats = self.transformer_encoder.forward_packed(both, pos, seg)    # (L, N, d)
         if isinstance(self.correspondence_decoder, CorrespondenceRegressor):
             corr, logits = self.correspondence_decoder.forward_packed(feats)
         else:
             corr, logits = self.correspondence_decoder.forward_packed(feats, xyz_c, pe, seg)
-        pose = ops.pair_pose(xyz_c, corr, logits[..., 0], seg.off, B, self.pose_threshold)
+        if seg.n_phantom:                  # drop the query-only phantom rows (_segments)
+            feats, corr, logits = (t[:, :xyz_c.shape[0]].contiguous() for t in (feats, corr, logits))
+        pose = ops.pair_pose(xyz_c, corr, logits[..., 0], seg.cloud_off, B, self.pose_threshold)
         return both, feats, corr, logits, pose
 
     def _apply(self, fn, *args, **kwargs):

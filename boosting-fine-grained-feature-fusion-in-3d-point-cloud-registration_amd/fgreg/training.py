@@ -154,6 +154,6 @@ def core_train(model, meta, seg, B):
         logits = linear_t(f, head.conf_logits_decoder.weight, head.conf_logits_decoder.bias)
     corr, logits = corr.view(L, N, 3), logits.view(L, N, 1)
     with torch.no_grad():
-        pose = ops.pair_pose(xyz_c, corr.detach(), logits.detach()[..., 0], seg.off, B,
+        pose = ops.pair_pose(xyz_c, corr.detach(), logits.detach()[..., 0], seg.cloud_off, B,
                              model.pose_threshold)
     return both, feats, corr, logits, pose

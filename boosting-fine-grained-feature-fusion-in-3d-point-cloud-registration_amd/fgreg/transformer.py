@@ -38,28 +38,42 @@ class Segments:
     """Device-side segment tables of one packed batch of 2B clouds (built before any graph
     capture: they are host -> device copies)."""
 
-    def __init__(self, lengths, device, n_layers=0):
+    def __init__(self, lengths, device, n_layers=0, phantoms=None):
+        """``phantoms``: optional per-cloud counts of query-only rows appended after the 2B
+        clouds' rows, grouped by cloud (the reference's padded positions, which it computes as
+        queries of every attention and never as keys: CorrespondenceDecoder top-k masking on
+        padded batches, finegrained_regtr.py:353-357). Each non-empty group is one more
+        segment whose key segment is its cloud (self-attention) or the partner (cross);
+        ``cloud_off`` = ``off[:2B + 1]`` is the clouds' own table."""
         self.lengths = [int(n) for n in lengths]
         n = len(self.lengths)
         assert n % 2 == 0
         self.B = n // 2
-        self.off = ops.offsets(self.lengths, device)
-        self.self_seg = torch.arange(n, dtype=torch.int32, device=device)
-        self.cross_seg = torch.tensor([(c + self.B) % n for c in range(n)], dtype=torch.int32,
-                                      device=device)
-        self.max_len = max(self.lengths) if n else 0
+        self.phantoms = [int(p) for p in phantoms] if phantoms is not None else [0] * n
+        assert len(self.phantoms) == n and min(self.phantoms, default=0) >= 0
+        # segment -> the cloud it belongs to (the clouds first, then the phantom groups)
+        self.seg_cloud = list(range(n)) + [c for c in range(n) if self.phantoms[c] > 0]
+        self.seg_lengths = self.lengths + [p for p in self.phantoms if p > 0]
+        self.n_phantom = sum(self.phantoms)
+        self.off = ops.offsets(self.seg_lengths, device)
+        self.cloud_off = self.off[:n + 1]
+        self.self_seg = torch.tensor(self.seg_cloud, dtype=torch.int32, device=device)
+        self.cross_seg = torch.tensor([(c + self.B) % n for c in self.seg_cloud],
+                                      dtype=torch.int32, device=device)
+        self.max_len = max(self.seg_lengths) if n else 0
         self.layer_tables = None
         if n_layers:
-            # (layer, cloud) segments of the L stacked layer outputs (L * N rows): segment
-            # l * 2B + c attends to l * 2B + partner(c); value rows = the partner's xyz rows
-            # built from the host lengths (reading self.off back would sync the stream)
-            N = sum(self.lengths)
+            # (layer, segment) segments of the L stacked layer outputs (L * N rows): segment
+            # l * S + s attends to l * S + partner(cloud of s); value rows = the partner's xyz
+            # rows, built from the host lengths (reading self.off back would sync the stream)
+            N = sum(self.seg_lengths)
+            S = len(self.seg_lengths)
             host_off = [0]
-            for ln in self.lengths[:-1]:
+            for ln in self.seg_lengths[:-1]:
                 host_off.append(host_off[-1] + ln)
             q_off = [l * N + o for l in range(n_layers) for o in host_off]
             q_off.append(n_layers * N)
-            kv_seg = [l * n + (c + self.B) % n for l in range(n_layers) for c in range(n)]
+            kv_seg = [l * S + (c + self.B) % n for l in range(n_layers) for c in self.seg_cloud]
             v_off = host_off * n_layers
             self.layer_tables = (torch.tensor(q_off, dtype=torch.int64, device=device),
                                  torch.tensor(kv_seg, dtype=torch.int32, device=device),

@@ -71,14 +71,14 @@ int fgr_time_next_call(void* start_event, void* end_event);
  * (cpp_subsampling/wrapper.cpp:62-333 -> grid_subsampling.cpp:5-211).
  * Voxel key and barycentre follow grid_subsampling.cpp bit for bit; voxels are
  * emitted in ascending key order per cloud, members summed in ascending point index.
- * `max_cells` selects the path: > 0 a counting sort over a dense voxel-key histogram of that
- * many counters (the clouds' key spaces nx*ny*nz laid end to end; 0 = the default
- * 8 n_points + 2^20), < 0 the radix-sort path (any key space). The same max_cells must be
+ * `max_cells`: a counting sort over a dense voxel-key histogram of that many counters (the
+ * clouds' key spaces nx*ny*nz laid end to end; 0 = the default 8 n_points + 2^20; < 0 is
+ * rejected: the round-1 radix-sort path was removed in round 5). The same max_cells must be
  * passed to all three calls.
  * 1) fgr_grid_subsample_count: writes counts[c] (voxels of cloud c) and
  *    counts[n_clouds] (total) as int64; keeps the sorted state in `ws`. Dense path only:
  *    if the key space exceeds max_cells, counts[n_clouds] = -(cells needed) and nothing else
- *    is valid -- call again with a larger max_cells (or -1).
+ *    is valid -- call again with a larger max_cells.
  * 2) fgr_grid_subsample_fill: writes out_points (total, 3) and optionally the
  *    voxel keys (total) from the same `ws` (must follow the count call). */
 int fgr_grid_subsample_workspace(int64_t n_points, int32_t n_clouds, int64_t max_cells,

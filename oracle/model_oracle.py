@@ -357,9 +357,12 @@ def weighted_procrustes(a, b, w, threshold=0.85):
 # Whole forward (models/finegrained_regtr.py:108-250)
 # ----------------------------------------------------------------------------------------
 @torch.no_grad()
-def forward(cfg, sd, src_xyz, tgt_xyz, meta=None, mode=geom.INDEX):
-    """The inference forward (eval(), no autograd)."""
-    return _forward(cfg, sd, src_xyz, tgt_xyz, meta, mode, train=False)
+def forward(cfg, sd, src_xyz, tgt_xyz, meta=None, mode=geom.INDEX, num_neighbors=0):
+    """The inference forward (eval(), no autograd). num_neighbors: the CorrespondenceDecoder's
+    top-k masking (a constructor argument the reference's RegTR never passes; on padded
+    batches its padded query rows take part as the reference computes them)."""
+    return _forward(cfg, sd, src_xyz, tgt_xyz, meta, mode, train=False,
+                    num_neighbors=num_neighbors)
 
 
 def forward_train(cfg, sd, src_xyz, tgt_xyz, meta=None, mode=geom.INDEX):
@@ -369,7 +372,7 @@ def forward_train(cfg, sd, src_xyz, tgt_xyz, meta=None, mode=geom.INDEX):
     return _forward(cfg, sd, src_xyz, tgt_xyz, meta, mode, train=True)
 
 
-def _forward(cfg, sd, src_xyz, tgt_xyz, meta, mode, train):
+def _forward(cfg, sd, src_xyz, tgt_xyz, meta, mode, train, num_neighbors=0):
     B = len(src_xyz)
     if meta is None:
         meta = preprocess(cfg, [np.asarray(c) for c in list(src_xyz) + list(tgt_xyz)], mode)
@@ -409,7 +412,8 @@ def _forward(cfg, sd, src_xyz, tgt_xyz, meta, mode, train):
                 + sd['correspondence_decoder.conf_logits_decoder.bias'])
 
     def simple_attention(query, key, value, kmask):                          # :328-363
-        return corr_simple_attention(sd, 'correspondence_decoder.', query, key, value, kmask)
+        return corr_simple_attention(sd, 'correspondence_decoder.', query, key, value, kmask,
+                                     num_neighbors)
 
     if cfg.get('direct_regress_coor', False):
         s_corr, t_corr = corr_mlp(s_cond), corr_mlp(t_cond)

@@ -479,16 +479,25 @@ def make_decoder_topk(fr):
       eq_k1    B = 1, one layer, 64 + 64 rows, k = 1: about a third of the rows NaN;
       b2_k6    B = 2, every cloud 48 rows (no padding), k = 6;
       ne_k8    B = 1, 40 src + 64 tgt rows, k = 8: records whether the reference raised
-               (an index >= 40 into the src query dim).
+               (an index >= 40 into the src query dim);
+      pad_k1   B = 2, one layer, src 24 / 48 and tgt 48 / 20 rows, k = 1: a padded batch, whose
+               padded query rows (random features here) feed the union;
+      pad_k2   B = 2, two layers, src 30 / 48 and tgt 48 / 26 rows, k = 2;
+      pad_ix   B = 2, two layers, src 30 / 48 and tgt 44 / 26 rows, k = 2: the reference raises
+               IndexError (a tgt query's top-k src index >= 44).
     Weights: nn.Linear default init under torch.manual_seed(20 + case), stored."""
     from transformer.position_embedding import PositionEmbeddingCoordsSine
-    arrays = {'cases': np.array(['eq_k4', 'eq_k24', 'eq_k1', 'b2_k6', 'ne_k8'])}
+    arrays = {'cases': np.array(['eq_k4', 'eq_k24', 'eq_k1', 'b2_k6', 'ne_k8', 'pad_k1',
+                                 'pad_k2', 'pad_ix'])}
     D = 32
     for ci, (name, L, ns, nt, k) in enumerate([('eq_k4', 3, [64], [64], 4),
                                                ('eq_k24', 3, [64], [64], 24),
                                                ('eq_k1', 1, [64], [64], 1),
                                                ('b2_k6', 3, [48, 48], [48, 48], 6),
-                                               ('ne_k8', 3, [40], [64], 8)]):
+                                               ('ne_k8', 3, [40], [64], 8),
+                                               ('pad_k1', 1, [24, 48], [48, 20], 1),
+                                               ('pad_k2', 2, [30, 48], [48, 26], 2),
+                                               ('pad_ix', 2, [30, 48], [44, 26], 2)]):
         torch.manual_seed(20 + ci)
         pe = PositionEmbeddingCoordsSine(3, D, scale=1.0)
         dec = fr.CorrespondenceDecoder(D, True, pe, num_neighbors=k).eval()

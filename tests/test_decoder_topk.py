@@ -7,7 +7,8 @@ tests/golden/decoder_topk.npz is the reference module's own output
 (tests/golden/make_golden.py make_decoder_topk). Checked here: the oracle's restatement
 (CPU) and the HIP path (fgr_corr_attention + fgr_corr_topk_mask, gpu): NaN rows identical,
 finite rows within 1e-4 normwise relative (the q / k projections are fp32-accurate f16x3
-GEMMs on the GPU).
+GEMMs on the GPU). Padded batches (pad_*): the reference's padded query rows feed the union;
+the HIP path carries them as query-only phantom rows (transformer.Segments(phantoms=...)).
 """
 import math
 
@@ -49,7 +50,10 @@ def test_fixture_has_nan_rows_and_a_raise():
     assert np.isnan(d['eq_k1.out.src_corr.0']).any()
 
 
-@pytest.mark.parametrize('case', ['eq_k4', 'eq_k24', 'eq_k1', 'b2_k6', 'ne_k8'])
+CASES = ['eq_k4', 'eq_k24', 'eq_k1', 'b2_k6', 'ne_k8', 'pad_k1', 'pad_k2', 'pad_ix']
+
+
+@pytest.mark.parametrize('case', CASES)
 def test_oracle_topk_matches_reference(case):
     d = golden(FIX)
     B, sd, sx, tx, sf, tf, k, raised = _case(d, case)
@@ -75,8 +79,28 @@ def test_oracle_topk_matches_reference(case):
         _check(tc[:, :n_t, b].numpy(), d[f'{case}.out.tgt_corr.{b}'])
 
 
+def test_padded_rows_change_the_union():
+    """pad_k1 discriminates: with the padded query rows left out of the union (what a packed
+    layout without phantom rows would compute) the NaN rows differ from the reference's."""
+    d = golden(FIX)
+    B, sd, sx, tx, sf, tf, k, _ = _case(d, 'pad_k1')
+    pe = lambda x: mo.sine_pos_embed(x, sf.shape[-1])          # noqa: E731
+    spe, _ = mo._pad([pe(x) for x in sx])
+    tpe, _ = mo._pad([pe(x) for x in tx])
+    sxp, smask = mo._pad(sx)
+    txp, tmask = mo._pad(tx)
+    q = sf + spe
+    q_real = q.clone()
+    for b in range(B):       # padded rows of src cloud b: copy a real row's top-k onto them
+        q_real[:, len(sx[b]):, b] = q[:, :1, b]
+    sc = mo.corr_simple_attention(sd, '', q_real, tf + tpe, txp, tmask, k)
+    differs = any(not np.array_equal(np.isnan(sc[:, :len(sx[b]), b].numpy()),
+                                     np.isnan(d[f'pad_k1.out.src_corr.{b}'])) for b in range(B))
+    assert differs
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize('case', ['eq_k4', 'eq_k24', 'eq_k1', 'b2_k6', 'ne_k8'])
+@pytest.mark.parametrize('case', CASES)
 def test_gpu_topk_matches_reference(gpu, case):
     import fgreg
     from fgreg.regtr import CorrespondenceDecoder
@@ -89,10 +113,15 @@ def test_gpu_topk_matches_reference(gpu, case):
     dec.load_state_dict(sd)
     dec = dec.to(gpu).eval()
     lens = [len(x) for x in sx] + [len(x) for x in tx]
+    Qs, Qt = sf.shape[1], tf.shape[1]
+    # the clouds' rows, then each padded cloud's padded rows as query-only phantom rows
+    phantoms = [Qs - n for n in lens[:B]] + [Qt - n for n in lens[B:]]
     feats = torch.cat([sf[:, :len(sx[b]), b] for b in range(B)]
-                      + [tf[:, :len(tx[b]), b] for b in range(B)], 1).contiguous().to(gpu)
+                      + [tf[:, :len(tx[b]), b] for b in range(B)]
+                      + [sf[:, len(sx[b]):, b] for b in range(B)]
+                      + [tf[:, len(tx[b]):, b] for b in range(B)], 1).contiguous().to(gpu)
     xyz = torch.cat(sx + tx, 0).contiguous().to(gpu)
-    seg = Segments(lens, gpu, n_layers=L)
+    seg = Segments(lens, gpu, n_layers=L, phantoms=phantoms)
     with torch.no_grad():
         pos = pe(xyz)
         if raised:
@@ -111,14 +140,36 @@ def test_gpu_topk_matches_reference(gpu, case):
 
 
 @pytest.mark.gpu
-def test_gpu_topk_padded_batch_raises(gpu):
-    from fgreg.regtr import CorrespondenceDecoder
-    from fgreg.transformer import PositionEmbeddingCoordsSine, Segments
-    D = 32
-    pe = PositionEmbeddingCoordsSine(3, D)
-    dec = CorrespondenceDecoder(D, True, pe, num_neighbors=2).to(gpu).eval()
-    lens = [30, 31, 30, 30]
-    xyz = torch.rand(sum(lens), 3, device=gpu)
-    feats = torch.randn(1, sum(lens), D, device=gpu)
-    with torch.no_grad(), pytest.raises(NotImplementedError):
-        dec.forward_packed(feats, xyz, pe(xyz), Segments(lens, gpu, n_layers=1))
+@pytest.mark.parametrize('k', [1, 3])
+def test_gpu_forward_topk_padded_batch_vs_oracle(gpu, k):
+    """A whole RegTR forward with the CorrespondenceDecoder's top-k masking on a padded batch
+    (the decoder fixture's two ModelNet pairs, whose coarse clouds differ in length) against
+    the oracle, which runs the reference's padded transformer and decoder: NaN rows
+    identical, finite rows within 1e-4; an IndexError of the oracle is raised too."""
+    import fgreg
+    from conftest import forward_fixture
+    cfg, sd, src, tgt, _, _ = forward_fixture('forward_modelnet_decoder')
+    model = fgreg.RegTR(cfg)
+    model.load_state_dict(sd, strict=False)
+    model.correspondence_decoder.num_neighbors = k
+    model = model.to(gpu).eval()
+    batch = {'src_xyz': [torch.from_numpy(c).to(gpu) for c in src],
+             'tgt_xyz': [torch.from_numpy(c).to(gpu) for c in tgt]}
+    try:
+        ref = mo.forward(cfg, sd, src, tgt, mode=mo.geom.INDEX, num_neighbors=k)
+    except IndexError:
+        with pytest.raises(IndexError):
+            model(batch)
+        return
+    out = model(batch)
+    lens = batch['kpconv_meta']['stack_lengths'][-1].tolist()
+    B = len(src)
+    assert len(set(lens[:B])) > 1 or len(set(lens[B:])) > 1, 'the batch must be padded'
+    n_nan = 0
+    for b in range(B):
+        for side in ('src', 'tgt'):
+            _check(out[f'{side}_kp_warped'][b].cpu().numpy(), ref[f'{side}_kp_warped'][b].numpy())
+            n_nan += int(np.isnan(ref[f'{side}_kp_warped'][b].numpy()).any(-1).sum())
+            assert rel_err(out[f'{side}_overlap'][b], ref[f'{side}_overlap'][b]) < 1e-4
+            assert rel_err(out[f'{side}_feat'][b], ref[f'{side}_feat'][b]) < 1e-4
+    print(f'\nk={k}: lengths {lens}, {n_nan} NaN rows in the reference restatement')

@@ -232,22 +232,36 @@ def test_radius_grid_matches_bruteforce_and_oracle(gpu, mode):
             assert torch.equal(c1, c2) and m1 == m2, name
 
 
-def test_grid_subsample_dense_matches_radix(gpu):
-    """The dense counting-sort path gives the radix-sort path's voxels bit for bit (order,
-    barycentres, keys), also after a key-space overflow retry (tiny max_cells)."""
+def test_grid_subsample_overflow_retry(gpu):
+    """A key space past the histogram (tiny max_cells) is reported and the count redone with
+    the needed capacity: the same voxels bit for bit (order, barycentres, keys) as the default
+    capacity and as the oracle; max_cells < 0 (the removed radix path) is rejected."""
     import fgreg.ops as ops
+    from fgreg._lib import FgrError
     for name, P, L, r in _grid_cases():
         pd = torch.from_numpy(P).to(gpu)
         lens, off = _lens_off(L, gpu)
         for dl in (0.4 * r, 0.8 * r):
             a = ops.grid_subsample(pd, off, lens, dl, return_keys=True)
-            b = ops.grid_subsample(pd, off, lens, dl, return_keys=True, max_cells=-1)
             c = ops.grid_subsample(pd, off, lens, dl, return_keys=True, max_cells=16)
-            for x in (b, c):
-                assert x[1] == a[1] and torch.equal(x[0], a[0]) and torch.equal(x[2], a[2]), name
+            assert c[1] == a[1] and torch.equal(c[0], a[0]) and torch.equal(c[2], a[2]), name
             o_pts, o_lens, o_keys = og.grid_subsample(P, L, dl, return_keys=True)
             assert a[1] == o_lens.tolist() and np.array_equal(a[0].cpu().numpy(), o_pts)
             assert np.array_equal(a[2].cpu().numpy(), o_keys)
+    with pytest.raises(FgrError):
+        ops.grid_subsample(pd, off, lens, 0.4 * r, max_cells=-1)
+
+
+def test_grid_subsample_key_space_limit_raises(gpu):
+    """Past 2^28 voxel cells (a 645-voxel cube per cloud) the dense path raises instead of
+    allocating a larger histogram."""
+    import fgreg.ops as ops
+    from fgreg._lib import FgrError
+    P = np.array([[0, 0, 0], [1000, 1000, 1000]], np.float32)
+    pd = torch.from_numpy(P).to(gpu)
+    lens, off = _lens_off([2], gpu)
+    with pytest.raises(FgrError, match='key space'):
+        ops.grid_subsample(pd, off, lens, 1.0)
 
 
 @pytest.mark.parametrize('n', [0, 1, 2, 16, 64, 65, 300])
