@@ -344,6 +344,7 @@ def main():
         return time.perf_counter() - t0
 
     from fgreg import regtr as fregtr
+    fpipe = sys.modules['fgreg.pipeline']            # the module (fgreg.pipeline is the function)
     with torch.no_grad():
         # >= 2 warmup steps: the second sighting of the batch's shape signature captures the
         # HIP graph of the post-preprocessing forward (fgreg/regtr.py), replayed from then on
@@ -367,6 +368,15 @@ def main():
             ops.TIMER = None
             # timed region: nothing instrumented (graph replay of the core forward)
             elapsed = timed(args.steps)
+            # one forward at a time (back-to-back model(batch), graph replay): the latency of
+            # a step, reported beside the pipelined throughput
+            elapsed_seq = None
+            if not args.no_pipeline:
+                no_pipe, args.no_pipeline = args.no_pipeline, True
+                try:
+                    elapsed_seq = timed(args.steps)
+                finally:
+                    args.no_pipeline = no_pipe
             # the same steps with the HIP-graph cache off (every launch eager): what inputs
             # whose shape signature never repeats get, reported beside `value`
             fregtr.GRAPHS = False
@@ -415,8 +425,16 @@ def main():
                                  'cache; preprocessing eager' if fregtr.GRAPHS else 'off'),
                    'pipeline': ('off: back-to-back model(batch) calls' if args.no_pipeline else
                                 'fgreg.pipeline: every step is a full forward; step i + 1\'s '
-                                'preprocessing runs on a side stream while step i\'s core runs')},
+                                'preprocessing runs on a side stream while step i\'s core runs; '
+                                f'consecutive cores alternate over {fpipe.STREAMS} core streams '
+                                '(one HIP-graph instance each), so their launches overlap')},
     }
+    if not args.profile and elapsed_seq is not None:
+        line['sequential'] = {
+            'value': n_total * args.steps / elapsed_seq, 'unit': 'pairs/s',
+            'ms_per_step': elapsed_seq / args.steps * 1e3,
+            'what': 'the same steps one forward at a time (back-to-back model(batch), graph '
+                    'replay, no overlap of consecutive forwards): the per-batch latency'}
     if not args.profile:
         line['eager'] = {
             'value': n_total * args.steps / elapsed_eager, 'unit': 'pairs/s',

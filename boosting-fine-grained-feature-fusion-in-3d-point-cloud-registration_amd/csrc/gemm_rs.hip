@@ -129,6 +129,10 @@ __device__ __forceinline__ void wait_vm_lgkm0_dyn(int n) {
 
 constexpr int kRsNb = 3;           // W panels in the LDS ring (two in flight while one computes)
 constexpr int kRsMaxNc = 64;       // panels per block (the per-block column scales / bias in LDS)
+#ifndef FGR_RS_LA
+#define FGR_RS_LA 4
+#endif
+constexpr int kRsLookahead = FGR_RS_LA;   // k-steps of W fragments read ahead of their MFMAs
 
 // the epilogue of one output, the activation fixed at compile time
 template <int ACT, bool RES>
@@ -431,16 +435,45 @@ __global__ void __launch_bounds__(256, KV ? 2 : 1) gemm_rs_kernel(RsArgs p) {
                               (uint32_t)(g * 16 + c) * 16;
 #pragma unroll
         for (int i = 0; i < RT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        // the fragments of RS_LA k-steps are read ahead of their MFMAs, pinned in that order by
+        // sched_group_barrier (left to itself the scheduler issued each ds_read right before
+        // its MFMA with an lgkmcnt(0) wait in between: one exposed LDS latency per k-step)
+        // (K <= 128: none -- the extra registers cost occupancy there, 4 blocks per CU:
+        // 11472 x 896 x 128 24.4 -> 27.9 us with it, profiles/r05_rs_lookahead_ab.txt)
+        constexpr int LA_ = KS <= 4 ? 0 : (KS < kRsLookahead ? KS : kRsLookahead);
+        if constexpr (LA_ == 0) {
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+                const f16x8 wh = __builtin_bit_cast(f16x8, *(lds_u4*)(uintptr_t)(base + (s * 2 + 0) * 64 * 16));
+                const f16x8 wl = __builtin_bit_cast(f16x8, *(lds_u4*)(uintptr_t)(base + (s * 2 + 1) * 64 * 16));
+#pragma unroll
+                for (int i = 0; i < RT; ++i) {
+                    acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, af[i][s][0], acc[i], 0, 0, 0);
+                    acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, af[i][s][1], acc[i], 0, 0, 0);
+                    acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, af[i][s][0], acc[i], 0, 0, 0);
+                }
+            }
+            return;
+        }
+        f16x8 wf[KS][2];
+        auto rd = [&](int s) {
+            wf[s][0] = __builtin_bit_cast(f16x8, *(lds_u4*)(uintptr_t)(base + (s * 2 + 0) * 64 * 16));
+            wf[s][1] = __builtin_bit_cast(f16x8, *(lds_u4*)(uintptr_t)(base + (s * 2 + 1) * 64 * 16));
+        };
+#pragma unroll
+        for (int s = 0; s < LA_; ++s) rd(s);
+        __builtin_amdgcn_sched_group_barrier(0x100, 2 * (LA_ > 0 ? LA_ : 1), 0);   // DS reads
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
-            const f16x8 wh = __builtin_bit_cast(f16x8, *(lds_u4*)(uintptr_t)(base + (s * 2 + 0) * 64 * 16));
-            const f16x8 wl = __builtin_bit_cast(f16x8, *(lds_u4*)(uintptr_t)(base + (s * 2 + 1) * 64 * 16));
+            if (s + LA_ < KS) rd(s + LA_);
 #pragma unroll
             for (int i = 0; i < RT; ++i) {
-                acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, af[i][s][0], acc[i], 0, 0, 0);
-                acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, af[i][s][1], acc[i], 0, 0, 0);
-                acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, af[i][s][0], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[s][1], af[i][s][0], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[s][0], af[i][s][1], acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[s][0], af[i][s][0], acc[i], 0, 0, 0);
             }
+            if (s + LA_ < KS) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // next reads
+            __builtin_amdgcn_sched_group_barrier(0x008, 3 * RT, 0);                // this step's MFMAs
         }
     };
     // panel q's epilogue: lane holds C[row = mw + 16i + c][n .. n + 3]
@@ -535,9 +568,13 @@ __global__ void __launch_bounds__(256, KV ? 2 : 1) gemm_rs_kernel(RsArgs p) {
         // too is merely stricter], DMA of panel q + 1 if any, and its epilogue stores (panel
         // q - 2)
         static_assert(LA == 2, "the wait counts below assume two panels in flight");
+#if defined(FGR_RS_WAIT0)
+        wait_vm_lgkm0_rs<0>();
+#else
         if (q == 0) wait_vm_lgkm0_dyn(np > 1 ? PW : 0);
         else wait_vm_lgkm0_dyn((q >= 3 ? nstore(q - 3) : 0) + (q >= 2 ? nstore(q - 2) : 0) +
                                (q + 1 < np ? PW : 0));
+#endif
         __builtin_amdgcn_s_barrier();                    // every wave's pieces; buffer of q - 1 free
 #ifdef FGR_RS_STAMP
         if (q == 0) st_[3] = __builtin_amdgcn_s_memtime();

@@ -10,10 +10,17 @@ enqueues the rest of the preprocessing.
 
 ``depth`` cores are kept enqueued ahead of the output being yielded (default 2): the
 preprocessing of batch i + 2 runs (with its host readbacks) while the cores of batches i and
-i + 1 are both queued on the current stream, so the GPU does not idle when a preprocessing
-takes longer than one core (the 20k-point workloads). depth = 1 is the one-ahead pipeline.
+i + 1 are both queued, so the GPU does not idle when a preprocessing takes longer than one
+core (the 20k-point workloads). depth = 1 is the one-ahead pipeline.
 Graph replays clone their outputs (fgreg.regtr._CoreGraph.run), so an output stays valid
 while the next core runs.
+
+``streams`` core streams (default 2, FGREG_PIPE_STREAMS): core i runs on core stream
+i mod streams (dedicated streams; streams = 1: the current stream), each replaying its own instance of
+the shape signature's HIP graph (RegTR._forward(slot=...)), so consecutive cores overlap on
+the GPU: the drain / ramp of every one of a core's ~300 dependent launches (a few us each)
+is filled by the other core's kernels. Each core is still one whole forward of its batch;
+its outputs are made visible to the current stream (an event wait) before they are yielded.
 
 Ordering contract (no extra synchronisation needed by the caller):
   * batch i + 1 is drawn from the iterator BEFORE batch i's core is enqueued, and the side
@@ -34,6 +41,7 @@ import torch
 from .regtr import RegTR
 
 DEPTH = int(os.environ.get('FGREG_PIPE_DEPTH', '2'))
+STREAMS = int(os.environ.get('FGREG_PIPE_STREAMS', '2'))
 
 
 def _meta_tensors(meta):
@@ -45,27 +53,39 @@ def _meta_tensors(meta):
         yield t
 
 
-def _prepare(model, batch, side, ready):
-    main = torch.cuda.current_stream()
+def _prepare(model, batch, side, ready, users):
     with torch.cuda.stream(side):
         side.wait_event(ready)
         meta = model._prepare(batch)
         done = torch.cuda.Event()
         done.record(side)
     for t in _meta_tensors(meta):
-        t.record_stream(main)
+        for st in users:
+            t.record_stream(st)
     for t in list(batch['src_xyz']) + list(batch['tgt_xyz']):
         t.record_stream(side)
     return meta, done
 
 
-def pipeline(model: RegTR, batches, depth=None):
+def _out_tensors(out):
+    for v in out.values():
+        if torch.is_tensor(v):
+            yield v
+        elif isinstance(v, (list, tuple)):
+            for t in v:
+                if torch.is_tensor(t):
+                    yield t
+
+
+def pipeline(model: RegTR, batches, depth=None, streams=None):
     """Yields model(batch) for each batch of ``batches`` (an iterable of forward() batch
     dicts on one device), preprocessing later batches while earlier cores run (``depth``
-    cores in flight ahead of the yielded output; default DEPTH = FGREG_PIPE_DEPTH or 2)."""
+    cores in flight ahead of the yielded output; default DEPTH = FGREG_PIPE_DEPTH or 2) on
+    ``streams`` core streams (default STREAMS = FGREG_PIPE_STREAMS or 2)."""
     if model.training and torch.is_grad_enabled():
         raise NotImplementedError('fgreg.pipeline is inference only (eval() / no_grad)')
     depth = max(1, int(DEPTH if depth is None else depth))
+    n_streams = max(1, int(STREAMS if streams is None else streams))
     it = iter(batches)
     first = next(it, None)
     if first is None:
@@ -76,6 +96,10 @@ def pipeline(model: RegTR, batches, depth=None):
     with torch.no_grad(), torch.cuda.device(dev):
         side = torch.cuda.Stream(dev)
         main = torch.cuda.current_stream()
+        # several core streams: all of them dedicated (a core on the current stream would queue
+        # behind the waits that make earlier outputs visible to the caller, serialising it
+        # with the core before it)
+        cores = [main] if n_streams == 1 else [torch.cuda.Stream(dev) for _ in range(n_streams)]
 
         def draw():
             """the next batch and an event recorded now, before any later core is enqueued"""
@@ -86,18 +110,33 @@ def pipeline(model: RegTR, batches, depth=None):
             ready.record()
             return b, ready
 
+        def finish(out, st):
+            """the core's outputs, visible to (and owned by) the current stream"""
+            if st is not main:
+                ev = torch.cuda.Event()
+                ev.record(st)
+                main.wait_event(ev)
+                for t in _out_tensors(out):
+                    t.record_stream(main)
+            return out
+
         ready = torch.cuda.Event()
         ready.record()
-        prepared = deque([(first,) + _prepare(model, first, side, ready)])
+        prepared = deque([(first,) + _prepare(model, first, side, ready, cores)])
         outs = deque()
+        i = 0
         while prepared:
             while prepared and len(outs) < depth:
                 b, meta, done = prepared.popleft()
                 item = draw()                       # before b's core is enqueued
-                main.wait_event(done)
-                outs.append(model._forward(b, meta))
+                st = cores[i % n_streams]
+                st.wait_event(done)
+                with torch.cuda.stream(st):
+                    out = model._forward(b, meta, slot=i % n_streams)
+                outs.append((out, st))
+                i += 1
                 if item is not None:
-                    prepared.append((item[0],) + _prepare(model, item[0], side, item[1]))
-            yield outs.popleft()
+                    prepared.append((item[0],) + _prepare(model, item[0], side, item[1], cores))
+            yield finish(*outs.popleft())
         while outs:
-            yield outs.popleft()
+            yield finish(*outs.popleft())

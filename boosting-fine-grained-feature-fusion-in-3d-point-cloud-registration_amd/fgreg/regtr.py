@@ -282,9 +282,12 @@ class RegTR(nn.Module):
             host_layout(meta, lvl)
         return meta
 
-    def _forward(self, batch, meta=None, train=False):
+    def _forward(self, batch, meta=None, train=False, slot=0):
         """meta: a kpconv_meta already prepared for this batch (fgreg.pipeline), else built
-        here. train: the training-mode core (fgreg/training.py) instead of the inference one."""
+        here. train: the training-mode core (fgreg/training.py) instead of the inference one.
+        slot: which of the shape signature's graph instances replays the core (fgreg.pipeline
+        runs consecutive cores on different streams: each stream replays its own instance, so
+        concurrent replays never share scratch buffers or static inputs)."""
         B = len(batch['src_xyz'])
         if meta is None:
             with torch.no_grad():
@@ -297,7 +300,7 @@ class RegTR(nn.Module):
             from .training import core_train
             res = core_train(self, meta, self._segments(slens_c, xyz_c), B)
         else:
-            core = (_graph_for(self, meta, slens_c, B)
+            core = (_graph_for(self, meta, slens_c, B, slot)
                     if GRAPHS and xyz_c.is_cuda and ops.TIMER is None else None)
             res = core.run(meta) if core is not None else self._core(
                 meta, self._segments(slens_c, xyz_c), B)
@@ -385,7 +388,7 @@ class RegTR(nn.Module):
 # update (version change), load_state_dict or .to() drops the model's graphs.
 # FGREG_GRAPHS=0 disables the path (A/B).
 GRAPHS = os.environ.get('FGREG_GRAPHS', '1') != '0'
-GRAPH_CACHE = 8
+GRAPH_CACHE = 16       # per model, over (stream slot, signature)
 SEEN_CACHE = 4096        # signatures remembered for the capture-on-second-sighting rule (LRU)
 _GRAPHS = weakref.WeakKeyDictionary()        # model -> {'ver', 'seen', 'graphs'}
 _META_IN = ('points', 'neighbors', 'pools')  # what the core reads (upsamples: decoder only)
@@ -432,14 +435,15 @@ def _params_version(model):
     return sum(p._version for p in plist), plist
 
 
-def _graph_for(model, meta, slens_c, B):
+def _graph_for(model, meta, slens_c, B, slot=0):
     ver, plist = _params_version(model)
     st = _GRAPHS.get(model)
     if st is None or st['ver'] != ver:
         st = {'ver': ver, 'params': plist, 'seen': OrderedDict(), 'graphs': OrderedDict()}
         _GRAPHS[model] = st
     from . import linear as _lin
-    sig = (B, _lin.MODE, HEAD_MODE, ops.ATTN_MODE, tuple(tuple(l) for l in meta['_host']['lengths']),
+    sig = (slot, B, _lin.MODE, HEAD_MODE, ops.ATTN_MODE,
+           tuple(tuple(l) for l in meta['_host']['lengths']),
            tuple(tuple(t.shape) for t in meta['neighbors']), tuple(tuple(t.shape) for t in meta['pools']))
     g = st['graphs'].get(sig)
     if g is not None:

@@ -1,6 +1,6 @@
 """fgreg.pipeline (preprocessing of later batches on a side stream while earlier cores run,
-1-3 cores in flight) yields exactly model(batch) for every batch: same kernels, same order
-of operations."""
+1-3 cores in flight, on 1-3 core streams) yields exactly model(batch) for every batch: same
+kernels, same order of operations."""
 import numpy as np
 import pytest
 import torch
@@ -27,28 +27,29 @@ def _same(a, b):
             assert torch.equal(x, y), k
 
 
-@pytest.mark.parametrize('depth', [1, 2, 3])
+@pytest.mark.parametrize('depth,streams', [(1, 1), (2, 1), (3, 1), (2, 2), (3, 3), (3, 2)])
 @pytest.mark.parametrize('kind', ['modelnet', '3dmatch'])
-def test_pipeline_equals_sequential(gpu, kind, depth):
+def test_pipeline_equals_sequential(gpu, kind, depth, streams):
     import fgreg
     torch.manual_seed(0)
     np.random.seed(0)
     model = fgreg.RegTR(fgreg.config.get(kind)).to(gpu).eval()
     P = 2 if kind == 'modelnet' else 1
-    # two shape signatures, each seen three times (the graph path captures on the second)
-    sizes = [(0, P), (5, P), (0, P), (5, P), (0, P), (5, P)]
+    # two shape signatures, each seen six times (the graph path captures on the second
+    # sighting per stream slot)
+    sizes = [(0, P), (5, P)] * 6
     batches = _batches(kind, gpu, sizes)
     with torch.no_grad():
         ref = [model(dict(b)) for b in batches]
-    got = list(fgreg.pipeline(model, [dict(b) for b in batches], depth=depth))
+    got = list(fgreg.pipeline(model, [dict(b) for b in batches], depth=depth, streams=streams))
     torch.cuda.synchronize()
     assert len(got) == len(ref)
     for a, b in zip(got, ref):
         _same(a, b)
 
 
-@pytest.mark.parametrize('depth', [1, 2])
-def test_pipeline_inputs_produced_on_the_current_stream(gpu, depth):
+@pytest.mark.parametrize('depth,streams', [(1, 1), (2, 1), (2, 2)])
+def test_pipeline_inputs_produced_on_the_current_stream(gpu, depth, streams):
     """Inputs written by the caller on the current stream right before each draw are read
     by the side-stream preprocessing only after that write (the ready event)."""
     import fgreg
@@ -67,7 +68,26 @@ def test_pipeline_inputs_produced_on_the_current_stream(gpu, depth):
                     d.copy_(s)
             yield b
     n = 0
-    for out in fgreg.pipeline(model, gen(), depth=depth):
+    for out in fgreg.pipeline(model, gen(), depth=depth, streams=streams):
         _same(out, ref)
         n += 1
     assert n == 4
+
+
+def test_pipeline_outputs_usable_on_the_current_stream(gpu):
+    """Cores on the second stream: their outputs are complete for work the caller enqueues on
+    the current stream right after the yield, and stay valid while later cores run."""
+    import fgreg
+    torch.manual_seed(2)
+    model = fgreg.RegTR(fgreg.config.get('modelnet')).to(gpu).eval()
+    batches = _batches('modelnet', gpu, [(0, 2), (3, 2)] * 4)
+    with torch.no_grad():
+        ref = [model(dict(b)) for b in batches]
+    sums, kept = [], []
+    for out in fgreg.pipeline(model, [dict(b) for b in batches], depth=3, streams=2):
+        sums.append(out['pose'].sum())              # enqueued on the current stream at once
+        kept.append(out)
+    torch.cuda.synchronize()
+    for s, out, r in zip(sums, kept, ref):
+        assert torch.equal(s, r['pose'].sum())
+        _same(out, r)
