@@ -167,12 +167,14 @@ def _cpu_model():
 
 def train_main(args):
     """ms per training step of the workload's batch on one GPU (trainer.py:110-125: forward,
-    loss.backward(), clip_grad_norm_, optimizer.step()). The reference's loss modules are not
-    part of the path (they stay the reference's own in the drop-in); the objective here is a
-    fixed random linear functional of every differentiable output (warped keypoints, overlap
-    logits, per-layer and un-projected features), so every parameter receives a gradient."""
+    compute_loss, loss.backward(), clip_grad_norm_, optimizer.step()). The loss is the
+    reference's compute_loss (finegrained_regtr.py:252-309) as a differentiable graph
+    (fgreg.loss.compute_loss_train: overlap BCE, InfoNCE on the match logits, correspondence
+    MAE, the reference's weights) against the synthetic pairs' ground-truth poses and
+    per-point overlap flags."""
     import fgreg
     from fgreg import linear as lin
+    from fgreg.loss import compute_loss_train
     from fgreg.synthetic import make_batch
     dev = torch.device('cuda', 0)
     torch.cuda.set_device(dev)
@@ -184,29 +186,20 @@ def train_main(args):
     model = fgreg.RegTR(cfg).to(dev).train()
     P = args.pairs_per_gpu or PAIRS[wl]
     kind = {'raw2048': 'modelnet_raw'}.get(wl, wl)
-    src, tgt, _ = make_batch(kind, P)
+    src, tgt, pose_gt = make_batch(kind, P)
+    flags = [_overlap_flags(a, b, p) for a, b, p in zip(src, tgt, pose_gt)]
     batch = {'src_xyz': [torch.from_numpy(a).to(dev) for a in src],
-             'tgt_xyz': [torch.from_numpy(b).to(dev) for b in tgt]}
+             'tgt_xyz': [torch.from_numpy(b).to(dev) for b in tgt],
+             'pose': torch.from_numpy(np.asarray(pose_gt, np.float32)).to(dev),
+             'src_overlap': [torch.from_numpy(f[0]).to(dev) for f in flags],
+             'tgt_overlap': [torch.from_numpy(f[1]).to(dev) for f in flags]}
     params = [p for p in model.parameters() if p.requires_grad]
     opt = torch.optim.AdamW(params, lr=1e-4, weight_decay=1e-4, foreach=True)
-    gen = torch.Generator(device=dev).manual_seed(1)
-    coef = {}
-
-    def objective(out):
-        tot = torch.zeros((), device=dev)
-        for key in ('src_kp_warped', 'tgt_kp_warped', 'src_overlap', 'tgt_overlap', 'src_feat',
-                    'tgt_feat', 'src_feat_un', 'tgt_feat_un'):
-            for i, t in enumerate(out[key]):
-                c = coef.get((key, i))
-                if c is None:
-                    c = coef[(key, i)] = torch.randn(t.shape, device=dev, generator=gen) / t.numel() ** 0.5
-                tot = tot + (t * c).sum()
-        return tot
 
     def step(split=None):
         opt.zero_grad(set_to_none=True)
         out = model(batch)
-        loss = objective(out)
+        loss = compute_loss_train(model, out, batch)['total']
         if split is not None:
             split[0].record()
         loss.backward()
@@ -234,10 +227,10 @@ def train_main(args):
             'pairs_per_s': P * args.steps / elapsed, 'dtype': DTYPE[lin.MODE],
             'data': DATA[wl], 'config': {'workload': WORKLOAD[wl].format(P=P), 'pairs_per_gpu': P,
                                          'precision': fgreg.precision(), 'mode': 'train()'},
-            'what': 'train() forward (Res2Net BatchNorm on batch statistics) + backward of a fixed '
-                    'random linear functional of every output + clip_grad_norm_(0.1) + AdamW '
-                    'step (torch foreach); eager launches (no HIP graph in training); gradients '
-                    'deterministic (no floating-point atomics)'}
+            'what': 'train() forward (Res2Net BatchNorm on batch statistics) + the reference\'s '
+                    'compute_loss (fgreg.loss.compute_loss_train) + backward + '
+                    'clip_grad_norm_(0.1) + AdamW step (torch foreach); eager launches (no HIP '
+                    'graph in training); gradients deterministic (no floating-point atomics)'}
     if not args.profile:
         # forward / backward split of extra steps (events around backward)
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]

@@ -931,8 +931,31 @@ __global__ void weight_scale_kernel(const float* __restrict__ w, int n, int k, i
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (row >= npad) return;
     float mx = 0.f;
-    if (row < n)
-        for (int j = lane; j < k; j += 64) mx = fmaxf(mx, fabsf(w[(int64_t)row * sn + j * sk]));
+    if (row < n) {
+        const float* wr = w + (int64_t)row * sn;
+        if (sk == 1 && k % 4 == 0 && (reinterpret_cast<uintptr_t>(wr) & 15) == 0) {
+            // contiguous rows: 16-B loads, four in flight per lane (a row of the long-K KPConv
+            // weights is 3840 floats: the scalar loop below waited on ~60 dependent trips)
+            const float4* p = reinterpret_cast<const float4*>(wr);
+            const int k4 = k / 4;
+            float m1 = 0.f, m2 = 0.f, m3 = 0.f;
+            int j = lane;
+            for (; j + 192 < k4; j += 256) {
+                const float4 a = p[j], b = p[j + 64], c = p[j + 128], d = p[j + 192];
+                mx = fmaxf(mx, fmaxf(fmaxf(fabsf(a.x), fabsf(a.y)), fmaxf(fabsf(a.z), fabsf(a.w))));
+                m1 = fmaxf(m1, fmaxf(fmaxf(fabsf(b.x), fabsf(b.y)), fmaxf(fabsf(b.z), fabsf(b.w))));
+                m2 = fmaxf(m2, fmaxf(fmaxf(fabsf(c.x), fabsf(c.y)), fmaxf(fabsf(c.z), fabsf(c.w))));
+                m3 = fmaxf(m3, fmaxf(fmaxf(fabsf(d.x), fabsf(d.y)), fmaxf(fabsf(d.z), fabsf(d.w))));
+            }
+            for (; j < k4; j += 64) {
+                const float4 a = p[j];
+                mx = fmaxf(mx, fmaxf(fmaxf(fabsf(a.x), fabsf(a.y)), fmaxf(fabsf(a.z), fabsf(a.w))));
+            }
+            mx = fmaxf(fmaxf(mx, m1), fmaxf(m2, m3));
+        } else {
+            for (int j = lane; j < k; j += 64) mx = fmaxf(mx, fabsf(wr[(int64_t)j * sk]));
+        }
+    }
     mx = wave_max(mx);
     if (lane == 0) {
         const int e = mx > 0.f ? min(15 - __builtin_amdgcn_frexp_expf(mx), 127) : 0;

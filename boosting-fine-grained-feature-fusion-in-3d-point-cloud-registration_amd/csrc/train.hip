@@ -27,6 +27,7 @@
 #include "common.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace fgr {
 namespace {
@@ -709,6 +710,235 @@ attn_bwd_dkdv_kernel(AttnBwd a) {
     }
 }
 
+// ---- attention backward on the fp32 matrix cores (head dim 16 / 32 / 64; round 5) -----------
+// The same two-kernel split as above, as tiled v_mfma_f32_16x16x4_f32 products (exact fp32
+// products, fp32 accumulation: the precision of the scalar kernels, ~6-10x their speed on the
+// forward's shapes). A wave owns 16 rows of its side (kernel 1: queries; kernel 2: keys), a
+// 256-thread block 64; the other side streams through LDS in tiles of 64 rows.
+// Lane maps of the 16x16x4 product (lane l, g = l >> 4, c = l & 15): A[i = c][k = g],
+// B[k = g][j = c], D[i = 4g + r][j = c]. The head-dim contraction pairs lane g with dims
+// g * KS + s at k-step s (KS = DH / 4), so a lane holds KS CONSECUTIVE dims of its row (vector
+// loads); the key / query contraction (dV, dK, dQ) pairs lane g with row 16n + 4g + r at k-step
+// (n, r) -- exactly the rows whose scores the lane holds after the score product, so P and dS
+// feed the next product from registers. Scores run in the log2 domain (q pre-scaled by
+// scale * log2 e, P = exp2(s - lse2)); the workspace keeps lse2 and D = dO . O per (row, head).
+__device__ __forceinline__ float xg_sum_tr(float v) {     // sum over lanes c, c^16, c^32, c^48
+    auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+    auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+__device__ __forceinline__ float xg_max_tr(float v) {
+    auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+    auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+constexpr float kLog2e = 1.4426950408889634f;
+
+// KS consecutive floats of a row (16-B aligned when KS % 4 == 0)
+template <int KS>
+__device__ __forceinline__ void load_ks(const float* p, float (&v)[KS], bool ok, float mul) {
+    if constexpr (KS % 4 == 0) {
+#pragma unroll
+        for (int s = 0; s < KS; s += 4) {
+            const float4 x = ok ? *reinterpret_cast<const float4*>(p + s) : make_float4(0.f, 0.f, 0.f, 0.f);
+            v[s] = x.x * mul; v[s + 1] = x.y * mul; v[s + 2] = x.z * mul; v[s + 3] = x.w * mul;
+        }
+    } else {
+#pragma unroll
+        for (int s = 0; s < KS; ++s) v[s] = ok ? p[s] * mul : 0.f;
+    }
+}
+
+// stage 64 rows x DH of `src` (row stride ld, head offset applied) into LDS rows of pitch LD,
+// rows >= n zero, each row scaled by mul
+template <int DH, int LD>
+__device__ __forceinline__ void stage_rows(float* dst, const float* src, int64_t ld, int n, float mul) {
+    constexpr int R4 = DH / 4;
+    for (int e = threadIdx.x; e < 64 * R4; e += 256) {
+        const int row = e / R4, d4 = (e % R4) * 4;
+        float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (row < n) x = *reinterpret_cast<const float4*>(src + row * ld + d4);
+        float* o = dst + row * LD + d4;
+        o[0] = x.x * mul; o[1] = x.y * mul; o[2] = x.z * mul; o[3] = x.w * mul;
+    }
+}
+
+template <int DH>
+__global__ void __launch_bounds__(256)
+attn_bwd_dq_mfma_kernel(AttnBwd a) {
+    constexpr int KS = DH / 4, DT = DH / 16, LD = DH + 4;
+    __shared__ float kt[64 * LD];
+    __shared__ float vt[64 * LD];
+    const int seg = blockIdx.x / a.q_blocks, qb = blockIdx.x % a.q_blocks, h = blockIdx.y;
+    const int64_t qb0 = a.q_off[seg], qe = a.q_off[seg + 1];
+    if (qb0 + (int64_t)qb * 64 >= qe) return;                 // block-uniform
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, g = lane >> 4, c = lane & 15;
+    const int64_t r = qb0 + (int64_t)qb * 64 + wv * 16 + c;  // this lane's query row
+    const bool ok = r < qe;
+    const int ks = a.kv_seg[seg];
+    const int64_t kb = a.kv_off[ks], ke = a.kv_off[ks + 1];
+    float qv[KS], dov[KS], ov[KS];
+    load_ks<KS>(a.q + r * a.ldq + h * DH + g * KS, qv, ok, a.scale * kLog2e);
+    load_ks<KS>(a.dout + r * a.lddo + h * DH + g * KS, dov, ok, 1.f);
+    load_ks<KS>(a.o + r * a.ldo + h * DH + g * KS, ov, ok, 1.f);
+    float dsum = 0.f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) dsum = fmaf(dov[s], ov[s], dsum);
+    dsum = xg_sum_tr(dsum);
+    // S^T tile n of the staged keys: lane (g, c) -> keys 16n + 4g + r of query c
+    auto scores = [&](const float* tile, const float (&rv)[KS], int n) {
+        f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+        const float* kr = tile + (16 * n + c) * LD + g * KS;
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(kr[s], rv[s], acc, 0, 0, 0);
+        return acc;
+    };
+    // pass 1: the row's max and sum (per lane over its keys, then over the 4 lanes of the row)
+    float m = -INFINITY, l = 0.f;
+    for (int64_t t0 = kb; t0 < ke; t0 += 64) {
+        const int nt = (int)min((int64_t)64, ke - t0);
+        __syncthreads();
+        stage_rows<DH, LD>(kt, a.k + t0 * a.ldk + h * DH, a.ldk, nt, 1.f);
+        __syncthreads();
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+            const f32x4_t s4 = scores(kt, qv, n);
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                if (16 * n + 4 * g + rr >= nt) continue;
+                const float sv = s4[rr];
+                if (sv > m) { l = l * __builtin_amdgcn_exp2f(m - sv) + 1.f; m = sv; }
+                else l += __builtin_amdgcn_exp2f(sv - m);
+            }
+        }
+    }
+    const float M = xg_max_tr(m);
+    const float lse2 = M + __builtin_amdgcn_logf(xg_sum_tr(m == -INFINITY ? 0.f : l * __builtin_amdgcn_exp2f(m - M)));
+    // pass 2: P, dP, dS and dQ^T += K^T dS^T
+    f32x4_t dq[DT];
+#pragma unroll
+    for (int t = 0; t < DT; ++t) dq[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int64_t t0 = kb; t0 < ke; t0 += 64) {
+        const int nt = (int)min((int64_t)64, ke - t0);
+        __syncthreads();
+        stage_rows<DH, LD>(kt, a.k + t0 * a.ldk + h * DH, a.ldk, nt, 1.f);
+        stage_rows<DH, LD>(vt, a.v + t0 * a.ldv + h * DH, a.ldv, nt, 1.f);
+        __syncthreads();
+        float ds[4][4];
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+            const f32x4_t s4 = scores(kt, qv, n);
+            const f32x4_t p4 = scores(vt, dov, n);                // dP^T = V dO^T
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                const bool in = 16 * n + 4 * g + rr < nt;
+                const float p = in ? __builtin_amdgcn_exp2f(s4[rr] - lse2) : 0.f;
+                ds[n][rr] = p * (p4[rr] - dsum);
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < DT; ++t)
+#pragma unroll
+            for (int n = 0; n < 4; ++n)
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr)
+                    dq[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                        kt[(16 * n + 4 * g + rr) * LD + 16 * t + c], ds[n][rr], dq[t], 0, 0, 0);
+    }
+    // dQ = scale * sum dS K; lane (g, c) holds dims 16t + 4g .. + 3 of query c
+    const int64_t rq = qb0 + (int64_t)qb * 64 + wv * 16 + c;
+    if (rq < qe) {
+#pragma unroll
+        for (int t = 0; t < DT; ++t)
+            *reinterpret_cast<float4*>(a.dq + rq * a.lddq + h * DH + 16 * t + 4 * g) =
+                make_float4(dq[t][0] * a.scale, dq[t][1] * a.scale, dq[t][2] * a.scale, dq[t][3] * a.scale);
+        if (g == 0) {
+            a.lse[rq * a.nhead + h] = lse2;
+            a.dsum[rq * a.nhead + h] = dsum;
+        }
+    }
+}
+
+template <int DH>
+__global__ void __launch_bounds__(256)
+attn_bwd_dkdv_mfma_kernel(AttnBwd a) {
+    constexpr int KS = DH / 4, DT = DH / 16, LD = DH + 4;
+    __shared__ float qt[64 * LD];
+    __shared__ float dt[64 * LD];
+    __shared__ float lt[64], st[64];
+    const int ks = blockIdx.x / a.kv_blocks, kbk = blockIdx.x % a.kv_blocks, h = blockIdx.y;
+    const int64_t kb0 = a.kv_off[ks], ke = a.kv_off[ks + 1];
+    if (kb0 + (int64_t)kbk * 64 >= ke) return;
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, g = lane >> 4, c = lane & 15;
+    const int64_t rk = kb0 + (int64_t)kbk * 64 + wv * 16 + c;   // this lane's key row
+    const bool ok = rk < ke;
+    float kv[KS], vv[KS];
+    load_ks<KS>(a.k + rk * a.ldk + h * DH + g * KS, kv, ok, 1.f);
+    load_ks<KS>(a.v + rk * a.ldv + h * DH + g * KS, vv, ok, 1.f);
+    f32x4_t dk[DT], dv[DT];
+#pragma unroll
+    for (int t = 0; t < DT; ++t) dk[t] = dv[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int seg = 0; seg < a.n_seg; ++seg) {
+        if (a.kv_seg[seg] != ks) continue;
+        const int64_t qb = a.q_off[seg], qe = a.q_off[seg + 1];
+        for (int64_t t0 = qb; t0 < qe; t0 += 64) {
+            const int nt = (int)min((int64_t)64, qe - t0);
+            __syncthreads();
+            stage_rows<DH, LD>(qt, a.q + t0 * a.ldq + h * DH, a.ldq, nt, a.scale * kLog2e);
+            stage_rows<DH, LD>(dt, a.dout + t0 * a.lddo + h * DH, a.lddo, nt, 1.f);
+            if (tid < 64) {
+                lt[tid] = tid < nt ? a.lse[(t0 + tid) * a.nhead + h] : INFINITY;   // P = 0 past the end
+                st[tid] = tid < nt ? a.dsum[(t0 + tid) * a.nhead + h] : 0.f;
+            }
+            __syncthreads();
+            float p[4][4], ds[4][4];
+#pragma unroll
+            for (int n = 0; n < 4; ++n) {
+                // S[query 16n + 4g + r][key c] = Q K^T, dP = dO V^T
+                f32x4_t s4 = {0.f, 0.f, 0.f, 0.f}, d4 = s4;
+                const float* qr = qt + (16 * n + c) * LD + g * KS;
+                const float* dr = dt + (16 * n + c) * LD + g * KS;
+#pragma unroll
+                for (int s = 0; s < KS; ++s) {
+                    s4 = __builtin_amdgcn_mfma_f32_16x16x4f32(qr[s], kv[s], s4, 0, 0, 0);
+                    d4 = __builtin_amdgcn_mfma_f32_16x16x4f32(dr[s], vv[s], d4, 0, 0, 0);
+                }
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) {
+                    const int qi = 16 * n + 4 * g + rr;
+                    p[n][rr] = __builtin_amdgcn_exp2f(s4[rr] - lt[qi]);
+                    ds[n][rr] = p[n][rr] * (d4[rr] - st[qi]);
+                }
+            }
+            // dV^T += dO^T P, dK^T += Q^T dS (k-step (n, r): query 16n + 4g + r)
+#pragma unroll
+            for (int t = 0; t < DT; ++t)
+#pragma unroll
+                for (int n = 0; n < 4; ++n)
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr) {
+                        const int qi = 16 * n + 4 * g + rr;
+                        dv[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(dt[qi * LD + 16 * t + c], p[n][rr], dv[t], 0, 0, 0);
+                        dk[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(qt[qi * LD + 16 * t + c], ds[n][rr], dk[t], 0, 0, 0);
+                    }
+        }
+    }
+    if (!ok) return;
+    // the staged q carried scale * log2 e: dK = scale * sum dS q = (sum dS qt) / log2 e
+    constexpr float il2 = 1.0f / kLog2e;
+#pragma unroll
+    for (int t = 0; t < DT; ++t) {
+        *reinterpret_cast<float4*>(a.dk + rk * a.lddk + h * DH + 16 * t + 4 * g) =
+            make_float4(dk[t][0] * il2, dk[t][1] * il2, dk[t][2] * il2, dk[t][3] * il2);
+        *reinterpret_cast<float4*>(a.dv + rk * a.lddv + h * DH + 16 * t + 4 * g) =
+            make_float4(dv[t][0], dv[t][1], dv[t][2], dv[t][3]);
+    }
+}
+
 // ---- CorrespondenceDecoder.simple_attention backward ----------------------------------------
 // corr[i] = sum_j P_ij v_j, P = softmax_j(s_ij), s_ij = scale q_i.k_j, v_j = the partner cloud's
 // xyz (3 columns, no gradient). With D_i = dO_i . corr_i and dS_ij = P_ij (dO_i . v_j - D_i):
@@ -1195,6 +1425,27 @@ extern "C" int fgr_attention_bwd(const float* q, int64_t ldq, const float* k, in
               (float*)ws + std::max<int64_t>(nq, 1) * nhead};
     hipStream_t st = as_stream(stream);
     dim3 g1((unsigned)(n_seg * a.q_blocks), nhead), g2((unsigned)(n_kv_seg * a.kv_blocks), nhead);
+    // head dim 16 / 32 / 64 with 16-B aligned rows: the fp32-MFMA kernels (FGR_ATTN_BWD=scalar:
+    // the scalar ones, for A/B)
+    const bool al = ((reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(k) |
+                      reinterpret_cast<uintptr_t>(v) | reinterpret_cast<uintptr_t>(o) |
+                      reinterpret_cast<uintptr_t>(dout) | reinterpret_cast<uintptr_t>(dq) |
+                      reinterpret_cast<uintptr_t>(dk) | reinterpret_cast<uintptr_t>(dv)) & 15) == 0 &&
+                    (ldq | ldk | ldv | ldo | lddo | lddq | lddk | lddv) % 4 == 0;
+    static const bool scalar_only = [] { const char* e = getenv("FGR_ATTN_BWD"); return e && e[0] == 's'; }();
+    if (al && !scalar_only && (dh == 16 || dh == 32 || dh == 64)) {
+        switch (dh) {
+#define ATM(D) case D: \
+            hipLaunchKernelGGL(attn_bwd_dq_mfma_kernel<D>, g1, dim3(256), 0, st, a); \
+            FGR_CHECK_LAUNCH("attn_bwd_dq_mfma_kernel"); \
+            hipLaunchKernelGGL(attn_bwd_dkdv_mfma_kernel<D>, g2, dim3(256), 0, st, a); \
+            break;
+            ATM(16) ATM(32) ATM(64)
+#undef ATM
+        }
+        FGR_CHECK_LAUNCH("attn_bwd_dkdv_mfma_kernel");
+        return FGR_OK;
+    }
     switch (dh) {
 #define ATB(D) case D: \
         hipLaunchKernelGGL(attn_bwd_dq_kernel<D>, g1, dim3(64), 0, st, a); \

@@ -63,11 +63,11 @@ def _relu_mask(dy, y):
 # ------------------------------------------------------------------------------------------
 class _LinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, residual, act):
+    def forward(ctx, x, w, b, residual, act, cache=True):
         assert act in (ACT_NONE, ACT_RELU)
-        y = linear(x, w, b, act=act, residual=residual)
+        y = linear(x, w, b, act=act, residual=residual, cache=cache)
         ctx.mode = lin.MODE          # the backward's products run in the forward's mode
-        ctx.act, ctx.has_b, ctx.has_r = act, b is not None, residual is not None
+        ctx.act, ctx.has_b, ctx.has_r, ctx.cache = act, b is not None, residual is not None, cache
         ctx.save_for_backward(x, w, y if act == ACT_RELU else None)
         return y
 
@@ -80,20 +80,21 @@ class _LinearFn(torch.autograd.Function):
         dx = dw = db = None
         with lin.mode_scope(ctx.mode):
             if ctx.needs_input_grad[0]:
-                dx = linear(dy, w, transpose=True, tag='bwd_dx')          # dY W
+                dx = linear(dy, w, transpose=True, tag='bwd_dx', cache=ctx.cache)   # dY W
             if ctx.needs_input_grad[1]:
                 dw = linear(dy.t().contiguous(), x, transpose=True, cache=False)   # dY^T X
         if ctx.has_b and ctx.needs_input_grad[2]:
             db = colsum(dy)
         dres = dy if ctx.has_r and ctx.needs_input_grad[3] else None
-        return dx, dw, db, dres, None
+        return dx, dw, db, dres, None, None
 
 
-def linear_t(x, w, b=None, act=ACT_NONE, residual=None):
+def linear_t(x, w, b=None, act=ACT_NONE, residual=None, cache=True):
     """act(x W^T + b) (+ residual after the activation is NOT supported: residual is added
-    before, as the transformer's out-projection / FFN epilogues use it with act NONE)."""
+    before, as the transformer's out-projection / FFN epilogues use it with act NONE).
+    cache=False: w is an activation (a new tensor every step), its image is not cached."""
     assert residual is None or act == ACT_NONE
-    return _LinearFn.apply(x, w, b, residual, act)
+    return _LinearFn.apply(x, w, b, residual, act, cache)
 
 
 # ------------------------------------------------------------------------------------------

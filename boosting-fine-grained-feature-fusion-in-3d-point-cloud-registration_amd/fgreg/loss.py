@@ -183,3 +183,80 @@ def compute_metrics(pred, batch):
         metrics[f'rot_err_deg{k[4:]}'] = err['rot_deg']
         metrics[f'trans_err{k[4:]}'] = err['trans']
     return metrics
+
+
+def compute_loss_train(model, pred, batch):
+    """RegTR.compute_loss (finegrained_regtr.py:252-309) as a differentiable graph: the same
+    keys, weights and reductions as compute_loss above, with the match logits on the
+    differentiable f16x3 GEMMs (fgreg.autograd.linear_t: A W_sym, then against the positives)
+    and the BCE / InfoNCE masks / L1 terms as torch ops on the device, so that
+    ``losses['total'].backward()`` reaches every parameter (trainer.py:110-125). The overlap
+    pyramid is a target (no gradient): fgr_overlap_pool as in compute_loss."""
+    import math
+    import torch.nn.functional as F
+    from .autograd import linear_t
+    cfg = model.cfg
+    if cfg.get('feature_loss_type', 'infonce') != 'infonce':
+        raise NotImplementedError('only the infonce feature loss is in the reference configs')
+    meta = batch['kpconv_meta']
+    pose = batch['pose'].float()
+    p = len(meta['stack_lengths']) - 1
+    with torch.no_grad():
+        pyr = compute_overlaps(batch)
+    batch['overlap_pyr'] = pyr
+    ov = pyr[f'pyr_{p}']
+    lens = [int(v) for v in meta['stack_lengths'][p].tolist()]
+    B = len(lens) // 2
+    src_w, tgt_w = torch.split(ov[:sum(lens[:B])], lens[:B]), torch.split(ov[sum(lens[:B]):], lens[B:])
+
+    def rigid(ps, x):
+        return x @ ps[:, :3].t() + ps[:, 3]
+
+    def w_sym(W):
+        t = torch.triu(W)
+        return t + t.t()
+
+    def infonce_pair(Ws, a, pp, a_xyz, p_xyz):
+        # feature_loss.py:283-314: the nearest positive within r_p is the target, every
+        # other positive within r_n leaves the partition sum
+        logits = linear_t(linear_t(a, Ws, cache=False), pp, cache=False)   # a W_sym p^T
+        with torch.no_grad():
+            dist = torch.cdist(a_xyz, p_xyz)
+            d1, j1 = dist.min(dim=1)
+            keep = d1 < cfg.r_p
+            excl = dist < cfg.r_n
+            excl[torch.arange(len(j1), device=excl.device), j1] = False
+        logits = logits.masked_fill(excl, -math.inf)
+        rows = torch.arange(len(j1), device=logits.device)
+        per_row = torch.logsumexp(logits, dim=1) - logits[rows, j1]
+        return per_row[keep].sum() / keep.sum()
+
+    losses = {}
+    logits = torch.cat(list(pred['src_overlap']) + list(pred['tgt_overlap']), dim=-2)
+    for i in cfg.overlap_loss_on:
+        losses[f'overlap_{i}'] = F.binary_cross_entropy_with_logits(logits[i, :, 0], ov)
+    a_xyz = [rigid(pose[b], pred['src_kp'][b]) for b in range(B)]
+    for i in cfg.feature_loss_on:
+        Ws = w_sym(model.feature_criterion.W)
+        losses[f'feature_{i}'] = torch.stack([
+            infonce_pair(Ws, pred['src_feat'][b][i], pred['tgt_feat'][b][i], a_xyz[b],
+                         pred['tgt_kp'][b]) for b in range(B)]).mean()
+    Wu = w_sym(model.feature_criterion_un.W)
+    losses['feature_un'] = torch.stack([
+        infonce_pair(Wu, pred['src_feat_un'][b], pred['tgt_feat_un'][b], a_xyz[b],
+                     pred['tgt_kp'][b]) for b in range(B)]).mean()
+
+    def corr_mae(kp, warped, poses, weights):
+        gt = torch.cat([rigid(poses[b], kp[b]) for b in range(len(kp))])
+        err = (torch.cat(list(warped)) - gt).abs().sum(1)
+        w = torch.cat(list(weights))
+        return (w * err).sum() / torch.clamp_min(w.sum(), 1e-6)
+
+    inv = torch.stack([torch.cat([pose[b, :, :3].t(), -(pose[b, :, :3].t() @ pose[b, :, 3:4])], 1)
+                       for b in range(B)])
+    for i in cfg.corr_loss_on:
+        losses[f'corr_{i}'] = (corr_mae(pred['src_kp'], [w[i] for w in pred['src_kp_warped']], pose, src_w)
+                               + corr_mae(pred['tgt_kp'], [w[i] for w in pred['tgt_kp_warped']], inv, tgt_w))
+    wd = weight_dict(cfg)
+    losses['total'] = torch.sum(torch.stack([losses[k] * wd[k] for k in losses]))
+    return losses

@@ -424,6 +424,46 @@ def test_train_step_vs_reference(gpu):
             assert rel_err(getattr(mods[name], stat), ref[k]) < 1e-5, k
 
 
+def test_compute_loss_train_vs_reference(gpu):
+    """fgreg.loss.compute_loss_train (the differentiable compute_loss that bench.py --train
+    backpropagates: the f16x3 GEMMs for the match logits, torch ops for the rest) on the GPU vs
+    the reference's own train() step (train_modelnet_small.npz): losses within 1e-5, every
+    parameter's gradient norm and the stored full gradients within GRAD_TOL, W / W_un included."""
+    import fgreg
+    from fgreg.loss import compute_loss_train
+    cfg, sd, src, tgt, meta, batch, W, W_un, ref = train_fixture()
+    model = fgreg.RegTR(cfg)
+    model.load_state_dict({k: v for k, v in sd.items()}, strict=False)
+    with torch.no_grad():
+        model.feature_criterion.W.copy_(W)
+        model.feature_criterion_un.W.copy_(W_un)
+    model = model.to(gpu).train()
+    model.preprocessor = fgreg.FixedMetaPreprocessor({k: [t.to(gpu) for t in v]
+                                                      for k, v in meta.items()})
+    xb = {'src_xyz': [torch.from_numpy(np.asarray(c)).to(gpu) for c in src],
+          'tgt_xyz': [torch.from_numpy(np.asarray(c)).to(gpu) for c in tgt]}
+    pred = model(xb)
+    xb['pose'] = batch['pose'].to(gpu)
+    xb['src_overlap'] = [t.to(gpu) for t in batch['src_overlap']]
+    xb['tgt_overlap'] = [t.to(gpu) for t in batch['tgt_overlap']]
+    losses = compute_loss_train(model, pred, xb)
+    losses['total'].backward()
+    for k in ref.files:
+        if k.startswith('loss.'):
+            v = float(ref[k])
+            assert abs(float(losses[k[5:]]) - v) <= 1e-5 * max(1.0, abs(v)), (k, float(losses[k[5:]]), v)
+    grads = {k: p.grad for k, p in model.named_parameters() if p.grad is not None}
+    norms = {k[6:] for k in ref.files if k.startswith('gnorm.')}
+    for k in norms:
+        n_ref = float(ref['gnorm.' + k])
+        e = abs(float(grads[k].double().norm()) - n_ref) / max(n_ref, 1e-12)
+        assert e < GRAD_TOL, (k, e)
+    for k in ref.files:
+        if k.startswith('grad.'):
+            e = fro(grads[k[5:]], torch.from_numpy(ref[k]))
+            assert e < GRAD_TOL, (k, e)
+
+
 @pytest.mark.parametrize('pre_norm,head', [(True, 'regressor'), (False, 'regressor'),
                                            (True, 'decoder')])
 def test_train_step_vs_oracle_modelnet(gpu, pre_norm, head):
