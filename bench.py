@@ -102,7 +102,7 @@ OTHER = {
     'instnorm': ('hbm', '8 N C bytes (+ 4 N C residual, + 4 N row divisor)'),
     'layernorm': ('hbm', '8 N d bytes (+ 4 N d per add / pre-bias)'),
     'pose': ('hbm', '28 B per (layer, point) + 48 B per pose'),
-    'max_pool': ('hbm', '8 H + 4 C bytes per query + 4 C per valid neighbour row'),
+    'max_pool': ('hbm', '8 H + 4 C bytes per query + 4 C per distinct support row'),
 }
 
 

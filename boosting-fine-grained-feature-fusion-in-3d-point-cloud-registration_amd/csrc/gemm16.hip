@@ -1164,8 +1164,10 @@ char h3_tile_kloop(int m, int n, int k) {
         return (k >= 2048 || n <= 64) ? 'S' : ((n <= 128 && k >= 1024 && tiles64 > 256) ? 'T' : 'W');
     if (g5ok && m <= 4096)
         return (n <= 512 || (n <= 1024 && k <= 512)) ? 'X' : 'Y';
+    // (512 <= K < 1024 took the g5 'Y' until round 5: 'y' measured 1.2-1.3x faster on every
+    // such shape, profiles/r05_gemm_tiles_k512.txt)
     if (n >= 512)
-        return k >= 1024 ? 'u' : (k >= 512 ? (g5ok ? 'Y' : 'k') : 'y');
+        return k >= 1024 ? 'u' : ((k >= 512 && !g5ok) ? 'k' : 'y');
     if (tiles64 >= 2048) return 'y';
     if (g5ok && (k >= 512 || m <= 16384)) return 'X';
     if (n <= 128 && k >= 1024) return 'f';

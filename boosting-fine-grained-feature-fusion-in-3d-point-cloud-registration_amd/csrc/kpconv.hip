@@ -532,6 +532,7 @@ extern "C" int fgr_max_pool(const float* x, int64_t ns, int32_t c, const int64_t
     FGR_REQUIRE(nq == 0 || (x && idx && out), "fgr_max_pool: null pointer");
     if (nq == 0) return FGR_OK;
     hipStream_t st = as_stream(stream);
+    TimedCall timed_(st);
     if (c == 64 || c == 128 || c == 256 || c == 512) {
         dim3 grid((unsigned)ceil_div(nq, 4));
         if (c == 64) hipLaunchKernelGGL(max_pool_wave<1>, grid, dim3(256), 0, st, x, ns, idx, nq, width, out);

@@ -343,6 +343,7 @@ extern "C" int fgr_res2net_chain_h3(const float* h, int64_t n, int32_t w, int32_
     if (n == 0) return FGR_OK;
     const dim3 grid((unsigned)ceil_div(n, kRows));
     hipStream_t st = as_stream(stream);
+    TimedCall timed_(st);
     const int kt = (w + 15) / 16;
 #define FGR_H3_CASE(KT)                                                                         \
     case KT:                                                                                    \
@@ -375,6 +376,7 @@ extern "C" int fgr_res2net_chain6(const float* h, int64_t n, int32_t w, int32_t 
                 "fgr_res2net_chain6: h must be 16-B aligned");
     if (n == 0) return FGR_OK;
     hipStream_t st = as_stream(stream);
+    TimedCall timed_(st);
     // w = 224 (one 14-wave block per CU): 48-row blocks when that saves a round of blocks
     // over 32-row ones (rounds x rows per block; 256 CUs); FGR_R2N_ROWS=32 forces 32 (A/B)
     const char* rr = getenv("FGR_R2N_ROWS");

@@ -364,11 +364,12 @@ def max_pool(x, idx) -> torch.Tensor:
 
 
 def max_pool_bytes(idx, ns, c):
-    """Algorithmic HBM bytes of one fgr_max_pool launch: sum_q [8 H (idx row) + 4 C (output
-    row)] + 4 C per valid neighbour row read (finegrained_kpconv_blocks.py:125-141)."""
+    """Algorithmic HBM bytes of one fgr_max_pool launch (finegrained_kpconv_blocks.py:125-141):
+    sum_q [8 H (idx row) + 4 C (output row)] + 4 C per DISTINCT support row named by the table
+    (each is needed from HBM once; its repeats across queries are cache traffic)."""
     nq, H = idx.shape
-    v = int((idx < ns).sum().item())
-    return nq * (8 * H + 4 * c) + v * 4 * c
+    u = int(torch.unique(idx[idx < ns]).numel())
+    return nq * (8 * H + 4 * c) + u * 4 * c
 
 
 # ------------------------------------------------------------------------------------------

@@ -55,6 +55,8 @@ def main():
         KSPLITS = ['1', '2', '4', '8']
     bf = 'bf16' in sys.argv[2:]
     shapes = SHAPES_3D if '3d' in sys.argv[2:] else SHAPES
+    if os.environ.get('GEMM_SHAPES'):          # "M,N,K;M,N,K": these shapes only
+        shapes = [tuple(int(v) for v in t.split(',')) for t in os.environ['GEMM_SHAPES'].split(';')]
     env = 'FGR_GEMM_BF16_TILE' if bf else 'FGR_GEMM16_TILE'
     dev = torch.device('cuda:0')
     lin.set_mode('bf16' if bf else 'f16x3')
