@@ -127,8 +127,16 @@ __device__ __forceinline__ void wait_vm_lgkm0_dyn(int n) {
     }
 }
 
-constexpr int kRsNb = 3;           // W panels in the LDS ring (two in flight while one computes)
-constexpr int kRsMaxNc = 64;       // panels per block (the per-block column scales / bias in LDS)
+// W panels per pipeline stage: the panel loop waits for the stage's DMA, meets at one barrier
+// and runs the MFMAs of all its panels; one stage is in flight while one computes (a ring of
+// 2 * PPS panels). PPS = 1 is the round-4 loop (a 3-panel ring, two in flight). Round 5: a
+// panel took ~0.3 us of MFMA plus ~0.7 us of wait / barrier latency, and doubling its MFMA
+// work added the whole MFMA time (profiles/r05_rs_pps_ab.txt), so panels share the waits.
+#ifndef FGR_RS_PPS
+#define FGR_RS_PPS 2
+#endif
+constexpr int kRsPps = FGR_RS_PPS;
+constexpr int kRsMaxNc = 32;       // panels per block (the per-block column scales / bias in LDS)
 #ifndef FGR_RS_LA
 #define FGR_RS_LA 4
 #endif
@@ -163,8 +171,13 @@ __global__ void __launch_bounds__(256, KV ? 2 : 1) gemm_rs_kernel(RsArgs p) {
     constexpr int PANEL_U = KS * 128;                  // 16-B units per W panel
     constexpr int PW = PANEL_U / 256;                  // DMA pieces (1 KiB) per wave per panel
     static_assert(PANEL_U % 256 == 0, "KS even");
-    constexpr int NB = kRsNb;                          // W panel ring
-    constexpr int LA = NB - 1;                         // DMA lookahead in panels
+    // panels per stage (the LN + K/V + side-output variant keeps one: with two its register
+    // peak passes the 256 VGPRs of two waves per SIMD; so do K <= 128, sized for 4 blocks / CU;
+    // the plain LN prologue (linear1) measured 30.8 us with one, 33.0 us with two)
+    constexpr int PPS = ((KV && LNM == 3) || KS <= 4 || (LN && !KV)) ? 1 : kRsPps;
+    constexpr int NB = PPS == 1 ? 3 : 2 * PPS;         // W panel ring
+    constexpr int LA = PPS == 1 ? NB - 1 : PPS;        // DMA lookahead in panels
+    static_assert(PPS == 1 || NB == 2 * PPS, "one stage in flight while one computes");
     __shared__ u32x4 ring[NB * PANEL_U];
     __shared__ float4 colw[kRsMaxNc * 4], colb[kRsMaxNc * 4];   // per (panel, g): wsc, bias
     __shared__ float4 lng[LN ? KS * 8 : 1], lnb[LN ? KS * 8 : 1];  // LN gamma / beta (K / 4)
@@ -207,8 +220,9 @@ __global__ void __launch_bounds__(256, KV ? 2 : 1) gemm_rs_kernel(RsArgs p) {
                                              (__attribute__((address_space(3))) void*)(dst + j * 4096),
                                              16, 0, 0);
     };
-    dma(0);
-    if (LA >= 2 && np > 1) dma(1);
+#pragma unroll
+    for (int d = 0; d < LA; ++d)
+        if (d < np) dma(d);
 
     // activation rows -> registers, one scale per row, split once
     f16x8 af[RT][KS][2];
@@ -559,43 +573,125 @@ __global__ void __launch_bounds__(256, KV ? 2 : 1) gemm_rs_kernel(RsArgs p) {
 #ifdef FGR_RS_STAMP
     st_[2] = __builtin_amdgcn_s_memtime();
 #endif
-    float4 rcur[RT];
-    f32x4 prev[RT];
-    for (int q = 0; q < np; ++q) {
-        // vector-memory ops issued after panel q's DMA (issued in iteration q - 2), counted so
-        // that vmcnt guarantees that DMA has landed: the epilogue stores of iteration q - 2
-        // (panel q - 3), then iteration q - 1's [residual loads, not counted: waiting for them
-        // too is merely stricter], DMA of panel q + 1 if any, and its epilogue stores (panel
-        // q - 2)
-        static_assert(LA == 2, "the wait counts below assume two panels in flight");
-#if defined(FGR_RS_WAIT0)
-        wait_vm_lgkm0_rs<0>();
-#else
-        if (q == 0) wait_vm_lgkm0_dyn(np > 1 ? PW : 0);
-        else wait_vm_lgkm0_dyn((q >= 3 ? nstore(q - 3) : 0) + (q >= 2 ? nstore(q - 2) : 0) +
-                               (q + 1 < np ? PW : 0));
-#endif
-        __builtin_amdgcn_s_barrier();                    // every wave's pieces; buffer of q - 1 free
-#ifdef FGR_RS_STAMP
-        if (q == 0) st_[3] = __builtin_amdgcn_s_memtime();
-        if (q == np - 1) st_[4] = __builtin_amdgcn_s_memtime();
-#endif
-        if constexpr (KV)
-            if (kv_pend) kv_finish();                    // block-uniform
-        if constexpr (RES)
-            if (q >= 1) load_res(q - 1, rcur);
-        if (q + LA < np) dma(q + LA);
-        f32x4 acc[RT];
-        panel_mfma(q, acc);
-        // the previous panel's epilogue after this panel's MFMAs: its VALU and stores issue in
-        // the MFMA shadows instead of between two panels' matrix work (measured 1.09-1.17x on
-        // the LN-fused and 57264-row shapes, equal elsewhere: profiles/r04_rs_defer_ab.txt)
-        if (q >= 1) epilogue(q - 1, prev, rcur);
+    if constexpr (PPS == 1) {
+        float4 rcur[RT];
+        f32x4 prev[RT];
+        for (int q = 0; q < np; ++q) {
+            // vector-memory ops issued after panel q's DMA (issued in iteration q - 2), counted so
+            // that vmcnt guarantees that DMA has landed: the epilogue stores of iteration q - 2
+            // (panel q - 3), then iteration q - 1's [residual loads, not counted: waiting for them
+            // too is merely stricter], DMA of panel q + 1 if any, and its epilogue stores (panel
+            // q - 2)
+            static_assert(PPS > 1 || LA == 2, "the wait counts below assume two panels in flight");
+    #if defined(FGR_RS_WAIT0)
+            wait_vm_lgkm0_rs<0>();
+    #else
+            if (q == 0) wait_vm_lgkm0_dyn(np > 1 ? PW : 0);
+            else wait_vm_lgkm0_dyn((q >= 3 ? nstore(q - 3) : 0) + (q >= 2 ? nstore(q - 2) : 0) +
+                                   (q + 1 < np ? PW : 0));
+    #endif
+            __builtin_amdgcn_s_barrier();                    // every wave's pieces; buffer of q - 1 free
+    #ifdef FGR_RS_STAMP
+            if (q == 0) st_[3] = __builtin_amdgcn_s_memtime();
+            if (q == np - 1) st_[4] = __builtin_amdgcn_s_memtime();
+    #endif
+            if constexpr (KV)
+                if (kv_pend) kv_finish();                    // block-uniform
+            if constexpr (RES)
+                if (q >= 1) load_res(q - 1, rcur);
+            if (q + LA < np) dma(q + LA);
+            f32x4 acc[RT];
+            panel_mfma(q, acc);
+    #ifdef FGR_RS_MFMA2
+            {   // diagnostic build only (timing probe, wrong results): the panel's MFMA work twice
+                f32x4 acc2[RT];
+                panel_mfma(q, acc2);
+    #pragma unroll
+                for (int i = 0; i < RT; ++i) acc[i] += acc2[i];
+            }
+    #endif
+            // the previous panel's epilogue after this panel's MFMAs: its VALU and stores issue in
+            // the MFMA shadows instead of between two panels' matrix work (measured 1.09-1.17x on
+            // the LN-fused and 57264-row shapes, equal elsewhere: profiles/r04_rs_defer_ab.txt)
+            if (q >= 1) epilogue(q - 1, prev, rcur);
+    #pragma unroll
+            for (int i = 0; i < RT; ++i) prev[i] = acc[i];
+        }
+        if constexpr (RES) load_res(np - 1, rcur);
+        epilogue(np - 1, prev, rcur);
+    } else {
+        // stages of PPS panels: stage st = panels st * PPS .. + PPS - 1 (those < np), ring slots
+        // (st & 1) * PPS + j. Iteration st issues: [wait: DMA of stage st landed] [barrier]
+        // [K/V image stores of the previous head] [residual loads of stage st - 1] [DMA of stage
+        // st + 1] [MFMAs of stage st] [epilogue stores of stage st - 1]; the ops younger than
+        // stage st's DMA (issued in iteration st - 1) are that iteration's epilogue stores
+        // (stage st - 2): the wait leaves exactly those outstanding
+        const int nstage = (np + PPS - 1) / PPS;
+        float4 rcur[PPS][RT];
+        f32x4 prev[PPS][RT];
+        for (int st = 0; st < nstage; ++st) {
+            const int qa = st * PPS;
+            {
+                int cnt = 0;
+                if (st >= 2)
 #pragma unroll
-        for (int i = 0; i < RT; ++i) prev[i] = acc[i];
+                    for (int j = 0; j < PPS; ++j)
+                        if (qa - 2 * PPS + j < np) cnt += nstore(qa - 2 * PPS + j);
+                wait_vm_lgkm0_dyn(cnt);
+            }
+            __builtin_amdgcn_s_barrier();                    // every wave's pieces; stage st - 1's slots free
+#ifdef FGR_RS_STAMP
+            if (st == 0) st_[3] = __builtin_amdgcn_s_memtime();
+            if (st == nstage - 1) st_[4] = __builtin_amdgcn_s_memtime();
+#endif
+            if constexpr (KV)
+                if (kv_pend) kv_finish();                    // block-uniform
+            if constexpr (RES)
+                if (st >= 1)
+#pragma unroll
+                    for (int j = 0; j < PPS; ++j) load_res(qa - PPS + j, rcur[j]);
+#pragma unroll
+            for (int j = 0; j < PPS; ++j)
+                if (qa + PPS + j < np) dma(qa + PPS + j);
+            f32x4 acc[PPS][RT];
+#pragma unroll
+            for (int j = 0; j < PPS; ++j)
+                if (qa + j < np) panel_mfma(qa + j, acc[j]);     // block-uniform
+#ifdef FGR_RS_MFMA2
+#pragma unroll
+            for (int j = 0; j < PPS; ++j)
+                if (qa + j < np) {   // diagnostic build only (timing probe, wrong results)
+                    f32x4 acc2[RT];
+                    panel_mfma(qa + j, acc2);
+#pragma unroll
+                    for (int i = 0; i < RT; ++i) acc[j][i] += acc2[i];
+                }
+#endif
+            if (st >= 1)
+#pragma unroll
+                for (int j = 0; j < PPS; ++j) epilogue(qa - PPS + j, prev[j], rcur[j]);
+#pragma unroll
+            for (int j = 0; j < PPS; ++j)
+#pragma unroll
+                for (int i = 0; i < RT; ++i) prev[j][i] = acc[j][i];
+        }
+        const int ql = (nstage - 1) * PPS;
+        if constexpr (KV) {
+            // the head completed by the loop's last epilogue (stage nstage - 2) before the last
+            // stage's epilogue refills kvbuf
+            if (kv_pend) {                                   // block-uniform
+                __syncthreads();
+                kv_finish();
+                __syncthreads();
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < PPS; ++j) {
+            if (ql + j >= np) break;                         // block-uniform
+            if constexpr (RES) load_res(ql + j, rcur[j]);
+            epilogue(ql + j, prev[j], rcur[j]);
+        }
     }
-    if constexpr (RES) load_res(np - 1, rcur);
-    epilogue(np - 1, prev, rcur);
     if constexpr (KV) {
         if (kv_pend) {                                   // the last head of the block
             __syncthreads();
