@@ -459,15 +459,26 @@ layernorm_lpr_kernel(float* __restrict__ x, int64_t n, int d, const float* __res
     const int64_t rr = ok ? r : n - 1;
     float4 v[NV], gg[NV], bb[NV], ad[NV];
     const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    // every load unconditional (column clamped into the row, chunks past d zeroed after):
+    // guarded loads had put these arrays in scratch (round 5)
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
-        const int col = 4 * (l + LPR * j);
-        const bool in = col < d;
-        v[j] = in ? *reinterpret_cast<const float4*>(x + rr * d + col) : z;
-        gg[j] = in ? *reinterpret_cast<const float4*>(g + col) : z;
-        bb[j] = in ? *reinterpret_cast<const float4*>(bta + col) : z;
-        ad[j] = (in && add) ? *reinterpret_cast<const float4*>(add + rr * d + col) : z;
+        const int col = min(4 * (l + LPR * j), d - 4);
+        v[j] = *reinterpret_cast<const float4*>(x + rr * d + col);
+        gg[j] = *reinterpret_cast<const float4*>(g + col);
+        bb[j] = *reinterpret_cast<const float4*>(bta + col);
     }
+    if (add) {
+#pragma unroll
+        for (int j = 0; j < NV; ++j)
+            ad[j] = *reinterpret_cast<const float4*>(add + rr * d + min(4 * (l + LPR * j), d - 4));
+    } else {
+#pragma unroll
+        for (int j = 0; j < NV; ++j) ad[j] = z;
+    }
+#pragma unroll
+    for (int j = 0; j < NV; ++j)
+        if (4 * (l + LPR * j) >= d) v[j] = z;
     float s = 0.f;
 #pragma unroll
     for (int j = 0; j < NV; ++j) {

@@ -18,31 +18,36 @@ namespace {
 
 // dst[r0 + row][0..cols) = src[r0 + row][0..cols) for row < rows (rows past n skipped): the
 // concatenation tail of the chain kernels. 16-B accesses when every row start is 16-B aligned,
-// four of them in flight per thread (the element-wise loop exposed one memory round trip per
-// element: ~55 per thread for a 1024-channel x)
+// kCpU of them in flight per thread: every load unconditional (element index and row clamped
+// to valid ones, the store masked) -- round 5: guarded loads had put the staging array in
+// scratch with a vmcnt(0) wait after each load, one memory round trip per float4
+constexpr int kCpU = 8;
 __device__ __forceinline__ void copy_rows(float* __restrict__ dst, int64_t ldd,
                                           const float* __restrict__ src, int64_t lds, int64_t r0,
                                           int rows, int64_t n, int cols, int tid, int nth) {
     const bool v4 = ((cols | (int)(ldd & 3) | (int)(lds & 3)) & 3) == 0 &&
                     ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15) == 0;
     if (v4) {
-        const int c4 = cols / 4, tot = rows * c4;
-        for (int e0 = tid; e0 < tot; e0 += 4 * nth) {
-            float4 v[4];
-            int64_t so[4], dof[4];
-            bool ok[4];
+        const int c4 = cols / 4;
+        const int nr = (int)min<int64_t>(rows, n - r0);   // rows of this block below n
+        if (nr <= 0 || c4 == 0) return;
+        const int tot = nr * c4;
+        for (int e0 = tid; e0 < tot; e0 += kCpU * nth) {
+            float4 v[kCpU];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int e = e0 + u * nth;
+            for (int u = 0; u < kCpU; ++u) {
+                const int e = min(e0 + u * nth, tot - 1);
                 const int row = e / c4, cc = (e - row * c4) * 4;
-                ok[u] = e < tot && r0 + row < n;
-                so[u] = (r0 + row) * lds + cc;
-                dof[u] = (r0 + row) * ldd + cc;
-                if (ok[u]) v[u] = *reinterpret_cast<const float4*>(src + so[u]);
+                v[u] = *reinterpret_cast<const float4*>(src + (r0 + row) * lds + cc);
             }
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
-                if (ok[u]) *reinterpret_cast<float4*>(dst + dof[u]) = v[u];
+            for (int u = 0; u < kCpU; ++u) {
+                const int e = e0 + u * nth;
+                if (e < tot) {
+                    const int row = e / c4, cc = (e - row * c4) * 4;
+                    *reinterpret_cast<float4*>(dst + (r0 + row) * ldd + cc) = v[u];
+                }
+            }
         }
         return;
     }
