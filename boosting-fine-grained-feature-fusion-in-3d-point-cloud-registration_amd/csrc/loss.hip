@@ -4,6 +4,8 @@
 //   overlap loss          finegrained_regtr.py:264-267     fgr_bce_logits_mean
 //   se3_transform_list    utils/se3_torch.py:70-90         fgr_transform_points
 //   InfoNCELossFull       losses/feature_loss.py:268-314   (GEMMs) + fgr_infonce_rows/_reduce
+//   CircleLossFull        losses/feature_loss.py:160-243   fgr_circle_loss (feature_loss_type
+//                         circle, finegrained_regtr.py:86-88: Euclidean feature distances)
 //   CorrCriterion (mae)   losses/corr_loss.py:18-38         fgr_corr_loss
 //   se3_compare           utils/se3_torch.py:117-129        fgr_se3_compare
 // All reductions are deterministic (fixed lane / wave / block order).
@@ -208,6 +210,141 @@ infonce_reduce_kernel(const float* __restrict__ row_loss, const float* __restric
     if (threadIdx.x == 0) out[0] = total / (float)n_pairs;
 }
 
+// ---- CircleLossFull (feature_loss.py:160-243, Euclidean feature distances) ----------------
+// Per pair b: fd[i][j] = sqrt(sum_k (a_ik - p_jk)^2 + 1e-12) (cdist 'euclidean', :34-36),
+// cd[i][j] = torch.cdist of the points (its matrix-multiply form, cdist_mm); positives
+// cd < r_p, negatives cd > r_n. The reference masks by shifting fd by -/+1e5 and multiplying
+// by a clamped weight that is 0 on the masked entries, so a non-positive (non-negative) entry
+// contributes exp(0) = 1 to the positive (negative) log-sum-exp:
+//   tp = pos ? 10 (fd - 0.1) max(fd - 0.1, 0) : 0,  tn = neg ? 10 (1.4 - fd) max(1.4 - fd, 0) : 0
+//   line loss = softplus(lse(tp) + lse(tn)) / 10 over each row (and each column),
+// averaged over the rows (columns) that hold a positive and a negative; pair loss = (row mean
+// + column mean) / 2, the call's loss the mean over pairs. Three launches: fd tiles, one wave
+// per row / column, one reduction block; every sum in a fixed order.
+constexpr float kCircleScale = 10.f, kCirclePos = 0.1f, kCircleNeg = 1.4f;
+constexpr int kCdTile = 16, kCdChunk = 64;
+
+// fd of pair b in 16 x 16 tiles, features staged through LDS 64 at a time (rows padded by one
+// float: the 16 positive rows of a k step sit in distinct banks); packed per pair at fd_off[b]
+__global__ void __launch_bounds__(256)
+circle_fd_kernel(const float* __restrict__ af, const float* __restrict__ pf, int d,
+                 const int64_t* __restrict__ a_off, const int64_t* __restrict__ p_off,
+                 const int64_t* __restrict__ fd_off, float* __restrict__ fd) {
+    __shared__ float as[kCdTile][kCdChunk + 1], ps[kCdTile][kCdChunk + 1];
+    const int b = blockIdx.z;
+    const int64_t a0 = a_off[b], p0 = p_off[b];
+    const int na = (int)(a_off[b + 1] - a0), np = (int)(p_off[b + 1] - p0);
+    const int i0 = blockIdx.y * kCdTile, j0 = blockIdx.x * kCdTile;
+    if (i0 >= na || j0 >= np) return;                      // block-uniform
+    const int t = threadIdx.x, ti = t / kCdTile, tj = t % kCdTile;
+    float acc = 0.f;
+    for (int k0 = 0; k0 < d; k0 += kCdChunk) {
+#pragma unroll
+        for (int u = 0; u < kCdTile * kCdChunk / 256; ++u) {
+            const int e = t + 256 * u, r = e / kCdChunk, k = e % kCdChunk;
+            const bool kin = k0 + k < d;
+            as[r][k] = (kin && i0 + r < na) ? af[(a0 + i0 + r) * d + k0 + k] : 0.f;
+            ps[r][k] = (kin && j0 + r < np) ? pf[(p0 + j0 + r) * d + k0 + k] : 0.f;
+        }
+        __syncthreads();
+#pragma unroll 16
+        for (int k = 0; k < kCdChunk; ++k) {
+            const float df = as[ti][k] - ps[tj][k];
+            acc = fmaf(df, df, acc);
+        }
+        __syncthreads();
+    }
+    if (i0 + ti < na && j0 + tj < np)
+        fd[fd_off[b] + (int64_t)(i0 + ti) * np + j0 + tj] = sqrtf(acc + 1e-12f);
+}
+
+__device__ __forceinline__ void lse_push(float& m, float& s, float x) {
+    if (x > m) { s = s * expf(m - x) + 1.f; m = x; }
+    else s += expf(x - m);
+}
+__device__ __forceinline__ void lse_wave(float& m, float& s) {      // fixed butterfly order
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const float om = __shfl_xor(m, o, 64), os = __shfl_xor(s, o, 64);
+        const float M = fmaxf(m, om);
+        const float x = m == -INFINITY ? 0.f : s * expf(m - M);
+        const float y = om == -INFINITY ? 0.f : os * expf(om - M);
+        s = x + y;
+        m = M;
+    }
+}
+__device__ __forceinline__ float softplus_t(float x) {               // F.softplus, threshold 20
+    return x > 20.f ? x : log1pf(expf(x));
+}
+
+// one wave per line: waves [0, n_anchor) are the anchor rows, then one per positive column
+__global__ void __launch_bounds__(256)
+circle_lines_kernel(const float* __restrict__ fd, const float* __restrict__ axyz,
+                    const float* __restrict__ pxyz, const int64_t* __restrict__ a_off,
+                    const int64_t* __restrict__ p_off, const int64_t* __restrict__ fd_off,
+                    int n_pairs, int64_t n_anchor, int64_t n_pos, float r_p, float r_n,
+                    float* __restrict__ line_loss, float* __restrict__ line_sel) {
+    const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (w >= n_anchor + n_pos) return;                     // wave-uniform
+    const bool row = w < n_anchor;
+    const int64_t r = row ? w : w - n_anchor;
+    const int b = find_segment(row ? a_off : p_off, n_pairs, r);
+    const int64_t a0 = a_off[b], p0 = p_off[b];
+    const int na = (int)(a_off[b + 1] - a0), np = (int)(p_off[b + 1] - p0);
+    const int me = (int)(r - (row ? a0 : p0));              // this line's index in the pair
+    const int n_other = row ? np : na;
+    const float* base = fd + fd_off[b];
+    float mp = -INFINITY, sp = 0.f, mn = -INFINITY, sn = 0.f;
+    bool anyp = false, anyn = false;
+    for (int o = lane; o < n_other; o += 64) {
+        const int i = row ? me : o, j = row ? o : me;
+        const float* av = axyz + 3 * (a0 + i);
+        const float ax = av[0], ay = av[1], az = av[2];
+        const float cd = cdist_mm(ax, ay, az, (ax * ax + ay * ay) + az * az, pxyz + 3 * (p0 + j));
+        const float f = base[(int64_t)i * np + j];
+        const bool pos = cd < r_p, neg = cd > r_n;
+        anyp |= pos;
+        anyn |= neg;
+        lse_push(mp, sp, pos ? kCircleScale * (f - kCirclePos) * fmaxf(f - kCirclePos, 0.f) : 0.f);
+        lse_push(mn, sn, neg ? kCircleScale * (kCircleNeg - f) * fmaxf(kCircleNeg - f, 0.f) : 0.f);
+    }
+    lse_wave(mp, sp);
+    lse_wave(mn, sn);
+    const bool sel = __any(anyp) && __any(anyn);
+    if (lane == 0) {
+        line_loss[w] = n_other > 0 ? softplus_t((mp + logf(sp)) + (mn + logf(sn))) / kCircleScale
+                                   : __builtin_nanf("");
+        line_sel[w] = sel ? 1.f : 0.f;
+    }
+}
+
+// per pair: (mean of the selected rows + mean of the selected columns) / 2 (0 / 0 = NaN for a
+// pair without one, as torch's mean of an empty selection), then the mean over the pairs
+__global__ void __launch_bounds__(kRed)
+circle_reduce_kernel(const float* __restrict__ line_loss, const float* __restrict__ line_sel,
+                     const int64_t* __restrict__ a_off, const int64_t* __restrict__ p_off,
+                     int n_pairs, float* __restrict__ out) {
+    const int64_t n_anchor = a_off[n_pairs];
+    float total = 0.f;
+    for (int b = 0; b < n_pairs; ++b) {
+        float v[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int64_t i = a_off[b] + threadIdx.x; i < a_off[b + 1]; i += blockDim.x) {
+            const bool sl = line_sel[i] != 0.f;
+            v[0] += sl ? line_loss[i] : 0.f;
+            v[1] += sl ? 1.f : 0.f;
+        }
+        for (int64_t j = p_off[b] + threadIdx.x; j < p_off[b + 1]; j += blockDim.x) {
+            const bool sl = line_sel[n_anchor + j] != 0.f;
+            v[2] += sl ? line_loss[n_anchor + j] : 0.f;
+            v[3] += sl ? 1.f : 0.f;
+        }
+        block_sum<4>(v);
+        total += (v[0] / v[1] + v[2] / v[3]) / 2.f;
+    }
+    if (threadIdx.x == 0) out[0] = total / (float)n_pairs;
+}
+
 // CorrCriterion('mae') for both directions of finegrained_regtr.py:283-296: rows of cloud
 // c < B are compared with pose[c] applied to the coarse point, rows of tgt cloud c with
 // se3_inv(pose[c - B]); err = |dx| + |dy| + |dz|; each direction is an overlap-weighted mean
@@ -320,6 +457,51 @@ extern "C" int fgr_infonce_reduce(const float* row_loss, const float* row_mask,
     hipLaunchKernelGGL(infonce_reduce_kernel, dim3(1), dim3(kRed), 0, as_stream(stream), row_loss,
                        row_mask, a_off, n_pairs, out);
     FGR_CHECK_LAUNCH("infonce_reduce_kernel");
+    return FGR_OK;
+}
+
+extern "C" int fgr_circle_loss_workspace(int64_t fd_elems, int64_t n_anchor, int64_t n_pos,
+                                         size_t* bytes) {
+    FGR_REQUIRE(bytes && fd_elems >= 0 && n_anchor >= 0 && n_pos >= 0,
+                "fgr_circle_loss_workspace: bad arguments");
+    *bytes = (size_t)(fd_elems + 2 * (n_anchor + n_pos)) * sizeof(float);
+    return FGR_OK;
+}
+
+extern "C" int fgr_circle_loss(const float* anchor_feat, const float* pos_feat, int32_t d,
+                               const float* axyz, const float* pxyz, const int64_t* a_off,
+                               const int64_t* p_off, const int64_t* fd_off, int32_t n_pairs,
+                               int64_t n_anchor, int64_t n_pos, int32_t max_anchor,
+                               int32_t max_pos, int64_t fd_elems, float r_p, float r_n,
+                               void* ws, size_t ws_bytes, float* out, void* stream) {
+    FGR_REQUIRE(n_pairs > 0 && d > 0 && n_anchor >= 0 && n_pos >= 0 && max_anchor >= 0 &&
+                    max_pos >= 0 && fd_elems >= 0,
+                "fgr_circle_loss: bad arguments");
+    FGR_REQUIRE(anchor_feat && pos_feat && axyz && pxyz && a_off && p_off && fd_off && ws && out,
+                "fgr_circle_loss: null pointer");
+    size_t need = 0;
+    fgr_circle_loss_workspace(fd_elems, n_anchor, n_pos, &need);
+    FGR_REQUIRE(ws_bytes >= need, "fgr_circle_loss: workspace %zu < %zu bytes", ws_bytes, need);
+    hipStream_t st = as_stream(stream);
+    float* fd = static_cast<float*>(ws);
+    float* line_loss = fd + fd_elems;
+    float* line_sel = line_loss + (n_anchor + n_pos);
+    if (max_anchor > 0 && max_pos > 0) {
+        hipLaunchKernelGGL(circle_fd_kernel,
+                           dim3((unsigned)ceil_div(max_pos, kCdTile),
+                                (unsigned)ceil_div(max_anchor, kCdTile), (unsigned)n_pairs),
+                           dim3(256), 0, st, anchor_feat, pos_feat, d, a_off, p_off, fd_off, fd);
+        FGR_CHECK_LAUNCH("circle_fd_kernel");
+    }
+    if (n_anchor + n_pos > 0) {
+        hipLaunchKernelGGL(circle_lines_kernel, dim3((unsigned)ceil_div(n_anchor + n_pos, 4)),
+                           dim3(256), 0, st, (const float*)fd, axyz, pxyz, a_off, p_off, fd_off,
+                           n_pairs, n_anchor, n_pos, r_p, r_n, line_loss, line_sel);
+        FGR_CHECK_LAUNCH("circle_lines_kernel");
+    }
+    hipLaunchKernelGGL(circle_reduce_kernel, dim3(1), dim3(kRed), 0, st, (const float*)line_loss,
+                       (const float*)line_sel, a_off, p_off, n_pairs, out);
+    FGR_CHECK_LAUNCH("circle_reduce_kernel");
     return FGR_OK;
 }
 

@@ -13,6 +13,8 @@ on the packed forward outputs, so ``GenericRegModel.test_step`` runs at GPU spee
 Same keys, weights (finegrained_regtr.py:94-98) and reduction order as the reference; all
 arithmetic in fp32 on the GPU (no CPU path: the ops raise on CPU tensors).
 """
+import itertools
+
 import torch
 
 from . import _lib, ops
@@ -100,6 +102,32 @@ def infonce(W, anchor_feat, positive_feat, anchor_xyz, positive_xyz, a_off, p_of
     return out
 
 
+def circle(anchor_feat, positive_feat, anchor_xyz, positive_xyz, a_lens, p_lens, a_off, p_off,
+           r_p, r_n):
+    """CircleLossFull.forward (feature_loss.py:232-243, Euclidean feature distances as
+    finegrained_regtr.py:87 builds it) over B pairs packed along rows -> 0-d tensor
+    (fgr_circle_loss). a_lens / p_lens: host lengths of the pairs' anchor / positive rows."""
+    _dev(anchor_feat, positive_feat, anchor_xyz, positive_xyz, a_off, p_off)
+    A = _c(anchor_feat, torch.float32)
+    P = _c(positive_feat, torch.float32)
+    assert A.shape[1] == P.shape[1] and len(a_lens) == len(p_lens)
+    sizes = [a * b for a, b in zip(a_lens, p_lens)]
+    fd_off = torch.tensor([0] + list(itertools.accumulate(sizes)), dtype=torch.int64,
+                          device=A.device)
+    n_a, n_p, fd_elems = A.shape[0], P.shape[0], sum(sizes)
+    L = _lib.load()
+    nb = _lib._sz(0)
+    _lib.check(L.fgr_circle_loss_workspace(fd_elems, n_a, n_p, nb), 'fgr_circle_loss_workspace')
+    ws = torch.empty(nb.value, dtype=torch.uint8, device=A.device)
+    out = torch.empty((), dtype=torch.float32, device=A.device)
+    axyz, pxyz = _c(anchor_xyz, torch.float32), _c(positive_xyz, torch.float32)
+    _lib.check(L.fgr_circle_loss(_ptr(A), _ptr(P), A.shape[1], _ptr(axyz), _ptr(pxyz),
+                                 _ptr(a_off), _ptr(p_off), _ptr(fd_off), len(a_lens), n_a, n_p,
+                                 max(a_lens), max(p_lens), fd_elems, float(r_p), float(r_n),
+                                 _ptr(ws), nb.value, _ptr(out), _stream()), 'fgr_circle_loss')
+    return out
+
+
 def corr_loss(xyz, corr, w, seg_off, pose) -> torch.Tensor:
     """src (pose) + tgt (se3_inv(pose)) CorrCriterion('mae') with overlap weights."""
     _dev(xyz, corr, w, seg_off, pose)
@@ -137,8 +165,10 @@ def compute_loss(model, pred, batch):
     """RegTR.compute_loss (finegrained_regtr.py:252-309) -> dict of 0-d tensors with the
     reference's keys; adds batch['overlap_pyr'] like the reference."""
     cfg = model.cfg
-    if cfg.get('feature_loss_type', 'infonce') != 'infonce':
-        raise NotImplementedError('only the infonce feature loss is in the reference configs')
+    ftype = cfg.get('feature_loss_type', 'infonce')
+    if ftype not in ('infonce', 'circle'):
+        raise NotImplementedError(f'feature_loss_type {ftype!r} (the reference builds infonce '
+                                  'and circle, finegrained_regtr.py:83-90)')
     meta = batch['kpconv_meta']
     pose_gt = _c(batch['pose'].float(), torch.float32)           # (B, 3, 4)
     p = len(meta['stack_lengths']) - 1
@@ -157,14 +187,19 @@ def compute_loss(model, pred, batch):
         losses[f'overlap_{i}'] = bce_with_logits_mean(logits[i, :, 0], ov)
     src_kp, tgt_kp = torch.cat(list(pred['src_kp'])), torch.cat(list(pred['tgt_kp']))
     axyz = transform_points(src_kp, a_off, pose_gt)
+    if ftype == 'circle':        # CircleLossFull for both feature losses (:87-88, no weights)
+        feat = lambda crit, a, pp: circle(a, pp, axyz, tgt_kp, lens[:B], lens[B:], a_off, p_off,
+                                          cfg.r_p, cfg.r_n)
+    else:
+        feat = lambda crit, a, pp: infonce(crit.W, a, pp, axyz, tgt_kp, a_off, p_off, cfg.r_p,
+                                           cfg.r_n)
     for i in cfg.feature_loss_on:
-        losses[f'feature_{i}'] = infonce(
-            model.feature_criterion.W, torch.cat([s[i] for s in pred['src_feat']]),
-            torch.cat([t[i] for t in pred['tgt_feat']]), axyz, tgt_kp, a_off, p_off,
-            cfg.r_p, cfg.r_n)
-    losses['feature_un'] = infonce(
-        model.feature_criterion_un.W, torch.cat(list(pred['src_feat_un'])),
-        torch.cat(list(pred['tgt_feat_un'])), axyz, tgt_kp, a_off, p_off, cfg.r_p, cfg.r_n)
+        losses[f'feature_{i}'] = feat(getattr(model, 'feature_criterion', None),
+                                      torch.cat([s[i] for s in pred['src_feat']]),
+                                      torch.cat([t[i] for t in pred['tgt_feat']]))
+    losses['feature_un'] = feat(getattr(model, 'feature_criterion_un', None),
+                                torch.cat(list(pred['src_feat_un'])),
+                                torch.cat(list(pred['tgt_feat_un'])))
     xyz = torch.cat([src_kp, tgt_kp])
     for i in cfg.corr_loss_on:
         corr = torch.cat([w[i] for w in pred['src_kp_warped']] +
@@ -196,8 +231,10 @@ def compute_loss_train(model, pred, batch):
     import torch.nn.functional as F
     from .autograd import linear_t
     cfg = model.cfg
-    if cfg.get('feature_loss_type', 'infonce') != 'infonce':
-        raise NotImplementedError('only the infonce feature loss is in the reference configs')
+    ftype = cfg.get('feature_loss_type', 'infonce')
+    if ftype not in ('infonce', 'circle'):
+        raise NotImplementedError(f'feature_loss_type {ftype!r} (the reference builds infonce '
+                                  'and circle, finegrained_regtr.py:83-90)')
     meta = batch['kpconv_meta']
     pose = batch['pose'].float()
     p = len(meta['stack_lengths']) - 1
@@ -231,20 +268,42 @@ def compute_loss_train(model, pred, batch):
         per_row = torch.logsumexp(logits, dim=1) - logits[rows, j1]
         return per_row[keep].sum() / keep.sum()
 
+    def circle_pair(a, pp, a_xyz, p_xyz):
+        # CircleLossFull.get_circle_loss (feature_loss.py:191-230), Euclidean feature distances
+        # by the Gram form on the differentiable f16x3 GEMM (|a|^2 + |p|^2 - 2 a.p, clamped);
+        # non-positive / non-negative entries contribute exp(0) = 1 as in the reference (its
+        # +-1e5 shift is multiplied by a zero weight), the weights are detached as there
+        sq = (a * a).sum(1)[:, None] + (pp * pp).sum(1)[None, :] - 2.0 * linear_t(a, pp, cache=False)
+        fd = torch.sqrt(torch.clamp_min(sq, 0.0) + 1e-12)
+        with torch.no_grad():
+            cd = torch.cdist(a_xyz, p_xyz)
+            pos, neg = cd < cfg.r_p, cd > cfg.r_n
+            wp = torch.clamp_min(fd - 0.1, 0.0)
+            wn = torch.clamp_min(1.4 - fd, 0.0)
+        zero = torch.zeros_like(fd)
+        tp = torch.where(pos, 10.0 * (fd - 0.1) * wp, zero)
+        tn = torch.where(neg, 10.0 * (1.4 - fd) * wn, zero)
+        row = F.softplus(torch.logsumexp(tp, 1) + torch.logsumexp(tn, 1)) / 10.0
+        col = F.softplus(torch.logsumexp(tp, 0) + torch.logsumexp(tn, 0)) / 10.0
+        return (row[pos.any(1) & neg.any(1)].mean() + col[pos.any(0) & neg.any(0)].mean()) / 2
+
     losses = {}
     logits = torch.cat(list(pred['src_overlap']) + list(pred['tgt_overlap']), dim=-2)
     for i in cfg.overlap_loss_on:
         losses[f'overlap_{i}'] = F.binary_cross_entropy_with_logits(logits[i, :, 0], ov)
     a_xyz = [rigid(pose[b], pred['src_kp'][b]) for b in range(B)]
+    if ftype == 'circle':
+        feat = lambda crit, a, pp, b: circle_pair(a, pp, a_xyz[b], pred['tgt_kp'][b])
+    else:
+        feat = lambda crit, a, pp, b: infonce_pair(w_sym(crit.W), a, pp, a_xyz[b],
+                                                   pred['tgt_kp'][b])
     for i in cfg.feature_loss_on:
-        Ws = w_sym(model.feature_criterion.W)
+        crit = getattr(model, 'feature_criterion', None)
         losses[f'feature_{i}'] = torch.stack([
-            infonce_pair(Ws, pred['src_feat'][b][i], pred['tgt_feat'][b][i], a_xyz[b],
-                         pred['tgt_kp'][b]) for b in range(B)]).mean()
-    Wu = w_sym(model.feature_criterion_un.W)
+            feat(crit, pred['src_feat'][b][i], pred['tgt_feat'][b][i], b) for b in range(B)]).mean()
+    crit = getattr(model, 'feature_criterion_un', None)
     losses['feature_un'] = torch.stack([
-        infonce_pair(Wu, pred['src_feat_un'][b], pred['tgt_feat_un'][b], a_xyz[b],
-                     pred['tgt_kp'][b]) for b in range(B)]).mean()
+        feat(crit, pred['src_feat_un'][b], pred['tgt_feat_un'][b], b) for b in range(B)]).mean()
 
     def corr_mae(kp, warped, poses, weights):
         gt = torch.cat([rigid(poses[b], kp[b]) for b in range(len(kp))])

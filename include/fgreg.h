@@ -391,6 +391,16 @@ int fgr_pair_pose(const float* xyz, const float* corr, const float* logits, int6
  *                       row_mask = (its distance < r_p), points closer than r_n ignored,
  *                       row_loss = logsumexp - positive logit;
  *  fgr_infonce_reduce   sum(loss[mask]) / sum(mask) per pair, mean over pairs (:295, 314);
+ *  fgr_circle_loss      CircleLossFull.forward (feature_loss.py:160-243) with Euclidean feature
+ *                       distances (feature_loss_type: circle, finegrained_regtr.py:86-88) over
+ *                       n_pairs pairs packed along rows (anchor rows a_off[b]..a_off[b+1] of
+ *                       anchor_feat (n_anchor, d) / axyz, positive rows p_off[b]..p_off[b+1]);
+ *                       fd_off[b] = sum_{b' < b} n_a(b') n_p(b') (int64, device), fd_elems its
+ *                       total; max_anchor / max_pos the largest per-pair counts; the workspace
+ *                       holds the per-pair distance matrices and per-line losses
+ *                       (fgr_circle_loss_workspace bytes); out = the 0-d loss (NaN for a pair
+ *                       with no row or no column holding both a positive and a negative, as
+ *                       the reference's mean over an empty selection);
  *  fgr_corr_loss        CorrCriterion('mae') for src (pose) + tgt (se3_inv(pose)) directions
  *                       with overlap weights w (corr_loss.py:18-38, finegrained_regtr.py:283-296);
  *  fgr_se3_compare      se3_compare(pred[l, b], gt[b]) (se3_torch.py:117-129) -> rotation
@@ -407,6 +417,12 @@ int fgr_infonce_rows(const float* logits, int64_t ld, const float* axyz, const f
                      float r_p, float r_n, float* row_loss, float* row_mask, void* stream);
 int fgr_infonce_reduce(const float* row_loss, const float* row_mask, const int64_t* a_off,
                        int32_t n_pairs, float* out, void* stream);
+int fgr_circle_loss_workspace(int64_t fd_elems, int64_t n_anchor, int64_t n_pos, size_t* bytes);
+int fgr_circle_loss(const float* anchor_feat, const float* pos_feat, int32_t d, const float* axyz,
+                    const float* pxyz, const int64_t* a_off, const int64_t* p_off,
+                    const int64_t* fd_off, int32_t n_pairs, int64_t n_anchor, int64_t n_pos,
+                    int32_t max_anchor, int32_t max_pos, int64_t fd_elems, float r_p, float r_n,
+                    void* ws, size_t ws_bytes, float* out, void* stream);
 int fgr_corr_loss(const float* xyz, const float* corr, const float* w, const int64_t* seg_off,
                   int32_t n_pairs, const float* pose, float* out, void* stream);
 int fgr_se3_compare(const float* pred, const float* gt, int32_t n_layers, int32_t n_pairs,

@@ -9,6 +9,8 @@ Restated (PyTorch CPU, fp32 unless noted):
 * compute_overlaps      models/backbone_kpconv/finegrained_kpconv.py:545-571
 * RegTR.compute_loss    models/finegrained_regtr.py:252-309
 * InfoNCELossFull       models/losses/feature_loss.py:246-314
+* CircleLossFull        models/losses/feature_loss.py:160-243 (feature_loss_type: circle,
+                        finegrained_regtr.py:86-88; pinned by loss_circle_modelnet_small.npz)
 * CorrCriterion('mae')  models/losses/corr_loss.py:8-38
 * se3_compare           utils/se3_torch.py:117-129 (via generic_reg_model.py:203-215)
 """
@@ -56,6 +58,29 @@ def infonce_pair(W, a_feat, p_feat, a_xyz, p_xyz, r_p, r_n):
     return per_row[keep].sum() / keep.sum()
 
 
+def circle_pair(a_feat, p_feat, a_xyz, p_xyz, r_p, r_n, log_scale=10.0, pos_margin=0.1,
+                neg_margin=1.4):
+    """CircleLossFull of one pair with Euclidean feature distances (sqrt(sum of squared
+    differences + 1e-12)). Positives: point distance < r_p, negatives: > r_n. The reference masks
+    by shifting the distances by -/+1e5 and then multiplies by a clamped weight that is 0 on the
+    masked entries, so every non-positive (non-negative) entry adds exp(0) = 1 to the positive
+    (negative) log-sum-exp. Rows / columns with at least one positive and one negative are
+    averaged; the weights are constants for the gradient (detached)."""
+    cd = torch.cdist(a_xyz, p_xyz)
+    fd = torch.sqrt(((a_feat[:, None, :] - p_feat[None, :, :]) ** 2).sum(-1) + 1e-12)
+    pos, neg = cd < r_p, cd > r_n
+    wp = torch.clamp_min(fd - pos_margin, 0.0).detach()
+    wn = torch.clamp_min(neg_margin - fd, 0.0).detach()
+    zero = torch.zeros_like(fd)
+    tp = torch.where(pos, log_scale * (fd - pos_margin) * wp, zero)
+    tn = torch.where(neg, log_scale * (neg_margin - fd) * wn, zero)
+    row = F.softplus(torch.logsumexp(tp, 1) + torch.logsumexp(tn, 1)) / log_scale
+    col = F.softplus(torch.logsumexp(tp, 0) + torch.logsumexp(tn, 0)) / log_scale
+    row_sel = pos.any(1) & neg.any(1)
+    col_sel = pos.any(0) & neg.any(0)
+    return (row[row_sel].mean() + col[col_sel].mean()) / 2
+
+
 def corr_mae(kp, kp_warped, poses, weights):
     """sum_i w_i |warped_i - T(kp_i)|_1 / max(sum w, 1e-6) over all pairs' rows."""
     gt = torch.cat([rigid_apply(poses[b], kp[b]) for b in range(len(kp))])
@@ -98,13 +123,17 @@ def compute_loss(cfg, W, W_un, pred, batch):
     for i in cfg.overlap_loss_on:
         losses[f'overlap_{i}'] = F.binary_cross_entropy_with_logits(logits[i, :, 0], ov)
     a_xyz = [rigid_apply(pose[b], pred['src_kp'][b]) for b in range(B)]
+    if cfg.get('feature_loss_type', 'infonce') == 'circle':
+        feat = lambda Wm, a, pp, b: circle_pair(a, pp, a_xyz[b], pred['tgt_kp'][b], cfg.r_p,
+                                                cfg.r_n)
+    else:
+        feat = lambda Wm, a, pp, b: infonce_pair(Wm, a, pp, a_xyz[b], pred['tgt_kp'][b],
+                                                 cfg.r_p, cfg.r_n)
     for i in cfg.feature_loss_on:
         losses[f'feature_{i}'] = torch.stack([
-            infonce_pair(W, pred['src_feat'][b][i], pred['tgt_feat'][b][i], a_xyz[b],
-                         pred['tgt_kp'][b], cfg.r_p, cfg.r_n) for b in range(B)]).mean()
+            feat(W, pred['src_feat'][b][i], pred['tgt_feat'][b][i], b) for b in range(B)]).mean()
     losses['feature_un'] = torch.stack([
-        infonce_pair(W_un, pred['src_feat_un'][b], pred['tgt_feat_un'][b], a_xyz[b],
-                     pred['tgt_kp'][b], cfg.r_p, cfg.r_n) for b in range(B)]).mean()
+        feat(W_un, pred['src_feat_un'][b], pred['tgt_feat_un'][b], b) for b in range(B)]).mean()
     inv = torch.stack([rigid_inverse(pose[b]) for b in range(B)])
     for i in cfg.corr_loss_on:
         losses[f'corr_{i}'] = (

@@ -573,6 +573,33 @@ def make_loss(fr, fk):
     save('loss_modelnet_small', **arrays)
 
 
+def make_loss_circle(fr, fk):
+    """The same test-step tail with `feature_loss_type: circle` (finegrained_regtr.py:86-88:
+    CircleLossFull with Euclidean feature distances, feature_loss.py:160-243, for both the
+    per-layer and the un-transformed feature losses): the reference's own compute_loss on the
+    forward / loss inputs of loss_modelnet_small (that fixture's pose and overlap flags)."""
+    cfg = load_cfg('modelnet.yaml', feature_loss_type='circle', **SMALL_MODELNET)
+    pairs = [modelnet_like_pair(i, n_raw=512) for i in range(2)]
+    src = [p[0] for p in pairs]
+    tgt = [p[1] for p in pairs]
+    model, meta, out = run_forward(fr, fk, cfg, src, tgt)
+    ref = np.load(os.path.join(HERE, 'forward_modelnet_small.npz'))
+    for b in range(2):          # same forward as the committed fixture
+        assert np.array_equal(out['src_feat'][b].numpy(), ref[f'out.src_feat.{b}'])
+    lf = np.load(os.path.join(HERE, 'loss_modelnet_small.npz'))
+    batch = {'src_xyz': [torch.from_numpy(c) for c in src],
+             'tgt_xyz': [torch.from_numpy(c) for c in tgt],
+             'kpconv_meta': meta, 'pose': torch.from_numpy(lf['pose']),
+             'src_overlap': [torch.from_numpy(lf[f'src_overlap.{b}']) for b in range(2)],
+             'tgt_overlap': [torch.from_numpy(lf[f'tgt_overlap.{b}']) for b in range(2)]}
+    with torch.no_grad(), cuda_to_cpu():
+        losses = model.compute_loss(out, batch)
+    arrays = {}
+    for k, v in losses.items():
+        arrays[f'loss.{k}'] = np.float32(v.item())
+    save('loss_circle_modelnet_small', **arrays)
+
+
 # parameters whose full gradient is stored (one of every kind on the path); every other
 # parameter is pinned by its gradient's L2 norm and sum
 TRAIN_FULL_GRADS = (
@@ -649,6 +676,9 @@ if __name__ == '__main__':
     if sys.argv[1:] == ['loss']:
         make_loss(fr, fk)
         sys.exit(0)
+    if sys.argv[1:] == ['loss_circle']:
+        make_loss_circle(fr, fk)
+        sys.exit(0)
     if sys.argv[1:] == ['train']:
         make_train(fr, fk)
         sys.exit(0)
@@ -668,4 +698,5 @@ if __name__ == '__main__':
     make_forward_postnorm(fr, fk)
     make_decoder_topk(fr)
     make_loss(fr, fk)
+    make_loss_circle(fr, fk)
     make_train(fr, fk)

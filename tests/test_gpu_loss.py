@@ -137,3 +137,89 @@ def test_infonce_empty_mask_is_nan(gpu):
     assert torch.isnan(out.cpu())
     ref = lo.infonce_pair(W, A, P, axyz, pxyz, 0.12, 0.24)
     assert torch.isnan(ref)
+
+
+def _circle_cfg(cfg):
+    c = type(cfg)(cfg)
+    c['feature_loss_type'] = 'circle'
+    return c
+
+
+def test_circle_loss_on_reference_outputs(gpu):
+    """feature_loss_type: circle (finegrained_regtr.py:86-88, CircleLossFull with Euclidean
+    feature distances, feature_loss.py:160-243) on the reference's own forward outputs: the
+    eval path (fgr_circle_loss) and the differentiable training path (compute_loss_train)
+    against the reference's compute_loss with that option (loss_circle_modelnet_small.npz)."""
+    from conftest import golden
+    from fgreg import loss as fl
+    cfg, pred, batch, _, _, _, _, _ = loss_fixture(gpu)
+    cfg = _circle_cfg(cfg)
+    g = golden('loss_circle_modelnet_small')
+    ref = {k[5:]: float(g[k]) for k in g.files}
+    losses = fl.compute_loss(_Model(cfg, None, None), pred, batch)
+    assert list(losses) == list(ref)
+    for k, v in ref.items():
+        assert _close(float(losses[k]), v), (k, float(losses[k]), v)
+    m = _Model(cfg, None, None)
+    del m.feature_criterion, m.feature_criterion_un
+    losses_t = fl.compute_loss_train(m, pred, batch)
+    for k, v in ref.items():
+        assert _close(float(losses_t[k]), v, 1e-4), (k, float(losses_t[k]), v)
+
+
+def test_circle_loss_gradients_vs_oracle(gpu):
+    """The training path's gradients of the circle feature losses w.r.t. the features against
+    torch autograd of the oracle's restatement in fp64 (1e-3 relative Frobenius: the Gram-form
+    distances on the f16x3 GEMM vs the explicit differences)."""
+    from fgreg import loss as fl
+    cfg, pred, batch, _, _, _, _, _ = loss_fixture(gpu)
+    cfg = _circle_cfg(cfg)
+    keys = ('src_feat', 'tgt_feat', 'src_feat_un', 'tgt_feat_un')
+    pg = {k: [t.detach().clone().requires_grad_(True) for t in pred[k]] for k in keys}
+    pred_g = dict(pred, **pg)
+    m = _Model(cfg, None, None)
+    del m.feature_criterion, m.feature_criterion_un
+    losses = fl.compute_loss_train(m, pred_g, batch)
+    (losses['feature_un'] + sum(losses[f'feature_{i}'] for i in cfg.feature_loss_on)).backward()
+    B = len(pred['src_kp'])
+    pose = batch['pose'].cpu().double()
+    pc = {k: [t.detach().cpu().double().requires_grad_(True) for t in pred[k]] for k in keys}
+    a_xyz = [lo.rigid_apply(pose[b], pred['src_kp'][b].cpu().double()) for b in range(B)]
+    p_xyz = [t.cpu().double() for t in pred['tgt_kp']]
+    tot = 0
+    for i in cfg.feature_loss_on:
+        tot = tot + torch.stack([lo.circle_pair(pc['src_feat'][b][i], pc['tgt_feat'][b][i],
+                                                a_xyz[b], p_xyz[b], cfg.r_p, cfg.r_n)
+                                 for b in range(B)]).mean()
+    tot = tot + torch.stack([lo.circle_pair(pc['src_feat_un'][b], pc['tgt_feat_un'][b], a_xyz[b],
+                                            p_xyz[b], cfg.r_p, cfg.r_n) for b in range(B)]).mean()
+    tot.backward()
+    for k in keys:
+        for b in range(B):
+            got, want = pg[k][b].grad.cpu().double(), pc[k][b].grad
+            assert float((got - want).norm()) <= 1e-3 * float(want.norm()) + 1e-12, (k, b)
+
+
+def test_circle_loss_full_size_vs_oracle(gpu):
+    """ModelNet B = 8 sizes (random features of d = 256, ~600 keypoints per cloud) through
+    fgr_circle_loss against the oracle; and a pair with no negative anywhere gives NaN."""
+    from fgreg import loss as fl
+    from fgreg import ops
+    g = torch.Generator().manual_seed(1)
+    B, d = 8, 256
+    na = [590 + 7 * b for b in range(B)]
+    npp = [600 - 5 * b for b in range(B)]
+    A = [torch.randn(n, d, generator=g) * 0.1 for n in na]
+    P = [torch.randn(n, d, generator=g) * 0.1 for n in npp]
+    ax = [torch.rand(n, 3, generator=g) for n in na]
+    px = [torch.rand(n, 3, generator=g) for n in npp]
+    T = lambda L: torch.cat(L).to(gpu)
+    out = fl.circle(T(A), T(P), T(ax), T(px), na, npp, ops.offsets(na, gpu), ops.offsets(npp, gpu),
+                    0.12, 0.24)
+    ref = torch.stack([lo.circle_pair(A[b], P[b], ax[b], px[b], 0.12, 0.24)
+                       for b in range(B)]).mean()
+    assert _close(float(out), float(ref)), (float(out), float(ref))
+    # r_n beyond every distance: no negatives -> empty selections -> NaN, as the reference
+    out = fl.circle(T(A[:1]), T(P[:1]), T(ax[:1]), T(px[:1]), na[:1], npp[:1],
+                    ops.offsets(na[:1], gpu), ops.offsets(npp[:1], gpu), 0.12, 10.0)
+    assert torch.isnan(out.cpu()) and torch.isnan(lo.circle_pair(A[0], P[0], ax[0], px[0], 0.12, 10.0))

@@ -162,6 +162,23 @@ def test_oracle_kpconv_and_instnorm_match_reference():
     assert rel_err(mo.instance_norm(T(n['x']), T(n['lengths'].astype(np.int64))), n['out']) < 1e-6
 
 
+def test_circle_loss_oracle_matches_reference():
+    """The oracle's CircleLossFull (feature_loss_type: circle) vs the reference's own
+    compute_loss with that option on the same forward outputs and loss inputs
+    (tests/golden/loss_circle_modelnet_small.npz)."""
+    import loss_oracle as lo
+    from conftest import loss_fixture, golden
+    cfg, pred, batch, _, _, _, W, W_un = loss_fixture()
+    cfg = type(cfg)(cfg)
+    cfg['feature_loss_type'] = 'circle'
+    g = golden('loss_circle_modelnet_small')
+    ref = {k[5:]: float(g[k]) for k in g.files}
+    losses, _ = lo.compute_loss(cfg, None, None, pred, batch)
+    assert set(losses) == set(ref)
+    for k, v in ref.items():
+        assert abs(float(losses[k]) - v) <= 1e-5 * max(1.0, abs(v)), (k, float(losses[k]), v)
+
+
 def test_loss_oracle_matches_reference():
     """oracle/loss_oracle.py vs the reference's own compute_loss / _compute_metrics on its
     own forward outputs (tests/golden/loss_modelnet_small.npz)."""
