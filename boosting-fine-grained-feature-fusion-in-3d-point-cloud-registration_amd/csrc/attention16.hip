@@ -27,6 +27,7 @@
 //   V: [term 2][key 64][DH] f16, 16-B chunk index XOR v_swz<DH>(key)
 // Tile t of kv segment s sits at tile index kv_off[s] / 64 + s + t; the (e_k, e_v) scale
 // exponents of all tiles follow the images.
+#include <algorithm>
 #include <type_traits>
 
 #include "common.h"
@@ -202,13 +203,17 @@ __device__ __forceinline__ void split8_pk(const float (&x)[8], float one, u32x4&
     l = u32x4{l0, l1, l2, l3};
 }
 
-template <int DH>
+// DROP (training only, fgr_attention_f16x3_drop): the softmax weights of the PV product are
+// masked by attn_drop_hash (common.h) -- the row sum l keeps every weight, and the kept ones
+// are scaled by 1 / (1 - p) with the final 1 / l (P stays <= 2^14 in fp16's range)
+template <int DH, bool DROP = false>
 __global__ void __launch_bounds__(256, DH == 64 ? 2 : 5)
 attn_f16x3_v2_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __restrict__ img,
                      const int2* __restrict__ sc, float* __restrict__ o, int64_t ld_o,
                      const int64_t* __restrict__ q_off, const int64_t* __restrict__ kv_off,
                      const int32_t* __restrict__ kv_seg, int n_head, int n_seg, int n_qblk,
-                     float scale_log2, int global_tiles) {
+                     float scale_log2, int global_tiles, uint32_t drop_seed = 0,
+                     uint32_t drop_thresh = 0, float inv_keep = 1.f) {
     constexpr int KD = DH / 32, TD = DH / 16;
     constexpr int UN = units<DH>();
     constexpr int PW = UN / 64 / 4;                              // DMA pieces per wave per tile
@@ -367,6 +372,11 @@ attn_f16x3_v2_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __r
                 const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[n][r], f, -m14));
                 s[n][r] = p;
                 rs += p;
+                if constexpr (DROP) {
+                    // packed key row of this entry (tile-local key 16n + 4g + r)
+                    const int64_t key = kb - lead + (int64_t)tt * 64 + 16 * n + 4 * g + r;
+                    if (attn_drop_hash(drop_seed, head, qrow, key) < drop_thresh) s[n][r] = 0.f;
+                }
             }
         l_run = l_run * alpha + rs;
 
@@ -426,7 +436,7 @@ attn_f16x3_v2_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __r
     }
 
     // O^T (dh 16t + 4g + r, query c) / l (both in 2^14 units)
-    const float inv = 1.0f / xg_sum16(l_run);
+    const float inv = (DROP ? inv_keep : 1.0f) / xg_sum16(l_run);
     if (qrow < qe) {
 #pragma unroll
         for (int t = 0; t < TD; ++t) {
@@ -455,13 +465,13 @@ extern "C" int fgr_attention_f16x3_workspace(int64_t n_kv_rows, int32_t n_kv_seg
     return FGR_OK;
 }
 
-extern "C" int fgr_attention_f16x3(const float* q, int64_t ld_q, const float* k, int64_t ld_k,
-                                   const float* v, int64_t ld_v, float* o, int64_t ld_o,
-                                   const int64_t* q_off, const int64_t* kv_off,
-                                   const int32_t* kv_seg, int32_t n_seg, int32_t n_kv_seg,
-                                   int64_t n_kv_rows, int32_t max_q_len, int32_t max_kv_len,
-                                   int32_t n_head, int32_t head_dim, float scale,
-                                   void* workspace, int64_t ws_bytes, void* stream) {
+static int attention_f16x3_impl(const float* q, int64_t ld_q, const float* k, int64_t ld_k,
+                                const float* v, int64_t ld_v, float* o, int64_t ld_o,
+                                const int64_t* q_off, const int64_t* kv_off,
+                                const int32_t* kv_seg, int32_t n_seg, int32_t n_kv_seg,
+                                int64_t n_kv_rows, int32_t max_q_len, int32_t max_kv_len,
+                                int32_t n_head, int32_t head_dim, float scale, void* workspace,
+                                int64_t ws_bytes, uint32_t drop_seed, float drop_p, void* stream) {
     FGR_REQUIRE(q && k && v && o && q_off && kv_off && kv_seg && workspace && n_seg > 0 &&
                     n_kv_seg > 0 && n_head > 0 && max_q_len >= 0 && max_kv_len >= 0,
                 "fgr_attention_f16x3: bad arguments");
@@ -497,16 +507,54 @@ extern "C" int fgr_attention_f16x3(const float* q, int64_t ld_q, const float* k,
     const int n_qblk = (int)ceil_div(max_q_len, 64);
     const int64_t n_blocks = ceil_div((int64_t)n_seg * n_head, 8) * 8 * n_qblk;
     const float sl2 = scale * 1.4426950408889634f;
-    if (dh == 32)
+    if (drop_p > 0.f) {
+        const uint32_t thresh = (uint32_t)std::min(4294967295.0, (double)drop_p * 4294967296.0);
+        const float inv_keep = 1.0f / (1.0f - drop_p);
+        if (dh == 32)
+            hipLaunchKernelGGL((attn_f16x3_v2_kernel<32, true>), dim3((unsigned)n_blocks), dim3(256), 0,
+                               st, q, ld_q, (const uint4*)img, (const int2*)sc, o, ld_o, q_off, kv_off,
+                               kv_seg, n_head, n_seg, n_qblk, sl2, 0, drop_seed, thresh, inv_keep);
+        else
+            hipLaunchKernelGGL((attn_f16x3_v2_kernel<64, true>), dim3((unsigned)n_blocks), dim3(256), 0,
+                               st, q, ld_q, (const uint4*)img, (const int2*)sc, o, ld_o, q_off, kv_off,
+                               kv_seg, n_head, n_seg, n_qblk, sl2, 0, drop_seed, thresh, inv_keep);
+    } else if (dh == 32) {
         hipLaunchKernelGGL((attn_f16x3_v2_kernel<32>), dim3((unsigned)n_blocks), dim3(256), 0, st, q,
                            ld_q, (const uint4*)img, (const int2*)sc, o, ld_o, q_off, kv_off, kv_seg,
-                           n_head, n_seg, n_qblk, sl2, 0);
-    else
+                           n_head, n_seg, n_qblk, sl2, 0, 0u, 0u, 1.f);
+    } else {
         hipLaunchKernelGGL((attn_f16x3_v2_kernel<64>), dim3((unsigned)n_blocks), dim3(256), 0, st, q,
                            ld_q, (const uint4*)img, (const int2*)sc, o, ld_o, q_off, kv_off, kv_seg,
-                           n_head, n_seg, n_qblk, sl2, 0);
+                           n_head, n_seg, n_qblk, sl2, 0, 0u, 0u, 1.f);
+    }
     FGR_CHECK_LAUNCH("attn_f16x3_v2_kernel");
     return FGR_OK;
+}
+
+extern "C" int fgr_attention_f16x3(const float* q, int64_t ld_q, const float* k, int64_t ld_k,
+                                   const float* v, int64_t ld_v, float* o, int64_t ld_o,
+                                   const int64_t* q_off, const int64_t* kv_off,
+                                   const int32_t* kv_seg, int32_t n_seg, int32_t n_kv_seg,
+                                   int64_t n_kv_rows, int32_t max_q_len, int32_t max_kv_len,
+                                   int32_t n_head, int32_t head_dim, float scale,
+                                   void* workspace, int64_t ws_bytes, void* stream) {
+    return attention_f16x3_impl(q, ld_q, k, ld_k, v, ld_v, o, ld_o, q_off, kv_off, kv_seg, n_seg,
+                                n_kv_seg, n_kv_rows, max_q_len, max_kv_len, n_head, head_dim,
+                                scale, workspace, ws_bytes, 0u, 0.f, stream);
+}
+
+extern "C" int fgr_attention_f16x3_drop(const float* q, int64_t ld_q, const float* k, int64_t ld_k,
+                                        const float* v, int64_t ld_v, float* o, int64_t ld_o,
+                                        const int64_t* q_off, const int64_t* kv_off,
+                                        const int32_t* kv_seg, int32_t n_seg, int32_t n_kv_seg,
+                                        int64_t n_kv_rows, int32_t max_q_len, int32_t max_kv_len,
+                                        int32_t n_head, int32_t head_dim, float scale,
+                                        void* workspace, int64_t ws_bytes, uint32_t seed,
+                                        float p, void* stream) {
+    FGR_REQUIRE(p >= 0.f && p < 1.f, "fgr_attention_f16x3_drop: dropout p %f not in [0, 1)", p);
+    return attention_f16x3_impl(q, ld_q, k, ld_k, v, ld_v, o, ld_o, q_off, kv_off, kv_seg, n_seg,
+                                n_kv_seg, n_kv_rows, max_q_len, max_kv_len, n_head, head_dim,
+                                scale, workspace, ws_bytes, seed, p, stream);
 }
 
 // The attention on K / V images of GLOBAL 64-row tiles written by fgr_gemm_f16x3_ln_qkv (head
@@ -537,10 +585,12 @@ extern "C" int fgr_attention_f16x3_img(const float* q, int64_t ld_q, const void*
     const float sl2 = scale * 1.4426950408889634f;
     if (head_dim == 32)
         hipLaunchKernelGGL((attn_f16x3_v2_kernel<32>), dim3((unsigned)n_blocks), dim3(256), 0, st, q, ld_q,
-                           img, sc, o, ld_o, q_off, kv_off, kv_seg, n_head, n_seg, n_qblk, sl2, 1);
+                           img, sc, o, ld_o, q_off, kv_off, kv_seg, n_head, n_seg, n_qblk, sl2, 1,
+                           0u, 0u, 1.f);
     else
         hipLaunchKernelGGL((attn_f16x3_v2_kernel<64>), dim3((unsigned)n_blocks), dim3(256), 0, st, q, ld_q,
-                           img, sc, o, ld_o, q_off, kv_off, kv_seg, n_head, n_seg, n_qblk, sl2, 1);
+                           img, sc, o, ld_o, q_off, kv_off, kv_seg, n_head, n_seg, n_qblk, sl2, 1,
+                           0u, 0u, 1.f);
     FGR_CHECK_LAUNCH("attn_f16x3_v2_kernel (global tiles)");
     return FGR_OK;
 }

@@ -159,4 +159,20 @@ __device__ __forceinline__ void split8_f16(const float (&x)[8], float sc, u32x4&
     l = u32x4{l0, l1, l2, l3};
 }
 
+// Attention-weight dropout in training (nn.MultiheadAttention(dropout = p), transformers.py:
+// 95-96): entry (head, query row, key row) of the softmax weights is dropped iff
+// attn_drop_hash(seed, head, q, k) < thresh = p * 2^32 (rows are the packed token rows). A
+// counter-based hash, so the forward and the two backward kernels draw the same mask without
+// storing it (fgreg/autograd.py restates it for the tests). Not torch's Philox stream: masks
+// differ from the reference's draw-for-draw, the distribution is the same (Bernoulli(1 - p)
+// per entry, kept entries scaled by 1 / (1 - p)).
+__device__ __forceinline__ uint32_t attn_drop_hash(uint32_t seed, int head, int64_t q, int64_t k) {
+    uint32_t x = seed ^ ((uint32_t)head * 0x9E3779B9u);
+    x ^= (uint32_t)q * 0x85EBCA6Bu;
+    x = (x ^ (x >> 16)) * 0x7FEB352Du;
+    x ^= (uint32_t)k * 0xC2B2AE35u;
+    x = (x ^ (x >> 15)) * 0x846CA68Bu;
+    return x ^ (x >> 16);
+}
+
 }  // namespace fgr

@@ -575,6 +575,10 @@ struct AttnBwd {
     float scale;
     float* lse;      // (Nq, nhead)
     float* dsum;     // (Nq, nhead)
+    // attention-weight dropout (MFMA kernels, DROP): entries with attn_drop_hash < drop_thresh
+    // are dropped, kept ones scaled by inv_keep (the forward's mask: fgr_attention_f16x3_drop)
+    uint32_t drop_seed, drop_thresh;
+    float inv_keep;
 };
 
 template <int DH>
@@ -766,7 +770,9 @@ __device__ __forceinline__ void stage_rows(float* dst, const float* src, int64_t
     }
 }
 
-template <int DH>
+// DROP: with M the forward's scaled mask (0 or 1 / (1 - p)), O = (P o M) V, so dV = (P o M)^T dO,
+// dP = M o (dO V^T) and dS = P o (dP - D) with D = rowsum(dO o O) unchanged.
+template <int DH, bool DROP = false>
 __global__ void __launch_bounds__(256)
 attn_bwd_dq_mfma_kernel(AttnBwd a) {
     constexpr int KS = DH / 4, DT = DH / 16, LD = DH + 4;
@@ -837,7 +843,11 @@ attn_bwd_dq_mfma_kernel(AttnBwd a) {
             for (int rr = 0; rr < 4; ++rr) {
                 const bool in = 16 * n + 4 * g + rr < nt;
                 const float p = in ? __builtin_amdgcn_exp2f(s4[rr] - lse2) : 0.f;
-                ds[n][rr] = p * (p4[rr] - dsum);
+                float dp = p4[rr];
+                if constexpr (DROP)
+                    dp = attn_drop_hash(a.drop_seed, h, r, t0 + 16 * n + 4 * g + rr) < a.drop_thresh
+                             ? 0.f : dp * a.inv_keep;
+                ds[n][rr] = p * (dp - dsum);
             }
         }
 #pragma unroll
@@ -863,7 +873,7 @@ attn_bwd_dq_mfma_kernel(AttnBwd a) {
     }
 }
 
-template <int DH>
+template <int DH, bool DROP = false>
 __global__ void __launch_bounds__(256)
 attn_bwd_dkdv_mfma_kernel(AttnBwd a) {
     constexpr int KS = DH / 4, DT = DH / 16, LD = DH + 4;
@@ -910,8 +920,16 @@ attn_bwd_dkdv_mfma_kernel(AttnBwd a) {
 #pragma unroll
                 for (int rr = 0; rr < 4; ++rr) {
                     const int qi = 16 * n + 4 * g + rr;
-                    p[n][rr] = __builtin_amdgcn_exp2f(s4[rr] - lt[qi]);
-                    ds[n][rr] = p[n][rr] * (d4[rr] - st[qi]);
+                    const float pv = __builtin_amdgcn_exp2f(s4[rr] - lt[qi]);
+                    if constexpr (DROP) {
+                        const float mk = attn_drop_hash(a.drop_seed, h, t0 + qi, rk) < a.drop_thresh
+                                             ? 0.f : a.inv_keep;
+                        p[n][rr] = pv * mk;                    // dV uses the dropped weights
+                        ds[n][rr] = pv * (d4[rr] * mk - st[qi]);
+                    } else {
+                        p[n][rr] = pv;
+                        ds[n][rr] = pv * (d4[rr] - st[qi]);
+                    }
                 }
             }
             // dV^T += dO^T P, dK^T += Q^T dS (k-step (n, r): query 16n + 4g + r)
@@ -1404,13 +1422,14 @@ extern "C" int fgr_attention_bwd_workspace(int64_t nq, int32_t nhead, size_t* by
     return FGR_OK;
 }
 
-extern "C" int fgr_attention_bwd(const float* q, int64_t ldq, const float* k, int64_t ldk, const float* v,
-                                 int64_t ldv, const float* o, int64_t ldo, const float* dout,
-                                 int64_t lddo, float* dq, int64_t lddq, float* dk, int64_t lddk,
-                                 float* dv, int64_t lddv, const int64_t* q_off, const int64_t* kv_off,
-                                 const int32_t* kv_seg, int32_t n_seg, int32_t n_kv_seg, int64_t nq,
-                                 int64_t max_q_len, int64_t max_kv_len, int32_t nhead, int32_t dh,
-                                 float scale, void* ws, size_t ws_bytes, void* stream) {
+static int attention_bwd_impl(const float* q, int64_t ldq, const float* k, int64_t ldk,
+                              const float* v, int64_t ldv, const float* o, int64_t ldo,
+                              const float* dout, int64_t lddo, float* dq, int64_t lddq, float* dk,
+                              int64_t lddk, float* dv, int64_t lddv, const int64_t* q_off,
+                              const int64_t* kv_off, const int32_t* kv_seg, int32_t n_seg,
+                              int32_t n_kv_seg, int64_t nq, int64_t max_q_len, int64_t max_kv_len,
+                              int32_t nhead, int32_t dh, float scale, void* ws, size_t ws_bytes,
+                              uint32_t drop_seed, float drop_p, void* stream) {
     FGR_REQUIRE(n_seg > 0 && n_kv_seg > 0 && nhead > 0 && nq >= 0 &&
                     (dh == 4 || dh == 8 || dh == 16 || dh == 32 || dh == 64),
                 "fgr_attention_bwd: bad arguments (head dim 4 / 8 / 16 / 32 / 64)");
@@ -1422,7 +1441,10 @@ extern "C" int fgr_attention_bwd(const float* q, int64_t ldq, const float* k, in
     AttnBwd a{q, ldq, k, ldk, v, ldv, o, ldo, dout, lddo, dq, lddq, dk, lddk, dv, lddv, q_off, kv_off,
               kv_seg, n_seg, n_kv_seg, nhead, (int)std::max<int64_t>(1, ceil_div(max_q_len, 64)),
               (int)std::max<int64_t>(1, ceil_div(max_kv_len, 64)), scale, (float*)ws,
-              (float*)ws + std::max<int64_t>(nq, 1) * nhead};
+              (float*)ws + std::max<int64_t>(nq, 1) * nhead, drop_seed,
+              (uint32_t)std::min(4294967295.0, (double)drop_p * 4294967296.0),
+              drop_p > 0.f ? 1.0f / (1.0f - drop_p) : 1.f};
+    const bool drop = drop_p > 0.f;
     hipStream_t st = as_stream(stream);
     dim3 g1((unsigned)(n_seg * a.q_blocks), nhead), g2((unsigned)(n_kv_seg * a.kv_blocks), nhead);
     // head dim 16 / 32 / 64 with 16-B aligned rows: the fp32-MFMA kernels (FGR_ATTN_BWD=scalar:
@@ -1433,7 +1455,23 @@ extern "C" int fgr_attention_bwd(const float* q, int64_t ldq, const float* k, in
                       reinterpret_cast<uintptr_t>(dk) | reinterpret_cast<uintptr_t>(dv)) & 15) == 0 &&
                     (ldq | ldk | ldv | ldo | lddo | lddq | lddk | lddv) % 4 == 0;
     static const bool scalar_only = [] { const char* e = getenv("FGR_ATTN_BWD"); return e && e[0] == 's'; }();
-    if (al && !scalar_only && (dh == 16 || dh == 32 || dh == 64)) {
+    const bool mfma = al && !scalar_only && (dh == 16 || dh == 32 || dh == 64);
+    FGR_REQUIRE(!drop || (al && (dh == 16 || dh == 32 || dh == 64)),
+                "fgr_attention_bwd_drop: dropout needs head dim 16 / 32 / 64 and 16-B aligned rows");
+    if (drop) {
+        switch (dh) {
+#define ATD(D) case D: \
+            hipLaunchKernelGGL((attn_bwd_dq_mfma_kernel<D, true>), g1, dim3(256), 0, st, a); \
+            FGR_CHECK_LAUNCH("attn_bwd_dq_mfma_kernel"); \
+            hipLaunchKernelGGL((attn_bwd_dkdv_mfma_kernel<D, true>), g2, dim3(256), 0, st, a); \
+            break;
+            ATD(16) ATD(32) ATD(64)
+#undef ATD
+        }
+        FGR_CHECK_LAUNCH("attn_bwd_dkdv_mfma_kernel");
+        return FGR_OK;
+    }
+    if (mfma) {
         switch (dh) {
 #define ATM(D) case D: \
             hipLaunchKernelGGL(attn_bwd_dq_mfma_kernel<D>, g1, dim3(256), 0, st, a); \
@@ -1457,4 +1495,31 @@ extern "C" int fgr_attention_bwd(const float* q, int64_t ldq, const float* k, in
     }
     FGR_CHECK_LAUNCH("attn_bwd_dkdv_kernel");
     return FGR_OK;
+}
+
+extern "C" int fgr_attention_bwd(const float* q, int64_t ldq, const float* k, int64_t ldk, const float* v,
+                                 int64_t ldv, const float* o, int64_t ldo, const float* dout,
+                                 int64_t lddo, float* dq, int64_t lddq, float* dk, int64_t lddk,
+                                 float* dv, int64_t lddv, const int64_t* q_off, const int64_t* kv_off,
+                                 const int32_t* kv_seg, int32_t n_seg, int32_t n_kv_seg, int64_t nq,
+                                 int64_t max_q_len, int64_t max_kv_len, int32_t nhead, int32_t dh,
+                                 float scale, void* ws, size_t ws_bytes, void* stream) {
+    return attention_bwd_impl(q, ldq, k, ldk, v, ldv, o, ldo, dout, lddo, dq, lddq, dk, lddk, dv,
+                              lddv, q_off, kv_off, kv_seg, n_seg, n_kv_seg, nq, max_q_len,
+                              max_kv_len, nhead, dh, scale, ws, ws_bytes, 0u, 0.f, stream);
+}
+
+extern "C" int fgr_attention_bwd_drop(const float* q, int64_t ldq, const float* k, int64_t ldk,
+                                      const float* v, int64_t ldv, const float* o, int64_t ldo,
+                                      const float* dout, int64_t lddo, float* dq, int64_t lddq,
+                                      float* dk, int64_t lddk, float* dv, int64_t lddv,
+                                      const int64_t* q_off, const int64_t* kv_off,
+                                      const int32_t* kv_seg, int32_t n_seg, int32_t n_kv_seg,
+                                      int64_t nq, int64_t max_q_len, int64_t max_kv_len,
+                                      int32_t nhead, int32_t dh, float scale, void* ws,
+                                      size_t ws_bytes, uint32_t seed, float p, void* stream) {
+    FGR_REQUIRE(p >= 0.f && p < 1.f, "fgr_attention_bwd_drop: dropout p %f not in [0, 1)", p);
+    return attention_bwd_impl(q, ldq, k, ldk, v, ldv, o, ldo, dout, lddo, dq, lddq, dk, lddk, dv,
+                              lddv, q_off, kv_off, kv_seg, n_seg, n_kv_seg, nq, max_q_len,
+                              max_kv_len, nhead, dh, scale, ws, ws_bytes, seed, p, stream);
 }

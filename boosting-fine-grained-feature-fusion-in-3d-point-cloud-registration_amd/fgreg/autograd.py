@@ -328,21 +328,39 @@ def layernorm_t(x, norm, add=None):
 # ------------------------------------------------------------------------------------------
 # attention
 # ------------------------------------------------------------------------------------------
+def attn_drop_mask(seed, p, head, q_rows, k_rows):
+    """The attention-weight dropout mask of fgr_attention_f16x3_drop / fgr_attention_bwd_drop
+    (common.h attn_drop_hash) for one head over packed query / key rows -> bool (len(q_rows),
+    len(k_rows)), True = dropped. Restated with numpy uint32 arithmetic (tests)."""
+    import numpy as np
+    m32 = lambda v: v & np.uint64(0xFFFFFFFF)
+    q = np.asarray(q_rows, dtype=np.uint64)[:, None]
+    k = np.asarray(k_rows, dtype=np.uint64)[None, :]
+    x = np.uint64(seed & 0xFFFFFFFF) ^ m32(np.uint64(head) * np.uint64(0x9E3779B9))
+    x = x ^ m32(q * np.uint64(0x85EBCA6B))
+    x = m32((x ^ (x >> np.uint64(16))) * np.uint64(0x7FEB352D))
+    x = x ^ m32(k * np.uint64(0xC2B2AE35))
+    x = m32((x ^ (x >> np.uint64(15))) * np.uint64(0x846CA68B))
+    x = x ^ (x >> np.uint64(16))
+    thresh = min(int(p * 4294967296.0), 4294967295)
+    return x < np.uint64(thresh)
+
+
 class _AttentionFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, qkv, off, kv_seg, max_len, nhead):
+    def forward(ctx, qkv, off, kv_seg, max_len, nhead, p=0.0, seed=0):
         qkv = _c(qkv, torch.float32)
         d = qkv.shape[1] // 3
         o = ops.attention(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], off, off, kv_seg, max_len,
-                          nhead)
-        ctx.meta = (d, int(max_len), int(nhead))
+                          nhead, dropout=(seed, p) if p > 0.0 else None)
+        ctx.meta = (d, int(max_len), int(nhead), float(p), int(seed))
         ctx.save_for_backward(qkv, o, off, kv_seg)
         return o
 
     @staticmethod
     def backward(ctx, do):
         qkv, o, off, kv_seg = ctx.saved_tensors
-        d, max_len, nhead = ctx.meta
+        d, max_len, nhead, p_drop, seed = ctx.meta
         do = _c(do, torch.float32)
         n = qkv.shape[0]
         dh = d // nhead
@@ -353,17 +371,26 @@ class _AttentionFn(torch.autograd.Function):
         ws = torch.empty(nb.value, dtype=torch.uint8, device=qkv.device)
         p, dp, ld = qkv.data_ptr(), dqkv.data_ptr(), qkv.stride(0)
         n_seg = off.numel() - 1
-        _lib.check(L.fgr_attention_bwd(
-            p, ld, p + 4 * d, ld, p + 8 * d, ld, _ptr(o), o.stride(0), _ptr(do), do.stride(0),
-            dp, ld, dp + 4 * d, ld, dp + 8 * d, ld, _ptr(off), _ptr(off), _ptr(kv_seg), n_seg,
-            n_seg, n, max_len, max_len, nhead, dh, float(math.sqrt(1.0 / float(dh))), _ptr(ws),
-            nb.value, _stream()), 'fgr_attention_bwd')
-        return dqkv, None, None, None, None
+        args = (p, ld, p + 4 * d, ld, p + 8 * d, ld, _ptr(o), o.stride(0), _ptr(do), do.stride(0),
+                dp, ld, dp + 4 * d, ld, dp + 8 * d, ld, _ptr(off), _ptr(off), _ptr(kv_seg), n_seg,
+                n_seg, n, max_len, max_len, nhead, dh, float(math.sqrt(1.0 / float(dh))),
+                _ptr(ws), nb.value)
+        if p_drop > 0.0:
+            _lib.check(L.fgr_attention_bwd_drop(*args, seed & 0xFFFFFFFF, p_drop, _stream()),
+                       'fgr_attention_bwd_drop')
+        else:
+            _lib.check(L.fgr_attention_bwd(*args, _stream()), 'fgr_attention_bwd')
+        return dqkv, None, None, None, None, None, None
 
 
-def attention_t(qkv, off, kv_seg, max_len, nhead):
+def attention_t(qkv, off, kv_seg, max_len, nhead, dropout=0.0):
     """Packed-segment MHA core on a fused (N, 3d) [q | k | v] tensor: query segment i attends
-    to key segment kv_seg[i] (self- or cross-attention over one segmentation)."""
+    to key segment kv_seg[i] (self- or cross-attention over one segmentation). ``dropout`` > 0:
+    nn.MultiheadAttention's attention-weight dropout in training, the mask seeded from torch's
+    CPU generator (torch.manual_seed reproduces a step)."""
+    if dropout > 0.0:
+        seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
+        return _AttentionFn.apply(qkv, off, kv_seg, max_len, nhead, float(dropout), seed)
     return _AttentionFn.apply(qkv, off, kv_seg, max_len, nhead)
 
 

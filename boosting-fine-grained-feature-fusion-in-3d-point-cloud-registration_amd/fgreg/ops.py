@@ -567,12 +567,14 @@ assert ATTN_MODE in ('f16x3', 'bf16'), ATTN_MODE
 
 
 def attention(q, k, v, q_off, kv_off, kv_seg, max_q_len, n_head, out=None,
-              max_kv_len=None) -> torch.Tensor:
+              max_kv_len=None, dropout=None) -> torch.Tensor:
     """Packed-segment MHA core: rows of query segment i attend to key segment kv_seg[i].
 
     q, k, v: (rows, n_head * dh) views with unit column stride (may be column slices of
     one fused QKV tensor). Returns o (Nq, n_head * dh). ``max_kv_len`` defaults to
-    ``max_q_len`` (self / cross attention over one segmentation).
+    ``max_q_len`` (self / cross attention over one segmentation). ``dropout`` = (seed, p):
+    the training forward's attention-weight dropout (fgr_attention_f16x3_drop; f16x3 mode,
+    head dim 32 / 64).
     """
     _dev(q, k, v, q_off, kv_off, kv_seg)
     for t in (q, k, v):
@@ -590,7 +592,21 @@ def attention(q, k, v, q_off, kv_off, kv_seg, max_q_len, n_head, out=None,
     split = (dh in (32, 64)
              and all(t.stride(0) % 4 == 0 and t.data_ptr() % 16 == 0 for t in (q, k, v, out)))
     t0 = _begin('attention')
-    if split:
+    if dropout is not None and float(dropout[1]) > 0.0:
+        if not (split and ATTN_MODE == 'f16x3'):
+            raise NotImplementedError('attention dropout needs the f16x3 mode, head dim 32 / 64 '
+                                      'and 16-B aligned rows')
+        nb = _lib._sz(0)
+        _lib.check(L.fgr_attention_f16x3_workspace(k.shape[0], n_kv_seg, n_head, nb),
+                   'fgr_attention_f16x3_workspace')
+        ws = _workspace(q.device, nb.value)
+        _lib.check(L.fgr_attention_f16x3_drop(
+            _ptr(q), q.stride(0), _ptr(k), k.stride(0), _ptr(v), v.stride(0), _ptr(out),
+            out.stride(0), _ptr(q_off), _ptr(kv_off), _ptr(kv_seg), n_seg, n_kv_seg, k.shape[0],
+            int(max_q_len), int(max_kv_len), n_head, dh, float(math.sqrt(1.0 / float(dh))),
+            _ptr(ws), ws.numel(), int(dropout[0]) & 0xFFFFFFFF, float(dropout[1]), _stream()),
+            'fgr_attention_f16x3_drop')
+    elif split:
         name = 'fgr_attention_' + ATTN_MODE
         nb = _lib._sz(0)
         _lib.check(getattr(L, name + '_workspace')(k.shape[0], n_kv_seg, n_head, nb),

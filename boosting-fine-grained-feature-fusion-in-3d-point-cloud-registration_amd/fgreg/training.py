@@ -14,6 +14,7 @@ finegrained_regtr.py:252-309).
 import math
 
 import torch
+import torch.nn.functional as F
 
 from . import ops
 from . import linear as lin
@@ -71,29 +72,45 @@ def block_train(block, x, meta):
     return leaky(y + shortcut)
 
 
+def _residual(x, y_fn, lin, p):
+    """x + dropout_p(lin(y)): the residual fused into the GEMM epilogue when p = 0, else the
+    layer's dropout1/2/3 (transformers.py:108-110) between the product and the add."""
+    if p > 0.0:
+        return x + F.dropout(linear_t(y_fn, lin.weight, lin.bias), p, training=True)
+    return linear_t(y_fn, lin.weight, lin.bias, residual=x)
+
+
+def _ffn_hidden(layer, h, p):
+    """activation(linear1(h)), then the FFN's own dropout (:102, :233) when p > 0."""
+    h = linear_t(h, layer.linear1.weight, layer.linear1.bias, act=ACT_RELU)
+    return F.dropout(h, p, training=True) if p > 0.0 else h
+
+
 def layer_train(layer, x, pos, seg):
     """TransformerCrossEncoderLayer.forward_pre (transformers.py:183-244), both clouds packed;
-    forward_post (:109-181) for pre_norm: False."""
+    forward_post (:109-181) for pre_norm: False. With dropout p > 0 (the layer's
+    nn.MultiheadAttention(dropout=p), dropout, dropout1/2/3, :95-110): attention-weight dropout
+    in the attention kernels, torch dropout on the FFN hidden and the sub-layer outputs."""
     if not layer.normalize_before:
         return _layer_post_train(layer, x, pos, seg)
+    p = float(layer.self_attn.dropout)
     for norm, mha, kv_seg in ((layer.norm1, layer.self_attn, seg.self_seg),
                               (layer.norm2, layer.multihead_attn, seg.cross_seg)):
         h = layernorm_t(x, norm, add=pos)
         qkv = linear_t(h, mha.in_proj_weight, mha.in_proj_bias)
-        o = attention_t(qkv, seg.off, kv_seg, seg.max_len, layer.nhead)
-        x = linear_t(o, mha.out_proj.weight, mha.out_proj.bias, residual=x)
-    h = linear_t(layernorm_t(x, layer.norm3), layer.linear1.weight, layer.linear1.bias, act=ACT_RELU)
-    return linear_t(h, layer.linear2.weight, layer.linear2.bias, residual=x)
+        o = attention_t(qkv, seg.off, kv_seg, seg.max_len, layer.nhead, dropout=p)
+        x = _residual(x, o, mha.out_proj, p)
+    return _residual(x, _ffn_hidden(layer, layernorm_t(x, layer.norm3), p), layer.linear2, p)
 
 
 def _layer_post_train(layer, x, pos, seg):
+    p = float(layer.self_attn.dropout)
     for norm, mha, kv_seg in ((layer.norm1, layer.self_attn, seg.self_seg),
                               (layer.norm2, layer.multihead_attn, seg.cross_seg)):
         qkv = linear_t(x if pos is None else x + pos, mha.in_proj_weight, mha.in_proj_bias)
-        o = attention_t(qkv, seg.off, kv_seg, seg.max_len, layer.nhead)
-        x = layernorm_t(linear_t(o, mha.out_proj.weight, mha.out_proj.bias, residual=x), norm)
-    h = linear_t(x, layer.linear1.weight, layer.linear1.bias, act=ACT_RELU)
-    return layernorm_t(linear_t(h, layer.linear2.weight, layer.linear2.bias, residual=x), layer.norm3)
+        o = attention_t(qkv, seg.off, kv_seg, seg.max_len, layer.nhead, dropout=p)
+        x = layernorm_t(_residual(x, o, mha.out_proj, p), norm)
+    return layernorm_t(_residual(x, _ffn_hidden(layer, x, p), layer.linear2, p), layer.norm3)
 
 
 def check_trainable(model):
@@ -104,10 +121,13 @@ def check_trainable(model):
         raise NotImplementedError('training with value-without-positional-embedding attention is '
                                   'not in the reference configs')
     if float(cfg.get('dropout', 0.0) or 0.0) > 0.0:
-        # transformers.py:102-110, 201-238 apply dropout1/2/3 and the MHA's own dropout in
-        # train(); every shipped config sets 0.0 (conf/*.yaml), and this forward has none
-        raise NotImplementedError(f'training with dropout {cfg.dropout} > 0 (the reference '
-                                  'configs train with 0.0)')
+        # transformers.py:95-110: the attention-weight dropout runs in the f16x3 attention
+        # kernels (head dim 32 / 64); the bf16 mode's attention has none
+        dh = cfg.d_embed // cfg.nhead
+        if lin.MODE != 'f16x3' or dh not in (32, 64):
+            raise NotImplementedError(f'training with dropout {cfg.dropout} > 0 needs the fp32 '
+                                      f'(f16x3) mode and head dim 32 / 64 (mode {lin.MODE}, '
+                                      f'head dim {dh})')
     if getattr(model.correspondence_decoder, 'num_neighbors', 0) > 0:
         raise NotImplementedError('training the CorrespondenceDecoder with num_neighbors > 0 (a '
                                   'constructor argument the reference RegTR never passes)')

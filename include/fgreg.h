@@ -605,6 +605,27 @@ int fgr_attention_bwd(const float* q, int64_t ldq, const float* k, int64_t ldk, 
                       int32_t n_seg, int32_t n_kv_seg, int64_t nq, int64_t max_q_len,
                       int64_t max_kv_len, int32_t nhead, int32_t dh, float scale, void* ws,
                       size_t ws_bytes, void* stream);
+/* Training with nn.MultiheadAttention(dropout = p > 0): the same forward / backward with the
+ * attention weights of the PV product dropped by a counter-based hash of (seed, head, query
+ * row, key row) -- kept with probability 1 - p and scaled by 1 / (1 - p), the softmax sum
+ * over every weight (transformers.py:95-96; common.h attn_drop_hash). The backward with the
+ * same seed / p reproduces the forward's mask; head dim 16 / 32 / 64 (the forward: 32 / 64),
+ * 16-B aligned rows. Masks are not torch's Philox draws (same distribution). */
+int fgr_attention_f16x3_drop(const float* q, int64_t ld_q, const float* k, int64_t ld_k,
+                             const float* v, int64_t ld_v, float* o, int64_t ld_o,
+                             const int64_t* q_off, const int64_t* kv_off, const int32_t* kv_seg,
+                             int32_t n_seg, int32_t n_kv_seg, int64_t n_kv_rows, int32_t max_q_len,
+                             int32_t max_kv_len, int32_t n_head, int32_t head_dim, float scale,
+                             void* workspace, int64_t ws_bytes, uint32_t seed, float p,
+                             void* stream);
+int fgr_attention_bwd_drop(const float* q, int64_t ldq, const float* k, int64_t ldk,
+                           const float* v, int64_t ldv, const float* o, int64_t ldo,
+                           const float* dout, int64_t lddo, float* dq, int64_t lddq, float* dk,
+                           int64_t lddk, float* dv, int64_t lddv, const int64_t* q_off,
+                           const int64_t* kv_off, const int32_t* kv_seg, int32_t n_seg,
+                           int32_t n_kv_seg, int64_t nq, int64_t max_q_len, int64_t max_kv_len,
+                           int32_t nhead, int32_t dh, float scale, void* ws, size_t ws_bytes,
+                           uint32_t seed, float p, void* stream);
 
 #ifdef __cplusplus
 }

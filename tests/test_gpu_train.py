@@ -270,6 +270,93 @@ def test_attention_backward(gpu, d, nhead, kind):
         assert e < 1e-5, (name, e)
 
 
+def _attn_ref_drop(qkv, lens, kv_seg, nhead, seed, p):
+    """_attn_ref with nn.MultiheadAttention's attention-weight dropout, the mask of
+    fgr_attention_f16x3_drop restated (fgreg.autograd.attn_drop_mask, packed row indices)."""
+    from fgreg.autograd import attn_drop_mask
+    d = qkv.shape[1] // 3
+    dh = d // nhead
+    off = np.cumsum([0] + lens)
+    outs = []
+    for i in range(len(lens)):
+        j = kv_seg[i]
+        q = qkv[off[i]:off[i + 1], :d].reshape(-1, nhead, dh).transpose(0, 1) / math.sqrt(dh)
+        k = qkv[off[j]:off[j + 1], d:2 * d].reshape(-1, nhead, dh).transpose(0, 1)
+        v = qkv[off[j]:off[j + 1], 2 * d:].reshape(-1, nhead, dh).transpose(0, 1)
+        P = torch.softmax(q @ k.transpose(1, 2), -1)
+        keep = torch.stack([torch.from_numpy(~attn_drop_mask(seed, p, h, range(off[i], off[i + 1]),
+                                                             range(off[j], off[j + 1])))
+                            for h in range(nhead)]).to(P.dtype)
+        outs.append(((P * keep / (1 - p)) @ v).transpose(0, 1).reshape(-1, d))
+    return torch.cat(outs, 0)
+
+
+@pytest.mark.parametrize('d,nhead', [(256, 8), (512, 8)])
+@pytest.mark.parametrize('kind', ['self', 'cross'])
+def test_attention_dropout_forward_backward(gpu, d, nhead, kind):
+    """Training-mode attention-weight dropout (nn.MultiheadAttention(dropout=p),
+    transformers.py:95-96): fgr_attention_f16x3_drop / fgr_attention_bwd_drop against fp64
+    softmax attention with the SAME mask (the kernels' counter-based hash restated in numpy):
+    output and dq / dk / dv; the dropped fraction is p; p = 0 is the plain path."""
+    from fgreg import ops
+    from fgreg.autograd import _AttentionFn, attn_drop_mask
+    lens = [130, 1, 65, 300]
+    B = len(lens) // 2
+    kv_seg = list(range(4)) if kind == 'self' else [(c + B) % 4 for c in range(4)]
+    g = torch.Generator().manual_seed(d + 7)
+    qkv, qkv64 = _leaf(torch.randn(sum(lens), 3 * d, generator=g), gpu)
+    off = ops.offsets(lens, gpu)
+    ks = torch.tensor(kv_seg, dtype=torch.int32, device=gpu)
+    seed, p = 987654321, 0.3
+    o = _AttentionFn.apply(qkv, off, ks, max(lens), nhead, p, seed)
+    o64 = _attn_ref_drop(qkv64, lens, kv_seg, nhead, seed, p)
+    R = torch.randn(o64.shape, generator=g)
+    (o * R.to(gpu)).sum().backward()
+    (o64 * R.double()).sum().backward()
+    assert rel_err(o, o64) < 1e-5
+    for sl, name in ((slice(0, d), 'dq'), (slice(d, 2 * d), 'dk'), (slice(2 * d, 3 * d), 'dv')):
+        e = rel_err(qkv.grad[:, sl], qkv64.grad[:, sl])
+        assert e < 1e-5, (name, e)
+    m = attn_drop_mask(seed, p, 3, range(300), range(300))
+    assert abs(float(m.mean()) - p) < 0.01
+    o0 = _AttentionFn.apply(qkv.detach(), off, ks, max(lens), nhead, 0.0, seed)
+    assert rel_err(o0, _attn_ref(qkv64.detach(), lens, kv_seg, nhead)) < 1e-5
+
+
+def test_train_step_with_dropout(gpu):
+    """A ModelNet training step with dropout 0.1 (every transformer dropout of
+    transformers.py:95-110): finite losses and gradients, bit-identical under the same
+    torch seed, different under another; dropout 0 gives the round-4 step."""
+    import fgreg
+    import fgreg.config as fc
+    from fgreg.loss import compute_loss_train
+    from fgreg.synthetic import make_batch
+
+    def step(drop, seed):
+        torch.manual_seed(0)
+        np.random.seed(0)                # kernel points and the synthetic crops draw from numpy
+        model = fgreg.RegTR(fc.get('modelnet', dropout=drop)).to(gpu).train()
+        src, tgt, pose = make_batch('modelnet', 2)
+        batch = {'src_xyz': [torch.from_numpy(a).to(gpu) for a in src],
+                 'tgt_xyz': [torch.from_numpy(b).to(gpu) for b in tgt],
+                 'pose': torch.from_numpy(np.asarray(pose, np.float32)).to(gpu),
+                 'src_overlap': [torch.ones(len(a), device=gpu) for a in src],
+                 'tgt_overlap': [torch.ones(len(b), device=gpu) for b in tgt]}
+        torch.manual_seed(seed)
+        out = model(batch)
+        loss = compute_loss_train(model, out, batch)['total']
+        loss.backward()
+        g = torch.cat([p.grad.flatten() for p in model.parameters() if p.grad is not None])
+        return float(loss.detach()), g
+    l1, g1 = step(0.1, 5)
+    l2, g2 = step(0.1, 5)
+    l3, g3 = step(0.1, 6)
+    l0, g0 = step(0.0, 5)
+    assert math.isfinite(l1) and bool(torch.isfinite(g1).all())
+    assert l1 == l2 and torch.equal(g1, g2)
+    assert l1 != l3 and l1 != l0
+
+
 @pytest.mark.parametrize('d', [64, 256])
 def test_corr_attention_backward(gpu, d):
     """corr_attention_t (CorrespondenceDecoder.simple_attention over the (layer, cloud)

@@ -200,18 +200,24 @@ def test_training_mode_refuses_host_tensors():
 @pytest.mark.parametrize('what', ['dropout', 'num_neighbors'])
 def test_training_refuses_untrainable_configs(what):
     """Configurations the training forward does not restate raise NotImplementedError before
-    any work (the reference applies dropout1/2/3 + the MHA dropout in train(),
-    transformers.py:102-110, 201-238; every shipped config sets 0.0)."""
+    any work: dropout > 0 in the bf16 mode (its attention kernels have no dropout; the f16x3
+    mode trains with dropout, transformers.py:95-110, tests/test_gpu_train.py), and the
+    decoder's num_neighbors > 0."""
     import fgreg
     import fgreg.config as fc
-    if what == 'dropout':
-        model = fgreg.RegTR(fc.get('modelnet', dropout=0.1)).train()
-    else:
-        model = fgreg.RegTR(fc.get('modelnet', direct_regress_coor=False)).train()
-        model.correspondence_decoder.num_neighbors = 4
-    batch = {'src_xyz': [torch.zeros(8, 3)], 'tgt_xyz': [torch.zeros(8, 3)]}
-    with pytest.raises(NotImplementedError, match=what.replace('_', '.')):
-        model(batch)
+    prev = fgreg.precision()
+    try:
+        if what == 'dropout':
+            model = fgreg.RegTR(fc.get('modelnet', dropout=0.1)).train()
+            fgreg.set_precision('bf16')
+        else:
+            model = fgreg.RegTR(fc.get('modelnet', direct_regress_coor=False)).train()
+            model.correspondence_decoder.num_neighbors = 4
+        batch = {'src_xyz': [torch.zeros(8, 3)], 'tgt_xyz': [torch.zeros(8, 3)]}
+        with pytest.raises(NotImplementedError, match=what.replace('_', '.')):
+            model(batch)
+    finally:
+        fgreg.set_precision(prev)
     model.eval()                     # inference has no dropout and restates num_neighbors
     with pytest.raises(fgreg.FgrError):
         model(batch)
