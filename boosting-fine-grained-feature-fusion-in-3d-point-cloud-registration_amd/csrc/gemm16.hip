@@ -1028,6 +1028,66 @@ __global__ void split_weights_h3_kernel(const float* __restrict__ w, int n, int 
     img[u] = __builtin_bit_cast(u32x4, out);
 }
 
+// weight_scale_kernel + split_weights_h3_kernel in one launch for k <= kSplitFusedK: one block
+// per 16-row panel takes the panel's row maxima (lanes along whichever stride is 1, so the
+// reads coalesce for W and for W^T alike), then writes the panel's image units. Same scales,
+// same image bits; training re-splits every weight twice per step (forward and transposed
+// images), so this halves those launches.
+constexpr int kSplitFusedK = 1024;
+
+__global__ void __launch_bounds__(256)
+split_weights_h3_fused_kernel(const float* __restrict__ w, int n, int k, int64_t sn, int64_t sk,
+                              int ksteps, float* __restrict__ wsc, u32x4* __restrict__ img) {
+    const int panel = blockIdx.x, tid = threadIdx.x;
+    const int r0 = panel * 16;
+    // phase 1: row maxima; (row, k-lane) = (tid % 16, tid / 16) when rows are contiguous in
+    // memory (sn == 1), else (tid / 16, tid % 16)
+    const bool rows_fast = sn == 1 && sk != 1;
+    const int ri = rows_fast ? (tid & 15) : (tid >> 4), kl = rows_fast ? (tid >> 4) : (tid & 15);
+    const int row = r0 + ri;
+    float mx = 0.f;
+    if (row < n) {
+        const float* wr = w + (int64_t)row * sn;
+        int j = kl;
+        for (; j + 48 < k; j += 64) {
+            const float a = wr[(int64_t)j * sk], b = wr[(int64_t)(j + 16) * sk];
+            const float c = wr[(int64_t)(j + 32) * sk], d = wr[(int64_t)(j + 48) * sk];
+            mx = fmaxf(mx, fmaxf(fmaxf(fabsf(a), fabsf(b)), fmaxf(fabsf(c), fabsf(d))));
+        }
+        for (; j < k; j += 16) mx = fmaxf(mx, fabsf(wr[(int64_t)j * sk]));
+    }
+    __shared__ float red[16][17];
+    __shared__ float scale_inv[16];
+    red[ri][kl] = mx;
+    __syncthreads();
+    if (tid < 16) {
+        float m = 0.f;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) m = fmaxf(m, red[tid][q]);
+        const int e = m > 0.f ? min(15 - __builtin_amdgcn_frexp_expf(m), 127) : 0;
+        const bool ok = r0 + tid < n;
+        scale_inv[tid] = ok ? __builtin_ldexpf(1.f, e) : 0.f;
+        wsc[r0 + tid] = ok ? __builtin_ldexpf(1.f, -e) : 0.f;
+    }
+    __syncthreads();
+    // phase 2: the panel's units [kstep][term][g][i], as split_weights_h3_kernel
+    const int units = ksteps * 128;
+    for (int u = tid; u < units; u += 256) {
+        const int i = u & 15, g = (u >> 4) & 3, t = (u >> 6) & 1, s = u >> 7;
+        const int rr = r0 + i;
+        const float sc = scale_inv[i];
+        f16x8 out;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int col = s * 32 + 8 * g + e;
+            const float x = (rr < n && col < k) ? w[(int64_t)rr * sn + (int64_t)col * sk] * sc : 0.f;
+            const _Float16 h = (_Float16)x;
+            out[e] = t == 0 ? h : (_Float16)(x - (float)h);
+        }
+        img[(int64_t)panel * units + u] = __builtin_bit_cast(u32x4, out);
+    }
+}
+
 template <int BM, int BN, bool EPI = false>
 void launch_h3(const GemmH3Args& a, hipStream_t st) {
     const int nbm = (a.M + BM - 1) / BM, nbn = (a.N + BN - 1) / BN;
@@ -1099,6 +1159,13 @@ extern "C" int fgr_split_weights_h3(const float* w, int32_t n, int32_t k, int64_
     const int npad = (n + 15) / 16 * 16;
     float* wsc = reinterpret_cast<float*>(static_cast<char*>(img) + image_bytes_h3(n, k));
     hipStream_t st = as_stream(stream);
+    static const bool fused_on = [] { const char* e = getenv("FGR_SPLIT_FUSED"); return !(e && e[0] == '0'); }();
+    if (k <= kSplitFusedK && fused_on) {
+        hipLaunchKernelGGL(split_weights_h3_fused_kernel, dim3((unsigned)(npad / 16)), dim3(256), 0, st,
+                           w, n, k, stride_n, stride_k, ksteps, wsc, (u32x4*)img);
+        FGR_CHECK_LAUNCH("split_weights_h3_fused_kernel");
+        return FGR_OK;
+    }
     if (stride_n == 1 && k >= 1024) {
         // column-major W (the backward's transposed activations): coalesced chunked maxima;
         // >= 512 blocks of 64 rows x kchunk (a multiple of 64)

@@ -206,7 +206,11 @@ res2net_chain6_kernel(const float* __restrict__ h, int64_t n, int scale, int num
 // ------------------------------------------------------------------------------------
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
-template <int KT>
+// R rows per block (32, or 48 at w = 224 when that saves a round of blocks, as in chain6).
+// Each step issues the whole step's W_i fragments (KS x 2 per lane) before the build, so the
+// matrix-core loop never waits on L2; rmax is double-buffered (reset in the previous step's
+// epilogue): 3 barriers per step.
+template <int KT, int R = kRows>
 __global__ void __launch_bounds__(64 * KT)
 res2net_chain_h3_kernel(const float* __restrict__ h, int64_t n, int w, int scale, int nums,
                         const u32x4* __restrict__ wf, const float* __restrict__ wsc,
@@ -214,40 +218,39 @@ res2net_chain_h3_kernel(const float* __restrict__ h, int64_t n, int w, int scale
                         float* __restrict__ cat, int64_t ld) {
     // W = the width padded to whole 16-column tiles (one wave each); w <= W the real width
     // (w % 4 == 0): columns past w carry zero weights and are never stored
-    constexpr int W = 16 * KT, KS = (W + 31) / 32, NU = kRows * KS * 4;   // A units per term
+    constexpr int W = 16 * KT, KS = (W + 31) / 32, NU = R * KS * 4;       // A units per term
     constexpr int IT = (NU + 64 * KT - 1) / (64 * KT);                    // build units / thread
+    constexpr int RF = R / 16;                                            // row fragments
     __shared__ u32x4 img[2 * NU];
-    __shared__ float sp[kRows * W];
-    __shared__ int rmax[kRows];
+    __shared__ float sp[R * W];
+    __shared__ int rmax[2][R];
     const int tid = threadIdx.x, nth = 64 * KT;
     const int wv = tid / 64, lane = tid % 64, g = lane >> 4, c = lane & 15;
-    const int64_t r0 = (int64_t)blockIdx.x * kRows;
+    const int64_t r0 = (int64_t)blockIdx.x * R;
     const int64_t hw = (int64_t)scale * w;
     const int col0 = wv * 16 + 4 * g;                  // this lane's 4 output columns
     const bool col_ok = col0 < w;
+    if (tid < R) rmax[0][tid] = 0;
+    __syncthreads();
 
     for (int i = 0; i < nums; ++i) {
+        int* rm = rmax[i & 1];
         const u32x4* wb = wf + (((int64_t)i * KT + wv) * KS) * 128 + lane;
-        u32x4 bq[3][2];                                // ring: k-steps ks, ks+1, ks+2
+        u32x4 bq[KS][2];
 #pragma unroll
-        for (int q = 0; q < 2; ++q)
-            if (q < KS) {
+        for (int q = 0; q < KS; ++q)
 #pragma unroll
-                for (int t = 0; t < 2; ++t) bq[q][t] = wb[(q * 2 + t) * 64];
-            }
+            for (int t = 0; t < 2; ++t) bq[q][t] = wb[(q * 2 + t) * 64];
         const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
         const float4 wsv = col_ok ? *reinterpret_cast<const float4*>(wsc + i * w + col0) : z4;
         const float4 bc = col_ok ? *reinterpret_cast<const float4*>(bias + i * w + col0) : z4;
-        if (tid < kRows) rmax[tid] = 0;
-        __syncthreads();
-        // a = sp_{i-1} + h_i: unit u -> (row = u % 32, kg = u / 32), 8 k each
+        // a = sp_{i-1} + h_i: unit u -> (row = u % R, kg = u / R), 8 k each
         float a[IT][8];
 #pragma unroll
         for (int it = 0; it < IT; ++it) {
             const int u = tid + nth * it;
-            const int row = u % kRows, kg = u / kRows, k0 = 8 * kg;
+            const int row = u % R, kg = u / R, k0 = 8 * kg;
             const int64_t gr = r0 + row;
-            float cm = 0.f;
 #pragma unroll
             for (int e = 0; e < 8; e += 4) {
                 float4 hv = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -255,20 +258,26 @@ res2net_chain_h3_kernel(const float* __restrict__ h, int64_t n, int w, int scale
                     hv = *reinterpret_cast<const float4*>(h + gr * hw + (int64_t)i * w + k0 + e);
                 a[it][e] = hv.x; a[it][e + 1] = hv.y; a[it][e + 2] = hv.z; a[it][e + 3] = hv.w;
             }
+        }
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int u = tid + nth * it;
+            const int row = u % R, kg = u / R, k0 = 8 * kg;
+            float cm = 0.f;
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
                 if (i > 0 && u < NU && k0 + e < w) a[it][e] += sp[row * W + k0 + e];
                 cm = fmaxf(cm, fabsf(a[it][e]));
             }
-            if (u < NU && cm > 0.f) atomicMax(&rmax[row], __float_as_int(cm));
+            if (u < NU && cm > 0.f) atomicMax(&rm[row], __float_as_int(cm));
         }
         __syncthreads();
 #pragma unroll
         for (int it = 0; it < IT; ++it) {
             const int u = tid + nth * it;
             if (u >= NU) break;
-            const int row = u % kRows, kg = u / kRows;
-            const float mx = __int_as_float(rmax[row]);
+            const int row = u % R, kg = u / R;
+            const float mx = __int_as_float(rm[row]);
             const float s = __builtin_ldexpf(1.f, mx > 0.f ? min(15 - __builtin_amdgcn_frexp_expf(mx), 127) : 0);
             f16x8 th, tm;
 #pragma unroll
@@ -278,38 +287,38 @@ res2net_chain_h3_kernel(const float* __restrict__ h, int64_t n, int w, int scale
                 th[e] = hh;
                 tm[e] = (_Float16)(xs - (float)hh);
             }
-            img[0 * NU + kg * kRows + row] = __builtin_bit_cast(u32x4, th);
-            img[1 * NU + kg * kRows + row] = __builtin_bit_cast(u32x4, tm);
+            img[0 * NU + kg * R + row] = __builtin_bit_cast(u32x4, th);
+            img[1 * NU + kg * R + row] = __builtin_bit_cast(u32x4, tm);
         }
         __syncthreads();
-        f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+        f32x4 acc[RF];
+#pragma unroll
+        for (int f = 0; f < RF; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
-            if (ks + 2 < KS) {
+            const f16x8 wh = __builtin_bit_cast(f16x8, bq[ks][0]);
+            const f16x8 wl = __builtin_bit_cast(f16x8, bq[ks][1]);
+            const int base = (ks * 4 + g) * R;
+            f16x8 ah[RF], am[RF];
 #pragma unroll
-                for (int t = 0; t < 2; ++t) bq[(ks + 2) % 3][t] = wb[((ks + 2) * 2 + t) * 64];
+            for (int f = 0; f < RF; ++f) {
+                ah[f] = __builtin_bit_cast(f16x8, img[0 * NU + base + 16 * f + c]);
+                am[f] = __builtin_bit_cast(f16x8, img[1 * NU + base + 16 * f + c]);
             }
-            const f16x8 wh = __builtin_bit_cast(f16x8, bq[ks % 3][0]);
-            const f16x8 wl = __builtin_bit_cast(f16x8, bq[ks % 3][1]);
-            const int base = (ks * 4 + g) * kRows;
-            const f16x8 a0h = __builtin_bit_cast(f16x8, img[0 * NU + base + c]);
-            const f16x8 a0m = __builtin_bit_cast(f16x8, img[1 * NU + base + c]);
-            const f16x8 a1h = __builtin_bit_cast(f16x8, img[0 * NU + base + 16 + c]);
-            const f16x8 a1m = __builtin_bit_cast(f16x8, img[1 * NU + base + 16 + c]);
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, a0h, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, a1h, acc1, 0, 0, 0);
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, a0m, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, a1m, acc1, 0, 0, 0);
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, a0h, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, a1h, acc1, 0, 0, 0);
+#pragma unroll
+            for (int f = 0; f < RF; ++f) acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, ah[f], acc[f], 0, 0, 0);
+#pragma unroll
+            for (int f = 0; f < RF; ++f) acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, am[f], acc[f], 0, 0, 0);
+#pragma unroll
+            for (int f = 0; f < RF; ++f) acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, ah[f], acc[f], 0, 0, 0);
         }
         // epilogue: lane (g, c) holds sp_i[row rg * 16 + c][cols col0 .. col0 + 3]
 #pragma unroll
-        for (int rg = 0; rg < 2; ++rg) {
+        for (int rg = 0; rg < RF; ++rg) {
             const int row = rg * 16 + c;
-            const float mx = __int_as_float(rmax[row]);
+            const float mx = __int_as_float(rm[row]);
             const float rs = __builtin_ldexpf(1.f, mx > 0.f ? -min(15 - __builtin_amdgcn_frexp_expf(mx), 127) : 0);
-            const f32x4 av = rg ? acc1 : acc0;
+            const f32x4 av = acc[rg];
             float4 y;
             y.x = fmaxf(av[0] * rs * wsv.x + bc.x, 0.f);
             y.y = fmaxf(av[1] * rs * wsv.y + bc.y, 0.f);
@@ -319,11 +328,12 @@ res2net_chain_h3_kernel(const float* __restrict__ h, int64_t n, int w, int scale
                 *reinterpret_cast<float4*>(cat + (r0 + row) * ld + (int64_t)i * w + col0) = y;
             *reinterpret_cast<float4*>(sp + row * W + col0) = y;
         }
+        if (tid < R) rmax[(i + 1) & 1][tid] = 0;       // next step's row maxima
         __syncthreads();
     }
-    copy_rows(cat + (int64_t)nums * w, ld, h + (int64_t)nums * w, hw, r0, kRows, n,
+    copy_rows(cat + (int64_t)nums * w, ld, h + (int64_t)nums * w, hw, r0, R, n,
               (scale - nums) * w, tid, nth);
-    if (x) copy_rows(cat + hw, ld, x, cin, r0, kRows, n, cin, tid, nth);
+    if (x) copy_rows(cat + hw, ld, x, cin, r0, R, n, cin, tid, nth);
 }
 
 }  // namespace
@@ -346,16 +356,27 @@ extern "C" int fgr_res2net_chain_h3(const float* h, int64_t n, int32_t w, int32_
                     (scale * w) % 4 == 0,
                 "fgr_res2net_chain_h3: h / cat / w_scale / bias must be 16-B aligned");
     if (n == 0) return FGR_OK;
-    const dim3 grid((unsigned)ceil_div(n, kRows));
     hipStream_t st = as_stream(stream);
     TimedCall timed_(st);
     const int kt = (w + 15) / 16;
+    // w > 112 (one 14-wave block per CU): 48-row blocks when that saves a round of blocks
+    // (rounds x rows per block over 256 CUs, as fgr_res2net_chain6); FGR_R2N_ROWS=32 forces 32
+    const char* rr = getenv("FGR_R2N_ROWS");
+    const bool r48 = kt == 14 && !(rr && rr[0] == '3') &&
+                     ceil_div(ceil_div(n, 48), 256) * 48 < ceil_div(ceil_div(n, 32), 256) * 32;
 #define FGR_H3_CASE(KT)                                                                         \
     case KT:                                                                                    \
-        hipLaunchKernelGGL(res2net_chain_h3_kernel<KT>, grid, dim3(64 * KT), 0, st, h, n, w,    \
-                           scale, scale - 1, (const u32x4*)w_img, w_scale, bias, x, cin, cat,   \
-                           ld_cat);                                                             \
+        hipLaunchKernelGGL(res2net_chain_h3_kernel<KT>, dim3((unsigned)ceil_div(n, kRows)),     \
+                           dim3(64 * KT), 0, st, h, n, w, scale, scale - 1, (const u32x4*)w_img, \
+                           w_scale, bias, x, cin, cat, ld_cat);                                 \
         break;
+    if (r48) {
+        hipLaunchKernelGGL((res2net_chain_h3_kernel<14, 48>), dim3((unsigned)ceil_div(n, 48)),
+                           dim3(64 * 14), 0, st, h, n, w, scale, scale - 1, (const u32x4*)w_img,
+                           w_scale, bias, x, cin, cat, ld_cat);
+        FGR_CHECK_LAUNCH("res2net_chain_h3_kernel");
+        return FGR_OK;
+    }
     switch (kt) {
         FGR_H3_CASE(2)
         FGR_H3_CASE(4)

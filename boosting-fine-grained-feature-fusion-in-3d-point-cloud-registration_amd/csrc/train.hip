@@ -28,6 +28,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <initializer_list>
 
 namespace fgr {
 namespace {
@@ -439,6 +440,244 @@ segnorm_bwd_apply_kernel(SegApply p, const float* __restrict__ dy, const float* 
     const float dz = gr * act_grad(xh * g + bt, p.act);
     const float m1 = sums[2 * sc] * inv_n, m2 = sums[2 * sc + 1] * inv_n;
     dx[t] = rs * g * (dz - m1 - xh * m2) / rd;
+}
+
+// ---- the same four kernels on 16-B rows (c % 4 == 0, aligned): one float4 of channels per
+// thread, four rows in flight per thread in the statistics (the scalar kernels above kept one
+// dependent load per row and channel: 22 / 38 us per ModelNet call), 32-bit element indices
+// and the segment table in LDS for the elementwise passes. Same partial layout and chunking,
+// so the merges are shared.
+constexpr int kSegLds = 64;        // segment tables up to this many segments cached in LDS
+
+__device__ __forceinline__ int seg_of_row(const int64_t* so_lds, const int64_t* so, int n_seg, int64_t r) {
+    return n_seg <= kSegLds ? find_segment(so_lds, n_seg, r) : find_segment(so, n_seg, r);
+}
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+__global__ void __launch_bounds__(256)
+segnorm_stats4_kernel(SegArgs a, double* __restrict__ part) {
+    const int seg = blockIdx.y, chunk = blockIdx.x;
+    const int qd = threadIdx.x & 15, rg = threadIdx.x >> 4;          // 16 quads x 16 row groups
+    const int ch = blockIdx.z * 64 + 4 * qd;
+    const int C = a.c;
+    const int64_t b = a.seg_off[seg], e = a.seg_off[seg + 1];
+    const int64_t r0 = b + (int64_t)chunk * kRowsChunk;
+    double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+    int cnt = 0;
+    if (ch < C && r0 < e) {
+        const float4 pv = ld4(a.x + b * C + ch);
+        const float pd = a.row_div ? a.row_div[b] : 1.f;
+        const double piv[4] = {(double)(a.row_div ? pv.x / pd : pv.x), (double)(a.row_div ? pv.y / pd : pv.y),
+                               (double)(a.row_div ? pv.z / pd : pv.z), (double)(a.row_div ? pv.w / pd : pv.w)};
+        const int64_t r1 = min(e, r0 + kRowsChunk);
+        for (int64_t r = r0 + rg; r < r1; r += 64) {
+            float4 v[4];
+            float rd[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int64_t rr = min(r + 16 * u, r1 - 1);
+                v[u] = ld4(a.x + rr * C + ch);
+                rd[u] = a.row_div ? a.row_div[rr] : 1.f;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (r + 16 * u >= r1) break;
+                const float vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const float f = a.row_div ? vv[j] / rd[u] : vv[j];
+                    const double d = (double)f - piv[j];
+                    s1[j] += d;
+                    s2[j] += d * d;
+                }
+                ++cnt;
+            }
+        }
+    }
+    __shared__ double l1[16][64], l2[16][64];
+    __shared__ int lc[16][16];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        l1[rg][4 * qd + j] = s1[j];
+        l2[rg][4 * qd + j] = s2[j];
+    }
+    lc[rg][qd] = cnt;
+    __syncthreads();
+    const int l = threadIdx.x;
+    if (l < 64 && blockIdx.z * 64 + l < C) {
+        double t1 = 0.0, t2 = 0.0;
+        int tc = 0;
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+            t1 += l1[g][l];
+            t2 += l2[g][l];
+            tc += lc[g][l >> 2];
+        }
+        double* p = part + (((int64_t)seg * a.n_chunks + chunk) * C + blockIdx.z * 64 + l) * 3;
+        p[0] = t1;
+        p[1] = t2;
+        p[2] = (double)tc;
+    }
+}
+
+__global__ void __launch_bounds__(256)
+segnorm_apply4_kernel(SegApply p, float* __restrict__ out) {
+    __shared__ int64_t so[kSegLds + 1];
+    if (p.a.n_seg <= kSegLds)
+        for (int i = threadIdx.x; i <= p.a.n_seg; i += 256) so[i] = p.a.seg_off[i];
+    __syncthreads();
+    const int c4 = p.a.c >> 2;
+    const int t = blockIdx.x * 256 + threadIdx.x;                  // float4 index (< 2^31)
+    if (t >= (int)(p.n * c4)) return;
+    const int r = t / c4;
+    const int ch = 4 * (t - r * c4);
+    const int seg = seg_of_row(so, p.a.seg_off, p.a.n_seg, r);
+    const int64_t sc = (int64_t)seg * p.a.c + ch;
+    const float4 xv = ld4(p.a.x + 4 * (int64_t)t);
+    const float rd = p.a.row_div ? p.a.row_div[r] : 1.f;
+    const float4 mu = ld4(p.mean + sc), rs = ld4(p.rstd + sc);
+    float4 gm = make_float4(1.f, 1.f, 1.f, 1.f), bt = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (p.gamma) {
+        gm = ld4(p.gamma + ch);
+        bt = ld4(p.beta + ch);
+    }
+    float4 rv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (p.residual) rv = ld4(p.residual + 4 * (int64_t)t);
+    const float xs[4] = {xv.x, xv.y, xv.z, xv.w}, ms[4] = {mu.x, mu.y, mu.z, mu.w};
+    const float ss[4] = {rs.x, rs.y, rs.z, rs.w}, gs[4] = {gm.x, gm.y, gm.z, gm.w};
+    const float bs[4] = {bt.x, bt.y, bt.z, bt.w}, res[4] = {rv.x, rv.y, rv.z, rv.w};
+    float y[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const float v = p.a.row_div ? xs[j] / rd : xs[j];
+        float z = (v - ms[j]) * ss[j];
+        if (p.gamma) z = z * gs[j] + bs[j];
+        y[j] = act_fwd(z, p.act);
+        if (p.residual) y[j] = act_fwd(y[j] + res[j], p.post_act);
+    }
+    *reinterpret_cast<float4*>(out + 4 * (int64_t)t) = make_float4(y[0], y[1], y[2], y[3]);
+}
+
+__global__ void __launch_bounds__(256)
+segnorm_bwd_stats4_kernel(SegApply p, const float* __restrict__ dy, const float* __restrict__ y,
+                          double* __restrict__ part) {
+    const int seg = blockIdx.y, chunk = blockIdx.x;
+    const int qd = threadIdx.x & 15, rg = threadIdx.x >> 4;
+    const int ch = blockIdx.z * 64 + 4 * qd;
+    const int C = p.a.c;
+    const int64_t b = p.a.seg_off[seg], e = p.a.seg_off[seg + 1];
+    const int64_t r0 = b + (int64_t)chunk * kRowsChunk;
+    double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+    if (ch < C && r0 < e) {
+        const int64_t sc = (int64_t)seg * C + ch;
+        const float4 mu4 = ld4(p.mean + sc), rs4 = ld4(p.rstd + sc);
+        float4 g4 = make_float4(1.f, 1.f, 1.f, 1.f), b4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (p.gamma) {
+            g4 = ld4(p.gamma + ch);
+            b4 = ld4(p.beta + ch);
+        }
+        const float mu[4] = {mu4.x, mu4.y, mu4.z, mu4.w}, rs[4] = {rs4.x, rs4.y, rs4.z, rs4.w};
+        const float gg[4] = {g4.x, g4.y, g4.z, g4.w}, bb[4] = {b4.x, b4.y, b4.z, b4.w};
+        const int64_t r1 = min(e, r0 + kRowsChunk);
+        for (int64_t r = r0 + rg; r < r1; r += 64) {
+            float4 xv[4], dv[4], yv[4];
+            float rd[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int64_t rr = min(r + 16 * u, r1 - 1);
+                const int64_t o = rr * C + ch;
+                xv[u] = ld4(p.a.x + o);
+                dv[u] = ld4(dy + o);
+                yv[u] = p.residual ? ld4(y + o) : make_float4(0.f, 0.f, 0.f, 0.f);
+                rd[u] = p.a.row_div ? p.a.row_div[rr] : 1.f;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (r + 16 * u >= r1) break;
+                const float xs[4] = {xv[u].x, xv[u].y, xv[u].z, xv[u].w};
+                const float ds[4] = {dv[u].x, dv[u].y, dv[u].z, dv[u].w};
+                const float ys[4] = {yv[u].x, yv[u].y, yv[u].z, yv[u].w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const float v = p.a.row_div ? xs[j] / rd[u] : xs[j];
+                    const float xh = (v - mu[j]) * rs[j];
+                    float gr = ds[j];
+                    if (p.residual) gr *= act_grad(ys[j], p.post_act);
+                    const float dz = gr * act_grad(xh * gg[j] + bb[j], p.act);
+                    s1[j] += (double)dz;
+                    s2[j] += (double)dz * (double)xh;
+                }
+            }
+        }
+    }
+    __shared__ double l1[16][64], l2[16][64];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        l1[rg][4 * qd + j] = s1[j];
+        l2[rg][4 * qd + j] = s2[j];
+    }
+    __syncthreads();
+    const int l = threadIdx.x;
+    if (l < 64 && blockIdx.z * 64 + l < C) {
+        double t1 = 0.0, t2 = 0.0;
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+            t1 += l1[g][l];
+            t2 += l2[g][l];
+        }
+        double* q = part + (((int64_t)seg * p.a.n_chunks + chunk) * C + blockIdx.z * 64 + l) * 2;
+        q[0] = t1;
+        q[1] = t2;
+    }
+}
+
+__global__ void __launch_bounds__(256)
+segnorm_bwd_apply4_kernel(SegApply p, const float* __restrict__ dy, const float* __restrict__ y,
+                          const float* __restrict__ sums, float* __restrict__ dx,
+                          float* __restrict__ dres) {
+    __shared__ int64_t so[kSegLds + 1];
+    if (p.a.n_seg <= kSegLds)
+        for (int i = threadIdx.x; i <= p.a.n_seg; i += 256) so[i] = p.a.seg_off[i];
+    __syncthreads();
+    const int C = p.a.c, c4 = C >> 2;
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= (int)(p.n * c4)) return;
+    const int r = t / c4;
+    const int ch = 4 * (t - r * c4);
+    const int seg = seg_of_row(so, p.a.seg_off, p.a.n_seg, r);
+    const int64_t sc = (int64_t)seg * C + ch;
+    const int64_t o = 4 * (int64_t)t;
+    const float inv_n = 1.0f / (float)(p.a.seg_off[seg + 1] - p.a.seg_off[seg]);
+    const float4 mu4 = ld4(p.mean + sc), rs4 = ld4(p.rstd + sc);
+    float4 g4 = make_float4(1.f, 1.f, 1.f, 1.f), b4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (p.gamma) {
+        g4 = ld4(p.gamma + ch);
+        b4 = ld4(p.beta + ch);
+    }
+    const float rd = p.a.row_div ? p.a.row_div[r] : 1.f;
+    const float4 xv = ld4(p.a.x + o), dv = ld4(dy + o);
+    const float4 yv = p.residual ? ld4(y + o) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 sa = ld4(sums + 2 * sc), sb = ld4(sums + 2 * sc + 4);   // (s1, s2) per channel
+    const float mu[4] = {mu4.x, mu4.y, mu4.z, mu4.w}, rs[4] = {rs4.x, rs4.y, rs4.z, rs4.w};
+    const float gg[4] = {g4.x, g4.y, g4.z, g4.w}, bb[4] = {b4.x, b4.y, b4.z, b4.w};
+    const float xs[4] = {xv.x, xv.y, xv.z, xv.w}, ds[4] = {dv.x, dv.y, dv.z, dv.w};
+    const float ys[4] = {yv.x, yv.y, yv.z, yv.w};
+    const float m1s[4] = {sa.x, sa.z, sb.x, sb.z}, m2s[4] = {sa.y, sa.w, sb.y, sb.w};
+    float gx[4], gres[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const float v = xs[j] / rd;
+        const float xh = (v - mu[j]) * rs[j];
+        float gr = ds[j];
+        if (p.residual) gr *= act_grad(ys[j], p.post_act);
+        gres[j] = gr;
+        const float dz = gr * act_grad(xh * gg[j] + bb[j], p.act);
+        const float m1 = m1s[j] * inv_n, m2 = m2s[j] * inv_n;
+        gx[j] = rs[j] * gg[j] * (dz - m1 - xh * m2) / rd;
+    }
+    if (dres) *reinterpret_cast<float4*>(dres + o) = make_float4(gres[0], gres[1], gres[2], gres[3]);
+    *reinterpret_cast<float4*>(dx + o) = make_float4(gx[0], gx[1], gx[2], gx[3]);
 }
 
 // ---- LayerNorm backward ------------------------------------------------------------------
@@ -1276,6 +1515,15 @@ extern "C" int fgr_corr_attention_bwd(const float* q, int64_t ld_q, const float*
     return FGR_OK;
 }
 
+// the float4 segment-norm kernels: c % 4 == 0, every given pointer 16-B aligned (NULL
+// allowed), float4 indices below 2^31
+static bool seg_vec_ok(int64_t n, int c, std::initializer_list<const void*> ptrs) {
+    if (c % 4 != 0 || n * c / 4 >= (int64_t)1 << 31) return false;
+    for (const void* q : ptrs)
+        if (reinterpret_cast<uintptr_t>(q) & 15) return false;
+    return true;
+}
+
 static int seg_chunks(int64_t max_seg_len) { return (int)std::max<int64_t>(1, ceil_div(max_seg_len, kRowsChunk)); }
 
 extern "C" int fgr_segnorm_workspace(int64_t max_seg_len, int32_t c, int32_t n_seg, size_t* bytes) {
@@ -1295,8 +1543,12 @@ extern "C" int fgr_segnorm_stats(const float* x, int64_t n, int32_t c, const int
     FGR_REQUIRE(ws_bytes >= need, "fgr_segnorm_stats: workspace too small");
     SegArgs a{x, row_div, seg_off, n_seg, c, seg_chunks(max_seg_len)};
     hipStream_t st = as_stream(stream);
-    hipLaunchKernelGGL(segnorm_stats_kernel, dim3(a.n_chunks, n_seg, (unsigned)ceil_div(c, 64)), dim3(256),
-                       0, st, a, (double*)ws);
+    if (seg_vec_ok(n, c, {x}))
+        hipLaunchKernelGGL(segnorm_stats4_kernel, dim3(a.n_chunks, n_seg, (unsigned)ceil_div(c, 64)),
+                           dim3(256), 0, st, a, (double*)ws);
+    else
+        hipLaunchKernelGGL(segnorm_stats_kernel, dim3(a.n_chunks, n_seg, (unsigned)ceil_div(c, 64)),
+                           dim3(256), 0, st, a, (double*)ws);
     FGR_CHECK_LAUNCH("segnorm_stats_kernel");
     hipLaunchKernelGGL(segnorm_merge_kernel, dim3((unsigned)ceil_div((int64_t)n_seg * c, 256)), dim3(256),
                        0, st, a, (const double*)ws, eps, mean, rstd, var);
@@ -1312,8 +1564,12 @@ extern "C" int fgr_segnorm_apply(const float* x, int64_t n, int32_t c, const int
     if (n == 0) return FGR_OK;
     FGR_REQUIRE(x && seg_off && mean && rstd && out, "fgr_segnorm_apply: null pointer");
     SegApply p{{x, row_div, seg_off, n_seg, c, 1}, n, mean, rstd, gamma, beta, act, residual, post_act};
-    hipLaunchKernelGGL(segnorm_apply_kernel, dim3((unsigned)ceil_div(n * c, 256)), dim3(256), 0,
-                       as_stream(stream), p, out);
+    if (seg_vec_ok(n, c, {x, out, residual, mean, rstd, gamma, beta}))
+        hipLaunchKernelGGL(segnorm_apply4_kernel, dim3((unsigned)ceil_div(n * c / 4, 256)), dim3(256), 0,
+                           as_stream(stream), p, out);
+    else
+        hipLaunchKernelGGL(segnorm_apply_kernel, dim3((unsigned)ceil_div(n * c, 256)), dim3(256), 0,
+                           as_stream(stream), p, out);
     FGR_CHECK_LAUNCH("segnorm_apply_kernel");
     return FGR_OK;
 }
@@ -1340,15 +1596,25 @@ extern "C" int fgr_segnorm_bwd(const float* x, int64_t n, int32_t c, const int64
     SegApply p{{x, row_div, seg_off, n_seg, c, nch}, n, mean, rstd, gamma, beta, act,
                has_residual ? y : nullptr, post_act};
     hipStream_t st = as_stream(stream);
-    hipLaunchKernelGGL(segnorm_bwd_stats_kernel, dim3(nch, n_seg, (unsigned)ceil_div(c, 64)), dim3(256), 0,
-                       st, p, dy, y, part);
+    const bool vec = seg_vec_ok(n, c, {x, dy, has_residual ? y : nullptr, dx, has_residual ? dres : nullptr,
+                                       mean, rstd, gamma, beta, sums});
+    if (vec)
+        hipLaunchKernelGGL(segnorm_bwd_stats4_kernel, dim3(nch, n_seg, (unsigned)ceil_div(c, 64)), dim3(256),
+                           0, st, p, dy, y, part);
+    else
+        hipLaunchKernelGGL(segnorm_bwd_stats_kernel, dim3(nch, n_seg, (unsigned)ceil_div(c, 64)), dim3(256),
+                           0, st, p, dy, y, part);
     FGR_CHECK_LAUNCH("segnorm_bwd_stats_kernel");
     hipLaunchKernelGGL(segnorm_bwd_merge_kernel, dim3((unsigned)ceil_div((int64_t)n_seg * c, 256)),
                        dim3(256), 0, st, p.a, (const double*)part, sums, dgamma, dbeta);
     FGR_CHECK_LAUNCH("segnorm_bwd_merge_kernel");
     if (n == 0) return FGR_OK;
-    hipLaunchKernelGGL(segnorm_bwd_apply_kernel, dim3((unsigned)ceil_div(n * c, 256)), dim3(256), 0, st,
-                       p, dy, y, (const float*)sums, dx, has_residual ? dres : nullptr);
+    if (vec)
+        hipLaunchKernelGGL(segnorm_bwd_apply4_kernel, dim3((unsigned)ceil_div(n * c / 4, 256)), dim3(256), 0,
+                           st, p, dy, y, (const float*)sums, dx, has_residual ? dres : nullptr);
+    else
+        hipLaunchKernelGGL(segnorm_bwd_apply_kernel, dim3((unsigned)ceil_div(n * c, 256)), dim3(256), 0, st,
+                           p, dy, y, (const float*)sums, dx, has_residual ? dres : nullptr);
     FGR_CHECK_LAUNCH("segnorm_bwd_apply_kernel");
     return FGR_OK;
 }

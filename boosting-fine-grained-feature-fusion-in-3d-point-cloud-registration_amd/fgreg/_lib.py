@@ -124,6 +124,8 @@ SIGNATURES = {
                         _vp, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp],
     'fgr_colsum_workspace': [_i64, _i32, ctypes.POINTER(_sz)],
     'fgr_colsum': [_vp, _i64, _i32, _i64, _vp, _vp, _sz, _vp],
+    'fgr_gemm_wgrad_workspace': [_i64, _i32, _i32, _i32, ctypes.POINTER(_sz)],
+    'fgr_gemm_f16x3_wgrad': [_vp, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _i64, _vp, _vp, _sz, _vp],
     'fgr_layernorm_bwd_workspace': [_i64, _i32, ctypes.POINTER(_sz)],
     'fgr_layernorm_bwd': [_vp, _i64, _i32, _vp, _f32, _vp, _vp, _vp, _vp, _sz, _vp],
     'fgr_attention_bwd_workspace': [_i64, _i32, ctypes.POINTER(_sz)],
@@ -180,3 +182,22 @@ def check(rc, name):
     if rc != 0:
         msg = load().fgr_last_error().decode(errors='replace')
         raise FgrError(f'{name} failed ({rc}): {msg}')
+
+
+_WS_SIZES = {}
+
+
+def ws_size(name, *args):
+    """Bytes a `*_workspace(args..., size_t* bytes)` entry point reports, memoised per
+    (name, args): the queries are pure functions of the shape, and training issues hundreds
+    per step."""
+    key = (name,) + args
+    v = _WS_SIZES.get(key)
+    if v is None:
+        nb = _sz(0)
+        check(getattr(load(), name)(*args, nb), name)
+        v = nb.value
+        if len(_WS_SIZES) > 65536:
+            _WS_SIZES.clear()
+        _WS_SIZES[key] = v
+    return v

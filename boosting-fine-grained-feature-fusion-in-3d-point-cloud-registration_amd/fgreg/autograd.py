@@ -29,6 +29,7 @@ Elementwise glue between them (ReLU masks, the bottleneck's LeakyReLU(x + shortc
 concatenation) is torch on the same device. No CPU path: every op raises on host tensors.
 """
 import math
+import os
 
 import torch
 import torch.nn.functional as F
@@ -46,16 +47,51 @@ def colsum(x: torch.Tensor) -> torch.Tensor:
     n, c = x.shape
     out = torch.empty((c,), dtype=torch.float32, device=x.device)
     L = _lib.load()
-    nb = _lib._sz(0)
-    _lib.check(L.fgr_colsum_workspace(n, c, nb), 'fgr_colsum_workspace')
-    ws = torch.empty(nb.value, dtype=torch.uint8, device=x.device)
-    _lib.check(L.fgr_colsum(_ptr(x), n, c, max(x.stride(0), c), _ptr(out), _ptr(ws), nb.value,
+    nb = _lib.ws_size('fgr_colsum_workspace', n, c)
+    ws = torch.empty(nb, dtype=torch.uint8, device=x.device)
+    _lib.check(L.fgr_colsum(_ptr(x), n, c, max(x.stride(0), c), _ptr(out), _ptr(ws), nb,
                             _stream()), 'fgr_colsum')
     return out
 
 
+_WGRAD = os.environ.get('FGREG_WGRAD', '1') != '0'     # 0: dW on the generic GEMM (A/B)
+
+
+def _wgrad_ok(t):
+    return t.dim() == 2 and t.stride(1) == 1 and t.stride(0) % 4 == 0 and t.data_ptr() % 16 == 0
+
+
+def wgrad(a: torch.Tensor, b: torch.Tensor, bias_grad=False):
+    """a^T b (m, n) of row-major a (rows, m) and b (rows, n): the weight gradient dW = dY^T X
+    (and with bias_grad, also the column sums of a: (dW, db)). f16x3 mode with m, n % 4 == 0:
+    fgr_gemm_f16x3_wgrad straight from both activations, db in the same launches; otherwise
+    the GEMM of the transposed copy of a with b as its (transposed) weight image, and
+    fgr_colsum."""
+    rows, m = a.shape
+    n = b.shape[1]
+    if not (_WGRAD and lin.MODE == 'f16x3' and m % 4 == 0 and n % 4 == 0):
+        dw = linear(a.t().contiguous(), b, transpose=True, cache=False)
+        return (dw, colsum(a.contiguous())) if bias_grad else dw
+    _dev(a, b)
+    if not _wgrad_ok(a):
+        a = a.contiguous().clone() if a.is_contiguous() else a.contiguous()
+    if not _wgrad_ok(b):
+        b = b.contiguous().clone() if b.is_contiguous() else b.contiguous()
+    out = torch.empty((m, n), dtype=torch.float32, device=a.device)
+    db = torch.empty((m,), dtype=torch.float32, device=a.device) if bias_grad else None
+    nb = _lib.ws_size('fgr_gemm_wgrad_workspace', rows, m, n, int(bias_grad))
+    ws = ops._workspace(a.device, nb) if nb else None
+    t0 = ops._begin('gemm', (m, n, rows))
+    _lib.check(_lib.load().fgr_gemm_f16x3_wgrad(
+        _ptr(a), a.stride(0), _ptr(b), b.stride(0), rows, m, n, _ptr(out), out.stride(0), _ptr(db),
+        _ptr(ws), nb, _stream()), 'fgr_gemm_f16x3_wgrad')
+    ops._end('gemm', t0, 2 * m * n * rows)
+    return (out, db) if bias_grad else out
+
+
 def _relu_mask(dy, y):
-    return torch.where(y > 0, dy, torch.zeros_like(dy))
+    """dy where the ReLU output y > 0, else 0 (one elementwise launch)."""
+    return torch.ops.aten.threshold_backward(dy, y, 0)
 
 
 # ------------------------------------------------------------------------------------------
@@ -78,12 +114,16 @@ class _LinearFn(torch.autograd.Function):
         if ctx.act == ACT_RELU:
             dy = _relu_mask(dy, y)
         dx = dw = db = None
+        want_db = ctx.has_b and ctx.needs_input_grad[2]
         with lin.mode_scope(ctx.mode):
             if ctx.needs_input_grad[0]:
                 dx = linear(dy, w, transpose=True, tag='bwd_dx', cache=ctx.cache)   # dY W
             if ctx.needs_input_grad[1]:
-                dw = linear(dy.t().contiguous(), x, transpose=True, cache=False)   # dY^T X
-        if ctx.has_b and ctx.needs_input_grad[2]:
+                if want_db:                                     # dY^T X and the column sums
+                    dw, db = wgrad(dy, x, bias_grad=True)
+                else:
+                    dw = wgrad(dy, x)                                               # dY^T X
+        if want_db and db is None:
             db = colsum(dy)
         dres = dy if ctx.has_r and ctx.needs_input_grad[3] else None
         return dx, dw, db, dres, None, None
@@ -171,9 +211,7 @@ class _KPConvFn(torch.autograd.Function):
                 dx = kpconv_scatter(q, s, idx, dwf, kp, ctx.extent)
             if ctx.needs_input_grad[1]:
                 wf, _ = ops.kpconv_gather(q, s, idx, x, kp, ctx.extent)      # regathered
-                dWt = linear(dout.t().contiguous(), wf.view(nq, K * cin), transpose=True,
-                             cache=False)
-                dW = dWt.t().reshape(K, cin, cout)                           # (dout^T wf)^T
+                dW = wgrad(wf.view(nq, K * cin), dout).view(K, cin, cout)   # wf^T dout
         return dx, dW, None, None, None, None, None
 
 
@@ -215,9 +253,8 @@ def max_pool_t(x, idx):
 # normalisation
 # ------------------------------------------------------------------------------------------
 def _seg_ws(max_len, c, n_seg, extra=0, device=None):
-    nb = _lib._sz(0)
-    _lib.check(_lib.load().fgr_segnorm_workspace(max_len, c, n_seg, nb), 'fgr_segnorm_workspace')
-    return torch.empty(nb.value + extra, dtype=torch.uint8, device=device)
+    nb = _lib.ws_size('fgr_segnorm_workspace', max_len, c, n_seg)
+    return torch.empty(nb + extra, dtype=torch.uint8, device=device)
 
 
 class _SegNormFn(torch.autograd.Function):
@@ -277,7 +314,7 @@ def batchnorm_t(bn, x, act=ACT_NONE, residual=None, post_act=ACT_NONE):
     """nn.BatchNorm1d ``bn`` in training mode on (N, C) rows (batch statistics over all rows,
     running statistics updated in place as torch does: momentum, unbiased variance)."""
     n = x.shape[0]
-    off = torch.tensor([0, n], dtype=torch.int64, device=x.device)
+    off = ops.offsets([n], x.device)
     stats = [] if bn.track_running_stats else None
     y = segnorm_t(x, off, [n], act=act, residual=residual, post_act=post_act, gamma=bn.weight,
                   beta=bn.bias, eps=bn.eps, stats=stats)

@@ -18,9 +18,11 @@ statistics, every op differentiable on libfgreg's backward kernels) composes the
 in fgreg/training.py.
 """
 import math
+import os
 from typing import List
 
 import numpy as np
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -290,8 +292,8 @@ class my_Bottle2neck(nn.Module):  # noqa: N801 -- reference name (res2net.py:84)
                 if w1.is_cuda and self.nums > 0 and self.downsample is not None:
                     wst = torch.stack([wi for wi, _ in ws])
                     bst = torch.stack([bi for _, bi in ws]).contiguous()
-                    # w = 224: the bf16x6 chain (measured faster -- fewer barriers); else h3
-                    if self.width == 224:
+                    # w = 224: the bf16x6 chain unless FGREG_R2N224=h3 (A/B); else h3
+                    if self.width == 224 and os.environ.get('FGREG_R2N224', 'x6') != 'h3':
                         chain = (bst, ops.res2net_fragments3(wst), None)
                     elif ops.res2net_chain_supported(self.width, True):
                         chain = (bst,) + ops.res2net_fragments_h3(wst)

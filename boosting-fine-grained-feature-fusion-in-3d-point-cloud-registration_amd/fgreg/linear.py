@@ -137,14 +137,12 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act=ACT_NONE, residual=N
     L = _lib.load()
     t0 = _begin('gemm', (m, n, k))
     # split-K workspace where the dispatcher wants one (few rows, long K)
-    nb = _lib._sz(0)
-    _lib.check(L.fgr_gemm_workspace(m, n, k, 0 if MODE == 'f16x3' else 1, nb),
-               'fgr_gemm_workspace')
-    ws = ops._workspace(x.device, nb.value) if nb.value else None
+    nb = _lib.ws_size('fgr_gemm_workspace', m, n, k, 0 if MODE == 'f16x3' else 1)
+    ws = ops._workspace(x.device, nb) if nb else None
     _lib.check(getattr(L, 'fgr_gemm_' + MODE + '_ws')(
         _ptr(x), x.stride(0), _ptr(sw.img), _ptr(out), out.stride(0), _ptr(bias),
         _ptr(residual), residual.stride(0) if residual is not None else 0, m, n, k, act,
-        _ptr(ws), nb.value, _stream()), 'fgr_gemm_' + MODE)
+        _ptr(ws), nb, _stream()), 'fgr_gemm_' + MODE)
     _end('gemm', t0, 2 * m * n * k)
     return out
 

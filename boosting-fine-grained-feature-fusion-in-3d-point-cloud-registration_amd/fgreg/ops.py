@@ -132,12 +132,23 @@ def _c(t, dtype):
     return t.contiguous()
 
 
+def to_device(values, dtype, device) -> torch.Tensor:
+    """A host list -> a device tensor without draining the stream: staged through pinned
+    memory and copied asynchronously on the current stream (torch's caching host allocator
+    keeps the staging block until that copy has run); a pageable torch.tensor(..., device=)
+    would wait for all queued GPU work first."""
+    t = torch.tensor(values, dtype=dtype)
+    if torch.device(device).type != 'cuda':
+        return t.to(device)
+    return t.pin_memory().to(device, non_blocking=True)
+
+
 def offsets(lengths: Sequence[int], device) -> torch.Tensor:
     """Host lengths -> device int64 row offsets (len + 1)."""
     o = [0]
     for n in lengths:
         o.append(o[-1] + int(n))
-    return torch.tensor(o, dtype=torch.int64, device=device)
+    return to_device(o, torch.int64, device)
 
 
 # ------------------------------------------------------------------------------------------

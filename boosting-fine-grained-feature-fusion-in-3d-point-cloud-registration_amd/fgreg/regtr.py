@@ -199,7 +199,7 @@ class CorrespondenceDecoder(nn.Module):
         dev = q.device
         idx = torch.cat(rows).to(dev)
         off = ops.offsets(lens, dev)
-        kv_seg = torch.tensor(kv, dtype=torch.int32, device=dev)
+        kv_seg = ops.to_device(kv, torch.int32, dev)
         cp = corr[idx].contiguous()
         flags = ops.corr_topk_mask(cp, q[idx].contiguous(), k[idx].contiguous(), off, off, kv_seg,
                                    4 * B, max(lens), max_kv, 1.0 / math.sqrt(d),

@@ -57,9 +57,9 @@ class Segments:
         self.n_phantom = sum(self.phantoms)
         self.off = ops.offsets(self.seg_lengths, device)
         self.cloud_off = self.off[:n + 1]
-        self.self_seg = torch.tensor(self.seg_cloud, dtype=torch.int32, device=device)
-        self.cross_seg = torch.tensor([(c + self.B) % n for c in self.seg_cloud],
-                                      dtype=torch.int32, device=device)
+        self.self_seg = ops.to_device(self.seg_cloud, torch.int32, device)
+        self.cross_seg = ops.to_device([(c + self.B) % n for c in self.seg_cloud], torch.int32,
+                                       device)
         self.max_len = max(self.seg_lengths) if n else 0
         self.layer_tables = None
         if n_layers:
@@ -75,9 +75,9 @@ class Segments:
             q_off.append(n_layers * N)
             kv_seg = [l * S + (c + self.B) % n for l in range(n_layers) for c in self.seg_cloud]
             v_off = host_off * n_layers
-            self.layer_tables = (torch.tensor(q_off, dtype=torch.int64, device=device),
-                                 torch.tensor(kv_seg, dtype=torch.int32, device=device),
-                                 torch.tensor(v_off, dtype=torch.int64, device=device))
+            self.layer_tables = (ops.to_device(q_off, torch.int64, device),
+                                 ops.to_device(kv_seg, torch.int32, device),
+                                 ops.to_device(v_off, torch.int64, device))
 
 
 class TransformerCrossEncoderLayer(nn.Module):

@@ -627,6 +627,20 @@ int fgr_attention_bwd_drop(const float* q, int64_t ldq, const float* k, int64_t 
                            int32_t nhead, int32_t dh, float scale, void* ws, size_t ws_bytes,
                            uint32_t seed, float p, void* stream);
 
+/* Weight gradient of a dense product, dW = dY^T X (every nn.Linear / KPConv weight of the
+ * backward, trainer.py:110-125), read straight from the two row-major activations:
+ *   dw[i][j] = sum_{r < rows} dy[r * ld_dy + i] * x[r * ld_x + j]      (i < m, j < n)
+ * and, when db is not NULL, the bias gradient db[i] = sum_r dy[r * ld_dy + i] (fp64 sums).
+ * fp32-accurate (f16x3: per-chunk column scales, three fp16 products, fp32 accumulation);
+ * m, n, the row strides and ld_dw multiples of 4, dy / x / dw 16-B aligned. Rows are split
+ * into chunks whose partials are summed in chunk order (deterministic); the workspace
+ * fgr_gemm_wgrad_workspace(rows, m, n, db != NULL) bytes holds them (0 when one chunk
+ * suffices). rows == 0 writes zeros. */
+int fgr_gemm_wgrad_workspace(int64_t rows, int32_t m, int32_t n, int32_t with_bias, size_t* bytes);
+int fgr_gemm_f16x3_wgrad(const float* dy, int64_t ld_dy, const float* x, int64_t ld_x,
+                         int64_t rows, int32_t m, int32_t n, float* dw, int64_t ld_dw, float* db,
+                         void* ws, size_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

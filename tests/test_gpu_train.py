@@ -149,17 +149,19 @@ def _segnorm_ref(x, lens, row_div, gamma, beta, act, residual, post, eps=1e-5):
 
 @pytest.mark.parametrize('case', ['instnorm', 'instnorm_rowdiv_leaky', 'instnorm_residual',
                                   'batchnorm_relu', 'batchnorm_residual_relu', 'long_segments'])
-def test_segnorm_backward(gpu, case):
+@pytest.mark.parametrize('c', [72, 70])
+def test_segnorm_backward(gpu, case, c):
     """segnorm_t: InstanceNorm per cloud (with the KPConv row divisor, LeakyReLU, the
     bottleneck's residual + LeakyReLU) and training BatchNorm (one segment, affine, ReLU,
-    residual + ReLU) vs the same formulas in fp64."""
+    residual + ReLU) vs the same formulas in fp64; c = 72 runs the float4 kernels, 70 the
+    scalar ones."""
     from fgreg import ops
     from fgreg.autograd import segnorm_t
     g = torch.Generator().manual_seed(len(case))
     lens = [700, 300, 1, 513] if case != 'long_segments' else [20000, 9000]
     if case.startswith('batchnorm'):
         lens = [sum(lens)]
-    n, c = sum(lens), 72
+    n = sum(lens)
     x, x64 = _leaf(torch.randn(n, c, generator=g) * 3 + 5, gpu)
     rd = (1 + torch.randint(0, 9, (n,), generator=g)).float() if 'rowdiv' in case else None
     affine = case.startswith('batchnorm')
@@ -444,6 +446,41 @@ def test_colsum(gpu):
     assert rel_err(got, x.float().double()[:, 7:250].sum(0)) < 1e-6
 
 
+@pytest.mark.parametrize('rows,m,n', [(0, 64, 32), (1, 4, 4), (37, 12, 20), (1000, 132, 260),
+                                      (9544, 256, 256), (9544, 1024, 2048), (11472, 128, 1920),
+                                      (20000, 3840, 256)])
+@pytest.mark.parametrize('strided', [False, True])
+def test_wgrad(gpu, rows, m, n, strided):
+    """fgr_gemm_f16x3_wgrad (dW = dY^T X straight from the activations) vs fp64: every element
+    within 1e-6 of its Cauchy-Schwarz scale |dY[:, i]| |X[:, j]| -- columns spanning twelve
+    decades, so a per-tile (not per-column) scale would fail -- and bit-identical on a rerun."""
+    from fgreg import autograd as ag
+    from fgreg import linear as lin
+    assert lin.MODE == 'f16x3'
+    g = torch.Generator().manual_seed(rows + m + n)
+    a = torch.randn(rows, m, generator=g) * 10.0 ** torch.empty(m).uniform_(-6, 6, generator=g)
+    b = torch.randn(rows, n, generator=g) * 10.0 ** torch.empty(n).uniform_(-6, 6, generator=g)
+    a[: rows // 3] *= 1e-3                        # rows of very different size in one chunk
+    if strided:
+        ag_, bg_ = torch.zeros(rows, m + 12, device=gpu), torch.zeros(rows, n + 8, device=gpu)
+        ag_[:, 8:8 + m] = a.to(gpu)
+        bg_[:, 4:4 + n] = b.to(gpu)
+        ad, bd = ag_[:, 8:8 + m], bg_[:, 4:4 + n]
+    else:
+        ad, bd = a.to(gpu), b.to(gpu)
+    got = ag.wgrad(ad, bd)
+    assert torch.equal(got, ag.wgrad(ad, bd))
+    got2, db = ag.wgrad(ad, bd, bias_grad=True)        # the fused bias gradient: same dW
+    assert torch.equal(got, got2)
+    db_want = a.double().sum(0)
+    assert ((db.double().cpu() - db_want).abs() <= 1e-6 * a.double().abs().sum(0) + 1e-30).all()
+    got = got.double().cpu()
+    want = a.double().t() @ b.double()
+    scale = a.double().norm(dim=0)[:, None] * b.double().norm(dim=0)[None, :]
+    err = ((got - want).abs() / scale.clamp_min(1e-300)).max().item() if rows else got.abs().max().item()
+    assert err < 1e-6, err
+
+
 # ------------------------------------------------------------------------------------------
 # whole training steps
 # ------------------------------------------------------------------------------------------
@@ -607,3 +644,44 @@ def test_train_step_vs_oracle_modelnet(gpu, pre_norm, head):
     assert cos > 1 - cos_tol
     for k, e in errs.items():
         assert e < tol, (k, e)
+
+
+def _h3_image_ref(W):
+    """The f16x3 weight image of fgr_split_weights_h3 restated in numpy: rows scaled by 2^e
+    (max |w| in [2^14, 2^15)), two fp16 terms, units [panel][kstep][term][g][row][8]; then the
+    per-row inverse scales (0 past n)."""
+    n, k = W.shape
+    npad, ks = -(-n // 16) * 16, -(-k // 64) * 2
+    mx = np.abs(W).max(1)
+    e = np.where(mx > 0, np.minimum(15 - np.frexp(mx)[1], 127), 0)
+    wp = np.zeros((npad, ks * 32), np.float32)
+    wp[:n, :k] = W * np.ldexp(np.float32(1), e).astype(np.float32)[:, None]
+    hi = wp.astype(np.float16)
+    lo = (wp - hi.astype(np.float32)).astype(np.float16)
+    img = np.stack([hi, lo]).reshape(2, npad // 16, 16, ks, 4, 8).transpose(1, 3, 0, 4, 2, 5)
+    wsc = np.zeros(npad, np.float32)
+    wsc[:n] = np.ldexp(np.float32(1), -e)
+    return np.ascontiguousarray(img).tobytes() + wsc.tobytes()
+
+
+@pytest.mark.parametrize('shape,transpose', [((256, 256), False), ((1024, 256), False),
+                                             ((37, 100), False), ((256, 1024), False),
+                                             ((64, 2048), False), ((15, 16, 24), True),
+                                             ((15, 64, 256), True), ((1024, 96), True),
+                                             ((2048, 64), True)])
+def test_weight_image_bits(gpu, shape, transpose):
+    """Split weight images (the fused one-launch split for k <= 1024, the two-launch one beyond,
+    row-major W and the transposed views the backward uses) equal their numpy restatement bit
+    for bit."""
+    from fgreg import linear as lin
+    g = torch.Generator().manual_seed(sum(shape))
+    w = torch.randn(shape, generator=g) * 10.0 ** torch.empty(shape[0]).uniform_(-3, 3, generator=g).view(
+        -1, *([1] * (len(shape) - 1)))
+    if transpose:                              # W = w.reshape(k, n).t(): column-major rows
+        ent = lin.weight_image(w.to(gpu), transpose=True, mode='f16x3', cache=False)
+        ref = _h3_image_ref(w.reshape(-1, shape[-1]).t().contiguous().numpy())
+    else:
+        ent = lin.weight_image(w.to(gpu), mode='f16x3', cache=False)
+        ref = _h3_image_ref(w.numpy())
+    got = ent.img.cpu().numpy().tobytes()
+    assert len(got) == len(ref) and got == ref
