@@ -211,6 +211,22 @@ def train_main(args):
     for _ in range(max(args.warmup, 1)):
         step()
     torch.cuda.synchronize()
+    if args.gemm_table:
+        # per-shape device time of the dense products (forward + dX GEMMs) and of the weight
+        # gradients (fgr_gemm_f16x3_wgrad), events around each launch, 3 extra steps
+        from fgreg import ops
+        ops.TIMER = ops.KernelTimer(['gemm', 'wgrad'])
+        ops.TIMER.lead_cycles = args.lead_cycles
+        t_steps = 3
+        t0 = time.perf_counter()
+        for _ in range(t_steps):
+            step()
+        torch.cuda.synchronize()
+        step_ms = (time.perf_counter() - t0) / t_steps * 1e3
+        write_gemm_table(args.gemm_table, ops.TIMER, t_steps, step_ms, lin.MODE)
+        write_gemm_table(args.gemm_table.replace('.json', '') + '_wgrad.json', ops.TIMER, t_steps,
+                         step_ms, lin.MODE, name='wgrad')
+        ops.TIMER = None
     if args.profile:
         torch.cuda._sleep(1000)
     t0 = time.perf_counter()
@@ -554,7 +570,7 @@ def write_gather_table(path, rtimer, work, steps, step_ms):
                   f, indent=1)
 
 
-def write_gemm_table(path, rtimer, steps, step_ms, mode):
+def write_gemm_table(path, rtimer, steps, step_ms, mode, name='gemm'):
     """Per-shape table of the dense layers (bytes, flops, time and the binding
     roof per shape). bytes = the minimum operand traffic 4 M K (A) + 4 N K (f16x3 image:
     2 terms x 2 B; 2 N K for the single-term bf16 image) + 4 M N (C), assuming every operand
@@ -563,7 +579,7 @@ def write_gemm_table(path, rtimer, steps, step_ms, mode):
     wb = 2.0 if mode == 'bf16' else 4.0
     mfma_peak = F16_MFMA_PEAK_TFLOPS / pipe
     rows = []
-    for (m, n, k), (ms, cnt) in sorted(rtimer.per_label('gemm').items(),
+    for (m, n, k), (ms, cnt) in sorted(rtimer.per_label(name).items(),
                                        key=lambda kv: -kv[1][0]):
         us = ms * 1e3 / cnt
         flops = 2.0 * m * n * k

@@ -18,6 +18,7 @@
 // bias gradient the tile column j0 = 0 also sums its dy columns in fp64 (db = sum_r dy[r][i]),
 // partials per chunk summed in the same reduce launch: the separate column-sum pass goes away.
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -53,7 +54,7 @@ __device__ __forceinline__ int wg_scale_exp(float mx) {
     return mx > 0.f ? min(15 - __builtin_amdgcn_frexp_expf(mx), 127) : 0;
 }
 
-__global__ void __launch_bounds__(256) wgrad_f16x3_kernel(WgradArgs p) {
+__global__ void __launch_bounds__(256, 3) wgrad_f16x3_kernel(WgradArgs p) {   // 3 waves / SIMD
     __shared__ _Float16 img[2][2][kWgImg];         // [operand][term]: 40 KB (3 workgroups / CU)
     __shared__ float4 cmx[256];                    // pre-pass maxima per thread
     __shared__ float inv_s[2][kWgT];               // per operand column: 1 / scale
@@ -72,20 +73,48 @@ __global__ void __launch_bounds__(256) wgrad_f16x3_kernel(WgradArgs p) {
     const bool cok = col0 < lim;                   // lim % 4 == 0: all four or none
     const float* base = (op ? p.x : p.dy) + (cok ? col0 : 0);
 
-    // pre-pass: column maxima of the chunk (rows kg, kg + 4, ...; 4 loads in flight,
-    // every load unconditional at a clamped row)
+    // pre-pass: column maxima of the chunk (rows kg, kg + 4, ...; 8 loads in flight per
+    // thread, every load unconditional at a clamped row); the bias gradient rides on the dy
+    // reads of the first tile column (fp64 column sums of the chunk)
+    const bool bias_sums = p.db && op == 0 && tj == 0;
+    double bs[4] = {0.0, 0.0, 0.0, 0.0};
     float m0 = 0.f, m1 = 0.f, m2 = 0.f, m3 = 0.f;
-    for (int64_t r = rb + kg; r < re; r += 16) {
-        float4 v[4];
+    for (int64_t r = rb + kg; r < re; r += 32) {
+        float4 v[8];
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
+        for (int u = 0; u < 8; ++u)
             v[u] = *reinterpret_cast<const float4*>(base + min(r + 4 * u, re - 1) * ld);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < 8; ++u) {
             m0 = fmaxf(m0, fabsf(v[u].x));
             m1 = fmaxf(m1, fabsf(v[u].y));
             m2 = fmaxf(m2, fabsf(v[u].z));
             m3 = fmaxf(m3, fabsf(v[u].w));
+        }
+        if (bias_sums) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (r + 4 * u < re) {
+                    bs[0] += (double)v[u].x;
+                    bs[1] += (double)v[u].y;
+                    bs[2] += (double)v[u].z;
+                    bs[3] += (double)v[u].w;
+                }
+        }
+    }
+    if (p.db && tj == 0) {                         // (block-uniform) fold the 4 row groups
+        __shared__ double bred[4][kWgT];
+        if (op == 0) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) bred[kg][4 * c4 + q] = cok ? bs[q] : 0.0;
+        }
+        __syncthreads();
+        if (tid < kWgT && i0 + tid < p.m) {
+            const double t = ((bred[0][tid] + bred[1][tid]) + bred[2][tid]) + bred[3][tid];
+            if (p.part_db)
+                p.part_db[(int64_t)blockIdx.y * p.m + i0 + tid] = t;
+            else
+                p.db[i0 + tid] = (float)t;
         }
     }
     cmx[tid] = make_float4(m0, m1, m2, m3);
@@ -112,11 +141,11 @@ __global__ void __launch_bounds__(256) wgrad_f16x3_kernel(WgradArgs p) {
     for (int q = 0; q < 4; ++q) s[q] = scl[op][4 * c4 + q];
 
     const int nk = (int)((re - rb + kWgK - 1) / kWgK);
-    float v[8][4];                                 // this thread's 8 rows x 4 columns
-    // the bias gradient rides on the dy tiles of the first tile column: fp64 column sums
-    const bool bias_sums = p.db && op == 0 && tj == 0;
-    double bs[4] = {0.0, 0.0, 0.0, 0.0};
-    auto load = [&](int ks) {
+    // this thread's 8 rows x 4 columns of a k-step (the next k-step's loads are issued before
+    // the matrix-core work on the current one; a second register set measured slower: 282
+    // VGPRs, one workgroup per CU instead of three)
+    float va[8][4];
+    auto load = [&](float (&v)[8][4], int ks) {
         const int64_t r0 = rb + (int64_t)ks * kWgK + 8 * kg;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -129,7 +158,7 @@ __global__ void __launch_bounds__(256) wgrad_f16x3_kernel(WgradArgs p) {
             v[e][3] = ok ? t.w : 0.f;
         }
     };
-    auto store = [&]() {
+    auto store = [&](const float (&v)[8][4]) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             f16x8 th, tm;
@@ -152,21 +181,7 @@ __global__ void __launch_bounds__(256) wgrad_f16x3_kernel(WgradArgs p) {
     for (int fi = 0; fi < 4; ++fi)
 #pragma unroll
         for (int fj = 0; fj < 4; ++fj) acc[fi][fj] = f32x4{0.f, 0.f, 0.f, 0.f};
-    load(0);
-    for (int ks = 0; ks < nk; ++ks) {
-        if (ks) __syncthreads();                   // every wave is done with the last images
-        if (bias_sums) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                double t = 0.0;
-#pragma unroll
-                for (int e = 0; e < 8; ++e) t += (double)v[e][q];
-                bs[q] += t;
-            }
-        }
-        store();
-        if (ks + 1 < nk) load(ks + 1);
-        __syncthreads();
+    auto mfma_step = [&]() {
         f16x8 bh[4], bm[4];
 #pragma unroll
         for (int fj = 0; fj < 4; ++fj) {
@@ -186,21 +201,14 @@ __global__ void __launch_bounds__(256) wgrad_f16x3_kernel(WgradArgs p) {
                 acc[fi][fj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[fj], acc[fi][fj], 0, 0, 0);
             }
         }
-    }
-    if (p.db && tj == 0) {                         // (block-uniform) fold the 4 row groups
-        __shared__ double bred[4][kWgT];
-        if (op == 0) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) bred[kg][4 * c4 + q] = bs[q];
-        }
+    };
+    load(va, 0);
+    for (int ks = 0; ks < nk; ++ks) {
+        if (ks) __syncthreads();                   // every wave is done with the last images
+        store(va);
+        if (ks + 1 < nk) load(va, ks + 1);
         __syncthreads();
-        if (tid < kWgT && i0 + tid < p.m) {
-            const double t = ((bred[0][tid] + bred[1][tid]) + bred[2][tid]) + bred[3][tid];
-            if (p.part_db)
-                p.part_db[(int64_t)blockIdx.y * p.m + i0 + tid] = t;
-            else
-                p.db[i0 + tid] = (float)t;
-        }
+        mfma_step();
     }
     // epilogue: lane (g, c) holds D[64 wi + 16 fi + 4 g + r][64 wj + 16 fj + c]; both
     // inverse scales are powers of two (exact)
@@ -231,41 +239,66 @@ __global__ void __launch_bounds__(256) wgrad_f16x3_kernel(WgradArgs p) {
         }
 }
 
-// out[i][j] = sum over chunks, in chunk order, of part[chunk][i][j] (float4 per thread)
-// (and, past the m n / 4 tile items, db[i] = the fp64 sum of the chunks' bias partials)
+// out[i][j] = the sum over chunks of part[chunk][i][j]: a block takes 32 float4 outputs, its
+// 8 thread rows the chunks congruent to their row mod 8 (consecutive threads read consecutive
+// float4s of one chunk), the 8 partial sums combined in row order -- a fixed order, so the
+// result is deterministic. Blocks past the tile items sum the bias partials (fp64) the same way.
+constexpr int kRdQ = 32, kRdL = 8;
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ part, int chunks,
                                                            int m, int n, float* __restrict__ out,
                                                            int64_t ldo, const double* __restrict__ part_db,
                                                            float* __restrict__ db) {
-    const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int tq = threadIdx.x % kRdQ, tl = threadIdx.x / kRdQ;
     const int64_t mn4 = (int64_t)m * n / 4;
-    if (q >= mn4) {
-        const int64_t i = q - mn4;
-        if (!db || i >= m) return;
+    const int64_t tile_blocks = (mn4 + kRdQ - 1) / kRdQ;
+    if ((int64_t)blockIdx.x >= tile_blocks) {      // the bias gradient
+        __shared__ double sd[kRdL][kRdQ];
+        const int64_t i = ((int64_t)blockIdx.x - tile_blocks) * kRdQ + tq;
         double t = 0.0;
-        for (int ch = 0; ch < chunks; ++ch) t += part_db[(int64_t)ch * m + i];
-        db[i] = (float)t;
+        if (db && i < m)
+            for (int ch = tl; ch < chunks; ch += kRdL) t += part_db[(int64_t)ch * m + i];
+        sd[tl][tq] = t;
+        __syncthreads();
+        if (tl == 0 && db && i < m) {
+            double u = 0.0;
+#pragma unroll
+            for (int l = 0; l < kRdL; ++l) u += sd[l][tq];
+            db[i] = (float)u;
+        }
         return;
     }
+    const int64_t q = (int64_t)blockIdx.x * kRdQ + tq;
+    const int64_t qc = q < mn4 ? q : mn4 - 1;
     const float4* p4 = reinterpret_cast<const float4*>(part);
-    float4 s = p4[q];
-    int ch = 1;
-    for (; ch + 4 <= chunks; ch += 4) {
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    int ch = tl;
+    for (; ch + 3 * kRdL < chunks; ch += 4 * kRdL) {
         float4 t[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) t[u] = p4[(int64_t)(ch + u) * mn4 + q];
+        for (int u = 0; u < 4; ++u) t[u] = p4[(int64_t)(ch + u * kRdL) * mn4 + qc];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             s.x += t[u].x; s.y += t[u].y; s.z += t[u].z; s.w += t[u].w;
         }
     }
-    for (; ch < chunks; ++ch) {
-        const float4 t = p4[(int64_t)ch * mn4 + q];
+    for (; ch < chunks; ch += kRdL) {
+        const float4 t = p4[(int64_t)ch * mn4 + qc];
         s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
     }
-    const int64_t e = 4 * q;
-    const int64_t i = e / n, j = e - i * n;
-    *reinterpret_cast<float4*>(out + i * ldo + j) = s;
+    __shared__ float4 sf[kRdL][kRdQ];
+    sf[tl][tq] = s;
+    __syncthreads();
+    if (tl == 0 && q < mn4) {
+        float4 u = sf[0][tq];
+#pragma unroll
+        for (int l = 1; l < kRdL; ++l) {
+            const float4 t = sf[l][tq];
+            u.x += t.x; u.y += t.y; u.z += t.z; u.w += t.w;
+        }
+        const int64_t e = 4 * q;
+        const int64_t i = e / n, j = e - i * n;
+        *reinterpret_cast<float4*>(out + i * ldo + j) = u;
+    }
 }
 
 // chunks of rows per output tile: about two workgroups per CU (512) over the tiles, at least
@@ -278,10 +311,14 @@ struct WgradPlan {
 };
 
 WgradPlan wgrad_plan(int64_t rows, int m, int n) {
+    static const int64_t target = [] {           // FGR_WGRAD_WGS: workgroup target (A/B)
+        const char* e = getenv("FGR_WGRAD_WGS");
+        return (int64_t)(e ? std::max(1, atoi(e)) : 512);
+    }();
     WgradPlan pl;
     pl.tiles_n = (int)ceil_div(n, kWgT);
     pl.tiles = (int)ceil_div(m, kWgT) * pl.tiles_n;
-    int64_t ch = ceil_div(512, pl.tiles);
+    int64_t ch = ceil_div(target, pl.tiles);
     ch = std::min(ch, std::max<int64_t>(1, rows * (m + n) / ((int64_t)m * n)));
     ch = std::max<int64_t>(1, std::min(ch, ceil_div(rows, kWgK)));
     pl.kc = std::max<int64_t>(kWgK, ceil_div(ceil_div(rows, ch), kWgK) * kWgK);
@@ -338,8 +375,8 @@ extern "C" int fgr_gemm_f16x3_wgrad(const float* dy, int64_t ld_dy, const float*
     hipLaunchKernelGGL(wgrad_f16x3_kernel, dim3((unsigned)pl.tiles, (unsigned)pl.chunks), dim3(256), 0, st, a);
     FGR_CHECK_LAUNCH("wgrad_f16x3_kernel");
     if (pl.chunks > 1) {
-        const int64_t items = (int64_t)m * n / 4 + (db ? m : 0);
-        hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)ceil_div(items, 256)), dim3(256), 0, st,
+        const int64_t blocks = ceil_div((int64_t)m * n / 4, kRdQ) + (db ? ceil_div(m, kRdQ) : 0);
+        hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)blocks), dim3(kRdQ * kRdL), 0, st,
                            static_cast<const float*>(ws), pl.chunks, m, n, dw, ld_dw,
                            static_cast<const double*>(part_db), db);
         FGR_CHECK_LAUNCH("wgrad_reduce_kernel");

@@ -63,15 +63,22 @@ def _wgrad_ok(t):
 
 def wgrad(a: torch.Tensor, b: torch.Tensor, bias_grad=False):
     """a^T b (m, n) of row-major a (rows, m) and b (rows, n): the weight gradient dW = dY^T X
-    (and with bias_grad, also the column sums of a: (dW, db)). f16x3 mode with m, n % 4 == 0:
-    fgr_gemm_f16x3_wgrad straight from both activations, db in the same launches; otherwise
-    the GEMM of the transposed copy of a with b as its (transposed) weight image, and
-    fgr_colsum."""
+    (and with bias_grad, also the column sums of a: (dW, db)). f16x3 mode:
+    fgr_gemm_f16x3_wgrad straight from both activations (widths padded to a multiple of 4),
+    db in the same launches; otherwise the GEMM of the transposed copy of a with b as its
+    (transposed) weight image, and fgr_colsum."""
     rows, m = a.shape
     n = b.shape[1]
-    if not (_WGRAD and lin.MODE == 'f16x3' and m % 4 == 0 and n % 4 == 0):
+    if not (_WGRAD and lin.MODE == 'f16x3'):
         dw = linear(a.t().contiguous(), b, transpose=True, cache=False)
         return (dw, colsum(a.contiguous())) if bias_grad else dw
+    if m % 4 or n % 4:
+        # narrow operands (a 1- or 3-output head, KPConv's first layer: 15 x 1 inputs): zero
+        # columns up to a multiple of 4, then the kernel's result sliced (exact: zero columns
+        # add nothing and the per-column scales are independent)
+        pad = lambda t, k: t if k % 4 == 0 else F.pad(t, (0, (-k) % 4))      # noqa: E731
+        r = wgrad(pad(a, m), pad(b, n), bias_grad)
+        return (r[0][:m, :n].contiguous(), r[1][:m].contiguous()) if bias_grad else r[:m, :n].contiguous()
     _dev(a, b)
     if not _wgrad_ok(a):
         a = a.contiguous().clone() if a.is_contiguous() else a.contiguous()
@@ -81,11 +88,11 @@ def wgrad(a: torch.Tensor, b: torch.Tensor, bias_grad=False):
     db = torch.empty((m,), dtype=torch.float32, device=a.device) if bias_grad else None
     nb = _lib.ws_size('fgr_gemm_wgrad_workspace', rows, m, n, int(bias_grad))
     ws = ops._workspace(a.device, nb) if nb else None
-    t0 = ops._begin('gemm', (m, n, rows))
+    t0 = ops._begin('wgrad', (m, n, rows))       # (M, N, K) of the table: K = the rows
     _lib.check(_lib.load().fgr_gemm_f16x3_wgrad(
         _ptr(a), a.stride(0), _ptr(b), b.stride(0), rows, m, n, _ptr(out), out.stride(0), _ptr(db),
         _ptr(ws), nb, _stream()), 'fgr_gemm_f16x3_wgrad')
-    ops._end('gemm', t0, 2 * m * n * rows)
+    ops._end('wgrad', t0, 2 * m * n * rows)
     return (out, db) if bias_grad else out
 
 

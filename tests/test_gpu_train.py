@@ -447,6 +447,7 @@ def test_colsum(gpu):
 
 
 @pytest.mark.parametrize('rows,m,n', [(0, 64, 32), (1, 4, 4), (37, 12, 20), (1000, 132, 260),
+                                      (5000, 1, 256), (5000, 3, 130), (777, 15, 24),
                                       (9544, 256, 256), (9544, 1024, 2048), (11472, 128, 1920),
                                       (20000, 3840, 256)])
 @pytest.mark.parametrize('strided', [False, True])
