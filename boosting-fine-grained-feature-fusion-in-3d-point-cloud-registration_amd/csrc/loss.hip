@@ -192,6 +192,71 @@ infonce_rows_kernel(const float* __restrict__ logits, int64_t ld, const float* _
     }
 }
 
+// Backward of infonce_rows_kernel + the reduce (training: loss.backward() through
+// InfoNCELossFull, feature_loss.py:268-314): for anchor row i of pair b with weight
+// w_i = row_mask_i / (K_b n_pairs) (K_b = the pair's kept rows) and upstream gradient g,
+//   dlogits[i][j] = g w_i (softmax_ij - [j == positive])  over the pair's non-ignored columns,
+// 0 on ignored columns and on every column of the other pairs (the logits span all pairs).
+// The positive, the ignore mask and the log-sum-exp are recomputed exactly as the forward.
+__global__ void __launch_bounds__(256)
+infonce_rows_bwd_kernel(const float* __restrict__ logits, int64_t ld, const float* __restrict__ axyz,
+                        const float* __restrict__ pxyz, const int64_t* __restrict__ a_off,
+                        const int64_t* __restrict__ p_off, int n_pairs, int64_t n_anchor,
+                        int64_t n_cols, float r_n, const float* __restrict__ w,
+                        const float* __restrict__ g, float* __restrict__ dl, int64_t ldd) {
+    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (i >= n_anchor) return;                            // wave-uniform
+    const int b = find_segment(a_off, n_pairs, i);
+    const int p0 = (int)p_off[b], p1 = (int)p_off[b + 1];
+    float* drow = dl + i * ldd;
+    const float wi = w[i] * g[0];
+    // columns outside the pair's block, and every column of an unkept row: 0
+    for (int64_t j = lane; j < n_cols; j += 64)
+        if (j < p0 || j >= p1 || wi == 0.f) drow[j] = 0.f;
+    if (p1 <= p0 || wi == 0.f) return;
+    const float ax = axyz[3 * i], ay = axyz[3 * i + 1], az = axyz[3 * i + 2];
+    const float a2 = (ax * ax + ay * ay) + az * az;
+    float best = INFINITY;
+    int bj = p1;
+    for (int j = p0 + lane; j < p1; j += 64) {
+        const float d = cdist_mm(ax, ay, az, a2, pxyz + 3 * (int64_t)j);
+        if (d < best) { best = d; bj = j; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const float ob = __shfl_xor(best, o, 64);
+        const int oj = __shfl_xor(bj, o, 64);
+        if (ob < best || (ob == best && oj < bj)) { best = ob; bj = oj; }
+    }
+    if (bj >= p1) bj = p0;
+    const float* lrow = logits + i * ld;
+    float m = -INFINITY, s = 0.f;
+    for (int j = p0 + lane; j < p1; j += 64) {
+        const float d = cdist_mm(ax, ay, az, a2, pxyz + 3 * (int64_t)j);
+        if (d < r_n && j != bj) continue;
+        const float l = lrow[j];
+        if (l > m) { s = s * expf(m - l) + 1.f; m = l; }
+        else s += expf(l - m);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const float om = __shfl_xor(m, o, 64), os = __shfl_xor(s, o, 64);
+        const float M = fmaxf(m, om);
+        const float a = m == -INFINITY ? 0.f : s * expf(m - M);
+        const float c = om == -INFINITY ? 0.f : os * expf(om - M);
+        s = a + c;
+        m = M;
+    }
+    const float lse = m + logf(s);
+    for (int j = p0 + lane; j < p1; j += 64) {
+        const float d = cdist_mm(ax, ay, az, a2, pxyz + 3 * (int64_t)j);
+        float v = 0.f;
+        if (!(d < r_n && j != bj)) v = wi * (expf(lrow[j] - lse) - (j == bj ? 1.f : 0.f));
+        drow[j] = v;
+    }
+}
+
 // sum(loss[mask]) / sum(mask) per pair, then the mean over pairs (feature_loss.py:295, 314).
 __global__ void __launch_bounds__(kRed)
 infonce_reduce_kernel(const float* __restrict__ row_loss, const float* __restrict__ row_mask,
@@ -447,6 +512,24 @@ extern "C" int fgr_infonce_rows(const float* logits, int64_t ld, const float* ax
                        as_stream(stream), logits, ld, axyz, pxyz, a_off, p_off, n_pairs, n_anchor,
                        r_p, r_n, row_loss, row_mask);
     FGR_CHECK_LAUNCH("infonce_rows_kernel");
+    return FGR_OK;
+}
+
+extern "C" int fgr_infonce_rows_bwd(const float* logits, int64_t ld, const float* axyz,
+                                    const float* pxyz, const int64_t* a_off, const int64_t* p_off,
+                                    int32_t n_pairs, int64_t n_anchor, int64_t n_cols, float r_n,
+                                    const float* row_weight, const float* grad, float* dlogits,
+                                    int64_t ld_d, void* stream) {
+    FGR_REQUIRE(n_pairs > 0 && n_anchor >= 0 && n_cols >= 0 && ld >= n_cols && ld_d >= n_cols,
+                "fgr_infonce_rows_bwd: bad arguments");
+    FGR_REQUIRE(n_anchor == 0 || (logits && axyz && pxyz && a_off && p_off && row_weight && grad &&
+                                  dlogits),
+                "fgr_infonce_rows_bwd: null pointer");
+    if (n_anchor == 0) return FGR_OK;
+    hipLaunchKernelGGL(infonce_rows_bwd_kernel, dim3((unsigned)ceil_div(n_anchor, 4)), dim3(256), 0,
+                       as_stream(stream), logits, ld, axyz, pxyz, a_off, p_off, n_pairs, n_anchor,
+                       n_cols, r_n, row_weight, grad, dlogits, ld_d);
+    FGR_CHECK_LAUNCH("infonce_rows_bwd_kernel");
     return FGR_OK;
 }
 

@@ -93,6 +93,8 @@ SIGNATURES = {
     'fgr_transform_points': [_vp, _i64, _vp, _i32, _vp, _i32, _vp, _vp],
     'fgr_infonce_rows': [_vp, _i64, _vp, _vp, _vp, _vp, _i32, _i64, _f32, _f32, _vp, _vp, _vp],
     'fgr_infonce_reduce': [_vp, _vp, _vp, _i32, _vp, _vp],
+    'fgr_infonce_rows_bwd': [_vp, _i64, _vp, _vp, _vp, _vp, _i32, _i64, _i64, _f32, _vp, _vp, _vp, _i64,
+                             _vp],
     'fgr_circle_loss_workspace': [_i64, _i64, _i64, ctypes.POINTER(_sz)],
     'fgr_circle_loss': [_vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _i64, _i64, _i32, _i32,
                         _i64, _f32, _f32, _vp, _sz, _vp, _vp],

@@ -220,14 +220,56 @@ def compute_metrics(pred, batch):
     return metrics
 
 
+class _InfoNCEFn(torch.autograd.Function):
+    """InfoNCELossFull over B pairs packed along rows (feature_loss.py:268-314) from the match
+    logits over ALL pairs' positive rows, differentiable in the logits: forward
+    fgr_infonce_rows + fgr_infonce_reduce (as the evaluation path), backward
+    fgr_infonce_rows_bwd (softmax minus the positive's indicator, per row weight = kept /
+    (pair's kept rows * pairs)). One launch each way for every pair of the batch."""
+
+    @staticmethod
+    def forward(ctx, logits, axyz, pxyz, a_off, p_off, pair_idx, r_p, r_n):
+        n_a, n_p = logits.shape
+        n_pairs = a_off.numel() - 1
+        row_loss = torch.empty((n_a,), dtype=torch.float32, device=logits.device)
+        row_mask = torch.empty_like(row_loss)
+        L = _lib.load()
+        _lib.check(L.fgr_infonce_rows(_ptr(logits), logits.stride(0), _ptr(axyz), _ptr(pxyz),
+                                      _ptr(a_off), _ptr(p_off), n_pairs, n_a, float(r_p), float(r_n),
+                                      _ptr(row_loss), _ptr(row_mask), _stream()), 'fgr_infonce_rows')
+        out = torch.empty((), dtype=torch.float32, device=logits.device)
+        _lib.check(L.fgr_infonce_reduce(_ptr(row_loss), _ptr(row_mask), _ptr(a_off), n_pairs,
+                                        _ptr(out), _stream()), 'fgr_infonce_reduce')
+        ctx.r_n = float(r_n)
+        ctx.save_for_backward(logits, axyz, pxyz, a_off, p_off, pair_idx, row_mask)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        logits, axyz, pxyz, a_off, p_off, pair_idx, row_mask = ctx.saved_tensors
+        n_a, n_p = logits.shape
+        n_pairs = a_off.numel() - 1
+        kept = torch.zeros((n_pairs,), dtype=torch.float32, device=logits.device)
+        kept = kept.index_add_(0, pair_idx, row_mask)[pair_idx]
+        # a pair with no kept row: the reference's empty selection passes no gradient on
+        w = torch.where(kept > 0, row_mask / (kept * n_pairs), torch.zeros_like(row_mask))
+        dl = torch.empty_like(logits)
+        _lib.check(_lib.load().fgr_infonce_rows_bwd(
+            _ptr(logits), logits.stride(0), _ptr(axyz), _ptr(pxyz), _ptr(a_off), _ptr(p_off),
+            n_pairs, n_a, n_p, ctx.r_n, _ptr(w), _ptr(g.float().contiguous()), _ptr(dl), dl.stride(0),
+            _stream()), 'fgr_infonce_rows_bwd')
+        return dl, None, None, None, None, None, None, None
+
+
 def compute_loss_train(model, pred, batch):
     """RegTR.compute_loss (finegrained_regtr.py:252-309) as a differentiable graph: the same
-    keys, weights and reductions as compute_loss above, with the match logits on the
-    differentiable f16x3 GEMMs (fgreg.autograd.linear_t: A W_sym, then against the positives)
-    and the BCE / InfoNCE masks / L1 terms as torch ops on the device, so that
-    ``losses['total'].backward()`` reaches every parameter (trainer.py:110-125). The overlap
-    pyramid is a target (no gradient): fgr_overlap_pool as in compute_loss."""
-    import math
+    keys, weights and reductions as compute_loss above, with the match logits of all pairs on
+    the differentiable f16x3 GEMMs (fgreg.autograd.linear_t: A W_sym, then against the
+    positives), InfoNCE over all pairs in one autograd Function (_InfoNCEFn: the evaluation
+    kernels forward, fgr_infonce_rows_bwd backward), the BCE / CircleLoss / L1 terms as torch
+    ops on the device, so that ``losses['total'].backward()`` reaches every parameter
+    (trainer.py:110-125). The overlap pyramid and the warped keypoint targets carry no
+    gradient (fgr_overlap_pool, fgr_transform_points as in compute_loss)."""
     import torch.nn.functional as F
     from .autograd import linear_t
     cfg = model.cfg
@@ -242,31 +284,32 @@ def compute_loss_train(model, pred, batch):
         pyr = compute_overlaps(batch)
     batch['overlap_pyr'] = pyr
     ov = pyr[f'pyr_{p}']
-    lens = [int(v) for v in meta['stack_lengths'][p].tolist()]
+    host = meta.get('_host')          # the forward's host layout: no device read-back
+    lens = list(host['lengths'][p]) if host else [int(v) for v in meta['stack_lengths'][p].tolist()]
     B = len(lens) // 2
     src_w, tgt_w = torch.split(ov[:sum(lens[:B])], lens[:B]), torch.split(ov[sum(lens[:B]):], lens[B:])
-
-    def rigid(ps, x):
-        return x @ ps[:, :3].t() + ps[:, 3]
 
     def w_sym(W):
         t = torch.triu(W)
         return t + t.t()
 
-    def infonce_pair(Ws, a, pp, a_xyz, p_xyz):
-        # feature_loss.py:283-314: the nearest positive within r_p is the target, every
-        # other positive within r_n leaves the partition sum
-        logits = linear_t(linear_t(a, Ws, cache=False), pp, cache=False)   # a W_sym p^T
-        with torch.no_grad():
-            dist = torch.cdist(a_xyz, p_xyz)
-            d1, j1 = dist.min(dim=1)
-            keep = d1 < cfg.r_p
-            excl = dist < cfg.r_n
-            excl[torch.arange(len(j1), device=excl.device), j1] = False
-        logits = logits.masked_fill(excl, -math.inf)
-        rows = torch.arange(len(j1), device=logits.device)
-        per_row = torch.logsumexp(logits, dim=1) - logits[rows, j1]
-        return per_row[keep].sum() / keep.sum()
+    # the pairs packed along rows: anchors (src keypoints warped by the ground truth) and
+    # positives (tgt keypoints), as the evaluation path packs them
+    dev = pose.device
+    a_off, p_off = ops.offsets(lens[:B], dev), ops.offsets(lens[B:], dev)
+    with torch.no_grad():
+        axyz_all = transform_points(torch.cat(list(pred['src_kp'])), a_off, pose)
+        pxyz_all = torch.cat(list(pred['tgt_kp'])).float().contiguous()
+    pair_idx = ops.to_device([b for b in range(B) for _ in range(lens[b])], torch.int64, dev)
+
+    def infonce_all(W, A, P):
+        # feature_loss.py:283-314 for every pair at once: the logits over all pairs' rows on
+        # the differentiable f16x3 GEMMs (A W_sym P^T), each row's pair block read by
+        # fgr_infonce_rows (the nearest positive within r_p is the target, every other
+        # positive within r_n leaves the partition sum)
+        logits = linear_t(linear_t(A, w_sym(W), cache=False), P, cache=False)
+        return _InfoNCEFn.apply(logits, axyz_all, pxyz_all, a_off, p_off, pair_idx, cfg.r_p,
+                                cfg.r_n)
 
     def circle_pair(a, pp, a_xyz, p_xyz):
         # CircleLossFull.get_circle_loss (feature_loss.py:191-230), Euclidean feature distances
@@ -285,37 +328,43 @@ def compute_loss_train(model, pred, batch):
         tn = torch.where(neg, 10.0 * (1.4 - fd) * wn, zero)
         row = F.softplus(torch.logsumexp(tp, 1) + torch.logsumexp(tn, 1)) / 10.0
         col = F.softplus(torch.logsumexp(tp, 0) + torch.logsumexp(tn, 0)) / 10.0
-        return (row[pos.any(1) & neg.any(1)].mean() + col[pos.any(0) & neg.any(0)].mean()) / 2
+        # masked means without boolean indexing (no host sync); row / col are finite
+        rm, cm = (pos.any(1) & neg.any(1)).float(), (pos.any(0) & neg.any(0)).float()
+        return ((row * rm).sum() / rm.sum() + (col * cm).sum() / cm.sum()) / 2
 
     losses = {}
     logits = torch.cat(list(pred['src_overlap']) + list(pred['tgt_overlap']), dim=-2)
     for i in cfg.overlap_loss_on:
         losses[f'overlap_{i}'] = F.binary_cross_entropy_with_logits(logits[i, :, 0], ov)
-    a_xyz = [rigid(pose[b], pred['src_kp'][b]) for b in range(B)]
     if ftype == 'circle':
-        feat = lambda crit, a, pp, b: circle_pair(a, pp, a_xyz[b], pred['tgt_kp'][b])
+        a_xyz = torch.split(axyz_all, lens[:B])
+        for i in cfg.feature_loss_on:
+            losses[f'feature_{i}'] = torch.stack([
+                circle_pair(pred['src_feat'][b][i], pred['tgt_feat'][b][i], a_xyz[b], pred['tgt_kp'][b])
+                for b in range(B)]).mean()
+        losses['feature_un'] = torch.stack([
+            circle_pair(pred['src_feat_un'][b], pred['tgt_feat_un'][b], a_xyz[b], pred['tgt_kp'][b])
+            for b in range(B)]).mean()
     else:
-        feat = lambda crit, a, pp, b: infonce_pair(w_sym(crit.W), a, pp, a_xyz[b],
-                                                   pred['tgt_kp'][b])
-    for i in cfg.feature_loss_on:
-        crit = getattr(model, 'feature_criterion', None)
-        losses[f'feature_{i}'] = torch.stack([
-            feat(crit, pred['src_feat'][b][i], pred['tgt_feat'][b][i], b) for b in range(B)]).mean()
-    crit = getattr(model, 'feature_criterion_un', None)
-    losses['feature_un'] = torch.stack([
-        feat(crit, pred['src_feat_un'][b], pred['tgt_feat_un'][b], b) for b in range(B)]).mean()
+        for i in cfg.feature_loss_on:
+            losses[f'feature_{i}'] = infonce_all(
+                model.feature_criterion.W, torch.cat([pred['src_feat'][b][i] for b in range(B)]),
+                torch.cat([pred['tgt_feat'][b][i] for b in range(B)]))
+        losses['feature_un'] = infonce_all(
+            model.feature_criterion_un.W, torch.cat(list(pred['src_feat_un'])),
+            torch.cat(list(pred['tgt_feat_un'])))
 
-    def corr_mae(kp, warped, poses, weights):
-        gt = torch.cat([rigid(poses[b], kp[b]) for b in range(len(kp))])
+    def corr_mae(gt, warped, weights):
         err = (torch.cat(list(warped)) - gt).abs().sum(1)
         w = torch.cat(list(weights))
         return (w * err).sum() / torch.clamp_min(w.sum(), 1e-6)
 
-    inv = torch.stack([torch.cat([pose[b, :, :3].t(), -(pose[b, :, :3].t() @ pose[b, :, 3:4])], 1)
-                       for b in range(B)])
+    with torch.no_grad():                 # the targets: keypoints under the ground-truth pose
+        gt_src = axyz_all
+        gt_tgt = transform_points(pxyz_all, p_off, pose, inverse=True)
     for i in cfg.corr_loss_on:
-        losses[f'corr_{i}'] = (corr_mae(pred['src_kp'], [w[i] for w in pred['src_kp_warped']], pose, src_w)
-                               + corr_mae(pred['tgt_kp'], [w[i] for w in pred['tgt_kp_warped']], inv, tgt_w))
+        losses[f'corr_{i}'] = (corr_mae(gt_src, [w[i] for w in pred['src_kp_warped']], src_w)
+                               + corr_mae(gt_tgt, [w[i] for w in pred['tgt_kp_warped']], tgt_w))
     wd = weight_dict(cfg)
     losses['total'] = torch.sum(torch.stack([losses[k] * wd[k] for k in losses]))
     return losses

@@ -415,6 +415,16 @@ int fgr_transform_points(const float* xyz, int64_t n, const int64_t* seg_off, in
 int fgr_infonce_rows(const float* logits, int64_t ld, const float* axyz, const float* pxyz,
                      const int64_t* a_off, const int64_t* p_off, int32_t n_pairs, int64_t n_anchor,
                      float r_p, float r_n, float* row_loss, float* row_mask, void* stream);
+/* Training (loss.backward() through the InfoNCE above): dlogits (n_anchor, n_cols over all
+ * pairs' positive rows) = grad[0] * row_weight[i] * (softmax_ij - [j == positive]) over the
+ * row's pair block, ignored columns and other pairs' columns 0; row_weight[i] =
+ * row_mask[i] / (kept rows of the pair * n_pairs) makes it the gradient of
+ * fgr_infonce_reduce's output. The positive / ignore mask / log-sum-exp are recomputed as
+ * fgr_infonce_rows does. */
+int fgr_infonce_rows_bwd(const float* logits, int64_t ld, const float* axyz, const float* pxyz,
+                         const int64_t* a_off, const int64_t* p_off, int32_t n_pairs,
+                         int64_t n_anchor, int64_t n_cols, float r_n, const float* row_weight,
+                         const float* grad, float* dlogits, int64_t ld_d, void* stream);
 int fgr_infonce_reduce(const float* row_loss, const float* row_mask, const int64_t* a_off,
                        int32_t n_pairs, float* out, void* stream);
 int fgr_circle_loss_workspace(int64_t fd_elems, int64_t n_anchor, int64_t n_pos, size_t* bytes);
