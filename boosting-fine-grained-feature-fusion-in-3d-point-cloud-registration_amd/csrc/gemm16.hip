@@ -1070,19 +1070,37 @@ split_weights_h3_fused_kernel(const float* __restrict__ w, int n, int k, int64_t
         wsc[r0 + tid] = ok ? __builtin_ldexpf(1.f, -e) : 0.f;
     }
     __syncthreads();
-    // phase 2: the panel's units [kstep][term][g][i], as split_weights_h3_kernel
+    // phase 2: the panel's units [kstep][term][g][i], as split_weights_h3_kernel; rows of
+    // a row-major W with k % 8 == 0 read as two 16-B loads per unit
     const int units = ksteps * 128;
+    const bool vec = sk == 1 && k % 8 == 0 && sn % 4 == 0 && (reinterpret_cast<uintptr_t>(w) & 15) == 0;
     for (int u = tid; u < units; u += 256) {
         const int i = u & 15, g = (u >> 4) & 3, t = (u >> 6) & 1, s = u >> 7;
         const int rr = r0 + i;
         const float sc = scale_inv[i];
+        const int c0 = s * 32 + 8 * g;
+        float xv[8];
+        if (vec) {
+            const bool ok = rr < n && c0 < k;
+            const float* src = w + (int64_t)min(rr, n - 1) * sn + min(c0, k - 8);
+            const float4 a = *reinterpret_cast<const float4*>(src);
+            const float4 b = *reinterpret_cast<const float4*>(src + 4);
+            xv[0] = a.x; xv[1] = a.y; xv[2] = a.z; xv[3] = a.w;
+            xv[4] = b.x; xv[5] = b.y; xv[6] = b.z; xv[7] = b.w;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) xv[e] = ok ? xv[e] * sc : 0.f;
+        } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int col = c0 + e;
+                xv[e] = (rr < n && col < k) ? w[(int64_t)rr * sn + (int64_t)col * sk] * sc : 0.f;
+            }
+        }
         f16x8 out;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-            const int col = s * 32 + 8 * g + e;
-            const float x = (rr < n && col < k) ? w[(int64_t)rr * sn + (int64_t)col * sk] * sc : 0.f;
-            const _Float16 h = (_Float16)x;
-            out[e] = t == 0 ? h : (_Float16)(x - (float)h);
+            const _Float16 h = (_Float16)xv[e];
+            out[e] = t == 0 ? h : (_Float16)(xv[e] - (float)h);
         }
         img[(int64_t)panel * units + u] = __builtin_bit_cast(u32x4, out);
     }

@@ -306,7 +306,8 @@ segnorm_merge_kernel(SegArgs a, const double* __restrict__ part, float eps, floa
         return;
     }
     double s1 = 0.0, s2 = 0.0, n = 0.0;
-    for (int k = 0; k < a.n_chunks; ++k) {
+#pragma unroll 8
+    for (int k = 0; k < a.n_chunks; ++k) {                     // 8 chunk loads in flight
         const double* p = part + (((int64_t)seg * a.n_chunks + k) * a.c + ch) * 3;
         s1 += p[0];
         s2 += p[1];
@@ -396,6 +397,7 @@ segnorm_bwd_merge_kernel(SegArgs a, const double* __restrict__ part, float* __re
     if (t >= (int64_t)a.n_seg * a.c) return;
     const int seg = (int)(t / a.c), ch = (int)(t % a.c);
     double s1 = 0.0, s2 = 0.0;
+#pragma unroll 8
     for (int k = 0; k < a.n_chunks; ++k) {
         const double* p = part + (((int64_t)seg * a.n_chunks + k) * a.c + ch) * 2;
         s1 += p[0];
@@ -406,6 +408,7 @@ segnorm_bwd_merge_kernel(SegArgs a, const double* __restrict__ part, float* __re
     if (dgamma && seg == 0) {
         double g1 = 0.0, g2 = 0.0;
         for (int sg = 0; sg < a.n_seg; ++sg)
+#pragma unroll 8
             for (int k = 0; k < a.n_chunks; ++k) {
                 const double* p = part + (((int64_t)sg * a.n_chunks + k) * a.c + ch) * 2;
                 g1 += p[0];
@@ -684,7 +687,8 @@ segnorm_bwd_apply4_kernel(SegApply p, const float* __restrict__ dy, const float*
 // One wave per row (PER = d / 64 columns per lane), rows r = block * 64 + wave + 4 i; the
 // wave's lanes keep the column partials of dy * xhat and dy over its rows, merged per block
 // in LDS and written as the block's partial row (2 d floats) for fgr_colsum.
-constexpr int kLnRows = 64;
+constexpr int kLnRowsWave = 4;                 // rows per wave, loaded together
+constexpr int kLnRows = 4 * kLnRowsWave;       // rows per block (16: ~600 blocks at 9.5k rows)
 
 template <int PER>
 __global__ void __launch_bounds__(256)
@@ -692,26 +696,38 @@ layernorm_bwd_kernel(const float* __restrict__ x, int64_t n, int d, const float*
                      float eps, const float* __restrict__ dy, float* __restrict__ dx,
                      float* __restrict__ part) {
     const int wv = threadIdx.x / 64, lane = threadIdx.x % 64;
-    float pg[PER], pb[PER];
+    float pg[PER], pb[PER], gm[PER];
 #pragma unroll
-    for (int j = 0; j < PER; ++j) pg[j] = pb[j] = 0.f;
-    for (int i = 0; i < kLnRows / 4; ++i) {
-        const int64_t r = (int64_t)blockIdx.x * kLnRows + wv + 4 * i;
-        if (r >= n) break;
-        float v[PER], gy[PER];
-        float s = 0.f;
+    for (int j = 0; j < PER; ++j) {
+        pg[j] = pb[j] = 0.f;
+        const int col = lane + 64 * j;
+        gm[j] = col < d ? g[col] : 0.f;
+    }
+    // every load of the wave's rows first (one memory round trip), then the rows in turn
+    float v[kLnRowsWave][PER], gy[kLnRowsWave][PER];
+    const int64_t rb = (int64_t)blockIdx.x * kLnRows + wv * kLnRowsWave;
+#pragma unroll
+    for (int i = 0; i < kLnRowsWave; ++i) {
+        const int64_t r = min(rb + i, n - 1);
 #pragma unroll
         for (int j = 0; j < PER; ++j) {
-            const int col = lane + 64 * j;
-            v[j] = col < d ? x[r * d + col] : 0.f;
-            gy[j] = col < d ? dy[r * d + col] : 0.f;
-            s += v[j];
+            const int col = min(lane + 64 * j, d - 1);
+            v[i][j] = x[r * d + col];
+            gy[i][j] = dy[r * d + col];
         }
+    }
+#pragma unroll
+    for (int i = 0; i < kLnRowsWave; ++i) {
+        const int64_t r = rb + i;
+        if (r >= n) break;                         // wave-uniform
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < PER; ++j) s += (lane + 64 * j) < d ? v[i][j] : 0.f;
         const float mean = wave_sum(s) / (float)d;
         float sq = 0.f;
 #pragma unroll
         for (int j = 0; j < PER; ++j) {
-            const float a = (lane + 64 * j) < d ? v[j] - mean : 0.f;
+            const float a = (lane + 64 * j) < d ? v[i][j] - mean : 0.f;
             sq += a * a;
         }
         const float rstd = 1.0f / sqrtf(wave_sum(sq) / (float)d + eps);
@@ -720,21 +736,21 @@ layernorm_bwd_kernel(const float* __restrict__ x, int64_t n, int d, const float*
         for (int j = 0; j < PER; ++j) {
             const int col = lane + 64 * j;
             if (col < d) {
-                const float xh = (v[j] - mean) * rstd;
-                const float dxh = gy[j] * g[col];
+                const float xh = (v[i][j] - mean) * rstd;
+                const float dxh = gy[i][j] * gm[j];
                 s1 += dxh;
                 s2 += dxh * xh;
-                pg[j] += gy[j] * xh;
-                pb[j] += gy[j];
-                v[j] = xh;
-                gy[j] = dxh;
+                pg[j] += gy[i][j] * xh;
+                pb[j] += gy[i][j];
+                v[i][j] = xh;
+                gy[i][j] = dxh;
             }
         }
         const float m1 = wave_sum(s1) / (float)d, m2 = wave_sum(s2) / (float)d;
 #pragma unroll
         for (int j = 0; j < PER; ++j) {
             const int col = lane + 64 * j;
-            if (col < d) dx[r * d + col] = rstd * (gy[j] - m1 - v[j] * m2);
+            if (col < d) dx[r * d + col] = rstd * (gy[i][j] - m1 - v[i][j] * m2);
         }
     }
     __shared__ float lg[4][64 * PER], lb[4][64 * PER];

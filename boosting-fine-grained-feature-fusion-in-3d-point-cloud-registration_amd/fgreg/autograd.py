@@ -317,11 +317,19 @@ def segnorm_t(x, off, lengths, row_div=None, act=ACT_NONE, residual=None, post_a
                             eps, stats)
 
 
+_BN_OFF = {}
+
+
 def batchnorm_t(bn, x, act=ACT_NONE, residual=None, post_act=ACT_NONE):
     """nn.BatchNorm1d ``bn`` in training mode on (N, C) rows (batch statistics over all rows,
     running statistics updated in place as torch does: momentum, unbiased variance)."""
     n = x.shape[0]
-    off = ops.offsets([n], x.device)
+    key = (n, x.device)
+    off = _BN_OFF.get(key)
+    if off is None:                       # [0, n] on the device, made once per row count
+        if len(_BN_OFF) > 256:
+            _BN_OFF.clear()
+        off = _BN_OFF[key] = ops.offsets([n], x.device)
     stats = [] if bn.track_running_stats else None
     y = segnorm_t(x, off, [n], act=act, residual=residual, post_act=post_act, gamma=bn.weight,
                   beta=bn.bias, eps=bn.eps, stats=stats)
