@@ -1035,10 +1035,12 @@ __global__ void split_weights_h3_kernel(const float* __restrict__ w, int n, int 
 // images), so this halves those launches.
 constexpr int kSplitFusedK = 1024;
 
-__global__ void __launch_bounds__(256)
-split_weights_h3_fused_kernel(const float* __restrict__ w, int n, int k, int64_t sn, int64_t sk,
-                              int ksteps, float* __restrict__ wsc, u32x4* __restrict__ img) {
-    const int panel = blockIdx.x, tid = threadIdx.x;
+// one 16-row panel of fgr_split_weights_h3's image (the block's whole work in the fused and
+// the batched kernels)
+__device__ __forceinline__ void split_panel_h3(const float* __restrict__ w, int n, int k, int64_t sn,
+                                               int64_t sk, int ksteps, float* __restrict__ wsc,
+                                               u32x4* __restrict__ img, int panel) {
+    const int tid = threadIdx.x;
     const int r0 = panel * 16;
     // phase 1: row maxima; (row, k-lane) = (tid % 16, tid / 16) when rows are contiguous in
     // memory (sn == 1), else (tid / 16, tid % 16)
@@ -1106,6 +1108,31 @@ split_weights_h3_fused_kernel(const float* __restrict__ w, int n, int k, int64_t
     }
 }
 
+__global__ void __launch_bounds__(256)
+split_weights_h3_fused_kernel(const float* __restrict__ w, int n, int k, int64_t sn, int64_t sk,
+                              int ksteps, float* __restrict__ wsc, u32x4* __restrict__ img) {
+    split_panel_h3(w, n, k, sn, sk, ksteps, wsc, img, blockIdx.x);
+}
+
+// Many images in one launch (training re-splits every weight after each optimizer step):
+// block b takes panel b of the concatenated panel list, its image found by binary search
+// over the descriptors' first panels.
+__global__ void __launch_bounds__(256)
+split_weights_h3_batch_kernel(const fgr_split_desc* __restrict__ d, int count) {
+    const int64_t b = blockIdx.x;
+    int lo = 0, hi = count - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (d[mid].panel0 <= b) lo = mid; else hi = mid - 1;
+    }
+    const fgr_split_desc e = d[lo];
+    const int ksteps = (e.k + 63) / 64 * 2;
+    u32x4* img = static_cast<u32x4*>(e.img);
+    float* wsc = reinterpret_cast<float*>(static_cast<char*>(e.img) +
+                                          (size_t)((e.n + 15) / 16) * ksteps * 128 * 16);
+    split_panel_h3(e.w, e.n, e.k, e.stride_n, e.stride_k, ksteps, wsc, img, (int)(b - e.panel0));
+}
+
 template <int BM, int BN, bool EPI = false>
 void launch_h3(const GemmH3Args& a, hipStream_t st) {
     const int nbm = (a.M + BM - 1) / BM, nbn = (a.N + BN - 1) / BN;
@@ -1161,6 +1188,17 @@ void launch_h3v2(const GemmH3Args& a, hipStream_t st) {
 }  // namespace fgr
 
 using namespace fgr;
+
+extern "C" int fgr_split_weights_h3_batch(const void* descs, int32_t count, int64_t total_panels,
+                                          void* stream) {
+    FGR_REQUIRE(count >= 0 && total_panels >= 0 && (count == 0 || descs),
+                "fgr_split_weights_h3_batch: bad arguments");
+    if (count == 0 || total_panels == 0) return FGR_OK;
+    hipLaunchKernelGGL(split_weights_h3_batch_kernel, dim3((unsigned)total_panels), dim3(256), 0,
+                       as_stream(stream), static_cast<const fgr_split_desc*>(descs), count);
+    FGR_CHECK_LAUNCH("split_weights_h3_batch_kernel");
+    return FGR_OK;
+}
 
 extern "C" int fgr_split_weights_h3_bytes(int32_t n, int32_t k, size_t* bytes) {
     FGR_REQUIRE(bytes && n > 0 && k > 0, "fgr_split_weights_h3_bytes: bad arguments");

@@ -56,6 +56,7 @@ SIGNATURES = {
     'fgr_res2net_chain6': [_vp, _i64, _i32, _i32, _vp, _vp, _vp, _i32, _vp, _i64, _vp],
     'fgr_res2net_chain_h3': [_vp, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _i32, _vp, _i64, _vp],
     'fgr_split_weights_h3_bytes': [_i32, _i32, ctypes.POINTER(_sz)],
+    'fgr_split_weights_h3_batch': [_vp, _i32, _i64, _vp],
     'fgr_split_weights_h3': [_vp, _i32, _i32, _i64, _i64, _vp, _vp],
     'fgr_gemm_f16x3': [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _vp],
     'fgr_gemm_f16x3_ln_supported': [_i32, _i32, _i32],

@@ -14,6 +14,7 @@ library / PyTorch GEMM fallback: a shape the kernels reject raises.
 """
 import os
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -51,19 +52,22 @@ class mode_scope:  # noqa: N801 -- used as a context manager
 
 class _Image:
     """Split image of W (n, k), element (i, j) at w2[i * sn + j * sk]: fgr_split_weights_h3
-    (f16x3: two fp16 terms, per-row power-of-two scales) or fgr_split_weights_bf16."""
-    __slots__ = ('img', 'n', 'k', 'src', 'version', 'ptr')
+    (f16x3: two fp16 terms, per-row power-of-two scales) or fgr_split_weights_bf16. ``view``
+    keeps w2 when it is a view of the source's storage (so a stale f16x3 image can be
+    re-split in place by the batched refresh)."""
+    __slots__ = ('img', 'n', 'k', 'sn', 'sk', 'src', 'version', 'ptr', 'mode', 'view')
     FN = {'f16x3': 'fgr_split_weights_h3', 'bf16': 'fgr_split_weights_bf16'}
 
     def __init__(self, mode, w2: torch.Tensor, n, k, sn, sk, src: torch.Tensor):
         L = _lib.load()
         fn = self.FN[mode]
-        nb = _lib._sz(0)
-        _lib.check(getattr(L, fn + '_bytes')(n, k, nb), fn + '_bytes')
-        self.img = torch.empty(nb.value, dtype=torch.uint8, device=w2.device)
+        nb = _lib.ws_size(fn + '_bytes', n, k)
+        self.img = torch.empty(nb, dtype=torch.uint8, device=w2.device)
         _lib.check(getattr(L, fn)(_ptr(w2), n, k, sn, sk, _ptr(self.img), _stream()), fn)
-        self.n, self.k = n, k
+        self.n, self.k, self.sn, self.sk, self.mode = n, k, sn, sk, mode
         self.src, self.version, self.ptr = src, src._version, src.data_ptr()
+        shares = w2.untyped_storage().data_ptr() == src.untyped_storage().data_ptr()
+        self.view = w2 if shares else None
 
 
 _CACHE = {}
@@ -74,6 +78,36 @@ def _valid(ent, w):
             and ent.ptr == w.data_ptr())            # .to() / load_state_dict swap .data
 
 
+# fgr_split_desc (include/fgreg.h): w, img, stride_n, stride_k, panel0, n, k
+_DESC = np.dtype([('w', '<u8'), ('img', '<u8'), ('sn', '<i8'), ('sk', '<i8'), ('panel0', '<i8'),
+                  ('n', '<i4'), ('k', '<i4')])
+BATCH_REFRESH = os.environ.get('FGREG_SPLIT_BATCH', '1') != '0'
+
+
+def _refresh_stale(device):
+    """Re-split, in one launch (fgr_split_weights_h3_batch), every cached f16x3 image on
+    ``device`` whose weight was updated in place (same storage, new version) -- after an
+    optimizer step that is every weight the training step is about to use, so the step pays
+    one launch instead of one per image. Returns the number refreshed."""
+    stale = [e for e in _CACHE.values()
+             if e.mode == 'f16x3' and e.view is not None and e.src.device == device
+             and e.src._version != e.version and e.src.data_ptr() == e.ptr]
+    if len(stale) < 2:
+        return 0
+    d = np.zeros(len(stale), dtype=_DESC)
+    p0 = 0
+    for i, e in enumerate(stale):
+        d[i] = (e.view.data_ptr(), e.img.data_ptr(), e.sn, e.sk, p0, e.n, e.k)
+        p0 += (e.n + 15) // 16
+    dd = torch.frombuffer(bytearray(d.tobytes()), dtype=torch.uint8)
+    dd = dd.pin_memory().to(device, non_blocking=True)
+    _lib.check(_lib.load().fgr_split_weights_h3_batch(_ptr(dd), len(stale), p0, _stream()),
+               'fgr_split_weights_h3_batch')
+    for e in stale:
+        e.version = e.src._version
+    return len(stale)
+
+
 def weight_image(w: torch.Tensor, transpose=False, tag=None, mode=None, cache=True, rows=None):
     """Split image of w in ``mode`` (default: the current MODE), cached unless ``cache`` is
     False (operands that change every call, e.g. the backward's activations). ``rows`` =
@@ -82,6 +116,9 @@ def weight_image(w: torch.Tensor, transpose=False, tag=None, mode=None, cache=Tr
     mode = mode or MODE
     ck = (id(w), transpose, tag, mode, rows)
     ent = _CACHE.get(ck) if cache else None
+    if (BATCH_REFRESH and ent is not None and mode == 'f16x3' and ent.src is w
+            and ent.ptr == w.data_ptr() and ent.version != w._version and ent.view is not None):
+        _refresh_stale(w.device)          # this image and every other stale one, one launch
     if not _valid(ent, w):
         src = w
         if rows is not None:

@@ -214,6 +214,21 @@ int fgr_res2net_chain_h3(const float* h, int64_t n, int32_t w, int32_t scale, co
 int fgr_split_weights_h3_bytes(int32_t n, int32_t k, size_t* bytes);
 int fgr_split_weights_h3(const float* w, int32_t n, int32_t k, int64_t stride_n,
                          int64_t stride_k, void* img, void* stream);
+/* Many fgr_split_weights_h3 images in one launch (training re-splits every weight after each
+ * optimizer step): descs = a DEVICE array of count descriptors, panel0 = the running sum of
+ * the earlier descriptors' (n + 15) / 16, total_panels = the sum over all; every image
+ * bit-equal to fgr_split_weights_h3's. */
+typedef struct {
+    const float* w;       /* element (i, j) at w[i * stride_n + j * stride_k] */
+    void* img;            /* fgr_split_weights_h3_bytes(n, k) bytes, 16-B aligned */
+    int64_t stride_n;
+    int64_t stride_k;
+    int64_t panel0;
+    int32_t n;
+    int32_t k;
+} fgr_split_desc;
+int fgr_split_weights_h3_batch(const void* descs, int32_t count, int64_t total_panels,
+                               void* stream);
 int fgr_gemm_f16x3(const float* a, int64_t lda, const void* w_img, float* c, int64_t ldc,
                    const float* bias, const float* r, int64_t ldr, int32_t m, int32_t n,
                    int32_t k, int32_t act, void* stream);

@@ -686,3 +686,29 @@ def test_weight_image_bits(gpu, shape, transpose):
         ref = _h3_image_ref(w.numpy())
     got = ent.img.cpu().numpy().tobytes()
     assert len(got) == len(ref) and got == ref
+
+
+def test_weight_image_batch_refresh(gpu):
+    """After in-place updates (an optimizer step), the first weight_image call re-splits every
+    stale cached image in one batched launch (fgr_split_weights_h3_batch): each image then
+    equals its numpy restatement of the UPDATED weight, bit for bit, row-major, transposed and
+    row-slice images alike."""
+    from fgreg import linear as lin
+    g = torch.Generator().manual_seed(5)
+    ws = [torch.randn(s, generator=g).to(gpu) for s in [(256, 256), (1024, 96), (37, 100), (15, 16, 24)]]
+    imgs = [lin.weight_image(ws[0], mode='f16x3'), lin.weight_image(ws[1], transpose=True, mode='f16x3'),
+            lin.weight_image(ws[2], mode='f16x3'), lin.weight_image(ws[3], transpose=True, mode='f16x3'),
+            lin.weight_image(ws[0], mode='f16x3', rows=(64, 192))]
+    with torch.no_grad():
+        for w in ws:
+            w.mul_(-3.0).add_(0.25)
+    got = [lin.weight_image(ws[0], mode='f16x3'), lin.weight_image(ws[1], transpose=True, mode='f16x3'),
+           lin.weight_image(ws[2], mode='f16x3'), lin.weight_image(ws[3], transpose=True, mode='f16x3'),
+           lin.weight_image(ws[0], mode='f16x3', rows=(64, 192))]
+    assert all(a is b for a, b in zip(imgs, got))          # refreshed in place, not rebuilt
+    w0, w1, w2, w3 = (w.cpu() for w in ws)
+    refs = [_h3_image_ref(w0.numpy()), _h3_image_ref(w1.t().contiguous().numpy()),
+            _h3_image_ref(w2.numpy()), _h3_image_ref(w3.reshape(-1, 24).t().contiguous().numpy()),
+            _h3_image_ref(w0[64:192].contiguous().numpy())]
+    for e, ref in zip(got, refs):
+        assert e.img.cpu().numpy().tobytes() == ref
