@@ -5,18 +5,23 @@
 // operand image of X (the generic GEMM path needs both: three extra launches and two extra
 // passes over the activations per Linear).
 //
-// One 256-thread workgroup per (128 x 128 output tile, chunk of rows). Per chunk, the column
-// maxima of both operand tiles give power-of-two scales (max |s x| in [2^14, 2^15)); each
-// 32-row k-step is split into two fp16 terms (h = f16(s x), m = f16(s x - h)) straight into
-// LDS in MFMA fragment order (per column, 32 k contiguous, 80-B pitch: conflict-free
-// ds_read_b128), and the three products mh + hm + hh accumulate in fp32 on
-// mfma_f32_16x16x32_f16 -- the f16x3 scheme of gemm16.hip with the scales taken per chunk
-// column instead of per operand row. The four waves each own a 64 x 64 quarter (4 x 4
-// fragments). One set of LDS images (40 KB: three workgroups per CU hide each other's
-// barriers), the next k-step's global loads in flight during the matrix-core work. With more than one chunk the tiles are fp32
-// partials that wgrad_reduce_kernel sums in chunk order: deterministic, no atomics. With a
-// bias gradient the tile column j0 = 0 also sums its dy columns in fp64 (db = sum_r dy[r][i]),
-// partials per chunk summed in the same reduce launch: the separate column-sum pass goes away.
+// One 256-thread workgroup per (128 x 128 output tile, chunk of rows), one pass over the
+// chunk: every 32-row k-step is scaled per column by a running power of two (the largest
+// |value| seen so far in [2^14, 2^15); when a k-step raises a column's maximum the exponent
+// drops and the accumulated products are rescaled by the exact power of two -- the dynamic
+// row scaling of the g5 GEMM, here on the contraction's columns), split into two fp16 terms
+// (h = f16(s x), m = f16(s x - h)) straight into LDS in MFMA fragment order (per column, 32 k
+// contiguous, 80-B pitch: conflict-free ds_read_b128), and the three products mh + hm + hh
+// accumulate in fp32 on mfma_f32_16x16x32_f16. The four row groups of a column quad sit in one
+// wave, so a k-step's column maxima are two lane shuffles. The four waves each own a 64 x 64
+// quarter (4 x 4 fragments); one set of LDS images (40 KB: three workgroups per CU hide each
+// other's barriers), the next k-step's global loads in flight during the matrix-core work.
+// With more than one chunk the tiles are fp32 partials that wgrad_reduce_kernel sums in
+// chunk order: deterministic, no atomics. With a bias gradient the tile column j0 = 0 also
+// sums its dy columns in fp64 (db = sum_r dy[r][i]), partials per chunk summed in the same
+// reduce launch: the separate column-sum pass goes away. (Round 5: a pre-pass of per-chunk
+// column maxima read every chunk twice: 1141 -> 938 us over the 13 training shapes,
+// profiles/r05_wgrad_shapes.txt.)
 #include <algorithm>
 #include <cstdlib>
 
@@ -54,96 +59,41 @@ __device__ __forceinline__ int wg_scale_exp(float mx) {
     return mx > 0.f ? min(15 - __builtin_amdgcn_frexp_expf(mx), 127) : 0;
 }
 
-__global__ void __launch_bounds__(256, 3) wgrad_f16x3_kernel(WgradArgs p) {   // 3 waves / SIMD
+// one register set of k-step rows (the next k-step's loads in flight during the matrix-core
+// work; 166 VGPRs = 3 workgroups per CU -- a second set spilled or cost the occupancy)
+__global__ void __launch_bounds__(256, 3) wgrad_f16x3_kernel(WgradArgs p) {
     __shared__ _Float16 img[2][2][kWgImg];         // [operand][term]: 40 KB (3 workgroups / CU)
-    __shared__ float4 cmx[256];                    // pre-pass maxima per thread
-    __shared__ float inv_s[2][kWgT];               // per operand column: 1 / scale
-    __shared__ float scl[2][kWgT];                 // per operand column: scale
+    __shared__ int edel[2][kWgT];                  // per operand column: this k-step's exponent change
+    __shared__ int eend[2][kWgT];                  // per operand column: the final exponent
+    __shared__ int chg[2];                         // any exponent change at k-step parity
+    __shared__ double bred[4][kWgT];               // bias partial sums per row group
     const int tid = threadIdx.x;
     const int lane = tid & 63, wv = tid >> 6, g = lane >> 4, c = lane & 15;
     const int ti = blockIdx.x / p.tiles_n, tj = blockIdx.x % p.tiles_n;
     const int i0 = ti * kWgT, j0 = tj * kWgT;
     const int64_t rb = (int64_t)blockIdx.y * p.kc;
     const int64_t re = min(p.rows, rb + p.kc);
-    // thread -> (operand, column quad, row group of 8): threads 0..127 read dy, 128..255 x
-    const int op = tid >> 7, c4 = tid & 31, kg = (tid >> 5) & 3;
+    // thread -> (operand, column quad, row group of 8): waves 0-1 read dy, 2-3 x; in a wave
+    // lanes 16 kg + c4l, so the 4 row groups of a column quad sit in one wave (the column
+    // maxima of a k-step are two lane shuffles, no LDS round)
+    const int op = tid >> 7, kg = lane >> 4, c4 = ((tid >> 6) & 1) * 16 + (lane & 15);
     const int64_t ld = op ? p.ldx : p.ldy;
     const int lim = op ? p.n : p.m;
     const int col0 = (op ? j0 : i0) + 4 * c4;      // first of this thread's 4 columns
     const bool cok = col0 < lim;                   // lim % 4 == 0: all four or none
     const float* base = (op ? p.x : p.dy) + (cok ? col0 : 0);
-
-    // pre-pass: column maxima of the chunk (rows kg, kg + 4, ...; 8 loads in flight per
-    // thread, every load unconditional at a clamped row); the bias gradient rides on the dy
-    // reads of the first tile column (fp64 column sums of the chunk)
     const bool bias_sums = p.db && op == 0 && tj == 0;
-    double bs[4] = {0.0, 0.0, 0.0, 0.0};
-    float m0 = 0.f, m1 = 0.f, m2 = 0.f, m3 = 0.f;
-    for (int64_t r = rb + kg; r < re; r += 32) {
-        float4 v[8];
+    if (bias_sums) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
-            v[u] = *reinterpret_cast<const float4*>(base + min(r + 4 * u, re - 1) * ld);
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            m0 = fmaxf(m0, fabsf(v[u].x));
-            m1 = fmaxf(m1, fabsf(v[u].y));
-            m2 = fmaxf(m2, fabsf(v[u].z));
-            m3 = fmaxf(m3, fabsf(v[u].w));
-        }
-        if (bias_sums) {
-#pragma unroll
-            for (int u = 0; u < 8; ++u)
-                if (r + 4 * u < re) {
-                    bs[0] += (double)v[u].x;
-                    bs[1] += (double)v[u].y;
-                    bs[2] += (double)v[u].z;
-                    bs[3] += (double)v[u].w;
-                }
-        }
+        for (int q = 0; q < 4; ++q) bred[kg][4 * c4 + q] = 0.0;
     }
-    if (p.db && tj == 0) {                         // (block-uniform) fold the 4 row groups
-        __shared__ double bred[4][kWgT];
-        if (op == 0) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) bred[kg][4 * c4 + q] = cok ? bs[q] : 0.0;
-        }
-        __syncthreads();
-        if (tid < kWgT && i0 + tid < p.m) {
-            const double t = ((bred[0][tid] + bred[1][tid]) + bred[2][tid]) + bred[3][tid];
-            if (p.part_db)
-                p.part_db[(int64_t)blockIdx.y * p.m + i0 + tid] = t;
-            else
-                p.db[i0 + tid] = (float)t;
-        }
-    }
-    cmx[tid] = make_float4(m0, m1, m2, m3);
-    __syncthreads();
-    if (kg == 0) {
-        float4 a = cmx[tid];
-#pragma unroll
-        for (int q = 1; q < 4; ++q) {
-            const float4 b = cmx[tid + 32 * q];
-            a.x = fmaxf(a.x, b.x); a.y = fmaxf(a.y, b.y);
-            a.z = fmaxf(a.z, b.z); a.w = fmaxf(a.w, b.w);
-        }
-        const float am[4] = {a.x, a.y, a.z, a.w};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int e = wg_scale_exp(am[q]);
-            scl[op][4 * c4 + q] = __builtin_ldexpf(1.f, e);
-            inv_s[op][4 * c4 + q] = __builtin_ldexpf(1.f, -e);
-        }
-    }
-    __syncthreads();
-    float s[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) s[q] = scl[op][4 * c4 + q];
+    // running column exponents: the scale 2^e keeps the largest |value| seen so far in
+    // [2^14, 2^15); when a k-step raises a column's maximum the exponent drops and the
+    // accumulated products are rescaled by the (exact) power of two -- one pass over the data
+    int ecur[4] = {127, 127, 127, 127};
+    if (tid < 2) chg[tid] = 0;
 
     const int nk = (int)((re - rb + kWgK - 1) / kWgK);
-    // this thread's 8 rows x 4 columns of a k-step (the next k-step's loads are issued before
-    // the matrix-core work on the current one; a second register set measured slower: 282
-    // VGPRs, one workgroup per CU instead of three)
     float va[8][4];
     auto load = [&](float (&v)[8][4], int ks) {
         const int64_t r0 = rb + (int64_t)ks * kWgK + 8 * kg;
@@ -158,13 +108,24 @@ __global__ void __launch_bounds__(256, 3) wgrad_f16x3_kernel(WgradArgs p) {   //
             v[e][3] = ok ? t.w : 0.f;
         }
     };
-    auto store = [&](const float (&v)[8][4]) {
+    // exponents of this k-step, then the split images (and the bias sums)
+    auto store = [&](const float (&v)[8][4], int par) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
+            float m = 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf(v[e][q]));
+            m = fmaxf(m, __shfl_xor(m, 16, 64));
+            m = fmaxf(m, __shfl_xor(m, 32, 64));
+            const int en = m > 0.f ? min(ecur[q], wg_scale_exp(m)) : ecur[q];
+            if (kg == 0) edel[op][4 * c4 + q] = en - ecur[q];
+            if (en != ecur[q]) chg[par] = 1;
+            ecur[q] = en;
+            const float sc = __builtin_ldexpf(1.f, en);
             f16x8 th, tm;
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
-                const float xs = v[e][q] * s[q];
+                const float xs = v[e][q] * sc;
                 const _Float16 hh = (_Float16)xs;
                 th[e] = hh;
                 tm[e] = (_Float16)(xs - (float)hh);
@@ -172,6 +133,15 @@ __global__ void __launch_bounds__(256, 3) wgrad_f16x3_kernel(WgradArgs p) {   //
             const int o = (4 * c4 + q) * kWgPitch + 8 * kg;
             *reinterpret_cast<u32x4*>(&img[op][0][o]) = __builtin_bit_cast(u32x4, th);
             *reinterpret_cast<u32x4*>(&img[op][1][o]) = __builtin_bit_cast(u32x4, tm);
+        }
+        if (bias_sums) {                           // fp64 running sums in this thread's LDS slots
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                float t = 0.f;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) t += v[e][q];
+                bred[kg][4 * c4 + q] += (double)t;
+            }
         }
     };
 
@@ -181,7 +151,20 @@ __global__ void __launch_bounds__(256, 3) wgrad_f16x3_kernel(WgradArgs p) {   //
     for (int fi = 0; fi < 4; ++fi)
 #pragma unroll
         for (int fj = 0; fj < 4; ++fj) acc[fi][fj] = f32x4{0.f, 0.f, 0.f, 0.f};
-    auto mfma_step = [&]() {
+    auto mfma_step = [&](int par) {
+        if (chg[par]) {                            // block-uniform: rescale to the new exponents
+            float fb[4];
+#pragma unroll
+            for (int fj = 0; fj < 4; ++fj) fb[fj] = __builtin_ldexpf(1.f, edel[1][64 * wj + 16 * fj + c]);
+#pragma unroll
+            for (int fi = 0; fi < 4; ++fi)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float fa = __builtin_ldexpf(1.f, edel[0][64 * wi + 16 * fi + 4 * g + r]);
+#pragma unroll
+                    for (int fj = 0; fj < 4; ++fj) acc[fi][fj][r] *= fa * fb[fj];
+                }
+        }
         f16x8 bh[4], bm[4];
 #pragma unroll
         for (int fj = 0; fj < 4; ++fj) {
@@ -204,12 +187,30 @@ __global__ void __launch_bounds__(256, 3) wgrad_f16x3_kernel(WgradArgs p) {   //
     };
     load(va, 0);
     for (int ks = 0; ks < nk; ++ks) {
-        if (ks) __syncthreads();                   // every wave is done with the last images
-        store(va);
+        const int par = ks & 1;
+        // every wave is done with the last images, edel and chg[par ^ 1] (ks = 0: chg zeroed)
+        __syncthreads();
+        if (tid == 0) chg[par ^ 1] = 0;
+        store(va, par);
         if (ks + 1 < nk) load(va, ks + 1);
         __syncthreads();
-        mfma_step();
+        mfma_step(par);
     }
+    if (kg == 0) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) eend[op][4 * c4 + q] = ecur[q];
+    }
+    if (p.db && tj == 0) {                         // (block-uniform) fold the 4 row groups
+        __syncthreads();
+        if (tid < kWgT && i0 + tid < p.m) {
+            const double t = ((bred[0][tid] + bred[1][tid]) + bred[2][tid]) + bred[3][tid];
+            if (p.part_db)
+                p.part_db[(int64_t)blockIdx.y * p.m + i0 + tid] = t;
+            else
+                p.db[i0 + tid] = (float)t;
+        }
+    }
+    __syncthreads();
     // epilogue: lane (g, c) holds D[64 wi + 16 fi + 4 g + r][64 wj + 16 fj + c]; both
     // inverse scales are powers of two (exact)
     float* dst;
@@ -223,14 +224,14 @@ __global__ void __launch_bounds__(256, 3) wgrad_f16x3_kernel(WgradArgs p) {   //
     }
     float jb[4];
 #pragma unroll
-    for (int fj = 0; fj < 4; ++fj) jb[fj] = inv_s[1][64 * wj + 16 * fj + c];
+    for (int fj = 0; fj < 4; ++fj) jb[fj] = __builtin_ldexpf(1.f, -eend[1][64 * wj + 16 * fj + c]);
 #pragma unroll
     for (int fi = 0; fi < 4; ++fi)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int il = 64 * wi + 16 * fi + 4 * g + r;
             const int i = i0 + il;
-            const float ia = inv_s[0][il];
+            const float ia = __builtin_ldexpf(1.f, -eend[0][il]);
 #pragma unroll
             for (int fj = 0; fj < 4; ++fj) {
                 const int j = j0 + 64 * wj + 16 * fj + c;
@@ -318,8 +319,13 @@ WgradPlan wgrad_plan(int64_t rows, int m, int n) {
     WgradPlan pl;
     pl.tiles_n = (int)ceil_div(n, kWgT);
     pl.tiles = (int)ceil_div(m, kWgT) * pl.tiles_n;
+    static const double part_ratio = [] {       // FGR_WGRAD_PART: partial / operand bytes cap
+        const char* e = getenv("FGR_WGRAD_PART");
+        return e ? std::max(0.01, atof(e)) : 1.0;
+    }();
     int64_t ch = ceil_div(target, pl.tiles);
-    ch = std::min(ch, std::max<int64_t>(1, rows * (m + n) / ((int64_t)m * n)));
+    ch = std::min(ch, std::max<int64_t>(1, (int64_t)(part_ratio * (double)(rows * (m + n)) /
+                                                     ((double)m * n))));
     ch = std::max<int64_t>(1, std::min(ch, ceil_div(rows, kWgK)));
     pl.kc = std::max<int64_t>(kWgK, ceil_div(ceil_div(rows, ch), kWgK) * kWgK);
     pl.chunks = (int)std::max<int64_t>(1, ceil_div(rows, pl.kc));

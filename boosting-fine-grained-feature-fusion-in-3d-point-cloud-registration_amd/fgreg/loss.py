@@ -307,6 +307,11 @@ def compute_loss_train(model, pred, batch):
         # the differentiable f16x3 GEMMs (A W_sym P^T), each row's pair block read by
         # fgr_infonce_rows (the nearest positive within r_p is the target, every other
         # positive within r_n leaves the partition sum)
+        # the positives padded with zero rows to a multiple of 8: the logits' extra columns
+        # are read by no pair, and the backward GEMMs' contraction (K = positives) takes the
+        # 16-B-aligned kernels
+        if P.shape[0] % 8:
+            P = F.pad(P, (0, 0, 0, (-P.shape[0]) % 8))
         logits = linear_t(linear_t(A, w_sym(W), cache=False), P, cache=False)
         return _InfoNCEFn.apply(logits, axyz_all, pxyz_all, a_off, p_off, pair_idx, cfg.r_p,
                                 cfg.r_n)

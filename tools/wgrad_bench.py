@@ -10,12 +10,13 @@ import torch
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, 'boosting-fine-grained-feature-fusion-in-3d-point-cloud-registration_amd'))
 
-# (rows, m = cout, n = cin): transformer in_proj / out_proj / FFN, Res2Net conv1 / splits /
-# conv3+downsample, KPConv (m = 15 cin), unary
-SHAPES = [(9544, 768, 256), (9544, 256, 256), (9544, 1024, 256), (9544, 256, 1024),
-          (9544, 1792, 256), (9544, 224, 224), (9544, 1024, 2048), (9544, 3840, 256),
-          (11472, 1920, 128), (11472, 896, 128), (11472, 112, 112), (11472, 512, 1024),
-          (57264, 256, 528)]
+# (rows, m = cout, n = cin) of the ModelNet B=8 training step (profiles/r05_train_wgrad_table.json):
+# transformer in_proj / out_proj / FFN, Res2Net conv1 / splits / conv3, KPConv (m = 15 cin),
+# the InfoNCE logits (m = padded positives), the head
+SHAPES = [(9544, 768, 256), (9544, 1024, 1792), (9544, 1024, 256), (9544, 256, 1024),
+          (9544, 224, 224), (9544, 256, 256), (9544, 3840, 256), (11472, 112, 112),
+          (11472, 512, 896), (4753, 4800, 256), (57264, 256, 256), (9544, 1792, 256),
+          (11472, 1920, 128)]
 PEAK_TF = 2500.0 / 3           # f16x3: three fp16 products per fp32 product
 
 
