@@ -165,6 +165,9 @@ def _cpu_model():
     return platform.processor() or 'unknown'
 
 
+_TRAIN_STEP_HOOK = None
+
+
 def train_main(args):
     """ms per training step of the workload's batch on one GPU (trainer.py:110-125: forward,
     compute_loss, loss.backward(), clip_grad_norm_, optimizer.step()). The loss is the
@@ -211,6 +214,8 @@ def train_main(args):
     for _ in range(max(args.warmup, 1)):
         step()
     torch.cuda.synchronize()
+    if _TRAIN_STEP_HOOK is not None:          # tools/train_torch_prof.py: the step closure
+        _TRAIN_STEP_HOOK(step)
     if args.gemm_table:
         # per-shape device time of the dense products (forward + dX GEMMs) and of the weight
         # gradients (fgr_gemm_f16x3_wgrad), events around each launch, 3 extra steps

@@ -287,7 +287,7 @@ def compute_loss_train(model, pred, batch):
     host = meta.get('_host')          # the forward's host layout: no device read-back
     lens = list(host['lengths'][p]) if host else [int(v) for v in meta['stack_lengths'][p].tolist()]
     B = len(lens) // 2
-    src_w, tgt_w = torch.split(ov[:sum(lens[:B])], lens[:B]), torch.split(ov[sum(lens[:B]):], lens[B:])
+    src_w, tgt_w = ov[:sum(lens[:B])], ov[sum(lens[:B]):]          # overlap weights (targets)
 
     def w_sym(W):
         t = torch.triu(W)
@@ -338,7 +338,11 @@ def compute_loss_train(model, pred, batch):
         return ((row * rm).sum() / rm.sum() + (col * cm).sum() / cm.sum()) / 2
 
     losses = {}
-    logits = torch.cat(list(pred['src_overlap']) + list(pred['tgt_overlap']), dim=-2)
+    pk = pred.get('_packed')                    # the packed outputs of RegTR's training forward
+    if pk is not None:
+        logits = pk['logits']
+    else:
+        logits = torch.cat(list(pred['src_overlap']) + list(pred['tgt_overlap']), dim=-2)
     for i in cfg.overlap_loss_on:
         losses[f'overlap_{i}'] = F.binary_cross_entropy_with_logits(logits[i, :, 0], ov)
     if ftype == 'circle':
@@ -350,6 +354,13 @@ def compute_loss_train(model, pred, batch):
         losses['feature_un'] = torch.stack([
             circle_pair(pred['src_feat_un'][b], pred['tgt_feat_un'][b], a_xyz[b], pred['tgt_kp'][b])
             for b in range(B)]).mean()
+    elif pk is not None:
+        ns = pk['n_src']
+        for i in cfg.feature_loss_on:
+            f = pk['feats'][i]
+            losses[f'feature_{i}'] = infonce_all(model.feature_criterion.W, f[:ns], f[ns:])
+        losses['feature_un'] = infonce_all(model.feature_criterion_un.W, pk['both'][:ns],
+                                           pk['both'][ns:])
     else:
         for i in cfg.feature_loss_on:
             losses[f'feature_{i}'] = infonce_all(
@@ -359,17 +370,20 @@ def compute_loss_train(model, pred, batch):
             model.feature_criterion_un.W, torch.cat(list(pred['src_feat_un'])),
             torch.cat(list(pred['tgt_feat_un'])))
 
-    def corr_mae(gt, warped, weights):
-        err = (torch.cat(list(warped)) - gt).abs().sum(1)
-        w = torch.cat(list(weights))
+    def corr_mae(gt, warped, w):
+        err = ((warped if torch.is_tensor(warped) else torch.cat(list(warped))) - gt).abs().sum(1)
         return (w * err).sum() / torch.clamp_min(w.sum(), 1e-6)
 
     with torch.no_grad():                 # the targets: keypoints under the ground-truth pose
         gt_src = axyz_all
         gt_tgt = transform_points(pxyz_all, p_off, pose, inverse=True)
     for i in cfg.corr_loss_on:
-        losses[f'corr_{i}'] = (corr_mae(gt_src, [w[i] for w in pred['src_kp_warped']], src_w)
-                               + corr_mae(gt_tgt, [w[i] for w in pred['tgt_kp_warped']], tgt_w))
+        if pk is not None:
+            ns = pk['n_src']
+            ws, wt = pk['corr'][i, :ns], pk['corr'][i, ns:]
+        else:
+            ws, wt = [w[i] for w in pred['src_kp_warped']], [w[i] for w in pred['tgt_kp_warped']]
+        losses[f'corr_{i}'] = corr_mae(gt_src, ws, src_w) + corr_mae(gt_tgt, wt, tgt_w)
     wd = weight_dict(cfg)
     losses['total'] = torch.sum(torch.stack([losses[k] * wd[k] for k in losses]))
     return losses

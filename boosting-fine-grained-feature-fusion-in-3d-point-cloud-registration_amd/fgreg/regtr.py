@@ -323,6 +323,12 @@ class RegTR(nn.Module):
             'tgt_overlap': [logits[:, b:e] for b, e in rows[B:]],
             'pose': pose,
         }
+        if train:
+            # the packed tensors behind the per-cloud views (src clouds first): the training
+            # loss reads them whole, so its backward sees one slice per tensor instead of a
+            # view per cloud (fgreg.loss.compute_loss_train)
+            outputs['_packed'] = {'both': both, 'feats': feats, 'corr': corr, 'logits': logits,
+                                  'n_src': offs[B]}
         return outputs
 
     def _segments(self, slens_c, xyz_c):

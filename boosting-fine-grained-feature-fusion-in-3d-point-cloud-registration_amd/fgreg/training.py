@@ -31,11 +31,28 @@ def unary_train(u: UnaryBlock, x, off, lens, residual=None, post_act=ACT_NONE):
     return segnorm_t(y, off, lens, act=act, residual=residual, post_act=post_act)
 
 
+class _ColSplitFn(torch.autograd.Function):
+    """torch.split(h, w, 1) whose backward is one concatenation of the chunk gradients (the
+    generic split backward materialises a zero tensor of h's shape per chunk, copies the
+    chunk's gradient into it and adds the chunks up)."""
+
+    @staticmethod
+    def forward(ctx, h, w, n):
+        ctx.w = w
+        return tuple(h.narrow(1, i * w, w) for i in range(n))
+
+    @staticmethod
+    def backward(ctx, *grads):
+        ref = next(g for g in grads if g is not None)
+        full = [g if g is not None else ref.new_zeros(ref.shape[0], ctx.w) for g in grads]
+        return torch.cat(full, 1), None, None
+
+
 def bottle2neck_train(m, x):
     """my_Bottle2neck.forward (res2net.py:126-159) with BatchNorm1d on batch statistics."""
     w = m.width
     h = batchnorm_t(m.bn1, linear_t(x, m.conv1.weight), act=ACT_RELU)
-    chunks = torch.split(h, w, 1)
+    chunks = _ColSplitFn.apply(h, w, h.shape[1] // w)
     outs, sp = [], None
     for i in range(m.nums):
         sp = chunks[i] if i == 0 else sp + chunks[i]
