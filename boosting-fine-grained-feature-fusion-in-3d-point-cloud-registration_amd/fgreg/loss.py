@@ -338,7 +338,7 @@ def compute_loss_train(model, pred, batch):
         return ((row * rm).sum() / rm.sum() + (col * cm).sum() / cm.sum()) / 2
 
     losses = {}
-    pk = pred.get('_packed')                    # the packed outputs of RegTR's training forward
+    pk = getattr(pred, 'packed', None)          # the packed outputs of RegTR's training forward
     if pk is not None:
         logits = pk['logits']
     else:

@@ -324,11 +324,13 @@ class RegTR(nn.Module):
             'pose': pose,
         }
         if train:
-            # the packed tensors behind the per-cloud views (src clouds first): the training
-            # loss reads them whole, so its backward sees one slice per tensor instead of a
-            # view per cloud (fgreg.loss.compute_loss_train)
-            outputs['_packed'] = {'both': both, 'feats': feats, 'corr': corr, 'logits': logits,
-                                  'n_src': offs[B]}
+            # the packed tensors behind the per-cloud views (src clouds first), as an attribute
+            # of the output dict (its keys stay the reference's): the training loss reads them
+            # whole, so its backward sees one slice per tensor instead of a view per cloud
+            # (fgreg.loss.compute_loss_train)
+            outputs = _TrainOutputs(outputs)
+            outputs.packed = {'both': both, 'feats': feats, 'corr': corr, 'logits': logits,
+                              'n_src': offs[B]}
         return outputs
 
     def _segments(self, slens_c, xyz_c):
@@ -377,6 +379,12 @@ class RegTR(nn.Module):
     def _apply(self, fn, *args, **kwargs):
         _GRAPHS.pop(self, None)        # .to() / .cuda() move the weights the graphs point at
         return super()._apply(fn, *args, **kwargs)
+
+
+class _TrainOutputs(dict):
+    """RegTR.forward's output dict in training mode, carrying the packed tensors (``packed``)
+    beside the reference's keys."""
+    packed = None
 
 
 # ------------------------------------------------------------------------------------------
