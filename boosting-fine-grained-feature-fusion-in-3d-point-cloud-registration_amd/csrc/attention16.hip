@@ -213,7 +213,7 @@ attn_f16x3_v2_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __r
                      const int64_t* __restrict__ q_off, const int64_t* __restrict__ kv_off,
                      const int32_t* __restrict__ kv_seg, int n_head, int n_seg, int n_qblk,
                      float scale_log2, int global_tiles, uint32_t drop_seed = 0,
-                     uint32_t drop_thresh = 0, float inv_keep = 1.f) {
+                     uint32_t drop_thresh = 0, float inv_keep = 1.f, float* __restrict__ lse_out = nullptr) {
     constexpr int KD = DH / 32, TD = DH / 16;
     constexpr int UN = units<DH>();
     constexpr int PW = UN / 64 / 4;                              // DMA pieces per wave per tile
@@ -436,7 +436,12 @@ attn_f16x3_v2_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __r
     }
 
     // O^T (dh 16t + 4g + r, query c) / l (both in 2^14 units)
-    const float inv = (DROP ? inv_keep : 1.0f) / xg_sum16(l_run);
+    const float lsum = xg_sum16(l_run);
+    const float inv = (DROP ? inv_keep : 1.0f) / lsum;
+    // training: the row's log2-sum-exp of the scaled scores (l in 2^14 units) for the
+    // backward, which then skips its own first pass (fgr_attention_bwd_train)
+    if (lse_out && qrow < qe && g == 0)
+        lse_out[qrow * n_head + head] = m_run + __builtin_amdgcn_logf(lsum) - 14.f;
     if (qrow < qe) {
 #pragma unroll
         for (int t = 0; t < TD; ++t) {
@@ -471,7 +476,8 @@ static int attention_f16x3_impl(const float* q, int64_t ld_q, const float* k, in
                                 const int32_t* kv_seg, int32_t n_seg, int32_t n_kv_seg,
                                 int64_t n_kv_rows, int32_t max_q_len, int32_t max_kv_len,
                                 int32_t n_head, int32_t head_dim, float scale, void* workspace,
-                                int64_t ws_bytes, uint32_t drop_seed, float drop_p, void* stream) {
+                                int64_t ws_bytes, uint32_t drop_seed, float drop_p, void* stream,
+                                float* lse_out = nullptr) {
     FGR_REQUIRE(q && k && v && o && q_off && kv_off && kv_seg && workspace && n_seg > 0 &&
                     n_kv_seg > 0 && n_head > 0 && max_q_len >= 0 && max_kv_len >= 0,
                 "fgr_attention_f16x3: bad arguments");
@@ -513,19 +519,19 @@ static int attention_f16x3_impl(const float* q, int64_t ld_q, const float* k, in
         if (dh == 32)
             hipLaunchKernelGGL((attn_f16x3_v2_kernel<32, true>), dim3((unsigned)n_blocks), dim3(256), 0,
                                st, q, ld_q, (const uint4*)img, (const int2*)sc, o, ld_o, q_off, kv_off,
-                               kv_seg, n_head, n_seg, n_qblk, sl2, 0, drop_seed, thresh, inv_keep);
+                               kv_seg, n_head, n_seg, n_qblk, sl2, 0, drop_seed, thresh, inv_keep, lse_out);
         else
             hipLaunchKernelGGL((attn_f16x3_v2_kernel<64, true>), dim3((unsigned)n_blocks), dim3(256), 0,
                                st, q, ld_q, (const uint4*)img, (const int2*)sc, o, ld_o, q_off, kv_off,
-                               kv_seg, n_head, n_seg, n_qblk, sl2, 0, drop_seed, thresh, inv_keep);
+                               kv_seg, n_head, n_seg, n_qblk, sl2, 0, drop_seed, thresh, inv_keep, lse_out);
     } else if (dh == 32) {
         hipLaunchKernelGGL((attn_f16x3_v2_kernel<32>), dim3((unsigned)n_blocks), dim3(256), 0, st, q,
                            ld_q, (const uint4*)img, (const int2*)sc, o, ld_o, q_off, kv_off, kv_seg,
-                           n_head, n_seg, n_qblk, sl2, 0, 0u, 0u, 1.f);
+                           n_head, n_seg, n_qblk, sl2, 0, 0u, 0u, 1.f, lse_out);
     } else {
         hipLaunchKernelGGL((attn_f16x3_v2_kernel<64>), dim3((unsigned)n_blocks), dim3(256), 0, st, q,
                            ld_q, (const uint4*)img, (const int2*)sc, o, ld_o, q_off, kv_off, kv_seg,
-                           n_head, n_seg, n_qblk, sl2, 0, 0u, 0u, 1.f);
+                           n_head, n_seg, n_qblk, sl2, 0, 0u, 0u, 1.f, lse_out);
     }
     FGR_CHECK_LAUNCH("attn_f16x3_v2_kernel");
     return FGR_OK;
@@ -555,6 +561,21 @@ extern "C" int fgr_attention_f16x3_drop(const float* q, int64_t ld_q, const floa
     return attention_f16x3_impl(q, ld_q, k, ld_k, v, ld_v, o, ld_o, q_off, kv_off, kv_seg, n_seg,
                                 n_kv_seg, n_kv_rows, max_q_len, max_kv_len, n_head, head_dim,
                                 scale, workspace, ws_bytes, seed, p, stream);
+}
+
+extern "C" int fgr_attention_f16x3_train(const float* q, int64_t ld_q, const float* k, int64_t ld_k,
+                                         const float* v, int64_t ld_v, float* o, int64_t ld_o,
+                                         const int64_t* q_off, const int64_t* kv_off,
+                                         const int32_t* kv_seg, int32_t n_seg, int32_t n_kv_seg,
+                                         int64_t n_kv_rows, int32_t max_q_len, int32_t max_kv_len,
+                                         int32_t n_head, int32_t head_dim, float scale,
+                                         void* workspace, int64_t ws_bytes, uint32_t seed, float p,
+                                         float* lse, void* stream) {
+    FGR_REQUIRE(p >= 0.f && p < 1.f, "fgr_attention_f16x3_train: dropout p %f not in [0, 1)", p);
+    FGR_REQUIRE(lse, "fgr_attention_f16x3_train: null lse");
+    return attention_f16x3_impl(q, ld_q, k, ld_k, v, ld_v, o, ld_o, q_off, kv_off, kv_seg, n_seg,
+                                n_kv_seg, n_kv_rows, max_q_len, max_kv_len, n_head, head_dim,
+                                scale, workspace, ws_bytes, seed, p, stream, lse);
 }
 
 // The attention on K / V images of GLOBAL 64-row tiles written by fgr_gemm_f16x3_ln_qkv (head

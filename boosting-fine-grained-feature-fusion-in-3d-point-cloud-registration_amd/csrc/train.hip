@@ -834,6 +834,9 @@ struct AttnBwd {
     // are dropped, kept ones scaled by inv_keep (the forward's mask: fgr_attention_f16x3_drop)
     uint32_t drop_seed, drop_thresh;
     float inv_keep;
+    // training: the forward's log2-sum-exp per (row, head) (fgr_attention_f16x3_train); the
+    // MFMA dQ kernel then skips its max / sum pass
+    const float* lse_in;
 };
 
 template <int DH>
@@ -1059,8 +1062,9 @@ attn_bwd_dq_mfma_kernel(AttnBwd a) {
         return acc;
     };
     // pass 1: the row's max and sum (per lane over its keys, then over the 4 lanes of the row)
+    // -- or the forward's log-sum-exp
     float m = -INFINITY, l = 0.f;
-    for (int64_t t0 = kb; t0 < ke; t0 += 64) {
+    for (int64_t t0 = a.lse_in ? ke : kb; t0 < ke; t0 += 64) {
         const int nt = (int)min((int64_t)64, ke - t0);
         __syncthreads();
         stage_rows<DH, LD>(kt, a.k + t0 * a.ldk + h * DH, a.ldk, nt, 1.f);
@@ -1078,7 +1082,8 @@ attn_bwd_dq_mfma_kernel(AttnBwd a) {
         }
     }
     const float M = xg_max_tr(m);
-    const float lse2 = M + __builtin_amdgcn_logf(xg_sum_tr(m == -INFINITY ? 0.f : l * __builtin_amdgcn_exp2f(m - M)));
+    const float lse2 = a.lse_in ? (ok ? a.lse_in[r * a.nhead + h] : 0.f)
+                                : M + __builtin_amdgcn_logf(xg_sum_tr(m == -INFINITY ? 0.f : l * __builtin_amdgcn_exp2f(m - M)));
     // pass 2: P, dP, dS and dQ^T += K^T dS^T
     f32x4_t dq[DT];
 #pragma unroll
@@ -1590,6 +1595,19 @@ extern "C" int fgr_segnorm_apply(const float* x, int64_t n, int32_t c, const int
     return FGR_OK;
 }
 
+extern "C" int fgr_segnorm_fwd(const float* x, int64_t n, int32_t c, const int64_t* seg_off,
+                               int32_t n_seg, int64_t max_seg_len, const float* row_div, float eps,
+                               float* mean, float* rstd, float* var, const float* gamma,
+                               const float* beta, int32_t act, const float* residual,
+                               int32_t post_act, float* out, void* ws, size_t ws_bytes,
+                               void* stream) {
+    const int rc = fgr_segnorm_stats(x, n, c, seg_off, n_seg, max_seg_len, row_div, eps, mean, rstd,
+                                     var, ws, ws_bytes, stream);
+    if (rc != FGR_OK) return rc;
+    return fgr_segnorm_apply(x, n, c, seg_off, n_seg, row_div, mean, rstd, gamma, beta, act, residual,
+                             post_act, out, stream);
+}
+
 extern "C" int fgr_segnorm_bwd(const float* x, int64_t n, int32_t c, const int64_t* seg_off,
                                int32_t n_seg, int64_t max_seg_len, const float* row_div,
                                const float* mean, const float* rstd, const float* gamma,
@@ -1711,7 +1729,8 @@ static int attention_bwd_impl(const float* q, int64_t ldq, const float* k, int64
                               const int64_t* kv_off, const int32_t* kv_seg, int32_t n_seg,
                               int32_t n_kv_seg, int64_t nq, int64_t max_q_len, int64_t max_kv_len,
                               int32_t nhead, int32_t dh, float scale, void* ws, size_t ws_bytes,
-                              uint32_t drop_seed, float drop_p, void* stream) {
+                              uint32_t drop_seed, float drop_p, void* stream,
+                              const float* lse_in = nullptr) {
     FGR_REQUIRE(n_seg > 0 && n_kv_seg > 0 && nhead > 0 && nq >= 0 &&
                     (dh == 4 || dh == 8 || dh == 16 || dh == 32 || dh == 64),
                 "fgr_attention_bwd: bad arguments (head dim 4 / 8 / 16 / 32 / 64)");
@@ -1725,7 +1744,7 @@ static int attention_bwd_impl(const float* q, int64_t ldq, const float* k, int64
               (int)std::max<int64_t>(1, ceil_div(max_kv_len, 64)), scale, (float*)ws,
               (float*)ws + std::max<int64_t>(nq, 1) * nhead, drop_seed,
               (uint32_t)std::min(4294967295.0, (double)drop_p * 4294967296.0),
-              drop_p > 0.f ? 1.0f / (1.0f - drop_p) : 1.f};
+              drop_p > 0.f ? 1.0f / (1.0f - drop_p) : 1.f, lse_in};
     const bool drop = drop_p > 0.f;
     hipStream_t st = as_stream(stream);
     dim3 g1((unsigned)(n_seg * a.q_blocks), nhead), g2((unsigned)(n_kv_seg * a.kv_blocks), nhead);
@@ -1789,6 +1808,23 @@ extern "C" int fgr_attention_bwd(const float* q, int64_t ldq, const float* k, in
     return attention_bwd_impl(q, ldq, k, ldk, v, ldv, o, ldo, dout, lddo, dq, lddq, dk, lddk, dv,
                               lddv, q_off, kv_off, kv_seg, n_seg, n_kv_seg, nq, max_q_len,
                               max_kv_len, nhead, dh, scale, ws, ws_bytes, 0u, 0.f, stream);
+}
+
+extern "C" int fgr_attention_bwd_train(const float* q, int64_t ldq, const float* k, int64_t ldk,
+                                       const float* v, int64_t ldv, const float* o, int64_t ldo,
+                                       const float* dout, int64_t lddo, float* dq, int64_t lddq,
+                                       float* dk, int64_t lddk, float* dv, int64_t lddv,
+                                       const int64_t* q_off, const int64_t* kv_off,
+                                       const int32_t* kv_seg, int32_t n_seg, int32_t n_kv_seg,
+                                       int64_t nq, int64_t max_q_len, int64_t max_kv_len,
+                                       int32_t nhead, int32_t dh, float scale, void* ws,
+                                       size_t ws_bytes, uint32_t seed, float p, const float* lse,
+                                       void* stream) {
+    FGR_REQUIRE(p >= 0.f && p < 1.f, "fgr_attention_bwd_train: dropout p %f not in [0, 1)", p);
+    FGR_REQUIRE(lse, "fgr_attention_bwd_train: null lse");
+    return attention_bwd_impl(q, ldq, k, ldk, v, ldv, o, ldo, dout, lddo, dq, lddq, dk, lddk, dv,
+                              lddv, q_off, kv_off, kv_seg, n_seg, n_kv_seg, nq, max_q_len,
+                              max_kv_len, nhead, dh, scale, ws, ws_bytes, seed, p, stream, lse);
 }
 
 extern "C" int fgr_attention_bwd_drop(const float* q, int64_t ldq, const float* k, int64_t ldk,

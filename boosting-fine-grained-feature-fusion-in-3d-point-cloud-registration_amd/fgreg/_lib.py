@@ -50,6 +50,9 @@ SIGNATURES = {
     'fgr_attention_f16x3_drop': [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i32,
                                  _i32, _i64, _i32, _i32, _i32, _i32, _f32, _vp, _i64,
                                  ctypes.c_uint32, _f32, _vp],
+    'fgr_attention_f16x3_train': [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i32,
+                                  _i32, _i64, _i32, _i32, _i32, _i32, _f32, _vp, _i64,
+                                  ctypes.c_uint32, _f32, _vp, _vp],
     'fgr_attention_bf16_workspace': [_i64, _i32, _i32, ctypes.POINTER(_sz)],
     'fgr_attention_bf16': [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i32, _i32,
                            _i64, _i32, _i32, _i32, _i32, _f32, _vp, _i64, _vp],
@@ -123,6 +126,8 @@ SIGNATURES = {
     'fgr_segnorm_stats': [_vp, _i64, _i32, _vp, _i32, _i64, _vp, _f32, _vp, _vp, _vp, _vp, _sz, _vp],
     'fgr_segnorm_apply': [_vp, _i64, _i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _i32, _vp,
                           _vp],
+    'fgr_segnorm_fwd': [_vp, _i64, _i32, _vp, _i32, _i64, _vp, _f32, _vp, _vp, _vp, _vp, _vp, _i32, _vp,
+                        _i32, _vp, _vp, _sz, _vp],
     'fgr_segnorm_bwd': [_vp, _i64, _i32, _vp, _i32, _i64, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32,
                         _vp, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp],
     'fgr_colsum_workspace': [_i64, _i32, ctypes.POINTER(_sz)],
@@ -138,6 +143,9 @@ SIGNATURES = {
     'fgr_attention_bwd_drop': [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64,
                                _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i32, _i32, _i64, _i64, _i64,
                                _i32, _i32, _f32, _vp, _sz, ctypes.c_uint32, _f32, _vp],
+    'fgr_attention_bwd_train': [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64,
+                                _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i32, _i32, _i64, _i64, _i64,
+                                _i32, _i32, _f32, _vp, _sz, ctypes.c_uint32, _f32, _vp, _vp],
     'fgr_crop_max_points': [ctypes.POINTER(_i32)],
     'fgr_crop_pairs_mask': [_vp, _i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     'fgr_crop_pairs_assemble': [_vp, _i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp,

@@ -55,6 +55,7 @@ def colsum(x: torch.Tensor) -> torch.Tensor:
 
 
 _WGRAD = os.environ.get('FGREG_WGRAD', '1') != '0'     # 0: dW on the generic GEMM (A/B)
+_ATTN_LSE = os.environ.get('FGREG_ATTN_LSE', '1') != '0'  # 0: the backward recomputes it (A/B)
 
 
 def _wgrad_ok(t):
@@ -184,13 +185,12 @@ def kpconv_scatter(q, s, idx, dwf, kp, extent):
     start, pos, _ = nbr_inverse(idx, ns)
     dx = torch.empty((ns, cin), dtype=torch.float32, device=dwf.device)
     L = _lib.load()
-    nb = _lib._sz(0)
-    _lib.check(L.fgr_kpconv_scatter_workspace(nq, width, cin, nb), 'fgr_kpconv_scatter_workspace')
-    ws = torch.empty(nb.value, dtype=torch.uint8, device=dwf.device)
+    nb = _lib.ws_size('fgr_kpconv_scatter_workspace', nq, width, cin)
+    ws = ops._workspace(dwf.device, nb)         # grow-only scratch, not a fresh buffer per call
     _lib.check(L.fgr_kpconv_scatter(
         _ptr(_c(q, torch.float32)), _ptr(_c(s, torch.float32)), nq, ns, _ptr(_c(idx, torch.int64)),
         width, _ptr(dwf), cin, _ptr(_c(kp, torch.float32)), K, float(extent), _ptr(start),
-        _ptr(pos), _ptr(dx), _ptr(ws), nb.value, _stream()), 'fgr_kpconv_scatter')
+        _ptr(pos), _ptr(dx), _ptr(ws), nb, _stream()), 'fgr_kpconv_scatter')
     return dx
 
 
@@ -278,14 +278,12 @@ class _SegNormFn(torch.autograd.Function):
         rstd, var = torch.empty_like(mean), torch.empty_like(mean)
         ws = _seg_ws(max_len, c, n_seg, device=x.device)
         rd = _c(row_div, torch.float32) if row_div is not None else None
-        _lib.check(L.fgr_segnorm_stats(_ptr(x), n, c, _ptr(seg_off), n_seg, max_len, _ptr(rd),
-                                       float(eps), _ptr(mean), _ptr(rstd), _ptr(var), _ptr(ws),
-                                       ws.numel(), _stream()), 'fgr_segnorm_stats')
         res = _c(residual, torch.float32) if residual is not None else None
         y = torch.empty_like(x)
-        _lib.check(L.fgr_segnorm_apply(_ptr(x), n, c, _ptr(seg_off), n_seg, _ptr(rd), _ptr(mean),
-                                       _ptr(rstd), _ptr(gamma), _ptr(beta), act, _ptr(res), post_act,
-                                       _ptr(y), _stream()), 'fgr_segnorm_apply')
+        _lib.check(L.fgr_segnorm_fwd(_ptr(x), n, c, _ptr(seg_off), n_seg, max_len, _ptr(rd),
+                                     float(eps), _ptr(mean), _ptr(rstd), _ptr(var), _ptr(gamma),
+                                     _ptr(beta), act, _ptr(res), post_act, _ptr(y), _ptr(ws),
+                                     ws.numel(), _stream()), 'fgr_segnorm_fwd')
         if stats is not None:
             stats.append((mean, var, n))
         ctx.meta = (n, c, n_seg, max_len, act, post_act, residual is not None, gamma is not None)
@@ -403,15 +401,19 @@ class _AttentionFn(torch.autograd.Function):
     def forward(ctx, qkv, off, kv_seg, max_len, nhead, p=0.0, seed=0):
         qkv = _c(qkv, torch.float32)
         d = qkv.shape[1] // 3
-        o = ops.attention(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], off, off, kv_seg, max_len,
-                          nhead, dropout=(seed, p) if p > 0.0 else None)
+        q, k, v = qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:]
+        # the forward's log2-sum-exp per (row, head) for the backward (fgr_attention_*_train)
+        lse = (torch.empty((qkv.shape[0], nhead), dtype=torch.float32, device=qkv.device)
+               if _ATTN_LSE and ops.attention_lse_ok(q, k, v, nhead) else None)
+        o = ops.attention(q, k, v, off, off, kv_seg, max_len, nhead,
+                          dropout=(seed, p) if p > 0.0 else None, lse=lse)
         ctx.meta = (d, int(max_len), int(nhead), float(p), int(seed))
-        ctx.save_for_backward(qkv, o, off, kv_seg)
+        ctx.save_for_backward(qkv, o, off, kv_seg, lse)
         return o
 
     @staticmethod
     def backward(ctx, do):
-        qkv, o, off, kv_seg = ctx.saved_tensors
+        qkv, o, off, kv_seg, lse = ctx.saved_tensors
         d, max_len, nhead, p_drop, seed = ctx.meta
         do = _c(do, torch.float32)
         n = qkv.shape[0]
@@ -427,7 +429,10 @@ class _AttentionFn(torch.autograd.Function):
                 dp, ld, dp + 4 * d, ld, dp + 8 * d, ld, _ptr(off), _ptr(off), _ptr(kv_seg), n_seg,
                 n_seg, n, max_len, max_len, nhead, dh, float(math.sqrt(1.0 / float(dh))),
                 _ptr(ws), nb.value)
-        if p_drop > 0.0:
+        if lse is not None:
+            _lib.check(L.fgr_attention_bwd_train(*args, seed & 0xFFFFFFFF, p_drop, _ptr(lse),
+                                                 _stream()), 'fgr_attention_bwd_train')
+        elif p_drop > 0.0:
             _lib.check(L.fgr_attention_bwd_drop(*args, seed & 0xFFFFFFFF, p_drop, _stream()),
                        'fgr_attention_bwd_drop')
         else:

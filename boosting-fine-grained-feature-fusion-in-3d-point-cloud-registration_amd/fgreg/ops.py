@@ -578,14 +578,16 @@ assert ATTN_MODE in ('f16x3', 'bf16'), ATTN_MODE
 
 
 def attention(q, k, v, q_off, kv_off, kv_seg, max_q_len, n_head, out=None,
-              max_kv_len=None, dropout=None) -> torch.Tensor:
+              max_kv_len=None, dropout=None, lse=None) -> torch.Tensor:
     """Packed-segment MHA core: rows of query segment i attend to key segment kv_seg[i].
 
     q, k, v: (rows, n_head * dh) views with unit column stride (may be column slices of
     one fused QKV tensor). Returns o (Nq, n_head * dh). ``max_kv_len`` defaults to
     ``max_q_len`` (self / cross attention over one segmentation). ``dropout`` = (seed, p):
     the training forward's attention-weight dropout (fgr_attention_f16x3_drop; f16x3 mode,
-    head dim 32 / 64).
+    head dim 32 / 64). ``lse`` (rows, n_head) fp32: the training forward
+    (fgr_attention_f16x3_train) also writes each row's log2-sum-exp there for the backward
+    (only for shapes ``attention_lse_ok`` accepts).
     """
     _dev(q, k, v, q_off, kv_off, kv_seg)
     for t in (q, k, v):
@@ -603,7 +605,18 @@ def attention(q, k, v, q_off, kv_off, kv_seg, max_q_len, n_head, out=None,
     split = (dh in (32, 64)
              and all(t.stride(0) % 4 == 0 and t.data_ptr() % 16 == 0 for t in (q, k, v, out)))
     t0 = _begin('attention')
-    if dropout is not None and float(dropout[1]) > 0.0:
+    if lse is not None:
+        assert split and ATTN_MODE == 'f16x3' and lse.is_contiguous() and lse.shape == (q.shape[0], n_head)
+        seed, p = (int(dropout[0]), float(dropout[1])) if dropout is not None else (0, 0.0)
+        nb = _lib.ws_size('fgr_attention_f16x3_workspace', k.shape[0], n_kv_seg, n_head)
+        ws = _workspace(q.device, nb)
+        _lib.check(L.fgr_attention_f16x3_train(
+            _ptr(q), q.stride(0), _ptr(k), k.stride(0), _ptr(v), v.stride(0), _ptr(out),
+            out.stride(0), _ptr(q_off), _ptr(kv_off), _ptr(kv_seg), n_seg, n_kv_seg, k.shape[0],
+            int(max_q_len), int(max_kv_len), n_head, dh, float(math.sqrt(1.0 / float(dh))),
+            _ptr(ws), ws.numel(), seed & 0xFFFFFFFF, p, _ptr(lse), _stream()),
+            'fgr_attention_f16x3_train')
+    elif dropout is not None and float(dropout[1]) > 0.0:
         if not (split and ATTN_MODE == 'f16x3'):
             raise NotImplementedError('attention dropout needs the f16x3 mode, head dim 32 / 64 '
                                       'and 16-B aligned rows')
@@ -636,6 +649,13 @@ def attention(q, k, v, q_off, kv_off, kv_seg, max_q_len, n_head, out=None,
                    'fgr_attention')
     _end('attention', t0, lambda: attention_flops(q_off, kv_off, kv_seg, d))
     return out
+
+
+def attention_lse_ok(q, k, v, n_head) -> bool:
+    """True if ops.attention can hand the backward its log-sum-exp (``lse``)."""
+    dh = q.shape[1] // n_head
+    return (ATTN_MODE == 'f16x3' and dh in (32, 64)
+            and all(t.stride(0) % 4 == 0 and t.data_ptr() % 16 == 0 for t in (q, k, v)))
 
 
 def copy_batch(srcs, dsts):

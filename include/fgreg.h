@@ -610,6 +610,12 @@ int fgr_segnorm_apply(const float* x, int64_t n, int32_t c, const int64_t* seg_o
                       const float* row_div, const float* mean, const float* rstd, const float* gamma,
                       const float* beta, int32_t act, const float* residual, int32_t post_act,
                       float* out, void* stream);
+/* fgr_segnorm_stats then fgr_segnorm_apply in one call (the training forward). */
+int fgr_segnorm_fwd(const float* x, int64_t n, int32_t c, const int64_t* seg_off, int32_t n_seg,
+                    int64_t max_seg_len, const float* row_div, float eps, float* mean, float* rstd,
+                    float* var, const float* gamma, const float* beta, int32_t act,
+                    const float* residual, int32_t post_act, float* out, void* ws, size_t ws_bytes,
+                    void* stream);
 int fgr_segnorm_bwd(const float* x, int64_t n, int32_t c, const int64_t* seg_off, int32_t n_seg,
                     int64_t max_seg_len, const float* row_div, const float* mean, const float* rstd,
                     const float* gamma, const float* beta, int32_t act, int32_t has_residual,
@@ -643,6 +649,25 @@ int fgr_attention_f16x3_drop(const float* q, int64_t ld_q, const float* k, int64
                              int32_t max_kv_len, int32_t n_head, int32_t head_dim, float scale,
                              void* workspace, int64_t ws_bytes, uint32_t seed, float p,
                              void* stream);
+/* Training pair (dropout p >= 0 as the _drop pair): the forward also writes, per (row, head),
+ * the log2-sum-exp of the scaled scores to lse (n_rows * n_head floats); the backward reads it
+ * back and skips its own max / sum pass over the keys (head dim 16 / 32 / 64, 16-B aligned
+ * rows; other shapes recompute it). */
+int fgr_attention_f16x3_train(const float* q, int64_t ld_q, const float* k, int64_t ld_k,
+                              const float* v, int64_t ld_v, float* o, int64_t ld_o,
+                              const int64_t* q_off, const int64_t* kv_off, const int32_t* kv_seg,
+                              int32_t n_seg, int32_t n_kv_seg, int64_t n_kv_rows, int32_t max_q_len,
+                              int32_t max_kv_len, int32_t n_head, int32_t head_dim, float scale,
+                              void* workspace, int64_t ws_bytes, uint32_t seed, float p, float* lse,
+                              void* stream);
+int fgr_attention_bwd_train(const float* q, int64_t ldq, const float* k, int64_t ldk,
+                            const float* v, int64_t ldv, const float* o, int64_t ldo,
+                            const float* dout, int64_t lddo, float* dq, int64_t lddq, float* dk,
+                            int64_t lddk, float* dv, int64_t lddv, const int64_t* q_off,
+                            const int64_t* kv_off, const int32_t* kv_seg, int32_t n_seg,
+                            int32_t n_kv_seg, int64_t nq, int64_t max_q_len, int64_t max_kv_len,
+                            int32_t nhead, int32_t dh, float scale, void* ws, size_t ws_bytes,
+                            uint32_t seed, float p, const float* lse, void* stream);
 int fgr_attention_bwd_drop(const float* q, int64_t ldq, const float* k, int64_t ldk,
                            const float* v, int64_t ldv, const float* o, int64_t ldo,
                            const float* dout, int64_t lddo, float* dq, int64_t lddq, float* dk,
