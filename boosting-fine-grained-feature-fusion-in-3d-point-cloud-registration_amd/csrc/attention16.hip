@@ -80,13 +80,13 @@ __device__ __forceinline__ int v_swz(int key) {
 }
 
 template <int DH>
-__global__ void __launch_bounds__(256)
-attn_kv_image16_kernel(const float* __restrict__ k, int64_t ld_k, const float* __restrict__ v,
-                       int64_t ld_v, const int64_t* __restrict__ kv_off, int n_head,
-                       uint4* __restrict__ img, int2* __restrict__ sc) {
+__device__ __forceinline__ void kv_image16(const float* __restrict__ k, int64_t ld_k,
+                                           const float* __restrict__ v, int64_t ld_v,
+                                           const int64_t* __restrict__ kv_off, int n_head,
+                                           uint4* __restrict__ img, int2* __restrict__ sc, int s,
+                                           int h, int tt) {
     constexpr int NF = DH / 16;                                  // float4s per thread
     constexpr int RU = DH / 4;                                   // float4s per key row
-    const int s = blockIdx.z, h = blockIdx.y, tt = blockIdx.x;
     const int64_t kb = kv_off[s];
     const int nk = (int)(kv_off[s + 1] - kb);
     if (tt * 64 >= nk) return;                                   // block-uniform
@@ -103,8 +103,10 @@ attn_kv_image16_kernel(const float* __restrict__ k, int64_t ld_k, const float* _
         const int64_t row = kb + tt * 64 + key;
         const float4 kx = ok ? *reinterpret_cast<const float4*>(k + row * ld_k + h * DH + d0)
                              : make_float4(0.f, 0.f, 0.f, 0.f);
-        const float4 vx = ok ? *reinterpret_cast<const float4*>(v + row * ld_v + h * DH + d0)
-                             : make_float4(0.f, 0.f, 0.f, 0.f);
+        // v == k (the backward's one-matrix images): one read
+        const float4 vx = v == k ? kx
+                          : ok   ? *reinterpret_cast<const float4*>(v + row * ld_v + h * DH + d0)
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
         kf[i][0] = kx.x; kf[i][1] = kx.y; kf[i][2] = kx.z; kf[i][3] = kx.w;
         vf[i][0] = vx.x; vf[i][1] = vx.y; vf[i][2] = vx.z; vf[i][3] = vx.w;
 #pragma unroll
@@ -144,6 +146,34 @@ attn_kv_image16_kernel(const float* __restrict__ k, int64_t ld_k, const float* _
                 *reinterpret_cast<const uint2*>(vt[t]);
         }
     }
+}
+
+template <int DH>
+__global__ void __launch_bounds__(256)
+attn_kv_image16_kernel(const float* __restrict__ k, int64_t ld_k, const float* __restrict__ v,
+                       int64_t ld_v, const int64_t* __restrict__ kv_off, int n_head,
+                       uint4* __restrict__ img, int2* __restrict__ sc) {
+    kv_image16<DH>(k, ld_k, v, ld_v, kv_off, n_head, img, sc, blockIdx.z, blockIdx.y, blockIdx.x);
+}
+
+// the training backward's images of one matrix each (k = v = src: both parts), up to four
+// matrices in one launch: blockIdx.z = job * max_seg + segment
+struct ImgJobs {
+    const float* src[4];
+    int64_t ld[4];
+    const int64_t* off[4];
+    uint4* img[4];
+    int2* sc[4];
+    int n_seg[4];
+    int max_seg;
+};
+
+template <int DH>
+__global__ void __launch_bounds__(256) attn_image16_jobs_kernel(ImgJobs j) {
+    const int job = blockIdx.z / j.max_seg, s = blockIdx.z % j.max_seg;
+    if (s >= j.n_seg[job]) return;
+    kv_image16<DH>(j.src[job], j.ld[job], j.src[job], j.ld[job], j.off[job], (int)gridDim.y,
+                   j.img[job], j.sc[job], s, blockIdx.y, blockIdx.x);
 }
 
 template <int N>
@@ -455,7 +485,567 @@ attn_f16x3_v2_kernel(const float* __restrict__ q, int64_t ld_q, const uint4* __r
 
 int64_t n_tiles16(int64_t n_kv_rows, int32_t n_kv_seg) { return n_kv_rows / 64 + n_kv_seg + 1; }
 
+// ---- training: dQ of the attention on the f16 matrix cores (f16x3), given the forward's
+// log2-sum-exp (fgr_attention_bwd_train). The forward kernel's structure with three images per
+// 64-key tile, built by attn_kv_image16_kernel (per-segment tiles):
+//   imgK = (K as the K operand, K as the V operand), imgV = (V as the K operand, unused):
+//   S^T[key][query]  = K Q^T        A = K (imgK, K part), B = Q (registers, split once)
+//   dP^T[key][query] = V dO^T       A = V (imgV, K part), B = dO (registers, split once)
+//   P = exp2(S - lse2) (no running max: the forward's lse), dS = P (dP - D), D = dO . O;
+//   dQ^T[dh][query] += K^T dS^T     A = K (imgK, V part: transposed reads), B = dS (registers,
+//                                   per query and tile scaled into fp16's range and split)
+// dQ = scale * sum dS K. Same lane maps, DMA double buffer and barriers as the forward.
+template <int DH, bool DROP>
+__global__ void __launch_bounds__(256, DH == 64 ? 2 : 4)
+attn_bwd_dq_f16x3_kernel(const float* __restrict__ q, int64_t ld_q, const float* __restrict__ dout,
+                         int64_t ld_do, const float* __restrict__ o, int64_t ld_o,
+                         const uint4* __restrict__ imgk, const int2* __restrict__ sck,
+                         const uint4* __restrict__ imgv, const int2* __restrict__ scv,
+                         float* __restrict__ dq, int64_t ld_dq, const int64_t* __restrict__ q_off,
+                         const int64_t* __restrict__ kv_off, const int32_t* __restrict__ kv_seg,
+                         int n_head, int n_seg, int n_qblk, float scale, float scale_log2,
+                         const float* __restrict__ lse_in, float* __restrict__ lse_out,
+                         float* __restrict__ dsum_out, float* __restrict__ lsed_t,
+                         uint32_t drop_seed, uint32_t drop_thresh, float inv_keep) {
+    constexpr int KD = DH / 32, TD = DH / 16;
+    constexpr int UN = units<DH>();                              // imgK units per tile
+    constexpr int UK = unit_v<DH>();                             // the K part (imgV)
+    constexpr int PW = UN / 64 / 4, PWV = UK / 64 / 4;           // DMA pieces per wave per tile
+    __shared__ u32x4 lk0[UN], lk1[UN], lv0[UK], lv1[UK];
+    typedef __attribute__((address_space(3))) char lds_c;
+    const int L = blockIdx.x, xcd = L & 7, j0 = L >> 3;
+    const int pair = (j0 / n_qblk) * 8 + xcd, qblk = j0 % n_qblk;
+    if (pair >= n_seg * n_head) return;
+    const int seg = pair / n_head, head = pair % n_head;
+    const int64_t qb = q_off[seg], qe = q_off[seg + 1];
+    const int64_t q0 = qb + (int64_t)qblk * 64;
+    if (q0 >= qe) return;                                        // block-uniform
+    const int ks = kv_seg[seg];
+    const int64_t kb = kv_off[ks];
+    const int nk = (int)(kv_off[ks + 1] - kb);
+    const int ntile = (nk + 63) / 64;
+    const int64_t tile0 = (kb / 64 + ks) * n_head + head;
+    const int64_t tile_stride_k = (int64_t)n_head * UN, tile_stride_v = (int64_t)n_head * UN;
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+    const int g = lane >> 4, c = lane & 15;
+    const u32x4* srck = reinterpret_cast<const u32x4*>(imgk) + tile0 * UN + wv * PW * 64 + lane;
+    const u32x4* srcv = reinterpret_cast<const u32x4*>(imgv) + tile0 * UN + wv * PWV * 64 + lane;
+
+    // this lane's query row: q (scaled into the log2 domain), dO, and D = dO . O
+    const int64_t qrow = q0 + wv * 16 + c;
+    const bool qok = qrow < qe;
+    float x[KD][8], y[KD][8];
+    float dpart = 0.f;
+#pragma unroll
+    for (int kd = 0; kd < KD; ++kd) {
+        float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a, da = a, db = a, oa = a, ob = a;
+        if (qok) {
+            const int64_t col = head * DH + 32 * kd + 8 * g;
+            const float4* pq = reinterpret_cast<const float4*>(q + qrow * ld_q + col);
+            const float4* pd = reinterpret_cast<const float4*>(dout + qrow * ld_do + col);
+            const float4* po = reinterpret_cast<const float4*>(o + qrow * ld_o + col);
+            a = pq[0]; b = pq[1]; da = pd[0]; db = pd[1]; oa = po[0]; ob = po[1];
+        }
+        x[kd][0] = a.x; x[kd][1] = a.y; x[kd][2] = a.z; x[kd][3] = a.w;
+        x[kd][4] = b.x; x[kd][5] = b.y; x[kd][6] = b.z; x[kd][7] = b.w;
+        y[kd][0] = da.x; y[kd][1] = da.y; y[kd][2] = da.z; y[kd][3] = da.w;
+        y[kd][4] = db.x; y[kd][5] = db.y; y[kd][6] = db.z; y[kd][7] = db.w;
+        dpart += ((da.x * oa.x + da.y * oa.y) + (da.z * oa.z + da.w * oa.w)) +
+                 ((db.x * ob.x + db.y * ob.y) + (db.z * ob.z + db.w * ob.w));
+    }
+    const float D = xg_sum16(dpart);
+    const float lse2 = qok ? lse_in[qrow * n_head + head] : 0.f;
+    float qm = 0.f, dm = 0.f;
+#pragma unroll
+    for (int kd = 0; kd < KD; ++kd)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            x[kd][e] *= scale_log2;
+            qm = fmaxf(qm, fabsf(x[kd][e]));
+            dm = fmaxf(dm, fabsf(y[kd][e]));
+        }
+    const int eq = range_exp(xg_max16(qm)), edo = range_exp(xg_max16(dm));
+    const float sq = __builtin_ldexpf(1.f, eq), sdo = __builtin_ldexpf(1.f, edo);
+    f16x8 qt[KD][2], dt[KD][2];
+#pragma unroll
+    for (int kd = 0; kd < KD; ++kd)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            _Float16 h, m;
+            split2(x[kd][e] * sq, h, m);
+            qt[kd][0][e] = h; qt[kd][1][e] = m;
+            split2(y[kd][e] * sdo, h, m);
+            dt[kd][0][e] = h; dt[kd][1][e] = m;
+        }
+    f32x4 acc[TD];
+#pragma unroll
+    for (int t = 0; t < TD; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const float one = 1.0f;
+    const uint32_t kaddr = (uint32_t)(g * 64 + c) * 16;
+    const int qq = c >> 2, pp = c & 3;
+    uint32_t vaddr[TD];
+#pragma unroll
+    for (int t = 0; t < TD; ++t)
+        vaddr[t] = unit_v<DH>() * 16 + (4 * g + qq) * (2 * DH) +
+                   (((2 * t + (pp >> 1)) ^ v_swz<DH>(4 * g + qq)) * 16) + (pp & 1) * 8;
+
+    auto dma = [&](int t, auto buf_tag) {
+        constexpr int BUF = decltype(buf_tag)::value;
+        const u32x4* sk = srck + (int64_t)t * tile_stride_k;
+        const u32x4* sv = srcv + (int64_t)t * tile_stride_v;
+        lds_c* dk = (lds_c*)(BUF == 0 ? lk0 : lk1) + wv * PW * 1024;
+        lds_c* dv = (lds_c*)(BUF == 0 ? lv0 : lv1) + wv * PWV * 1024;
+#pragma unroll
+        for (int j = 0; j < PW; ++j)
+            __builtin_amdgcn_global_load_lds((const void*)(sk + j * 64),
+                                             (__attribute__((address_space(3))) void*)(dk + j * 1024), 16, 0, 0);
+#pragma unroll
+        for (int j = 0; j < PWV; ++j)
+            __builtin_amdgcn_global_load_lds((const void*)(sv + j * 64),
+                                             (__attribute__((address_space(3))) void*)(dv + j * 1024), 16, 0, 0);
+    };
+    if (ntile > 0) dma(0, std::integral_constant<int, 0>{});
+
+    auto tile = [&](int tt, auto buf_tag) {
+        constexpr int BUF = decltype(buf_tag)::value;
+        wait_vm_lgkm0_a<0>();
+        __builtin_amdgcn_s_barrier();
+        if (tt + 1 < ntile) dma(tt + 1, std::integral_constant<int, 1 - BUF>{});
+        const int2 ek2 = sck[tile0 + (int64_t)__builtin_amdgcn_readfirstlane(tt) * n_head];
+        const int2 ev2 = scv[tile0 + (int64_t)__builtin_amdgcn_readfirstlane(tt) * n_head];
+        lds_c* const bk = (lds_c*)(BUF == 0 ? lk0 : lk1);
+        lds_c* const bv = (lds_c*)(BUF == 0 ? lv0 : lv1);
+        typedef __attribute__((address_space(3))) u32x4 lds_u4;
+        typedef __attribute__((address_space(3))) s16x4 lds_s4;
+        f32x4 sc4[4], dp4[4];
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+            f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f}, b = a;
+#pragma unroll
+            for (int kd = 0; kd < KD; ++kd) {
+                const int ko = (((kd * 2 + 0) * 4) * 64 + 16 * n) * 16, lo = (((kd * 2 + 1) * 4) * 64 + 16 * n) * 16;
+                const f16x8 kh = __builtin_bit_cast(f16x8, *(lds_u4*)(bk + kaddr + ko));
+                const f16x8 kl = __builtin_bit_cast(f16x8, *(lds_u4*)(bk + kaddr + lo));
+                const f16x8 vh = __builtin_bit_cast(f16x8, *(lds_u4*)(bv + kaddr + ko));
+                const f16x8 vl = __builtin_bit_cast(f16x8, *(lds_u4*)(bv + kaddr + lo));
+                a = __builtin_amdgcn_mfma_f32_16x16x32_f16(kl, qt[kd][0], a, 0, 0, 0);
+                a = __builtin_amdgcn_mfma_f32_16x16x32_f16(kh, qt[kd][1], a, 0, 0, 0);
+                a = __builtin_amdgcn_mfma_f32_16x16x32_f16(kh, qt[kd][0], a, 0, 0, 0);
+                b = __builtin_amdgcn_mfma_f32_16x16x32_f16(vl, dt[kd][0], b, 0, 0, 0);
+                b = __builtin_amdgcn_mfma_f32_16x16x32_f16(vh, dt[kd][1], b, 0, 0, 0);
+                b = __builtin_amdgcn_mfma_f32_16x16x32_f16(vh, dt[kd][0], b, 0, 0, 0);
+            }
+            sc4[n] = a;
+            dp4[n] = b;
+        }
+        const float fs = __builtin_ldexpf(1.f, -(ek2.x + eq));
+        const float fd = __builtin_ldexpf(1.f, -(ev2.x + edo));
+        const int hi = nk - tt * 64;                             // valid keys [0, hi)
+        float ds[16];
+        float dmx = 0.f;
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int kl = 16 * n + 4 * g + r;
+                const float p = kl < hi ? __builtin_amdgcn_exp2f(__builtin_fmaf(sc4[n][r], fs, -lse2)) : 0.f;
+                float dp = dp4[n][r] * fd;
+                if constexpr (DROP) {
+                    const int64_t key = kb + (int64_t)tt * 64 + kl;
+                    dp = attn_drop_hash(drop_seed, head, qrow, key) < drop_thresh ? 0.f : dp * inv_keep;
+                }
+                const float v = p * (dp - D);
+                ds[4 * n + r] = v;
+                dmx = fmaxf(dmx, fabsf(v));
+            }
+        // per (query, tile) power of two bringing dS into fp16's range
+        const int eds = range_exp(xg_max16(dmx));
+        const float sds = __builtin_ldexpf(1.f, eds);
+        f32x4 tmp[TD];
+#pragma unroll
+        for (int t = 0; t < TD; ++t) tmp[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            // dS^T operand of step j (keys 32j + 4g + {0..3}, 32j + 16 + 4g + {0..3})
+            const float pv[8] = {ds[8 * j + 0] * sds, ds[8 * j + 1] * sds, ds[8 * j + 2] * sds, ds[8 * j + 3] * sds,
+                                 ds[8 * j + 4] * sds, ds[8 * j + 5] * sds, ds[8 * j + 6] * sds, ds[8 * j + 7] * sds};
+            u32x4 ph, pl;
+            split8_pk(pv, one, ph, pl);
+            const f16x8 pt0 = __builtin_bit_cast(f16x8, ph), pt1 = __builtin_bit_cast(f16x8, pl);
+#pragma unroll
+            for (int t = 0; t < TD; ++t) {
+                f16x8 vf[2];
+#pragma unroll
+                for (int tm = 0; tm < 2; ++tm) {
+                    lds_c* const vb = bk + vaddr[t] + tm * (128 * DH) + j * 32 * (2 * DH);
+                    const s16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)vb);
+                    const s16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(vb + 16 * (2 * DH)));
+                    vf[tm] = __builtin_bit_cast(f16x8, __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7));
+                }
+                f32x4 a = tmp[t];
+                a = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf[1], pt0, a, 0, 0, 0);
+                a = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf[0], pt1, a, 0, 0, 0);
+                a = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf[0], pt0, a, 0, 0, 0);
+                tmp[t] = a;
+            }
+        }
+        const float fv = __builtin_ldexpf(1.f, -(ek2.y + eds));
+#pragma unroll
+        for (int t = 0; t < TD; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[t][r] = __builtin_fmaf(tmp[t][r], fv, acc[t][r]);
+    };
+    using B0 = std::integral_constant<int, 0>;
+    using B1 = std::integral_constant<int, 1>;
+    int tt = 0;
+    for (; tt + 2 <= ntile; tt += 2) {
+        tile(tt, B0{});
+        tile(tt + 1, B1{});
+    }
+    if (tt < ntile) tile(tt, B0{});
+
+    if (qok) {
+#pragma unroll
+        for (int t = 0; t < TD; ++t) {
+            float4 w;
+            w.x = acc[t][0] * scale; w.y = acc[t][1] * scale;
+            w.z = acc[t][2] * scale; w.w = acc[t][3] * scale;
+            *reinterpret_cast<float4*>(dq + qrow * ld_dq + head * DH + 16 * t + 4 * g) = w;
+        }
+        if (g == 0 && lse_out) {
+            lse_out[qrow * n_head + head] = lse2;
+            dsum_out[qrow * n_head + head] = D;
+        }
+    }
+    // lse2 / D of the block's 64 query rows by query tile for attn_bwd_dkdv_f16x3_kernel (rows
+    // past the segment: lse +inf, D 0, so their P and dS vanish there without a mask)
+    if (lsed_t && g == 0) {
+        float* t = lsed_t + ((qb / 64 + seg + qblk) * n_head + head) * 128 + wv * 16 + c;
+        t[0] = qok ? lse2 : INFINITY;
+        t[64] = qok ? D : 0.f;
+    }
+}
+
+// ---- training: dK / dV of the attention on the f16 matrix cores (f16x3). One block per (key
+// segment, 64-key block, head), 4 waves x 16 keys; over the 64-query tiles of every query
+// segment attending the key segment, with per-query-tile images of Q and dO
+// (attn_kv_image16_kernel: K part for the row products, V part for the transposed ones):
+//   S[query][key]  = Q K^T       A = Q (imgQ, K part), B = K (registers, scaled into the log2
+//                                domain and split once)
+//   dP[query][key] = dO V^T      A = dO (imgD, K part), B = V (registers)
+//   P = exp2(S - lse2), dS = P (dP m - D)   (lse2 / D per query from the dQ kernel's tile array;
+//                                m the dropout mask, 0 or 1 / (1 - p))
+//   dV^T[dh][key] += dO^T (P k)  A = dO (imgD, V part, transposed reads), B = 2^14 P k, k the
+//                                0 / 1 keep mask (1 / (1 - p) applied once at the end)
+//   dK^T[dh][key] += Q^T dS      A = Q (imgQ, V part), B = dS scaled per (key, tile)
+// dK = scale sum dS q, dV = sum P m dO. Per-key lanes: no atomics, each block owns its keys.
+template <int DH, bool DROP>
+__global__ void __launch_bounds__(256, DH == 64 ? 1 : 2)
+attn_bwd_dkdv_f16x3_kernel(const float* __restrict__ k, int64_t ld_k, const float* __restrict__ v,
+                           int64_t ld_v, const uint4* __restrict__ imgq, const int2* __restrict__ scq,
+                           const uint4* __restrict__ imgd, const int2* __restrict__ scd,
+                           const float* __restrict__ lsed_t, float* __restrict__ dk, int64_t ld_dk,
+                           float* __restrict__ dv, int64_t ld_dv, const int64_t* __restrict__ q_off,
+                           const int64_t* __restrict__ kv_off, const int32_t* __restrict__ kv_seg,
+                           int n_head, int n_seg, int n_kv_seg, int n_kblk, float scale,
+                           float scale_log2, uint32_t drop_seed, uint32_t drop_thresh, float inv_keep) {
+    constexpr int KD = DH / 32, TD = DH / 16;
+    constexpr int UN = units<DH>();
+    constexpr int PW = UN / 64 / 4;
+    __shared__ u32x4 lq0[UN], lq1[UN], ld0[UN], ld1[UN];
+    __shared__ u32x4 ls0[32], ls1[32];                           // [lse2 64 | D 64] per tile
+    typedef __attribute__((address_space(3))) char lds_c;
+    const int L = blockIdx.x, xcd = L & 7, j0 = L >> 3;
+    const int pair = (j0 / n_kblk) * 8 + xcd, kblk = j0 % n_kblk;
+    if (pair >= n_kv_seg * n_head) return;
+    const int ks = pair / n_head, head = pair % n_head;
+    const int64_t kb = kv_off[ks], ke = kv_off[ks + 1];
+    const int64_t k0 = kb + (int64_t)kblk * 64;
+    if (k0 >= ke) return;                                        // block-uniform
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+    const int g = lane >> 4, c = lane & 15;
+    const int64_t krow = k0 + wv * 16 + c;
+    const bool kok = krow < ke;
+    float x[KD][8], y[KD][8];
+    float km = 0.f, vm = 0.f;
+#pragma unroll
+    for (int kd = 0; kd < KD; ++kd) {
+        float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a, va = a, vb = a;
+        if (kok) {
+            const int64_t col = head * DH + 32 * kd + 8 * g;
+            const float4* pk = reinterpret_cast<const float4*>(k + krow * ld_k + col);
+            const float4* pv = reinterpret_cast<const float4*>(v + krow * ld_v + col);
+            a = pk[0]; b = pk[1]; va = pv[0]; vb = pv[1];
+        }
+        x[kd][0] = a.x; x[kd][1] = a.y; x[kd][2] = a.z; x[kd][3] = a.w;
+        x[kd][4] = b.x; x[kd][5] = b.y; x[kd][6] = b.z; x[kd][7] = b.w;
+        y[kd][0] = va.x; y[kd][1] = va.y; y[kd][2] = va.z; y[kd][3] = va.w;
+        y[kd][4] = vb.x; y[kd][5] = vb.y; y[kd][6] = vb.z; y[kd][7] = vb.w;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            x[kd][e] *= scale_log2;
+            km = fmaxf(km, fabsf(x[kd][e]));
+            vm = fmaxf(vm, fabsf(y[kd][e]));
+        }
+    }
+    const int ek = range_exp(xg_max16(km)), ev = range_exp(xg_max16(vm));
+    const float sk = __builtin_ldexpf(1.f, ek), sv = __builtin_ldexpf(1.f, ev);
+    f16x8 kt[KD][2], vt[KD][2];
+#pragma unroll
+    for (int kd = 0; kd < KD; ++kd)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            _Float16 h, m;
+            split2(x[kd][e] * sk, h, m);
+            kt[kd][0][e] = h; kt[kd][1][e] = m;
+            split2(y[kd][e] * sv, h, m);
+            vt[kd][0][e] = h; vt[kd][1][e] = m;
+        }
+    f32x4 adk[TD], adv[TD];
+#pragma unroll
+    for (int t = 0; t < TD; ++t) adk[t] = adv[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const float one = 1.0f;
+    const uint32_t kaddr = (uint32_t)(g * 64 + c) * 16;
+    const int qq = c >> 2, pp = c & 3;
+    uint32_t vaddr[TD];
+#pragma unroll
+    for (int t = 0; t < TD; ++t)
+        vaddr[t] = unit_v<DH>() * 16 + (4 * g + qq) * (2 * DH) +
+                   (((2 * t + (pp >> 1)) ^ v_swz<DH>(4 * g + qq)) * 16) + (pp & 1) * 8;
+    typedef __attribute__((address_space(3))) u32x4 lds_u4;
+    typedef __attribute__((address_space(3))) s16x4 lds_s4;
+    typedef __attribute__((address_space(3))) f32x4 lds_v4;
+
+    for (int seg = 0; seg < n_seg; ++seg) {
+        if (kv_seg[seg] != ks) continue;                         // block-uniform
+        const int64_t qb = q_off[seg];
+        const int nq = (int)(q_off[seg + 1] - qb);
+        const int ntile = (nq + 63) / 64;
+        if (ntile == 0) continue;
+        const int64_t tile0 = (qb / 64 + seg) * n_head + head;
+        const int64_t tstride = (int64_t)n_head * UN;
+        const u32x4* srcq = reinterpret_cast<const u32x4*>(imgq) + tile0 * UN + wv * PW * 64 + lane;
+        const u32x4* srcd = reinterpret_cast<const u32x4*>(imgd) + tile0 * UN + wv * PW * 64 + lane;
+        const u32x4* srcl = reinterpret_cast<const u32x4*>(lsed_t) + tile0 * 32 + lane;
+        auto dma = [&](int t, auto buf_tag) {
+            constexpr int BUF = decltype(buf_tag)::value;
+            lds_c* dq_ = (lds_c*)(BUF == 0 ? lq0 : lq1) + wv * PW * 1024;
+            lds_c* dd_ = (lds_c*)(BUF == 0 ? ld0 : ld1) + wv * PW * 1024;
+#pragma unroll
+            for (int j = 0; j < PW; ++j) {
+                __builtin_amdgcn_global_load_lds((const void*)(srcq + t * tstride + j * 64),
+                                                 (__attribute__((address_space(3))) void*)(dq_ + j * 1024), 16, 0, 0);
+                __builtin_amdgcn_global_load_lds((const void*)(srcd + t * tstride + j * 64),
+                                                 (__attribute__((address_space(3))) void*)(dd_ + j * 1024), 16, 0, 0);
+            }
+            if (wv == 0 && lane < 32)
+                __builtin_amdgcn_global_load_lds((const void*)(srcl + (int64_t)t * n_head * 32),
+                                                 (__attribute__((address_space(3))) void*)(BUF == 0 ? ls0 : ls1),
+                                                 16, 0, 0);
+        };
+        __syncthreads();                                         // the previous segment's buffers
+        dma(0, std::integral_constant<int, 0>{});
+
+        auto tile = [&](int tt, auto buf_tag) {
+            constexpr int BUF = decltype(buf_tag)::value;
+            wait_vm_lgkm0_a<0>();
+            __builtin_amdgcn_s_barrier();
+            if (tt + 1 < ntile) dma(tt + 1, std::integral_constant<int, 1 - BUF>{});
+            const int64_t ti = tile0 + (int64_t)__builtin_amdgcn_readfirstlane(tt) * n_head;
+            const int2 eq2 = scq[ti], ed2 = scd[ti];
+            lds_c* const bq = (lds_c*)(BUF == 0 ? lq0 : lq1);
+            lds_c* const bd = (lds_c*)(BUF == 0 ? ld0 : ld1);
+            lds_c* const bl = (lds_c*)(BUF == 0 ? ls0 : ls1);
+            f32x4 s4[4], d4[4];
+#pragma unroll
+            for (int n = 0; n < 4; ++n) {
+                f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f}, b = a;
+#pragma unroll
+                for (int kd = 0; kd < KD; ++kd) {
+                    const int ko = (((kd * 2 + 0) * 4) * 64 + 16 * n) * 16, lo = (((kd * 2 + 1) * 4) * 64 + 16 * n) * 16;
+                    const f16x8 qh = __builtin_bit_cast(f16x8, *(lds_u4*)(bq + kaddr + ko));
+                    const f16x8 ql = __builtin_bit_cast(f16x8, *(lds_u4*)(bq + kaddr + lo));
+                    const f16x8 dh_ = __builtin_bit_cast(f16x8, *(lds_u4*)(bd + kaddr + ko));
+                    const f16x8 dl_ = __builtin_bit_cast(f16x8, *(lds_u4*)(bd + kaddr + lo));
+                    a = __builtin_amdgcn_mfma_f32_16x16x32_f16(ql, kt[kd][0], a, 0, 0, 0);
+                    a = __builtin_amdgcn_mfma_f32_16x16x32_f16(qh, kt[kd][1], a, 0, 0, 0);
+                    a = __builtin_amdgcn_mfma_f32_16x16x32_f16(qh, kt[kd][0], a, 0, 0, 0);
+                    b = __builtin_amdgcn_mfma_f32_16x16x32_f16(dl_, vt[kd][0], b, 0, 0, 0);
+                    b = __builtin_amdgcn_mfma_f32_16x16x32_f16(dh_, vt[kd][1], b, 0, 0, 0);
+                    b = __builtin_amdgcn_mfma_f32_16x16x32_f16(dh_, vt[kd][0], b, 0, 0, 0);
+                }
+                s4[n] = a;
+                d4[n] = b;
+            }
+            const float fs = __builtin_ldexpf(1.f, -(eq2.x + ek));
+            const float fd = __builtin_ldexpf(1.f, -(ed2.x + ev));
+            float pk[16], ds[16];
+            float dmx = 0.f;
+#pragma unroll
+            for (int n = 0; n < 4; ++n) {
+                const f32x4 lv = *(lds_v4*)(bl + (16 * n + 4 * g) * 4);
+                const f32x4 Dv = *(lds_v4*)(bl + 256 + (16 * n + 4 * g) * 4);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s4[n][r], fs, -lv[r]));
+                    float dp = d4[n][r] * fd, pkeep = p;
+                    if constexpr (DROP) {
+                        const int64_t qrow = qb + (int64_t)tt * 64 + 16 * n + 4 * g + r;
+                        const bool drop = attn_drop_hash(drop_seed, head, qrow, krow) < drop_thresh;
+                        dp = drop ? 0.f : dp * inv_keep;
+                        pkeep = drop ? 0.f : p;
+                    }
+                    pk[4 * n + r] = pkeep * 16384.f;
+                    const float d = p * (dp - Dv[r]);
+                    ds[4 * n + r] = d;
+                    dmx = fmaxf(dmx, fabsf(d));
+                }
+            }
+            const int eds = range_exp(xg_max16(dmx));
+            const float sds = __builtin_ldexpf(1.f, eds);
+            f32x4 tv[TD], tk[TD];
+#pragma unroll
+            for (int t = 0; t < TD; ++t) tv[t] = tk[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const float pv[8] = {pk[8 * j + 0], pk[8 * j + 1], pk[8 * j + 2], pk[8 * j + 3],
+                                     pk[8 * j + 4], pk[8 * j + 5], pk[8 * j + 6], pk[8 * j + 7]};
+                const float sv8[8] = {ds[8 * j + 0] * sds, ds[8 * j + 1] * sds, ds[8 * j + 2] * sds, ds[8 * j + 3] * sds,
+                                      ds[8 * j + 4] * sds, ds[8 * j + 5] * sds, ds[8 * j + 6] * sds, ds[8 * j + 7] * sds};
+                u32x4 ph, pl, sh, sl;
+                split8_pk(pv, one, ph, pl);
+                split8_pk(sv8, one, sh, sl);
+                const f16x8 p0 = __builtin_bit_cast(f16x8, ph), p1 = __builtin_bit_cast(f16x8, pl);
+                const f16x8 s0 = __builtin_bit_cast(f16x8, sh), s1 = __builtin_bit_cast(f16x8, sl);
+#pragma unroll
+                for (int t = 0; t < TD; ++t) {
+                    f16x8 of[2], qf[2];
+#pragma unroll
+                    for (int tm = 0; tm < 2; ++tm) {
+                        const uint32_t off = vaddr[t] + tm * (128 * DH) + j * 32 * (2 * DH);
+                        const s16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(bd + off));
+                        const s16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(bd + off + 16 * (2 * DH)));
+                        of[tm] = __builtin_bit_cast(f16x8, __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7));
+                        const s16x4 b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(bq + off));
+                        const s16x4 b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(bq + off + 16 * (2 * DH)));
+                        qf[tm] = __builtin_bit_cast(f16x8, __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7));
+                    }
+                    f32x4 a = tv[t], b = tk[t];
+                    a = __builtin_amdgcn_mfma_f32_16x16x32_f16(of[1], p0, a, 0, 0, 0);
+                    a = __builtin_amdgcn_mfma_f32_16x16x32_f16(of[0], p1, a, 0, 0, 0);
+                    a = __builtin_amdgcn_mfma_f32_16x16x32_f16(of[0], p0, a, 0, 0, 0);
+                    b = __builtin_amdgcn_mfma_f32_16x16x32_f16(qf[1], s0, b, 0, 0, 0);
+                    b = __builtin_amdgcn_mfma_f32_16x16x32_f16(qf[0], s1, b, 0, 0, 0);
+                    b = __builtin_amdgcn_mfma_f32_16x16x32_f16(qf[0], s0, b, 0, 0, 0);
+                    tv[t] = a;
+                    tk[t] = b;
+                }
+            }
+            const float fv = __builtin_ldexpf(1.f, -(ed2.y + 14));
+            const float fk = __builtin_ldexpf(1.f, -(eq2.y + eds));
+#pragma unroll
+            for (int t = 0; t < TD; ++t)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    adv[t][r] = __builtin_fmaf(tv[t][r], fv, adv[t][r]);
+                    adk[t][r] = __builtin_fmaf(tk[t][r], fk, adk[t][r]);
+                }
+        };
+        using B0 = std::integral_constant<int, 0>;
+        using B1 = std::integral_constant<int, 1>;
+        int tt = 0;
+        for (; tt + 2 <= ntile; tt += 2) {
+            tile(tt, B0{});
+            tile(tt + 1, B1{});
+        }
+        if (tt < ntile) tile(tt, B0{});
+    }
+    if (!kok) return;
+    const float fdv = DROP ? inv_keep : 1.f;
+#pragma unroll
+    for (int t = 0; t < TD; ++t) {
+        *reinterpret_cast<float4*>(dk + krow * ld_dk + head * DH + 16 * t + 4 * g) =
+            make_float4(adk[t][0] * scale, adk[t][1] * scale, adk[t][2] * scale, adk[t][3] * scale);
+        *reinterpret_cast<float4*>(dv + krow * ld_dv + head * DH + 16 * t + 4 * g) =
+            make_float4(adv[t][0] * fdv, adv[t][1] * fdv, adv[t][2] * fdv, adv[t][3] * fdv);
+    }
+}
+
 }  // namespace
+
+// fgr_attention_bwd_train on the f16 matrix cores (called from train.hip): the K / V / Q / dO
+// per-tile images, then attn_bwd_dq_f16x3_kernel and (dkdv) attn_bwd_dkdv_f16x3_kernel; without
+// dkdv, lse_out / dsum_out receive the rows' lse2 and D for train.hip's fp32-MFMA dK / dV
+// kernel. q_off and kv_off index one packed row space of n_rows rows (q and kv segments of the
+// same tensors, self- or cross-attention). ws: attn_bwd_f16x3_bytes.
+size_t attn_bwd_f16x3_bytes(int64_t n_rows, int32_t n_seg, int32_t n_head, int32_t dh) {
+    const int64_t nt = n_tiles16(n_rows, n_seg) * n_head;
+    const int un = dh == 32 ? units<32>() : units<64>();
+    return (size_t)4 * (nt * un * 16 + nt * 8) + (size_t)nt * 128 * 4;
+}
+
+int attn_bwd_f16x3(const float* q, int64_t ldq, const float* k, int64_t ldk, const float* v,
+                   int64_t ldv, const float* o, int64_t ldo, const float* dout, int64_t lddo,
+                   float* dq, int64_t lddq, float* dk, int64_t lddk, float* dv, int64_t lddv,
+                   const int64_t* q_off, const int64_t* kv_off, const int32_t* kv_seg,
+                   int32_t n_seg, int32_t n_kv_seg, int64_t n_rows, int64_t max_q_len,
+                   int64_t max_kv_len, int32_t nhead, int32_t dh, float scale, const float* lse_in,
+                   float* lse_out, float* dsum_out, bool dkdv, void* ws, uint32_t drop_seed,
+                   uint32_t drop_thresh, float inv_keep, hipStream_t st) {
+    const int32_t nsm = std::max(n_seg, n_kv_seg);
+    const int64_t nt = n_tiles16(n_rows, nsm) * nhead;
+    const int un = dh == 32 ? units<32>() : units<64>();
+    const int64_t ib = nt * un * 16 + nt * 8;                      // one image + its exponents
+    char* base = static_cast<char*>(ws);
+    auto img = [&](int i) { return reinterpret_cast<uint4*>(base + i * ib); };
+    auto sc = [&](int i) { return reinterpret_cast<int2*>(base + i * ib + nt * un * 16); };
+    float* lsed = reinterpret_cast<float*>(base + 4 * ib);
+    const int n_qblk = (int)ceil_div(max_q_len, 64), n_kblk = (int)ceil_div(max_kv_len, 64);
+    const int64_t n_blocks = ceil_div((int64_t)n_seg * nhead, 8) * 8 * n_qblk;
+    const int64_t n_kblocks = ceil_div((int64_t)n_kv_seg * nhead, 8) * 8 * n_kblk;
+    const float sl2 = scale * 1.4426950408889634f;
+    const bool drop = drop_thresh != 0;
+    ImgJobs jobs{{k, v, q, dout}, {ldk, ldv, ldq, lddo}, {kv_off, kv_off, q_off, q_off},
+                 {img(0), img(1), img(2), img(3)}, {sc(0), sc(1), sc(2), sc(3)},
+                 {n_kv_seg, n_kv_seg, n_seg, n_seg}, nsm};
+    const dim3 igrid((unsigned)ceil_div(std::max(max_q_len, max_kv_len), 64), (unsigned)nhead,
+                     (unsigned)((dkdv ? 4 : 2) * nsm));
+#define FGR_BWD16(D)                                                                                 \
+    hipLaunchKernelGGL(attn_image16_jobs_kernel<D>, igrid, dim3(256), 0, st, jobs);                   \
+    if (drop)                                                                                        \
+        hipLaunchKernelGGL((attn_bwd_dq_f16x3_kernel<D, true>), dim3((unsigned)n_blocks), dim3(256), 0, st, \
+                           q, ldq, dout, lddo, o, ldo, img(0), sc(0), img(1), sc(1), dq, lddq, q_off,   \
+                           kv_off, kv_seg, nhead, n_seg, n_qblk, scale, sl2, lse_in,                  \
+                           dkdv ? nullptr : lse_out, dsum_out, dkdv ? lsed : nullptr, drop_seed,      \
+                           drop_thresh, inv_keep);                                                   \
+    else                                                                                             \
+        hipLaunchKernelGGL((attn_bwd_dq_f16x3_kernel<D, false>), dim3((unsigned)n_blocks), dim3(256), 0, st, \
+                           q, ldq, dout, lddo, o, ldo, img(0), sc(0), img(1), sc(1), dq, lddq, q_off,   \
+                           kv_off, kv_seg, nhead, n_seg, n_qblk, scale, sl2, lse_in,                  \
+                           dkdv ? nullptr : lse_out, dsum_out, dkdv ? lsed : nullptr, drop_seed,      \
+                           drop_thresh, inv_keep);                                                   \
+    if (dkdv) {                                                                                      \
+        if (drop)                                                                                    \
+            hipLaunchKernelGGL((attn_bwd_dkdv_f16x3_kernel<D, true>), dim3((unsigned)n_kblocks), dim3(256), 0, \
+                               st, k, ldk, v, ldv, img(2), sc(2), img(3), sc(3), lsed, dk, lddk, dv,  \
+                               lddv, q_off, kv_off, kv_seg, nhead, n_seg, n_kv_seg, n_kblk, scale,   \
+                               sl2, drop_seed, drop_thresh, inv_keep);                               \
+        else                                                                                         \
+            hipLaunchKernelGGL((attn_bwd_dkdv_f16x3_kernel<D, false>), dim3((unsigned)n_kblocks), dim3(256), 0, \
+                               st, k, ldk, v, ldv, img(2), sc(2), img(3), sc(3), lsed, dk, lddk, dv,  \
+                               lddv, q_off, kv_off, kv_seg, nhead, n_seg, n_kv_seg, n_kblk, scale,   \
+                               sl2, drop_seed, drop_thresh, inv_keep);                               \
+    }
+    if (dh == 32) {
+        FGR_BWD16(32)
+    } else {
+        FGR_BWD16(64)
+    }
+#undef FGR_BWD16
+    FGR_CHECK_LAUNCH("attn_bwd_f16x3");
+    return FGR_OK;
+}
+
 }  // namespace fgr
 
 using namespace fgr;

@@ -175,4 +175,15 @@ __device__ __forceinline__ uint32_t attn_drop_hash(uint32_t seed, int head, int6
     return x ^ (x >> 16);
 }
 
+// attention16.hip: the training attention backward on the f16 matrix cores (fgr_attention_bwd_train)
+size_t attn_bwd_f16x3_bytes(int64_t n_rows, int32_t n_seg, int32_t n_head, int32_t dh);
+int attn_bwd_f16x3(const float* q, int64_t ldq, const float* k, int64_t ldk, const float* v,
+                   int64_t ldv, const float* o, int64_t ldo, const float* dout, int64_t lddo,
+                   float* dq, int64_t lddq, float* dk, int64_t lddk, float* dv, int64_t lddv,
+                   const int64_t* q_off, const int64_t* kv_off, const int32_t* kv_seg,
+                   int32_t n_seg, int32_t n_kv_seg, int64_t n_rows, int64_t max_q_len,
+                   int64_t max_kv_len, int32_t nhead, int32_t dh, float scale, const float* lse_in,
+                   float* lse_out, float* dsum_out, bool dkdv, void* ws, uint32_t drop_seed,
+                   uint32_t drop_thresh, float inv_keep, hipStream_t st);
+
 }  // namespace fgr

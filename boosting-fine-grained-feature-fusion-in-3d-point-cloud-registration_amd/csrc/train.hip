@@ -1730,7 +1730,7 @@ static int attention_bwd_impl(const float* q, int64_t ldq, const float* k, int64
                               int32_t n_kv_seg, int64_t nq, int64_t max_q_len, int64_t max_kv_len,
                               int32_t nhead, int32_t dh, float scale, void* ws, size_t ws_bytes,
                               uint32_t drop_seed, float drop_p, void* stream,
-                              const float* lse_in = nullptr) {
+                              const float* lse_in = nullptr, int64_t n_kv_rows = -1) {
     FGR_REQUIRE(n_seg > 0 && n_kv_seg > 0 && nhead > 0 && nq >= 0 &&
                     (dh == 4 || dh == 8 || dh == 16 || dh == 32 || dh == 64),
                 "fgr_attention_bwd: bad arguments (head dim 4 / 8 / 16 / 32 / 64)");
@@ -1759,6 +1759,37 @@ static int attention_bwd_impl(const float* q, int64_t ldq, const float* k, int64
     const bool mfma = al && !scalar_only && (dh == 16 || dh == 32 || dh == 64);
     FGR_REQUIRE(!drop || (al && (dh == 16 || dh == 32 || dh == 64)),
                 "fgr_attention_bwd_drop: dropout needs head dim 16 / 32 / 64 and 16-B aligned rows");
+    // training with the forward's lse (head dim 32 / 64): the f16x3 kernels (attention16.hip
+    // attn_bwd_f16x3), their K / V / Q / dO images after lse / D in ws
+    // (fgr_attention_bwd_train_workspace). FGR_ATTN_BWD16=0: the fp32-MFMA kernels, =q: only dQ
+    // on the f16 matrix cores (A/B)
+    static const int bwd16 = [] {
+        const char* e = getenv("FGR_ATTN_BWD16");
+        return e && e[0] == '0' ? 0 : e && e[0] == 'q' ? 1 : 2;
+    }();
+    const size_t lse_bytes = (need + 255) & ~(size_t)255;
+    const int64_t n_rows = std::max(nq, n_kv_rows);
+    if (bwd16 && lse_in && n_kv_rows >= 0 && al && (dh == 32 || dh == 64) &&
+        ws_bytes >= lse_bytes + attn_bwd_f16x3_bytes(n_rows, std::max(n_seg, n_kv_seg), nhead, dh)) {
+        FGR_REQUIRE((reinterpret_cast<uintptr_t>(ws) & 15) == 0, "fgr_attention_bwd_train: ws alignment");
+        const bool dkdv16 = bwd16 == 2;
+        const int rc = attn_bwd_f16x3(q, ldq, k, ldk, v, ldv, o, ldo, dout, lddo, dq, lddq, dk, lddk, dv,
+                                      lddv, q_off, kv_off, kv_seg, n_seg, n_kv_seg, n_rows, max_q_len,
+                                      max_kv_len, nhead, dh, scale, lse_in, a.lse, a.dsum, dkdv16,
+                                      static_cast<char*>(ws) + lse_bytes, a.drop_seed,
+                                      a.drop_thresh, a.inv_keep, st);
+        if (rc != FGR_OK || dkdv16) return rc;
+        switch (dh) {
+#define AT16(D) case D: \
+            if (drop) hipLaunchKernelGGL((attn_bwd_dkdv_mfma_kernel<D, true>), g2, dim3(256), 0, st, a); \
+            else hipLaunchKernelGGL((attn_bwd_dkdv_mfma_kernel<D, false>), g2, dim3(256), 0, st, a); \
+            break;
+            AT16(32) AT16(64)
+#undef AT16
+        }
+        FGR_CHECK_LAUNCH("attn_bwd_dkdv_mfma_kernel");
+        return FGR_OK;
+    }
     if (drop) {
         switch (dh) {
 #define ATD(D) case D: \
@@ -1819,12 +1850,30 @@ extern "C" int fgr_attention_bwd_train(const float* q, int64_t ldq, const float*
                                        int64_t nq, int64_t max_q_len, int64_t max_kv_len,
                                        int32_t nhead, int32_t dh, float scale, void* ws,
                                        size_t ws_bytes, uint32_t seed, float p, const float* lse,
-                                       void* stream) {
+                                       int64_t n_kv_rows, void* stream) {
     FGR_REQUIRE(p >= 0.f && p < 1.f, "fgr_attention_bwd_train: dropout p %f not in [0, 1)", p);
     FGR_REQUIRE(lse, "fgr_attention_bwd_train: null lse");
     return attention_bwd_impl(q, ldq, k, ldk, v, ldv, o, ldo, dout, lddo, dq, lddq, dk, lddk, dv,
                               lddv, q_off, kv_off, kv_seg, n_seg, n_kv_seg, nq, max_q_len,
-                              max_kv_len, nhead, dh, scale, ws, ws_bytes, seed, p, stream, lse);
+                              max_kv_len, nhead, dh, scale, ws, ws_bytes, seed, p, stream, lse,
+                              n_kv_rows);
+}
+
+// fgr_attention_bwd_train's workspace: lse / D per (query row, head), then (head dim 32 / 64)
+// the f16x3 kernels' K / V / Q / dO tile images (nq query rows in n_seg segments, n_kv_rows key
+// rows in n_kv_seg segments, one packed row space)
+extern "C" int fgr_attention_bwd_train_workspace(int64_t nq, int32_t n_seg, int64_t n_kv_rows,
+                                                 int32_t n_kv_seg, int32_t nhead, int32_t dh,
+                                                 size_t* bytes) {
+    FGR_REQUIRE(bytes && nq >= 0 && n_seg > 0 && n_kv_rows >= 0 && n_kv_seg > 0 && nhead > 0,
+                "fgr_attention_bwd_train_workspace: bad arguments");
+    size_t need = 0;
+    fgr_attention_bwd_workspace(nq, nhead, &need);
+    *bytes = need;
+    if (dh == 32 || dh == 64)
+        *bytes = ((need + 255) & ~(size_t)255) +
+                 attn_bwd_f16x3_bytes(std::max(nq, n_kv_rows), std::max(n_seg, n_kv_seg), nhead, dh);
+    return FGR_OK;
 }
 
 extern "C" int fgr_attention_bwd_drop(const float* q, int64_t ldq, const float* k, int64_t ldk,

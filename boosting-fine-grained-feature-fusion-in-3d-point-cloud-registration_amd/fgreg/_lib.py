@@ -145,7 +145,8 @@ SIGNATURES = {
                                _i32, _i32, _f32, _vp, _sz, ctypes.c_uint32, _f32, _vp],
     'fgr_attention_bwd_train': [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64,
                                 _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i32, _i32, _i64, _i64, _i64,
-                                _i32, _i32, _f32, _vp, _sz, ctypes.c_uint32, _f32, _vp, _vp],
+                                _i32, _i32, _f32, _vp, _sz, ctypes.c_uint32, _f32, _vp, _i64, _vp],
+    'fgr_attention_bwd_train_workspace': [_i64, _i32, _i64, _i32, _i32, _i32, ctypes.POINTER(_sz)],
     'fgr_crop_max_points': [ctypes.POINTER(_i32)],
     'fgr_crop_pairs_mask': [_vp, _i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     'fgr_crop_pairs_assemble': [_vp, _i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp,

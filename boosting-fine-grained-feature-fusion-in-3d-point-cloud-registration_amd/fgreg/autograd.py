@@ -421,16 +421,21 @@ class _AttentionFn(torch.autograd.Function):
         dqkv = torch.empty_like(qkv)
         L = _lib.load()
         nb = _lib._sz(0)
-        _lib.check(L.fgr_attention_bwd_workspace(n, nhead, nb), 'fgr_attention_bwd_workspace')
-        ws = torch.empty(nb.value, dtype=torch.uint8, device=qkv.device)
-        p, dp, ld = qkv.data_ptr(), dqkv.data_ptr(), qkv.stride(0)
         n_seg = off.numel() - 1
+        if lse is not None:
+            # lse / D and the f16x3 kernels' tile images (fgr_attention_bwd_train)
+            _lib.check(L.fgr_attention_bwd_train_workspace(n, n_seg, n, n_seg, nhead, dh, nb),
+                       'fgr_attention_bwd_train_workspace')
+        else:
+            _lib.check(L.fgr_attention_bwd_workspace(n, nhead, nb), 'fgr_attention_bwd_workspace')
+        ws = ops._workspace(qkv.device, nb.value)
+        p, dp, ld = qkv.data_ptr(), dqkv.data_ptr(), qkv.stride(0)
         args = (p, ld, p + 4 * d, ld, p + 8 * d, ld, _ptr(o), o.stride(0), _ptr(do), do.stride(0),
                 dp, ld, dp + 4 * d, ld, dp + 8 * d, ld, _ptr(off), _ptr(off), _ptr(kv_seg), n_seg,
                 n_seg, n, max_len, max_len, nhead, dh, float(math.sqrt(1.0 / float(dh))),
                 _ptr(ws), nb.value)
         if lse is not None:
-            _lib.check(L.fgr_attention_bwd_train(*args, seed & 0xFFFFFFFF, p_drop, _ptr(lse),
+            _lib.check(L.fgr_attention_bwd_train(*args, seed & 0xFFFFFFFF, p_drop, _ptr(lse), n,
                                                  _stream()), 'fgr_attention_bwd_train')
         elif p_drop > 0.0:
             _lib.check(L.fgr_attention_bwd_drop(*args, seed & 0xFFFFFFFF, p_drop, _stream()),

@@ -667,7 +667,15 @@ int fgr_attention_bwd_train(const float* q, int64_t ldq, const float* k, int64_t
                             const int64_t* kv_off, const int32_t* kv_seg, int32_t n_seg,
                             int32_t n_kv_seg, int64_t nq, int64_t max_q_len, int64_t max_kv_len,
                             int32_t nhead, int32_t dh, float scale, void* ws, size_t ws_bytes,
-                            uint32_t seed, float p, const float* lse, void* stream);
+                            uint32_t seed, float p, const float* lse, int64_t n_kv_rows,
+                            void* stream);
+/* fgr_attention_bwd_train's workspace over nq query rows in n_seg segments and n_kv_rows packed
+ * key rows in n_kv_seg segments: lse / D per (row, head) and, at head dim 32 / 64, the K / V /
+ * Q / dO tile images of the dQ and dK / dV kernels on the f16 matrix cores (split-fp16 x3
+ * products, as fgr_attention_f16x3). A workspace of fgr_attention_bwd_workspace's size runs the
+ * fp32-MFMA kernels instead. */
+int fgr_attention_bwd_train_workspace(int64_t nq, int32_t n_seg, int64_t n_kv_rows,
+                                      int32_t n_kv_seg, int32_t nhead, int32_t dh, size_t* bytes);
 int fgr_attention_bwd_drop(const float* q, int64_t ldq, const float* k, int64_t ldk,
                            const float* v, int64_t ldv, const float* o, int64_t ldo,
                            const float* dout, int64_t lddo, float* dq, int64_t lddq, float* dk,
