@@ -683,6 +683,186 @@ segnorm_bwd_apply4_kernel(SegApply p, const float* __restrict__ dy, const float*
     *reinterpret_cast<float4*>(dx + o) = make_float4(gx[0], gx[1], gx[2], gx[3]);
 }
 
+// ---- the merges folded into the apply passes (segments of at most kSegFuseChunks chunks, e.g.
+// ModelNet's per-cloud InstanceNorms): one block per (chunk, segment, 64 channels) as the
+// statistics pass, whose first 64 threads merge the 64 channels' chunk partials exactly as the
+// merge kernels do (same order, same roundings: bit-identical results) into LDS, then the block
+// applies them to its chunk's rows. The chunk-0 block writes mean / rstd / var (forward) or
+// dgamma / dbeta (backward, segment 0). One launch per norm and direction instead of two.
+constexpr int kSegFuseChunks = 16;
+
+__global__ void __launch_bounds__(256)
+segnorm_merge_apply4_kernel(SegApply p, const double* __restrict__ part, float eps, float* __restrict__ mean,
+                            float* __restrict__ rstd, float* __restrict__ var, float* __restrict__ out) {
+    __shared__ float smu[64], srs[64];
+    const int seg = blockIdx.y, chunk = blockIdx.x;
+    const int C = p.a.c;
+    const int64_t b = p.a.seg_off[seg], e = p.a.seg_off[seg + 1];
+    const int64_t r0 = b + (int64_t)chunk * kRowsChunk;
+    if (r0 >= e && chunk != 0) return;                         // block-uniform
+    const int tid = threadIdx.x;
+    if (tid < 64 && blockIdx.z * 64 + tid < C) {
+        const int ch = blockIdx.z * 64 + tid;
+        const int64_t t = (int64_t)seg * C + ch;
+        float mu = 0.f, rs = 0.f, vr = 0.f;
+        if (e > b) {
+            double s1 = 0.0, s2 = 0.0, n = 0.0;
+#pragma unroll 8
+            for (int k = 0; k < p.a.n_chunks; ++k) {
+                const double* q = part + (((int64_t)seg * p.a.n_chunks + k) * C + ch) * 3;
+                s1 += q[0];
+                s2 += q[1];
+                n += q[2];
+            }
+            const double piv = (double)(p.a.row_div ? p.a.x[b * C + ch] / p.a.row_div[b] : p.a.x[b * C + ch]);
+            const double m1 = s1 / n;
+            const double vv = fmax(s2 / n - m1 * m1, 0.0);
+            mu = (float)(piv + m1);
+            vr = (float)vv;
+            rs = (float)(1.0 / sqrt(vv + (double)eps));
+        }
+        smu[tid] = mu;
+        srs[tid] = rs;
+        if (chunk == 0) {
+            mean[t] = mu;
+            rstd[t] = rs;
+            var[t] = vr;
+        }
+    }
+    __syncthreads();
+    if (r0 >= e) return;
+    const int qd = tid & 15, rg = tid >> 4;
+    const int ch = blockIdx.z * 64 + 4 * qd;
+    if (ch >= C) return;
+    const float ms[4] = {smu[4 * qd], smu[4 * qd + 1], smu[4 * qd + 2], smu[4 * qd + 3]};
+    const float ss[4] = {srs[4 * qd], srs[4 * qd + 1], srs[4 * qd + 2], srs[4 * qd + 3]};
+    float4 gm = make_float4(1.f, 1.f, 1.f, 1.f), bt = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (p.gamma) {
+        gm = ld4(p.gamma + ch);
+        bt = ld4(p.beta + ch);
+    }
+    const float gs[4] = {gm.x, gm.y, gm.z, gm.w}, bs[4] = {bt.x, bt.y, bt.z, bt.w};
+    const int64_t r1 = min(e, r0 + kRowsChunk);
+    for (int64_t r = r0 + rg; r < r1; r += 64) {
+        float4 xv[4], rv[4];
+        float rd[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t rr = min(r + 16 * u, r1 - 1);
+            xv[u] = ld4(p.a.x + rr * C + ch);
+            rd[u] = p.a.row_div ? p.a.row_div[rr] : 1.f;
+            rv[u] = p.residual ? ld4(p.residual + rr * C + ch) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (r + 16 * u >= r1) break;
+            const float xs[4] = {xv[u].x, xv[u].y, xv[u].z, xv[u].w};
+            const float res[4] = {rv[u].x, rv[u].y, rv[u].z, rv[u].w};
+            float y[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float v = p.a.row_div ? xs[j] / rd[u] : xs[j];
+                float z = (v - ms[j]) * ss[j];
+                if (p.gamma) z = z * gs[j] + bs[j];
+                y[j] = act_fwd(z, p.act);
+                if (p.residual) y[j] = act_fwd(y[j] + res[j], p.post_act);
+            }
+            *reinterpret_cast<float4*>(out + (r + 16 * u) * C + ch) = make_float4(y[0], y[1], y[2], y[3]);
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256)
+segnorm_bwd_merge_apply4_kernel(SegApply p, const float* __restrict__ dy, const float* __restrict__ y,
+                                const double* __restrict__ part, float* __restrict__ dgamma,
+                                float* __restrict__ dbeta, float* __restrict__ dx, float* __restrict__ dres) {
+    __shared__ float sm1[64], sm2[64];
+    const int seg = blockIdx.y, chunk = blockIdx.x;
+    const int C = p.a.c;
+    const int64_t b = p.a.seg_off[seg], e = p.a.seg_off[seg + 1];
+    const int64_t r0 = b + (int64_t)chunk * kRowsChunk;
+    const bool gblock = dgamma && seg == 0 && chunk == 0;
+    if (r0 >= e && !gblock) return;                            // block-uniform
+    const int tid = threadIdx.x;
+    if (tid < 64 && blockIdx.z * 64 + tid < C) {
+        const int ch = blockIdx.z * 64 + tid;
+        double s1 = 0.0, s2 = 0.0;
+#pragma unroll 8
+        for (int k = 0; k < p.a.n_chunks; ++k) {
+            const double* q = part + (((int64_t)seg * p.a.n_chunks + k) * C + ch) * 2;
+            s1 += q[0];
+            s2 += q[1];
+        }
+        sm1[tid] = (float)s1;
+        sm2[tid] = (float)s2;
+        if (gblock) {
+            double g1 = 0.0, g2 = 0.0;
+            for (int sg = 0; sg < p.a.n_seg; ++sg)
+#pragma unroll 8
+                for (int k = 0; k < p.a.n_chunks; ++k) {
+                    const double* q = part + (((int64_t)sg * p.a.n_chunks + k) * C + ch) * 2;
+                    g1 += q[0];
+                    g2 += q[1];
+                }
+            dbeta[ch] = (float)g1;
+            dgamma[ch] = (float)g2;
+        }
+    }
+    __syncthreads();
+    if (r0 >= e) return;
+    const int qd = tid & 15, rg = tid >> 4;
+    const int ch = blockIdx.z * 64 + 4 * qd;
+    if (ch >= C) return;
+    const int64_t sc = (int64_t)seg * C + ch;
+    const float inv_n = 1.0f / (float)(e - b);
+    const float4 mu4 = ld4(p.mean + sc), rs4 = ld4(p.rstd + sc);
+    float4 g4 = make_float4(1.f, 1.f, 1.f, 1.f), b4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (p.gamma) {
+        g4 = ld4(p.gamma + ch);
+        b4 = ld4(p.beta + ch);
+    }
+    const float mu[4] = {mu4.x, mu4.y, mu4.z, mu4.w}, rs[4] = {rs4.x, rs4.y, rs4.z, rs4.w};
+    const float gg[4] = {g4.x, g4.y, g4.z, g4.w}, bb[4] = {b4.x, b4.y, b4.z, b4.w};
+    const float m1s[4] = {sm1[4 * qd], sm1[4 * qd + 1], sm1[4 * qd + 2], sm1[4 * qd + 3]};
+    const float m2s[4] = {sm2[4 * qd], sm2[4 * qd + 1], sm2[4 * qd + 2], sm2[4 * qd + 3]};
+    const int64_t r1 = min(e, r0 + kRowsChunk);
+    for (int64_t r = r0 + rg; r < r1; r += 64) {
+        float4 xv[4], dv[4], yv[4];
+        float rdv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t rr = min(r + 16 * u, r1 - 1);
+            const int64_t o = rr * C + ch;
+            xv[u] = ld4(p.a.x + o);
+            dv[u] = ld4(dy + o);
+            yv[u] = p.residual ? ld4(y + o) : make_float4(0.f, 0.f, 0.f, 0.f);
+            rdv[u] = p.a.row_div ? p.a.row_div[rr] : 1.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (r + 16 * u >= r1) break;
+            const int64_t o = (r + 16 * u) * C + ch;
+            const float xs[4] = {xv[u].x, xv[u].y, xv[u].z, xv[u].w}, ds[4] = {dv[u].x, dv[u].y, dv[u].z, dv[u].w};
+            const float ys[4] = {yv[u].x, yv[u].y, yv[u].z, yv[u].w};
+            const float rd = rdv[u];
+            float gx[4], gres[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float v = xs[j] / rd;
+                const float xh = (v - mu[j]) * rs[j];
+                float gr = ds[j];
+                if (p.residual) gr *= act_grad(ys[j], p.post_act);
+                gres[j] = gr;
+                const float dz = gr * act_grad(xh * gg[j] + bb[j], p.act);
+                const float m1 = m1s[j] * inv_n, m2 = m2s[j] * inv_n;
+                gx[j] = rs[j] * gg[j] * (dz - m1 - xh * m2) / rd;
+            }
+            if (dres) *reinterpret_cast<float4*>(dres + o) = make_float4(gres[0], gres[1], gres[2], gres[3]);
+            *reinterpret_cast<float4*>(dx + o) = make_float4(gx[0], gx[1], gx[2], gx[3]);
+        }
+    }
+}
+
 // ---- LayerNorm backward ------------------------------------------------------------------
 // One wave per row (PER = d / 64 columns per lane), rows r = block * 64 + wave + 4 i; the
 // wave's lanes keep the column partials of dy * xhat and dy over its rows, merged per block
@@ -1601,6 +1781,24 @@ extern "C" int fgr_segnorm_fwd(const float* x, int64_t n, int32_t c, const int64
                                const float* beta, int32_t act, const float* residual,
                                int32_t post_act, float* out, void* ws, size_t ws_bytes,
                                void* stream) {
+    static const bool fuse = [] { const char* e = getenv("FGR_SEG_FUSED"); return !(e && e[0] == '0'); }();
+    if (fuse && n > 0 && c > 0 && n_seg > 0 && max_seg_len > 0 && seg_chunks(max_seg_len) <= kSegFuseChunks &&
+        x && seg_off && mean && rstd && var && out && ws &&
+        seg_vec_ok(n, c, {x, out, residual, mean, rstd, gamma, beta}) && (!gamma == !beta)) {
+        size_t need = 0;
+        fgr_segnorm_workspace(max_seg_len, c, n_seg, &need);
+        FGR_REQUIRE(ws_bytes >= need, "fgr_segnorm_fwd: workspace too small");
+        SegApply p{{x, row_div, seg_off, n_seg, c, seg_chunks(max_seg_len)}, n, mean, rstd, gamma, beta, act,
+                   residual, post_act};
+        hipStream_t st = as_stream(stream);
+        const dim3 grid(p.a.n_chunks, n_seg, (unsigned)ceil_div(c, 64));
+        hipLaunchKernelGGL(segnorm_stats4_kernel, grid, dim3(256), 0, st, p.a, (double*)ws);
+        FGR_CHECK_LAUNCH("segnorm_stats4_kernel");
+        hipLaunchKernelGGL(segnorm_merge_apply4_kernel, grid, dim3(256), 0, st, p, (const double*)ws, eps,
+                           mean, rstd, var, out);
+        FGR_CHECK_LAUNCH("segnorm_merge_apply4_kernel");
+        return FGR_OK;
+    }
     const int rc = fgr_segnorm_stats(x, n, c, seg_off, n_seg, max_seg_len, row_div, eps, mean, rstd,
                                      var, ws, ws_bytes, stream);
     if (rc != FGR_OK) return rc;
@@ -1632,6 +1830,16 @@ extern "C" int fgr_segnorm_bwd(const float* x, int64_t n, int32_t c, const int64
     hipStream_t st = as_stream(stream);
     const bool vec = seg_vec_ok(n, c, {x, dy, has_residual ? y : nullptr, dx, has_residual ? dres : nullptr,
                                        mean, rstd, gamma, beta, sums});
+    static const bool fuse = [] { const char* e = getenv("FGR_SEG_FUSED"); return !(e && e[0] == '0'); }();
+    if (fuse && vec && n > 0 && nch <= kSegFuseChunks) {
+        const dim3 grid(nch, n_seg, (unsigned)ceil_div(c, 64));
+        hipLaunchKernelGGL(segnorm_bwd_stats4_kernel, grid, dim3(256), 0, st, p, dy, y, part);
+        FGR_CHECK_LAUNCH("segnorm_bwd_stats4_kernel");
+        hipLaunchKernelGGL(segnorm_bwd_merge_apply4_kernel, grid, dim3(256), 0, st, p, dy, y,
+                           (const double*)part, dgamma, dbeta, dx, has_residual ? dres : nullptr);
+        FGR_CHECK_LAUNCH("segnorm_bwd_merge_apply4_kernel");
+        return FGR_OK;
+    }
     if (vec)
         hipLaunchKernelGGL(segnorm_bwd_stats4_kernel, dim3(nch, n_seg, (unsigned)ceil_div(c, 64)), dim3(256),
                            0, st, p, dy, y, part);

@@ -189,6 +189,27 @@ def test_segnorm_backward(gpu, case, c):
         assert rel_err(r.grad, r64.grad) < 1e-5
 
 
+def test_segnorm_fused_bit_identical(gpu, tmp_path):
+    """The fused merge + apply kernels (segments of <= 16 chunks: one launch per direction
+    fewer) give bit-identical outputs and gradients to the separate merge kernels
+    (FGR_SEG_FUSED=0 in a subprocess): InstanceNorm with row divisor + residual, BatchNorm
+    with gamma / beta."""
+    import os
+    import subprocess
+    import sys
+    sys.path.insert(0, os.path.dirname(__file__))
+    import _segnorm_dump
+    here = _segnorm_dump.run(gpu)
+    f = tmp_path / 'unfused.npz'
+    env = dict(os.environ, FGR_SEG_FUSED='0')
+    subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), '_segnorm_dump.py'), str(f)],
+                   env=env, check=True, timeout=240)
+    ref = np.load(f)
+    assert sorted(ref.files) == sorted(here)
+    for k in ref.files:
+        assert np.array_equal(ref[k], here[k]), k
+
+
 def test_batchnorm_running_stats(gpu):
     """batchnorm_t updates running_mean / running_var / num_batches_tracked like
     nn.BatchNorm1d.train() (momentum, unbiased variance)."""
