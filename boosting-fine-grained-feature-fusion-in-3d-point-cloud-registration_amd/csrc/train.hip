@@ -689,18 +689,38 @@ segnorm_bwd_apply4_kernel(SegApply p, const float* __restrict__ dy, const float*
 // merge kernels do (same order, same roundings: bit-identical results) into LDS, then the block
 // applies them to its chunk's rows. The chunk-0 block writes mean / rstd / var (forward) or
 // dgamma / dbeta (backward, segment 0). One launch per norm and direction instead of two.
-constexpr int kSegFuseChunks = 16;
+constexpr int kSegFuseChunks = 16;          // up to here the merge order of the merge kernels
+constexpr int kSegFuseChunksMax = 64;       // beyond: the separate merge kernels
 
 __global__ void __launch_bounds__(256)
 segnorm_merge_apply4_kernel(SegApply p, const double* __restrict__ part, float eps, float* __restrict__ mean,
                             float* __restrict__ rstd, float* __restrict__ var, float* __restrict__ out) {
     __shared__ float smu[64], srs[64];
+    __shared__ double sred[3][3][64];
     const int seg = blockIdx.y, chunk = blockIdx.x;
     const int C = p.a.c;
     const int64_t b = p.a.seg_off[seg], e = p.a.seg_off[seg + 1];
     const int64_t r0 = b + (int64_t)chunk * kRowsChunk;
     if (r0 >= e && chunk != 0) return;                         // block-uniform
     const int tid = threadIdx.x;
+    // more than kSegFuseChunks chunks (the BatchNorms over every row): the four waves sum the
+    // chunks congruent to their index mod 4, combined in wave order
+    const bool split4 = p.a.n_chunks > kSegFuseChunks;
+    if (split4 && tid >= 64 && blockIdx.z * 64 + (tid & 63) < C) {
+        const int ch = blockIdx.z * 64 + (tid & 63), w = tid >> 6;
+        double s1 = 0.0, s2 = 0.0, n = 0.0;
+#pragma unroll 4
+        for (int k = w; k < p.a.n_chunks; k += 4) {
+            const double* q = part + (((int64_t)seg * p.a.n_chunks + k) * C + ch) * 3;
+            s1 += q[0];
+            s2 += q[1];
+            n += q[2];
+        }
+        sred[w - 1][0][tid & 63] = s1;
+        sred[w - 1][1][tid & 63] = s2;
+        sred[w - 1][2][tid & 63] = n;
+    }
+    if (split4) __syncthreads();
     if (tid < 64 && blockIdx.z * 64 + tid < C) {
         const int ch = blockIdx.z * 64 + tid;
         const int64_t t = (int64_t)seg * C + ch;
@@ -708,12 +728,18 @@ segnorm_merge_apply4_kernel(SegApply p, const double* __restrict__ part, float e
         if (e > b) {
             double s1 = 0.0, s2 = 0.0, n = 0.0;
 #pragma unroll 8
-            for (int k = 0; k < p.a.n_chunks; ++k) {
+            for (int k = 0; k < p.a.n_chunks; k += split4 ? 4 : 1) {
                 const double* q = part + (((int64_t)seg * p.a.n_chunks + k) * C + ch) * 3;
                 s1 += q[0];
                 s2 += q[1];
                 n += q[2];
             }
+            if (split4)
+                for (int w = 0; w < 3; ++w) {
+                    s1 += sred[w][0][tid];
+                    s2 += sred[w][1][tid];
+                    n += sred[w][2][tid];
+                }
             const double piv = (double)(p.a.row_div ? p.a.x[b * C + ch] / p.a.row_div[b] : p.a.x[b * C + ch]);
             const double m1 = s1 / n;
             const double vv = fmax(s2 / n - m1 * m1, 0.0);
@@ -777,6 +803,7 @@ segnorm_bwd_merge_apply4_kernel(SegApply p, const float* __restrict__ dy, const 
                                 const double* __restrict__ part, float* __restrict__ dgamma,
                                 float* __restrict__ dbeta, float* __restrict__ dx, float* __restrict__ dres) {
     __shared__ float sm1[64], sm2[64];
+    __shared__ double sred[3][2][64];
     const int seg = blockIdx.y, chunk = blockIdx.x;
     const int C = p.a.c;
     const int64_t b = p.a.seg_off[seg], e = p.a.seg_off[seg + 1];
@@ -784,15 +811,34 @@ segnorm_bwd_merge_apply4_kernel(SegApply p, const float* __restrict__ dy, const 
     const bool gblock = dgamma && seg == 0 && chunk == 0;
     if (r0 >= e && !gblock) return;                            // block-uniform
     const int tid = threadIdx.x;
-    if (tid < 64 && blockIdx.z * 64 + tid < C) {
-        const int ch = blockIdx.z * 64 + tid;
+    const bool split4 = p.a.n_chunks > kSegFuseChunks;         // as the forward
+    if (split4 && tid >= 64 && blockIdx.z * 64 + (tid & 63) < C) {
+        const int ch = blockIdx.z * 64 + (tid & 63), w = tid >> 6;
         double s1 = 0.0, s2 = 0.0;
-#pragma unroll 8
-        for (int k = 0; k < p.a.n_chunks; ++k) {
+#pragma unroll 4
+        for (int k = w; k < p.a.n_chunks; k += 4) {
             const double* q = part + (((int64_t)seg * p.a.n_chunks + k) * C + ch) * 2;
             s1 += q[0];
             s2 += q[1];
         }
+        sred[w - 1][0][tid & 63] = s1;
+        sred[w - 1][1][tid & 63] = s2;
+    }
+    if (split4) __syncthreads();
+    if (tid < 64 && blockIdx.z * 64 + tid < C) {
+        const int ch = blockIdx.z * 64 + tid;
+        double s1 = 0.0, s2 = 0.0;
+#pragma unroll 8
+        for (int k = 0; k < p.a.n_chunks; k += split4 ? 4 : 1) {
+            const double* q = part + (((int64_t)seg * p.a.n_chunks + k) * C + ch) * 2;
+            s1 += q[0];
+            s2 += q[1];
+        }
+        if (split4)
+            for (int w = 0; w < 3; ++w) {
+                s1 += sred[w][0][tid];
+                s2 += sred[w][1][tid];
+            }
         sm1[tid] = (float)s1;
         sm2[tid] = (float)s2;
         if (gblock) {
@@ -1782,7 +1828,7 @@ extern "C" int fgr_segnorm_fwd(const float* x, int64_t n, int32_t c, const int64
                                int32_t post_act, float* out, void* ws, size_t ws_bytes,
                                void* stream) {
     static const bool fuse = [] { const char* e = getenv("FGR_SEG_FUSED"); return !(e && e[0] == '0'); }();
-    if (fuse && n > 0 && c > 0 && n_seg > 0 && max_seg_len > 0 && seg_chunks(max_seg_len) <= kSegFuseChunks &&
+    if (fuse && n > 0 && c > 0 && n_seg > 0 && max_seg_len > 0 && seg_chunks(max_seg_len) <= kSegFuseChunksMax &&
         x && seg_off && mean && rstd && var && out && ws &&
         seg_vec_ok(n, c, {x, out, residual, mean, rstd, gamma, beta}) && (!gamma == !beta)) {
         size_t need = 0;
@@ -1831,7 +1877,7 @@ extern "C" int fgr_segnorm_bwd(const float* x, int64_t n, int32_t c, const int64
     const bool vec = seg_vec_ok(n, c, {x, dy, has_residual ? y : nullptr, dx, has_residual ? dres : nullptr,
                                        mean, rstd, gamma, beta, sums});
     static const bool fuse = [] { const char* e = getenv("FGR_SEG_FUSED"); return !(e && e[0] == '0'); }();
-    if (fuse && vec && n > 0 && nch <= kSegFuseChunks) {
+    if (fuse && vec && n > 0 && nch <= kSegFuseChunksMax) {
         const dim3 grid(nch, n_seg, (unsigned)ceil_div(c, 64));
         hipLaunchKernelGGL(segnorm_bwd_stats4_kernel, grid, dim3(256), 0, st, p, dy, y, part);
         FGR_CHECK_LAUNCH("segnorm_bwd_stats4_kernel");

@@ -148,19 +148,21 @@ def _segnorm_ref(x, lens, row_div, gamma, beta, act, residual, post, eps=1e-5):
 
 
 @pytest.mark.parametrize('case', ['instnorm', 'instnorm_rowdiv_leaky', 'instnorm_residual',
-                                  'batchnorm_relu', 'batchnorm_residual_relu', 'long_segments'])
+                                  'batchnorm_relu', 'batchnorm_residual_relu', 'long_segments',
+                                  'batchnorm_large'])
 @pytest.mark.parametrize('c', [72, 70])
 def test_segnorm_backward(gpu, case, c):
     """segnorm_t: InstanceNorm per cloud (with the KPConv row divisor, LeakyReLU, the
     bottleneck's residual + LeakyReLU) and training BatchNorm (one segment, affine, ReLU,
     residual + ReLU) vs the same formulas in fp64; c = 72 runs the float4 kernels, 70 the
-    scalar ones."""
+    scalar ones. Chunks of 256 rows per segment: <= 16 (merge fused in order), 47
+    (batchnorm_large: the fused four-way merge), 79 (long_segments: separate merges)."""
     from fgreg import ops
     from fgreg.autograd import segnorm_t
     g = torch.Generator().manual_seed(len(case))
     lens = [700, 300, 1, 513] if case != 'long_segments' else [20000, 9000]
     if case.startswith('batchnorm'):
-        lens = [sum(lens)]
+        lens = [sum(lens)] if case != 'batchnorm_large' else [12000]
     n = sum(lens)
     x, x64 = _leaf(torch.randn(n, c, generator=g) * 3 + 5, gpu)
     rd = (1 + torch.randint(0, 9, (n,), generator=g)).float() if 'rowdiv' in case else None
@@ -170,7 +172,8 @@ def test_segnorm_backward(gpu, case, c):
     res = 'residual' in case
     r, r64 = _leaf(torch.randn(n, c, generator=g), gpu) if res else (None, None)
     act = {'instnorm': 'none', 'instnorm_rowdiv_leaky': 'leaky', 'instnorm_residual': 'none',
-           'batchnorm_relu': 'relu', 'batchnorm_residual_relu': 'none', 'long_segments': 'leaky'}[case]
+           'batchnorm_relu': 'relu', 'batchnorm_residual_relu': 'none', 'long_segments': 'leaky',
+           'batchnorm_large': 'relu'}[case]
     post = 'relu' if case == 'batchnorm_residual_relu' else 'leaky'
     A = {'none': ops.ACT_NONE, 'relu': ops.ACT_RELU, 'leaky': ops.ACT_LEAKY}
     off = ops.offsets(lens, gpu)

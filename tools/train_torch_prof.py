@@ -22,11 +22,22 @@ def main():
     bench.main()
     fn = steps['fn']
     from torch.profiler import ProfilerActivity, profile
-    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
         for _ in range(2):
             fn()
         torch.cuda.synchronize()
     text = prof.key_averages().table(sort_by='count', row_limit=60)
+    # where the elementwise ops come from (top Python frames of each call site)
+    keep = ('aten::add', 'aten::add_', 'aten::mul', 'aten::copy_', 'aten::cat', 'aten::fill_',
+            'aten::zero_', 'aten::div', 'aten::sub')
+    rows = [e for e in prof.key_averages(group_by_stack_n=6) if e.key in keep]
+    rows.sort(key=lambda e: -e.count)
+    lines = []
+    for e in rows[:40]:
+        lines.append(f'{e.count:6d}  {e.key}')
+        for fr in e.stack[:6]:
+            lines.append(f'          {fr}')
+    text += '\n\n' + '\n'.join(lines)
     if out:
         with open(out, 'w') as f:
             f.write(text)
