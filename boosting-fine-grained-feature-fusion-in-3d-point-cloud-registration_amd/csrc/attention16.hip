@@ -84,7 +84,7 @@ __device__ __forceinline__ void kv_image16(const float* __restrict__ k, int64_t 
                                            const float* __restrict__ v, int64_t ld_v,
                                            const int64_t* __restrict__ kv_off, int n_head,
                                            uint4* __restrict__ img, int2* __restrict__ sc, int s,
-                                           int h, int tt) {
+                                           int h, int tt, bool v_part = true) {
     constexpr int NF = DH / 16;                                  // float4s per thread
     constexpr int RU = DH / 4;                                   // float4s per key row
     const int64_t kb = kv_off[s];
@@ -141,9 +141,10 @@ __device__ __forceinline__ void kv_image16(const float* __restrict__ k, int64_t 
         for (int t = 0; t < 2; ++t) {
             *reinterpret_cast<uint2*>(base + (((ks * 2 + t) * 4 + g) * 64 + key) * 16 + half * 8) =
                 *reinterpret_cast<const uint2*>(kt[t]);
-            *reinterpret_cast<uint2*>(base + unit_v<DH>() * 16 + t * (128 * DH) + key * (2 * DH) +
-                                      vch * 16 + half * 8) =
-                *reinterpret_cast<const uint2*>(vt[t]);
+            if (v_part)
+                *reinterpret_cast<uint2*>(base + unit_v<DH>() * 16 + t * (128 * DH) + key * (2 * DH) +
+                                          vch * 16 + half * 8) =
+                    *reinterpret_cast<const uint2*>(vt[t]);
         }
     }
 }
@@ -165,6 +166,7 @@ struct ImgJobs {
     uint4* img[4];
     int2* sc[4];
     int n_seg[4];
+    int v_part[4];                   // 0: only the K part is read (the dQ kernel's V image)
     int max_seg;
 };
 
@@ -173,7 +175,7 @@ __global__ void __launch_bounds__(256) attn_image16_jobs_kernel(ImgJobs j) {
     const int job = blockIdx.z / j.max_seg, s = blockIdx.z % j.max_seg;
     if (s >= j.n_seg[job]) return;
     kv_image16<DH>(j.src[job], j.ld[job], j.src[job], j.ld[job], j.off[job], (int)gridDim.y,
-                   j.img[job], j.sc[job], s, blockIdx.y, blockIdx.x);
+                   j.img[job], j.sc[job], s, blockIdx.y, blockIdx.x, j.v_part[job] != 0);
 }
 
 template <int N>
@@ -1007,7 +1009,7 @@ int attn_bwd_f16x3(const float* q, int64_t ldq, const float* k, int64_t ldk, con
     const bool drop = drop_thresh != 0;
     ImgJobs jobs{{k, v, q, dout}, {ldk, ldv, ldq, lddo}, {kv_off, kv_off, q_off, q_off},
                  {img(0), img(1), img(2), img(3)}, {sc(0), sc(1), sc(2), sc(3)},
-                 {n_kv_seg, n_kv_seg, n_seg, n_seg}, nsm};
+                 {n_kv_seg, n_kv_seg, n_seg, n_seg}, {1, 0, 1, 1}, nsm};
     const dim3 igrid((unsigned)ceil_div(std::max(max_q_len, max_kv_len), 64), (unsigned)nhead,
                      (unsigned)((dkdv ? 4 : 2) * nsm));
 #define FGR_BWD16(D)                                                                                 \
