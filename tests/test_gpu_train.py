@@ -271,17 +271,21 @@ def _attn_ref(qkv, lens, kv_seg, nhead):
     return torch.cat(outs, 0)
 
 
+_KV_SEG = {'self': [0, 1, 2, 3], 'cross': [2, 3, 0, 1], 'shared': [3, 3, 0, 0]}
+
+
 @pytest.mark.parametrize('d,nhead', [(32, 8), (256, 8), (512, 8)])
-@pytest.mark.parametrize('kind', ['self', 'cross'])
+@pytest.mark.parametrize('kind', ['self', 'cross', 'shared'])
 def test_attention_backward(gpu, d, nhead, kind):
-    """attention_t (fused QKV; self = every cloud to itself, cross = cloud c to (c + B) mod 2B)
-    vs fp64 softmax attention: dq, dk, dv through fgr_attention_bwd, unequal lengths incl. a
-    1-row cloud and clouds past one 64-row tile."""
+    """attention_t (fused QKV; self = every cloud to itself, cross = cloud c to (c + B) mod 2B,
+    shared = two query clouds on one key cloud: its dK / dV sum over both) vs fp64 softmax
+    attention: dq, dk, dv through fgr_attention_bwd (head dim 4) / fgr_attention_bwd_train
+    (head dims 32 / 64: the f16x3 kernels), unequal lengths incl. a 1-row cloud and clouds past
+    one 64-row tile."""
     from fgreg import ops
     from fgreg.autograd import attention_t
     lens = [130, 1, 65, 300]
-    B = len(lens) // 2
-    kv_seg = list(range(4)) if kind == 'self' else [(c + B) % 4 for c in range(4)]
+    kv_seg = _KV_SEG[kind]
     g = torch.Generator().manual_seed(d)
     qkv, qkv64 = _leaf(torch.randn(sum(lens), 3 * d, generator=g), gpu)
     off = ops.offsets(lens, gpu)
@@ -318,7 +322,7 @@ def _attn_ref_drop(qkv, lens, kv_seg, nhead, seed, p):
 
 
 @pytest.mark.parametrize('d,nhead', [(256, 8), (512, 8)])
-@pytest.mark.parametrize('kind', ['self', 'cross'])
+@pytest.mark.parametrize('kind', ['self', 'cross', 'shared'])
 def test_attention_dropout_forward_backward(gpu, d, nhead, kind):
     """Training-mode attention-weight dropout (nn.MultiheadAttention(dropout=p),
     transformers.py:95-96): fgr_attention_f16x3_drop / fgr_attention_bwd_drop against fp64
@@ -327,8 +331,7 @@ def test_attention_dropout_forward_backward(gpu, d, nhead, kind):
     from fgreg import ops
     from fgreg.autograd import _AttentionFn, attn_drop_mask
     lens = [130, 1, 65, 300]
-    B = len(lens) // 2
-    kv_seg = list(range(4)) if kind == 'self' else [(c + B) % 4 for c in range(4)]
+    kv_seg = _KV_SEG[kind]
     g = torch.Generator().manual_seed(d + 7)
     qkv, qkv64 = _leaf(torch.randn(sum(lens), 3 * d, generator=g), gpu)
     off = ops.offsets(lens, gpu)
