@@ -105,7 +105,15 @@ def _end(name, start, work=None):
         TIMER.end(name, start, work)
 
 
+# the current stream's raw handle without building a torch.cuda.Stream object per launch (the
+# eager training step calls this ~1500 times)
+_raw_stream = getattr(torch._C, '_cuda_getCurrentRawStream', None)
+_cur_dev = getattr(torch._C, '_cuda_getDevice', None)
+
+
 def _stream():
+    if _raw_stream is not None:
+        return _raw_stream(_cur_dev())
     return torch.cuda.current_stream().cuda_stream
 
 
@@ -717,7 +725,8 @@ def _workspace(device, nbytes):
     scope's own (each captured graph has one)."""
     if _WS_SCOPE is not None:
         return _WS_SCOPE.get(device, nbytes)
-    key = (device, torch.cuda.current_stream(device).cuda_stream)
+    key = (device, _raw_stream(device.index) if _raw_stream is not None and device.index is not None
+           else torch.cuda.current_stream(device).cuda_stream)
     buf = _WS.get(key)
     if buf is None or buf.numel() < nbytes:
         if buf is not None:
