@@ -106,8 +106,9 @@ def _end(name, start, work=None):
 
 
 # the current stream's raw handle without building a torch.cuda.Stream object per launch (the
-# eager training step calls this ~1500 times)
-_raw_stream = getattr(torch._C, '_cuda_getCurrentRawStream', None)
+# eager training step calls this ~1500 times; FGREG_RAW_STREAM=0: torch.cuda.current_stream, A/B)
+_raw_stream = (getattr(torch._C, '_cuda_getCurrentRawStream', None)
+               if os.environ.get('FGREG_RAW_STREAM', '1') != '0' else None)
 _cur_dev = getattr(torch._C, '_cuda_getDevice', None)
 
 
