@@ -1283,6 +1283,11 @@ char h3_tile_kloop(int m, int n, int k) {
     // very few tiles with a long K (3DMatch's 2120 x 256 x 3840, 2120 x 128 x 1920 KPConv
     // products): split-K over 64 x 64 tiles (h3_ksplit; profiles/r02_gemm_splitk_sweep.txt)
     if (g5ok && splitk_shape(m, n, k)) return k >= 2048 ? 'X' : 'W';
+    // short row counts with a long contraction and wide outputs (3DMatch's 2120 x 1024 x 2048
+    // KPConv product): the 64 x 64 staged g5 'X' -- 82.0 -> 51.4 us in the forward
+    // (profiles/r05_gemm_longk_ab.txt; 'Y' before). FGR_GEMM_LONGK=0: the old choice (A/B)
+    static const bool longk = [] { const char* e = getenv("FGR_GEMM_LONGK"); return !(e && e[0] == '0'); }();
+    if (longk && g5ok && m <= 4096 && k >= 2048 && n >= 512) return 'X';
     if (g5ok && tiles64 <= 400 && k >= 512 && n >= 32)
         return (k >= 2048 || n <= 64) ? 'S' : ((n <= 128 && k >= 1024 && tiles64 > 256) ? 'T' : 'W');
     if (g5ok && m <= 4096)
