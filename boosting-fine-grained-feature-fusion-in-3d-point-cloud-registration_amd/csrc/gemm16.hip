@@ -1288,8 +1288,10 @@ char h3_tile_kloop(int m, int n, int k) {
     // (profiles/r05_gemm_longk_ab.txt; 'Y' before). FGR_GEMM_LONGK=0: the old choice (A/B)
     static const bool longk = [] { const char* e = getenv("FGR_GEMM_LONGK"); return !(e && e[0] == '0'); }();
     if (longk && g5ok && m <= 4096 && k >= 2048 && n >= 512) return 'X';
+    // (K >= 2048 took 'S' until round 5; the training backward's 4753 x 256 x 4792 runs 1.4x
+    // faster on 'W', profiles/r05_gemm_train_tiles.txt)
     if (g5ok && tiles64 <= 400 && k >= 512 && n >= 32)
-        return (k >= 2048 || n <= 64) ? 'S' : ((n <= 128 && k >= 1024 && tiles64 > 256) ? 'T' : 'W');
+        return n <= 64 ? 'S' : ((n <= 128 && k >= 1024 && tiles64 > 256) ? 'T' : 'W');
     if (g5ok && m <= 4096)
         return (n <= 512 || (n <= 1024 && k <= 512)) ? 'X' : 'Y';
     // (512 <= K < 1024 took the g5 'Y' until round 5: 'y' measured 1.2-1.3x faster on every
