@@ -588,6 +588,28 @@ extern "C" int fgr_circle_loss(const float* anchor_feat, const float* pos_feat, 
     return FGR_OK;
 }
 
+// the Euclidean feature distances alone (feature_loss.py:11-36 cdist 'euclidean': direct
+// differences, sqrt(sum + 1e-12)), packed per pair at fd_off[b]: the forward of the training
+// CircleLoss (fgreg.loss, its backward on the GEMMs)
+extern "C" int fgr_pair_cdist(const float* anchor_feat, const float* pos_feat, int32_t d,
+                              const int64_t* a_off, const int64_t* p_off, const int64_t* fd_off,
+                              int32_t n_pairs, int32_t max_anchor, int32_t max_pos, float* fd,
+                              void* stream) {
+    FGR_REQUIRE(n_pairs > 0 && d > 0 && max_anchor >= 0 && max_pos >= 0,
+                "fgr_pair_cdist: bad arguments");
+    FGR_REQUIRE(anchor_feat && pos_feat && a_off && p_off && fd_off && fd,
+                "fgr_pair_cdist: null pointer");
+    if (max_anchor > 0 && max_pos > 0) {
+        hipLaunchKernelGGL(circle_fd_kernel,
+                           dim3((unsigned)ceil_div(max_pos, kCdTile),
+                                (unsigned)ceil_div(max_anchor, kCdTile), (unsigned)n_pairs),
+                           dim3(256), 0, as_stream(stream), anchor_feat, pos_feat, d, a_off, p_off,
+                           fd_off, fd);
+        FGR_CHECK_LAUNCH("circle_fd_kernel");
+    }
+    return FGR_OK;
+}
+
 extern "C" int fgr_corr_loss(const float* xyz, const float* corr, const float* w,
                              const int64_t* seg_off, int32_t n_pairs, const float* pose,
                              float* out, void* stream) {

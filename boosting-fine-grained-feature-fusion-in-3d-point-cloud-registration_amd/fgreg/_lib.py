@@ -102,6 +102,7 @@ SIGNATURES = {
     'fgr_circle_loss_workspace': [_i64, _i64, _i64, ctypes.POINTER(_sz)],
     'fgr_circle_loss': [_vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _i64, _i64, _i32, _i32,
                         _i64, _f32, _f32, _vp, _sz, _vp, _vp],
+    'fgr_pair_cdist': [_vp, _vp, _i32, _vp, _vp, _vp, _i32, _i32, _i32, _vp, _vp],
     'fgr_corr_loss': [_vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp],
     'fgr_se3_compare': [_vp, _vp, _i32, _i32, _vp, _vp, _vp],
     'fgr_corr_attention': [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32,

@@ -298,6 +298,8 @@ class my_Bottle2neck(nn.Module):  # noqa: N801 -- reference name (res2net.py:84)
                     elif ops.res2net_chain_supported(self.width, True):
                         chain = (bst,) + ops.res2net_fragments_h3(wst)
             self._folded = (key, w1, b1, ws, w3d, b3d, chain)
+            ops.note_state(w1, b1, w3d, b3d, *[t for wb in ws for t in wb],
+                           *(chain if chain is not None else ()))
         return self._folded[1:]
 
     def forward(self, x, shortcut=None):

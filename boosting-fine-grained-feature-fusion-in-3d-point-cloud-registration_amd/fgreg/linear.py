@@ -101,10 +101,14 @@ def _refresh_stale(device):
         p0 += (e.n + 15) // 16
     dd = torch.frombuffer(bytearray(d.tobytes()), dtype=torch.uint8)
     dd = dd.pin_memory().to(device, non_blocking=True)
+    # the images are rewritten in place: forwards still in flight on other streams (a
+    # pipeline's core streams) read them, so the refresh waits for those first
+    ops.wait_state_readers()
     _lib.check(_lib.load().fgr_split_weights_h3_batch(_ptr(dd), len(stale), p0, _stream()),
                'fgr_split_weights_h3_batch')
     for e in stale:
         e.version = e.src._version
+    ops.note_state(*[e.img for e in stale])
     return len(stale)
 
 
@@ -134,6 +138,7 @@ def weight_image(w: torch.Tensor, transpose=False, tag=None, mode=None, cache=Tr
             ent = _Image(mode, w2, w2.shape[0], w2.shape[1], w2.shape[1], 1, src)
         if cache:
             _CACHE[ck] = ent
+            ops.note_state(ent.img)
     return ent
 
 

@@ -33,6 +33,37 @@ def overlap_pool(prev: torch.Tensor, pools: torch.Tensor) -> torch.Tensor:
     return out
 
 
+class _FeatCdistFn(torch.autograd.Function):
+    """The reference's cdist(a, p, 'euclidean') of one pair (feature_loss.py:11-36: direct
+    differences, sqrt(sum + 1e-12)) for the training CircleLoss: forward by fgr_pair_cdist,
+    backward d fd_ij / d a_i = (a_i - p_j) / fd_ij as GEMMs of W = grad / fd:
+    da = rowsum(W) a - W p, dp = colsum(W) p - W^T a (no Gram-form cancellation in either)."""
+
+    @staticmethod
+    def forward(ctx, a, pp):
+        a, pp = _c(a, torch.float32), _c(pp, torch.float32)
+        _dev(a, pp)
+        na, npos, d = a.shape[0], pp.shape[0], a.shape[1]
+        fd = torch.empty((na, npos), dtype=torch.float32, device=a.device)
+        t = ops.to_device([0, na, 0, npos, 0], torch.int64, a.device)   # a_off, p_off, fd_off
+        _lib.check(_lib.load().fgr_pair_cdist(_ptr(a), _ptr(pp), d, _ptr(t[0:2]), _ptr(t[2:4]),
+                                              _ptr(t[4:5]), 1, na, npos, _ptr(fd), _stream()),
+                   'fgr_pair_cdist')
+        ctx.save_for_backward(a, pp, fd)
+        return fd
+
+    @staticmethod
+    def backward(ctx, g):
+        a, pp, fd = ctx.saved_tensors
+        w = (g / fd).contiguous()
+        da = dp = None
+        if ctx.needs_input_grad[0]:
+            da = a * w.sum(1, keepdim=True) - linear(w, pp.t().contiguous(), cache=False)
+        if ctx.needs_input_grad[1]:
+            dp = pp * w.sum(0)[:, None] - linear(w.t().contiguous(), a.t().contiguous(), cache=False)
+        return da, dp
+
+
 def compute_overlaps(batch):
     """finegrained_kpconv.py:545-571: {'pyr_0': cat(src_overlap + tgt_overlap), 'pyr_p': ...}."""
     meta = batch['kpconv_meta']
@@ -318,11 +349,11 @@ def compute_loss_train(model, pred, batch):
 
     def circle_pair(a, pp, a_xyz, p_xyz):
         # CircleLossFull.get_circle_loss (feature_loss.py:191-230), Euclidean feature distances
-        # by the Gram form on the differentiable f16x3 GEMM (|a|^2 + |p|^2 - 2 a.p, clamped);
-        # non-positive / non-negative entries contribute exp(0) = 1 as in the reference (its
-        # +-1e5 shift is multiplied by a zero weight), the weights are detached as there
-        sq = (a * a).sum(1)[:, None] + (pp * pp).sum(1)[None, :] - 2.0 * linear_t(a, pp, cache=False)
-        fd = torch.sqrt(torch.clamp_min(sq, 0.0) + 1e-12)
+        # by direct differences as the reference's cdist (_FeatCdistFn: the evaluation kernel's
+        # first stage, its backward on the f16x3 GEMMs); non-positive / non-negative entries
+        # contribute exp(0) = 1 as in the reference (its +-1e5 shift is multiplied by a zero
+        # weight), the weights are detached as there
+        fd = _FeatCdistFn.apply(a, pp)
         with torch.no_grad():
             cd = torch.cdist(a_xyz, p_xyz)
             pos, neg = cd < cfg.r_p, cd > cfg.r_n

@@ -118,6 +118,43 @@ def _stream():
     return torch.cuda.current_stream().cuda_stream
 
 
+# ------------------------------------------------------------------------------------------
+# Lazily built model state (weight images, BN-folded weights, stacked head weights): built on
+# the stream of the forward that first needs it, read by every later forward. fgreg.pipeline
+# runs consecutive forwards on different streams, so it must order the forward after one that
+# built state (STATE_EPOCH changed during its enqueue) and mark the new tensors as used by
+# every core stream (take_new_state -> record_stream).
+# ------------------------------------------------------------------------------------------
+STATE_EPOCH = 0
+_NEW_STATE = []
+# streams on which forwards may still be reading cached state, stream -> the event recorded
+# after their last enqueued forward (fgreg.pipeline registers its core streams here): an
+# in-place refresh of a cached weight image waits for them first (linear._refresh_stale)
+STATE_READERS = {}
+
+
+def note_state(*tensors):
+    """Called by the code that builds (or rewrites in place) cached model state."""
+    global STATE_EPOCH
+    STATE_EPOCH += 1
+    _NEW_STATE.extend(t for t in tensors if torch.is_tensor(t))
+
+
+def take_new_state():
+    """The tensors noted since the last call (and forgets them)."""
+    out = list(_NEW_STATE)
+    _NEW_STATE.clear()
+    return out
+
+
+def wait_state_readers():
+    """The current stream waits for every registered reader stream's last forward."""
+    cur = torch.cuda.current_stream()
+    for st, ev in list(STATE_READERS.items()):
+        if st != cur and ev is not None:
+            cur.wait_event(ev)
+
+
 def _dev(*tensors):
     """Operands must be GPU tensors on the CURRENT device: launches go to that device's
     current stream (_stream), so a tensor on another device would hand foreign pointers
@@ -593,8 +630,8 @@ def attention(q, k, v, q_off, kv_off, kv_seg, max_q_len, n_head, out=None,
     q, k, v: (rows, n_head * dh) views with unit column stride (may be column slices of
     one fused QKV tensor). Returns o (Nq, n_head * dh). ``max_kv_len`` defaults to
     ``max_q_len`` (self / cross attention over one segmentation). ``dropout`` = (seed, p):
-    the training forward's attention-weight dropout (fgr_attention_f16x3_drop; f16x3 mode,
-    head dim 32 / 64). ``lse`` (rows, n_head) fp32: the training forward
+    the training forward's attention-weight dropout (fgr_attention_f16x3_drop, in either
+    precision mode; head dim 32 / 64). ``lse`` (rows, n_head) fp32: the training forward
     (fgr_attention_f16x3_train) also writes each row's log2-sum-exp there for the backward
     (only for shapes ``attention_lse_ok`` accepts).
     """
@@ -626,9 +663,12 @@ def attention(q, k, v, q_off, kv_off, kv_seg, max_q_len, n_head, out=None,
             _ptr(ws), ws.numel(), seed & 0xFFFFFFFF, p, _ptr(lse), _stream()),
             'fgr_attention_f16x3_train')
     elif dropout is not None and float(dropout[1]) > 0.0:
-        if not (split and ATTN_MODE == 'f16x3'):
-            raise NotImplementedError('attention dropout needs the f16x3 mode, head dim 32 / 64 '
-                                      'and 16-B aligned rows')
+        # training with dropout: the f16x3 kernel in either precision mode (the bf16 mode's
+        # training attention with dropout is fp32-accurate; its backward, fgr_attention_bwd_drop,
+        # is fp32 in both modes and draws the same mask)
+        if not split:
+            raise NotImplementedError('attention dropout needs head dim 32 / 64 and 16-B aligned '
+                                      'rows')
         nb = _lib._sz(0)
         _lib.check(L.fgr_attention_f16x3_workspace(k.shape[0], n_kv_seg, n_head, nb),
                    'fgr_attention_f16x3_workspace')

@@ -31,13 +31,21 @@ Ordering contract (no extra synchronisation needed by the caller):
   * batch i's core waits for its preprocessing's completion event; every kpconv_meta tensor
     is marked as used by the current stream (record_stream), so the caching allocator does not
     hand its memory to the side stream while the current stream may still read it;
-  * outputs are produced on the current stream, as with ``model(batch)``.
+  * outputs are produced on the current stream, as with ``model(batch)``;
+  * lazily built model state (weight images, BN-folded weights: ops.note_state) is built by
+    the first forward that needs it, on that forward's core stream: a core whose enqueue
+    built state (ops.STATE_EPOCH moved) is waited for by the next core (every later core is
+    then ordered after it), and the new tensors are marked as used by every core stream. A
+    cold model therefore runs its first core(s) one after the other; once the state exists
+    the cores overlap. The core streams are registered in ops.STATE_READERS while the
+    pipeline runs, so an in-place weight-image refresh waits for their forwards.
 """
 import os
 from collections import deque
 
 import torch
 
+from . import ops
 from .regtr import RegTR
 
 DEPTH = int(os.environ.get('FGREG_PIPE_DEPTH', '2'))
@@ -125,18 +133,42 @@ def pipeline(model: RegTR, batches, depth=None, streams=None):
         prepared = deque([(first,) + _prepare(model, first, side, ready, cores)])
         outs = deque()
         i = 0
-        while prepared:
-            while prepared and len(outs) < depth:
-                b, meta, done = prepared.popleft()
-                item = draw()                       # before b's core is enqueued
-                st = cores[i % n_streams]
-                st.wait_event(done)
-                with torch.cuda.stream(st):
-                    out = model._forward(b, meta, slot=i % n_streams)
-                outs.append((out, st))
-                i += 1
-                if item is not None:
-                    prepared.append((item[0],) + _prepare(model, item[0], side, item[1], cores))
-            yield finish(*outs.popleft())
-        while outs:
-            yield finish(*outs.popleft())
+        built = None            # event after the last core whose enqueue built model state
+        ops.take_new_state()    # state built before the pipeline: ordered by the current stream
+        for st in cores:
+            if st is not main:
+                ops.STATE_READERS[st] = None
+        try:
+            while prepared:
+                while prepared and len(outs) < depth:
+                    b, meta, done = prepared.popleft()
+                    item = draw()                       # before b's core is enqueued
+                    st = cores[i % n_streams]
+                    st.wait_event(done)
+                    if built is not None:
+                        st.wait_event(built)
+                        built = None
+                    epoch = ops.STATE_EPOCH
+                    with torch.cuda.stream(st):
+                        out = model._forward(b, meta, slot=i % n_streams)
+                    end = torch.cuda.Event()
+                    end.record(st)
+                    if st is not main:
+                        ops.STATE_READERS[st] = end
+                    if ops.STATE_EPOCH != epoch:
+                        # this core built state the next ones read: order them after it and
+                        # keep the allocator from reusing it under another core stream
+                        built = end
+                        for t in ops.take_new_state():
+                            for s2 in cores:
+                                t.record_stream(s2)
+                    outs.append((out, st))
+                    i += 1
+                    if item is not None:
+                        prepared.append((item[0],) + _prepare(model, item[0], side, item[1], cores))
+                yield finish(*outs.popleft())
+            while outs:
+                yield finish(*outs.popleft())
+        finally:
+            for st in cores:
+                ops.STATE_READERS.pop(st, None)

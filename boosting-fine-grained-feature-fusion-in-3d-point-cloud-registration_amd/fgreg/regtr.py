@@ -66,6 +66,7 @@ class CorrespondenceRegressor(nn.Module):
                 b[d] = self.conf_logits_decoder.bias[0]
             st = (key, w, b)
             object.__setattr__(self, '_stack_cache', st)     # not a parameter / buffer
+            ops.note_state(w, b)
         return st[1], st[2]
 
     def forward_packed(self, feats):

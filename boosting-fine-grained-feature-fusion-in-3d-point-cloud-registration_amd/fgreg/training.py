@@ -139,12 +139,11 @@ def check_trainable(model):
                                   'not in the reference configs')
     if float(cfg.get('dropout', 0.0) or 0.0) > 0.0:
         # transformers.py:95-110: the attention-weight dropout runs in the f16x3 attention
-        # kernels (head dim 32 / 64); the bf16 mode's attention has none
+        # kernels (head dim 32 / 64) in both precision modes (ops.attention)
         dh = cfg.d_embed // cfg.nhead
-        if lin.MODE != 'f16x3' or dh not in (32, 64):
-            raise NotImplementedError(f'training with dropout {cfg.dropout} > 0 needs the fp32 '
-                                      f'(f16x3) mode and head dim 32 / 64 (mode {lin.MODE}, '
-                                      f'head dim {dh})')
+        if dh not in (32, 64):
+            raise NotImplementedError(f'training with dropout {cfg.dropout} > 0 needs head dim '
+                                      f'32 / 64 (head dim {dh})')
     if getattr(model.correspondence_decoder, 'num_neighbors', 0) > 0:
         raise NotImplementedError('training the CorrespondenceDecoder with num_neighbors > 0 (a '
                                   'constructor argument the reference RegTR never passes)')

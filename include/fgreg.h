@@ -416,6 +416,10 @@ int fgr_pair_pose(const float* xyz, const float* corr, const float* logits, int6
  *                       (fgr_circle_loss_workspace bytes); out = the 0-d loss (NaN for a pair
  *                       with no row or no column holding both a positive and a negative, as
  *                       the reference's mean over an empty selection);
+ *  fgr_pair_cdist       the circle loss's first stage alone: fd (packed per pair at fd_off[b],
+ *                       row-major n_a(b) x n_p(b)) = sqrt(sum_k (a_ik - p_jk)^2 + 1e-12), the
+ *                       reference's cdist 'euclidean' by direct differences
+ *                       (feature_loss.py:11-36): the training CircleLoss forward;
  *  fgr_corr_loss        CorrCriterion('mae') for src (pose) + tgt (se3_inv(pose)) directions
  *                       with overlap weights w (corr_loss.py:18-38, finegrained_regtr.py:283-296);
  *  fgr_se3_compare      se3_compare(pred[l, b], gt[b]) (se3_torch.py:117-129) -> rotation
@@ -448,6 +452,9 @@ int fgr_circle_loss(const float* anchor_feat, const float* pos_feat, int32_t d, 
                     const int64_t* fd_off, int32_t n_pairs, int64_t n_anchor, int64_t n_pos,
                     int32_t max_anchor, int32_t max_pos, int64_t fd_elems, float r_p, float r_n,
                     void* ws, size_t ws_bytes, float* out, void* stream);
+int fgr_pair_cdist(const float* anchor_feat, const float* pos_feat, int32_t d, const int64_t* a_off,
+                   const int64_t* p_off, const int64_t* fd_off, int32_t n_pairs, int32_t max_anchor,
+                   int32_t max_pos, float* fd, void* stream);
 int fgr_corr_loss(const float* xyz, const float* corr, const float* w, const int64_t* seg_off,
                   int32_t n_pairs, const float* pose, float* out, void* stream);
 int fgr_se3_compare(const float* pred, const float* gt, int32_t n_layers, int32_t n_pairs,

@@ -91,3 +91,45 @@ def test_pipeline_outputs_usable_on_the_current_stream(gpu):
     for s, out, r in zip(sums, kept, ref):
         assert torch.equal(s, r['pose'].sum())
         _same(out, r)
+
+
+@pytest.mark.parametrize('kind', ['modelnet', '3dmatch'])
+def test_pipeline_on_a_cold_model(gpu, kind):
+    """A freshly built model whose weight images / BN-folded weights do not exist yet: the first
+    cores build them on their own core streams, and the later cores (on the other stream) are
+    ordered after that (ops.note_state / STATE_EPOCH). Outputs equal model(batch) run
+    afterwards, bit for bit."""
+    import fgreg
+    from fgreg import ops
+    torch.manual_seed(3)
+    np.random.seed(3)
+    model = fgreg.RegTR(fgreg.config.get(kind)).to(gpu).eval()
+    P = 2 if kind == 'modelnet' else 1
+    batches = _batches(kind, gpu, [(0, P), (4, P)] * 3)
+    got = list(fgreg.pipeline(model, [dict(b) for b in batches], depth=2, streams=2))
+    torch.cuda.synchronize()
+    assert not ops.STATE_READERS                      # unregistered when the pipeline ends
+    with torch.no_grad():
+        ref = [model(dict(b)) for b in batches]
+    for a, b in zip(got, ref):
+        _same(a, b)
+
+
+def test_pipeline_then_weight_update(gpu):
+    """An in-place weight update between two pipelines (the training -> evaluation pattern):
+    the stale images are re-split (in place, after the core streams' forwards) and the second
+    pipeline equals model(batch) with the new weights."""
+    import fgreg
+    torch.manual_seed(4)
+    model = fgreg.RegTR(fgreg.config.get('modelnet')).to(gpu).eval()
+    batches = _batches('modelnet', gpu, [(0, 2), (3, 2)] * 2)
+    list(fgreg.pipeline(model, [dict(b) for b in batches], depth=2, streams=2))
+    with torch.no_grad():
+        for p in model.parameters():
+            p.mul_(1.01)
+    got = list(fgreg.pipeline(model, [dict(b) for b in batches], depth=2, streams=2))
+    torch.cuda.synchronize()
+    with torch.no_grad():
+        ref = [model(dict(b)) for b in batches]
+    for a, b in zip(got, ref):
+        _same(a, b)

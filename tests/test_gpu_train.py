@@ -321,13 +321,26 @@ def _attn_ref_drop(qkv, lens, kv_seg, nhead, seed, p):
     return torch.cat(outs, 0)
 
 
+@pytest.mark.parametrize('prec', ['fp32', 'bf16'])
 @pytest.mark.parametrize('d,nhead', [(256, 8), (512, 8)])
 @pytest.mark.parametrize('kind', ['self', 'cross', 'shared'])
-def test_attention_dropout_forward_backward(gpu, d, nhead, kind):
+def test_attention_dropout_forward_backward(gpu, d, nhead, kind, prec):
     """Training-mode attention-weight dropout (nn.MultiheadAttention(dropout=p),
     transformers.py:95-96): fgr_attention_f16x3_drop / fgr_attention_bwd_drop against fp64
     softmax attention with the SAME mask (the kernels' counter-based hash restated in numpy):
-    output and dq / dk / dv; the dropped fraction is p; p = 0 is the plain path."""
+    output and dq / dk / dv; the dropped fraction is p; p = 0 is the plain path. In the bf16
+    mode the dropout path runs the same fp32-accurate kernels (same mask, same bound); its
+    p = 0 path is the bf16 attention (bf16 bound)."""
+    import fgreg
+    prev = fgreg.precision()
+    fgreg.set_precision(prec)
+    try:
+        _attention_dropout_case(gpu, d, nhead, kind, prec)
+    finally:
+        fgreg.set_precision(prev)
+
+
+def _attention_dropout_case(gpu, d, nhead, kind, prec):
     from fgreg import ops
     from fgreg.autograd import _AttentionFn, attn_drop_mask
     lens = [130, 1, 65, 300]
@@ -349,7 +362,7 @@ def test_attention_dropout_forward_backward(gpu, d, nhead, kind):
     m = attn_drop_mask(seed, p, 3, range(300), range(300))
     assert abs(float(m.mean()) - p) < 0.01
     o0 = _AttentionFn.apply(qkv.detach(), off, ks, max(lens), nhead, 0.0, seed)
-    assert rel_err(o0, _attn_ref(qkv64.detach(), lens, kv_seg, nhead)) < 1e-5
+    assert rel_err(o0, _attn_ref(qkv64.detach(), lens, kv_seg, nhead)) < (1e-5 if prec == "fp32" else 5e-2)
 
 
 def test_train_step_with_dropout(gpu):
@@ -384,6 +397,18 @@ def test_train_step_with_dropout(gpu):
     assert math.isfinite(l1) and bool(torch.isfinite(g1).all())
     assert l1 == l2 and torch.equal(g1, g2)
     assert l1 != l3 and l1 != l0
+    # the bf16 mode trains with dropout too (round 6): reproducible under one seed, and close to
+    # the fp32-accurate step with the same masks (the bf16 products' own error)
+    prev = fgreg.precision()
+    fgreg.set_precision('bf16')
+    try:
+        b1, h1 = step(0.1, 5)
+        b2, h2 = step(0.1, 5)
+    finally:
+        fgreg.set_precision(prev)
+    assert math.isfinite(b1) and bool(torch.isfinite(h1).all())
+    assert b1 == b2 and torch.equal(h1, h2)
+    assert abs(b1 - l1) < 5e-2 * abs(l1)
 
 
 @pytest.mark.parametrize('d', [64, 256])

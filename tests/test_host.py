@@ -200,15 +200,15 @@ def test_training_mode_refuses_host_tensors():
 @pytest.mark.parametrize('what', ['dropout', 'num_neighbors'])
 def test_training_refuses_untrainable_configs(what):
     """Configurations the training forward does not restate raise NotImplementedError before
-    any work: dropout > 0 in the bf16 mode (its attention kernels have no dropout; the f16x3
-    mode trains with dropout, transformers.py:95-110, tests/test_gpu_train.py), and the
-    decoder's num_neighbors > 0."""
+    any work: dropout > 0 with a head dim the dropout attention kernels do not take (both
+    precision modes train with dropout at head dim 32 / 64, transformers.py:95-110,
+    tests/test_gpu_train.py), and the decoder's num_neighbors > 0."""
     import fgreg
     import fgreg.config as fc
     prev = fgreg.precision()
     try:
         if what == 'dropout':
-            model = fgreg.RegTR(fc.get('modelnet', dropout=0.1)).train()
+            model = fgreg.RegTR(fc.get('modelnet', dropout=0.1, nhead=16)).train()   # head dim 16
             fgreg.set_precision('bf16')
         else:
             model = fgreg.RegTR(fc.get('modelnet', direct_regress_coor=False)).train()
