@@ -584,16 +584,24 @@ def write_gemm_table(path, rtimer, steps, step_ms, mode, name='gemm'):
     wb = 2.0 if mode == 'bf16' else 4.0
     mfma_peak = F16_MFMA_PEAK_TFLOPS / pipe
     rows = []
-    for (m, n, k), (ms, cnt) in sorted(rtimer.per_label(name).items(),
-                                       key=lambda kv: -kv[1][0]):
+    for lab, (ms, cnt) in sorted(rtimer.per_label(name).items(), key=lambda kv: -kv[1][0]):
         us = ms * 1e3 / cnt
-        flops = 2.0 * m * n * k
-        byt = 4.0 * m * k + wb * n * k + 4.0 * m * n
+        if lab[0] == 'ffn':
+            # the fused feed-forward sub-layer (ops.ffn): M x d in, hidden F, two products;
+            # bytes = x read once, both weight images, the output
+            _, m, n, k = lab
+            flops = 4.0 * m * n * k
+            byt = 4.0 * m * n + 2 * wb * n * k + 4.0 * m * n
+        else:
+            m, n, k = lab
+            flops = 2.0 * m * n * k
+            byt = 4.0 * m * k + wb * n * k + 4.0 * m * n
         tf = flops / (us * 1e-6) / 1e12
         gbs = byt / (us * 1e-6) / 1e9
         t_mfma = flops / (mfma_peak * 1e12) * 1e6
         t_hbm = byt / (HBM_PEAK_GBS * 1e9) * 1e6
         rows.append({'M': m, 'N': n, 'K': k, 'launches_per_step': cnt / steps, 'us': us,
+                     'kind': 'ffn (d = N, hidden = K)' if lab[0] == 'ffn' else 'gemm',
                      'us_per_step': ms * 1e3 / steps, 'gflop': flops / 1e9, 'mbytes': byt / 1e6,
                      'tflops_fp32_equiv': tf, 'gbs': gbs, 'mfma_frac': tf / mfma_peak,
                      'hbm_frac': gbs / HBM_PEAK_GBS,

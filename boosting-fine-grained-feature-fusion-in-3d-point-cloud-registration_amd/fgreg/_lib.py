@@ -67,6 +67,11 @@ SIGNATURES = {
                           _i32, _i32, _vp],
     'fgr_gemm_f16x3_ln_out2': [_vp, _i64, _vp, _vp, _f32, _vp, _i64, _vp, _vp, _i64, _vp, _i32,
                                _i32, _i32, _i32, _vp, _vp, _vp, _i64, _vp],
+    'fgr_split_weights_ffn2_bytes': [_i32, _i32, ctypes.POINTER(_sz)],
+    'fgr_split_weights_ffn2': [_vp, _i32, _i32, _i64, _i64, _vp, _vp],
+    'fgr_ffn_f16x3_supported': [_i32, _i32, _i32],
+    'fgr_ffn_f16x3': [_vp, _i64, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _i32,
+                      _i32, _vp],
     'fgr_split_weights_bf16_bytes': [_i32, _i32, ctypes.POINTER(_sz)],
     'fgr_split_weights_bf16': [_vp, _i32, _i32, _i64, _i64, _vp, _vp],
     'fgr_gemm_bf16': [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _vp],
@@ -148,6 +153,8 @@ SIGNATURES = {
                                 _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i32, _i32, _i64, _i64, _i64,
                                 _i32, _i32, _f32, _vp, _sz, ctypes.c_uint32, _f32, _vp, _i64, _vp],
     'fgr_attention_bwd_train_workspace': [_i64, _i32, _i64, _i32, _i32, _i32, ctypes.POINTER(_sz)],
+    'fgr_modelnet_metrics_workspace': [_i32, _i32, ctypes.POINTER(_sz)],
+    'fgr_modelnet_metrics': [_vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _vp, _sz, _vp, _vp],
     'fgr_crop_max_points': [ctypes.POINTER(_i32)],
     'fgr_crop_pairs_mask': [_vp, _i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     'fgr_crop_pairs_assemble': [_vp, _i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp,

@@ -56,7 +56,10 @@ class _Image:
     keeps w2 when it is a view of the source's storage (so a stale f16x3 image can be
     re-split in place by the batched refresh)."""
     __slots__ = ('img', 'n', 'k', 'sn', 'sk', 'src', 'version', 'ptr', 'mode', 'view')
-    FN = {'f16x3': 'fgr_split_weights_h3', 'bf16': 'fgr_split_weights_bf16'}
+    # 'ffn2': the fused feed-forward kernel's linear2 image (chunk-major, k-permuted f16x3,
+    # fgr_split_weights_ffn2; ops.ffn)
+    FN = {'f16x3': 'fgr_split_weights_h3', 'bf16': 'fgr_split_weights_bf16',
+          'ffn2': 'fgr_split_weights_ffn2'}
 
     def __init__(self, mode, w2: torch.Tensor, n, k, sn, sk, src: torch.Tensor):
         L = _lib.load()

@@ -861,6 +861,38 @@ def qkv_attention(h, w_img, bias, q_off, kv_seg, max_len, n_head, mode='f16x3'):
     return o
 
 
+FFN_FUSE = os.environ.get('FGREG_FFN_FUSE', '1') != '0'
+
+
+def ffn_supported(m, d, f) -> bool:
+    """True if the pre-norm feed-forward sub-layer of an (m, d) input with hidden width f runs
+    as one launch (fgr_ffn_f16x3: d = 256, the ModelNet transformer; FGREG_FFN_FUSE=0 off)."""
+    return FFN_FUSE and bool(_lib.load().fgr_ffn_f16x3_supported(m, d, f))
+
+
+def ffn(x, norm, w1_img, b1, w2_img, b2, bound, out=None) -> torch.Tensor:
+    """x + linear2(ReLU(linear1(norm(x)))) in one launch (transformers.py:231-238):
+    w1_img = linear.weight_image(linear1.weight, mode='f16x3'), w2_img =
+    linear.weight_image(linear2.weight, mode='ffn2'), bound (2,) = {max_j ||W1_j||, max |b1|}
+    on the device."""
+    _dev(x, b1, b2, bound)
+    m, d = x.shape
+    f = b1.numel()
+    assert x.dtype == torch.float32 and x.stride(1) == 1 and b2.numel() == d
+    x = x if (x.stride(0) % 4 == 0 and x.data_ptr() % 16 == 0) else x.contiguous()
+    g, b = norm.weight.contiguous(), norm.bias.contiguous()
+    b1, b2, bound = b1.contiguous(), b2.contiguous(), bound.contiguous()
+    if out is None:
+        out = torch.empty((m, d), dtype=torch.float32, device=x.device)
+    t0 = _begin('gemm', ('ffn', m, d, f))
+    _lib.check(_lib.load().fgr_ffn_f16x3(
+        _ptr(x), x.stride(0), _ptr(g), _ptr(b), float(norm.eps), _ptr(w1_img.img), _ptr(b1),
+        _ptr(w2_img.img), _ptr(b2), _ptr(bound), _ptr(out), out.stride(0), m, d, f, _stream()),
+        'fgr_ffn_f16x3')
+    _end('gemm', t0, 4 * m * d * f)
+    return out
+
+
 def corr_head_supported(m, d) -> bool:
     return bool(_lib.load().fgr_corr_head_supported(int(m), int(d)))
 

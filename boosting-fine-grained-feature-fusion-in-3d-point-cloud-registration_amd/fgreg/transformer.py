@@ -199,9 +199,29 @@ class TransformerCrossEncoderLayer(nn.Module):
                              seg.cross_seg)
         x = linear(o, self.multihead_attn.out_proj.weight, self.multihead_attn.out_proj.bias,
                    residual=x)
-        # position-wise feed-forward (:231-238); linear_ln falls back to layernorm + linear
+        # position-wise feed-forward (:231-238): one launch where supported (ops.ffn: the
+        # hidden activations stay on chip), else linear_ln (or layernorm + linear) then linear
+        if lin.MODE == 'f16x3' and ops.ffn_supported(n, d, self.linear1.out_features):
+            return ops.ffn(x, self.norm3, lin.weight_image(self.linear1.weight, mode='f16x3'),
+                           self.linear1.bias, lin.weight_image(self.linear2.weight, mode='ffn2'),
+                           self.linear2.bias, self._ffn_bound()), None
         h = linear_ln(x, self.norm3, self.linear1.weight, self.linear1.bias, act=ops.ACT_RELU)
         return linear(h, self.linear2.weight, self.linear2.bias, residual=x), None
+
+    def _ffn_bound(self):
+        """{max_j ||linear1.weight[j]||_2, max_j |linear1.bias[j]|} on the device (the fused
+        feed-forward kernel's hidden-value scale, ops.ffn), rebuilt when either tensor changes."""
+        w, b = self.linear1.weight, self.linear1.bias
+        key = (w.data_ptr(), w._version, b.data_ptr(), b._version)
+        st = self.__dict__.get('_ffn_bound_cache')
+        if st is None or st[0] != key:
+            with torch.no_grad():
+                bound = torch.stack([w.detach().norm(dim=1).max(),
+                                     b.detach().abs().max()]).float().contiguous()
+            st = (key, bound)
+            self.__dict__['_ffn_bound_cache'] = st          # not a parameter / buffer
+            ops.note_state(bound)
+        return st[1]
 
     def _forward_post(self, x, pos, seg: Segments, pending_bias=None):
         """forward_post (transformers.py:109-181): each sub-block's residual sum is formed in

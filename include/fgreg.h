@@ -281,6 +281,26 @@ int fgr_gemm_f16x3_ln_out2(const float* x, int64_t ldx, const float* gamma, cons
                            int32_t k, int32_t act, const float* gamma2, const float* beta2,
                            float* out2, int64_t ld_out2, void* stream);
 
+/* Pre-norm position-wise feed-forward sub-layer in one launch (transformers.py:231-238):
+ *   out = x + linear2(ReLU(linear1(LayerNorm_eps(x) * gamma + beta)))
+ * x, out (m, d) (out may be x itself), linear1 (f, d) + b1, linear2 (d, f) + b2, the f16x3
+ * products of fgr_gemm_f16x3; the (m, f) hidden activations never leave the chip.
+ * w1_img: fgr_split_weights_h3 of linear1.weight; w2_img: fgr_split_weights_ffn2 of
+ * linear2.weight (the chunk-major image in the k order the fused kernel consumes; bytes from
+ * fgr_split_weights_ffn2_bytes(d, f), f % 32 == 0); bound (device, 2 floats) = {max_j
+ * ||linear1.weight[j]||_2, max_j |b1[j]|} (sets the hidden values' fp16 scale). All pointers
+ * 16-B aligned, row strides multiples of 4. fgr_ffn_f16x3_supported(m, d, f): d = 256,
+ * 64 <= f <= 2048, f % 64 == 0 (the ModelNet transformer). Replaces the two-launch
+ * linear1 (fgr_gemm_f16x3_ln) -> linear2 (fgr_gemm_f16x3_ws, residual) sequence. */
+int fgr_split_weights_ffn2_bytes(int32_t n, int32_t k, size_t* bytes);
+int fgr_split_weights_ffn2(const float* w, int32_t n, int32_t k, int64_t stride_n,
+                           int64_t stride_k, void* img, void* stream);
+int fgr_ffn_f16x3_supported(int32_t m, int32_t d, int32_t f);
+int fgr_ffn_f16x3(const float* x, int64_t ldx, const float* gamma, const float* beta, float eps,
+                  const void* w1_img, const float* b1, const void* w2_img, const float* b2,
+                  const float* bound, float* out, int64_t ldo, int32_t m, int32_t d, int32_t f,
+                  void* stream);
+
 int fgr_split_weights_bf16_bytes(int32_t n, int32_t k, size_t* bytes);
 int fgr_split_weights_bf16(const float* w, int32_t n, int32_t k, int64_t stride_n,
                            int64_t stride_k, void* img, void* stream);
@@ -459,6 +479,19 @@ int fgr_corr_loss(const float* xyz, const float* corr, const float* w, const int
                   int32_t n_pairs, const float* pose, float* out, void* stream);
 int fgr_se3_compare(const float* pred, const float* gt, int32_t n_layers, int32_t n_pairs,
                     float* rot_deg, float* trans, void* stream);
+
+/* ---- ModelNet evaluation metrics (benchmark/benchmark_modelnet.py:33-82 compute_metrics, the
+ * ModelNet branch of GenericRegModel.test_step, generic_reg_model.py:138-147) -------------------
+ * pred, gt (n_pairs, 3, 4) fp32 poses; src, ref (n_pairs, n_pts, 3) the input clouds; raw
+ * (n_pairs, n_raw, 3) the clean reference clouds (points_raw); all contiguous.
+ * out (n_pairs, 7) fp64 = r_mse, r_mae (the 'xyz' Euler angles in degrees, scipy's from_matrix
+ * orthogonalisation restated), t_mse, t_mae, err_r_deg, err_t (isotropic), chamfer_dist (the
+ * modified Chamfer distance over the raw cloud). Workspace: fgr_modelnet_metrics_workspace
+ * bytes (the per-point squared minima). Two launches, deterministic. */
+int fgr_modelnet_metrics_workspace(int32_t n_pairs, int32_t n_pts, size_t* bytes);
+int fgr_modelnet_metrics(const float* pred, const float* gt, const float* src, const float* ref,
+                         const float* raw, int32_t n_pairs, int32_t n_pts, int32_t n_raw, void* ws,
+                         size_t ws_bytes, double* out, void* stream);
 
 /* ---- Input side: the ModelNet crop test pipeline on the GPU ----------
  * Replaces, for a batch of samples, the geometry of data_loaders/modelnet_transforms.py

@@ -671,6 +671,46 @@ def make_train(fr, fk):
     save('train_modelnet_small', **arrays)
 
 
+def make_modelnet_metrics():
+    """benchmark/benchmark_modelnet.py:33-82 compute_metrics -- the ModelNet test step's metrics
+    (generic_reg_model.py:138-147) -- on synthetic pairs: 6 pairs of 717 src / ref points and
+    2048 raw points, predicted poses 2-12 degrees / 1-5 cm off the ground truth (ModelNet's
+    RandomTransformSE3_euler magnitudes for gt), one pair predicted exactly."""
+    sys.path.insert(0, os.path.join(REF, 'benchmark'))
+    import benchmark_modelnet as bm
+    from scipy.spatial.transform import Rotation
+    rng = np.random.default_rng(11)
+    B, N, R = 6, 717, 2048
+
+    def pose(rot, t):
+        P = np.zeros((3, 4), np.float32)
+        P[:, :3] = rot.as_matrix()
+        P[:, 3] = t
+        return P
+    gt, pred = [], []
+    for b in range(B):
+        rg = Rotation.from_euler('zyx', rng.uniform(-45, 45, 3), degrees=True)
+        tg = rng.uniform(-0.5, 0.5, 3)
+        gt.append(pose(rg, tg))
+        if b == 0:
+            pred.append(gt[-1].copy())
+            continue
+        ax = rng.normal(size=3)
+        dr = Rotation.from_rotvec(ax / np.linalg.norm(ax) * np.radians(rng.uniform(2, 12)))
+        pred.append(pose(dr * rg, tg + rng.uniform(-0.05, 0.05, 3)))
+    gt, pred = np.stack(gt), np.stack(pred)
+    raw = rng.uniform(-1, 1, (B, R, 3)).astype(np.float32)
+    src = (raw[:, :N] + 0.01 * rng.normal(size=(B, N, 3))).astype(np.float32)
+    ref = (raw[:, R - N:] + 0.01 * rng.normal(size=(B, N, 3))).astype(np.float32)
+    data = {'points_src': torch.from_numpy(src), 'points_ref': torch.from_numpy(ref),
+            'points_raw': torch.from_numpy(raw), 'transform_gt': torch.from_numpy(gt)}
+    m = bm.compute_metrics(data, torch.from_numpy(pred))
+    s = bm.summarize_metrics(m)
+    save('modelnet_metrics', points_src=src, points_ref=ref, points_raw=raw, transform_gt=gt,
+         pred_transforms=pred, **{'m_' + k: np.asarray(v) for k, v in m.items()},
+         **{'s_' + k: np.asarray(v) for k, v in s.items()})
+
+
 if __name__ == '__main__':
     fr, fk = import_reference()
     if sys.argv[1:] == ['loss']:
@@ -691,6 +731,9 @@ if __name__ == '__main__':
     if sys.argv[1:] == ['topk']:
         make_decoder_topk(fr)
         sys.exit(0)
+    if sys.argv[1:] == ['metrics']:
+        make_modelnet_metrics()
+        sys.exit(0)
     make_geometry()
     make_modules(fr, fk)
     make_forward(fr, fk)
@@ -700,3 +743,4 @@ if __name__ == '__main__':
     make_loss(fr, fk)
     make_loss_circle(fr, fk)
     make_train(fr, fk)
+    make_modelnet_metrics()

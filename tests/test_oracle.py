@@ -217,3 +217,34 @@ def test_train_oracle_matches_reference():
     for k in ref.files:
         if k.startswith('grad.'):
             assert rel_err(grads[k[5:]], ref[k]) < 1e-4, (k, rel_err(grads[k[5:]], ref[k]))
+
+
+# fp32 floor of the reference's isotropic rotation error: acos of a value within a few fp32
+# roundings of 1 (0.5 (trace - 1) with trace a 9-product fp32 sum) -- sqrt(2 * 8 * 2^-24) rad
+ISO_ROT_FLOOR_DEG = float(np.degrees(np.sqrt(16 * 2.0 ** -24)))
+
+
+def check_modelnet_metrics(got, ref_m, rel=1e-4):
+    """compute_metrics outputs against the reference's (benchmark_modelnet.py:33-82): every
+    value within `rel` relative (of the array's max) -- err_r_deg also within the fp32 floor
+    of the reference's own acos near zero error."""
+    for k, v in ref_m.items():
+        g = np.asarray(got[k], np.float64)
+        v = np.asarray(v, np.float64)
+        assert g.shape == v.shape, k
+        tol = rel * max(float(np.abs(v).max()), 1e-30) + (ISO_ROT_FLOOR_DEG if k == 'err_r_deg' else 0.0)
+        assert float(np.abs(g - v).max()) <= tol, (k, g, v)
+
+
+def test_metrics_oracle_matches_reference():
+    """oracle/metrics_oracle.py against the reference's own benchmark_modelnet.compute_metrics
+    and summarize_metrics (tests/golden/modelnet_metrics.npz)."""
+    import metrics_oracle as mt
+    g = golden('modelnet_metrics')
+    m = mt.compute_metrics(g['points_src'], g['points_ref'], g['points_raw'], g['transform_gt'],
+                           g['pred_transforms'])
+    ref_m = {k[2:]: g[k] for k in g.files if k.startswith('m_')}
+    check_modelnet_metrics(m, ref_m, rel=1e-5)
+    s = mt.summarize_metrics({k[2:]: g[k] for k in g.files if k.startswith('m_')})
+    for k in s:
+        assert np.allclose(s[k], g['s_' + k], rtol=1e-6, atol=0), k
