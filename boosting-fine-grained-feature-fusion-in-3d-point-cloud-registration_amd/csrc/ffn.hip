@@ -40,6 +40,7 @@
 // fgr_split_weights_ffn2 below ([chunk F/32][panel d/16][term][g][16] x 16 B in the permuted k
 // order, then the d per-row inverse scales).
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -420,6 +421,306 @@ __global__ void __launch_bounds__(256, 1) ffn_f16x3_kernel(FfnArgs p) {
 #endif
 }
 
+// ---------------------------------------------------------------------------------------------
+// Version 2 (default): the same sub-layer with the waves splitting the WEIGHTS instead of the rows.
+//
+// The ring version above streams every weight unit to all 4 waves of a block through LDS (each
+// wave multiplies it against its own 16 rows): per 16 KB unit the CU pays 16 LDS-DMA pieces, 64
+// KB of LDS fragment reads and a barrier for 96 MFMAs, and its in-kernel clock stamps put the
+// DMA / read issue (446 cycles per unit) and the DMA wait (209) beside 384 cycles of MFMA.
+// Here the block's 64 LayerNorm'd rows are split ONCE into an LDS image (4 row tiles x 8 k32
+// steps x 2 terms, 64 KB), and each wave owns weights, read straight from global memory (L2)
+// into registers, each byte by one wave only:
+//   * linear1: wave w computes hidden chunk 4 st + w (32 units) of step st for all 64 rows (its
+//     W1 fragments x the row image from LDS), bias + ReLU + scale + split as in version 1, and
+//     writes the 64 rows x 32 hidden fragments to an LDS hand-off buffer (8 KB per wave);
+//   * one barrier per step (128 hidden units), then linear2: wave w owns output panels
+//     4 w .. 4 w + 3 (64 columns) and contracts them over the step's 128 hidden units (the four
+//     waves' fragments from LDS, its W2 fragments from global), accumulating 4 row tiles x 4
+//     panels in registers; no cross-wave reduction at the end.
+// Per step and wave: 64 x 16-B weight loads per lane (its 32 KB of W1 and 32 KB of W2), 96 LDS
+// fragment reads, 384 MFMAs; 8 barriers per launch at F = 1024. The weight loads run 3 groups
+// (12 loads) ahead of their MFMAs through a 4-group register ring.
+constexpr int kV2Groups = 16;          // load groups per step: 8 linear1 k32 steps, 8 linear2 halves
+constexpr int kV2Ring = 4;             // register ring of groups (3 in flight while one computes)
+static_assert(kV2Groups % kV2Ring == 0, "ring slot = group index mod kV2Ring at compile time");
+
+// s_waitcnt vmcnt(n) (lgkmcnt / expcnt untouched) for n <= 12
+__device__ __forceinline__ void wait_vm_only(int n) {
+    // vmcnt field bits 3:0 and 15:14, expcnt 6:4 = 7, lgkmcnt 11:8 = 15 (no wait)
+#define FGR_VMW(N) __builtin_amdgcn_s_waitcnt(((N) & 15) | (((N) >> 4) << 14) | (7 << 4) | (15 << 8))
+    switch (n) {
+        case 0: FGR_VMW(0); break;   case 4: FGR_VMW(4); break;
+        case 8: FGR_VMW(8); break;   default: FGR_VMW(12); break;
+    }
+#undef FGR_VMW
+}
+
+__global__ void __launch_bounds__(256, 1) ffn_nsplit_kernel(FfnArgs p) {
+    __shared__ u32x4 act[4 * kFfnKS * 2 * 64];            // [row tile][k32 step][term][lane]
+    __shared__ u32x4 hbuf[2][4][4][2][64];                // [step & 1][src wave][row tile][term][lane]
+    __shared__ float4 cw1[kFfnMaxF / 4], cb1[kFfnMaxF / 4];
+    __shared__ float4 cw2[kFfnD / 4], cb2[kFfnD / 4];
+    __shared__ float4 lng[kFfnD / 4], lnb[kFfnD / 4];
+    __shared__ float2 rowpar[64];                         // per row: (rs_a S, S)
+
+    const int nbm = (p.M + 63) / 64;
+    int t = blockIdx.x;
+    {   // XCD-aware order: each XCD a contiguous range of row blocks
+        const int q = nbm / 8, r = nbm % 8, x = t % 8, lo = t / 8;
+        t = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + lo;
+    }
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+    const int g = lane >> 4, c = lane & 15;
+    const int r0 = t * 64;                                // the block's first row
+    const int nst = p.F / 128;                            // steps of 128 hidden units
+
+    // 1. this wave's row tile (rows r0 + 16 wv + c), parameters -> LDS
+    float xr[kFfnKS][8];
+    {
+        const int64_t row = min(r0 + 16 * wv + c, p.M - 1);
+        const float* ar = p.x + row * p.ldx;
+#pragma unroll
+        for (int s = 0; s < kFfnKS; ++s) {
+            const float4 a0 = *reinterpret_cast<const float4*>(ar + 32 * s + 8 * g);
+            const float4 a1 = *reinterpret_cast<const float4*>(ar + 32 * s + 8 * g + 4);
+            xr[s][0] = a0.x; xr[s][1] = a0.y; xr[s][2] = a0.z; xr[s][3] = a0.w;
+            xr[s][4] = a1.x; xr[s][5] = a1.y; xr[s][6] = a1.z; xr[s][7] = a1.w;
+        }
+    }
+    {
+        const int nf4 = p.F / 4;
+        const int j0 = min(tid, nf4 - 1), j1 = min(tid + 256, nf4 - 1);
+        const float4 pw1a = reinterpret_cast<const float4*>(p.wsc1)[j0];
+        const float4 pb1a = reinterpret_cast<const float4*>(p.b1)[j0];
+        const float4 pw1b = reinterpret_cast<const float4*>(p.wsc1)[j1];
+        const float4 pb1b = reinterpret_cast<const float4*>(p.b1)[j1];
+        const int t4 = tid & (kFfnD / 4 - 1);
+        const float4 pw2 = reinterpret_cast<const float4*>(p.wsc2)[t4];
+        const float4 pb2 = reinterpret_cast<const float4*>(p.b2)[t4];
+        const float4 pg = reinterpret_cast<const float4*>(p.ln_g)[t4];
+        const float4 pbe = reinterpret_cast<const float4*>(p.ln_b)[t4];
+        if (tid < nf4) { cw1[tid] = pw1a; cb1[tid] = pb1a; }
+        if (tid + 256 < nf4) { cw1[tid + 256] = pw1b; cb1[tid + 256] = pb1b; }
+        if (tid < kFfnD / 4) { cw2[tid] = pw2; cb2[tid] = pb2; lng[tid] = pg; lnb[tid] = pbe; }
+    }
+    const float bM1 = p.bound[0], bMb = p.bound[1];
+    __syncthreads();
+
+    // 2. LayerNorm3, ||a||, the row split into the LDS row image, the per-row scales
+    {
+        float sm = 0.f;
+#pragma unroll
+        for (int s = 0; s < kFfnKS; ++s)
+            sm += ((xr[s][0] + xr[s][1]) + (xr[s][2] + xr[s][3])) +
+                  ((xr[s][4] + xr[s][5]) + (xr[s][6] + xr[s][7]));
+        const float mean = xg_sum_f(sm) / (float)kFfnD;
+        float sq = 0.f;
+#pragma unroll
+        for (int s = 0; s < kFfnKS; ++s)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float d = xr[s][e] - mean;
+                sq += d * d;
+            }
+        const float rstd = 1.0f / sqrtf(xg_sum_f(sq) / (float)kFfnD + p.eps);
+        float mx = 0.f, nn = 0.f;
+#pragma unroll
+        for (int s = 0; s < kFfnKS; ++s) {
+            const int k = 32 * s + 8 * g;
+            const float4 g0 = lng[k / 4], g1 = lng[k / 4 + 1];
+            const float4 b0 = lnb[k / 4], b1 = lnb[k / 4 + 1];
+            const float gg[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+            const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float a = (xr[s][e] - mean) * rstd * gg[e] + bb[e];
+                xr[s][e] = a;
+                nn = fmaf(a, a, nn);
+            }
+            mx = fmaxf(mx, max3_abs(xr[s][0], xr[s][1], xr[s][2]));
+            mx = fmaxf(mx, max3_abs(xr[s][3], xr[s][4], xr[s][5]));
+            mx = fmaxf(mx, max3_abs(xr[s][6], xr[s][7], 0.f));
+        }
+        mx = xg_max_f(mx);
+        nn = xg_sum_f(nn);
+        const int ea = mx > 0.f ? min(15 - __builtin_amdgcn_frexp_expf(mx), 127) : 0;
+        const float sca = __builtin_ldexpf(1.f, ea);
+#pragma unroll
+        for (int s = 0; s < kFfnKS; ++s) {
+            u32x4 h, l;
+            split8_f16(xr[s], sca, h, l);
+            act[((wv * kFfnKS + s) * 2 + 0) * 64 + lane] = h;
+            act[((wv * kFfnKS + s) * 2 + 1) * 64 + lane] = l;
+        }
+        const float bnd = sqrtf(nn) * bM1 + bMb;
+        const int eh = bnd > 0.f ? max(min(15 - __builtin_amdgcn_frexp_expf(bnd), 127), -126) : 0;
+        if (g == 0) rowpar[16 * wv + c] = make_float2(__builtin_ldexpf(1.f, eh - ea), __builtin_ldexpf(1.f, eh));
+    }
+    __syncthreads();
+
+    // 3. the steps. Load group j of a step: j < 8 = linear1 k32 step j of this wave's chunk (W1
+    //    panels 2 ch, 2 ch + 1 x 2 terms); j >= 8 = linear2 source wave (j - 8) / 2, output panel
+    //    pair (j - 8) % 2 of this wave's four (x 2 terms)
+    auto issue = [&](int st, int j, u32x4 (&slot)[4]) {
+        if (j < 8) {
+            const int ch = 4 * st + wv;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int pp = e >> 1, tt = e & 1;
+                slot[e] = p.w1[(int64_t)(2 * ch + pp) * kUnit + (j * 2 + tt) * 64 + lane];
+            }
+        } else {
+            const int ch = 4 * st + ((j - 8) >> 1), q0 = 4 * wv + 2 * ((j - 8) & 1);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int qq = e >> 1, tt = e & 1;
+                slot[e] = p.w2[((int64_t)(ch * kFfnNP + q0 + qq) * 2 + tt) * 64 + lane];
+            }
+        }
+    };
+    u32x4 ring[kV2Ring][4];
+    f32x4 accy[4][4];                                     // [row tile][output panel of the wave]
+#pragma unroll
+    for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) accy[rt][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < kV2Ring - 1; ++j) issue(0, j, ring[j]);
+    // LDS fragments of a group, double-buffered: the 4 row tiles' (hi, lo) row-image fragments
+    // of a k32 step (linear1), or the 4 row tiles' (hi, lo) hidden fragments of a source wave
+    // (linear2); the next group's are read while this group's MFMAs run
+    u32x4 fa[2][8];
+    auto read_act = [&](int s, u32x4 (&f)[8]) {
+#pragma unroll
+        for (int rt = 0; rt < 4; ++rt) {
+            f[2 * rt + 0] = act[((rt * kFfnKS + s) * 2 + 0) * 64 + lane];
+            f[2 * rt + 1] = act[((rt * kFfnKS + s) * 2 + 1) * 64 + lane];
+        }
+    };
+    auto read_h = [&](int buf, int sw, u32x4 (&f)[8]) {
+#pragma unroll
+        for (int rt = 0; rt < 4; ++rt) {
+            f[2 * rt + 0] = hbuf[buf][sw][rt][0][lane];
+            f[2 * rt + 1] = hbuf[buf][sw][rt][1][lane];
+        }
+    };
+
+    for (int st = 0; st < nst; ++st) {
+        const int ch = 4 * st + wv;
+        // the last step's look-ahead re-reads its own groups (no branch in the body; drained
+        // after the loop)
+        const int stn = min(st + 1, nst - 1);
+        f32x4 acc1[4][2];
+#pragma unroll
+        for (int rt = 0; rt < 4; ++rt) acc1[rt][0] = acc1[rt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+        read_act(0, fa[0]);
+#pragma unroll
+        for (int j = 0; j < kV2Groups; ++j) {
+            const int jn = j + kV2Ring - 1;               // group j + 3 (this step or the next)
+            issue(jn < kV2Groups ? st : stn, jn % kV2Groups, ring[jn % kV2Ring]);
+            wait_vm_only(4 * (kV2Ring - 1));              // group j landed
+            u32x4 (&wf)[4] = ring[j % kV2Ring];
+            if (j < 8) {
+                u32x4 (&cur)[8] = fa[j & 1];
+                if (j < 7) read_act(j + 1, fa[(j + 1) & 1]);
+                __builtin_amdgcn_sched_group_barrier(0x020, 4, 0);      // this group's + 3 loads
+                if (j < 7) __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);   // next reads
+                // linear1 k32 step j: W1 (panel pp, term) x the 4 row tiles' fragments
+#pragma unroll
+                for (int rt = 0; rt < 4; ++rt) {
+                    const f16x8 ah = __builtin_bit_cast(f16x8, cur[2 * rt + 0]);
+                    const f16x8 al = __builtin_bit_cast(f16x8, cur[2 * rt + 1]);
+#pragma unroll
+                    for (int pp = 0; pp < 2; ++pp) {
+                        const f16x8 wh = __builtin_bit_cast(f16x8, wf[2 * pp]);
+                        const f16x8 wl = __builtin_bit_cast(f16x8, wf[2 * pp + 1]);
+                        acc1[rt][pp] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, ah, acc1[rt][pp], 0, 0, 0);
+                        acc1[rt][pp] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, al, acc1[rt][pp], 0, 0, 0);
+                        acc1[rt][pp] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, ah, acc1[rt][pp], 0, 0, 0);
+                    }
+                }
+                __builtin_amdgcn_sched_group_barrier(0x008, 24, 0);
+                __builtin_amdgcn_sched_barrier(0);                      // nothing crosses groups
+                if (j == 7) {
+                    // bias + ReLU + S, split: the chunk's linear2 B fragments -> the hand-off buffer
+#pragma unroll
+                    for (int rt = 0; rt < 4; ++rt) {
+                        const float2 rp = rowpar[16 * rt + c];
+                        float hv[8];
+#pragma unroll
+                        for (int pp = 0; pp < 2; ++pp) {
+                            const int n = 32 * ch + 16 * pp + 4 * g;
+                            const float4 w4 = cw1[n / 4], b4 = cb1[n / 4];
+                            hv[4 * pp + 0] = fmaxf(fmaf(acc1[rt][pp][0], rp.x * w4.x, rp.y * b4.x), 0.f);
+                            hv[4 * pp + 1] = fmaxf(fmaf(acc1[rt][pp][1], rp.x * w4.y, rp.y * b4.y), 0.f);
+                            hv[4 * pp + 2] = fmaxf(fmaf(acc1[rt][pp][2], rp.x * w4.z, rp.y * b4.z), 0.f);
+                            hv[4 * pp + 3] = fmaxf(fmaf(acc1[rt][pp][3], rp.x * w4.w, rp.y * b4.w), 0.f);
+                        }
+                        u32x4 h, l;
+                        split8_f16(hv, 1.f, h, l);
+                        hbuf[st & 1][wv][rt][0][lane] = h;
+                        hbuf[st & 1][wv][rt][1][lane] = l;
+                    }
+                    // every wave's chunk in LDS (and every wave done with the buffer's previous
+                    // use, step st - 2, which ended before its barrier of step st - 1)
+                    __builtin_amdgcn_s_waitcnt((15) | (7 << 4) | (0 << 8) | (3 << 14));   // lgkmcnt(0)
+                    __builtin_amdgcn_s_barrier();
+                    read_h(st & 1, 0, fa[0]);
+                }
+            } else {
+                // linear2: source wave sw's chunk (k32 step of 32 hidden), output panels 2 qh, +1
+                const int sw = (j - 8) >> 1, qh = (j - 8) & 1;
+                u32x4 (&cur)[8] = fa[sw & 1];
+                const bool pre = qh == 0 && sw < 3;
+                if (pre) read_h(st & 1, sw + 1, fa[(sw + 1) & 1]);
+                __builtin_amdgcn_sched_group_barrier(0x020, 4, 0);
+                if (pre) __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+#pragma unroll
+                for (int rt = 0; rt < 4; ++rt) {
+                    const f16x8 hh = __builtin_bit_cast(f16x8, cur[2 * rt + 0]);
+                    const f16x8 hl = __builtin_bit_cast(f16x8, cur[2 * rt + 1]);
+#pragma unroll
+                    for (int qq = 0; qq < 2; ++qq) {
+                        const f16x8 wh = __builtin_bit_cast(f16x8, wf[2 * qq]);
+                        const f16x8 wl = __builtin_bit_cast(f16x8, wf[2 * qq + 1]);
+                        f32x4& a = accy[rt][2 * qh + qq];
+                        a = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, hh, a, 0, 0, 0);
+                        a = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, hl, a, 0, 0, 0);
+                        a = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, hh, a, 0, 0, 0);
+                    }
+                }
+                __builtin_amdgcn_sched_group_barrier(0x008, 24, 0);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+    }
+    wait_vm_only(0);                                      // the last step's redundant look-ahead
+
+    // 4. y = acc * wsc2 / S + b2 + x for the wave's 4 output panels of the 64 rows
+#pragma unroll
+    for (int rt = 0; rt < 4; ++rt) {
+        const int rr = r0 + 16 * rt + c;
+        const int64_t row = min(rr, p.M - 1);
+        const float inv_s = 1.f / rowpar[16 * rt + c].y;       // exact: a power of two
+        const float* xrow = p.x + row * p.ldx;
+        float4 res[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) res[q] = *reinterpret_cast<const float4*>(xrow + 16 * (4 * wv + q) + 4 * g);
+        float* orow = p.out + row * p.ldo;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int n = 16 * (4 * wv + q) + 4 * g;
+            const float4 w4 = cw2[n / 4], b4 = cb2[n / 4];
+            const float4 y = make_float4(fmaf(accy[rt][q][0], w4.x * inv_s, b4.x) + res[q].x,
+                                         fmaf(accy[rt][q][1], w4.y * inv_s, b4.y) + res[q].y,
+                                         fmaf(accy[rt][q][2], w4.z * inv_s, b4.z) + res[q].z,
+                                         fmaf(accy[rt][q][3], w4.w * inv_s, b4.w) + res[q].w);
+            if (rr < p.M) *reinterpret_cast<float4*>(orow + n) = y;
+        }
+    }
+}
+
 // W2 (d, F) -> the chunk-major, k-permuted f16x3 image: block = output panel q (16 rows);
 // unit (chunk cc, panel q, term t, g, i) holds W2s[16 q + i][32 cc + 16 (e / 4) + 4 g + e % 4],
 // e = 0..7, W2s = the row scaled by 2^e_row (max in [2^14, 2^15)); then wsc2[n] = 2^-e_row
@@ -520,7 +821,12 @@ extern "C" int fgr_ffn_f16x3(const float* x, int64_t ldx, const float* gamma, co
               (const u32x4*)i1, (const float*)(i1 + (size_t)(f / 16) * kFfnKS * 128 * 16), b1,
               (const u32x4*)i2, (const float*)(i2 + ffn_image_bytes(d, f)), b2,
               bound, out, ldo, m, f};
-    hipLaunchKernelGGL(ffn_f16x3_kernel, dim3((unsigned)((m + 63) / 64)), dim3(256), 0, st, a);
+    // FGR_FFN_V=1: the LDS-ring version (A/B); default the weight-split version 2 (f % 128 == 0)
+    static const int ver = [] { const char* e = getenv("FGR_FFN_V"); return (e && e[0] == '1') ? 1 : 2; }();
+    if (ver == 2 && f % 128 == 0)
+        hipLaunchKernelGGL(ffn_nsplit_kernel, dim3((unsigned)((m + 63) / 64)), dim3(256), 0, st, a);
+    else
+        hipLaunchKernelGGL(ffn_f16x3_kernel, dim3((unsigned)((m + 63) / 64)), dim3(256), 0, st, a);
     FGR_CHECK_LAUNCH("ffn_f16x3_kernel");
     return FGR_OK;
 }
