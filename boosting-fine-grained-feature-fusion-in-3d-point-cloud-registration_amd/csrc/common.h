@@ -186,4 +186,16 @@ int attn_bwd_f16x3(const float* q, int64_t ldq, const float* k, int64_t ldk, con
                    float* lse_out, float* dsum_out, bool dkdv, void* ws, uint32_t drop_seed,
                    uint32_t drop_thresh, float inv_keep, hipStream_t st);
 
+// gemm_ws.hip: the weight-split row-stationary f16x3 GEMM (K = 256, N = 256 / 768, many rows);
+// `ln` (optional): LayerNorm prologue (+ add, + side output out2, + K / V attention images)
+struct WsLn {
+    const float* g; const float* b; const float* add; int64_t ld_add; float eps;
+    const float* g2; const float* b2; float* out2; int64_t ld_out2;
+    char* kv_img; int2* kv_sc; int n_head; int kv_col0;
+};
+bool gemm_ws_supported(int m, int n, int k);
+bool gemm_ws_f16x3(const float* A, int64_t lda, const void* W, const float* wsc, float* C,
+                   int64_t ldc, const float* bias, const float* R, int64_t ldr, int M, int N,
+                   int K, int act, hipStream_t st, const WsLn* ln);
+
 }  // namespace fgr

@@ -442,16 +442,21 @@ __global__ void __launch_bounds__(256, 1) ffn_f16x3_kernel(FfnArgs p) {
 // fragment reads, 384 MFMAs; 8 barriers per launch at F = 1024. The weight loads run 3 groups
 // (12 loads) ahead of their MFMAs through a 4-group register ring.
 constexpr int kV2Groups = 16;          // load groups per step: 8 linear1 k32 steps, 8 linear2 halves
-constexpr int kV2Ring = 4;             // register ring of groups (3 in flight while one computes)
+#ifndef FGR_FFN_RING
+#define FGR_FFN_RING 4
+#endif
+constexpr int kV2Ring = FGR_FFN_RING;  // register ring of groups (kV2Ring - 1 in flight)
 static_assert(kV2Groups % kV2Ring == 0, "ring slot = group index mod kV2Ring at compile time");
 
-// s_waitcnt vmcnt(n) (lgkmcnt / expcnt untouched) for n <= 12
+// s_waitcnt vmcnt(n) (lgkmcnt / expcnt untouched) for n = 4 k <= 28
 __device__ __forceinline__ void wait_vm_only(int n) {
     // vmcnt field bits 3:0 and 15:14, expcnt 6:4 = 7, lgkmcnt 11:8 = 15 (no wait)
 #define FGR_VMW(N) __builtin_amdgcn_s_waitcnt(((N) & 15) | (((N) >> 4) << 14) | (7 << 4) | (15 << 8))
     switch (n) {
         case 0: FGR_VMW(0); break;   case 4: FGR_VMW(4); break;
-        case 8: FGR_VMW(8); break;   default: FGR_VMW(12); break;
+        case 8: FGR_VMW(8); break;   case 12: FGR_VMW(12); break;
+        case 16: FGR_VMW(16); break; case 20: FGR_VMW(20); break;
+        case 24: FGR_VMW(24); break; default: FGR_VMW(28); break;
     }
 #undef FGR_VMW
 }
@@ -475,7 +480,20 @@ __global__ void __launch_bounds__(256, 1) ffn_nsplit_kernel(FfnArgs p) {
     const int r0 = t * 64;                                // the block's first row
     const int nst = p.F / 128;                            // steps of 128 hidden units
 
-    // 1. this wave's row tile (rows r0 + 16 wv + c), parameters -> LDS
+    // 1. parameters (issued first: their LDS stores wait for them alone), this wave's row tile
+    //    (rows r0 + 16 wv + c); parameters -> LDS
+    const int nf4 = p.F / 4;
+    const int j0 = min(tid, nf4 - 1), j1 = min(tid + 256, nf4 - 1);
+    const float4 pw1a = reinterpret_cast<const float4*>(p.wsc1)[j0];
+    const float4 pb1a = reinterpret_cast<const float4*>(p.b1)[j0];
+    const float4 pw1b = reinterpret_cast<const float4*>(p.wsc1)[j1];
+    const float4 pb1b = reinterpret_cast<const float4*>(p.b1)[j1];
+    const int t4 = tid & (kFfnD / 4 - 1);
+    const float4 pw2 = reinterpret_cast<const float4*>(p.wsc2)[t4];
+    const float4 pb2 = reinterpret_cast<const float4*>(p.b2)[t4];
+    const float4 pg = reinterpret_cast<const float4*>(p.ln_g)[t4];
+    const float4 pbe = reinterpret_cast<const float4*>(p.ln_b)[t4];
+    __builtin_amdgcn_sched_barrier(0);                    // keep them ahead of the row loads
     float xr[kFfnKS][8];
     {
         const int64_t row = min(r0 + 16 * wv + c, p.M - 1);
@@ -489,17 +507,6 @@ __global__ void __launch_bounds__(256, 1) ffn_nsplit_kernel(FfnArgs p) {
         }
     }
     {
-        const int nf4 = p.F / 4;
-        const int j0 = min(tid, nf4 - 1), j1 = min(tid + 256, nf4 - 1);
-        const float4 pw1a = reinterpret_cast<const float4*>(p.wsc1)[j0];
-        const float4 pb1a = reinterpret_cast<const float4*>(p.b1)[j0];
-        const float4 pw1b = reinterpret_cast<const float4*>(p.wsc1)[j1];
-        const float4 pb1b = reinterpret_cast<const float4*>(p.b1)[j1];
-        const int t4 = tid & (kFfnD / 4 - 1);
-        const float4 pw2 = reinterpret_cast<const float4*>(p.wsc2)[t4];
-        const float4 pb2 = reinterpret_cast<const float4*>(p.b2)[t4];
-        const float4 pg = reinterpret_cast<const float4*>(p.ln_g)[t4];
-        const float4 pbe = reinterpret_cast<const float4*>(p.ln_b)[t4];
         if (tid < nf4) { cw1[tid] = pw1a; cb1[tid] = pb1a; }
         if (tid + 256 < nf4) { cw1[tid + 256] = pw1b; cb1[tid + 256] = pb1b; }
         if (tid < kFfnD / 4) { cw2[tid] = pw2; cb2[tid] = pb2; lng[tid] = pg; lnb[tid] = pbe; }

@@ -1354,6 +1354,13 @@ static int gemm_f16x3_impl(const float* a, int64_t lda, const void* w_img, float
     // for tuning (a = 128x128, b = 64x128, c = 64x64, d = 128x64, e..x: v2-v4 variants, A..Z,
     // 0..9: g5)
     char cfg = h3_tile(m, n, k);
+    // ws (gemm_ws.hip): K = 256, N = 256 / 768 over many rows, 16-B aligned operands
+    if (vec && vo && (!bias || (reinterpret_cast<uintptr_t>(bias) & 15) == 0) &&
+        getenv("FGR_GEMM16_TILE") == nullptr &&
+        gemm_ws_f16x3(a, lda, w_img, wsc, c, ldc, bias, r, ldr, m, n, k, act, st, nullptr)) {
+        FGR_CHECK_LAUNCH("gemm_ws");
+        return FGR_OK;
+    }
     // rs (gemm_rs.hip): K <= 256, 16-B aligned operands
     if (cfg == 'z') {
         if (vec && vo && gemm_rs_f16x3(a, lda, w_img, ksteps_h3(k), wsc, c, ldc, bias, r, ldr, m,
@@ -1435,7 +1442,7 @@ extern "C" int fgr_gemm_f16x3_ws(const float* a, int64_t lda, const void* w_img,
 // LayerNorm -> (+ add) -> Linear in one launch (the row-stationary kernel's LN prologue,
 // gemm_rs.hip): supported where the dispatcher picks that kernel for (m, n, k).
 extern "C" int fgr_gemm_f16x3_ln_supported(int32_t m, int32_t n, int32_t k) {
-    return (m > 0 && n > 0 && k > 0 && h3_tile(m, n, k) == 'z') ? 1 : 0;
+    return (m > 0 && n > 0 && k > 0 && (gemm_ws_supported(m, n, k) || h3_tile(m, n, k) == 'z')) ? 1 : 0;
 }
 
 static int gemm_f16x3_ln_impl(const float* x, int64_t ldx, const float* gamma, const float* beta,
@@ -1464,6 +1471,13 @@ static int gemm_f16x3_ln_impl(const float* x, int64_t ldx, const float* gamma, c
                                                       image_bytes_h3(n, k));
     hipStream_t st = as_stream(stream);
     TimedCall timed_(st);
+    if (act == FGR_ACT_NONE || act == FGR_ACT_RELU) {
+        const WsLn wl{gamma, beta, add, ld_add, eps, gamma2, beta2, out2, ld_out2, nullptr, nullptr, 0, 0};
+        if (gemm_ws_f16x3(x, ldx, w_img, wsc, c, ldc, bias, nullptr, 0, m, n, k, act, st, &wl)) {
+            FGR_CHECK_LAUNCH("gemm_ws_ln");
+            return FGR_OK;
+        }
+    }
     const RsLn ln{gamma, beta, add, ld_add, eps, gamma2, beta2, out2, ld_out2, nullptr, nullptr, 0, 0};
     FGR_REQUIRE(gemm_rs_f16x3(x, ldx, w_img, ksteps_h3(k), wsc, c, ldc, bias, nullptr, 0, m, n, k,
                               act, st, &ln),
@@ -1609,6 +1623,15 @@ extern "C" int fgr_gemm_f16x3_ln_qkv(const float* x, int64_t ldx, const float* g
     const int64_t nt = ceil_div(m, 64) * n_head;
     hipStream_t st = as_stream(stream);
     TimedCall timed_(st);
+    {
+        const WsLn wl{gamma, beta, add, ld_add, eps, gamma2, beta2, out2, ld_out2,
+                      static_cast<char*>(kv_img),
+                      reinterpret_cast<int2*>(static_cast<char*>(kv_img) + nt * 1024 * 16), n_head, d};
+        if (gemm_ws_f16x3(x, ldx, w_img, wsc, q, ld_q, bias, nullptr, 0, m, n, d, FGR_ACT_NONE, st, &wl)) {
+            FGR_CHECK_LAUNCH("gemm_ws_ln_qkv");
+            return FGR_OK;
+        }
+    }
     const RsLn ln{gamma, beta, add, ld_add, eps, gamma2, beta2, out2, ld_out2,
                   static_cast<char*>(kv_img),
                   reinterpret_cast<int2*>(static_cast<char*>(kv_img) + nt * 1024 * 16), n_head, d};

@@ -313,7 +313,8 @@ def _res2net_case(gpu, cin, cout, my_Bottle2neck, my_res2Net):
 
 
 @pytest.mark.parametrize('m,n,k', [(11472, 128, 1920), (9200, 1024, 2048), (1000, 3, 256),
-                                   (333, 896, 128), (64, 256, 36), (5000, 768, 256)])
+                                   (333, 896, 128), (64, 256, 36), (5000, 768, 256),
+                                   (9544, 256, 256), (4097, 256, 256)])
 def test_gemm_split_vs_fp64(gpu, m, n, k):
     """The f16x3 GEMM vs fp64, bias / ReLU / residual / ReLU-residual-LeakyReLU epilogues,
     strided A, the KPConv weight layout, a row slice of a cached weight: at fp32 level, no
@@ -383,6 +384,34 @@ def test_gemm_f16x3_dynamic_range(gpu, tile, monkeypatch):
     err = ((out - ref32).abs() / den).max()
     assert err < 2e-6, float(err)
     del ref
+
+
+@pytest.mark.parametrize('n', [256, 768])
+def test_gemm_ws_dynamic_range(gpu, n):
+    """The weight-split row-stationary kernel (gemm_ws.hip: K = 256, N = 256 / 768, >= 4096
+    rows, one scale per row) under the adversarial magnitudes of test_gemm_f16x3_dynamic_range:
+    every output row within 2e-6 of its own scale."""
+    from fgreg import linear as fl
+    from fgreg import _lib
+    m, k = 4200, 256
+    assert _lib.load().fgr_gemm_f16x3_ln_supported(m, n, k)
+    g = torch.Generator().manual_seed(n)
+    x = torch.randn(m, k, generator=g, dtype=torch.float64)
+    x *= torch.tensor([10.0 ** e for e in np.linspace(-15, 15, m)], dtype=torch.float64)[:, None]
+    x[5] = 0
+    x[17, :160] = 0
+    ramp = torch.pow(2.0, torch.linspace(0, 40, k, dtype=torch.float64))
+    x[30:60] *= ramp
+    x[60:90] *= ramp.flip(0)
+    w = torch.randn(n, k, generator=g, dtype=torch.float64) / math.sqrt(k)
+    w[3] *= 1e-10
+    w[4] *= 1e10
+    X, W = x.float().to(gpu), w.float().to(gpu)
+    ref32 = X.double().cpu() @ W.double().cpu().t()
+    out = fl.linear(X, W).double().cpu()
+    assert torch.isfinite(out).all() and (out[5] == 0).all()
+    den = (X.double().cpu().abs() @ W.double().cpu().abs().t()).clamp_min(1e-300)
+    assert float(((out - ref32).abs() / den).max()) < 2e-6
 
 
 @pytest.mark.parametrize('tile', list('abcdefghijklmnopqrstuvwxyz') + list('ABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789'))

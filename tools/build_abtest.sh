@@ -11,7 +11,7 @@ rm -rf $tmp && mkdir -p $tmp/pkg/csrc $tmp/pkg/fgreg $tmp/include $root/abtest
 cp $pkg/csrc/*.hip $pkg/csrc/*.h $pkg/csrc/*.cpp $pkg/csrc/Makefile $tmp/pkg/csrc/
 cp $pkg/csrc/*.o $tmp/pkg/csrc/ 2>/dev/null || true
 cp $root/include/*.h $tmp/include/
-touch $tmp/pkg/csrc/ffn.hip
+for f in ${TOUCH:-ffn.hip gemm_ws.hip}; do touch $tmp/pkg/csrc/$f; done
 make -C $tmp/pkg/csrc -j8 \
     "COMMON=-O3 -std=c++17 -fPIC --offload-arch=gfx950 -fhip-fp32-correctly-rounded-divide-sqrt -Wall -Wno-unused-function -mllvm -amdgpu-mfma-vgpr-form=1 $extra" > $tmp/build.log 2>&1 \
   || { tail -30 $tmp/build.log; exit 1; }
