@@ -110,6 +110,38 @@ def test_instnorm_fusions_vs_torch(gpu, lens, c, mu):
                    ref_res) < TOL
 
 
+@pytest.mark.parametrize('lens,c', [([20000, 13389], 64), ([1025, 30000, 2, 4097, 1500], 128),
+                                    ([6000, 2100], 1024)])
+def test_instnorm_long_repeat_and_graph(gpu, lens, c):
+    """The long-segment path (shifted sums, fp64 merge): repeated eager calls and HIP-graph
+    replays give the same bits and match the oracle; short segments beside long ones, 1024
+    channels (one row per 256-thread iteration)."""
+    import fgreg.ops as ops
+    rng = np.random.default_rng(11)
+    x = torch.from_numpy(rng.normal(7.0, 2.0, (sum(lens), c)).astype(np.float32))
+    ref = torch.nn.functional.leaky_relu(mo.instance_norm(x, torch.tensor(lens)), 0.1)
+    off = ops.offsets(lens, gpu)
+    X = x.to(gpu)
+    outs = [ops.instnorm(X, off, lens, act=ops.ACT_LEAKY) for _ in range(3)]
+    assert rel_err(outs[0], ref) < TOL
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    out = torch.empty_like(X)
+    with torch.cuda.stream(s):
+        ops.instnorm(X, off, lens, act=ops.ACT_LEAKY, out=out)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        ops.instnorm(X, off, lens, act=ops.ACT_LEAKY, out=out)
+    for _ in range(3):
+        out.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, outs[0])
+
+
 @pytest.mark.parametrize('d', [32, 256, 512])
 def test_sine_pos_embed_vs_reference(gpu, d):
     import fgreg.ops as ops
