@@ -442,6 +442,7 @@ __global__ void __launch_bounds__(256, 1) ffn_f16x3_kernel(FfnArgs p) {
 // fragment reads, 384 MFMAs; 8 barriers per launch at F = 1024. The weight loads run 3 groups
 // (12 loads) ahead of their MFMAs through a 4-group register ring.
 constexpr int kV2Groups = 16;          // load groups per step: 8 linear1 k32 steps, 8 linear2 halves
+constexpr int kCusFfn = 256;           // MI355X compute units (one block per CU)
 #ifndef FGR_FFN_RING
 #define FGR_FFN_RING 4
 #endif
@@ -461,15 +462,20 @@ __device__ __forceinline__ void wait_vm_only(int n) {
 #undef FGR_VMW
 }
 
+// RT row tiles per block (16 RT rows): 4, or 3 where 48-row blocks still fit the CUs in one
+// round (ModelNet's 9544 rows: 199 blocks instead of 150 -- every block 25 % shorter)
+template <int RT>
 __global__ void __launch_bounds__(256, 1) ffn_nsplit_kernel(FfnArgs p) {
-    __shared__ u32x4 act[4 * kFfnKS * 2 * 64];            // [row tile][k32 step][term][lane]
-    __shared__ u32x4 hbuf[2][4][4][2][64];                // [step & 1][src wave][row tile][term][lane]
+    static_assert(RT >= 1 && RT <= 4, "row tiles");
+    __shared__ u32x4 act[RT * kFfnKS * 2 * 64];           // [row tile][k32 step][term][lane]
+    __shared__ u32x4 hbuf[2][4][RT][2][64];               // [step & 1][src wave][row tile][term][lane]
     __shared__ float4 cw1[kFfnMaxF / 4], cb1[kFfnMaxF / 4];
     __shared__ float4 cw2[kFfnD / 4], cb2[kFfnD / 4];
     __shared__ float4 lng[kFfnD / 4], lnb[kFfnD / 4];
     __shared__ float2 rowpar[64];                         // per row: (rs_a S, S)
 
-    const int nbm = (p.M + 63) / 64;
+    constexpr int BR = 16 * RT;                           // rows per block
+    const int nbm = (p.M + BR - 1) / BR;
     int t = blockIdx.x;
     {   // XCD-aware order: each XCD a contiguous range of row blocks
         const int q = nbm / 8, r = nbm % 8, x = t % 8, lo = t / 8;
@@ -477,7 +483,7 @@ __global__ void __launch_bounds__(256, 1) ffn_nsplit_kernel(FfnArgs p) {
     }
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
     const int g = lane >> 4, c = lane & 15;
-    const int r0 = t * 64;                                // the block's first row
+    const int r0 = t * BR;                                // the block's first row
     const int nst = p.F / 128;                            // steps of 128 hidden units
 
     // 1. parameters (issued first: their LDS stores wait for them alone), this wave's row tile
@@ -496,7 +502,7 @@ __global__ void __launch_bounds__(256, 1) ffn_nsplit_kernel(FfnArgs p) {
     __builtin_amdgcn_sched_barrier(0);                    // keep them ahead of the row loads
     float xr[kFfnKS][8];
     {
-        const int64_t row = min(r0 + 16 * wv + c, p.M - 1);
+        const int64_t row = min(r0 + 16 * min(wv, RT - 1) + c, p.M - 1);   // RT < 4: wave 3 idles
         const float* ar = p.x + row * p.ldx;
 #pragma unroll
         for (int s = 0; s < kFfnKS; ++s) {
@@ -553,16 +559,19 @@ __global__ void __launch_bounds__(256, 1) ffn_nsplit_kernel(FfnArgs p) {
         nn = xg_sum_f(nn);
         const int ea = mx > 0.f ? min(15 - __builtin_amdgcn_frexp_expf(mx), 127) : 0;
         const float sca = __builtin_ldexpf(1.f, ea);
+        if (wv < RT) {
 #pragma unroll
-        for (int s = 0; s < kFfnKS; ++s) {
-            u32x4 h, l;
-            split8_f16(xr[s], sca, h, l);
-            act[((wv * kFfnKS + s) * 2 + 0) * 64 + lane] = h;
-            act[((wv * kFfnKS + s) * 2 + 1) * 64 + lane] = l;
+            for (int s = 0; s < kFfnKS; ++s) {
+                u32x4 h, l;
+                split8_f16(xr[s], sca, h, l);
+                act[((wv * kFfnKS + s) * 2 + 0) * 64 + lane] = h;
+                act[((wv * kFfnKS + s) * 2 + 1) * 64 + lane] = l;
+            }
         }
         const float bnd = sqrtf(nn) * bM1 + bMb;
         const int eh = bnd > 0.f ? max(min(15 - __builtin_amdgcn_frexp_expf(bnd), 127), -126) : 0;
-        if (g == 0) rowpar[16 * wv + c] = make_float2(__builtin_ldexpf(1.f, eh - ea), __builtin_ldexpf(1.f, eh));
+        if (g == 0 && wv < RT)
+            rowpar[16 * wv + c] = make_float2(__builtin_ldexpf(1.f, eh - ea), __builtin_ldexpf(1.f, eh));
     }
     __syncthreads();
 
@@ -587,9 +596,9 @@ __global__ void __launch_bounds__(256, 1) ffn_nsplit_kernel(FfnArgs p) {
         }
     };
     u32x4 ring[kV2Ring][4];
-    f32x4 accy[4][4];                                     // [row tile][output panel of the wave]
+    f32x4 accy[RT][4];                                    // [row tile][output panel of the wave]
 #pragma unroll
-    for (int rt = 0; rt < 4; ++rt)
+    for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
         for (int q = 0; q < 4; ++q) accy[rt][q] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -597,17 +606,17 @@ __global__ void __launch_bounds__(256, 1) ffn_nsplit_kernel(FfnArgs p) {
     // LDS fragments of a group, double-buffered: the 4 row tiles' (hi, lo) row-image fragments
     // of a k32 step (linear1), or the 4 row tiles' (hi, lo) hidden fragments of a source wave
     // (linear2); the next group's are read while this group's MFMAs run
-    u32x4 fa[2][8];
-    auto read_act = [&](int s, u32x4 (&f)[8]) {
+    u32x4 fa[2][2 * RT];
+    auto read_act = [&](int s, u32x4 (&f)[2 * RT]) {
 #pragma unroll
-        for (int rt = 0; rt < 4; ++rt) {
+        for (int rt = 0; rt < RT; ++rt) {
             f[2 * rt + 0] = act[((rt * kFfnKS + s) * 2 + 0) * 64 + lane];
             f[2 * rt + 1] = act[((rt * kFfnKS + s) * 2 + 1) * 64 + lane];
         }
     };
-    auto read_h = [&](int buf, int sw, u32x4 (&f)[8]) {
+    auto read_h = [&](int buf, int sw, u32x4 (&f)[2 * RT]) {
 #pragma unroll
-        for (int rt = 0; rt < 4; ++rt) {
+        for (int rt = 0; rt < RT; ++rt) {
             f[2 * rt + 0] = hbuf[buf][sw][rt][0][lane];
             f[2 * rt + 1] = hbuf[buf][sw][rt][1][lane];
         }
@@ -618,9 +627,9 @@ __global__ void __launch_bounds__(256, 1) ffn_nsplit_kernel(FfnArgs p) {
         // the last step's look-ahead re-reads its own groups (no branch in the body; drained
         // after the loop)
         const int stn = min(st + 1, nst - 1);
-        f32x4 acc1[4][2];
+        f32x4 acc1[RT][2];
 #pragma unroll
-        for (int rt = 0; rt < 4; ++rt) acc1[rt][0] = acc1[rt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int rt = 0; rt < RT; ++rt) acc1[rt][0] = acc1[rt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
         read_act(0, fa[0]);
 #pragma unroll
         for (int j = 0; j < kV2Groups; ++j) {
@@ -629,13 +638,13 @@ __global__ void __launch_bounds__(256, 1) ffn_nsplit_kernel(FfnArgs p) {
             wait_vm_only(4 * (kV2Ring - 1));              // group j landed
             u32x4 (&wf)[4] = ring[j % kV2Ring];
             if (j < 8) {
-                u32x4 (&cur)[8] = fa[j & 1];
+                u32x4 (&cur)[2 * RT] = fa[j & 1];
                 if (j < 7) read_act(j + 1, fa[(j + 1) & 1]);
                 __builtin_amdgcn_sched_group_barrier(0x020, 4, 0);      // this group's + 3 loads
-                if (j < 7) __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);   // next reads
-                // linear1 k32 step j: W1 (panel pp, term) x the 4 row tiles' fragments
+                if (j < 7) __builtin_amdgcn_sched_group_barrier(0x100, 2 * RT, 0);   // next reads
+                // linear1 k32 step j: W1 (panel pp, term) x the row tiles' fragments
 #pragma unroll
-                for (int rt = 0; rt < 4; ++rt) {
+                for (int rt = 0; rt < RT; ++rt) {
                     const f16x8 ah = __builtin_bit_cast(f16x8, cur[2 * rt + 0]);
                     const f16x8 al = __builtin_bit_cast(f16x8, cur[2 * rt + 1]);
 #pragma unroll
@@ -647,12 +656,12 @@ __global__ void __launch_bounds__(256, 1) ffn_nsplit_kernel(FfnArgs p) {
                         acc1[rt][pp] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, ah, acc1[rt][pp], 0, 0, 0);
                     }
                 }
-                __builtin_amdgcn_sched_group_barrier(0x008, 24, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 6 * RT, 0);
                 __builtin_amdgcn_sched_barrier(0);                      // nothing crosses groups
                 if (j == 7) {
                     // bias + ReLU + S, split: the chunk's linear2 B fragments -> the hand-off buffer
 #pragma unroll
-                    for (int rt = 0; rt < 4; ++rt) {
+                    for (int rt = 0; rt < RT; ++rt) {
                         const float2 rp = rowpar[16 * rt + c];
                         float hv[8];
 #pragma unroll
@@ -678,13 +687,13 @@ __global__ void __launch_bounds__(256, 1) ffn_nsplit_kernel(FfnArgs p) {
             } else {
                 // linear2: source wave sw's chunk (k32 step of 32 hidden), output panels 2 qh, +1
                 const int sw = (j - 8) >> 1, qh = (j - 8) & 1;
-                u32x4 (&cur)[8] = fa[sw & 1];
+                u32x4 (&cur)[2 * RT] = fa[sw & 1];
                 const bool pre = qh == 0 && sw < 3;
                 if (pre) read_h(st & 1, sw + 1, fa[(sw + 1) & 1]);
                 __builtin_amdgcn_sched_group_barrier(0x020, 4, 0);
-                if (pre) __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+                if (pre) __builtin_amdgcn_sched_group_barrier(0x100, 2 * RT, 0);
 #pragma unroll
-                for (int rt = 0; rt < 4; ++rt) {
+                for (int rt = 0; rt < RT; ++rt) {
                     const f16x8 hh = __builtin_bit_cast(f16x8, cur[2 * rt + 0]);
                     const f16x8 hl = __builtin_bit_cast(f16x8, cur[2 * rt + 1]);
 #pragma unroll
@@ -697,16 +706,16 @@ __global__ void __launch_bounds__(256, 1) ffn_nsplit_kernel(FfnArgs p) {
                         a = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, hh, a, 0, 0, 0);
                     }
                 }
-                __builtin_amdgcn_sched_group_barrier(0x008, 24, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 6 * RT, 0);
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
     }
     wait_vm_only(0);                                      // the last step's redundant look-ahead
 
-    // 4. y = acc * wsc2 / S + b2 + x for the wave's 4 output panels of the 64 rows
+    // 4. y = acc * wsc2 / S + b2 + x for the wave's 4 output panels of the block's rows
 #pragma unroll
-    for (int rt = 0; rt < 4; ++rt) {
+    for (int rt = 0; rt < RT; ++rt) {
         const int rr = r0 + 16 * rt + c;
         const int64_t row = min(rr, p.M - 1);
         const float inv_s = 1.f / rowpar[16 * rt + c].y;       // exact: a power of two
@@ -830,9 +839,20 @@ extern "C" int fgr_ffn_f16x3(const float* x, int64_t ldx, const float* gamma, co
               bound, out, ldo, m, f};
     // FGR_FFN_V=1: the LDS-ring version (A/B); default the weight-split version 2 (f % 128 == 0)
     static const int ver = [] { const char* e = getenv("FGR_FFN_V"); return (e && e[0] == '1') ? 1 : 2; }();
-    if (ver == 2 && f % 128 == 0)
-        hipLaunchKernelGGL(ffn_nsplit_kernel, dim3((unsigned)((m + 63) / 64)), dim3(256), 0, st, a);
-    else
+    // row tiles per block (version 2): 3 when 48-row blocks fit one round of the CUs and
+    // 64-row ones do not fill them, else 4 (FGR_FFN_RT overrides: A/B)
+    static const int rt_env = [] { const char* e = getenv("FGR_FFN_RT"); return e ? atoi(e) : 0; }();
+    const int rt = (rt_env >= 1 && rt_env <= 4) ? rt_env
+                   : ((m + 47) / 48 <= kCusFfn && (m + 63) / 64 < kCusFfn) ? 3 : 4;
+    if (ver == 2 && f % 128 == 0) {
+        const unsigned nb = (unsigned)((m + 16 * rt - 1) / (16 * rt));
+        switch (rt) {
+            case 1: hipLaunchKernelGGL(ffn_nsplit_kernel<1>, dim3(nb), dim3(256), 0, st, a); break;
+            case 2: hipLaunchKernelGGL(ffn_nsplit_kernel<2>, dim3(nb), dim3(256), 0, st, a); break;
+            case 3: hipLaunchKernelGGL(ffn_nsplit_kernel<3>, dim3(nb), dim3(256), 0, st, a); break;
+            default: hipLaunchKernelGGL(ffn_nsplit_kernel<4>, dim3(nb), dim3(256), 0, st, a); break;
+        }
+    } else
         hipLaunchKernelGGL(ffn_f16x3_kernel, dim3((unsigned)((m + 63) / 64)), dim3(256), 0, st, a);
     FGR_CHECK_LAUNCH("ffn_f16x3_kernel");
     return FGR_OK;

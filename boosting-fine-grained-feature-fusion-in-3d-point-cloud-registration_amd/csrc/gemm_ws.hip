@@ -109,27 +109,29 @@ __device__ __forceinline__ float finish_ws(float y, float b, float r) {
 // stay in registers (64 per pass and lane), the side output (LNM 3) in LDS, and the stores go
 // out after the last MFMA. The first weight groups are requested with the rows, and the column
 // scales / bias sit in LDS.
-template <int NPW, int LNM, bool KV, bool RES, int ACT>
+template <int NPW, int LNM, bool KV, bool RES, int ACT, int RT>
 __global__ void __launch_bounds__(256, 1) gemm_ws_kernel(WsArgs p) {
     static_assert(NPW % 4 == 0, "passes of 4 panels");
+    static_assert(RT >= 1 && RT <= 4 && (!KV || RT == 4), "row tiles (K / V images: 64-row tiles)");
+    constexpr int BR = 16 * RT;                           // rows per block
     static_assert(!KV || (LNM >= 2 && !RES && ACT == FGR_ACT_NONE), "K / V images: the in_proj");
     constexpr int NPASS = NPW / 4;
     constexpr int N = 64 * NPW;
     // RES, one pass: the residual is loaded with the weights and added before the activation;
     // several passes (registers): fin holds y + b and the store stage adds the residual
     constexpr bool kResEarly = RES && NPASS == 1;
-    __shared__ u32x4 act[4 * kWsKS * 2 * 64];             // [row tile][k32 step][term][lane]
-    __shared__ float rowrs[64];                           // per row: 2^-e
+    __shared__ u32x4 act[RT * kWsKS * 2 * 64];            // [row tile][k32 step][term][lane]
+    __shared__ float rowrs[BR];                           // per row: 2^-e
     __shared__ float4 colw[N / 4], colb[N / 4];           // per column: 2^-e_n, bias
     __shared__ float4 lng[LNM ? 64 : 1], lnb[LNM ? 64 : 1];
     __shared__ float4 lng2[LNM == 3 ? 64 : 1], lnb2[LNM == 3 ? 64 : 1];
-    __shared__ float4 side[LNM == 3 ? 64 * 64 : 1];       // LNM 3: out2 rows, row-major
+    __shared__ float4 side[LNM == 3 ? BR * 64 : 1];       // LNM 3: out2 rows, row-major
 
 #ifdef FGR_WS_STAMP
     unsigned long long st_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     st_[0] = __builtin_amdgcn_s_memtime();
 #endif
-    const int nbm = (p.M + 63) / 64;
+    const int nbm = (p.M + BR - 1) / BR;
     int t = blockIdx.x;
     {   // XCD-aware order: each XCD a contiguous range of row blocks
         const int q = nbm / 8, r = nbm % 8, x = t % 8, lo = t / 8;
@@ -137,8 +139,8 @@ __global__ void __launch_bounds__(256, 1) gemm_ws_kernel(WsArgs p) {
     }
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
     const int g = lane >> 4, c = lane & 15;
-    const int r0 = t * 64;
-    const int rrow = r0 + 16 * wv + c;                    // the lane's prologue row
+    const int r0 = t * BR;
+    const int rrow = r0 + 16 * min(wv, RT - 1) + c;       // the lane's prologue row (RT < 4: wave 3 idles)
     const int64_t row = min(rrow, p.M - 1);
     const int pw0 = wv * NPW;                             // the wave's first panel
 
@@ -185,11 +187,11 @@ __global__ void __launch_bounds__(256, 1) gemm_ws_kernel(WsArgs p) {
             }
         }
     }
-    float4 rres[kResEarly ? 4 : 1][4];                    // RES, one pass: the residual
+    float4 rres[kResEarly ? RT : 1][4];                    // RES, one pass: the residual
     if constexpr (kResEarly) {
         const int col0 = pw0 * 16;
 #pragma unroll
-        for (int rt = 0; rt < 4; ++rt) {
+        for (int rt = 0; rt < RT; ++rt) {
             const int64_t orow = min(r0 + 16 * rt + c, p.M - 1);
 #pragma unroll
             for (int pp = 0; pp < 4; ++pp)
@@ -237,7 +239,7 @@ __global__ void __launch_bounds__(256, 1) gemm_ws_kernel(WsArgs p) {
                 sq += d * d;
             }
         const float rstd = 1.0f / sqrtf(xg_sum_w(sq) / 256.f + p.eps);
-        if constexpr (LNM == 3) {                         // out2 rows -> LDS (stored at the end)
+        if (LNM == 3 && wv < RT) {                        // out2 rows -> LDS (stored at the end)
 #pragma unroll
             for (int s = 0; s < kWsKS; ++s) {
                 const int k = 32 * s + 8 * g;
@@ -275,14 +277,16 @@ __global__ void __launch_bounds__(256, 1) gemm_ws_kernel(WsArgs p) {
         mx = xg_max_w(mx);
         const int e = mx > 0.f ? min(15 - __builtin_amdgcn_frexp_expf(mx), 127) : 0;
         const float sc = __builtin_ldexpf(1.f, e);
+        if (wv < RT) {
 #pragma unroll
-        for (int s = 0; s < kWsKS; ++s) {
-            u32x4 h, l;
-            split8_f16(xr[s], sc, h, l);
-            act[((wv * kWsKS + s) * 2 + 0) * 64 + lane] = h;
-            act[((wv * kWsKS + s) * 2 + 1) * 64 + lane] = l;
+            for (int s = 0; s < kWsKS; ++s) {
+                u32x4 h, l;
+                split8_f16(xr[s], sc, h, l);
+                act[((wv * kWsKS + s) * 2 + 0) * 64 + lane] = h;
+                act[((wv * kWsKS + s) * 2 + 1) * 64 + lane] = l;
+            }
+            if (g == 0) rowrs[16 * wv + c] = __builtin_ldexpf(1.f, -e);
         }
-        if (g == 0) rowrs[16 * wv + c] = __builtin_ldexpf(1.f, -e);
     }
     // LDS writes done, no vector-memory wait (the weight groups stay in flight)
     __builtin_amdgcn_s_waitcnt((15) | (7 << 4) | (0 << 8) | (3 << 14));
@@ -292,26 +296,26 @@ __global__ void __launch_bounds__(256, 1) gemm_ws_kernel(WsArgs p) {
 #endif
 
     // 2. the wave's panels, 4 per pass; k32 group G = pass * 8 + s loads W (panel, s, term)
-    auto read_act = [&](int s, u32x4 (&f)[8]) {
+    auto read_act = [&](int s, u32x4 (&f)[2 * RT]) {
 #pragma unroll
-        for (int rt = 0; rt < 4; ++rt) {
+        for (int rt = 0; rt < RT; ++rt) {
             f[2 * rt + 0] = act[((rt * kWsKS + s) * 2 + 0) * 64 + lane];
             f[2 * rt + 1] = act[((rt * kWsKS + s) * 2 + 1) * 64 + lane];
         }
     };
-    u32x4 fa[2][8];
+    u32x4 fa[2][2 * RT];
     // finished values of each pass (stored at the end): plain -> 4 floats, KV -> hi / lo
     // halves of 4 dims; [pass][row tile][panel]
-    u32x4 fin[NPASS][4][4];
+    u32x4 fin[NPASS][RT][4];
     int kv_e[NPASS][2];                                   // KV: the pass's two head exponents
-    float rs[4];
+    float rs[RT];
 #pragma unroll
     for (int pass = 0; pass < NPASS; ++pass) {
         const int col0 = (pw0 + 4 * pass) * 16;
         const bool kvp = KV && col0 >= p.kv_col0;          // wave-uniform: two K or V heads
-        f32x4 acc[4][4];
+        f32x4 acc[RT][4];
 #pragma unroll
-        for (int rt = 0; rt < 4; ++rt)
+        for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
             for (int pp = 0; pp < 4; ++pp) acc[rt][pp] = f32x4{0.f, 0.f, 0.f, 0.f};
         read_act(0, fa[0]);
@@ -322,12 +326,12 @@ __global__ void __launch_bounds__(256, 1) gemm_ws_kernel(WsArgs p) {
             // group G landed: the groups issued after it may still be in flight
             wait_groups_ws(NG - 1 - G < kWsRing - 1 ? NG - 1 - G : kWsRing - 1);
             u32x4 (&wf)[8] = ring[G % kWsRing];
-            u32x4 (&cur)[8] = fa[s & 1];
+            u32x4 (&cur)[2 * RT] = fa[s & 1];
             if (s + 1 < kWsKS) read_act(s + 1, fa[(s + 1) & 1]);
             __builtin_amdgcn_sched_group_barrier(0x020, 8, 0);
-            if (s + 1 < kWsKS) __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+            if (s + 1 < kWsKS) __builtin_amdgcn_sched_group_barrier(0x100, 2 * RT, 0);
 #pragma unroll
-            for (int rt = 0; rt < 4; ++rt) {
+            for (int rt = 0; rt < RT; ++rt) {
                 const f16x8 ah = __builtin_bit_cast(f16x8, cur[2 * rt + 0]);
                 const f16x8 al = __builtin_bit_cast(f16x8, cur[2 * rt + 1]);
 #pragma unroll
@@ -339,7 +343,7 @@ __global__ void __launch_bounds__(256, 1) gemm_ws_kernel(WsArgs p) {
                     acc[rt][pp] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, ah, acc[rt][pp], 0, 0, 0);
                 }
             }
-            __builtin_amdgcn_sched_group_barrier(0x008, 48, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, 12 * RT, 0);
             __builtin_amdgcn_sched_barrier(0);
         }
 #ifdef FGR_WS_STAMP
@@ -349,7 +353,7 @@ __global__ void __launch_bounds__(256, 1) gemm_ws_kernel(WsArgs p) {
         //    col0 + 16 pp + 4 g .. + 3
         if (pass == 0)
 #pragma unroll
-            for (int rt = 0; rt < 4; ++rt) rs[rt] = rowrs[16 * rt + c];
+            for (int rt = 0; rt < RT; ++rt) rs[rt] = rowrs[16 * rt + c];
         if (kvp) {
 #pragma unroll
             for (int hh = 0; hh < 2; ++hh) {
@@ -360,7 +364,7 @@ __global__ void __launch_bounds__(256, 1) gemm_ws_kernel(WsArgs p) {
                     const int n = col0 + 32 * hh + 16 * pp + 4 * g;
                     const float4 ws = colw[n / 4], bv = colb[n / 4];
 #pragma unroll
-                    for (int rt = 0; rt < 4; ++rt) {
+                    for (int rt = 0; rt < RT; ++rt) {
                         const bool ok = r0 + 16 * rt + c < p.M;      // rows past M: zeros
                         const f32x4 a = acc[rt][2 * hh + pp];
                         y[rt][pp][0] = ok ? a[0] * (rs[rt] * ws.x) + bv.x : 0.f;
@@ -375,7 +379,7 @@ __global__ void __launch_bounds__(256, 1) gemm_ws_kernel(WsArgs p) {
                 kv_e[pass][hh] = e;
                 const float sc = __builtin_ldexpf(1.f, e);
 #pragma unroll
-                for (int rt = 0; rt < 4; ++rt)
+                for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
                     for (int pp = 0; pp < 2; ++pp) {
                         _Float16 hv[4], lv[4];
@@ -396,7 +400,7 @@ __global__ void __launch_bounds__(256, 1) gemm_ws_kernel(WsArgs p) {
                 const int n = col0 + 16 * pp + 4 * g;
                 const float4 ws = colw[n / 4], bv = colb[n / 4];
 #pragma unroll
-                for (int rt = 0; rt < 4; ++rt) {
+                for (int rt = 0; rt < RT; ++rt) {
                     float4 r4 = make_float4(0.f, 0.f, 0.f, 0.f);
                     if constexpr (kResEarly) r4 = rres[rt][pp];
                     const f32x4 a = acc[rt][pp];
@@ -428,7 +432,7 @@ __global__ void __launch_bounds__(256, 1) gemm_ws_kernel(WsArgs p) {
                 if (lane == 0) reinterpret_cast<int*>(p.kv_sc + tile)[isv] = kv_e[pass][hh];
                 char* base = p.kv_img + tile * (kKvUnitsWs * 16);
 #pragma unroll
-                for (int rt = 0; rt < 4; ++rt) {
+                for (int rt = 0; rt < RT; ++rt) {
                     const int key = 16 * rt + c;
 #pragma unroll
                     for (int pp = 0; pp < 2; ++pp) {
@@ -450,7 +454,7 @@ __global__ void __launch_bounds__(256, 1) gemm_ws_kernel(WsArgs p) {
             }
         } else {
 #pragma unroll
-            for (int rt = 0; rt < 4; ++rt) {
+            for (int rt = 0; rt < RT; ++rt) {
                 const int rr = r0 + 16 * rt + c;
                 if (rr < p.M) {
 #pragma unroll
@@ -471,10 +475,10 @@ __global__ void __launch_bounds__(256, 1) gemm_ws_kernel(WsArgs p) {
         }
     }
     if constexpr (LNM == 3) {
-        // out2: the block's 64 rows x 256 from LDS, 16 B per lane, whole rows per instruction
+        // out2: the block's rows x 256 from LDS, 16 B per lane, whole rows per instruction
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const int u = tid + 256 * i;                  // float4 index in [64 rows][64]
+        for (int i = 0; i < 4 * RT; ++i) {
+            const int u = tid + 256 * i;                  // float4 index in [BR rows][64]
             const int rr = r0 + (u >> 6);
             if (rr < p.M) *reinterpret_cast<float4*>(p.out2 + (int64_t)rr * p.ld_out2 + 4 * (u & 63)) = side[u];
         }
@@ -485,10 +489,22 @@ __global__ void __launch_bounds__(256, 1) gemm_ws_kernel(WsArgs p) {
 #endif
 }
 
+// row tiles per block: 3 (48-row blocks) where they fit the CUs in one round and 64-row
+// blocks leave CUs idle (ModelNet's 9544 rows: 199 blocks instead of 150), else 4; the K / V
+// image epilogue writes whole 64-row tiles (4 only). FGR_WS_RT overrides (A/B).
+constexpr int kCusWs = 256;
 template <int NPW, int LNM, bool KV, bool RES, int ACT>
 void launch_ws(const WsArgs& a, hipStream_t st) {
-    hipLaunchKernelGGL((gemm_ws_kernel<NPW, LNM, KV, RES, ACT>), dim3((unsigned)((a.M + 63) / 64)),
-                       dim3(256), 0, st, a);
+    static const int rt_env = [] { const char* e = getenv("FGR_WS_RT"); return e ? atoi(e) : 0; }();
+    int rt = (rt_env >= 3 && rt_env <= 4) ? rt_env
+             : ((a.M + 47) / 48 <= kCusWs && (a.M + 63) / 64 < kCusWs) ? 3 : 4;
+    if (KV) rt = 4;
+    if (rt == 3)
+        hipLaunchKernelGGL((gemm_ws_kernel<NPW, LNM, KV, RES, ACT, KV ? 4 : 3>),
+                           dim3((unsigned)((a.M + 47) / 48)), dim3(256), 0, st, a);
+    else
+        hipLaunchKernelGGL((gemm_ws_kernel<NPW, LNM, KV, RES, ACT, 4>), dim3((unsigned)((a.M + 63) / 64)),
+                           dim3(256), 0, st, a);
 }
 
 }  // namespace

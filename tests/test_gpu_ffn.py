@@ -55,7 +55,8 @@ def _run(gpu, x, norm, w1, b1, w2, b2, out=None):
                    fl.weight_image(W2, mode='ffn2', cache=False), B2, bound, out=out)
 
 
-@pytest.mark.parametrize('m,f', [(9544, 1024), (1, 1024), (65, 1024), (1000, 64), (777, 2048)])
+@pytest.mark.parametrize('m,f', [(9544, 1024), (1, 1024), (65, 1024), (1000, 64), (777, 2048),
+                                 (13000, 1024)])
 @pytest.mark.parametrize('case', ['plain', 'big_row', 'neg_bias'])
 def test_ffn_vs_fp64(gpu, m, f, case):
     from fgreg import ops
