@@ -109,7 +109,9 @@ __device__ __forceinline__ float finish_ws(float y, float b, float r) {
 // stay in registers (64 per pass and lane), the side output (LNM 3) in LDS, and the stores go
 // out after the last MFMA. The first weight groups are requested with the rows, and the column
 // scales / bias sit in LDS.
-template <int NPW, int LNM, bool KV, bool RES, int ACT, int RT>
+// NPART > 1: the output columns split over NPART blocks per row tile (each NPW panels per
+// wave), the row tile's blocks adjacent in the XCD order (one L2 serves their row loads)
+template <int NPW, int LNM, bool KV, bool RES, int ACT, int RT, int NPART>
 __global__ void __launch_bounds__(256, 1) gemm_ws_kernel(WsArgs p) {
     static_assert(NPW % 4 == 0, "passes of 4 panels");
     static_assert(RT >= 1 && RT <= 4 && (!KV || RT == 4), "row tiles (K / V images: 64-row tiles)");
@@ -131,18 +133,21 @@ __global__ void __launch_bounds__(256, 1) gemm_ws_kernel(WsArgs p) {
     unsigned long long st_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     st_[0] = __builtin_amdgcn_s_memtime();
 #endif
-    const int nbm = (p.M + BR - 1) / BR;
+    const int nblk = (p.M + BR - 1) / BR * NPART;
     int t = blockIdx.x;
-    {   // XCD-aware order: each XCD a contiguous range of row blocks
-        const int q = nbm / 8, r = nbm % 8, x = t % 8, lo = t / 8;
+    {   // XCD-aware order: each XCD a contiguous range of (row block, part)
+        const int q = nblk / 8, r = nblk % 8, x = t % 8, lo = t / 8;
         t = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + lo;
     }
+    const int part = t % NPART;
+    t /= NPART;                                           // the row block
+    const int cb4 = part * (N / 4);                       // the part's first column / 4
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
     const int g = lane >> 4, c = lane & 15;
     const int r0 = t * BR;
     const int rrow = r0 + 16 * min(wv, RT - 1) + c;       // the lane's prologue row (RT < 4: wave 3 idles)
     const int64_t row = min(rrow, p.M - 1);
-    const int pw0 = wv * NPW;                             // the wave's first panel
+    const int pw0 = part * 4 * NPW + wv * NPW;            // the wave's first panel
 
     // 1. loads, in this order (vmcnt is in order): LayerNorm parameters, column scales / bias,
     //    the wave's row tile and its row add, the first weight groups
@@ -161,8 +166,8 @@ __global__ void __launch_bounds__(256, 1) gemm_ws_kernel(WsArgs p) {
 #pragma unroll
     for (int i = 0; i < NC4; ++i) {
         const int j = min(tid + 256 * i, N / 4 - 1);
-        pcw[i] = reinterpret_cast<const float4*>(p.wsc)[j];
-        pcb[i] = p.bias ? reinterpret_cast<const float4*>(p.bias)[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+        pcw[i] = reinterpret_cast<const float4*>(p.wsc)[cb4 + j];
+        pcb[i] = p.bias ? reinterpret_cast<const float4*>(p.bias)[cb4 + j] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
     __builtin_amdgcn_sched_barrier(0);
     float xr[kWsKS][8];
@@ -362,7 +367,7 @@ __global__ void __launch_bounds__(256, 1) gemm_ws_kernel(WsArgs p) {
 #pragma unroll
                 for (int pp = 0; pp < 2; ++pp) {
                     const int n = col0 + 32 * hh + 16 * pp + 4 * g;
-                    const float4 ws = colw[n / 4], bv = colb[n / 4];
+                    const float4 ws = colw[n / 4 - cb4], bv = colb[n / 4 - cb4];
 #pragma unroll
                     for (int rt = 0; rt < RT; ++rt) {
                         const bool ok = r0 + 16 * rt + c < p.M;      // rows past M: zeros
@@ -398,7 +403,7 @@ __global__ void __launch_bounds__(256, 1) gemm_ws_kernel(WsArgs p) {
 #pragma unroll
             for (int pp = 0; pp < 4; ++pp) {
                 const int n = col0 + 16 * pp + 4 * g;
-                const float4 ws = colw[n / 4], bv = colb[n / 4];
+                const float4 ws = colw[n / 4 - cb4], bv = colb[n / 4 - cb4];
 #pragma unroll
                 for (int rt = 0; rt < RT; ++rt) {
                     float4 r4 = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -474,7 +479,7 @@ __global__ void __launch_bounds__(256, 1) gemm_ws_kernel(WsArgs p) {
             }
         }
     }
-    if constexpr (LNM == 3) {
+    if (LNM == 3 && part == 0) {
         // out2: the block's rows x 256 from LDS, 16 B per lane, whole rows per instruction
 #pragma unroll
         for (int i = 0; i < 4 * RT; ++i) {
@@ -493,18 +498,18 @@ __global__ void __launch_bounds__(256, 1) gemm_ws_kernel(WsArgs p) {
 // blocks leave CUs idle (ModelNet's 9544 rows: 199 blocks instead of 150), else 4; the K / V
 // image epilogue writes whole 64-row tiles (4 only). FGR_WS_RT overrides (A/B).
 constexpr int kCusWs = 256;
-template <int NPW, int LNM, bool KV, bool RES, int ACT>
+template <int NPW, int LNM, bool KV, bool RES, int ACT, int NPART = 1>
 void launch_ws(const WsArgs& a, hipStream_t st) {
     static const int rt_env = [] { const char* e = getenv("FGR_WS_RT"); return e ? atoi(e) : 0; }();
     int rt = (rt_env >= 3 && rt_env <= 4) ? rt_env
              : ((a.M + 47) / 48 <= kCusWs && (a.M + 63) / 64 < kCusWs) ? 3 : 4;
     if (KV) rt = 4;
     if (rt == 3)
-        hipLaunchKernelGGL((gemm_ws_kernel<NPW, LNM, KV, RES, ACT, KV ? 4 : 3>),
-                           dim3((unsigned)((a.M + 47) / 48)), dim3(256), 0, st, a);
+        hipLaunchKernelGGL((gemm_ws_kernel<NPW, LNM, KV, RES, ACT, KV ? 4 : 3, NPART>),
+                           dim3((unsigned)((a.M + 47) / 48 * NPART)), dim3(256), 0, st, a);
     else
-        hipLaunchKernelGGL((gemm_ws_kernel<NPW, LNM, KV, RES, ACT, 4>), dim3((unsigned)((a.M + 63) / 64)),
-                           dim3(256), 0, st, a);
+        hipLaunchKernelGGL((gemm_ws_kernel<NPW, LNM, KV, RES, ACT, 4, NPART>),
+                           dim3((unsigned)((a.M + 63) / 64 * NPART)), dim3(256), 0, st, a);
 }
 
 }  // namespace
@@ -538,7 +543,13 @@ bool gemm_ws_f16x3(const float* A, int64_t lda, const void* W, const float* wsc,
         }
         if (ln->kv_img) {
             if (relu || !ln->add || ln->n_head * 64 + ln->kv_col0 != N || ln->kv_col0 != 256) return false;
+            // without the side output: q | k | v over three blocks per row tile (450 blocks at
+            // ModelNet's 9544 rows, two resident per CU; 28.2 -> 25.3 us), unless FGR_WS_SPLIT=0.
+            // With it (its 64 KB LDS staging: one block per CU) one block per row tile (31.3 us
+            // vs 35.6 split; profiles/r06_ws_split_ab.txt)
+            static const bool split = [] { const char* e = getenv("FGR_WS_SPLIT"); return !(e && e[0] == '0'); }();
             if (ln->out2) launch_ws<12, 3, true, false, FGR_ACT_NONE>(a, st);
+            else if (split) launch_ws<4, 2, true, false, FGR_ACT_NONE, 3>(a, st);
             else launch_ws<12, 2, true, false, FGR_ACT_NONE>(a, st);
             return true;
         }

@@ -56,7 +56,15 @@ def main():
             x.data_ptr(), d, norm.weight.data_ptr(), norm.bias.data_ptr(), 1e-5, pos.data_ptr(), d,
             i3.img.data_ptr(), q.data_ptr(), d, b3.data_ptr(), m, d, nh, img.data_ptr(), None, None,
             None, 0, ops._stream()), 'qkv')
+    out2 = torch.empty(m, d, device=dev)
+
+    def qkv2():
+        _lib.check(L.fgr_gemm_f16x3_ln_qkv(
+            x.data_ptr(), d, norm.weight.data_ptr(), norm.bias.data_ptr(), 1e-5, pos.data_ptr(), d,
+            i3.img.data_ptr(), q.data_ptr(), d, b3.data_ptr(), m, d, nh, img.data_ptr(),
+            norm.weight.data_ptr(), norm.bias.data_ptr(), out2.data_ptr(), d, ops._stream()), 'qkv2')
     cases = {'in_proj LN+pos+KV 9544x768x256': qkv,
+             'in_proj LN+pos+KV+out2 9544x768x256': qkv2,
              'out_proj +res 9544x256x256': lambda: lin.linear(x, w1, b1, residual=pos),
              'plain 9544x768x256': lambda: lin.linear(x, w3, b3)}
     for name, fn in cases.items():
