@@ -112,7 +112,8 @@ __device__ __forceinline__ float finish_ws(float y, float b, float r) {
 // NPART > 1: the output columns split over NPART blocks per row tile (each NPW panels per
 // wave), the row tile's blocks adjacent in the XCD order (one L2 serves their row loads)
 template <int NPW, int LNM, bool KV, bool RES, int ACT, int RT, int NPART>
-__global__ void __launch_bounds__(256, 1) gemm_ws_kernel(WsArgs p) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((KV && NPART > 1) ? 2 : 1)))
+gemm_ws_kernel(WsArgs p) {
     static_assert(NPW % 4 == 0, "passes of 4 panels");
     static_assert(RT >= 1 && RT <= 4 && (!KV || RT == 4), "row tiles (K / V images: 64-row tiles)");
     constexpr int BR = 16 * RT;                           // rows per block
@@ -127,7 +128,10 @@ __global__ void __launch_bounds__(256, 1) gemm_ws_kernel(WsArgs p) {
     __shared__ float4 colw[N / 4], colb[N / 4];           // per column: 2^-e_n, bias
     __shared__ float4 lng[LNM ? 64 : 1], lnb[LNM ? 64 : 1];
     __shared__ float4 lng2[LNM == 3 ? 64 : 1], lnb2[LNM == 3 ? 64 : 1];
-    __shared__ float4 side[LNM == 3 ? BR * 64 : 1];       // LNM 3: out2 rows, row-major
+    // LNM 3, one block per row tile: the out2 rows staged in LDS, row-major; NPART > 1: part 0
+    // recomputes them at the end from re-read rows (no 64 KB staging: two blocks per CU)
+    constexpr bool kSideLds = LNM == 3 && NPART == 1;
+    __shared__ float4 side[kSideLds ? BR * 64 : 1];
 
 #ifdef FGR_WS_STAMP
     unsigned long long st_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -224,6 +228,7 @@ __global__ void __launch_bounds__(256, 1) gemm_ws_kernel(WsArgs p) {
         const int j = tid + 256 * i;
         if (j < N / 4) { colw[j] = pcw[i]; colb[j] = pcb[i]; }
     }
+    float ln_mean = 0.f, ln_rstd = 0.f;                   // the lane's row (LNM 3, NPART > 1)
     if constexpr (LNM > 0) {
         if (tid < 64) { lng[tid] = lpg; lnb[tid] = lpb; }
         if constexpr (LNM == 3)
@@ -244,7 +249,9 @@ __global__ void __launch_bounds__(256, 1) gemm_ws_kernel(WsArgs p) {
                 sq += d * d;
             }
         const float rstd = 1.0f / sqrtf(xg_sum_w(sq) / 256.f + p.eps);
-        if (LNM == 3 && wv < RT) {                        // out2 rows -> LDS (stored at the end)
+        ln_mean = mean;
+        ln_rstd = rstd;
+        if (kSideLds && wv < RT) {                        // out2 rows -> LDS (stored at the end)
 #pragma unroll
             for (int s = 0; s < kWsKS; ++s) {
                 const int k = 32 * s + 8 * g;
@@ -479,7 +486,29 @@ __global__ void __launch_bounds__(256, 1) gemm_ws_kernel(WsArgs p) {
             }
         }
     }
-    if (LNM == 3 && part == 0) {
+    if (LNM == 3 && !kSideLds && part == 0 && wv < RT) {
+        // out2 = LN(x) g2 + b2 of the wave's rows from a second read of x (L2), after every
+        // other store of the block
+        const float* ar = p.A + row * p.lda;
+#pragma unroll
+        for (int s = 0; s < kWsKS; ++s) {
+            const int k = 32 * s + 8 * g;
+            const float4 a0 = *reinterpret_cast<const float4*>(ar + k);
+            const float4 a1 = *reinterpret_cast<const float4*>(ar + k + 4);
+            const float4 h0 = lng2[k / 4], h1 = lng2[k / 4 + 1];
+            const float4 c0 = lnb2[k / 4], c1 = lnb2[k / 4 + 1];
+            if (rrow < p.M) {
+                float* o2 = p.out2 + (int64_t)rrow * p.ld_out2 + k;
+                *reinterpret_cast<float4*>(o2) = make_float4(
+                    (a0.x - ln_mean) * ln_rstd * h0.x + c0.x, (a0.y - ln_mean) * ln_rstd * h0.y + c0.y,
+                    (a0.z - ln_mean) * ln_rstd * h0.z + c0.z, (a0.w - ln_mean) * ln_rstd * h0.w + c0.w);
+                *reinterpret_cast<float4*>(o2 + 4) = make_float4(
+                    (a1.x - ln_mean) * ln_rstd * h1.x + c1.x, (a1.y - ln_mean) * ln_rstd * h1.y + c1.y,
+                    (a1.z - ln_mean) * ln_rstd * h1.z + c1.z, (a1.w - ln_mean) * ln_rstd * h1.w + c1.w);
+            }
+        }
+    }
+    if (kSideLds) {
         // out2: the block's rows x 256 from LDS, 16 B per lane, whole rows per instruction
 #pragma unroll
         for (int i = 0; i < 4 * RT; ++i) {
@@ -548,8 +577,11 @@ bool gemm_ws_f16x3(const float* A, int64_t lda, const void* W, const float* wsc,
             // With it (its 64 KB LDS staging: one block per CU) one block per row tile (31.3 us
             // vs 35.6 split; profiles/r06_ws_split_ab.txt)
             static const bool split = [] { const char* e = getenv("FGR_WS_SPLIT"); return !(e && e[0] == '0'); }();
-            if (ln->out2) launch_ws<12, 3, true, false, FGR_ACT_NONE>(a, st);
-            else if (split) launch_ws<4, 2, true, false, FGR_ACT_NONE, 3>(a, st);
+            static const bool split3 = [] { const char* e = getenv("FGR_WS_SPLIT3"); return !(e && e[0] == '0'); }();
+            if (ln->out2) {
+                if (split && split3) launch_ws<4, 3, true, false, FGR_ACT_NONE, 3>(a, st);
+                else launch_ws<12, 3, true, false, FGR_ACT_NONE>(a, st);
+            } else if (split) launch_ws<4, 2, true, false, FGR_ACT_NONE, 3>(a, st);
             else launch_ws<12, 2, true, false, FGR_ACT_NONE>(a, st);
             return true;
         }
