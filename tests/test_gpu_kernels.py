@@ -324,7 +324,16 @@ def test_res2net_chain6_rows_bitexact(gpu, n, monkeypatch):
     assert torch.equal(a, b)
 
 
-def _res2net_case(gpu, cin, cout, my_Bottle2neck, my_res2Net):
+@pytest.mark.parametrize('n', [1500, 9544])
+def test_res2net_block_h3_width224(gpu, n, monkeypatch):
+    """The f16x3 chain at width 224 (FGREG_R2N224=h3: 14-wave blocks of 32 rows at 1500
+    rows, 48 rows at ModelNet's 9544) vs the CPU restatement; ragged last blocks."""
+    from fgreg.backbone import my_Bottle2neck, my_res2Net
+    monkeypatch.setenv('FGREG_R2N224', 'h3')
+    _res2net_case(gpu, 256, 1024, my_Bottle2neck, my_res2Net, n=n)
+
+
+def _res2net_case(gpu, cin, cout, my_Bottle2neck, my_res2Net, n=1500):
     torch.manual_seed(cout)
     m = my_res2Net(my_Bottle2neck, cin, cout, baseWidth=14, scale=8)
     g = torch.Generator().manual_seed(cin)
@@ -336,7 +345,7 @@ def _res2net_case(gpu, cin, cout, my_Bottle2neck, my_res2Net):
                 mod.weight.copy_(1 + 0.1 * torch.randn(mod.weight.shape, generator=g))
                 mod.bias.copy_(0.1 * torch.randn(mod.bias.shape, generator=g))
     sd = {k: v.clone() for k, v in m.state_dict().items()}
-    x = torch.randn(1500, cin, generator=g)
+    x = torch.randn(n, cin, generator=g)
     ref = mo.res2net(sd, '', x) if False else mo.res2net({f'r.{k}': v for k, v in sd.items()}, 'r', x)
     m = m.to(gpu).eval()
     with torch.no_grad():
