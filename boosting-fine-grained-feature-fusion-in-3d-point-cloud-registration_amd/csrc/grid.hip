@@ -108,8 +108,11 @@ __global__ void __launch_bounds__(kSB) scan_offsets_kernel(int2* __restrict__ ti
     }
 }
 
-// io[i] <- exclusive prefix (in place) for i in [0, n]; ord[i] <- exclusive count of non-zero
-template <bool DUAL>
+// io[i] <- exclusive prefix (in place) for i in [0, n]; ord[i] <- exclusive count of non-zero.
+// RAW: `tiles` holds the raw tile totals (at most kSB tiles) and each block sums those before
+// its own (one load per thread and a block reduction) -- the scan without its one-block
+// offsets launch; else `tiles` holds the exclusive tile offsets (scan_offsets_kernel)
+template <bool DUAL, bool RAW = false>
 __global__ void __launch_bounds__(kSB) scan_final_kernel(int* __restrict__ io, int* __restrict__ ord,
                                                          const int64_t* __restrict__ n_dev,
                                                          int64_t n_static,
@@ -117,7 +120,13 @@ __global__ void __launch_bounds__(kSB) scan_final_kernel(int* __restrict__ io, i
     const int64_t n = scan_n(n_dev, n_static);
     const int64_t base = (int64_t)blockIdx.x * kST;
     if (base > n) return;                                   // block-uniform
-    int2 carry = tiles[blockIdx.x];
+    int2 carry;
+    if constexpr (RAW) {
+        const int2 v = (int)threadIdx.x < (int)blockIdx.x ? tiles[threadIdx.x] : make_int2(0, 0);
+        block_excl_scan2(v, &carry);                        // carry = the sum over earlier tiles
+    } else {
+        carry = tiles[blockIdx.x];
+    }
     for (int k = 0; k < kSI; ++k) {
         const int64_t i = base + k * kSB + threadIdx.x;
         const int v = i < n ? io[i] : 0;
@@ -139,6 +148,13 @@ int launch_scan(int* io, int* ord, const int64_t* n_dev, int64_t n_max, int2* ti
     const int nt = scan_tiles(n_max);
     hipLaunchKernelGGL(scan_tile_kernel<DUAL>, dim3(nt), dim3(kSB), 0, st, io, n_dev, n_max, tiles);
     FGR_CHECK_LAUNCH("scan_tile_kernel");
+    static const bool two = [] { const char* e = getenv("FGR_SCAN2"); return !(e && e[0] == '0'); }();
+    if (two && nt <= kSB) {                                 // <= 1M counters: two launches
+        hipLaunchKernelGGL((scan_final_kernel<DUAL, true>), dim3(nt), dim3(kSB), 0, st, io, ord, n_dev,
+                           n_max, tiles);
+        FGR_CHECK_LAUNCH("scan_final_kernel");
+        return FGR_OK;
+    }
     hipLaunchKernelGGL(scan_offsets_kernel, dim3(1), dim3(kSB), 0, st, tiles, nt);
     FGR_CHECK_LAUNCH("scan_offsets_kernel");
     hipLaunchKernelGGL(scan_final_kernel<DUAL>, dim3(nt), dim3(kSB), 0, st, io, ord, n_dev, n_max,
