@@ -194,6 +194,7 @@ struct WsLn {
     char* kv_img; int2* kv_sc; int n_head; int kv_col0;
 };
 bool gemm_ws_supported(int m, int n, int k);
+bool gemm_ws_ln_supported(int m, int n, int k);   // the LayerNorm-prologue forms (N 256 / 768)
 bool gemm_ws_f16x3(const float* A, int64_t lda, const void* W, const float* wsc, float* C,
                    int64_t ldc, const float* bias, const float* R, int64_t ldr, int M, int N,
                    int K, int act, hipStream_t st, const WsLn* ln);

@@ -1442,7 +1442,7 @@ extern "C" int fgr_gemm_f16x3_ws(const float* a, int64_t lda, const void* w_img,
 // LayerNorm -> (+ add) -> Linear in one launch (the row-stationary kernel's LN prologue,
 // gemm_rs.hip): supported where the dispatcher picks that kernel for (m, n, k).
 extern "C" int fgr_gemm_f16x3_ln_supported(int32_t m, int32_t n, int32_t k) {
-    return (m > 0 && n > 0 && k > 0 && (gemm_ws_supported(m, n, k) || h3_tile(m, n, k) == 'z')) ? 1 : 0;
+    return (m > 0 && n > 0 && k > 0 && (gemm_ws_ln_supported(m, n, k) || h3_tile(m, n, k) == 'z')) ? 1 : 0;
 }
 
 static int gemm_f16x3_ln_impl(const float* x, int64_t ldx, const float* gamma, const float* beta,

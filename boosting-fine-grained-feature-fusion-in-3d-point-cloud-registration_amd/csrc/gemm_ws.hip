@@ -112,7 +112,7 @@ __device__ __forceinline__ float finish_ws(float y, float b, float r) {
 // NPART > 1: the output columns split over NPART blocks per row tile (each NPW panels per
 // wave), the row tile's blocks adjacent in the XCD order (one L2 serves their row loads)
 template <int NPW, int LNM, bool KV, bool RES, int ACT, int RT, int NPART>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((KV && NPART > 1) ? 2 : 1)))
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((NPART > 1 && !RES) ? 2 : 1)))
 gemm_ws_kernel(WsArgs p) {
     static_assert(NPW % 4 == 0, "passes of 4 panels");
     static_assert(RT >= 1 && RT <= 4 && (!KV || RT == 4), "row tiles (K / V images: 64-row tiles)");
@@ -547,7 +547,16 @@ void launch_ws(const WsArgs& a, hipStream_t st) {
 // 16-B aligned (checked by the caller). FGR_GEMM_WS=0 disables it (the rs kernel then).
 bool gemm_ws_supported(int m, int n, int k) {
     static const bool on = [] { const char* e = getenv("FGR_GEMM_WS"); return !(e && e[0] == '0'); }();
-    return on && k == 256 && (n == 256 || n == 768) && m >= 4096;
+    if (!on || k != 256 || m < 4096) return false;
+    // N = 512 / 1024: the columns over N / 256 blocks per row tile (ModelNet's 9544 x 512 x 256:
+    // 22.2-22.9 -> 19.4-19.6 us; 9544 x 1792 x 256 measured equal to the row-stationary kernel
+    // and left there, profiles/r06_ws_wide_ab.txt); FGR_GEMM_WSN=0 keeps them off (A/B)
+    static const bool wide = [] { const char* e = getenv("FGR_GEMM_WSN"); return !(e && e[0] == '0'); }();
+    return n == 256 || n == 768 || (wide && (n == 512 || n == 1024));
+}
+
+bool gemm_ws_ln_supported(int m, int n, int k) {
+    return (n == 256 || n == 768) && gemm_ws_supported(m, n, k);
 }
 
 bool gemm_ws_f16x3(const float* A, int64_t lda, const void* W, const float* wsc, float* C,
@@ -563,6 +572,18 @@ bool gemm_ws_f16x3(const float* A, int64_t lda, const void* W, const float* wsc,
              ln ? ln->ld_out2 : 0, ln ? ln->kv_img : nullptr, ln ? ln->kv_sc : nullptr,
              ln ? ln->n_head : 0, ln ? ln->kv_col0 : N};
     const bool relu = act == FGR_ACT_RELU;
+    if (N != 256 && N != 768) {                  // 512 / 1024: N / 256 blocks per row tile
+        if (ln) return false;
+#define FGR_WS_PARTS(P)                                                                         \
+        if (R) { if (relu) launch_ws<4, 0, false, true, FGR_ACT_RELU, P>(a, st);                \
+                 else launch_ws<4, 0, false, true, FGR_ACT_NONE, P>(a, st); }                   \
+        else if (relu) launch_ws<4, 0, false, false, FGR_ACT_RELU, P>(a, st);                   \
+        else launch_ws<4, 0, false, false, FGR_ACT_NONE, P>(a, st);
+        if (N == 512) { FGR_WS_PARTS(2) }
+        else { FGR_WS_PARTS(4) }
+#undef FGR_WS_PARTS
+        return true;
+    }
     if (N == 768) {
         if (!ln) {
             if (R) launch_ws<12, 0, false, true, FGR_ACT_NONE>(a, st);

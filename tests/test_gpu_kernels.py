@@ -357,7 +357,8 @@ def _res2net_case(gpu, cin, cout, my_Bottle2neck, my_res2Net, n=1500):
                                    (333, 896, 128), (64, 256, 36), (5000, 768, 256),
                                    (9544, 256, 256), (4097, 256, 256), (13000, 256, 256),
                                    (12300, 768, 256), (2120, 512, 512), (2120, 1024, 512),
-                                   (1001, 512, 512), (300, 1024, 512)])
+                                   (1001, 512, 512), (300, 1024, 512), (9544, 1792, 256),
+                                   (5000, 512, 256), (4100, 1024, 256)])
 def test_gemm_split_vs_fp64(gpu, m, n, k):
     """The f16x3 GEMM vs fp64, bias / ReLU / residual / ReLU-residual-LeakyReLU epilogues,
     strided A, the KPConv weight layout, a row slice of a cached weight: at fp32 level, no
