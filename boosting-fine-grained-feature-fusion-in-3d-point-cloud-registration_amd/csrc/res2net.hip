@@ -92,8 +92,12 @@ res2net_chain6_kernel(const float* __restrict__ h, int64_t n, int scale, int num
                       const u32x4* __restrict__ wf, const float* __restrict__ bias,
                       const float* __restrict__ x, int cin, float* __restrict__ cat, int64_t ld) {
     constexpr int W = 16 * KT, KS = (W + 31) / 32, NU = R * KS * 4;   // A units per term
+    // sp rows padded to W + 4 floats: at a stride of W (a multiple of 32 floats here) the
+    // build's reads -- consecutive lanes on consecutive rows -- hit 2-4 of the 64 LDS banks
+    // (16-32-way conflicts); at W + 4 the 16-B reads of a wave spread over all of them
+    constexpr int SPW = W + 4;
     __shared__ u32x4 img[3 * NU];
-    __shared__ float sp[R * W];
+    __shared__ float sp[R * SPW];
     const int tid = threadIdx.x, nth = 64 * KT;
     const int wv = tid / 64, lane = tid % 64, g = lane >> 4, c = lane & 15;
     const int64_t r0 = (int64_t)blockIdx.x * R;
@@ -123,10 +127,11 @@ res2net_chain6_kernel(const float* __restrict__ h, int64_t n, int scale, int num
                     hv = *reinterpret_cast<const float4*>(h + gr * hw + (int64_t)i * W + k0 + e);
                 a[e] = hv.x; a[e + 1] = hv.y; a[e + 2] = hv.z; a[e + 3] = hv.w;
             }
-            if (i > 0) {
-#pragma unroll
-                for (int e = 0; e < 8; ++e)
-                    if (k0 + e < W) a[e] += sp[row * W + k0 + e];
+            if (i > 0 && k0 < W) {                      // k0 + 8 <= W: W % 16 == 0
+                const float4 s0 = *reinterpret_cast<const float4*>(sp + row * SPW + k0);
+                const float4 s1 = *reinterpret_cast<const float4*>(sp + row * SPW + k0 + 4);
+                a[0] += s0.x; a[1] += s0.y; a[2] += s0.z; a[3] += s0.w;
+                a[4] += s1.x; a[5] += s1.y; a[6] += s1.z; a[7] += s1.w;
             }
             bf16x8 th, tm, tl;
 #pragma unroll
@@ -184,7 +189,7 @@ res2net_chain6_kernel(const float* __restrict__ h, int64_t n, int scale, int num
                 const int row = rg * 16 + 4 * g + r;
                 const float y = fmaxf(acc[rg][r] + bc, 0.f);
                 if (r0 + row < n) cat[(r0 + row) * ld + (int64_t)i * W + col] = y;
-                sp[row * W + col] = y;
+                sp[row * SPW + col] = y;
             }
         }
         __syncthreads();
@@ -221,8 +226,9 @@ res2net_chain_h3_kernel(const float* __restrict__ h, int64_t n, int w, int scale
     constexpr int W = 16 * KT, KS = (W + 31) / 32, NU = R * KS * 4;       // A units per term
     constexpr int IT = (NU + 64 * KT - 1) / (64 * KT);                    // build units / thread
     constexpr int RF = R / 16;                                            // row fragments
+    constexpr int SPW = W + 4;                 // padded sp rows (bank spread, as in chain6)
     __shared__ u32x4 img[2 * NU];
-    __shared__ float sp[R * W];
+    __shared__ float sp[R * SPW];
     __shared__ int rmax[2][R];
     const int tid = threadIdx.x, nth = 64 * KT;
     const int wv = tid / 64, lane = tid % 64, g = lane >> 4, c = lane & 15;
@@ -264,11 +270,16 @@ res2net_chain_h3_kernel(const float* __restrict__ h, int64_t n, int w, int scale
             const int u = tid + nth * it;
             const int row = u % R, kg = u / R, k0 = 8 * kg;
             float cm = 0.f;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                if (i > 0 && u < NU && k0 + e < w) a[it][e] += sp[row * W + k0 + e];
-                cm = fmaxf(cm, fabsf(a[it][e]));
+            if (i > 0 && u < NU && k0 < W) {            // k0 < W => k0 + 8 <= W (W % 16 == 0)
+                // sp columns in [w, W) hold 0 (zero weights and bias there); units at k0 >= W
+                // are the k32 steps' padding past W (no sp columns)
+                const float4 s0 = *reinterpret_cast<const float4*>(sp + row * SPW + k0);
+                const float4 s1 = *reinterpret_cast<const float4*>(sp + row * SPW + k0 + 4);
+                a[it][0] += s0.x; a[it][1] += s0.y; a[it][2] += s0.z; a[it][3] += s0.w;
+                a[it][4] += s1.x; a[it][5] += s1.y; a[it][6] += s1.z; a[it][7] += s1.w;
             }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) cm = fmaxf(cm, fabsf(a[it][e]));
             if (u < NU && cm > 0.f) atomicMax(&rm[row], __float_as_int(cm));
         }
         __syncthreads();
@@ -326,7 +337,7 @@ res2net_chain_h3_kernel(const float* __restrict__ h, int64_t n, int w, int scale
             y.w = fmaxf(av[3] * rs * wsv.w + bc.w, 0.f);
             if (r0 + row < n && col_ok)
                 *reinterpret_cast<float4*>(cat + (r0 + row) * ld + (int64_t)i * w + col0) = y;
-            *reinterpret_cast<float4*>(sp + row * W + col0) = y;
+            *reinterpret_cast<float4*>(sp + row * SPW + col0) = y;
         }
         if (tid < R) rmax[(i + 1) & 1][tid] = 0;       // next step's row maxima
         __syncthreads();
