@@ -224,13 +224,15 @@ def test_encoder_bench_size_vs_oracle(gpu):
 
 
 @pytest.mark.parametrize('lens,side', [([717, 596, 1, 700, 64, 130, 5000, 2336], False),
-                                       ([596] * 16, True), ([65, 63, 64, 1, 128], False)])
+                                       ([596] * 16, True), ([65, 63, 64, 1, 128], False),
+                                       ([6000, 5999, 6001, 6000], False), ([3001] * 8, True)])
 def test_ln_qkv_images_vs_two_launch_path(gpu, lens, side):
     """fgr_gemm_f16x3_ln_qkv (the in_proj writing q fp32 and the K / V images of every global
     64-row tile, head dim 32) + fgr_attention_f16x3_img vs the path it replaces (LN-fused in_proj
     -> fp32 q | k | v -> fgr_attention_f16x3 with per-segment images): segments starting
     anywhere inside a tile (incl. a 1-row cloud and tiles shared by three clouds), self- and
-    cross-attention, the side output. Both are fp32-accurate: <= 2e-6 normwise apart and
+    cross-attention, the side output; 24000 rows: several (tile, column part) items per block of
+    the persistent in_proj kernel (gemm_ws.hip, gemm_wsp_kernel). Both are fp32-accurate: <= 2e-6 normwise apart and
     <= 1e-5 from a float64 LayerNorm -> in_proj -> softmax attention."""
     from fgreg import linear as lin
     from fgreg import ops

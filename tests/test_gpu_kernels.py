@@ -358,7 +358,8 @@ def _res2net_case(gpu, cin, cout, my_Bottle2neck, my_res2Net, n=1500):
                                    (9544, 256, 256), (4097, 256, 256), (13000, 256, 256),
                                    (12300, 768, 256), (2120, 512, 512), (2120, 1024, 512),
                                    (1001, 512, 512), (300, 1024, 512), (9544, 1792, 256),
-                                   (5000, 512, 256), (4100, 1024, 256)])
+                                   (5000, 512, 256), (4100, 1024, 256), (20000, 256, 256),
+                                   (40000, 1024, 256)])
 def test_gemm_split_vs_fp64(gpu, m, n, k):
     """The f16x3 GEMM vs fp64, bias / ReLU / residual / ReLU-residual-LeakyReLU epilogues,
     strided A, the KPConv weight layout, a row slice of a cached weight: at fp32 level, no
@@ -430,10 +431,10 @@ def test_gemm_f16x3_dynamic_range(gpu, tile, monkeypatch):
     del ref
 
 
-@pytest.mark.parametrize('n', [256, 768])
+@pytest.mark.parametrize('n', [256, 512, 768, 1024])
 def test_gemm_ws_dynamic_range(gpu, n):
-    """The weight-split row-stationary kernel (gemm_ws.hip: K = 256, N = 256 / 768, >= 4096
-    rows, one scale per row) under the adversarial magnitudes of test_gemm_f16x3_dynamic_range:
+    """The weight-split row-stationary kernels (gemm_ws.hip: K = 256, >= 4096 rows, one scale
+    per row; N = 256 / 512 / 1024 the persistent pipelined form, 768 the one-round form) under the adversarial magnitudes of test_gemm_f16x3_dynamic_range:
     every output row within 2e-6 of its own scale."""
     from fgreg import linear as fl
     from fgreg import _lib

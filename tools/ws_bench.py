@@ -67,6 +67,12 @@ def main():
              'in_proj LN+pos+KV+out2 9544x768x256': qkv2,
              'out_proj +res 9544x256x256': lambda: lin.linear(x, w1, b1, residual=pos),
              'plain 9544x768x256': lambda: lin.linear(x, w3, b3)}
+    # blocks per launch (stamps of blocks a launch did not run are stale): the split in_proj
+    # runs three 64-row blocks per row tile, the others one 48-row block
+    nblocks = {'in_proj LN+pos+KV 9544x768x256': 3 * ((m + 63) // 64),
+               'in_proj LN+pos+KV+out2 9544x768x256': 3 * ((m + 63) // 64),
+               'out_proj +res 9544x256x256': (m + 47) // 48,
+               'plain 9544x768x256': (m + 47) // 48}
     for name, fn in cases.items():
         print(f'{name}: {timeit(fn, iters):.1f} us')
     if hasattr(L, 'fgr_debug_ws_stamps'):
@@ -74,18 +80,23 @@ def main():
         for name, fn in cases.items():
             fn()
             torch.cuda.synchronize()
-            nbk = (m + 63) // 64
+            nbk = min(nblocks[name], 2048)
             buf = (ctypes.c_uint64 * (nbk * 32))()
             assert L.fgr_debug_ws_stamps(ctypes.cast(buf, ctypes.c_void_p), nbk) == 0
             a = np.frombuffer(buf, dtype=np.uint64).reshape(nbk, 4, 8).astype(np.float64)
             t0 = a[:, :, 0].min()
             rel = a - a[:, :, :1]
             print(f'  {name}: block start spread {np.median(a[:, 0, 0] - t0):.0f} (median) / '
-                  f'{np.max(a[:, 0, 0] - t0):.0f} (max) cycles; median per wave: prologue '
+                  f'{np.max(a[:, 0, 0] - t0):.0f} (max) cycles, last block end {np.max(a[:, :, 3]) - t0:.0f}; '
+                  f'median per wave: prologue '
                   f'{np.median(rel[:, :, 1]):.0f}, ' + ', '.join(
                       f'pass{p} mfma {np.median(rel[:, :, 2 + 2 * p] - rel[:, :, 1 + 2 * p if p else 1]):.0f} '
                       f'epi {np.median(rel[:, :, 3 + 2 * p] - rel[:, :, 2 + 2 * p]):.0f}'
-                      for p in range(3) if np.median(a[:, :, 3 + 2 * p]) > 0))
+                      for p in range(3) if np.median(a[:, :, 3 + 2 * p]) > 0) +
+                  (f', stores {np.median(rel[:, :, 7] - rel[:, :, 3]):.0f} (p90 '
+                   f'{np.percentile(rel[:, :, 7] - rel[:, :, 3], 90):.0f}), wave total '
+                   f'{np.median(rel[:, :, 7]):.0f} (p90 {np.percentile(rel[:, :, 7], 90):.0f})'
+                   if np.median(a[:, :, 7]) > 0 else ''))
 
 
 if __name__ == '__main__':
