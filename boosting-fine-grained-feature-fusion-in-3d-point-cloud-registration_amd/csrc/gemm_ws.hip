@@ -525,442 +525,6 @@ gemm_ws_kernel(WsArgs p) {
 #endif
 }
 
-// ------------------------------------------------------------------------------------
-// "wsp": the same product (64-row items, 4 MFMA waves splitting the item's output panels, W
-// fragments streamed from L2 into a register ring) as a PERSISTENT, software-pipelined kernel
-// with role-split waves.
-//
-// Why (stamps of the one-round kernel above, tools/ws_bench.py, profiles/r06_wsp_ab.txt): with
-// every block resident at once, the whole chip loads its rows, then multiplies, then stores --
-// in_proj (LN + pos + K / V) spends 15.7k cycles per wave in the prologue against 9.5k of MFMA
-// loop, out_proj 11.5k against 5.8k: the HBM traffic is not overlapped with anything. And a
-// wave cannot overlap its own stores with the weight stream: vmcnt counts loads and stores in
-// issue order, so a store ahead of a weight group delays that group's wait.
-//
-// So a block (one per CU, 8 waves) takes a contiguous run of (row tile, column part) items of
-// its XCD and pipelines them over two 64 KB LDS buffers:
-//   waves 0-3 (MFMA): only weight loads (vmcnt holds nothing else), LDS fragment reads and MFMAs
-//     for item k out of buffer k & 1; the finished values (scaled, + bias, or the K / V image
-//     bytes) go back into the SAME buffer once every wave has read it.
-//   waves 4-7 (IO), meanwhile: load item k + 1's rows, copy item k - 1's finished values (in
-//     buffer (k + 1) & 1) to global memory (+ residual, activation), then LayerNorm / split item
-//     k + 1's rows into that buffer. IO wave w owns 16 KB region w of both buffers (row tile w of
-//     the act image, chunk w of the results), so it never overwrites what another wave still
-//     reads.
-// Two barriers per item (act image ready / results written). The next item's first two weight
-// groups are requested during the current item's last k32 steps, so the ring does not drain.
-// ------------------------------------------------------------------------------------
-constexpr int kWspBufU = 4 * kWsKS * 2 * 64;             // 16-B units per buffer (64 KB)
-constexpr int kCusWsp = 256;
-
-struct WspArgs {
-    const float* A; int64_t lda;
-    const u32x4* W; const float* wsc; const float* bias;
-    float* C; int64_t ldc;
-    const float* R; int64_t ldr;
-    int M, N, ntile;
-    const float* ln_g; const float* ln_b; float eps;
-    const float* add; int64_t ld_add;
-    const float* g2; const float* b2; float* out2; int64_t ld_out2;
-    char* kv_img; int2* kv_sc; int n_head, kv_col0;
-};
-
-// NPW panels (16 columns) per MFMA wave: a part (item) covers 64 NPW columns, N = NPART 64 NPW.
-// LNM: 0 plain A, 2 LayerNorm(A) + add, 3 as 2 plus out2 (from part 0 items).
-template <int NPW, int LNM, bool KV, bool RES, int ACT, int NPART>
-__global__ void __launch_bounds__(512) gemm_wsp_kernel(WspArgs p) {
-    static_assert(NPW == 2 || NPW == 4, "panels per wave");
-    static_assert(LNM == 0 || LNM == 2 || LNM == 3, "prologue");
-    static_assert(!KV || (LNM >= 2 && !RES && ACT == FGR_ACT_NONE), "K / V images: the in_proj");
-    static_assert(!RES || LNM == 0, "residual: plain A");
-    constexpr int N = NPART * 64 * NPW;
-    constexpr int GL = 2 * NPW;                           // loads per weight group
-    constexpr int UR = 16 * NPW;                          // result units (16 B) per row of an item
-    __shared__ u32x4 buf[2 * kWspBufU];
-    __shared__ float rowrs[2][64];
-    __shared__ float4 colw[N / 4], colb[N / 4];
-    __shared__ float4 lng[LNM ? 64 : 1], lnb[LNM ? 64 : 1];
-    __shared__ float4 lng2[LNM == 3 ? 64 : 1], lnb2[LNM == 3 ? 64 : 1];
-    __shared__ int kvx[4][2];                             // K / V: the item's head exponents
-
-    // items of this block: XCD x = blockIdx % 8 owns row tiles [t_lo, t_hi) (all parts of a
-    // tile on one L2), its blocks take items l, l + bpx, ... (item j: tile j / NPART, part j % NPART)
-    const int x = blockIdx.x % 8, l = blockIdx.x / 8, bpx = gridDim.x / 8;
-    const int t_lo = (int)((int64_t)p.ntile * x / 8), t_hi = (int)((int64_t)p.ntile * (x + 1) / 8);
-    const int n_x = (t_hi - t_lo) * NPART;
-    const int nmy = l < n_x ? (n_x - l + bpx - 1) / bpx : 0;
-    if (nmy == 0) return;                                 // the whole block
-    auto item_tile = [&](int i) { return t_lo + (l + i * bpx) / NPART; };
-    auto item_part = [&](int i) { return (l + i * bpx) % NPART; };
-
-    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
-    const int g = lane >> 4, c = lane & 15;
-    const bool mfma = wv < 4;
-
-    if (mfma) {
-        // ============================ MFMA waves ============================
-        const int wm = wv;
-        auto issue = [&](int i, int s, u32x4 (&slot)[GL]) {
-            const int pw0 = item_part(i) * 4 * NPW + wm * NPW;
-#pragma unroll
-            for (int e = 0; e < GL; ++e) {
-                const int pp = e >> 1, tt = e & 1;
-                slot[e] = p.W[(int64_t)(pw0 + pp) * kWsPanelU + (s * 2 + tt) * 64 + lane];
-            }
-        };
-        u32x4 ring[3][GL];
-        issue(0, 0, ring[0]);
-        issue(0, 1, ring[1]);
-        __syncthreads();                                  // P: parameters in LDS
-        __syncthreads();                                  // item 0's act image
-        for (int k = 0; k < nmy; ++k) {
-            const bool has_next = k + 1 < nmy;
-            const u32x4* act = buf + (k & 1) * kWspBufU;
-            auto read_act = [&](int s, u32x4 (&f)[8]) {
-#pragma unroll
-                for (int rt = 0; rt < 4; ++rt) {
-                    f[2 * rt + 0] = act[((rt * kWsKS + s) * 2 + 0) * 64 + lane];
-                    f[2 * rt + 1] = act[((rt * kWsKS + s) * 2 + 1) * 64 + lane];
-                }
-            };
-            f32x4 acc[4][NPW];
-#pragma unroll
-            for (int rt = 0; rt < 4; ++rt)
-#pragma unroll
-                for (int pp = 0; pp < NPW; ++pp) acc[rt][pp] = f32x4{0.f, 0.f, 0.f, 0.f};
-            u32x4 fa[2][8];
-            read_act(0, fa[0]);
-#pragma unroll
-            for (int s = 0; s < kWsKS; ++s) {
-                // group s sits in ring[s % 3]; groups s + 1, s + 2 (or the next item's 0) behind it
-                if (s + 2 < kWsKS) {
-                    issue(k, s + 2, ring[(s + 2) % 3]);
-                    wait_vm_ws<2 * GL>();
-                } else if (s + 2 == kWsKS) {
-                    wait_vm_ws<GL>();
-                } else {
-                    wait_vm_ws<0>();
-                    if (has_next) issue(k + 1, 0, ring[0]);
-                }
-                u32x4 (&wf)[GL] = ring[s % 3];
-                u32x4 (&cur)[8] = fa[s & 1];
-                if (s + 1 < kWsKS) read_act(s + 1, fa[(s + 1) & 1]);
-#pragma unroll
-                for (int rt = 0; rt < 4; ++rt) {
-                    const f16x8 ah = __builtin_bit_cast(f16x8, cur[2 * rt + 0]);
-                    const f16x8 al = __builtin_bit_cast(f16x8, cur[2 * rt + 1]);
-#pragma unroll
-                    for (int pp = 0; pp < NPW; ++pp) {
-                        const f16x8 wh = __builtin_bit_cast(f16x8, wf[2 * pp]);
-                        const f16x8 wl = __builtin_bit_cast(f16x8, wf[2 * pp + 1]);
-                        acc[rt][pp] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, ah, acc[rt][pp], 0, 0, 0);
-                        acc[rt][pp] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, al, acc[rt][pp], 0, 0, 0);
-                        acc[rt][pp] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, ah, acc[rt][pp], 0, 0, 0);
-                    }
-                }
-            }
-            if (has_next) issue(k + 1, 1, ring[1]);
-
-            // finished values (registers): lane holds rows 16 rt + c, columns 16 pp + 4 g .. + 3
-            // of the wave's 16 NPW
-            const int t = item_tile(k), part = item_part(k);
-            const int col0 = part * 64 * NPW + wm * 16 * NPW;   // the wave's first column
-            const bool kvp = KV && col0 >= p.kv_col0;
-            float rs[4];
-#pragma unroll
-            for (int rt = 0; rt < 4; ++rt) rs[rt] = rowrs[k & 1][16 * rt + c];
-            u32x4 fin[4][NPW];
-            int ex[2] = {0, 0};
-            if (kvp) {
-#pragma unroll
-                for (int hh = 0; hh < NPW / 2; ++hh) {
-                    float y[4][2][4];
-                    float mx = 0.f;
-#pragma unroll
-                    for (int pp = 0; pp < 2; ++pp) {
-                        const int n = col0 + 32 * hh + 16 * pp + 4 * g;
-                        const float4 ws = colw[n / 4], bv = colb[n / 4];
-#pragma unroll
-                        for (int rt = 0; rt < 4; ++rt) {
-                            const bool ok = t * 64 + 16 * rt + c < p.M;   // rows past M: zeros
-                            const f32x4 a = acc[rt][2 * hh + pp];
-                            y[rt][pp][0] = ok ? a[0] * (rs[rt] * ws.x) + bv.x : 0.f;
-                            y[rt][pp][1] = ok ? a[1] * (rs[rt] * ws.y) + bv.y : 0.f;
-                            y[rt][pp][2] = ok ? a[2] * (rs[rt] * ws.z) + bv.z : 0.f;
-                            y[rt][pp][3] = ok ? a[3] * (rs[rt] * ws.w) + bv.w : 0.f;
-                            mx = fmaxf(mx, max3_abs(y[rt][pp][0], y[rt][pp][1],
-                                                    fmaxf(fabsf(y[rt][pp][2]), fabsf(y[rt][pp][3]))));
-                        }
-                    }
-                    mx = xg_max_w(row16_max(mx));
-                    const int e = mx > 0.f ? min(15 - __builtin_amdgcn_frexp_expf(mx), 127) : 0;
-                    ex[hh] = e;
-                    const float sc = __builtin_ldexpf(1.f, e);
-#pragma unroll
-                    for (int rt = 0; rt < 4; ++rt)
-#pragma unroll
-                        for (int pp = 0; pp < 2; ++pp) {
-                            _Float16 hv[4], lv[4];
-#pragma unroll
-                            for (int r = 0; r < 4; ++r) {
-                                const float xs = y[rt][pp][r] * sc;
-                                hv[r] = (_Float16)xs;
-                                lv[r] = (_Float16)(xs - (float)hv[r]);
-                            }
-                            const uint2 h2 = *reinterpret_cast<const uint2*>(hv);
-                            const uint2 l2 = *reinterpret_cast<const uint2*>(lv);
-                            fin[rt][2 * hh + pp] = u32x4{h2.x, h2.y, l2.x, l2.y};
-                        }
-                }
-            } else {
-#pragma unroll
-                for (int pp = 0; pp < NPW; ++pp) {
-                    const int n = col0 + 16 * pp + 4 * g;
-                    const float4 ws = colw[n / 4], bv = colb[n / 4];
-#pragma unroll
-                    for (int rt = 0; rt < 4; ++rt) {
-                        const f32x4 a = acc[rt][pp];
-                        constexpr int A1 = RES ? FGR_ACT_NONE : ACT;      // RES: IO waves finish
-                        const float4 yv = make_float4(finish_ws<A1, false>(a[0] * (rs[rt] * ws.x), bv.x, 0.f),
-                                                      finish_ws<A1, false>(a[1] * (rs[rt] * ws.y), bv.y, 0.f),
-                                                      finish_ws<A1, false>(a[2] * (rs[rt] * ws.z), bv.z, 0.f),
-                                                      finish_ws<A1, false>(a[3] * (rs[rt] * ws.w), bv.w, 0.f));
-                        fin[rt][pp] = __builtin_bit_cast(u32x4, yv);
-                    }
-                }
-            }
-            __syncthreads();                              // B: every wave read buffer k & 1
-            // results -> buffer k & 1, chunk wm (the IO wave wm copies it out)
-            u32x4* res = buf + (k & 1) * kWspBufU + wm * 1024;
-            if (kvp) {
-#pragma unroll
-                for (int hh = 0; hh < NPW / 2; ++hh) {
-                    const int hd = (col0 + 32 * hh - p.kv_col0) >> 5;
-                    const int isv = hd >= p.n_head ? 1 : 0;
-                    char* hb = reinterpret_cast<char*>(res) + hh * 8192;
-                    if (lane == 0) kvx[wm][hh] = ex[hh];
-#pragma unroll
-                    for (int rt = 0; rt < 4; ++rt) {
-                        const int key = 16 * rt + c;
-#pragma unroll
-                        for (int pp = 0; pp < 2; ++pp) {
-                            const int gq = 2 * pp + (g >> 1);
-                            const u32x4 f = fin[rt][2 * hh + pp];
-#pragma unroll
-                            for (int tt = 0; tt < 2; ++tt) {
-                                const int off = isv ? tt * (128 * 32) + key * 64 +
-                                                          (gq ^ (((key >> 2) & 1) << 1)) * 16 + 8 * (g & 1)
-                                                    : ((tt * 4 + gq) * 64 + key) * 16 + 8 * (g & 1);
-                                *reinterpret_cast<uint2*>(hb + off) = tt ? uint2{f[2], f[3]} : uint2{f[0], f[1]};
-                            }
-                        }
-                    }
-                }
-            } else {
-                // row 16 rt + c of the item -> chunk rt, its 16-B unit u at (u ^ c) (conflict-free)
-#pragma unroll
-                for (int rt = 0; rt < 4; ++rt)
-#pragma unroll
-                    for (int pp = 0; pp < NPW; ++pp) {
-                        const int u = 4 * NPW * wm + 4 * pp + g;
-                        buf[(k & 1) * kWspBufU + rt * 1024 + c * UR + (u ^ c)] = fin[rt][pp];
-                    }
-            }
-            __syncthreads();                              // C: results of item k in buffer k & 1
-        }
-        return;
-    }
-
-    // ============================== IO waves ==============================
-    const int wi = wv - 4, itid = tid - 256;
-    // parameters -> LDS
-    for (int j = itid; j < N / 4; j += 256) {
-        colw[j] = reinterpret_cast<const float4*>(p.wsc)[j];
-        colb[j] = p.bias ? reinterpret_cast<const float4*>(p.bias)[j] : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    if constexpr (LNM > 0) {
-        if (itid < 64) {
-            lng[itid] = reinterpret_cast<const float4*>(p.ln_g)[itid];
-            lnb[itid] = reinterpret_cast<const float4*>(p.ln_b)[itid];
-            if constexpr (LNM == 3) {
-                lng2[itid] = reinterpret_cast<const float4*>(p.g2)[itid];
-                lnb2[itid] = reinterpret_cast<const float4*>(p.b2)[itid];
-            }
-        }
-    }
-    float xr[kWsKS][8];
-    float dr[LNM >= 2 ? kWsKS : 1][8];
-    // the lane's row of item i: tile row 16 wi + c, k columns 32 s + 8 g .. + 7
-    auto load_rows = [&](int i) {
-        const int64_t row = min(item_tile(i) * 64 + 16 * wi + c, p.M - 1);
-        const float* ar = p.A + row * p.lda;
-#pragma unroll
-        for (int s = 0; s < kWsKS; ++s) {
-            const float4 a0 = *reinterpret_cast<const float4*>(ar + 32 * s + 8 * g);
-            const float4 a1 = *reinterpret_cast<const float4*>(ar + 32 * s + 8 * g + 4);
-            xr[s][0] = a0.x; xr[s][1] = a0.y; xr[s][2] = a0.z; xr[s][3] = a0.w;
-            xr[s][4] = a1.x; xr[s][5] = a1.y; xr[s][6] = a1.z; xr[s][7] = a1.w;
-        }
-        if constexpr (LNM >= 2) {
-            const float* dp = p.add + row * p.ld_add;
-#pragma unroll
-            for (int s = 0; s < kWsKS; ++s) {
-                const float4 d0 = *reinterpret_cast<const float4*>(dp + 32 * s + 8 * g);
-                const float4 d1 = *reinterpret_cast<const float4*>(dp + 32 * s + 8 * g + 4);
-                dr[s][0] = d0.x; dr[s][1] = d0.y; dr[s][2] = d0.z; dr[s][3] = d0.w;
-                dr[s][4] = d1.x; dr[s][5] = d1.y; dr[s][6] = d1.z; dr[s][7] = d1.w;
-            }
-        }
-    };
-    // LayerNorm (+ add, + out2) and the split of the loaded rows into region wi of buffer b
-    auto prep_rows = [&](int i, int b) {
-        if constexpr (LNM > 0) {
-            float sm = 0.f;
-#pragma unroll
-            for (int s = 0; s < kWsKS; ++s)
-                sm += ((xr[s][0] + xr[s][1]) + (xr[s][2] + xr[s][3])) +
-                      ((xr[s][4] + xr[s][5]) + (xr[s][6] + xr[s][7]));
-            const float mean = xg_sum_w(sm) / 256.f;
-            float sq = 0.f;
-#pragma unroll
-            for (int s = 0; s < kWsKS; ++s)
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    const float d = xr[s][e] - mean;
-                    sq += d * d;
-                }
-            const float rstd = 1.0f / sqrtf(xg_sum_w(sq) / 256.f + p.eps);
-            // normalise in place, then out2 (LNM 3, part 0 items: stored at once) and the
-            // in_proj input LN(x) g + b + add
-#pragma unroll
-            for (int s = 0; s < kWsKS; ++s)
-#pragma unroll
-                for (int e = 0; e < 8; ++e) xr[s][e] = (xr[s][e] - mean) * rstd;
-            if constexpr (LNM == 3) {
-                const int rrow = item_tile(i) * 64 + 16 * wi + c;
-                if (item_part(i) == 0 && rrow < p.M) {
-                    float* o2 = p.out2 + (int64_t)rrow * p.ld_out2;
-#pragma unroll
-                    for (int s = 0; s < kWsKS; ++s) {
-                        const int kk = 32 * s + 8 * g;
-                        const float4 h0 = lng2[kk / 4], h1 = lng2[kk / 4 + 1];
-                        const float4 c0 = lnb2[kk / 4], c1 = lnb2[kk / 4 + 1];
-                        *reinterpret_cast<float4*>(o2 + kk) =
-                            make_float4(xr[s][0] * h0.x + c0.x, xr[s][1] * h0.y + c0.y,
-                                        xr[s][2] * h0.z + c0.z, xr[s][3] * h0.w + c0.w);
-                        *reinterpret_cast<float4*>(o2 + kk + 4) =
-                            make_float4(xr[s][4] * h1.x + c1.x, xr[s][5] * h1.y + c1.y,
-                                        xr[s][6] * h1.z + c1.z, xr[s][7] * h1.w + c1.w);
-                    }
-                }
-            }
-#pragma unroll
-            for (int s = 0; s < kWsKS; ++s) {
-                const int kk = 32 * s + 8 * g;
-                const float4 g0 = lng[kk / 4], g1 = lng[kk / 4 + 1];
-                const float4 b0 = lnb[kk / 4], b1 = lnb[kk / 4 + 1];
-                const float gg[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
-                const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    xr[s][e] = xr[s][e] * gg[e] + bb[e];
-                    if constexpr (LNM >= 2) xr[s][e] += dr[s][e];
-                }
-            }
-        }
-        float mx = 0.f;
-#pragma unroll
-        for (int s = 0; s < kWsKS; ++s) {
-            mx = fmaxf(mx, max3_abs(xr[s][0], xr[s][1], xr[s][2]));
-            mx = fmaxf(mx, max3_abs(xr[s][3], xr[s][4], xr[s][5]));
-            mx = fmaxf(mx, max3_abs(xr[s][6], xr[s][7], 0.f));
-        }
-        mx = xg_max_w(mx);
-        const int e = mx > 0.f ? min(15 - __builtin_amdgcn_frexp_expf(mx), 127) : 0;
-        const float sc = __builtin_ldexpf(1.f, e);
-        u32x4* act = buf + b * kWspBufU;
-#pragma unroll
-        for (int s = 0; s < kWsKS; ++s) {
-            u32x4 h, lo;
-            split8_f16(xr[s], sc, h, lo);
-            act[((wi * kWsKS + s) * 2 + 0) * 64 + lane] = h;
-            act[((wi * kWsKS + s) * 2 + 1) * 64 + lane] = lo;
-        }
-        if (g == 0) rowrs[b][16 * wi + c] = __builtin_ldexpf(1.f, -e);
-    };
-    // item i's finished values (buffer b, chunk wi) -> global memory; R: residual rows loaded first
-    float4 rr[RES ? 4 * NPW : 1];
-    auto load_res = [&](int i) {
-        if constexpr (RES) {
-            const int t = item_tile(i), cb = item_part(i) * 64 * NPW;
-#pragma unroll
-            for (int it = 0; it < 4 * NPW; ++it) {
-                const int f = it * 64 + lane, row = f / UR, u = f % UR;
-                const int64_t grow = min(t * 64 + 16 * wi + row, p.M - 1);
-                rr[it] = *reinterpret_cast<const float4*>(p.R + grow * p.ldr + cb + 4 * u);
-            }
-        }
-    };
-    auto store_item = [&](int i, int b) {
-        const int t = item_tile(i), part = item_part(i);
-        const u32x4* res = buf + b * kWspBufU + wi * 1024;
-        const int col0 = part * 64 * NPW + wi * 16 * NPW;   // MFMA wave wi's columns
-        if (KV && col0 >= p.kv_col0) {
-#pragma unroll
-            for (int hh = 0; hh < NPW / 2; ++hh) {
-                const int hd = (col0 + 32 * hh - p.kv_col0) >> 5;
-                const int isv = hd >= p.n_head ? 1 : 0, head = hd - isv * p.n_head;
-                const int64_t tile = (int64_t)t * p.n_head + head;
-                if (lane == 0) reinterpret_cast<int*>(p.kv_sc + tile)[isv] = kvx[wi][hh];
-                u32x4* dst = reinterpret_cast<u32x4*>(p.kv_img + tile * (kKvUnitsWs * 16)) + isv * kKvUnitVWs;
-#pragma unroll
-                for (int it = 0; it < 8; ++it) dst[it * 64 + lane] = res[hh * 512 + it * 64 + lane];
-            }
-        } else {
-#pragma unroll
-            for (int it = 0; it < 4 * NPW; ++it) {
-                const int f = it * 64 + lane, row = f / UR, u = f % UR;
-                const int grow = t * 64 + 16 * wi + row;
-                float4 v = __builtin_bit_cast(float4, res[row * UR + (u ^ (row & 15))]);
-                if constexpr (RES) {
-                    v = make_float4(finish_ws<ACT, true>(v.x, 0.f, rr[it].x), finish_ws<ACT, true>(v.y, 0.f, rr[it].y),
-                                    finish_ws<ACT, true>(v.z, 0.f, rr[it].z), finish_ws<ACT, true>(v.w, 0.f, rr[it].w));
-                }
-                if (grow < p.M)
-                    *reinterpret_cast<float4*>(p.C + (int64_t)grow * p.ldc + part * 64 * NPW + 4 * u) = v;
-            }
-        }
-    };
-
-    load_rows(0);
-    __syncthreads();                                      // P: parameters in LDS
-    prep_rows(0, 0);
-    __syncthreads();                                      // item 0's act image
-    for (int k = 0; k < nmy; ++k) {
-        const bool has_next = k + 1 < nmy;
-        const int b1 = (k + 1) & 1;                       // item k - 1's results / item k + 1's rows
-        if (k >= 1) load_res(k - 1);
-        if (has_next) load_rows(k + 1);
-        if (k >= 1) store_item(k - 1, b1);
-        if (has_next) prep_rows(k + 1, b1);
-        __syncthreads();                                  // B
-        __syncthreads();                                  // C
-    }
-    load_res(nmy - 1);
-    store_item(nmy - 1, (nmy - 1) & 1);
-}
-
-template <int NPW, int LNM, bool KV, bool RES, int ACT, int NPART>
-void launch_wsp(const WsArgs& a, hipStream_t st) {
-    const int ntile = (a.M + 63) / 64;
-    const int items = ntile * NPART;
-    const int grid = min(kCusWsp, (items + 7) / 8 * 8);
-    const WspArgs w{a.A, a.lda, a.W, a.wsc, a.bias, a.C, a.ldc, a.R, a.ldr, a.M, a.N, ntile,
-                    a.ln_g, a.ln_b, a.eps, a.add, a.ld_add, a.g2, a.b2, a.out2, a.ld_out2,
-                    a.kv_img, a.kv_sc, a.n_head, a.kv_col0};
-    hipLaunchKernelGGL((gemm_wsp_kernel<NPW, LNM, KV, RES, ACT, NPART>), dim3((unsigned)grid), dim3(512), 0, st, w);
-}
-
 // row tiles per block: 3 (48-row blocks) where they fit the CUs in one round and 64-row
 // blocks leave CUs idle (ModelNet's 9544 rows: 199 blocks instead of 150), else 4; the K / V
 // image epilogue writes whole 64-row tiles (4 only). FGR_WS_RT overrides (A/B).
@@ -1010,34 +574,6 @@ bool gemm_ws_f16x3(const float* A, int64_t lda, const void* W, const float* wsc,
              ln ? ln->ld_out2 : 0, ln ? ln->kv_img : nullptr, ln ? ln->kv_sc : nullptr,
              ln ? ln->n_head : 0, ln ? ln->kv_col0 : N};
     const bool relu = act == FGR_ACT_RELU;
-    // the persistent pipelined form (gemm_wsp_kernel) for the in_proj with K / V images and the
-    // plain / residual N = 256 / 512 / 1024 shapes when FGR_GEMM_WSP=1 (under validation),
-    // FGR_WSP_NPW=4 gives the plain N >= 512 shapes 64-column instead of 32-column wave slices
-    static const bool wsp = [] { const char* e = getenv("FGR_GEMM_WSP"); return e && e[0] == '1'; }();
-    static const int wsp_npw = [] { const char* e = getenv("FGR_WSP_NPW"); return e && atoi(e) == 4 ? 4 : 2; }();
-    if (wsp && ln && ln->kv_img && N == 768 && !relu && ln->add && ln->n_head * 64 + ln->kv_col0 == N &&
-        ln->kv_col0 == 256) {
-        if (ln->out2) launch_wsp<4, 3, true, false, FGR_ACT_NONE, 3>(a, st);
-        else launch_wsp<4, 2, true, false, FGR_ACT_NONE, 3>(a, st);
-        return true;
-    }
-    if (wsp && !ln && (N == 256 || N == 512 || N == 1024)) {
-#define FGR_WSP_PLAIN(NPW, P)                                                                   \
-        if (R) { if (relu) launch_wsp<NPW, 0, false, true, FGR_ACT_RELU, P>(a, st);             \
-                 else launch_wsp<NPW, 0, false, true, FGR_ACT_NONE, P>(a, st); }                \
-        else if (relu) launch_wsp<NPW, 0, false, false, FGR_ACT_RELU, P>(a, st);                \
-        else launch_wsp<NPW, 0, false, false, FGR_ACT_NONE, P>(a, st);
-        if (wsp_npw == 4 && N > 256) {
-            if (N == 512) { FGR_WSP_PLAIN(4, 2) }
-            else { FGR_WSP_PLAIN(4, 4) }
-        } else {
-            if (N == 256) { FGR_WSP_PLAIN(2, 2) }
-            else if (N == 512) { FGR_WSP_PLAIN(2, 4) }
-            else { FGR_WSP_PLAIN(2, 8) }
-        }
-#undef FGR_WSP_PLAIN
-        return true;
-    }
     if (N != 256 && N != 768) {                  // 512 / 1024: N / 256 blocks per row tile
         if (ln) return false;
 #define FGR_WS_PARTS(P)                                                                         \

@@ -231,8 +231,8 @@ def test_ln_qkv_images_vs_two_launch_path(gpu, lens, side):
     64-row tile, head dim 32) + fgr_attention_f16x3_img vs the path it replaces (LN-fused in_proj
     -> fp32 q | k | v -> fgr_attention_f16x3 with per-segment images): segments starting
     anywhere inside a tile (incl. a 1-row cloud and tiles shared by three clouds), self- and
-    cross-attention, the side output; 24000 rows: several (tile, column part) items per block of
-    the persistent in_proj kernel (gemm_ws.hip, gemm_wsp_kernel). Both are fp32-accurate: <= 2e-6 normwise apart and
+    cross-attention, the side output, 24000 rows (1125 blocks of the split in_proj, more than one
+    round on the chip). Both are fp32-accurate: <= 2e-6 normwise apart and
     <= 1e-5 from a float64 LayerNorm -> in_proj -> softmax attention."""
     from fgreg import linear as lin
     from fgreg import ops
