@@ -391,20 +391,18 @@ gemm_ws_kernel(WsArgs p) {
                 const int e = mx > 0.f ? min(15 - __builtin_amdgcn_frexp_expf(mx), 127) : 0;
                 kv_e[pass][hh] = e;
                 const float sc = __builtin_ldexpf(1.f, e);
+                // the split of two row tiles' 4 dims at once: 16 v_fma_mix (split8_f16, the
+                // bits of hi = f16(y sc), lo = f16(y sc - hi))
 #pragma unroll
-                for (int rt = 0; rt < RT; ++rt)
+                for (int rt = 0; rt < RT; rt += 2)
 #pragma unroll
                     for (int pp = 0; pp < 2; ++pp) {
-                        _Float16 hv[4], lv[4];
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            const float x = y[rt][pp][r] * sc;
-                            hv[r] = (_Float16)x;
-                            lv[r] = (_Float16)(x - (float)hv[r]);
-                        }
-                        const uint2 h2 = *reinterpret_cast<const uint2*>(hv);
-                        const uint2 l2 = *reinterpret_cast<const uint2*>(lv);
-                        fin[pass][rt][2 * hh + pp] = u32x4{h2.x, h2.y, l2.x, l2.y};
+                        const float v8[8] = {y[rt][pp][0], y[rt][pp][1], y[rt][pp][2], y[rt][pp][3],
+                                             y[rt + 1][pp][0], y[rt + 1][pp][1], y[rt + 1][pp][2], y[rt + 1][pp][3]};
+                        u32x4 h, l;
+                        split8_f16(v8, sc, h, l);
+                        fin[pass][rt][2 * hh + pp] = u32x4{h[0], h[1], l[0], l[1]};
+                        fin[pass][rt + 1][2 * hh + pp] = u32x4{h[2], h[3], l[2], l[3]};
                     }
             }
         } else {
