@@ -129,8 +129,9 @@ gemm_ws_kernel(WsArgs p) {
     __shared__ float4 colw[N / 4], colb[N / 4];           // per column: 2^-e_n, bias
     __shared__ float4 lng[LNM ? 64 : 1], lnb[LNM ? 64 : 1];
     __shared__ float4 lng2[LNM == 3 ? 64 : 1], lnb2[LNM == 3 ? 64 : 1];
-    // LNM 3, one block per row tile: the out2 rows staged in LDS, row-major; NPART > 1: part 0
-    // recomputes them at the end from re-read rows (no 64 KB staging: two blocks per CU)
+    // LNM 3, one block per row tile: the out2 rows staged in LDS, row-major; NPART > 1: the
+    // parts recompute them at the end from re-read rows, a k range each (no 64 KB staging: two
+    // blocks per CU)
     constexpr bool kSideLds = LNM == 3 && NPART == 1;
     __shared__ float4 side[kSideLds ? BR * 64 : 1];
 
@@ -485,25 +486,33 @@ gemm_ws_kernel(WsArgs p) {
             }
         }
     }
-    if (LNM == 3 && !kSideLds && part == 0 && wv < RT) {
+    if (LNM == 3 && !kSideLds && wv < RT) {
         // out2 = LN(x) g2 + b2 of the wave's rows from a second read of x (L2), after every
-        // other store of the block
+        // other store of the block; the row tile's NPART blocks take a k32-step range each
+        // (part p: steps [8p / NPART, 8(p + 1) / NPART)), all loads issued before the stores
+        const int s_lo = part * kWsKS / NPART, s_hi = (part + 1) * kWsKS / NPART;
+        constexpr int SPP = (kWsKS + NPART - 1) / NPART;  // steps per part, at most
         const float* ar = p.A + row * p.lda;
+        float4 a0[SPP], a1[SPP];
 #pragma unroll
-        for (int s = 0; s < kWsKS; ++s) {
-            const int k = 32 * s + 8 * g;
-            const float4 a0 = *reinterpret_cast<const float4*>(ar + k);
-            const float4 a1 = *reinterpret_cast<const float4*>(ar + k + 4);
-            const float4 h0 = lng2[k / 4], h1 = lng2[k / 4 + 1];
-            const float4 c0 = lnb2[k / 4], c1 = lnb2[k / 4 + 1];
-            if (rrow < p.M) {
+        for (int j = 0; j < SPP; ++j) {
+            const int kk = 32 * min(s_lo + j, kWsKS - 1) + 8 * g;
+            a0[j] = *reinterpret_cast<const float4*>(ar + kk);
+            a1[j] = *reinterpret_cast<const float4*>(ar + kk + 4);
+        }
+#pragma unroll
+        for (int j = 0; j < SPP; ++j) {
+            const int k = 32 * (s_lo + j) + 8 * g;
+            if (s_lo + j < s_hi && rrow < p.M) {
+                const float4 h0 = lng2[k / 4], h1 = lng2[k / 4 + 1];
+                const float4 c0 = lnb2[k / 4], c1 = lnb2[k / 4 + 1];
                 float* o2 = p.out2 + (int64_t)rrow * p.ld_out2 + k;
                 *reinterpret_cast<float4*>(o2) = make_float4(
-                    (a0.x - ln_mean) * ln_rstd * h0.x + c0.x, (a0.y - ln_mean) * ln_rstd * h0.y + c0.y,
-                    (a0.z - ln_mean) * ln_rstd * h0.z + c0.z, (a0.w - ln_mean) * ln_rstd * h0.w + c0.w);
+                    (a0[j].x - ln_mean) * ln_rstd * h0.x + c0.x, (a0[j].y - ln_mean) * ln_rstd * h0.y + c0.y,
+                    (a0[j].z - ln_mean) * ln_rstd * h0.z + c0.z, (a0[j].w - ln_mean) * ln_rstd * h0.w + c0.w);
                 *reinterpret_cast<float4*>(o2 + 4) = make_float4(
-                    (a1.x - ln_mean) * ln_rstd * h1.x + c1.x, (a1.y - ln_mean) * ln_rstd * h1.y + c1.y,
-                    (a1.z - ln_mean) * ln_rstd * h1.z + c1.z, (a1.w - ln_mean) * ln_rstd * h1.w + c1.w);
+                    (a1[j].x - ln_mean) * ln_rstd * h1.x + c1.x, (a1[j].y - ln_mean) * ln_rstd * h1.y + c1.y,
+                    (a1[j].z - ln_mean) * ln_rstd * h1.z + c1.z, (a1[j].w - ln_mean) * ln_rstd * h1.w + c1.w);
             }
         }
     }
